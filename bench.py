@@ -1,0 +1,248 @@
+"""Headline benchmark: batched iLQR iterations/s, nx=12 nu=4 T=100, batch 4096 per GPU.
+
+A "step" is one fit iteration (iLQR.fit's loop body, /root/reference/src/forward_pass.jl:162-175:
+backward_pass + forward_pass with its line search) over the whole per-GPU batch,
+started from the cold trajectory (u = 0 and its rollout, prev_cost = Inf) so that
+every step does the same full work (the line search accepts α = 1 on the first
+trial from a cold start; trials are counted and reported). Inputs are resident in
+HBM before the timed region. Data: synthetic, per-instance randomised
+hover-linearised quadrotors (ilqr_amd.problems.quadrotor_batch).
+
+Multi-GPU (one process per GPU, torch.distributed over RCCL): trajectories are
+independent, so each rank solves its own 4096 instances (seeds rank·4096 + i) with
+no data-path collective (weak scaling); after the timed region the per-trajectory
+costs are all-gathered once (the fit result exchange) and that time is reported
+separately.
+
+Prints ONE JSON line (rank 0).
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "ilqr.jl_amd")]
+
+from ilqr_amd import _lib  # noqa: E402
+from ilqr_amd.problems import quadrotor_batch  # noqa: E402
+from ilqr_amd.solver import Solver, _ptr  # noqa: E402
+
+NX, NU = 12, 4
+FP64_PEAK_TFLOPS = 78.6   # MI355X FP64 dense (vector = matrix), AMD spec; not listed in the container guides
+HBM_PEAK_GBPS = 8000.0    # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def algorithmic_counts(T, nx=NX, nu=NU):
+    """SURVEY.md §8(d) per-trajectory algorithmic bytes / flops (fused design)."""
+    w = 8
+    P = 3 * nx * nx + nx * nu + nu * nu
+    traj = (T + 1) * nx + T * nu
+    gains = T * nu * (nx + 1)
+    bw_bytes = w * (traj + gains + P)                       # backward: read x,u,P; write K,d
+    fw_bytes = w * (2 * traj + gains + P)                   # forward: read x,u,K,d,P; write x̄,ū (1 trial)
+    n, m = nx, nu
+    bw_flops_step = 2 * (2 * n**3 + 4 * n * n * m + 2 * n * m * m + 2 * n * n + 4 * n * m
+                         + m**3 / 3 + (n + 3) * m * m)
+    fw_flops_step = 2 * (2 * n * n + 2 * n * m + m * m + 2 * n + 3 * m)
+    return dict(bw_bytes=bw_bytes, fw_bytes=fw_bytes, bw_flops=bw_flops_step * T,
+                fw_flops=fw_flops_step * T)
+
+
+def load_pmc_traffic(profiles_dir):
+    """HBM bytes per backward launch from committed rocprofv3 PMC passes
+    (profiles/pmc_*.json, written by profiles/collect_pmc.py), or None."""
+    best = None
+    if os.path.isdir(profiles_dir):
+        for f in sorted(os.listdir(profiles_dir)):
+            if f.startswith("pmc_") and f.endswith(".json"):
+                try:
+                    best = json.load(open(os.path.join(profiles_dir, f)))
+                except Exception:
+                    pass
+    return best
+
+
+def cpu_baseline(lq, x, u, budget_s):
+    """Time the C restatement (oracle/, kind 'port') on a bounded sample of the
+    same workload: one cold-start iteration (backward + forward) per trajectory."""
+    from oracle import cref
+    threads = min(16, os.cpu_count() or 1)
+    n = 32
+    elapsed = 0.0
+    while True:
+        idx = np.arange(n) % lq.batch
+        sub = type(lq)(lq.A[idx], lq.B[idx], lq.Q[idx], lq.R[idx], lq.Qf[idx])
+        t0 = time.perf_counter()
+        d, K, _ = cref.lq_backward(sub, x[idx], u[idx], symmetrize=True, nthreads=threads)
+        cref.lq_forward(sub, x[idx], u[idx], None, d, K, np.inf, nthreads=threads)
+        elapsed = time.perf_counter() - t0
+        if elapsed > budget_s / 4 or n >= 1 << 16:
+            break
+        n *= 2
+    rate = n / elapsed  # trajectory-iterations / s
+    return {"value": rate / lq.batch, "unit": "batched iterations/s (batch=4096)", "cores": threads,
+            "kind": "port",
+            "sample": f"{n} trajectories x 1 cold-start iteration (C restatement oracle/ilqr_ref.c, "
+                      f"OpenMP {threads} threads, -O3), {elapsed:.2f} s; trajectory-iterations/s="
+                      f"{rate:.1f}"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=4096, help="trajectories per GPU")
+    ap.add_argument("--T", type=int, default=100)
+    ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds for the CPU baseline sample")
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = world > 1
+    if dist:
+        import torch.distributed as tdist
+        torch.cuda.set_device(local)
+        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    B, T = args.batch, args.T
+    lq, x0, u0 = quadrotor_batch(B, T=T, seed0=rank * B)
+    s = Solver(NX, NU, T, B, device=local)
+    s.set_problem(lq)
+    x = torch.from_numpy(x0).to(dev)
+    u = torch.from_numpy(u0).to(dev)
+    xn, un = torch.empty_like(x), torch.empty_like(u)
+    pc = torch.empty((B,), dtype=torch.float64, device=dev)
+    st = torch.empty((B,), dtype=torch.int32, device=dev)
+    trials = torch.empty((B,), dtype=torch.int32, device=dev)
+    opts = _lib.default_options(tol=-1.0)  # tol disabled: no trajectory leaves the batch
+    stream = torch.cuda.current_stream(dev)
+    s._bind_stream()
+
+    def step():
+        pc.fill_(float("inf"))
+        st.zero_()
+        s.iterate(x, u, xn, un, pc, st, trials=trials, options=opts)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        tdist.barrier()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for _ in range(args.steps):
+        step()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    if dist:
+        tdist.barrier()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    ms = e0.elapsed_time(e1) / args.steps
+    ms_wall = wall * 1000.0 / args.steps
+    ms_step = max(ms, ms_wall)
+    if dist:
+        tt = torch.tensor([ms_step], dtype=torch.float64, device=dev)
+        tdist.all_reduce(tt, op=tdist.ReduceOp.MAX)
+        ms_step = float(tt.item())
+    mean_trials = float(trials.double().mean().item())
+    ok = bool((st == 0).all().item())
+
+    # dominant kernel: the backward pass, timed alone on the same stream
+    d = torch.empty((B, T, NU), dtype=torch.float64, device=dev)
+    K = torch.empty((B, T, NU, NX), dtype=torch.float64, device=dev)
+    o = _lib.default_options()
+    nrep = max(5, args.steps)
+    for _ in range(2):
+        s.lib.ilqr_backward(s.h, s._p(), C.byref(o), _ptr(x), _ptr(u), _ptr(d), _ptr(K), None)
+    b0, b1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    b0.record(stream)
+    for _ in range(nrep):
+        s.lib.ilqr_backward(s.h, s._p(), C.byref(o), _ptr(x), _ptr(u), _ptr(d), _ptr(K), None)
+    b1.record(stream)
+    torch.cuda.synchronize()
+    bw_ms = b0.elapsed_time(b1) / nrep
+
+    # result exchange (fit output): all-gather the per-trajectory costs over RCCL
+    gather_ms = None
+    if dist:
+        out = [torch.empty_like(pc) for _ in range(world)]
+        tdist.barrier()
+        torch.cuda.synchronize()
+        g0 = time.perf_counter()
+        tdist.all_gather(out, pc)
+        torch.cuda.synchronize()
+        gather_ms = (time.perf_counter() - g0) * 1000.0
+
+    cnt = algorithmic_counts(T)
+    bw_flops = cnt["bw_flops"] * B
+    bw_bytes = cnt["bw_bytes"] * B
+    it_bytes = (cnt["bw_bytes"] + cnt["fw_bytes"]) * B
+    it_flops = (cnt["bw_flops"] + cnt["fw_flops"]) * B
+    pmc = load_pmc_traffic(os.path.join(ROOT, "profiles"))
+    traffic = None
+    if pmc and pmc.get("batch") == B and pmc.get("T") == T:
+        traffic = pmc.get("hbm_bytes_per_backward_launch")
+    achieved_tf = bw_flops / (bw_ms * 1e-3) / 1e12
+
+    result = {
+        "metric": "batched iLQR iterations/sec (fwd+bwd pass), nx=12 nu=4 T=100, 1/2/4/8 MI355X",
+        "value": world * 1000.0 / ms_step,
+        "unit": "batched iterations/s (one batched iteration = 4096 trajectories per GPU, backward+forward)",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic: per-instance randomised hover-linearised quadrotor LQ (SURVEY.md §8d)",
+        "config": {"workload": "quadrotor-style LQ fit iteration (cold start)", "nx": NX, "nu": NU,
+                   "T": T, "batch_per_gpu": B, "global_batch": B * world,
+                   "parallelism": f"independent trajectories, {world} rank(s), no data-path collective"},
+        "roofline": {"bound": "mfma", "kernel": "lq_backward (backward_pass, v_mfma_f64_16x16x4_f64)",
+                     "achieved": achieved_tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": achieved_tf / FP64_PEAK_TFLOPS, "traffic": traffic,
+                     "avg_launch_ms": bw_ms, "algorithmic_flops_per_launch": bw_flops,
+                     "algorithmic_bytes_per_launch": bw_bytes,
+                     "hbm_achieved_gbps": bw_bytes / (bw_ms * 1e-3) / 1e9},
+        "iteration": {"traj_iters_per_s": world * B * 1000.0 / ms_step,
+                      "algorithmic_bytes": it_bytes, "algorithmic_flops": it_flops,
+                      "hbm_gbps": it_bytes / (ms_step * 1e-3) / 1e9,
+                      "hbm_frac": it_bytes / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBPS,
+                      "fp64_tflops": it_flops / (ms_step * 1e-3) / 1e12,
+                      "mean_line_search_trials": mean_trials, "all_ok": ok,
+                      "event_ms": ms, "wall_ms": ms_wall},
+        "allgather_costs_ms": gather_ms,
+        "cpu_baseline": None,
+    }
+    if rank == 0 and not args.no_cpu:
+        try:
+            result["cpu_baseline"] = cpu_baseline(lq, x0, u0, args.cpu_budget)
+        except Exception as e:  # the baseline is reported, never required
+            result["cpu_baseline"] = {"error": repr(e)}
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    s.close()
+    if dist:
+        tdist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

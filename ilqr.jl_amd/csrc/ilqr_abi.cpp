@@ -1,0 +1,338 @@
+// C ABI of libilqr_hip.so (include/ilqr.h): handle/workspace management, argument
+// validation with the reference's error behaviour mapped to status codes, and the
+// fit driver (src/forward_pass.jl:148-179) on top of the fused iteration kernel.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/ilqr.h"
+#include "ilqr_internal.h"
+
+struct ilqr_handle {
+  int device = 0;
+  int nx = 0, nu = 0, T = 0, batch = 0;
+  hipStream_t stream = nullptr;
+  // workspace (fit): ping-pong trajectories, gains, per-trajectory state
+  double* xbuf[2] = {nullptr, nullptr};
+  double* ubuf[2] = {nullptr, nullptr};
+  double* K = nullptr;
+  double* d = nullptr;
+  double* prev_cost = nullptr;
+  double* du2 = nullptr;
+  int32_t* trials = nullptr;
+  int32_t* status = nullptr;
+  int32_t* res_parity = nullptr;
+  int32_t* iters = nullptr;
+};
+
+namespace {
+
+thread_local std::string g_last_error;
+
+ilqr_status hip_fail(hipError_t e, const char* what) {
+  g_last_error = std::string(what) + ": " + hipGetErrorString(e);
+  return ILQR_ERR_HIP;
+}
+
+#define HIP_TRY(expr)                                  \
+  do {                                                 \
+    hipError_t e_ = (expr);                            \
+    if (e_ != hipSuccess) return hip_fail(e_, #expr);  \
+  } while (0)
+
+ilqr::LQParams lq_params(const ilqr_problem* p) {
+  return ilqr::LQParams{p->A, p->B, p->Q, p->R, p->Qf};
+}
+
+ilqr_status check_problem(const ilqr_handle* h, const ilqr_problem* p) {
+  if (!h || !p) return ILQR_ERR_BAD_ARG;
+  if (p->kind != ILQR_PROBLEM_LQ) return ILQR_ERR_UNSUPPORTED;
+  if (!p->A || !p->B || !p->Q || !p->R || !p->Qf) return ILQR_ERR_BAD_ARG;
+  if (!ilqr::lq_supported(h->nx, h->nu)) return ILQR_ERR_UNSUPPORTED;
+  return ILQR_OK;
+}
+
+ilqr::LSParams ls_params(const ilqr_options* o) {
+  ilqr_options def;
+  ilqr_default_options(&def);
+  if (!o) o = &def;
+  return ilqr::LSParams{o->mu, o->alpha0, o->shrink, o->tol, o->max_trials};
+}
+
+ilqr_status check_options(const ilqr_options* o) {
+  if (!o) return ILQR_OK;
+  if (o->max_trials < 1 || o->max_iter < 0) return ILQR_ERR_BAD_ARG;
+  if (!(o->shrink > 0.0 && o->shrink < 1.0) || !(o->alpha0 > 0.0) || std::isnan(o->mu))
+    return ILQR_ERR_BAD_ARG;
+  return ILQR_OK;
+}
+
+// Reduce per-trajectory status to the call status (host copy, synchronising).
+ilqr_status fold_status(ilqr_handle* h, const int32_t* dev_status) {
+  std::vector<int32_t> st(h->batch);
+  HIP_TRY(hipMemcpyAsync(st.data(), dev_status, sizeof(int32_t) * h->batch, hipMemcpyDeviceToHost,
+                         h->stream));
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  bool nan = false, ls = false;
+  for (int32_t s : st) {
+    nan |= s == ILQR_TRAJ_NAN;
+    ls |= s == ILQR_TRAJ_LS_EXHAUSTED;
+  }
+  return nan ? ILQR_ERR_NAN : (ls ? ILQR_ERR_LS_EXHAUSTED : ILQR_OK);
+}
+
+}  // namespace
+
+extern "C" {
+
+int ilqr_abi_version(void) { return ILQR_ABI_VERSION; }
+
+const char* ilqr_status_string(ilqr_status s) {
+  switch (s) {
+    case ILQR_OK: return "ok";
+    case ILQR_ERR_BAD_DIMS: return "bad dimensions (size(x,1) must equal size(u,1)+1)";
+    case ILQR_ERR_BAD_ARG: return "bad argument";
+    case ILQR_ERR_UNSUPPORTED: return "unsupported problem kind or (nx, nu)";
+    case ILQR_ERR_HIP: return "HIP runtime error";
+    case ILQR_ERR_NAN: return "NaN in a trajectory";
+    case ILQR_ERR_LS_EXHAUSTED: return "line search exhausted";
+  }
+  return "unknown status";
+}
+
+const char* ilqr_last_error(void) { return g_last_error.c_str(); }
+
+void ilqr_default_options(ilqr_options* o) {
+  if (!o) return;
+  o->max_iter = 100;     // forward_pass.jl:152
+  o->max_trials = 64;    // reference is unbounded (forward_pass.jl:70); 0.5^63 ≈ 1e-19
+  o->tol = 1e-6;         // forward_pass.jl:152
+  o->mu = 0.01;          // backward_pass.jl:214
+  o->alpha0 = 1.0;       // forward_pass.jl:66
+  o->shrink = 0.5;       // forward_pass.jl:82
+}
+
+int ilqr_supported(int32_t kind, int nx, int nu) {
+  return kind == ILQR_PROBLEM_LQ && ilqr::lq_supported(nx, nu) ? 1 : 0;
+}
+
+ilqr_status ilqr_create(ilqr_handle** out, int device, int nx, int nu, int T, int batch) {
+  if (!out) return ILQR_ERR_BAD_ARG;
+  *out = nullptr;
+  if (nx <= 0 || nu <= 0 || T <= 0 || batch <= 0) return ILQR_ERR_BAD_DIMS;
+  HIP_TRY(hipSetDevice(device));
+  auto* h = new ilqr_handle;
+  h->device = device;
+  h->nx = nx;
+  h->nu = nu;
+  h->T = T;
+  h->batch = batch;
+  const size_t B = (size_t)batch;
+  hipError_t e = hipSuccess;
+  for (int i = 0; i < 2 && e == hipSuccess; ++i) {
+    e = hipMalloc(&h->xbuf[i], sizeof(double) * B * (T + 1) * nx);
+    if (e == hipSuccess) e = hipMalloc(&h->ubuf[i], sizeof(double) * B * T * nu);
+  }
+  if (e == hipSuccess) e = hipMalloc(&h->K, sizeof(double) * B * T * nu * nx);
+  if (e == hipSuccess) e = hipMalloc(&h->d, sizeof(double) * B * T * nu);
+  if (e == hipSuccess) e = hipMalloc(&h->prev_cost, sizeof(double) * B);
+  if (e == hipSuccess) e = hipMalloc(&h->du2, sizeof(double) * B);
+  if (e == hipSuccess) e = hipMalloc(&h->trials, sizeof(int32_t) * B);
+  if (e == hipSuccess) e = hipMalloc(&h->status, sizeof(int32_t) * B);
+  if (e == hipSuccess) e = hipMalloc(&h->res_parity, sizeof(int32_t) * B);
+  if (e == hipSuccess) e = hipMalloc(&h->iters, sizeof(int32_t) * B);
+  if (e != hipSuccess) {
+    ilqr_destroy(h);
+    return hip_fail(e, "ilqr_create: hipMalloc");
+  }
+  *out = h;
+  return ILQR_OK;
+}
+
+ilqr_status ilqr_destroy(ilqr_handle* h) {
+  if (!h) return ILQR_OK;
+  (void)hipSetDevice(h->device);
+  for (int i = 0; i < 2; ++i) {
+    (void)hipFree(h->xbuf[i]);
+    (void)hipFree(h->ubuf[i]);
+  }
+  (void)hipFree(h->K);
+  (void)hipFree(h->d);
+  (void)hipFree(h->prev_cost);
+  (void)hipFree(h->du2);
+  (void)hipFree(h->trials);
+  (void)hipFree(h->status);
+  (void)hipFree(h->res_parity);
+  (void)hipFree(h->iters);
+  delete h;
+  return ILQR_OK;
+}
+
+ilqr_status ilqr_set_stream(ilqr_handle* h, void* s) {
+  if (!h) return ILQR_ERR_BAD_ARG;
+  h->stream = (hipStream_t)s;
+  return ILQR_OK;
+}
+
+ilqr_status ilqr_sync(ilqr_handle* h) {
+  if (!h) return ILQR_ERR_BAD_ARG;
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  return ILQR_OK;
+}
+
+ilqr_status ilqr_backward(ilqr_handle* h, const ilqr_problem* p, const ilqr_options* o,
+                          const double* x, const double* u, double* d, double* K,
+                          int32_t* status) {
+  ilqr_status st = check_problem(h, p);
+  if (st != ILQR_OK) return st;
+  if ((st = check_options(o)) != ILQR_OK) return st;
+  if (!x || !u || !d || !K) return ILQR_ERR_BAD_ARG;
+  HIP_TRY(hipSetDevice(h->device));
+  HIP_TRY(ilqr::launch_lq_backward(h->nx, h->nu, lq_params(p), h->batch, h->T, x, u, d, K, status,
+                                   ls_params(o).mu, h->stream));
+  return status ? fold_status(h, status) : ILQR_OK;
+}
+
+ilqr_status ilqr_forward(ilqr_handle* h, const ilqr_problem* p, const ilqr_options* o,
+                         const double* x, const double* u, const double* x_traj,
+                         const double* d, const double* K, const double* prev_cost,
+                         double* x_new, double* u_new, double* new_cost, int32_t* trials,
+                         int32_t* status) {
+  ilqr_status st = check_problem(h, p);
+  if (st != ILQR_OK) return st;
+  if ((st = check_options(o)) != ILQR_OK) return st;
+  if (!x || !u || !d || !K || !prev_cost || !x_new || !u_new || !new_cost) return ILQR_ERR_BAD_ARG;
+  HIP_TRY(hipSetDevice(h->device));
+  HIP_TRY(ilqr::launch_lq_forward(h->nx, h->nu, lq_params(p), h->batch, h->T, x, u, x_traj, d, K,
+                                  prev_cost, x_new, u_new, new_cost, trials, status, ls_params(o),
+                                  h->stream));
+  return status ? fold_status(h, status) : ILQR_OK;
+}
+
+ilqr_status ilqr_iterate(ilqr_handle* h, const ilqr_problem* p, const ilqr_options* o,
+                         const double* x, const double* u, const double* x_traj, double* x_new,
+                         double* u_new, double* prev_cost, double* du2, int32_t* trials,
+                         int32_t* status) {
+  ilqr_status st = check_problem(h, p);
+  if (st != ILQR_OK) return st;
+  if ((st = check_options(o)) != ILQR_OK) return st;
+  if (!x || !u || !x_new || !u_new || !prev_cost || !status) return ILQR_ERR_BAD_ARG;
+  HIP_TRY(hipSetDevice(h->device));
+  ilqr::IterArgs a{};
+  a.x = x;
+  a.u = u;
+  a.xtraj = x_traj;
+  a.xnew = x_new;
+  a.unew = u_new;
+  a.K = h->K;
+  a.d = h->d;
+  a.prev_cost = prev_cost;
+  a.du2 = du2;
+  a.trials = trials;
+  a.status = status;
+  a.res_parity = nullptr;
+  a.iters = nullptr;
+  a.parity = 0;
+  a.iter = 0;
+  HIP_TRY(ilqr::launch_lq_iterate(h->nx, h->nu, lq_params(p), h->batch, h->T, a, ls_params(o),
+                                  h->stream));
+  return ILQR_OK;
+}
+
+ilqr_status ilqr_fit(ilqr_handle* h, const ilqr_problem* p, const ilqr_options* o,
+                     const double* x_init, const double* u_init, const double* x_traj,
+                     double* x_out, double* u_out, double* cost, int32_t* iters,
+                     int32_t* status) {
+  ilqr_status st = check_problem(h, p);
+  if (st != ILQR_OK) return st;
+  if ((st = check_options(o)) != ILQR_OK) return st;
+  if (!x_init || !u_init || !x_out || !u_out) return ILQR_ERR_BAD_ARG;
+  ilqr_options def;
+  ilqr_default_options(&def);
+  if (!o) o = &def;
+  HIP_TRY(hipSetDevice(h->device));
+  const size_t B = (size_t)h->batch;
+  const size_t xbytes = sizeof(double) * B * (h->T + 1) * h->nx;
+  const size_t ubytes = sizeof(double) * B * h->T * h->nu;
+  hipStream_t s = h->stream;
+  HIP_TRY(hipMemcpyAsync(h->xbuf[0], x_init, xbytes, hipMemcpyDeviceToDevice, s));
+  HIP_TRY(hipMemcpyAsync(h->ubuf[0], u_init, ubytes, hipMemcpyDeviceToDevice, s));
+  HIP_TRY(ilqr::launch_fill_f64(h->prev_cost, h->batch, INFINITY, s));  // forward_pass.jl:159
+  HIP_TRY(ilqr::launch_fill_i32(h->status, h->batch, ILQR_TRAJ_OK, s));
+  HIP_TRY(ilqr::launch_fill_i32(h->res_parity, h->batch, 0, s));
+  HIP_TRY(ilqr::launch_fill_i32(h->iters, h->batch, 0, s));
+  const ilqr::LSParams ls = ls_params(o);
+  int par = 0;
+  for (int it = 1; it <= o->max_iter; ++it) {  // forward_pass.jl:161
+    ilqr::IterArgs a{};
+    a.x = h->xbuf[par];
+    a.u = h->ubuf[par];
+    a.xtraj = x_traj;
+    a.xnew = h->xbuf[par ^ 1];
+    a.unew = h->ubuf[par ^ 1];
+    a.K = h->K;
+    a.d = h->d;
+    a.prev_cost = h->prev_cost;
+    a.du2 = h->du2;
+    a.trials = h->trials;
+    a.status = h->status;
+    a.res_parity = h->res_parity;
+    a.iters = h->iters;
+    a.parity = par;
+    a.iter = it;
+    HIP_TRY(ilqr::launch_lq_iterate(h->nx, h->nu, lq_params(p), h->batch, h->T, a, ls, s));
+    par ^= 1;  // x̄ⁱ, ūⁱ = x̄ⁱ⁺¹, ūⁱ⁺¹ (:174-175)
+  }
+  // still-running trajectories (max_iter reached) return the last accepted iterate
+  HIP_TRY(ilqr::launch_gather_result(h->batch, h->T, h->nx, h->nu, h->xbuf[0], h->ubuf[0],
+                                     h->xbuf[1], h->ubuf[1], h->res_parity, h->status, par, x_out,
+                                     u_out, s));
+  if (cost) HIP_TRY(hipMemcpyAsync(cost, h->prev_cost, sizeof(double) * B, hipMemcpyDeviceToDevice, s));
+  if (iters) HIP_TRY(hipMemcpyAsync(iters, h->iters, sizeof(int32_t) * B, hipMemcpyDeviceToDevice, s));
+  if (status) HIP_TRY(hipMemcpyAsync(status, h->status, sizeof(int32_t) * B, hipMemcpyDeviceToDevice, s));
+  return fold_status(h, h->status);
+}
+
+ilqr_status ilqr_malloc(ilqr_handle* h, size_t bytes, void** ptr) {
+  if (!h || !ptr) return ILQR_ERR_BAD_ARG;
+  HIP_TRY(hipSetDevice(h->device));
+  HIP_TRY(hipMalloc(ptr, bytes));
+  return ILQR_OK;
+}
+
+ilqr_status ilqr_free(ilqr_handle* h, void* ptr) {
+  if (!h) return ILQR_ERR_BAD_ARG;
+  HIP_TRY(hipSetDevice(h->device));
+  HIP_TRY(hipFree(ptr));
+  return ILQR_OK;
+}
+
+ilqr_status ilqr_memcpy_h2d(ilqr_handle* h, void* dst, const void* src, size_t bytes) {
+  if (!h || !dst || !src) return ILQR_ERR_BAD_ARG;
+  HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, h->stream));
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  return ILQR_OK;
+}
+
+ilqr_status ilqr_memcpy_d2h(ilqr_handle* h, void* dst, const void* src, size_t bytes) {
+  if (!h || !dst || !src) return ILQR_ERR_BAD_ARG;
+  HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, h->stream));
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  return ILQR_OK;
+}
+
+ilqr_status ilqr_selftest(int device, int32_t* failures) {
+  const int f = ilqr::run_selftest(device);
+  if (f < 0) {
+    g_last_error = "selftest: HIP error";
+    return ILQR_ERR_HIP;
+  }
+  if (failures) *failures = f;
+  return ILQR_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,66 @@
+// Internal interface between the C ABI (ilqr_abi.cpp) and the HIP kernels
+// (ilqr_lq.hip). Not installed; see include/ilqr.h for the public ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ilqr {
+
+// Per-instance LQ problem data, device pointers, row-major, trajectory slowest.
+struct LQParams {
+  const double* A;   // (B, nx, nx)
+  const double* B;   // (B, nx, nu)
+  const double* Q;   // (B, nx, nx)
+  const double* R;   // (B, nu, nu)
+  const double* Qf;  // (B, nx, nx)
+};
+
+struct LSParams {
+  double mu;       // regulariser added to H (backward_pass.jl:214)
+  double alpha0;   // first line-search step (forward_pass.jl:66)
+  double shrink;   // step factor (forward_pass.jl:82)
+  double tol;      // convergence threshold on Σ(Δu)² (forward_pass.jl:171)
+  int max_trials;  // line-search cap
+};
+
+// Buffers of one fused iteration (fit loop body).
+struct IterArgs {
+  const double* x;      // (B, T+1, nx) current iterate
+  const double* u;      // (B, T, nu)
+  const double* xtraj;  // (B, T+1, nx) or nullptr (zeros)
+  double* xnew;         // (B, T+1, nx) next iterate
+  double* unew;         // (B, T, nu)
+  double* K;            // (B, T, nu, nx) gains workspace
+  double* d;            // (B, T, nu)
+  double* prev_cost;    // (B) in/out
+  double* du2;          // (B) out, may be null
+  int32_t* trials;      // (B) out, may be null
+  int32_t* status;      // (B) in/out (non-zero = skip)
+  int32_t* res_parity;  // (B) out, may be null: buffer parity holding the result when a trajectory stops
+  int32_t* iters;       // (B) out, may be null: last iteration index that processed the trajectory
+  int parity;           // parity of (x, u) in the fit ping-pong
+  int iter;             // 1-based iteration index (fit)
+};
+
+// Returns hipSuccess or the launch error. All launches are asynchronous on `s`.
+hipError_t launch_lq_backward(int nx, int nu, const LQParams& p, int B, int T, const double* x,
+                              const double* u, double* d, double* K, int32_t* status, double mu,
+                              hipStream_t s);
+hipError_t launch_lq_forward(int nx, int nu, const LQParams& p, int B, int T, const double* x,
+                             const double* u, const double* xtraj, const double* d,
+                             const double* K, const double* prev_cost, double* xnew,
+                             double* unew, double* new_cost, int32_t* trials, int32_t* status,
+                             const LSParams& ls, hipStream_t s);
+hipError_t launch_lq_iterate(int nx, int nu, const LQParams& p, int B, int T, const IterArgs& a,
+                             const LSParams& ls, hipStream_t s);
+// x_out[b] = (res_parity[b] ? x1 : x0)[b] (and u); status MAX_ITER for still-running ones.
+hipError_t launch_gather_result(int B, int T, int nx, int nu, const double* x0, const double* u0,
+                                const double* x1, const double* u1, const int32_t* res_parity,
+                                int32_t* status, int final_parity, double* x_out, double* u_out,
+                                hipStream_t s);
+hipError_t launch_fill_i32(int32_t* p, int n, int32_t v, hipStream_t s);
+hipError_t launch_fill_f64(double* p, int n, double v, hipStream_t s);
+bool lq_supported(int nx, int nu);
+int run_selftest(int device);  // number of failed checks, or -1 on HIP error
+
+}  // namespace ilqr

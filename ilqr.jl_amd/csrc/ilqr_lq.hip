@@ -1,0 +1,669 @@
+// MI355X (gfx950) kernels for the batched iLQR hot path, LQ problem family.
+//
+// Reference path (aabouman/iLQR.jl): backward_pass (src/backward_pass.jl:324-357,
+// with linearize_dynamics :25-40, immediate_cost_quadratization :81-109,
+// final_cost_quadratization :134-153, optimal_controller_param :177-186,
+// feedback_parameters :207-218, step_back :262-273) and forward_pass + line
+// search (src/forward_pass.jl:55-93, total_cost :182-196), one iteration of
+// fit (src/forward_pass.jl:161-176).
+//
+// Mapping:
+//  * backward: ONE WAVE PER TRAJECTORY. The value-function state is kept in the
+//    accumulator layout of v_mfma_f64_16x16x4_f64 as the symmetric 16×16 tile
+//        Sp = [[S, s], [sᵀ, 0]]      (rows/cols ≥ nx+1 zero)
+//    lane l = (c = l&15, q = l>>4) holds Sp[q+4r][c] in register r. Because Sp is
+//    symmetric, that same register is the MFMA A-operand fragment of Sp, so the
+//    recursion never leaves registers:
+//        Y  = Sp·F          F = [A | B]  (nx × (nx+nu), zero-padded)   ceil(nx/4) MFMAs
+//        Z  = L + Fᵀ·Y      L = blockdiag(Q+Qᵀ, R+Rᵀ)                  ceil(nx/4) MFMAs
+//    Z holds Qxx (= lxx + AᵀSA), G = BᵀSA (+lux = 0) and H = luu + BᵀSB; row nx of
+//    Y is sᵀF, giving g = lu + Bᵀs and lx + Aᵀs. The nu×nu solve (H + μI)⁻¹
+//    (LDLᵀ, redundantly in every lane) yields K_aug = [K | d]. The reference's
+//    step_back (:268-270) with G = -H_reg K, g = -H_reg d simplifies exactly to
+//        [S s] = [Qxx  lx+Aᵀs] - K_augᵀ (H + 2μI) K_aug
+//    which is ONE more MFMA (k = nu ≤ 4) with A = -K_augᵀ, B = (H+2μI)K_aug
+//    = -[G|g] + μ K_aug, accumulating into [Qxx | lx+Aᵀs].
+//  * forward: 16 lanes per trajectory (4 trajectories per wave); lane j < nx owns
+//    x̄_j, lanes nx.. own ū; the per-step mat-vecs broadcast operands through LDS.
+//  * one fit iteration = backward launch (4 waves/SIMD) + forward launch.
+#include <hip/hip_runtime.h>
+#include <math.h>
+
+#include "ilqr_internal.h"
+#include "../../include/ilqr.h"
+
+namespace ilqr {
+namespace {
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+typedef unsigned u2v __attribute__((ext_vector_type(2)));
+
+constexpr int WAVES_PER_WG = 4;   // trajectories per workgroup
+constexpr int BW_LDS = 80;        // doubles of backward scratch per wave: 4 rows of 16 + one row of 16
+constexpr int FW_LDS = 48;        // doubles of forward scratch per 16-lane group: dx, z, v rows
+
+__device__ __forceinline__ d4 mfma(double a, double b, d4 c) {
+  return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
+// all-reduce over lanes {l, l^16} with v_permlane16_swap (gfx950): one instruction
+// per dword gives every lane both its own and its partner row's value.
+__device__ __forceinline__ double xor16_sum(double v) {
+  u2v p = __builtin_bit_cast(u2v, v);
+  auto lo = __builtin_amdgcn_permlane16_swap(p.x, p.x, false, false);
+  auto hi = __builtin_amdgcn_permlane16_swap(p.y, p.y, false, false);
+  u2v a = {lo[0], hi[0]};
+  u2v b = {lo[1], hi[1]};
+  return __builtin_bit_cast(double, a) + __builtin_bit_cast(double, b);
+}
+__device__ __forceinline__ double xor32_sum(double v) {
+  u2v p = __builtin_bit_cast(u2v, v);
+  auto lo = __builtin_amdgcn_permlane32_swap(p.x, p.x, false, false);
+  auto hi = __builtin_amdgcn_permlane32_swap(p.y, p.y, false, false);
+  u2v a = {lo[0], hi[0]};
+  u2v b = {lo[1], hi[1]};
+  return __builtin_bit_cast(double, a) + __builtin_bit_cast(double, b);
+}
+// sum over the four lanes {c, c+16, c+32, c+48} of a column
+__device__ __forceinline__ double colsum4(double v) { return xor32_sum(xor16_sum(v)); }
+
+// sum over the 16 lanes of a row (one forward group)
+__device__ __forceinline__ double rowsum16(double v) {
+#pragma unroll
+  for (int m = 8; m >= 1; m >>= 1) v += __shfl_xor(v, m, 16);
+  return v;
+}
+
+// Cross-lane LDS hand-off inside one wave: DS ops of a wave execute in order, so
+// only the compiler must be kept from moving LDS accesses across this point.
+__device__ __forceinline__ void wave_lds_fence() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// 1/x: v_rcp_f64 + two Newton steps (≤1 ulp), no IEEE div sequence.
+__device__ __forceinline__ double rcp(double x) {
+  double r = __builtin_amdgcn_rcp(x);
+  double e = fma(-x, r, 1.0);
+  r = fma(r, e, r);
+  e = fma(-x, r, 1.0);
+  return fma(r, e, r);
+}
+
+// Load-or-zero without a branch: the address is clamped to `safe` when !ok so
+// the load is unconditional (no exec-masked load + vmcnt(0) per element).
+__device__ __forceinline__ double ldz(bool ok, const double* p, const double* safe) {
+  const double v = *(ok ? p : safe);
+  return ok ? v : 0.0;
+}
+
+// (H + μI) = L D Lᵀ (no pivoting; H symmetric, lower triangle read) and a solve
+// with a d4 right-hand side; NU ≤ 4, entries ≥ NU unused.
+template <int NU>
+struct LDLT {
+  double l[NU][NU];
+  double dinv[NU];
+  __device__ __forceinline__ void factor(const double (&h)[NU][NU], double mu) {
+    double t[NU][NU];  // t[i][k] = L[i][k] · D[k]
+#pragma unroll
+    for (int k = 0; k < NU; ++k) {
+      double dk = h[k][k] + mu;
+#pragma unroll
+      for (int p = 0; p < k; ++p) dk = fma(-l[k][p], t[k][p], dk);
+      dinv[k] = rcp(dk);
+#pragma unroll
+      for (int i = k + 1; i < NU; ++i) {
+        double v = h[i][k];
+#pragma unroll
+        for (int p = 0; p < k; ++p) v = fma(-l[i][p], t[k][p], v);
+        t[i][k] = v;
+        l[i][k] = v * dinv[k];
+      }
+    }
+  }
+  __device__ __forceinline__ d4 solve(d4 x) const {
+#pragma unroll
+    for (int i = 0; i < NU; ++i)
+#pragma unroll
+      for (int p = 0; p < i; ++p) x[i] = fma(-l[i][p], x[p], x[i]);
+#pragma unroll
+    for (int i = 0; i < NU; ++i) x[i] *= dinv[i];
+#pragma unroll
+    for (int i = NU - 1; i >= 0; --i)
+#pragma unroll
+      for (int p = i + 1; p < NU; ++p) x[i] = fma(-l[p][i], x[p], x[i]);
+    return x;
+  }
+};
+
+// ---------------------------------------------------------------------------
+// Backward pass of one trajectory by one wave (backward_pass.jl:324-357).
+// Writes d (T,NU) and K (T,NU,NX) of trajectory b. Returns true if any gain is NaN
+// (the reference's @assert !any(isnan, δu/K), :353-354).
+// ---------------------------------------------------------------------------
+template <int NX, int NU>
+__device__ bool lq_backward_wave(const LQParams& P, int b, int T, const double* __restrict__ x,
+                                 const double* __restrict__ u, double* __restrict__ d_out,
+                                 double* __restrict__ K_out, double mu, double* lds) {
+  static_assert(NX + NU <= 16 && NX < 16 && NU <= 4, "MFMA tile mapping needs nx+nu <= 16, nu <= 4");
+  constexpr int KS = (NX + 3) / 4;  // k-steps of 4 over the state dimension
+  constexpr int SROW = NX;          // row/column of Sp holding s
+  const int l = threadIdx.x & 63;
+  const int c = l & 15;
+  const int q = l >> 4;
+  const bool cx = c < NX;                  // state column
+  const bool cu = c >= NX && c < NX + NU;  // input column
+  const int ci = cx ? c : 0;
+  const int cj = cu ? c - NX : 0;
+
+  const double* Ab = P.A + (size_t)b * NX * NX;
+  const double* Bb = P.B + (size_t)b * NX * NU;
+  const double* Qb = P.Q + (size_t)b * NX * NX;
+  const double* Rb = P.R + (size_t)b * NU * NU;
+  const double* Qfb = P.Qf + (size_t)b * NX * NX;
+
+  // F fragments (A- and B-operand of the same MFMA family): fB[kk] = F[4kk+q][c], F = [A | B]
+  double fB[KS];
+#pragma unroll
+  for (int kk = 0; kk < KS; ++kk) {
+    const int i = 4 * kk + q;
+    const bool ri = i < NX;
+    const int ii = ri ? i : 0;
+    const double a = ldz(ri && cx, Ab + ii * NX + ci, Ab);
+    const double bb = ldz(ri && cu, Bb + ii * NU + cj, Bb);
+    fB[kk] = a + bb;
+  }
+  // Cost Hessian L = blockdiag(Q+Qᵀ, R+Rᵀ) in accumulator layout: Lc[r] = L[q+4r][c]
+  // (immediate_cost_quadratization :101-106 of ℓ = xᵀQx + uᵀRu: 𝐐 = Q+Qᵀ, 𝐑 = R+Rᵀ, 𝐏 = 0)
+  d4 Lc;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int i = q + 4 * r;
+    const bool rx = i < NX, ru = i >= NX && i < NX + NU;
+    const int ix = rx ? i : 0, iu = ru ? i - NX : 0;
+    const double lq = ldz(rx && cx, Qb + ix * NX + ci, Qb) + ldz(rx && cx, Qb + ci * NX + ix, Qb);
+    const double lr = ldz(ru && cu, Rb + iu * NU + cj, Rb) + ldz(ru && cu, Rb + cj * NU + iu, Rb);
+    Lc[r] = lq + lr;
+  }
+
+  double* Gl = lds;       // Gl[j*16 + c] = Z[NX+j][c]   (j < NU): [G | H] rows
+  double* gl = lds + 64;  // gl[c] = (L z + Fᵀ s)[c]:   [lx + Aᵀs | lu + Bᵀs]
+
+  // Terminal value function (final_cost_quadratization :134-153, ℓ_f = xᵀQf x):
+  // S = Qf+Qfᵀ, s = (Qf+Qfᵀ) x_N.
+  const double* xN = x + ((size_t)b * (T + 1) + T) * NX;
+  d4 Sp;
+  {
+    double part = 0.0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = q + 4 * r;
+      const bool rx = i < NX;
+      const int ix = rx ? i : 0;
+      const double v = ldz(rx && cx, Qfb + ix * NX + ci, Qfb) + ldz(rx && cx, Qfb + ci * NX + ix, Qfb);
+      Sp[r] = v;
+      part = fma(v, ldz(rx, xN + ix, xN), part);
+    }
+    const double sc = colsum4(part);  // s[c] for c < NX
+    if (q == 0) gl[c] = sc;
+    wave_lds_fence();
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = q + 4 * r;
+      const double sv = gl[i < NX ? i : 0];
+      if (c == SROW && i < NX) Sp[r] = sv;
+    }
+    wave_lds_fence();
+  }
+
+  bool nan = false;
+  // gradient operands z = [x_t; u_t] at rows q+4r, prefetched one step ahead
+  auto load_z = [&](int t) {
+    const double* xt = x + ((size_t)b * (T + 1) + t) * NX;
+    const double* ut = u + ((size_t)b * T + t) * NU;
+    d4 z;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = q + 4 * r;
+      const bool rx = i < NX, ru = i >= NX && i < NX + NU;
+      const double* p = rx ? xt + i : (ru ? ut + (i - NX) : xt);
+      const double v = *p;
+      z[r] = (rx || ru) ? v : 0.0;
+    }
+    return z;
+  };
+  d4 zc = load_z(T - 1);
+  double* Kb = K_out + (size_t)b * T * NU * NX;
+  double* db = d_out + (size_t)b * T * NU;
+
+  for (int t = T - 1; t >= 0; --t) {
+    const d4 zn = load_z(t > 0 ? t - 1 : 0);
+
+    // Y = Sp · F (optimal_controller_param's S'A, S'B and the row sᵀF)
+    d4 Y = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk) Y = mfma(Sp[kk], fB[kk], Y);
+    // Z = L + Fᵀ Y = [[lxx + AᵀSA, AᵀSB], [BᵀSA, luu + BᵀSB]]  (:182-183, first terms of :270)
+    d4 Z = Lc;
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk) Z = mfma(fB[kk], Y[kk], Z);
+
+    // gq[c] = (L z)[c] + (Fᵀ s)[c]: lx + Aᵀs (c < NX), g = lu + Bᵀs (c ≥ NX)  (:181, :269)
+    double part = 0.0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      part = fma(Lc[r], zc[r], part);
+      if (r == SROW / 4) part += (q == SROW % 4) ? Y[r] : 0.0;
+    }
+    const double gq = colsum4(part);
+
+    // hand the NU rows [G | H] and g to every lane
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = q + 4 * r;
+      if (i >= NX && i < NX + NU) Gl[(i - NX) * 16 + c] = Z[r];
+    }
+    if (q == 0) gl[c] = gq;
+    wave_lds_fence();
+    double h[NU][NU];
+#pragma unroll
+    for (int i = 0; i < NU; ++i)
+#pragma unroll
+      for (int k = 0; k <= i; ++k) h[i][k] = Gl[i * 16 + NX + k];
+    d4 col = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int j = 0; j < NU; ++j) {
+      const double Gj = Gl[j * 16 + c];
+      const double gj = gl[NX + j];
+      col[j] = cx ? Gj : (c == SROW ? gj : 0.0);
+    }
+    const int qq = q < NU ? q : 0;
+    const double Gq = Gl[qq * 16 + c];
+    const double gqq = gl[NX + qq];
+    const double colq = cx ? Gq : (c == SROW ? gqq : 0.0);
+    double qv[KS];
+#pragma unroll
+    for (int r = 0; r < KS; ++r) {
+      const int i = q + 4 * r;
+      const double gv = gl[i < NX ? i : 0];
+      qv[r] = (i < NX) ? gv : 0.0;
+    }
+    wave_lds_fence();
+
+    // feedback_parameters (:207-218): K_aug[:,c] = -(H + μI)⁻¹ [G | g][:,c]
+    LDLT<NU> f;
+    f.factor(h, mu);
+    const d4 xs = f.solve(col);
+    const double kq = (q < NU) ? -xs[qq] : 0.0;              // K_aug[q][c]
+    const double wk = (q < NU) ? fma(mu, kq, -colq) : 0.0;   // ((H + 2μI) K_aug)[q][c]
+    nan |= __builtin_isnan(kq);
+
+    if (q < NU) {
+      if (cx) Kb[((size_t)t * NU + q) * NX + c] = kq;
+      else if (c == SROW) db[(size_t)t * NU + q] = kq;
+    }
+
+    // step_back (:269-270): Sp ← [Qxx | lx + Aᵀs] − K_augᵀ (H + 2μI) K_aug
+    d4 Cin;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      double v = 0.0;
+      if (r < KS) v = cx ? Z[r] : (c == SROW ? qv[r] : 0.0);
+      Cin[r] = (q + 4 * r < NX) ? v : 0.0;
+    }
+    Sp = mfma(-kq, wk, Cin);
+    zc = zn;
+  }
+  return __any(nan);
+}
+
+// ---------------------------------------------------------------------------
+// Forward pass of up to 4 trajectories by one wave, 16 lanes each
+// (forward_pass.jl:55-93, total_cost :182-196).
+// ---------------------------------------------------------------------------
+struct FwdOut {
+  double cost;
+  int trials;
+  int accepted;  // 1 accepted, 0 exhausted / NaN
+};
+
+template <int NX, int NU>
+__device__ FwdOut lq_forward_group(const LQParams& P, int b, int T, const double* __restrict__ x,
+                                   const double* __restrict__ u, const double* __restrict__ xtraj,
+                                   const double* __restrict__ dg, const double* __restrict__ Kg,
+                                   double prev_cost, double* __restrict__ xnew,
+                                   double* __restrict__ unew, double* du2_out,
+                                   const LSParams& ls, double* lds) {
+  static_assert(NX + NU <= 16, "one 16-lane group per trajectory");
+  const int j = threadIdx.x & 15;
+  const bool is_x = j < NX;
+  const bool is_u = (j >= NX) && (j < NX + NU);
+  const int iu = j - NX;
+
+  const double* Ab = P.A + (size_t)b * NX * NX;
+  const double* Bb = P.B + (size_t)b * NX * NU;
+  const double* Qb = P.Q + (size_t)b * NX * NX;
+  const double* Rb = P.R + (size_t)b * NU * NU;
+  const double* Qfb = P.Qf + (size_t)b * NX * NX;
+
+  // row j of F = [A B] (lanes j < NX) and of L = blockdiag(Q, R) (ℓ = vᵀ L v)
+  double Fr[NX + NU], Lr[NX + NU];
+#pragma unroll
+  for (int k = 0; k < NX + NU; ++k) {
+    double f = 0.0, lv = 0.0;
+    if (is_x) {
+      f = (k < NX) ? Ab[j * NX + k] : Bb[j * NU + (k - NX)];
+      lv = (k < NX) ? Qb[j * NX + k] : 0.0;
+    } else if (is_u && k >= NX) {
+      lv = Rb[iu * NU + (k - NX)];
+    }
+    Fr[k] = f;
+    Lr[k] = lv;
+  }
+
+  double* dxl = lds;        // δx row
+  double* zl = lds + 16;    // z = [x̄; ū]
+  double* vl = lds + 32;    // v = [x̄ - x_traj; ū]
+
+  const double* xb0 = x + (size_t)b * (T + 1) * NX;
+  const double* ub0 = u + (size_t)b * T * NU;
+  const double* xt0 = xtraj ? xtraj + (size_t)b * (T + 1) * NX : nullptr;
+  const double* d0 = dg + (size_t)b * T * NU;
+  const double* K0 = Kg + (size_t)b * T * NU * NX;
+  double* xo = xnew + (size_t)b * (T + 1) * NX;
+  double* uo = unew + (size_t)b * T * NU;
+
+  double alpha = ls.alpha0;
+  FwdOut out{0.0, 0, 0};
+  double du2 = 0.0;
+  for (int trial = 1; trial <= ls.max_trials; ++trial) {
+    double xb = is_x ? xb0[j] : 0.0;  // x̄₁ = x₁ (:65)
+    double cost = 0.0;
+    du2 = 0.0;
+    for (int t = 0; t < T; ++t) {
+      const double xr = is_x ? xb0[(size_t)t * NX + j] : 0.0;
+      // δx = x̄ₖ − xₖ (:72)
+      if (is_x) dxl[j] = xb - xr;
+      wave_lds_fence();
+      double ub = 0.0, ur = 0.0;
+      if (is_u) {
+        ur = ub0[(size_t)t * NU + iu];
+        const double* Kr = K0 + ((size_t)t * NU + iu) * NX;
+        double acc = 0.0;
+#pragma unroll
+        for (int k = 0; k < NX; ++k) acc = fma(Kr[k], dxl[k], acc);
+        // ūₖ = uₖ + α δuₖ + Kₖ δx (:73) — α scales δu only
+        ub = fma(alpha, d0[(size_t)t * NU + iu], ur) + acc;
+      }
+      const double z = is_x ? xb : ub;
+      const double v = is_x ? (xt0 ? xb - xt0[(size_t)t * NX + j] : xb) : ub;
+      zl[j] = z;
+      vl[j] = v;
+      wave_lds_fence();
+      // ℓ(x̄ₖ − x_trajₖ, ūₖ) (:187-190)
+      double lv = 0.0, xn = 0.0;
+#pragma unroll
+      for (int k = 0; k < NX + NU; ++k) {
+        lv = fma(Lr[k], vl[k], lv);
+        xn = fma(Fr[k], zl[k], xn);  // x̄ₖ₊₁ = f(x̄ₖ, ūₖ) (:74)
+      }
+      wave_lds_fence();
+      cost = fma(v, lv, cost);
+      if (is_x) xo[(size_t)t * NX + j] = xb;
+      if (is_u) {
+        uo[(size_t)t * NU + iu] = ub;
+        const double e = ub - ur;
+        du2 = fma(e, e, du2);
+      }
+      xb = xn;
+    }
+    // final cost on raw x̄_N (:192)
+    if (is_x) {
+      xo[(size_t)T * NX + j] = xb;
+      zl[j] = xb;
+    }
+    wave_lds_fence();
+    double lf = 0.0;
+    if (is_x) {
+#pragma unroll
+      for (int k = 0; k < NX; ++k) lf = fma(Qfb[j * NX + k], zl[k], lf);
+      cost = fma(xb, lf, cost);
+    }
+    wave_lds_fence();
+    cost = rowsum16(cost);
+    out.trials = trial;
+    out.cost = cost;
+    if (prev_cost - cost > 0.0) {  // (:77-80); NaN compares false → keep searching
+      out.accepted = 1;
+      break;
+    }
+    alpha *= ls.shrink;  // (:82)
+  }
+  if (du2_out) *du2_out = rowsum16(du2);
+  return out;
+}
+
+// ---------------------------------------------------------------------------
+// Kernels
+// ---------------------------------------------------------------------------
+template <int NX, int NU>
+__global__ __launch_bounds__(256) void lq_backward_kernel(LQParams P, int B, int T,
+                                                          const double* __restrict__ x,
+                                                          const double* __restrict__ u,
+                                                          double* __restrict__ d,
+                                                          double* __restrict__ K,
+                                                          int32_t* __restrict__ status, double mu) {
+  __shared__ __attribute__((aligned(16))) double lds[WAVES_PER_WG * BW_LDS];
+  const int w = threadIdx.x >> 6;
+  const int b = blockIdx.x * WAVES_PER_WG + w;
+  if (b >= B) return;
+  const bool nan = lq_backward_wave<NX, NU>(P, b, T, x, u, d, K, mu, lds + w * BW_LDS);
+  if (status && (threadIdx.x & 63) == 0) status[b] = nan ? ILQR_TRAJ_NAN : ILQR_TRAJ_OK;
+}
+
+template <int NX, int NU>
+__global__ __launch_bounds__(64) void lq_forward_kernel(
+    LQParams P, int B, int T, const double* __restrict__ x, const double* __restrict__ u,
+    const double* __restrict__ xtraj, const double* __restrict__ d, const double* __restrict__ K,
+    const double* __restrict__ prev_cost, double* __restrict__ xnew, double* __restrict__ unew,
+    double* __restrict__ new_cost, int32_t* __restrict__ trials, int32_t* __restrict__ status,
+    LSParams ls) {
+  __shared__ __attribute__((aligned(16))) double lds[4 * FW_LDS];
+  const int g = threadIdx.x >> 4;
+  const int j = threadIdx.x & 15;
+  const int b = blockIdx.x * 4 + g;
+  if (b >= B) return;  // whole 16-lane group: no cross-group LDS traffic
+  const double pc = prev_cost ? prev_cost[b] : INFINITY;
+  FwdOut r = lq_forward_group<NX, NU>(P, b, T, x, u, xtraj, d, K, pc, xnew, unew, nullptr, ls,
+                                      lds + g * FW_LDS);
+  if (!r.accepted) {
+    // line search exhausted (the reference would loop forever): return the inputs.
+    // Lanes of a group write disjoint elements; nothing reads them in this launch.
+    for (int i = j; i < (T + 1) * NX; i += 16) xnew[(size_t)b * (T + 1) * NX + i] = x[(size_t)b * (T + 1) * NX + i];
+    for (int i = j; i < T * NU; i += 16) unew[(size_t)b * T * NU + i] = u[(size_t)b * T * NU + i];
+  }
+  if (j == 0) {
+    new_cost[b] = r.cost;
+    if (trials) trials[b] = r.trials;
+    if (status) status[b] = r.accepted ? ILQR_TRAJ_OK
+                                       : (r.cost != r.cost ? ILQR_TRAJ_NAN : ILQR_TRAJ_LS_EXHAUSTED);
+  }
+}
+
+// One fit iteration (forward_pass.jl:161-176), part 1: backward_pass for every
+// trajectory whose status is OK (4 waves / workgroup, one trajectory per wave).
+template <int NX, int NU>
+__global__ __launch_bounds__(256) void lq_iter_backward_kernel(LQParams P, int B, int T, IterArgs a,
+                                                               double mu) {
+  __shared__ __attribute__((aligned(16))) double lds[WAVES_PER_WG * BW_LDS];
+  const int w = threadIdx.x >> 6;
+  const int b = blockIdx.x * WAVES_PER_WG + w;
+  if (b >= B || a.status[b] != ILQR_TRAJ_OK) return;
+  const bool nan = lq_backward_wave<NX, NU>(P, b, T, a.x, a.u, a.d, a.K, mu, lds + w * BW_LDS);
+  if (nan && (threadIdx.x & 63) == 0) {
+    a.status[b] = ILQR_TRAJ_NAN;  // reference: AssertionError at backward_pass.jl:353
+    if (a.res_parity) a.res_parity[b] = a.parity;
+  }
+}
+
+// Part 2: forward_pass + line search + the convergence test (:163-175), four
+// trajectories per wave. The backward and forward are separate launches so the
+// backward keeps its 4 waves/SIMD register budget (≤128 VGPRs).
+template <int NX, int NU>
+__global__ __launch_bounds__(64) void lq_iter_forward_kernel(LQParams P, int B, int T, IterArgs a,
+                                                             LSParams ls) {
+  __shared__ __attribute__((aligned(16))) double lds[4 * FW_LDS];
+  const int g = threadIdx.x >> 4;
+  const int j = threadIdx.x & 15;
+  const int b = blockIdx.x * 4 + g;
+  if (b >= B || a.status[b] != ILQR_TRAJ_OK) return;
+  double du2 = 0.0;
+  const FwdOut r = lq_forward_group<NX, NU>(P, b, T, a.x, a.u, a.xtraj, a.d, a.K, a.prev_cost[b],
+                                            a.xnew, a.unew, &du2, ls, lds + g * FW_LDS);
+  if (j == 0) {
+    if (a.trials) a.trials[b] = r.trials;
+    if (a.du2) a.du2[b] = du2;
+    if (a.iters) a.iters[b] = a.iter;
+    if (!r.accepted) {
+      a.status[b] = (r.cost != r.cost) ? ILQR_TRAJ_NAN : ILQR_TRAJ_LS_EXHAUSTED;
+      if (a.res_parity) a.res_parity[b] = a.parity;
+    } else {
+      a.prev_cost[b] = r.cost;  // @assert(prev_cost > new_cost); prev_cost = new_cost (:168)
+      if (du2 <= ls.tol) {      // (:171) break BEFORE the update → result is the input iterate
+        a.status[b] = ILQR_TRAJ_CONVERGED;
+        if (a.res_parity) a.res_parity[b] = a.parity;
+      }
+    }
+  }
+}
+
+__global__ void gather_kernel(int B, int T, int nx, int nu, const double* x0, const double* u0,
+                              const double* x1, const double* u1, const int32_t* res_parity,
+                              int32_t* status, int final_parity, double* x_out, double* u_out) {
+  const int b = blockIdx.x;
+  if (b >= B) return;
+  const bool running = status[b] == ILQR_TRAJ_OK;
+  const int par = running ? final_parity : res_parity[b];
+  const double* xs = (par ? x1 : x0) + (size_t)b * (T + 1) * nx;
+  const double* us = (par ? u1 : u0) + (size_t)b * T * nu;
+  for (int i = threadIdx.x; i < (T + 1) * nx; i += blockDim.x) x_out[(size_t)b * (T + 1) * nx + i] = xs[i];
+  for (int i = threadIdx.x; i < T * nu; i += blockDim.x) u_out[(size_t)b * T * nu + i] = us[i];
+  if (threadIdx.x == 0 && running) status[b] = ILQR_TRAJ_MAX_ITER;
+}
+
+__global__ void fill_i32_kernel(int32_t* p, int n, int32_t v) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = v;
+}
+__global__ void fill_f64_kernel(double* p, int n, double v) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = v;
+}
+
+// -------- self-test of the lane maps the kernels depend on -------------------
+__global__ void selftest_kernel(int32_t* fails) {
+  const int l = threadIdx.x;
+  const int c = l & 15, q = l >> 4;
+  int bad = 0;
+  // permlane all-reduces
+  const double v = (double)(l * l + 1);
+  const double s16 = xor16_sum(v), s32 = xor32_sum(v), s4 = colsum4(v);
+  const double e16 = v + (double)((l ^ 16) * (l ^ 16) + 1);
+  const double e32 = v + (double)((l ^ 32) * (l ^ 32) + 1);
+  double e4 = 0;
+  for (int k = 0; k < 4; ++k) e4 += (double)((c + 16 * k) * (c + 16 * k) + 1);
+  bad += (s16 != e16) + (s32 != e32) + (s4 != e4);
+  // MFMA f64 16x16x4: A-operand lane l = A[l&15][l>>4], B = B[l>>4][l&15],
+  // C/D reg r of lane l = D[(l>>4) + 4r][l&15]. Use asymmetric integer data.
+  const double Aij = (double)(c * 7 + q * 3 + 1);   // A[c][q]
+  const double Bij = (double)(q * 5 + c * 2 + 2);   // B[q][c]
+  d4 acc = {0, 0, 0, 0};
+  acc = mfma(Aij, Bij, acc);
+  for (int r = 0; r < 4; ++r) {
+    const int i = q + 4 * r, jj = c;
+    double e = 0;
+    for (int k = 0; k < 4; ++k) e += (double)(i * 7 + k * 3 + 1) * (double)(k * 5 + jj * 2 + 2);
+    bad += (acc[r] != e);
+  }
+  // row-16 shuffle sum
+  const double rs = rowsum16((double)l);
+  double er = 0;
+  for (int k = 0; k < 16; ++k) er += (double)((l & ~15) + k);
+  bad += (rs != er);
+  if (bad) atomicAdd(fails, bad);
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// Launchers
+// ---------------------------------------------------------------------------
+bool lq_supported(int nx, int nu) { return nx == 12 && nu == 4; }
+
+#define ILQR_DISPATCH(NXV, NUV, CALL)            \
+  if (nx == NXV && nu == NUV) {                  \
+    constexpr int NX_ = NXV, NU_ = NUV;          \
+    CALL;                                        \
+    return hipGetLastError();                    \
+  }
+
+hipError_t launch_lq_backward(int nx, int nu, const LQParams& p, int B, int T, const double* x,
+                              const double* u, double* d, double* K, int32_t* status, double mu,
+                              hipStream_t s) {
+  const int grid = (B + WAVES_PER_WG - 1) / WAVES_PER_WG;
+  ILQR_DISPATCH(12, 4, (lq_backward_kernel<NX_, NU_><<<grid, 256, 0, s>>>(p, B, T, x, u, d, K, status, mu)));
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_lq_forward(int nx, int nu, const LQParams& p, int B, int T, const double* x,
+                             const double* u, const double* xtraj, const double* d,
+                             const double* K, const double* prev_cost, double* xnew,
+                             double* unew, double* new_cost, int32_t* trials, int32_t* status,
+                             const LSParams& ls, hipStream_t s) {
+  const int grid = (B + 3) / 4;
+  ILQR_DISPATCH(12, 4, (lq_forward_kernel<NX_, NU_><<<grid, 64, 0, s>>>(p, B, T, x, u, xtraj, d, K, prev_cost, xnew, unew, new_cost, trials, status, ls)));
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_lq_iterate(int nx, int nu, const LQParams& p, int B, int T, const IterArgs& a,
+                             const LSParams& ls, hipStream_t s) {
+  const int grid = (B + WAVES_PER_WG - 1) / WAVES_PER_WG;
+  ILQR_DISPATCH(12, 4, (lq_iter_backward_kernel<NX_, NU_><<<grid, 256, 0, s>>>(p, B, T, a, ls.mu),
+                        lq_iter_forward_kernel<NX_, NU_><<<(B + 3) / 4, 64, 0, s>>>(p, B, T, a, ls)));
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_gather_result(int B, int T, int nx, int nu, const double* x0, const double* u0,
+                                const double* x1, const double* u1, const int32_t* res_parity,
+                                int32_t* status, int final_parity, double* x_out, double* u_out,
+                                hipStream_t s) {
+  gather_kernel<<<B, 256, 0, s>>>(B, T, nx, nu, x0, u0, x1, u1, res_parity, status, final_parity,
+                                  x_out, u_out);
+  return hipGetLastError();
+}
+
+hipError_t launch_fill_i32(int32_t* p, int n, int32_t v, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  fill_i32_kernel<<<(n + 255) / 256, 256, 0, s>>>(p, n, v);
+  return hipGetLastError();
+}
+hipError_t launch_fill_f64(double* p, int n, double v, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  fill_f64_kernel<<<(n + 255) / 256, 256, 0, s>>>(p, n, v);
+  return hipGetLastError();
+}
+
+int run_selftest(int device) {
+  if (hipSetDevice(device) != hipSuccess) return -1;
+  int32_t* f = nullptr;
+  if (hipMalloc(&f, sizeof(int32_t)) != hipSuccess) return -1;
+  int32_t h = 0;
+  if (hipMemset(f, 0, sizeof(int32_t)) != hipSuccess) return -1;
+  selftest_kernel<<<1, 64>>>(f);
+  if (hipGetLastError() != hipSuccess) return -1;
+  if (hipMemcpy(&h, f, sizeof(int32_t), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  (void)hipFree(f);
+  return h;
+}
+
+}  // namespace ilqr

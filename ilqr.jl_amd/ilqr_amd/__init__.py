@@ -1,0 +1,20 @@
+"""ilqr_amd — MI355X-native batched iLQR (host-side mirror of aabouman/iLQR.jl's
+`iLQR` module over the C ABI of libilqr_hip.so; see include/ilqr.h)."""
+from .problems import (LinearDynamics, LQBatch, QuadraticCost, QuadraticFinalCost,
+                       lq_from_closures, quadrotor_batch, quadrotor_instance, random_lq_batch)
+
+__all__ = ["LinearDynamics", "QuadraticCost", "QuadraticFinalCost", "LQBatch",
+           "lq_from_closures", "quadrotor_batch", "quadrotor_instance", "random_lq_batch",
+           "fit", "backward_pass", "forward_pass", "Solver", "selftest", "LineSearchExhausted"]
+
+
+def __getattr__(name):
+    # the device API needs torch + libilqr_hip.so; import it lazily so problem
+    # definitions stay usable without them
+    if name in ("fit", "backward_pass", "forward_pass", "LineSearchExhausted"):
+        from . import api
+        return getattr(api, name)
+    if name in ("Solver", "selftest", "FitResult"):
+        from . import solver
+        return getattr(solver, name)
+    raise AttributeError(name)

@@ -1,0 +1,114 @@
+"""ctypes binding of libilqr_hip.so (include/ilqr.h).
+
+The library is built in-tree (ilqr.jl_amd/lib/libilqr_hip.so) by
+`make -C ilqr.jl_amd/csrc` or `__graft_entry__.build()`. There is no fallback:
+if the library is missing, importing the device API raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "lib",
+                        "libilqr_hip.so")
+
+# ilqr_status
+OK = 0
+ERR_BAD_DIMS = 1
+ERR_BAD_ARG = 2
+ERR_UNSUPPORTED = 3
+ERR_HIP = 4
+ERR_NAN = 5
+ERR_LS_EXHAUSTED = 6
+
+# per-trajectory status
+TRAJ_OK = 0
+TRAJ_CONVERGED = 1
+TRAJ_MAX_ITER = 2
+TRAJ_LS_EXHAUSTED = 3
+TRAJ_NAN = 4
+
+PROBLEM_LQ = 1
+
+
+class Problem(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("reserved", C.c_int32),
+                ("A", C.c_void_p), ("B", C.c_void_p), ("Q", C.c_void_p),
+                ("R", C.c_void_p), ("Qf", C.c_void_p)]
+
+
+class Options(C.Structure):
+    _fields_ = [("max_iter", C.c_int32), ("max_trials", C.c_int32), ("tol", C.c_double),
+                ("mu", C.c_double), ("alpha0", C.c_double), ("shrink", C.c_double)]
+
+
+# every symbol declared in include/ilqr.h, with its ctypes signature
+P = C.c_void_p
+SIGNATURES = {
+    "ilqr_abi_version": (C.c_int, []),
+    "ilqr_status_string": (C.c_char_p, [C.c_int]),
+    "ilqr_last_error": (C.c_char_p, []),
+    "ilqr_default_options": (None, [C.POINTER(Options)]),
+    "ilqr_supported": (C.c_int, [C.c_int32, C.c_int, C.c_int]),
+    "ilqr_create": (C.c_int, [C.POINTER(P), C.c_int, C.c_int, C.c_int, C.c_int, C.c_int]),
+    "ilqr_destroy": (C.c_int, [P]),
+    "ilqr_set_stream": (C.c_int, [P, P]),
+    "ilqr_sync": (C.c_int, [P]),
+    "ilqr_backward": (C.c_int, [P, C.POINTER(Problem), C.POINTER(Options), P, P, P, P, P]),
+    "ilqr_forward": (C.c_int, [P, C.POINTER(Problem), C.POINTER(Options), P, P, P, P, P, P,
+                               P, P, P, P, P]),
+    "ilqr_iterate": (C.c_int, [P, C.POINTER(Problem), C.POINTER(Options), P, P, P, P, P, P,
+                               P, P, P]),
+    "ilqr_fit": (C.c_int, [P, C.POINTER(Problem), C.POINTER(Options), P, P, P, P, P, P, P, P]),
+    "ilqr_malloc": (C.c_int, [P, C.c_size_t, C.POINTER(P)]),
+    "ilqr_free": (C.c_int, [P, P]),
+    "ilqr_memcpy_h2d": (C.c_int, [P, P, P, C.c_size_t]),
+    "ilqr_memcpy_d2h": (C.c_int, [P, P, P, C.c_size_t]),
+    "ilqr_selftest": (C.c_int, [C.c_int, C.POINTER(C.c_int32)]),
+}
+
+_lib = None
+
+
+def load(path: str = LIB_PATH) -> C.CDLL:
+    """Load libilqr_hip.so and declare every exported signature (raises if absent)."""
+    global _lib
+    if _lib is not None and path == LIB_PATH:
+        return _lib
+    if not os.path.exists(path):
+        raise ImportError(f"{path} not built: run `make -C ilqr.jl_amd/csrc` "
+                          "(the HIP path has no CPU fallback)")
+    lib = C.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.ilqr_abi_version() != 1:
+        raise ImportError("libilqr_hip.so ABI version mismatch")
+    if path == LIB_PATH:
+        _lib = lib
+    return lib
+
+
+class IlqrError(RuntimeError):
+    def __init__(self, status: int, where: str):
+        lib = load()
+        msg = lib.ilqr_status_string(status).decode()
+        extra = lib.ilqr_last_error().decode()
+        super().__init__(f"{where}: {msg}" + (f" ({extra})" if extra and status == ERR_HIP else ""))
+        self.status = status
+
+
+def check(status: int, where: str, allow=()) -> int:
+    if status != OK and status not in allow:
+        raise IlqrError(status, where)
+    return status
+
+
+def default_options(**overrides) -> Options:
+    o = Options()
+    load().ilqr_default_options(C.byref(o))
+    for k, v in overrides.items():
+        if v is not None:
+            setattr(o, k, v)
+    return o

@@ -1,0 +1,144 @@
+"""Host-side mirror of the reference API (aabouman/iLQR.jl, module `iLQR`), backed
+by the HIP kernels — same names, argument meaning and error behaviour:
+
+  fit(x_init, u_init, dynamicsf, immediate_cost, final_cost; x_traj, max_iter, tol)
+        /root/reference/src/forward_pass.jl:148-179
+  backward_pass(x, u, dynamicsf, immediate_cost, final_cost) -> (δu, K)
+        /root/reference/src/backward_pass.jl:324-357
+  forward_pass(x, u, x_traj, δu, K, prev_cost, dynamicsf, immediate_cost, final_cost)
+        -> (x̄, ū, new_cost)      /root/reference/src/forward_pass.jl:55-93
+
+Arrays follow the reference's per-trajectory layout (x: (N, nx) rows = time
+steps, u: (T, nu), δu: (T, nu), K: (T, nu, nx)); a leading batch dimension
+solves many independent problems at once. numpy inputs are copied to the GPU
+and results copied back; torch CUDA inputs stay on the device.
+
+Errors mirror the reference: AssertionError for N ≠ M+1 (backward_pass.jl:329,
+forward_pass.jl:62,156) and for NaNs (backward_pass.jl:353-354,
+forward_pass.jl:89-90), TypeError for a non-integer max_iter
+(forward_pass.jl:152). The reference's unbounded line search (:70-87) is capped
+(`max_trials`); an exhausted search raises `LineSearchExhausted` in
+forward_pass and, in fit, stops that trajectory at its current iterate.
+"""
+from __future__ import annotations
+
+import warnings
+
+import numpy as np
+import torch
+
+from . import _lib
+from .problems import lq_from_closures
+from .solver import Solver
+
+
+class LineSearchExhausted(RuntimeError):
+    pass
+
+
+def _device():
+    if not torch.cuda.is_available():
+        raise RuntimeError("the iLQR HIP path needs a GPU (no CPU fallback)")
+    return torch.cuda.current_device()
+
+
+def _as_batch(a, name, ndim):
+    """→ (device tensor with leading batch dim, was_batched, was_torch)."""
+    is_t = isinstance(a, torch.Tensor)
+    t = a if is_t else torch.from_numpy(np.ascontiguousarray(np.asarray(a, dtype=np.float64)))
+    if t.dim() == ndim:
+        t, batched = t.unsqueeze(0), False
+    elif t.dim() == ndim + 1:
+        batched = True
+    else:
+        raise AssertionError(f"{name}: expected {ndim} or {ndim + 1} dimensions")
+    t = t.to(device=_device(), dtype=torch.float64).contiguous()
+    return t, batched, is_t
+
+
+def _out(t, batched, as_torch):
+    if not batched:
+        t = t[0]
+    return t if as_torch else t.cpu().numpy()
+
+
+def _solver(xb, ub, dynamicsf, immediate_cost, final_cost):
+    nb, N, nx = xb.shape
+    _, M, nu = ub.shape
+    assert N == M + 1, "size(x)[1] == size(u)[1] + 1"   # backward_pass.jl:329
+    assert ub.shape[0] == nb, "batch sizes differ"
+    lq = lq_from_closures(dynamicsf, immediate_cost, final_cost, nb)
+    if (lq.nx, lq.nu) != (nx, nu):
+        raise AssertionError(f"problem is ({lq.nx}, {lq.nu}) but x/u are ({nx}, {nu})")
+    s = Solver(nx, nu, M, nb, device=_device())
+    s.set_problem(lq)
+    return s
+
+
+def backward_pass(x, u, dynamicsf, immediate_cost, final_cost):
+    """→ (δu, K) exactly like iLQR.backward_pass (backward_pass.jl:324-357)."""
+    xb, batched, is_t = _as_batch(x, "x", 2)
+    ub, _, _ = _as_batch(u, "u", 2)
+    s = _solver(xb, ub, dynamicsf, immediate_cost, final_cost)
+    d, K, st = s.backward(xb, ub)
+    s.close()
+    if bool((st == _lib.TRAJ_NAN).any()):
+        raise AssertionError("!any(isnan, δu/K) failed")   # backward_pass.jl:353-354
+    return _out(d, batched, is_t), _out(K, batched, is_t)
+
+
+def forward_pass(x, u, x_traj, du, K, prev_cost, dynamicsf, immediate_cost, final_cost,
+                 max_trials=None):
+    """→ (x̄, ū, new_cost) exactly like iLQR.forward_pass (forward_pass.jl:55-93)."""
+    xb, batched, is_t = _as_batch(x, "x", 2)
+    ub, _, _ = _as_batch(u, "u", 2)
+    nb, N, nx = xb.shape
+    assert N == ub.shape[1] + 1, "size(x)[1] == size(u)[1] + 1"   # forward_pass.jl:62
+    xt, _, _ = _as_batch(x_traj if x_traj is not None else np.zeros((nb, N, nx)) if batched
+                         else np.zeros((N, nx)), "x_traj", 2)
+    db, _, _ = _as_batch(du, "du", 2)
+    Kb, _, _ = _as_batch(K, "K", 3)
+    pc = torch.as_tensor(np.broadcast_to(np.asarray(prev_cost, dtype=np.float64), (nb,)).copy()
+                         if not isinstance(prev_cost, torch.Tensor) else prev_cost,
+                         dtype=torch.float64).reshape(nb).to(xb.device).contiguous()
+    s = _solver(xb, ub, dynamicsf, immediate_cost, final_cost)
+    xn, un, cost, trials, st = s.forward(xb, ub, db, Kb, pc, x_traj=xt, max_trials=max_trials)
+    s.close()
+    if bool((st == _lib.TRAJ_NAN).any()):
+        raise AssertionError("!any(isnan, ū/x̄) failed")   # forward_pass.jl:89-90
+    if bool((st == _lib.TRAJ_LS_EXHAUSTED).any()):
+        raise LineSearchExhausted("no cost decrease within max_trials (the reference loops forever)")
+    c = cost if is_t else cost.cpu().numpy()
+    return _out(xn, batched, is_t), _out(un, batched, is_t), (c if batched else float(c[0]))
+
+
+def fit(x_init, u_init, dynamicsf, immediate_cost, final_cost, *, x_traj=None,
+        max_iter: int = 100, tol: float = 1e-6, return_info: bool = False):
+    """→ (x̄, ū) exactly like iLQR.fit (forward_pass.jl:148-179), including its
+    quirk of returning the iterate BEFORE the update that met `tol` (:171)."""
+    if not isinstance(max_iter, (int, np.integer)) or isinstance(max_iter, bool):
+        raise TypeError("max_iter::Int64")   # forward_pass.jl:152
+    xb, batched, is_t = _as_batch(x_init, "x_init", 2)
+    ub, _, _ = _as_batch(u_init, "u_init", 2)
+    nb, N, nx = xb.shape
+    assert N == ub.shape[1] + 1, "size(x_init)[2] == size(u_init)[1]"   # forward_pass.jl:156
+    xt = None
+    if x_traj is not None:
+        xt, _, _ = _as_batch(x_traj, "x_traj", 2)
+    s = _solver(xb, ub, dynamicsf, immediate_cost, final_cost)
+    r = s.fit(xb, ub, x_traj=xt, max_iter=int(max_iter), tol=float(tol))
+    s.close()
+    st = r.status.cpu().numpy()
+    if (st == _lib.TRAJ_NAN).any():
+        raise AssertionError("NaN in a trajectory (reference: AssertionError)")
+    if (st == _lib.TRAJ_LS_EXHAUSTED).any():
+        warnings.warn("line search exhausted for %d trajectories (the reference would loop "
+                      "forever); they return their last iterate" % int((st == _lib.TRAJ_LS_EXHAUSTED).sum()))
+    out = (_out(r.x, batched, is_t), _out(r.u, batched, is_t))
+    if return_info:
+        info = {"cost": r.cost.cpu().numpy(), "iters": r.iters.cpu().numpy(), "status": st}
+        return out + (info,)
+    return out
+
+
+__all__ = ["fit", "backward_pass", "forward_pass", "LineSearchExhausted"]

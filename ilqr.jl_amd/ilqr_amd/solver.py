@@ -1,0 +1,176 @@
+"""Device-resident batched iLQR solver: a thin owner of one ilqr_handle.
+
+All tensors handed to a Solver are torch CUDA (HIP) float64/int32 tensors,
+contiguous, laid out as include/ilqr.h documents (trajectory slowest). Calls
+are asynchronous on torch's current stream of the solver's device unless the
+method says it synchronises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import torch
+
+from . import _lib
+from .problems import LQBatch
+
+
+def _ptr(t):
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+def _req(t, dtype, shape, name):
+    if not isinstance(t, torch.Tensor) or t.device.type != "cuda":
+        raise TypeError(f"{name}: expected a CUDA tensor")
+    if t.dtype != dtype:
+        raise TypeError(f"{name}: expected {dtype}, got {t.dtype}")
+    if tuple(t.shape) != tuple(shape):
+        raise AssertionError(f"{name}: expected shape {tuple(shape)}, got {tuple(t.shape)}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name}: must be contiguous")
+    return t
+
+
+@dataclass
+class FitResult:
+    x: torch.Tensor        # (B, T+1, nx) returned iterate (reference semantics)
+    u: torch.Tensor        # (B, T, nu)
+    cost: torch.Tensor     # (B,) last accepted forward-pass cost
+    iters: torch.Tensor    # (B,) iterations run
+    status: torch.Tensor   # (B,) ILQR_TRAJ_* codes
+    call_status: int       # ilqr_status of the whole call
+
+
+class Solver:
+    def __init__(self, nx: int, nu: int, T: int, batch: int, device: int = 0):
+        self.lib = _lib.load()
+        if not self.lib.ilqr_supported(_lib.PROBLEM_LQ, nx, nu):
+            raise NotImplementedError(f"(nx, nu) = ({nx}, {nu}) has no compiled kernel")
+        self.nx, self.nu, self.T, self.batch, self.device = nx, nu, T, batch, device
+        self.dev = torch.device("cuda", device)
+        h = C.c_void_p()
+        _lib.check(self.lib.ilqr_create(C.byref(h), device, nx, nu, T, batch), "ilqr_create")
+        self.h = h
+        self._problem = None
+        self._keep = ()
+
+    # -- setup ---------------------------------------------------------------------
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.ilqr_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _bind_stream(self):
+        s = torch.cuda.current_stream(self.dev).cuda_stream
+        _lib.check(self.lib.ilqr_set_stream(self.h, C.c_void_p(s)), "ilqr_set_stream")
+
+    def set_problem(self, lq):
+        """lq: LQBatch (host numpy, copied to the device) or a dict of CUDA tensors
+        A (B,nx,nx), B (B,nx,nu), Q (B,nx,nx), R (B,nu,nu), Qf (B,nx,nx)."""
+        nb, nx, nu = self.batch, self.nx, self.nu
+        if isinstance(lq, LQBatch):
+            t = {k: torch.from_numpy(getattr(lq, k)).to(self.dev) for k in ("A", "B", "Q", "R", "Qf")}
+        else:
+            t = dict(lq)
+        shapes = {"A": (nb, nx, nx), "B": (nb, nx, nu), "Q": (nb, nx, nx), "R": (nb, nu, nu),
+                  "Qf": (nb, nx, nx)}
+        for k, s in shapes.items():
+            _req(t[k], torch.float64, s, k)
+        self._keep = tuple(t[k] for k in shapes)
+        self._problem = _lib.Problem(_lib.PROBLEM_LQ, 0, *(t[k].data_ptr() for k in shapes))
+
+    def _p(self):
+        if self._problem is None:
+            raise RuntimeError("set_problem() first")
+        return C.byref(self._problem)
+
+    def alloc_traj(self, zero=True):
+        f = torch.zeros if zero else torch.empty
+        return (f((self.batch, self.T + 1, self.nx), dtype=torch.float64, device=self.dev),
+                f((self.batch, self.T, self.nu), dtype=torch.float64, device=self.dev))
+
+    # -- passes ----------------------------------------------------------------------
+    def backward(self, x, u, mu=None):
+        """iLQR.backward_pass for the batch → (d (B,T,nu), K (B,T,nu,nx), status (B,)).
+        Synchronises (folds the per-trajectory NaN status)."""
+        B, T, nx, nu = self.batch, self.T, self.nx, self.nu
+        _req(x, torch.float64, (B, T + 1, nx), "x")
+        _req(u, torch.float64, (B, T, nu), "u")
+        d = torch.empty((B, T, nu), dtype=torch.float64, device=self.dev)
+        K = torch.empty((B, T, nu, nx), dtype=torch.float64, device=self.dev)
+        st = torch.empty((B,), dtype=torch.int32, device=self.dev)
+        self._bind_stream()
+        o = _lib.default_options(mu=mu)
+        rc = self.lib.ilqr_backward(self.h, self._p(), C.byref(o), _ptr(x), _ptr(u), _ptr(d),
+                                    _ptr(K), _ptr(st))
+        _lib.check(rc, "ilqr_backward", allow=(_lib.ERR_NAN,))
+        return d, K, st
+
+    def forward(self, x, u, d, K, prev_cost, x_traj=None, alpha0=None, shrink=None,
+                max_trials=None):
+        """iLQR.forward_pass for the batch → (x_new, u_new, new_cost, trials, status).
+        Synchronises."""
+        B, T, nx, nu = self.batch, self.T, self.nx, self.nu
+        _req(x, torch.float64, (B, T + 1, nx), "x")
+        _req(u, torch.float64, (B, T, nu), "u")
+        _req(d, torch.float64, (B, T, nu), "d")
+        _req(K, torch.float64, (B, T, nu, nx), "K")
+        _req(prev_cost, torch.float64, (B,), "prev_cost")
+        if x_traj is not None:
+            _req(x_traj, torch.float64, (B, T + 1, nx), "x_traj")
+        xn, un = self.alloc_traj(zero=False)
+        cost = torch.empty((B,), dtype=torch.float64, device=self.dev)
+        trials = torch.empty((B,), dtype=torch.int32, device=self.dev)
+        st = torch.empty((B,), dtype=torch.int32, device=self.dev)
+        self._bind_stream()
+        o = _lib.default_options(alpha0=alpha0, shrink=shrink, max_trials=max_trials)
+        rc = self.lib.ilqr_forward(self.h, self._p(), C.byref(o), _ptr(x), _ptr(u), _ptr(x_traj),
+                                   _ptr(d), _ptr(K), _ptr(prev_cost), _ptr(xn), _ptr(un),
+                                   _ptr(cost), _ptr(trials), _ptr(st))
+        _lib.check(rc, "ilqr_forward", allow=(_lib.ERR_NAN, _lib.ERR_LS_EXHAUSTED))
+        return xn, un, cost, trials, st
+
+    def iterate(self, x, u, x_new, u_new, prev_cost, status, du2=None, trials=None,
+                x_traj=None, options=None):
+        """One fit iteration (backward + forward + convergence test), asynchronous.
+        No shape checks beyond the ABI's: the bench's hot loop."""
+        o = options if options is not None else _lib.default_options()
+        rc = self.lib.ilqr_iterate(self.h, self._p(), C.byref(o), _ptr(x), _ptr(u), _ptr(x_traj),
+                                   _ptr(x_new), _ptr(u_new), _ptr(prev_cost), _ptr(du2),
+                                   _ptr(trials), _ptr(status))
+        _lib.check(rc, "ilqr_iterate")
+
+    def fit(self, x_init, u_init, x_traj=None, max_iter=100, tol=1e-6, mu=None,
+            max_trials=None) -> FitResult:
+        """iLQR.fit for the batch (synchronises)."""
+        if not isinstance(max_iter, int):
+            raise TypeError("max_iter::Int64")  # forward_pass.jl:152
+        B, T, nx, nu = self.batch, self.T, self.nx, self.nu
+        _req(x_init, torch.float64, (B, T + 1, nx), "x_init")
+        _req(u_init, torch.float64, (B, T, nu), "u_init")
+        if x_traj is not None:
+            _req(x_traj, torch.float64, (B, T + 1, nx), "x_traj")
+        xo, uo = self.alloc_traj(zero=False)
+        cost = torch.empty((B,), dtype=torch.float64, device=self.dev)
+        iters = torch.empty((B,), dtype=torch.int32, device=self.dev)
+        st = torch.empty((B,), dtype=torch.int32, device=self.dev)
+        self._bind_stream()
+        o = _lib.default_options(max_iter=max_iter, tol=float(tol), mu=mu, max_trials=max_trials)
+        rc = self.lib.ilqr_fit(self.h, self._p(), C.byref(o), _ptr(x_init), _ptr(u_init),
+                               _ptr(x_traj), _ptr(xo), _ptr(uo), _ptr(cost), _ptr(iters), _ptr(st))
+        _lib.check(rc, "ilqr_fit", allow=(_lib.ERR_NAN, _lib.ERR_LS_EXHAUSTED))
+        return FitResult(xo, uo, cost, iters, st, rc)
+
+
+def selftest(device: int = 0) -> int:
+    lib = _lib.load()
+    f = C.c_int32(-1)
+    _lib.check(lib.ilqr_selftest(device, C.byref(f)), "ilqr_selftest")
+    return f.value

@@ -1,0 +1,169 @@
+/*
+ * ilqr.h — C ABI of the MI355X-native batched iLQR hot path (libilqr_hip.so).
+ *
+ * Drop-in boundary for aabouman/iLQR.jl's backward/forward passes. The
+ * reference has no FFI (it is pure Julia); each entry point below replaces one
+ * Julia function of the reference and is what a Julia `ccall` shim binds
+ * (julia/iLQRHIP.jl):
+ *
+ *   ilqr_backward  <- iLQR.backward_pass   /root/reference/src/backward_pass.jl:324-357
+ *   ilqr_forward   <- iLQR.forward_pass    /root/reference/src/forward_pass.jl:55-93
+ *   ilqr_fit       <- iLQR.fit             /root/reference/src/forward_pass.jl:148-179
+ *   ilqr_iterate   <- one iteration of fit's loop body, forward_pass.jl:162-175
+ *                     (backward_pass + forward_pass fused in one launch)
+ *
+ * The reference's callbacks (dynamicsf, immediate_cost, final_cost; documented
+ * at src/backward_pass.jl:11-19,54-70,122-127) are Julia closures that cannot
+ * run on the device; they are replaced by a problem descriptor (ilqr_problem)
+ * naming a device-side problem family. ILQR_PROBLEM_LQ is
+ *   dynamicsf(x,u)      = A x + B u
+ *   immediate_cost(x,u) = xᵀ Q x + uᵀ R u
+ *   final_cost(x)       = xᵀ Qf x
+ * with per-instance (per-trajectory) A, B, Q, R, Qf.
+ *
+ * Data layout (all arrays are DEVICE pointers, fp64, C row-major, trajectory
+ * slowest; the same memory is a Julia column-major Array with the dimension
+ * list reversed):
+ *   x      (batch, T+1, nx)     Julia Array{Float64,3} (nx, T+1, batch)
+ *   u, d   (batch, T,   nu)     Julia (nu, T, batch)
+ *   K      (batch, T, nu, nx)   K[b,t] is the reference's Ks[t,:,:] (nu × nx)
+ *   A      (batch, nx, nx)      B (batch, nx, nu)   Q, Qf (batch, nx, nx)   R (batch, nu, nu)
+ *   cost, prev_cost (batch)     status, trials, iters (batch) int32
+ *
+ * Errors: every call returns an ilqr_status; no exceptions or aborts cross the
+ * ABI. ILQR_ERR_BAD_DIMS replaces the reference's `@assert N == M+1`
+ * (backward_pass.jl:329, forward_pass.jl:62,156). NaNs (the reference's
+ * `@assert !any(isnan, ...)`, backward_pass.jl:353-354, forward_pass.jl:89-90)
+ * are reported per trajectory in `status` (ILQR_TRAJ_NAN) and as
+ * ILQR_ERR_NAN from ilqr_fit/ilqr_backward/ilqr_forward when any trajectory hit one.
+ *
+ * Threading: a handle is bound to one device and one HIP stream; calls are
+ * asynchronous on that stream except where noted; different handles may be
+ * used from different threads.
+ */
+#ifndef ILQR_H_
+#define ILQR_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ILQR_ABI_VERSION 1
+
+typedef enum {
+  ILQR_OK = 0,
+  ILQR_ERR_BAD_DIMS = 1,      /* shape mismatch (reference: @assert N == M+1)          */
+  ILQR_ERR_BAD_ARG = 2,       /* null pointer / bad option value                       */
+  ILQR_ERR_UNSUPPORTED = 3,   /* (nx, nu) or problem kind not built into this library  */
+  ILQR_ERR_HIP = 4,           /* HIP runtime error (see ilqr_last_error)               */
+  ILQR_ERR_NAN = 5,           /* a trajectory produced NaN (reference: AssertionError) */
+  ILQR_ERR_LS_EXHAUSTED = 6   /* a line search hit max_trials (reference: loops forever) */
+} ilqr_status;
+
+/* per-trajectory status word */
+enum {
+  ILQR_TRAJ_OK = 0,
+  ILQR_TRAJ_CONVERGED = 1,
+  ILQR_TRAJ_MAX_ITER = 2,
+  ILQR_TRAJ_LS_EXHAUSTED = 3,
+  ILQR_TRAJ_NAN = 4
+};
+
+typedef enum { ILQR_PROBLEM_LQ = 1 } ilqr_problem_kind;
+
+typedef struct {
+  int32_t kind;        /* ilqr_problem_kind */
+  int32_t reserved;
+  const double* A;     /* (batch, nx, nx) */
+  const double* B;     /* (batch, nx, nu) */
+  const double* Q;     /* (batch, nx, nx) */
+  const double* R;     /* (batch, nu, nu) */
+  const double* Qf;    /* (batch, nx, nx) */
+} ilqr_problem;
+
+typedef struct {
+  int32_t max_iter;    /* fit: forward_pass.jl:152 default 100                         */
+  int32_t max_trials;  /* line-search cap (reference: unbounded, forward_pass.jl:70)   */
+  double tol;          /* fit: forward_pass.jl:152 default 1e-6                         */
+  double mu;           /* H regulariser, backward_pass.jl:214 (0.01)                    */
+  double alpha0;       /* first step, forward_pass.jl:66 (1.0)                           */
+  double shrink;       /* step factor, forward_pass.jl:82 (0.5)                           */
+} ilqr_options;
+
+typedef struct ilqr_handle ilqr_handle;
+
+int ilqr_abi_version(void);
+const char* ilqr_status_string(ilqr_status s);
+/* last HIP error text recorded by this thread (empty string if none) */
+const char* ilqr_last_error(void);
+void ilqr_default_options(ilqr_options* opts);
+/* 1 if (nx, nu) has a compiled kernel for `kind` */
+int ilqr_supported(int32_t kind, int nx, int nu);
+
+/* Bind a handle to `device`, preallocating the workspace (trajectory ping-pong
+ * buffers, gains, per-trajectory state) for problems of this shape. Hot calls
+ * never allocate. */
+ilqr_status ilqr_create(ilqr_handle** out, int device, int nx, int nu, int T, int batch);
+ilqr_status ilqr_destroy(ilqr_handle* h);
+/* HIP stream (hipStream_t) the handle launches on; NULL = the null stream. */
+ilqr_status ilqr_set_stream(ilqr_handle* h, void* hip_stream);
+ilqr_status ilqr_sync(ilqr_handle* h);
+
+/* iLQR.backward_pass (backward_pass.jl:324-357): gains d (batch,T,nu) and
+ * K (batch,T,nu,nx) for every trajectory. With a status array (batch) the call
+ * synchronises and returns ILQR_ERR_NAN if any trajectory produced a NaN gain;
+ * with status == NULL it is asynchronous and reports nothing. */
+ilqr_status ilqr_backward(ilqr_handle* h, const ilqr_problem* p, const ilqr_options* o,
+                          const double* x, const double* u, double* d, double* K,
+                          int32_t* status);
+
+/* iLQR.forward_pass (forward_pass.jl:55-93): rollout + line search starting
+ * from alpha0, accepting the first alpha with prev_cost - new_cost > 0; a
+ * trajectory whose search exhausts max_trials gets x_new = x, u_new = u.
+ * x_traj may be NULL (zeros); trials may be NULL. status as for ilqr_backward
+ * (synchronising when given; ILQR_ERR_LS_EXHAUSTED / ILQR_ERR_NAN). */
+ilqr_status ilqr_forward(ilqr_handle* h, const ilqr_problem* p, const ilqr_options* o,
+                         const double* x, const double* u, const double* x_traj,
+                         const double* d, const double* K, const double* prev_cost,
+                         double* x_new, double* u_new, double* new_cost,
+                         int32_t* trials, int32_t* status);
+
+/* One iteration of fit's loop (forward_pass.jl:162-175) for every trajectory
+ * whose status is ILQR_TRAJ_OK, fused in one launch: backward, forward, the
+ * convergence test. Reads (x, u), writes (x_new, u_new); prev_cost is read and
+ * updated in place; du2 (batch) receives Σ(ū_new − u)²; trajectories whose
+ * status is non-zero are skipped. The bench "step". */
+ilqr_status ilqr_iterate(ilqr_handle* h, const ilqr_problem* p, const ilqr_options* o,
+                         const double* x, const double* u, const double* x_traj,
+                         double* x_new, double* u_new, double* prev_cost, double* du2,
+                         int32_t* trials, int32_t* status);
+
+/* iLQR.fit (forward_pass.jl:148-179) for the whole batch. x_init/u_init are
+ * the starting trajectories; x_out/u_out receive the result, which — like the
+ * reference — is the iterate BEFORE the update that met `tol` (forward_pass.jl:171).
+ * x_traj may be NULL. cost (batch) receives the cost of the returned iterate's
+ * successor (the reference's last new_cost); iters/status (batch) may be NULL.
+ * Returns ILQR_ERR_NAN / ILQR_ERR_LS_EXHAUSTED if any trajectory stopped that
+ * way (others still complete). Synchronises the stream. */
+ilqr_status ilqr_fit(ilqr_handle* h, const ilqr_problem* p, const ilqr_options* o,
+                     const double* x_init, const double* u_init, const double* x_traj,
+                     double* x_out, double* u_out, double* cost, int32_t* iters,
+                     int32_t* status);
+
+/* Device memory helpers so a host-language shim (Julia ccall) needs no GPU package. */
+ilqr_status ilqr_malloc(ilqr_handle* h, size_t bytes, void** ptr);
+ilqr_status ilqr_free(ilqr_handle* h, void* ptr);
+ilqr_status ilqr_memcpy_h2d(ilqr_handle* h, void* dst, const void* src, size_t bytes);
+ilqr_status ilqr_memcpy_d2h(ilqr_handle* h, void* dst, const void* src, size_t bytes);
+
+/* Diagnostic: runs the cross-lane and MFMA layout self-tests the kernels rely
+ * on (permlane swaps, v_mfma_f64_16x16x4 fragment maps) on `device`. */
+ilqr_status ilqr_selftest(int device, int32_t* failures);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ILQR_H_ */

@@ -1,0 +1,94 @@
+"""ctypes wrapper of oracle/ilqr_ref.c (C restatement of the reference's LQ hot
+path) — TEST INFRASTRUCTURE ONLY: the checker for large parity tests and the
+bench's cpu_baseline leg. Build with `make -C oracle`."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(_HERE, "lib", "libilqr_oracle.so")
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def load():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        _lib = C.CDLL(LIB)
+        _lib.oracle_max_threads.restype = C.c_int
+    return _lib
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+def _f64(a):
+    return np.ascontiguousarray(a, dtype=np.float64)
+
+
+def max_threads():
+    return load().oracle_max_threads()
+
+
+def lq_backward(lq, x, u, mu=0.01, symmetrize=False, nthreads=0):
+    """→ (d (B,T,m), K (B,T,m,n), status (B,))"""
+    lib = load()
+    nb, n, m = lq.B.shape
+    T = u.shape[1]
+    x, u = _f64(x), _f64(u)
+    d = np.empty((nb, T, m))
+    K = np.empty((nb, T, m, n))
+    st = np.empty(nb, dtype=np.int32)
+    rc = lib.oracle_lq_backward(nb, T, n, m, _p(lq.A), _p(lq.B), _p(lq.Q), _p(lq.R), _p(lq.Qf),
+                                _p(x), _p(u), C.c_double(mu), int(symmetrize), _p(d), _p(K), _p(st),
+                                nthreads)
+    assert rc >= 0
+    return d, K, st
+
+
+def lq_forward(lq, x, u, x_traj, d, K, prev_cost, max_trials=64, alpha0=1.0, shrink=0.5,
+               nthreads=0):
+    """→ (x_new, u_new, cost, trials) ; trials < 0 means exhausted."""
+    lib = load()
+    nb, n, m = lq.B.shape
+    T = u.shape[1]
+    x, u, d, K = _f64(x), _f64(u), _f64(d), _f64(K)
+    xt = None if x_traj is None else _f64(x_traj)
+    pc = _f64(np.broadcast_to(np.asarray(prev_cost, dtype=np.float64), (nb,)))
+    xn = np.empty((nb, T + 1, n))
+    un = np.empty((nb, T, m))
+    cost = np.empty(nb)
+    tr = np.empty(nb, dtype=np.int32)
+    lib.oracle_lq_forward(nb, T, n, m, _p(lq.A), _p(lq.B), _p(lq.Q), _p(lq.R), _p(lq.Qf), _p(x),
+                          _p(u), _p(xt), _p(d), _p(K), _p(pc), _p(xn), _p(un), _p(cost), _p(tr),
+                          max_trials, C.c_double(alpha0), C.c_double(shrink), nthreads)
+    return xn, un, cost, tr
+
+
+def lq_fit(lq, x_init, u_init, x_traj=None, max_iter=100, tol=1e-6, mu=0.01, max_trials=64,
+           symmetrize=False, nthreads=0):
+    """→ (x, u, cost, iters, status)   status: 1 converged, 2 max_iter, 3 LS exhausted, 4 NaN"""
+    lib = load()
+    nb, n, m = lq.B.shape
+    T = u_init.shape[1]
+    xi, ui = _f64(x_init), _f64(u_init)
+    xt = None if x_traj is None else _f64(x_traj)
+    xo = np.empty((nb, T + 1, n))
+    uo = np.empty((nb, T, m))
+    cost = np.empty(nb)
+    iters = np.empty(nb, dtype=np.int32)
+    st = np.empty(nb, dtype=np.int32)
+    lib.oracle_lq_fit(nb, T, n, m, _p(lq.A), _p(lq.B), _p(lq.Q), _p(lq.R), _p(lq.Qf), _p(xi),
+                      _p(ui), _p(xt), max_iter, C.c_double(tol), C.c_double(mu), int(symmetrize), max_trials,
+                      _p(xo), _p(uo), _p(cost), _p(iters), _p(st), nthreads)
+    return xo, uo, cost, iters, st

@@ -1,0 +1,126 @@
+"""Generate the golden vectors in tests/golden/ from the CPU restatement of the
+reference (oracle/ilqr_oracle.py, numpy + dual-number AD).
+
+The reference (aabouman/iLQR.jl) is pure Julia and cannot run here (no Julia
+toolchain), and its own tests pin no numeric outputs (unseeded rand(), broken
+as written — SURVEY.md §4), so these fixtures are the oracle's outputs on
+seeded inputs. The oracle itself is pinned by the known-answer tests in
+tests/test_oracle.py. Regenerate with:  python tests/golden/make_golden.py
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "ilqr.jl_amd")]
+
+from ilqr_amd.problems import quadrotor_batch, random_lq_batch  # noqa: E402
+from oracle import ilqr_oracle as O  # noqa: E402
+
+MAX_TRIALS = 60
+
+
+def lq_case(name, lq, x, u, xtraj=None, symmetrize=False, fit_iters=30, tol=1e-6):
+    nb = lq.batch
+    T = u.shape[1]
+    out = {"A": lq.A, "B": lq.B, "Q": lq.Q, "R": lq.R, "Qf": lq.Qf, "x": x, "u": u}
+    if xtraj is not None:
+        out["xtraj"] = xtraj
+    d = np.empty_like(u)
+    K = np.empty((nb, T, lq.nu, lq.nx))
+    xn, un = np.empty_like(x), np.empty_like(u)
+    cost = np.empty(nb)
+    trials = np.empty(nb, dtype=np.int32)
+    fx, fu = np.empty_like(x), np.empty_like(u)
+    fcost = np.full((nb, fit_iters), np.nan)
+    fiters = np.empty(nb, dtype=np.int32)
+    for b in range(nb):
+        f, l, lf = O.lq_closures(lq.A[b], lq.B[b], lq.Q[b], lq.R[b], lq.Qf[b])
+        xt = np.zeros_like(x[b]) if xtraj is None else xtraj[b]
+        d[b], K[b] = O.backward_pass(x[b], u[b], f, l, lf, symmetrize=symmetrize)
+        if not symmetrize:
+            # the literal recursion must be numerically healthy on a literal fixture
+            ds, Ks = O.backward_pass(x[b], u[b], f, l, lf, symmetrize=True)
+            rel = np.abs(K[b] - Ks).max() / np.abs(Ks).max()
+            assert rel < 1e-9, (name, b, rel)
+        st = {}
+        xn[b], un[b], cost[b] = O.forward_pass(x[b], u[b], xt, d[b], K[b], np.inf, f, l, lf,
+                                               max_trials=MAX_TRIALS, stats=st)
+        trials[b] = st["trials"]
+        hist = []
+        fx[b], fu[b] = O.fit(x[b], u[b], f, l, lf, x_traj=xt, max_iter=fit_iters, tol=tol,
+                             max_trials=MAX_TRIALS, history=hist, symmetrize=symmetrize)
+        fiters[b] = len(hist)
+        fcost[b, :len(hist)] = [h["cost"] for h in hist]
+    out.update(d=d, K=K, fw_x=xn, fw_u=un, fw_cost=cost, fw_trials=trials, fit_x=fx, fit_u=fu,
+               fit_cost=fcost, fit_iters=fiters,
+               meta=np.array(json.dumps({"symmetrize": symmetrize, "fit_max_iter": fit_iters,
+                                         "tol": tol, "max_trials": MAX_TRIALS})))
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), **out)
+    print(name, "fit iters", fiters.tolist(), "trials", trials.tolist())
+
+
+def twolink_case(name, x0s, T, fit_iters=40, tol=1e-6):
+    TL = O.TwoLink
+    nb = len(x0s)
+    x = np.stack([O.rollout(np.asarray(x0, float), np.zeros((T, 2)), TL.dynamicsf) for x0 in x0s])
+    u = np.zeros((nb, T, 2))
+    d = np.empty_like(u)
+    K = np.empty((nb, T, 2, 4))
+    xn, un = np.empty_like(x), np.empty_like(u)
+    cost = np.empty(nb)
+    fx, fu = np.empty_like(x), np.empty_like(u)
+    fcost = np.full((nb, fit_iters), np.nan)
+    fiters = np.empty(nb, dtype=np.int32)
+    for b in range(nb):
+        d[b], K[b] = O.backward_pass(x[b], u[b], TL.dynamicsf, TL.immediate_cost, TL.final_cost)
+        xn[b], un[b], cost[b] = O.forward_pass(x[b], u[b], np.zeros_like(x[b]), d[b], K[b], np.inf,
+                                               TL.dynamicsf, TL.immediate_cost, TL.final_cost,
+                                               max_trials=MAX_TRIALS)
+        hist = []
+        fx[b], fu[b] = O.fit(x[b], u[b], TL.dynamicsf, TL.immediate_cost, TL.final_cost,
+                             max_iter=fit_iters, tol=tol, max_trials=MAX_TRIALS, history=hist)
+        fiters[b] = len(hist)
+        fcost[b, :len(hist)] = [h["cost"] for h in hist]
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), x=x, u=u, d=d, K=K, fw_x=xn, fw_u=un,
+                        fw_cost=cost, fit_x=fx, fit_u=fu, fit_cost=fcost, fit_iters=fiters,
+                        meta=np.array(json.dumps({"T": T, "fit_max_iter": fit_iters, "tol": tol})))
+    print(name, "fit iters", fiters.tolist())
+
+
+def main():
+    # headline family, short horizon: the literal recursion is healthy for T ≲ 16 (rounding asymmetry grows ~3×/step)
+    lq, x, u = quadrotor_batch(4, T=16, seed0=0)
+    lq_case("quad_t16", lq, x, u)
+    # headline family, full horizon: the literal recursion diverges (~step 32), so
+    # the fixture uses the symmetrised oracle (identity in exact arithmetic)
+    lq, x, u = quadrotor_batch(2, T=100, seed0=100)
+    lq_case("quad_t100_sym", lq, x, u, symmetrize=True, fit_iters=12)
+    # dense per-instance LQ with random initial controls
+    lq, x, u = random_lq_batch(3, 12, 4, 16, seed=7)
+    lq_case("dense_t16", lq, x, u)
+    # dense, full horizon, symmetrised oracle
+    lq, x, u = random_lq_batch(3, 12, 4, 64, seed=9)
+    lq_case("dense_t64_sym", lq, x, u, symmetrize=True, fit_iters=12)
+    # x_traj enters only the line-search objective (forward_pass.jl:187-190)
+    lq, x, u = random_lq_batch(2, 12, 4, 16, seed=11)
+    xtraj = 0.3 * np.random.default_rng(12).standard_normal(x.shape)
+    lq_case("dense_xtraj", lq, x, u, xtraj=xtraj)
+    # 2-link arm (test/2_link_example): animate_2_link.jl:13's x0 and two seeded rand(4)
+    rng = np.random.default_rng(2024)
+    twolink_case("twolink_t50", [[0.1, -0.1, 0.0, 0.0], rng.random(4), rng.random(4)], T=50)
+    kat = {
+        "alpha": O.TwoLink.alpha, "beta": O.TwoLink.beta, "delta": O.TwoLink.delta,
+        "theta_star": O.TwoLink.inverse_kinematics(O.TwoLink.target_tool_loc).tolist(),
+    }
+    with open(os.path.join(HERE, "twolink_constants.json"), "w") as f:
+        json.dump(kat, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,80 @@
+"""CPU tests of the drop-in boundary: libilqr_hip.so loads and exports every symbol
+include/ilqr.h declares; argument validation works without touching a GPU."""
+import ctypes as C
+import os
+import re
+
+import pytest
+
+from ilqr_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "ilqr.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(ilqr_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_declares_the_bound_symbols():
+    names = declared_functions()
+    assert "ilqr_fit" in names and "ilqr_backward" in names and "ilqr_forward" in names
+    assert set(names) == set(_lib.SIGNATURES), set(names) ^ set(_lib.SIGNATURES)
+
+
+def test_library_loads_and_exports_every_symbol():
+    lib = _lib.load()
+    for name in declared_functions():
+        assert hasattr(lib, name), name
+    assert lib.ilqr_abi_version() == 1
+
+
+def test_status_strings_and_defaults():
+    lib = _lib.load()
+    for s in range(7):
+        assert lib.ilqr_status_string(s)
+    o = _lib.default_options()
+    # the reference's defaults: max_iter=100, tol=1e-6 (forward_pass.jl:152),
+    # μ = 0.01 (backward_pass.jl:214), α₀ = 1 (forward_pass.jl:66), α /= 2 (:82)
+    assert (o.max_iter, o.tol, o.mu, o.alpha0, o.shrink) == (100, 1e-6, 0.01, 1.0, 0.5)
+    assert o.max_trials >= 30
+
+
+def test_supported_shapes():
+    lib = _lib.load()
+    assert lib.ilqr_supported(_lib.PROBLEM_LQ, 12, 4) == 1
+    assert lib.ilqr_supported(_lib.PROBLEM_LQ, 5, 3) == 0
+    assert lib.ilqr_supported(99, 12, 4) == 0
+
+
+def test_argument_validation_needs_no_gpu():
+    lib = _lib.load()
+    h = C.c_void_p()
+    # reference: @assert N == M+1 / positive sizes → ILQR_ERR_BAD_DIMS before any HIP call
+    assert lib.ilqr_create(C.byref(h), 0, 12, 4, 0, 16) == _lib.ERR_BAD_DIMS
+    assert lib.ilqr_create(C.byref(h), 0, 12, 4, 100, 0) == _lib.ERR_BAD_DIMS
+    assert lib.ilqr_create(None, 0, 12, 4, 100, 16) == _lib.ERR_BAD_ARG
+    o = _lib.default_options()
+    p = _lib.Problem(_lib.PROBLEM_LQ, 0, None, None, None, None, None)
+    assert lib.ilqr_backward(None, C.byref(p), C.byref(o), None, None, None, None, None) == _lib.ERR_BAD_ARG
+    assert lib.ilqr_fit(None, C.byref(p), C.byref(o), None, None, None, None, None, None, None,
+                        None) == _lib.ERR_BAD_ARG
+    assert lib.ilqr_destroy(None) == _lib.OK
+
+
+def test_missing_library_fails_loudly(tmp_path):
+    with pytest.raises(ImportError):
+        _lib.load(str(tmp_path / "nope.so"))
+
+
+def test_no_oracle_in_the_product_path():
+    """The product (ilqr.jl_amd/) must never import or link the oracle."""
+    pkg = os.path.join(ROOT, "ilqr.jl_amd")
+    for dirpath, _, files in os.walk(pkg):
+        for f in files:
+            if f.endswith((".py", ".hip", ".cpp", ".h", ".jl")) or f == "Makefile":
+                txt = open(os.path.join(dirpath, f), encoding="utf-8").read()
+                for bad in ("import oracle", "from oracle", "libilqr_oracle", "ilqr_ref"):
+                    assert bad not in txt, (f, bad)

@@ -1,0 +1,241 @@
+"""GPU parity tests: the HIP path (through the C ABI) against the oracle.
+
+Tolerances (fp64): the device evaluates the reference's formulas in a different
+order and with the exact algebraic rewrite step_back(:268-270) ≡
+[Qxx | lx+Aᵀs] − K_augᵀ(H+2μI)K_aug, so results agree to rounding amplified by
+the Riccati recursion: K, d within rel 1e-8 of max|·| over a fixture; forward
+rollouts within rel 1e-10 given identical gains; costs rel 1e-11; line-search
+trial counts and fit iteration counts exactly. Full-size (B=4096, T=100)
+checks compare with the C restatement on a sample and use size-independent
+properties (KKT fixed point, monotone cost, idempotence).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from ilqr_amd import _lib
+from ilqr_amd.problems import LQBatch, quadrotor_batch, random_lq_batch
+from ilqr_amd.solver import Solver, selftest
+from oracle import cref
+from oracle import ilqr_oracle as O
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+LQ_FIXTURES = ["quad_t16", "quad_t100_sym", "dense_t16", "dense_t64_sym", "dense_xtraj"]
+
+TOL_GAIN = 1e-8
+TOL_ROLL = 1e-10
+TOL_COST = 1e-11
+
+
+def rel(a, b):
+    a = a.cpu().numpy() if isinstance(a, torch.Tensor) else np.asarray(a)
+    b = b.cpu().numpy() if isinstance(b, torch.Tensor) else np.asarray(b)
+    return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-300))
+
+
+def dev(a, dtype=torch.float64):
+    return torch.as_tensor(np.ascontiguousarray(a)).to("cuda", dtype).contiguous()
+
+
+def load(name):
+    z = np.load(os.path.join(GOLD, name + ".npz"), allow_pickle=False)
+    return {k: z[k] for k in z.files}
+
+
+def solver_for(g):
+    lq = LQBatch(g["A"], g["B"], g["Q"], g["R"], g["Qf"])
+    T = g["u"].shape[1]
+    s = Solver(lq.nx, lq.nu, T, lq.batch)
+    s.set_problem(lq)
+    return s, lq
+
+
+def test_selftest_lane_maps(gpu):
+    assert selftest(0) == 0
+
+
+@pytest.mark.parametrize("name", LQ_FIXTURES)
+def test_backward_matches_golden(gpu, name):
+    g = load(name)
+    s, _ = solver_for(g)
+    d, K, st = s.backward(dev(g["x"]), dev(g["u"]))
+    assert (st.cpu().numpy() == 0).all()
+    assert rel(K, g["K"]) < TOL_GAIN, rel(K, g["K"])
+    assert rel(d, g["d"]) < TOL_GAIN, rel(d, g["d"])
+
+
+@pytest.mark.parametrize("name", LQ_FIXTURES)
+def test_forward_matches_golden(gpu, name):
+    g = load(name)
+    s, _ = solver_for(g)
+    nb = g["A"].shape[0]
+    xt = dev(g["xtraj"]) if "xtraj" in g else None
+    pc = torch.full((nb,), float("inf"), dtype=torch.float64, device="cuda")
+    xn, un, c, tr, st = s.forward(dev(g["x"]), dev(g["u"]), dev(g["d"]), dev(g["K"]), pc, x_traj=xt)
+    assert (st.cpu().numpy() == 0).all()
+    assert rel(xn, g["fw_x"]) < TOL_ROLL and rel(un, g["fw_u"]) < TOL_ROLL
+    assert rel(c, g["fw_cost"]) < TOL_COST
+    assert np.array_equal(tr.cpu().numpy(), g["fw_trials"])
+
+
+@pytest.mark.parametrize("name", LQ_FIXTURES)
+def test_fit_matches_golden(gpu, name):
+    g = load(name)
+    meta = json.loads(str(g["meta"]))
+    s, _ = solver_for(g)
+    xt = dev(g["xtraj"]) if "xtraj" in g else None
+    r = s.fit(dev(g["x"]), dev(g["u"]), x_traj=xt, max_iter=meta["fit_max_iter"], tol=meta["tol"])
+    assert r.call_status == 0
+    assert np.array_equal(r.iters.cpu().numpy(), g["fit_iters"])
+    assert (r.status.cpu().numpy() == _lib.TRAJ_CONVERGED).all()
+    assert rel(r.u, g["fit_u"]) < 1e-8 and rel(r.x, g["fit_x"]) < 1e-8
+    last = np.array([g["fit_cost"][b, g["fit_iters"][b] - 1] for b in range(len(g["fit_iters"]))])
+    assert rel(r.cost, last) < 1e-9
+
+
+# -- reference API mirror ------------------------------------------------------------
+def test_reference_api_single_trajectory_numpy(gpu):
+    import ilqr_amd
+    g = load("quad_t16")
+    b = 1
+    f = ilqr_amd.LinearDynamics(g["A"][b], g["B"][b])
+    l = ilqr_amd.QuadraticCost(g["Q"][b], g["R"][b])
+    lf = ilqr_amd.QuadraticFinalCost(g["Qf"][b])
+    du, K = ilqr_amd.backward_pass(g["x"][b], g["u"][b], f, l, lf)
+    assert du.shape == (16, 4) and K.shape == (16, 4, 12)
+    assert rel(K, g["K"][b]) < TOL_GAIN
+    xb, ub, c = ilqr_amd.forward_pass(g["x"][b], g["u"][b], np.zeros_like(g["x"][b]), du, K, np.inf, f, l, lf)
+    assert isinstance(c, float) and rel(ub, g["fw_u"][b]) < 1e-9
+    xf, uf = ilqr_amd.fit(g["x"][b], g["u"][b], f, l, lf, max_iter=30, tol=1e-6)
+    assert rel(uf, g["fit_u"][b]) < 1e-8
+    # the closures are real callables (same objects a CPU reference would call)
+    assert np.allclose(f(g["x"][b, 0], g["u"][b, 0]), g["x"][b, 1])
+
+
+def test_reference_api_errors(gpu):
+    import ilqr_amd
+    g = load("quad_t16")
+    f = ilqr_amd.LinearDynamics(g["A"][0], g["B"][0])
+    l = ilqr_amd.QuadraticCost(g["Q"][0], g["R"][0])
+    lf = ilqr_amd.QuadraticFinalCost(g["Qf"][0])
+    with pytest.raises(AssertionError):                       # backward_pass.jl:329
+        ilqr_amd.backward_pass(g["x"][0][:-1], g["u"][0], f, l, lf)
+    with pytest.raises(TypeError):                            # forward_pass.jl:152
+        ilqr_amd.fit(g["x"][0], g["u"][0], f, l, lf, max_iter=1e5)
+    with pytest.raises(NotImplementedError):                  # arbitrary closures: no kernel
+        ilqr_amd.backward_pass(g["x"][0], g["u"][0], lambda x, u: x, l, lf)
+    with pytest.raises(AssertionError):                       # NaN → AssertionError (:353)
+        xbad = g["x"][0].copy()
+        xbad[5, 3] = np.nan
+        ilqr_amd.backward_pass(xbad, g["u"][0], f, l, lf)
+
+
+# -- edge cases -----------------------------------------------------------------------
+@pytest.mark.parametrize("nb,T", [(1, 1), (1, 2), (5, 3), (7, 17), (6, 40)])
+def test_ragged_batches_and_short_horizons(gpu, nb, T):
+    lq, x, u = random_lq_batch(nb, 12, 4, T, seed=nb * 100 + T)
+    s = Solver(12, 4, T, nb)
+    s.set_problem(lq)
+    d, K, st = s.backward(dev(x), dev(u))
+    dc, Kc, _ = cref.lq_backward(lq, x, u, symmetrize=True)
+    assert rel(K, Kc) < TOL_GAIN and rel(d, dc) < TOL_GAIN
+    pc = torch.full((nb,), float("inf"), dtype=torch.float64, device="cuda")
+    xn, un, c, tr, st = s.forward(dev(x), dev(u), d, K, pc)
+    xo, uo, co, tro = cref.lq_forward(lq, x, u, None, d.cpu().numpy(), K.cpu().numpy(), np.inf)
+    assert rel(xn, xo) < TOL_ROLL and rel(c, co) < TOL_COST and np.array_equal(tr.cpu().numpy(), tro)
+
+
+def test_line_search_exhaustion_returns_inputs(gpu):
+    """prev_cost = -Inf can never be beaten: the reference would loop forever
+    (forward_pass.jl:70-87); the device stops at max_trials and returns x, u."""
+    lq, x, u = random_lq_batch(4, 12, 4, 10, seed=3)
+    s = Solver(12, 4, 10, 4)
+    s.set_problem(lq)
+    d, K, _ = s.backward(dev(x), dev(u))
+    pc = torch.full((4,), -float("inf"), dtype=torch.float64, device="cuda")
+    xn, un, c, tr, st = s.forward(dev(x), dev(u), d, K, pc, max_trials=7)
+    assert (st.cpu().numpy() == _lib.TRAJ_LS_EXHAUSTED).all()
+    assert (tr.cpu().numpy() == 7).all()
+    assert torch.equal(xn.cpu(), torch.from_numpy(x)) and torch.equal(un.cpu(), torch.from_numpy(u))
+
+
+def test_nan_is_reported_per_trajectory(gpu):
+    lq, x, u = random_lq_batch(8, 12, 4, 12, seed=4)
+    x[3, 6, 2] = np.nan
+    s = Solver(12, 4, 12, 8)
+    s.set_problem(lq)
+    d, K, st = s.backward(dev(x), dev(u))
+    st = st.cpu().numpy()
+    assert st[3] == _lib.TRAJ_NAN and (np.delete(st, 3) == 0).all()
+    r = s.fit(dev(x), dev(u), max_iter=20, tol=1e-6)
+    st = r.status.cpu().numpy()
+    assert r.call_status == _lib.ERR_NAN and st[3] == _lib.TRAJ_NAN
+    assert (np.delete(st, 3) == _lib.TRAJ_CONVERGED).all()
+
+
+def test_x_traj_none_equals_zeros(gpu):
+    lq, x, u = random_lq_batch(4, 12, 4, 20, seed=8)
+    s = Solver(12, 4, 20, 4)
+    s.set_problem(lq)
+    a = s.fit(dev(x), dev(u), max_iter=10)
+    b = s.fit(dev(x), dev(u), x_traj=torch.zeros_like(dev(x)), max_iter=10)
+    assert torch.equal(a.x, b.x) and torch.equal(a.u, b.u)
+
+
+# -- headline size (B = 4096, T = 100) --------------------------------------------------
+@pytest.fixture(scope="module")
+def headline():
+    lq, x, u = quadrotor_batch(4096, T=100, seed0=0)
+    s = Solver(12, 4, 100, 4096)
+    s.set_problem(lq)
+    return s, lq, x, u
+
+
+def test_headline_backward_vs_c_oracle(gpu, headline):
+    s, lq, x, u = headline
+    d, K, st = s.backward(dev(x), dev(u))
+    assert (st.cpu().numpy() == 0).all()
+    idx = np.random.default_rng(0).choice(4096, 256, replace=False)
+    sub = lq.slice(0, 4096)
+    sub = LQBatch(lq.A[idx], lq.B[idx], lq.Q[idx], lq.R[idx], lq.Qf[idx])
+    dc, Kc, stc = cref.lq_backward(sub, x[idx], u[idx], symmetrize=True)
+    assert rel(K.cpu().numpy()[idx], Kc) < TOL_GAIN and rel(d.cpu().numpy()[idx], dc) < TOL_GAIN
+
+
+def test_headline_fit_reaches_kkt_and_cost_is_monotone(gpu, headline):
+    s, lq, x, u = headline
+    xi, ui = dev(x), dev(u)
+    xn, un = torch.empty_like(xi), torch.empty_like(ui)
+    pc = torch.full((4096,), float("inf"), dtype=torch.float64, device="cuda")
+    st = torch.zeros((4096,), dtype=torch.int32, device="cuda")
+    costs = []
+    o = _lib.default_options(tol=-1.0)  # tol disabled: every trajectory iterates
+    for _ in range(6):
+        s.iterate(xi, ui, xn, un, pc, st, options=o)
+        costs.append(pc.clone())
+        xi, xn, ui, un = xn, xi, un, ui
+    torch.cuda.synchronize()
+    assert (st.cpu().numpy() == 0).all()
+    c = torch.stack(costs).cpu().numpy()
+    assert (np.diff(c, axis=0) <= 0).all()  # @assert(prev_cost > new_cost) (:168) or equal at the fixed point
+    for b in (0, 1234, 4095):
+        X, U = O.lq_kkt_solution(lq.A[b], lq.B[b], lq.Q[b], lq.R[b], lq.Qf[b], x[b, 0], 100)
+        assert rel(ui[b], U) < 1e-6, rel(ui[b], U)
+
+
+def test_headline_iterate_matches_backward_plus_forward(gpu, headline):
+    """The fused iteration entry point equals backward_pass + forward_pass."""
+    s, lq, x, u = headline
+    xi, ui = dev(x), dev(u)
+    d, K, _ = s.backward(xi, ui)
+    pc = torch.full((4096,), float("inf"), dtype=torch.float64, device="cuda")
+    xf, uf, cf, _, _ = s.forward(xi, ui, d, K, pc)
+    xn, un = torch.empty_like(xi), torch.empty_like(ui)
+    st = torch.zeros((4096,), dtype=torch.int32, device="cuda")
+    s.iterate(xi, ui, xn, un, pc, st, options=_lib.default_options(tol=-1.0))
+    torch.cuda.synchronize()
+    assert torch.equal(xn, xf) and torch.equal(un, uf) and torch.equal(pc, cf)

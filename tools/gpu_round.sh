@@ -1,0 +1,27 @@
+#!/bin/bash
+# One GPU session: tests, smoke, bench, kernel-trace profile. Each GPU step has its own
+# time limit; a crash-class exit (fault/abort/segv/timeout) stops the script.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+step() {  # step <name> <timeout> <cmd...>
+  local name=$1 to=$2; shift 2
+  echo "=== $name" | tee -a gpurun_out/steps.log
+  timeout -k 10 "$to" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc" | tee -a gpurun_out/steps.log
+  tail -5 "gpurun_out/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+  return 0
+}
+WHAT=${1:-all}
+if [[ $WHAT == all || $WHAT == test ]]; then
+  step pytest_gpu 600 python -m pytest tests -m gpu -x -q
+  step smoke 180 python -c "import __graft_entry__ as g; g.smoke()"
+fi
+if [[ $WHAT == all || $WHAT == bench ]]; then
+  step bench 300 python bench.py --steps 20 --warmup 3
+fi
+if [[ $WHAT == all || $WHAT == prof ]]; then
+  step rocprof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu
+fi
