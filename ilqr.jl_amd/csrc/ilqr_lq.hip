@@ -23,8 +23,9 @@
 //        [S s] = [Qxx  lx+Aᵀs] - K_augᵀ (H + 2μI) K_aug
 //    which is ONE more MFMA (k = nu ≤ 4) with A = -K_augᵀ, B = (H+2μI)K_aug
 //    = -[G|g] + μ K_aug, accumulating into [Qxx | lx+Aᵀs].
-//  * forward: 16 lanes per trajectory (4 trajectories per wave); lane j < nx owns
-//    x̄_j, lanes nx.. own ū; the per-step mat-vecs broadcast operands through LDS.
+//  * forward: 16 lanes per trajectory (4 trajectories per wave, one DPP row each);
+//    lane j < nx owns x̄_j, lanes nx.. own ū; mat-vecs broadcast the distributed
+//    vector with v_fmac_f64_dpp row_newbcast, inputs prefetched 4 steps ahead.
 //  * one fit iteration = backward launch (4 waves/SIMD) + forward launch.
 #include <hip/hip_runtime.h>
 #include <math.h>
@@ -39,8 +40,8 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 typedef unsigned u2v __attribute__((ext_vector_type(2)));
 
 constexpr int WAVES_PER_WG = 4;   // trajectories per workgroup
-constexpr int BW_LDS = 80;        // doubles of backward scratch per wave: 4 rows of 16 + one row of 16
-constexpr int FW_LDS = 48;        // doubles of forward scratch per 16-lane group: dx, z, v rows
+constexpr int BW_LDS = 80 + 16 * 17;  // doubles of backward scratch per wave: [G|H] rows, g row, S tile
+constexpr int SYM_EVERY = 4;          // symmetrise S every this many steps
 
 __device__ __forceinline__ d4 mfma(double a, double b, d4 c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
@@ -313,18 +314,94 @@ __device__ bool lq_backward_wave(const LQParams& P, int b, int T, const double* 
     }
     Sp = mfma(-kq, wk, Cin);
     zc = zn;
+
+    // S ← (S + Sᵀ)/2 on the state block (the identity in exact arithmetic). The
+    // accumulator tile feeds the next Y MFMA as its own transpose, so rounding
+    // asymmetry E evolves as E ← −AᵀEA and grows like ρ(A)^2t on unstable A;
+    // a periodic projection bounds it at negligible cost.
+    if ((t % SYM_EVERY) == 0) {
+      double* tile = lds + 80;  // 16 × 17 (padded) doubles
+#pragma unroll
+      for (int r = 0; r < 4; ++r) tile[(q + 4 * r) * 17 + c] = Sp[r];
+      wave_lds_fence();
+#pragma unroll
+      for (int r = 0; r < KS; ++r) {
+        const int i = q + 4 * r;
+        const double other = tile[c * 17 + i];
+        if (i < NX && cx) Sp[r] = 0.5 * (Sp[r] + other);
+      }
+      wave_lds_fence();
+    }
   }
   return __any(nan);
 }
 
+// Σ_k<16 bcast_k(src)·c[k]: src is broadcast from lane k of each 16-lane row
+// (DPP64 row_newbcast, gfx90a+), 4 independent accumulators. `s_nop 4` covers the
+// VALU→DPP and EXEC→DPP hazards for whatever the compiler scheduled in front.
+__device__ __forceinline__ double dpp_dot16(double src, const double (&c)[16]) {
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+  asm("s_nop 4\n\t"
+      "v_fmac_f64_dpp %[a0], %[s], %[c0] row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[a1], %[s], %[c1] row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[a2], %[s], %[c2] row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[a3], %[s], %[c3] row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[a0], %[s], %[c4] row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[a1], %[s], %[c5] row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[a2], %[s], %[c6] row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[a3], %[s], %[c7] row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[a0], %[s], %[c8] row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[a1], %[s], %[c9] row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[a2], %[s], %[c10] row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[a3], %[s], %[c11] row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[a0], %[s], %[c12] row_newbcast:12 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[a1], %[s], %[c13] row_newbcast:13 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[a2], %[s], %[c14] row_newbcast:14 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[a3], %[s], %[c15] row_newbcast:15 row_mask:0xf bank_mask:0xf\n\t"
+      : [a0] "+v"(a0), [a1] "+v"(a1), [a2] "+v"(a2), [a3] "+v"(a3)
+      : [s] "v"(src), [c0] "v"(c[0]), [c1] "v"(c[1]), [c2] "v"(c[2]), [c3] "v"(c[3]), [c4] "v"(c[4]), [c5] "v"(c[5]), [c6] "v"(c[6]), [c7] "v"(c[7]), [c8] "v"(c[8]), [c9] "v"(c[9]), [c10] "v"(c[10]), [c11] "v"(c[11]), [c12] "v"(c[12]), [c13] "v"(c[13]), [c14] "v"(c[14]), [c15] "v"(c[15]));
+  return (a0 + a1) + (a2 + a3);
+}
+
+// Σ_k<12 bcast_k(src)·c[k]: src is broadcast from lane k of each 16-lane row
+// (DPP64 row_newbcast, gfx90a+), 4 independent accumulators. `s_nop 4` covers the
+// VALU→DPP and EXEC→DPP hazards for whatever the compiler scheduled in front.
+__device__ __forceinline__ double dpp_dot12(double src, const double (&c)[12]) {
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+  asm("s_nop 4\n\t"
+      "v_fmac_f64_dpp %[a0], %[s], %[c0] row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[a1], %[s], %[c1] row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[a2], %[s], %[c2] row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[a3], %[s], %[c3] row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[a0], %[s], %[c4] row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[a1], %[s], %[c5] row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[a2], %[s], %[c6] row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[a3], %[s], %[c7] row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[a0], %[s], %[c8] row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[a1], %[s], %[c9] row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[a2], %[s], %[c10] row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[a3], %[s], %[c11] row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+      : [a0] "+v"(a0), [a1] "+v"(a1), [a2] "+v"(a2), [a3] "+v"(a3)
+      : [s] "v"(src), [c0] "v"(c[0]), [c1] "v"(c[1]), [c2] "v"(c[2]), [c3] "v"(c[3]), [c4] "v"(c[4]), [c5] "v"(c[5]), [c6] "v"(c[6]), [c7] "v"(c[7]), [c8] "v"(c[8]), [c9] "v"(c[9]), [c10] "v"(c[10]), [c11] "v"(c[11]));
+  return (a0 + a1) + (a2 + a3);
+}
+
 // ---------------------------------------------------------------------------
-// Forward pass of up to 4 trajectories by one wave, 16 lanes each
-// (forward_pass.jl:55-93, total_cost :182-196).
+// Forward pass of up to 4 trajectories by one wave, 16 lanes each — one DPP row
+// per trajectory (forward_pass.jl:55-93, total_cost :182-196). Lane j < nx owns
+// x̄_j, lanes nx.. own ū. Mat-vecs broadcast the distributed vector with DPP
+// (no LDS); per-step inputs are prefetched PF steps ahead into a register ring.
 // ---------------------------------------------------------------------------
 struct FwdOut {
   double cost;
   int trials;
   int accepted;  // 1 accepted, 0 exhausted / NaN
+};
+
+template <int NX>
+struct FwdStepIn {
+  double xr, xtr, ur, dr;  // xₖ[j], x_trajₖ[j] (x lanes); uₖ, δuₖ (u lanes)
+  double Kr[NX];           // row of Kₖ (u lanes)
 };
 
 template <int NX, int NU>
@@ -333,12 +410,15 @@ __device__ FwdOut lq_forward_group(const LQParams& P, int b, int T, const double
                                    const double* __restrict__ dg, const double* __restrict__ Kg,
                                    double prev_cost, double* __restrict__ xnew,
                                    double* __restrict__ unew, double* du2_out,
-                                   const LSParams& ls, double* lds) {
-  static_assert(NX + NU <= 16, "one 16-lane group per trajectory");
+                                   const LSParams& ls) {
+  static_assert(NX + NU == 16, "one 16-lane DPP row per trajectory: nx + nu == 16");
+  static_assert(NX == 12, "dpp_dot12 is the K·δx product");
+  constexpr int PF = 4;  // prefetch distance (steps)
   const int j = threadIdx.x & 15;
   const bool is_x = j < NX;
-  const bool is_u = (j >= NX) && (j < NX + NU);
-  const int iu = j - NX;
+  const bool is_u = !is_x;
+  const int iu = is_u ? j - NX : 0;
+  const int jx = is_x ? j : 0;
 
   const double* Ab = P.A + (size_t)b * NX * NX;
   const double* Bb = P.B + (size_t)b * NX * NU;
@@ -347,89 +427,85 @@ __device__ FwdOut lq_forward_group(const LQParams& P, int b, int T, const double
   const double* Qfb = P.Qf + (size_t)b * NX * NX;
 
   // row j of F = [A B] (lanes j < NX) and of L = blockdiag(Q, R) (ℓ = vᵀ L v)
-  double Fr[NX + NU], Lr[NX + NU];
+  double Fr[16], Lr[16], Qfr[NX];
 #pragma unroll
-  for (int k = 0; k < NX + NU; ++k) {
-    double f = 0.0, lv = 0.0;
-    if (is_x) {
-      f = (k < NX) ? Ab[j * NX + k] : Bb[j * NU + (k - NX)];
-      lv = (k < NX) ? Qb[j * NX + k] : 0.0;
-    } else if (is_u && k >= NX) {
-      lv = Rb[iu * NU + (k - NX)];
-    }
-    Fr[k] = f;
-    Lr[k] = lv;
+  for (int k = 0; k < 16; ++k) {
+    const double a = ldz(is_x && k < NX, Ab + jx * NX + (k < NX ? k : 0), Ab);
+    const double bb = ldz(is_x && k >= NX, Bb + jx * NU + (k >= NX ? k - NX : 0), Bb);
+    Fr[k] = a + bb;
+    const double lq = ldz(is_x && k < NX, Qb + jx * NX + (k < NX ? k : 0), Qb);
+    const double lr = ldz(is_u && k >= NX, Rb + iu * NU + (k >= NX ? k - NX : 0), Rb);
+    Lr[k] = lq + lr;
   }
-
-  double* dxl = lds;        // δx row
-  double* zl = lds + 16;    // z = [x̄; ū]
-  double* vl = lds + 32;    // v = [x̄ - x_traj; ū]
+#pragma unroll
+  for (int k = 0; k < NX; ++k) Qfr[k] = ldz(is_x, Qfb + jx * NX + k, Qfb);
 
   const double* xb0 = x + (size_t)b * (T + 1) * NX;
   const double* ub0 = u + (size_t)b * T * NU;
-  const double* xt0 = xtraj ? xtraj + (size_t)b * (T + 1) * NX : nullptr;
+  // x_traj = NULL means zeros: read x itself with weight 0 (no branch around the load,
+  // which would make the compiler drain every prefetch with vmcnt(0))
+  const double* xt0 = (xtraj ? xtraj : x) + (size_t)b * (T + 1) * NX;
+  const double xtw = xtraj ? 1.0 : 0.0;
   const double* d0 = dg + (size_t)b * T * NU;
   const double* K0 = Kg + (size_t)b * T * NU * NX;
-  double* xo = xnew + (size_t)b * (T + 1) * NX;
-  double* uo = unew + (size_t)b * T * NU;
+  // each lane stores one element per step: x̄ₖ[j] (x lanes) or ūₖ[iu] (u lanes)
+  double* const out0 = is_x ? xnew + (size_t)b * (T + 1) * NX + jx : unew + (size_t)b * T * NU + iu;
+  const int out_stride = is_x ? NX : NU;
+
+  auto load = [&](int t, FwdStepIn<NX>& in) {
+    const int tt = t < T ? t : T - 1;  // clamped: loads past the horizon are discarded
+    in.xr = xb0[(size_t)tt * NX + jx];
+    in.xtr = xt0[(size_t)tt * NX + jx];
+    in.ur = ub0[(size_t)tt * NU + iu];
+    in.dr = d0[(size_t)tt * NU + iu];
+    const double2* kr = reinterpret_cast<const double2*>(K0 + ((size_t)tt * NU + iu) * NX);
+#pragma unroll
+    for (int k = 0; k < NX / 2; ++k) {
+      const double2 v = kr[k];
+      in.Kr[2 * k] = v.x;
+      in.Kr[2 * k + 1] = v.y;
+    }
+  };
 
   double alpha = ls.alpha0;
   FwdOut out{0.0, 0, 0};
   double du2 = 0.0;
   for (int trial = 1; trial <= ls.max_trials; ++trial) {
-    double xb = is_x ? xb0[j] : 0.0;  // x̄₁ = x₁ (:65)
+    double xb = is_x ? xb0[jx] : 0.0;  // x̄₁ = x₁ (:65)
     double cost = 0.0;
     du2 = 0.0;
-    for (int t = 0; t < T; ++t) {
-      const double xr = is_x ? xb0[(size_t)t * NX + j] : 0.0;
-      // δx = x̄ₖ − xₖ (:72)
-      if (is_x) dxl[j] = xb - xr;
-      wave_lds_fence();
-      double ub = 0.0, ur = 0.0;
-      if (is_u) {
-        ur = ub0[(size_t)t * NU + iu];
-        const double* Kr = K0 + ((size_t)t * NU + iu) * NX;
-        double acc = 0.0;
+    FwdStepIn<NX> ring[PF];
 #pragma unroll
-        for (int k = 0; k < NX; ++k) acc = fma(Kr[k], dxl[k], acc);
-        // ūₖ = uₖ + α δuₖ + Kₖ δx (:73) — α scales δu only
-        ub = fma(alpha, d0[(size_t)t * NU + iu], ur) + acc;
-      }
+    for (int s = 0; s < PF; ++s) load(s, ring[s]);
+    auto step = [&](int t, FwdStepIn<NX>& in) {
+      // δx = x̄ₖ − xₖ (:72); ūₖ = uₖ + α δuₖ + Kₖ δx (:73), α scales δu only
+      const double dx = is_x ? xb - in.xr : 0.0;
+      const double kdx = dpp_dot12(dx, in.Kr);
+      const double ub = fma(alpha, in.dr, in.ur) + kdx;
       const double z = is_x ? xb : ub;
-      const double v = is_x ? (xt0 ? xb - xt0[(size_t)t * NX + j] : xb) : ub;
-      zl[j] = z;
-      vl[j] = v;
-      wave_lds_fence();
-      // ℓ(x̄ₖ − x_trajₖ, ūₖ) (:187-190)
-      double lv = 0.0, xn = 0.0;
-#pragma unroll
-      for (int k = 0; k < NX + NU; ++k) {
-        lv = fma(Lr[k], vl[k], lv);
-        xn = fma(Fr[k], zl[k], xn);  // x̄ₖ₊₁ = f(x̄ₖ, ūₖ) (:74)
-      }
-      wave_lds_fence();
+      const double v = is_x ? fma(-xtw, in.xtr, xb) : ub;
+      const double e = is_x ? 0.0 : ub - in.ur;
+      load(t + PF, in);  // refill this slot PF steps ahead
+      // ℓ(x̄ₖ − x_trajₖ, ūₖ) (:187-190) and x̄ₖ₊₁ = f(x̄ₖ, ūₖ) = A x̄ₖ + B ūₖ (:74)
+      const double lv = dpp_dot16(v, Lr);
+      const double xn = dpp_dot16(z, Fr);
       cost = fma(v, lv, cost);
-      if (is_x) xo[(size_t)t * NX + j] = xb;
-      if (is_u) {
-        uo[(size_t)t * NU + iu] = ub;
-        const double e = ub - ur;
-        du2 = fma(e, e, du2);
-      }
+      out0[(size_t)t * out_stride] = z;
+      du2 = fma(e, e, du2);
       xb = xn;
-    }
-    // final cost on raw x̄_N (:192)
-    if (is_x) {
-      xo[(size_t)T * NX + j] = xb;
-      zl[j] = xb;
-    }
-    wave_lds_fence();
-    double lf = 0.0;
-    if (is_x) {
+    };
+    const int Tm = T - T % PF;
+    for (int t0 = 0; t0 < Tm; t0 += PF) {
 #pragma unroll
-      for (int k = 0; k < NX; ++k) lf = fma(Qfb[j * NX + k], zl[k], lf);
-      cost = fma(xb, lf, cost);
+      for (int s = 0; s < PF; ++s) step(t0 + s, ring[s]);
     }
-    wave_lds_fence();
+#pragma unroll
+    for (int s = 0; s < PF - 1; ++s)
+      if (Tm + s < T) step(Tm + s, ring[s]);
+    // final cost ℓ_f(x̄_N) on the raw state (:192)
+    if (is_x) xnew[(size_t)b * (T + 1) * NX + (size_t)T * NX + j] = xb;
+    const double lf = dpp_dot12(is_x ? xb : 0.0, Qfr);
+    cost = fma(is_x ? xb : 0.0, lf, cost);
     cost = rowsum16(cost);
     out.trials = trial;
     out.cost = cost;
@@ -468,14 +544,12 @@ __global__ __launch_bounds__(64) void lq_forward_kernel(
     const double* __restrict__ prev_cost, double* __restrict__ xnew, double* __restrict__ unew,
     double* __restrict__ new_cost, int32_t* __restrict__ trials, int32_t* __restrict__ status,
     LSParams ls) {
-  __shared__ __attribute__((aligned(16))) double lds[4 * FW_LDS];
   const int g = threadIdx.x >> 4;
   const int j = threadIdx.x & 15;
   const int b = blockIdx.x * 4 + g;
   if (b >= B) return;  // whole 16-lane group: no cross-group LDS traffic
   const double pc = prev_cost ? prev_cost[b] : INFINITY;
-  FwdOut r = lq_forward_group<NX, NU>(P, b, T, x, u, xtraj, d, K, pc, xnew, unew, nullptr, ls,
-                                      lds + g * FW_LDS);
+  FwdOut r = lq_forward_group<NX, NU>(P, b, T, x, u, xtraj, d, K, pc, xnew, unew, nullptr, ls);
   if (!r.accepted) {
     // line search exhausted (the reference would loop forever): return the inputs.
     // Lanes of a group write disjoint elements; nothing reads them in this launch.
@@ -512,14 +586,13 @@ __global__ __launch_bounds__(256) void lq_iter_backward_kernel(LQParams P, int B
 template <int NX, int NU>
 __global__ __launch_bounds__(64) void lq_iter_forward_kernel(LQParams P, int B, int T, IterArgs a,
                                                              LSParams ls) {
-  __shared__ __attribute__((aligned(16))) double lds[4 * FW_LDS];
   const int g = threadIdx.x >> 4;
   const int j = threadIdx.x & 15;
   const int b = blockIdx.x * 4 + g;
   if (b >= B || a.status[b] != ILQR_TRAJ_OK) return;
   double du2 = 0.0;
   const FwdOut r = lq_forward_group<NX, NU>(P, b, T, a.x, a.u, a.xtraj, a.d, a.K, a.prev_cost[b],
-                                            a.xnew, a.unew, &du2, ls, lds + g * FW_LDS);
+                                            a.xnew, a.unew, &du2, ls);
   if (j == 0) {
     if (a.trials) a.trials[b] = r.trials;
     if (a.du2) a.du2[b] = du2;

@@ -1,0 +1,68 @@
+"""CPU multi-process tests (gloo, world_size 2) of the sharded path: each rank fits
+its contiguous block of trajectories, then the per-trajectory costs/status are
+all-gathered; the result must equal a single-process fit of the whole batch.
+The per-rank solver here is the C restatement (CPU); on GPUs bench.py runs the
+same sharding and gather over RCCL with the HIP solver."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from ilqr_amd.dist import all_gather_ragged, gather_fit_results, shard_range
+from ilqr_amd.problems import quadrotor_batch
+
+
+def test_shard_range_covers_batch():
+    for n in (1, 7, 4096, 32768, 32771):
+        for w in (1, 2, 3, 8):
+            spans = [shard_range(n, r, w) for r in range(w)]
+            assert spans[0][0] == 0 and spans[-1][1] == n
+            assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+            assert max(h - l for l, h in spans) - min(h - l for l, h in spans) <= 1
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, n, q):
+    import torch.distributed as dist
+    from oracle import cref
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    lq, x, u = quadrotor_batch(n, T=12, seed0=0)
+    lo, hi = shard_range(n, rank, world)
+    sub = lq.slice(lo, hi)
+    _, _, cost, iters, st = cref.lq_fit(sub, x[lo:hi], u[lo:hi], max_iter=20, tol=1e-6, nthreads=1)
+    gc, gs = gather_fit_results(torch.from_numpy(cost), torch.from_numpy(st))
+    xs = all_gather_ragged(torch.arange(lo, hi, dtype=torch.int64))
+    if rank == 0:
+        q.put((gc.numpy(), gs.numpy(), xs.numpy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n", [10, 13])
+def test_two_rank_fit_gather_matches_single_process(n):
+    from oracle import cref
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, n, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    gc, gs, idx = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    lq, x, u = quadrotor_batch(n, T=12, seed0=0)
+    _, _, cost, iters, st = cref.lq_fit(lq, x, u, max_iter=20, tol=1e-6, nthreads=1)
+    assert np.array_equal(idx, np.arange(n))
+    assert np.array_equal(gc, cost) and np.array_equal(gs, st)

@@ -26,9 +26,14 @@ pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
 LQ_FIXTURES = ["quad_t16", "quad_t100_sym", "dense_t16", "dense_t64_sym", "dense_xtraj"]
 
-TOL_GAIN = 1e-8
+TOL_GAIN = 1e-8       # vs the LITERAL oracle: bounded by the literal recursion's own drift (< 1e-9 on these fixtures)
+TOL_GAIN_SYM = 1e-11  # vs the symmetrised oracle (identity in exact arithmetic)
 TOL_ROLL = 1e-10
 TOL_COST = 1e-11
+
+
+def tol_gain(g):
+    return TOL_GAIN_SYM if json.loads(str(g["meta"]))["symmetrize"] else TOL_GAIN
 
 
 def rel(a, b):
@@ -64,8 +69,8 @@ def test_backward_matches_golden(gpu, name):
     s, _ = solver_for(g)
     d, K, st = s.backward(dev(g["x"]), dev(g["u"]))
     assert (st.cpu().numpy() == 0).all()
-    assert rel(K, g["K"]) < TOL_GAIN, rel(K, g["K"])
-    assert rel(d, g["d"]) < TOL_GAIN, rel(d, g["d"])
+    assert rel(K, g["K"]) < tol_gain(g), rel(K, g["K"])
+    assert rel(d, g["d"]) < tol_gain(g), rel(d, g["d"])
 
 
 @pytest.mark.parametrize("name", LQ_FIXTURES)
@@ -142,7 +147,7 @@ def test_ragged_batches_and_short_horizons(gpu, nb, T):
     s.set_problem(lq)
     d, K, st = s.backward(dev(x), dev(u))
     dc, Kc, _ = cref.lq_backward(lq, x, u, symmetrize=True)
-    assert rel(K, Kc) < TOL_GAIN and rel(d, dc) < TOL_GAIN
+    assert rel(K, Kc) < TOL_GAIN_SYM and rel(d, dc) < TOL_GAIN_SYM
     pc = torch.full((nb,), float("inf"), dtype=torch.float64, device="cuda")
     xn, un, c, tr, st = s.forward(dev(x), dev(u), d, K, pc)
     xo, uo, co, tro = cref.lq_forward(lq, x, u, None, d.cpu().numpy(), K.cpu().numpy(), np.inf)
@@ -203,28 +208,36 @@ def test_headline_backward_vs_c_oracle(gpu, headline):
     sub = lq.slice(0, 4096)
     sub = LQBatch(lq.A[idx], lq.B[idx], lq.Q[idx], lq.R[idx], lq.Qf[idx])
     dc, Kc, stc = cref.lq_backward(sub, x[idx], u[idx], symmetrize=True)
-    assert rel(K.cpu().numpy()[idx], Kc) < TOL_GAIN and rel(d.cpu().numpy()[idx], dc) < TOL_GAIN
+    assert rel(K.cpu().numpy()[idx], Kc) < TOL_GAIN_SYM and rel(d.cpu().numpy()[idx], dc) < TOL_GAIN_SYM
 
 
 def test_headline_fit_reaches_kkt_and_cost_is_monotone(gpu, headline):
     s, lq, x, u = headline
+    # three iterations with tol disabled: every trajectory improves (α = 1 from cold,
+    # then strictly decreasing costs — the @assert(prev_cost > new_cost) of :168)
     xi, ui = dev(x), dev(u)
     xn, un = torch.empty_like(xi), torch.empty_like(ui)
     pc = torch.full((4096,), float("inf"), dtype=torch.float64, device="cuda")
     st = torch.zeros((4096,), dtype=torch.int32, device="cuda")
     costs = []
-    o = _lib.default_options(tol=-1.0)  # tol disabled: every trajectory iterates
-    for _ in range(6):
+    o = _lib.default_options(tol=-1.0)
+    for _ in range(3):
         s.iterate(xi, ui, xn, un, pc, st, options=o)
         costs.append(pc.clone())
         xi, xn, ui, un = xn, xi, un, ui
     torch.cuda.synchronize()
     assert (st.cpu().numpy() == 0).all()
     c = torch.stack(costs).cpu().numpy()
-    assert (np.diff(c, axis=0) <= 0).all()  # @assert(prev_cost > new_cost) (:168) or equal at the fixed point
+    assert (np.diff(c, axis=0) < 0).all()
+    # fit to the fixed point: iLQR's fixed point is the exact LQ minimiser (KKT). Once
+    # no step can lower the cost the reference's line search would spin forever; the
+    # device stops that trajectory (LS_EXHAUSTED) at its fixed point.
+    r = s.fit(dev(x), dev(u), max_iter=30, tol=1e-14)
+    stf = r.status.cpu().numpy()
+    assert np.isin(stf, [_lib.TRAJ_CONVERGED, _lib.TRAJ_LS_EXHAUSTED, _lib.TRAJ_MAX_ITER]).all()
     for b in (0, 1234, 4095):
         X, U = O.lq_kkt_solution(lq.A[b], lq.B[b], lq.Q[b], lq.R[b], lq.Qf[b], x[b, 0], 100)
-        assert rel(ui[b], U) < 1e-6, rel(ui[b], U)
+        assert rel(r.u[b], U) < 1e-6, rel(r.u[b], U)
 
 
 def test_headline_iterate_matches_backward_plus_forward(gpu, headline):
