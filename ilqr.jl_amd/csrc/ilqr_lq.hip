@@ -142,7 +142,10 @@ struct LDLT {
 // Writes d (T,NU) and K (T,NU,NX) of trajectory b. Returns true if any gain is NaN
 // (the reference's @assert !any(isnan, δu/K), :353-354).
 // ---------------------------------------------------------------------------
-template <int NX, int NU>
+// ABL: ablation bits for tools/ablate_bw.hip only (0 in the product): 1 skip the
+// factor/solve, 2 skip symmetrisation, 4 skip the LDS hand-off, 8 skip gain stores,
+// 16 skip the gradient reduction. Ablated variants compute wrong gains.
+template <int NX, int NU, int ABL = 0>
 __device__ bool lq_backward_wave(const LQParams& P, int b, int T, const double* __restrict__ x,
                                  const double* __restrict__ u, double* __restrict__ d_out,
                                  double* __restrict__ K_out, double mu, double* lds) {
@@ -256,7 +259,7 @@ __device__ bool lq_backward_wave(const LQParams& P, int b, int T, const double* 
       part = fma(Lc[r], zc[r], part);
       if (r == SROW / 4) part += (q == SROW % 4) ? Y[r] : 0.0;
     }
-    const double gq = colsum4(part);
+    const double gq = (ABL & 16) ? part : colsum4(part);
 
     // hand the NU rows [G | H] and g to every lane
 #pragma unroll
@@ -265,43 +268,64 @@ __device__ bool lq_backward_wave(const LQParams& P, int b, int T, const double* 
       if (i >= NX && i < NX + NU) Gl[(i - NX) * 16 + c] = Z[r];
     }
     if (q == 0) gl[c] = gq;
-    wave_lds_fence();
     double h[NU][NU];
-#pragma unroll
-    for (int i = 0; i < NU; ++i)
-#pragma unroll
-      for (int k = 0; k <= i; ++k) h[i][k] = Gl[i * 16 + NX + k];
     d4 col = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-    for (int j = 0; j < NU; ++j) {
-      const double Gj = Gl[j * 16 + c];
-      const double gj = gl[NX + j];
-      col[j] = cx ? Gj : (c == SROW ? gj : 0.0);
-    }
     const int qq = q < NU ? q : 0;
-    const double Gq = Gl[qq * 16 + c];
-    const double gqq = gl[NX + qq];
-    const double colq = cx ? Gq : (c == SROW ? gqq : 0.0);
+    double colq;
     double qv[KS];
+    if constexpr ((ABL & 4) != 0) {
 #pragma unroll
-    for (int r = 0; r < KS; ++r) {
-      const int i = q + 4 * r;
-      const double gv = gl[i < NX ? i : 0];
-      qv[r] = (i < NX) ? gv : 0.0;
+      for (int i = 0; i < NU; ++i)
+#pragma unroll
+        for (int k = 0; k <= i; ++k) h[i][k] = Z[(i + k) & 3] + (i == k ? 10.0 : 0.0);
+#pragma unroll
+      for (int j = 0; j < NU; ++j) col[j] = Z[j] * gq;
+      colq = Z[3];
+#pragma unroll
+      for (int r = 0; r < KS; ++r) qv[r] = gq;
+    } else {
+      wave_lds_fence();
+#pragma unroll
+      for (int i = 0; i < NU; ++i)
+#pragma unroll
+        for (int k = 0; k <= i; ++k) h[i][k] = Gl[i * 16 + NX + k];
+#pragma unroll
+      for (int j = 0; j < NU; ++j) {
+        const double Gj = Gl[j * 16 + c];
+        const double gj = gl[NX + j];
+        col[j] = cx ? Gj : (c == SROW ? gj : 0.0);
+      }
+      const double Gq = Gl[qq * 16 + c];
+      const double gqq = gl[NX + qq];
+      colq = cx ? Gq : (c == SROW ? gqq : 0.0);
+#pragma unroll
+      for (int r = 0; r < KS; ++r) {
+        const int i = q + 4 * r;
+        const double gv = gl[i < NX ? i : 0];
+        qv[r] = (i < NX) ? gv : 0.0;
+      }
+      wave_lds_fence();
     }
-    wave_lds_fence();
 
     // feedback_parameters (:207-218): K_aug[:,c] = -(H + μI)⁻¹ [G | g][:,c]
-    LDLT<NU> f;
-    f.factor(h, mu);
-    const d4 xs = f.solve(col);
+    d4 xs;
+    if constexpr ((ABL & 1) != 0) {
+      asm volatile("" ::"v"(h[0][0]), "v"(h[1][0]), "v"(h[2][1]), "v"(h[3][3]));
+      xs = col * 1e-3;
+    } else {
+      LDLT<NU> f;
+      f.factor(h, mu);
+      xs = f.solve(col);
+    }
     const double kq = (q < NU) ? -xs[qq] : 0.0;              // K_aug[q][c]
     const double wk = (q < NU) ? fma(mu, kq, -colq) : 0.0;   // ((H + 2μI) K_aug)[q][c]
     nan |= __builtin_isnan(kq);
 
-    if (q < NU) {
-      if (cx) Kb[((size_t)t * NU + q) * NX + c] = kq;
-      else if (c == SROW) db[(size_t)t * NU + q] = kq;
+    if constexpr ((ABL & 8) == 0) {
+      if (q < NU) {
+        if (cx) Kb[((size_t)t * NU + q) * NX + c] = kq;
+        else if (c == SROW) db[(size_t)t * NU + q] = kq;
+      }
     }
 
     // step_back (:269-270): Sp ← [Qxx | lx + Aᵀs] − K_augᵀ (H + 2μI) K_aug
@@ -319,7 +343,7 @@ __device__ bool lq_backward_wave(const LQParams& P, int b, int T, const double* 
     // accumulator tile feeds the next Y MFMA as its own transpose, so rounding
     // asymmetry E evolves as E ← −AᵀEA and grows like ρ(A)^2t on unstable A;
     // a periodic projection bounds it at negligible cost.
-    if ((t % SYM_EVERY) == 0) {
+    if ((ABL & 2) == 0 && (t % SYM_EVERY) == 0) {
       double* tile = lds + 80;  // 16 × 17 (padded) doubles
 #pragma unroll
       for (int r = 0; r < 4; ++r) tile[(q + 4 * r) * 17 + c] = Sp[r];

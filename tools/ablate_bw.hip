@@ -1,0 +1,55 @@
+// Ablation harness for the backward kernel (not part of the product): times
+// lq_backward_wave<12,4,ABL> for several ABL bit sets at B=4096, T=100 so the
+// share of MFMA / factor+solve / LDS hand-off / stores / gradient can be read off.
+#include "../ilqr.jl_amd/csrc/ilqr_lq.hip"
+#include <cstdio>
+#include <vector>
+#include <random>
+using namespace ilqr;
+template <int ABL>
+__global__ __launch_bounds__(256) void abl_kernel(LQParams P, int B, int T, const double* x, const double* u,
+                                                  double* d, double* K, int* flag) {
+  __shared__ __attribute__((aligned(16))) double lds[WAVES_PER_WG * BW_LDS];
+  const int w = threadIdx.x >> 6;
+  const int b = blockIdx.x * WAVES_PER_WG + w;
+  if (b >= B) return;
+  bool nan = lq_backward_wave<12, 4, ABL>(P, b, T, x, u, d, K, 0.01, lds + w * BW_LDS);
+  if (nan && (threadIdx.x & 63) == 0) atomicAdd(flag, 1);
+}
+#define CK(x) do { hipError_t e=(x); if(e!=hipSuccess){printf("err %s line %d\n",hipGetErrorString(e),__LINE__); return 1;} } while(0)
+template <int ABL>
+int run(const char* name, LQParams P, int B, int T, double* x, double* u, double* d, double* K, int* flag) {
+  hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  int grid = (B + 3) / 4;
+  for (int i = 0; i < 3; ++i) abl_kernel<ABL><<<grid, 256>>>(P, B, T, x, u, d, K, flag);
+  CK(hipDeviceSynchronize());
+  const int R = 20;
+  CK(hipEventRecord(e0));
+  for (int i = 0; i < R; ++i) abl_kernel<ABL><<<grid, 256>>>(P, B, T, x, u, d, K, flag);
+  CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+  float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+  printf("%-40s %8.1f us\n", name, 1000.0 * ms / R);
+  return 0;
+}
+int main() {
+  const int B = 4096, T = 100, n = 12, m = 4;
+  std::mt19937_64 g(1); std::uniform_real_distribution<double> U(-1, 1);
+  auto mk = [&](size_t N, double sc, bool eye, int dim) { std::vector<double> v(N); for (auto& e : v) e = sc * U(g);
+    if (eye) for (size_t b = 0; b < N / (dim * dim); ++b) for (int i = 0; i < dim; ++i) v[b * dim * dim + i * dim + i] += 1.0; return v; };
+  auto A = mk((size_t)B * n * n, 0.02, true, n), Bm = mk((size_t)B * n * m, 0.1, false, 1);
+  auto Q = mk((size_t)B * n * n, 0.0, true, n), R = mk((size_t)B * m * m, 0.0, true, m), Qf = Q;
+  auto x = mk((size_t)B * (T + 1) * n, 1.0, false, 1), u = mk((size_t)B * T * m, 0.1, false, 1);
+  auto up = [&](std::vector<double>& v) { double* p; hipMalloc(&p, v.size() * 8); hipMemcpy(p, v.data(), v.size() * 8, hipMemcpyHostToDevice); return p; };
+  LQParams P{up(A), up(Bm), up(Q), up(R), up(Qf)};
+  double *xd = up(x), *ud = up(u), *d, *K; int* flag;
+  CK(hipMalloc(&d, (size_t)B * T * m * 8)); CK(hipMalloc(&K, (size_t)B * T * m * n * 8)); CK(hipMalloc(&flag, 4));
+  run<0>("full", P, B, T, xd, ud, d, K, flag);
+  run<1>("no factor/solve", P, B, T, xd, ud, d, K, flag);
+  run<2>("no symmetrisation", P, B, T, xd, ud, d, K, flag);
+  run<4>("no LDS hand-off", P, B, T, xd, ud, d, K, flag);
+  run<8>("no K/d stores", P, B, T, xd, ud, d, K, flag);
+  run<16>("no gradient reduction", P, B, T, xd, ud, d, K, flag);
+  run<31>("MFMA chain + selects only", P, B, T, xd, ud, d, K, flag);
+  run<0>("full (again)", P, B, T, xd, ud, d, K, flag);
+  return 0;
+}
