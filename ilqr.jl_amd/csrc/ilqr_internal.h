@@ -51,8 +51,12 @@ hipError_t launch_lq_forward(int nx, int nu, const LQParams& p, int B, int T, co
                              const double* K, const double* prev_cost, double* xnew,
                              double* unew, double* new_cost, int32_t* trials, int32_t* status,
                              const LSParams& ls, hipStream_t s);
-hipError_t launch_lq_iterate(int nx, int nu, const LQParams& p, int B, int T, const IterArgs& a,
-                             const LSParams& ls, hipStream_t s);
+// The two halves of one fit iteration over trajectories [b0, b1) (pointers in
+// `a` and `p` address the whole batch).
+hipError_t launch_lq_iter_backward(int nx, int nu, const LQParams& p, int b0, int b1, int T,
+                                   const IterArgs& a, double mu, hipStream_t s);
+hipError_t launch_lq_iter_forward(int nx, int nu, const LQParams& p, int b0, int b1, int T,
+                                  const IterArgs& a, const LSParams& ls, hipStream_t s);
 // x_out[b] = (res_parity[b] ? x1 : x0)[b] (and u); status MAX_ITER for still-running ones.
 hipError_t launch_gather_result(int B, int T, int nx, int nu, const double* x0, const double* u0,
                                 const double* x1, const double* u1, const int32_t* res_parity,

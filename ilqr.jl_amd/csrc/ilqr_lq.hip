@@ -26,7 +26,8 @@
 //  * forward: 16 lanes per trajectory (4 trajectories per wave, one DPP row each);
 //    lane j < nx owns x̄_j, lanes nx.. own ū; mat-vecs broadcast the distributed
 //    vector with v_fmac_f64_dpp row_newbcast, inputs prefetched 4 steps ahead.
-//  * one fit iteration = backward launch (4 waves/SIMD) + forward launch.
+//  * one fit iteration = backward launch (4 waves/SIMD) + forward launch; the ABI
+//    pipelines them over two batch chunks on two streams (ilqr_abi.cpp).
 #include <hip/hip_runtime.h>
 #include <math.h>
 
@@ -82,7 +83,8 @@ __device__ __forceinline__ void wave_lds_fence() {
   __builtin_amdgcn_wave_barrier();
 }
 
-// 1/x: v_rcp_f64 + two Newton steps (≤1 ulp), no IEEE div sequence.
+// 1/x: v_rcp_f64 (≈2^-24 relative on gfx950) + two Newton steps. Measured by
+// tools/rcp_test.hip: 0 steps 2.5e8 ulp, 1 step 11 ulp, 2 steps 0 ulp.
 __device__ __forceinline__ double rcp(double x) {
   double r = __builtin_amdgcn_rcp(x);
   double e = fma(-x, r, 1.0);
@@ -437,7 +439,7 @@ __device__ FwdOut lq_forward_group(const LQParams& P, int b, int T, const double
                                    const LSParams& ls) {
   static_assert(NX + NU == 16, "one 16-lane DPP row per trajectory: nx + nu == 16");
   static_assert(NX == 12, "dpp_dot12 is the K·δx product");
-  constexpr int PF = 4;  // prefetch distance (steps)
+  constexpr int PF = 2;  // prefetch distance (steps)
   const int j = threadIdx.x & 15;
   const bool is_x = j < NX;
   const bool is_u = !is_x;
@@ -451,7 +453,7 @@ __device__ FwdOut lq_forward_group(const LQParams& P, int b, int T, const double
   const double* Qfb = P.Qf + (size_t)b * NX * NX;
 
   // row j of F = [A B] (lanes j < NX) and of L = blockdiag(Q, R) (ℓ = vᵀ L v)
-  double Fr[16], Lr[16], Qfr[NX];
+  double Fr[16], Lr[16];
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
     const double a = ldz(is_x && k < NX, Ab + jx * NX + (k < NX ? k : 0), Ab);
@@ -461,8 +463,6 @@ __device__ FwdOut lq_forward_group(const LQParams& P, int b, int T, const double
     const double lr = ldz(is_u && k >= NX, Rb + iu * NU + (k >= NX ? k - NX : 0), Rb);
     Lr[k] = lq + lr;
   }
-#pragma unroll
-  for (int k = 0; k < NX; ++k) Qfr[k] = ldz(is_x, Qfb + jx * NX + k, Qfb);
 
   const double* xb0 = x + (size_t)b * (T + 1) * NX;
   const double* ub0 = u + (size_t)b * T * NU;
@@ -528,6 +528,9 @@ __device__ FwdOut lq_forward_group(const LQParams& P, int b, int T, const double
       if (Tm + s < T) step(Tm + s, ring[s]);
     // final cost ℓ_f(x̄_N) on the raw state (:192)
     if (is_x) xnew[(size_t)b * (T + 1) * NX + (size_t)T * NX + j] = xb;
+    double Qfr[NX];
+#pragma unroll
+    for (int k = 0; k < NX; ++k) Qfr[k] = ldz(is_x, Qfb + jx * NX + k, Qfb);
     const double lf = dpp_dot12(is_x ? xb : 0.0, Qfr);
     cost = fma(is_x ? xb : 0.0, lf, cost);
     cost = rowsum16(cost);
@@ -722,11 +725,51 @@ hipError_t launch_lq_forward(int nx, int nu, const LQParams& p, int B, int T, co
   return hipErrorInvalidValue;
 }
 
-hipError_t launch_lq_iterate(int nx, int nu, const LQParams& p, int B, int T, const IterArgs& a,
-                             const LSParams& ls, hipStream_t s) {
+namespace {
+LQParams shift(const LQParams& p, int nx, int nu, int b0) {
+  return LQParams{p.A + (size_t)b0 * nx * nx, p.B + (size_t)b0 * nx * nu, p.Q + (size_t)b0 * nx * nx,
+                  p.R + (size_t)b0 * nu * nu, p.Qf + (size_t)b0 * nx * nx};
+}
+template <class T>
+T* off(T* p, size_t n) { return p ? p + n : p; }
+IterArgs shift(const IterArgs& a, int nx, int nu, int T, int b0) {
+  IterArgs r = a;
+  const size_t b = (size_t)b0;
+  r.x = off(a.x, b * (T + 1) * nx);
+  r.u = off(a.u, b * T * nu);
+  r.xtraj = off(a.xtraj, b * (T + 1) * nx);
+  r.xnew = off(a.xnew, b * (T + 1) * nx);
+  r.unew = off(a.unew, b * T * nu);
+  r.K = off(a.K, b * T * nu * nx);
+  r.d = off(a.d, b * T * nu);
+  r.prev_cost = off(a.prev_cost, b);
+  r.du2 = off(a.du2, b);
+  r.trials = off(a.trials, b);
+  r.status = off(a.status, b);
+  r.res_parity = off(a.res_parity, b);
+  r.iters = off(a.iters, b);
+  return r;
+}
+}  // namespace
+
+hipError_t launch_lq_iter_backward(int nx, int nu, const LQParams& p, int b0, int b1, int T,
+                                   const IterArgs& a, double mu, hipStream_t s) {
+  const int B = b1 - b0;
+  if (B <= 0) return hipSuccess;
   const int grid = (B + WAVES_PER_WG - 1) / WAVES_PER_WG;
-  ILQR_DISPATCH(12, 4, (lq_iter_backward_kernel<NX_, NU_><<<grid, 256, 0, s>>>(p, B, T, a, ls.mu),
-                        lq_iter_forward_kernel<NX_, NU_><<<(B + 3) / 4, 64, 0, s>>>(p, B, T, a, ls)));
+  const LQParams ps = shift(p, nx, nu, b0);
+  const IterArgs as = shift(a, nx, nu, T, b0);
+  ILQR_DISPATCH(12, 4, (lq_iter_backward_kernel<NX_, NU_><<<grid, 256, 0, s>>>(ps, B, T, as, mu)));
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_lq_iter_forward(int nx, int nu, const LQParams& p, int b0, int b1, int T,
+                                  const IterArgs& a, const LSParams& ls, hipStream_t s) {
+  const int B = b1 - b0;
+  if (B <= 0) return hipSuccess;
+  const LQParams ps = shift(p, nx, nu, b0);
+  const IterArgs as = shift(a, nx, nu, T, b0);
+  ILQR_DISPATCH(12, 4, (lq_iter_forward_kernel<NX_, NU_><<<(B + 3) / 4, 64, 0, s>>>(ps, B, T, as, ls)));
   return hipErrorInvalidValue;
 }
 

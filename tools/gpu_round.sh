@@ -1,6 +1,6 @@
 #!/bin/bash
-# One GPU session: tests, smoke, bench, kernel-trace profile. Each GPU step has its own
-# time limit; a crash-class exit (fault/abort/segv/timeout) stops the script.
+# One GPU session: tests, smoke, bench, kernel-trace profile, diagnostics. Each GPU
+# step has its own time limit; a crash-class exit (fault/abort/segv/timeout) stops.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -14,14 +14,14 @@ step() {  # step <name> <timeout> <cmd...>
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
   return 0
 }
-WHAT=${1:-all}
-if [[ $WHAT == all || $WHAT == test ]]; then
-  step pytest_gpu 600 python -m pytest tests -m gpu -x -q
-  step smoke 180 python -c "import __graft_entry__ as g; g.smoke()"
-fi
-if [[ $WHAT == all || $WHAT == bench ]]; then
-  step bench 300 python bench.py --steps 20 --warmup 3
-fi
-if [[ $WHAT == all || $WHAT == prof ]]; then
-  step rocprof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu
-fi
+for WHAT in "$@"; do
+case $WHAT in
+  test) step pytest_gpu 600 python -m pytest tests -m gpu -x -q
+        step smoke 180 python -c "import __graft_entry__ as g; g.smoke()" ;;
+  bench) step bench 300 python bench.py --steps 20 --warmup 3 ;;
+  prof) step rocprof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu ;;
+  ablate) step ablate 120 ./tools/ablate_bw ;;
+  rcp) step rcp 60 ./tools/rcp_test ;;
+  ubench) step ubench 120 ./tools/ubench_f64 ;;
+esac
+done
