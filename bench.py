@@ -131,10 +131,10 @@ def main():
     stream = torch.cuda.current_stream(dev)
     s._bind_stream()
 
-    def step():
-        pc.fill_(float("inf"))
-        st.zero_()
-        s.iterate(x, u, xn, un, pc, st, trials=trials, options=opts)
+    st.zero_()  # stays 0: from a cold start no trajectory converges or exhausts
+
+    def step():  # cold start: prev_cost = +Inf (NULL), the new cost lands in pc
+        s.iterate(x, u, xn, un, None, st, trials=trials, options=opts, new_cost=pc)
 
     for _ in range(args.warmup):
         step()

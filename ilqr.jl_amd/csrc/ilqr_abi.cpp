@@ -271,12 +271,13 @@ ilqr_status ilqr_forward(ilqr_handle* h, const ilqr_problem* p, const ilqr_optio
 
 ilqr_status ilqr_iterate(ilqr_handle* h, const ilqr_problem* p, const ilqr_options* o,
                          const double* x, const double* u, const double* x_traj, double* x_new,
-                         double* u_new, double* prev_cost, double* du2, int32_t* trials,
+                         double* u_new, const double* prev_cost, double* new_cost, double* du2,
+                         int32_t* trials,
                          int32_t* status) {
   ilqr_status st = check_problem(h, p);
   if (st != ILQR_OK) return st;
   if ((st = check_options(o)) != ILQR_OK) return st;
-  if (!x || !u || !x_new || !u_new || !prev_cost || !status) return ILQR_ERR_BAD_ARG;
+  if (!x || !u || !x_new || !u_new || !new_cost || !status) return ILQR_ERR_BAD_ARG;
   HIP_TRY(hipSetDevice(h->device));
   ilqr::IterArgs a{};
   a.x = x;
@@ -287,6 +288,7 @@ ilqr_status ilqr_iterate(ilqr_handle* h, const ilqr_problem* p, const ilqr_optio
   a.K = h->K;
   a.d = h->d;
   a.prev_cost = prev_cost;
+  a.new_cost = new_cost;
   a.du2 = du2;
   a.trials = trials;
   a.status = status;
@@ -330,7 +332,8 @@ ilqr_status ilqr_fit(ilqr_handle* h, const ilqr_problem* p, const ilqr_options* 
     a.unew = h->ubuf[par ^ 1];
     a.K = h->K;
     a.d = h->d;
-    a.prev_cost = h->prev_cost;
+    a.prev_cost = h->prev_cost;  // in place: prev_cost = new_cost (:168)
+    a.new_cost = h->prev_cost;
     a.du2 = h->du2;
     a.trials = h->trials;
     a.status = h->status;

@@ -32,7 +32,8 @@ struct IterArgs {
   double* unew;         // (B, T, nu)
   double* K;            // (B, T, nu, nx) gains workspace
   double* d;            // (B, T, nu)
-  double* prev_cost;    // (B) in/out
+  const double* prev_cost;  // (B) in; nullptr = +Inf (fit's first iteration, forward_pass.jl:159)
+  double* new_cost;         // (B) out: cost of the accepted rollout (may alias prev_cost)
   double* du2;          // (B) out, may be null
   int32_t* trials;      // (B) out, may be null
   int32_t* status;      // (B) in/out (non-zero = skip)

@@ -41,7 +41,7 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 typedef unsigned u2v __attribute__((ext_vector_type(2)));
 
 constexpr int WAVES_PER_WG = 4;   // trajectories per workgroup
-constexpr int BW_LDS = 80 + 16 * 17;  // doubles of backward scratch per wave: [G|H] rows, g row, S tile
+constexpr int BW_LDS = 96 + 16 * 17;  // doubles of backward scratch per wave: [G|H] rows, g row, zero, S tile
 constexpr int SYM_EVERY = 4;          // symmetrise S every this many steps
 
 __device__ __forceinline__ d4 mfma(double a, double b, d4 c) {
@@ -194,6 +194,17 @@ __device__ bool lq_backward_wave(const LQParams& P, int b, int T, const double* 
 
   double* Gl = lds;       // Gl[j*16 + c] = Z[NX+j][c]   (j < NU): [G | H] rows
   double* gl = lds + 64;  // gl[c] = (L z + Fᵀ s)[c]:   [lx + Aᵀs | lu + Bᵀs]
+  constexpr int ZERO = 80;  // a slot holding 0.0: lanes with nothing to read read it
+  lds[ZERO] = 0.0;
+  // per-lane LDS addresses of the hand-off reads (branch-free: one ds_read each)
+  int col_at[NU];
+#pragma unroll
+  for (int j = 0; j < NU; ++j) col_at[j] = cx ? j * 16 + c : (c == SROW ? 64 + NX + j : ZERO);
+  const int qq = q < NU ? q : 0;
+  const int colq_at = cx ? qq * 16 + c : (c == SROW ? 64 + NX + qq : ZERO);
+  int qv_at[KS];
+#pragma unroll
+  for (int r = 0; r < KS; ++r) qv_at[r] = (c == SROW && q + 4 * r < NX) ? 64 + q + 4 * r : ZERO;
 
   // Terminal value function (final_cost_quadratization :134-153, ℓ_f = xᵀQf x):
   // S = Qf+Qfᵀ, s = (Qf+Qfᵀ) x_N.
@@ -269,10 +280,9 @@ __device__ bool lq_backward_wave(const LQParams& P, int b, int T, const double* 
       const int i = q + 4 * r;
       if (i >= NX && i < NX + NU) Gl[(i - NX) * 16 + c] = Z[r];
     }
-    if (q == 0) gl[c] = gq;
+    gl[c] = gq;  // the four lanes of column c hold the same value
     double h[NU][NU];
     d4 col = {0.0, 0.0, 0.0, 0.0};
-    const int qq = q < NU ? q : 0;
     double colq;
     double qv[KS];
     if constexpr ((ABL & 4) != 0) {
@@ -292,20 +302,10 @@ __device__ bool lq_backward_wave(const LQParams& P, int b, int T, const double* 
 #pragma unroll
         for (int k = 0; k <= i; ++k) h[i][k] = Gl[i * 16 + NX + k];
 #pragma unroll
-      for (int j = 0; j < NU; ++j) {
-        const double Gj = Gl[j * 16 + c];
-        const double gj = gl[NX + j];
-        col[j] = cx ? Gj : (c == SROW ? gj : 0.0);
-      }
-      const double Gq = Gl[qq * 16 + c];
-      const double gqq = gl[NX + qq];
-      colq = cx ? Gq : (c == SROW ? gqq : 0.0);
+      for (int j = 0; j < NU; ++j) col[j] = lds[col_at[j]];     // [G | g][j][c], 0 for c > NX
+      colq = lds[colq_at];                                      // [G | g][q][c]
 #pragma unroll
-      for (int r = 0; r < KS; ++r) {
-        const int i = q + 4 * r;
-        const double gv = gl[i < NX ? i : 0];
-        qv[r] = (i < NX) ? gv : 0.0;
-      }
+      for (int r = 0; r < KS; ++r) qv[r] = lds[qv_at[r]];       // (lx + Aᵀs)[q+4r] in column NX
       wave_lds_fence();
     }
 
@@ -324,10 +324,8 @@ __device__ bool lq_backward_wave(const LQParams& P, int b, int T, const double* 
     nan |= __builtin_isnan(kq);
 
     if constexpr ((ABL & 8) == 0) {
-      if (q < NU) {
-        if (cx) Kb[((size_t)t * NU + q) * NX + c] = kq;
-        else if (c == SROW) db[(size_t)t * NU + q] = kq;
-      }
+      double* dst = cx ? Kb + ((size_t)t * NU + qq) * NX + c : db + (size_t)t * NU + qq;
+      if (q < NU && c <= SROW) *dst = kq;
     }
 
     // step_back (:269-270): Sp ← [Qxx | lx + Aᵀs] − K_augᵀ (H + 2μI) K_aug
@@ -335,7 +333,7 @@ __device__ bool lq_backward_wave(const LQParams& P, int b, int T, const double* 
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       double v = 0.0;
-      if (r < KS) v = cx ? Z[r] : (c == SROW ? qv[r] : 0.0);
+      if (r < KS) v = cx ? Z[r] : qv[r];
       Cin[r] = (q + 4 * r < NX) ? v : 0.0;
     }
     Sp = mfma(-kq, wk, Cin);
@@ -346,15 +344,16 @@ __device__ bool lq_backward_wave(const LQParams& P, int b, int T, const double* 
     // asymmetry E evolves as E ← −AᵀEA and grows like ρ(A)^2t on unstable A;
     // a periodic projection bounds it at negligible cost.
     if ((ABL & 2) == 0 && (t % SYM_EVERY) == 0) {
-      double* tile = lds + 80;  // 16 × 17 (padded) doubles
+      double* tile = lds + 96;  // 16 × 17 (padded) doubles
 #pragma unroll
       for (int r = 0; r < 4; ++r) tile[(q + 4 * r) * 17 + c] = Sp[r];
       wave_lds_fence();
 #pragma unroll
       for (int r = 0; r < KS; ++r) {
         const int i = q + 4 * r;
-        const double other = tile[c * 17 + i];
-        if (i < NX && cx) Sp[r] = 0.5 * (Sp[r] + other);
+        const double other = tile[c * 17 + (i < NX ? i : 0)];  // unconditional read
+        const double avg = 0.5 * (Sp[r] + other);
+        Sp[r] = (i < NX && cx) ? avg : Sp[r];
       }
       wave_lds_fence();
     }
@@ -550,7 +549,7 @@ __device__ FwdOut lq_forward_group(const LQParams& P, int b, int T, const double
 // Kernels
 // ---------------------------------------------------------------------------
 template <int NX, int NU>
-__global__ __launch_bounds__(256) void lq_backward_kernel(LQParams P, int B, int T,
+__global__ __launch_bounds__(256, 4) void lq_backward_kernel(LQParams P, int B, int T,
                                                           const double* __restrict__ x,
                                                           const double* __restrict__ u,
                                                           double* __restrict__ d,
@@ -594,7 +593,7 @@ __global__ __launch_bounds__(64) void lq_forward_kernel(
 // One fit iteration (forward_pass.jl:161-176), part 1: backward_pass for every
 // trajectory whose status is OK (4 waves / workgroup, one trajectory per wave).
 template <int NX, int NU>
-__global__ __launch_bounds__(256) void lq_iter_backward_kernel(LQParams P, int B, int T, IterArgs a,
+__global__ __launch_bounds__(256, 4) void lq_iter_backward_kernel(LQParams P, int B, int T, IterArgs a,
                                                                double mu) {
   __shared__ __attribute__((aligned(16))) double lds[WAVES_PER_WG * BW_LDS];
   const int w = threadIdx.x >> 6;
@@ -618,7 +617,8 @@ __global__ __launch_bounds__(64) void lq_iter_forward_kernel(LQParams P, int B, 
   const int b = blockIdx.x * 4 + g;
   if (b >= B || a.status[b] != ILQR_TRAJ_OK) return;
   double du2 = 0.0;
-  const FwdOut r = lq_forward_group<NX, NU>(P, b, T, a.x, a.u, a.xtraj, a.d, a.K, a.prev_cost[b],
+  const double pc = a.prev_cost ? a.prev_cost[b] : INFINITY;
+  const FwdOut r = lq_forward_group<NX, NU>(P, b, T, a.x, a.u, a.xtraj, a.d, a.K, pc,
                                             a.xnew, a.unew, &du2, ls);
   if (j == 0) {
     if (a.trials) a.trials[b] = r.trials;
@@ -628,7 +628,7 @@ __global__ __launch_bounds__(64) void lq_iter_forward_kernel(LQParams P, int B, 
       a.status[b] = (r.cost != r.cost) ? ILQR_TRAJ_NAN : ILQR_TRAJ_LS_EXHAUSTED;
       if (a.res_parity) a.res_parity[b] = a.parity;
     } else {
-      a.prev_cost[b] = r.cost;  // @assert(prev_cost > new_cost); prev_cost = new_cost (:168)
+      a.new_cost[b] = r.cost;  // @assert(prev_cost > new_cost); prev_cost = new_cost (:168)
       if (du2 <= ls.tol) {      // (:171) break BEFORE the update → result is the input iterate
         a.status[b] = ILQR_TRAJ_CONVERGED;
         if (a.res_parity) a.res_parity[b] = a.parity;
@@ -743,6 +743,7 @@ IterArgs shift(const IterArgs& a, int nx, int nu, int T, int b0) {
   r.K = off(a.K, b * T * nu * nx);
   r.d = off(a.d, b * T * nu);
   r.prev_cost = off(a.prev_cost, b);
+  r.new_cost = off(a.new_cost, b);
   r.du2 = off(a.du2, b);
   r.trials = off(a.trials, b);
   r.status = off(a.status, b);

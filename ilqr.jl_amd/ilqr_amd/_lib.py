@@ -58,7 +58,7 @@ SIGNATURES = {
     "ilqr_forward": (C.c_int, [P, C.POINTER(Problem), C.POINTER(Options), P, P, P, P, P, P,
                                P, P, P, P, P]),
     "ilqr_iterate": (C.c_int, [P, C.POINTER(Problem), C.POINTER(Options), P, P, P, P, P, P,
-                               P, P, P]),
+                               P, P, P, P]),
     "ilqr_fit": (C.c_int, [P, C.POINTER(Problem), C.POINTER(Options), P, P, P, P, P, P, P, P]),
     "ilqr_malloc": (C.c_int, [P, C.c_size_t, C.POINTER(P)]),
     "ilqr_free": (C.c_int, [P, P]),

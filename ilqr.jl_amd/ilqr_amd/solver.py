@@ -138,13 +138,15 @@ class Solver:
         return xn, un, cost, trials, st
 
     def iterate(self, x, u, x_new, u_new, prev_cost, status, du2=None, trials=None,
-                x_traj=None, options=None):
+                x_traj=None, options=None, new_cost=None):
         """One fit iteration (backward + forward + convergence test), asynchronous.
-        No shape checks beyond the ABI's: the bench's hot loop."""
+        prev_cost None = +Inf (cold start); new_cost defaults to prev_cost (in
+        place, fit semantics). No shape checks beyond the ABI's: the bench's hot loop."""
         o = options if options is not None else _lib.default_options()
+        nc = new_cost if new_cost is not None else prev_cost
         rc = self.lib.ilqr_iterate(self.h, self._p(), C.byref(o), _ptr(x), _ptr(u), _ptr(x_traj),
-                                   _ptr(x_new), _ptr(u_new), _ptr(prev_cost), _ptr(du2),
-                                   _ptr(trials), _ptr(status))
+                                   _ptr(x_new), _ptr(u_new), _ptr(prev_cost), _ptr(nc),
+                                   _ptr(du2), _ptr(trials), _ptr(status))
         _lib.check(rc, "ilqr_iterate")
 
     def fit(self, x_init, u_init, x_traj=None, max_iter=100, tol=1e-6, mu=None,

@@ -132,14 +132,16 @@ ilqr_status ilqr_forward(ilqr_handle* h, const ilqr_problem* p, const ilqr_optio
                          int32_t* trials, int32_t* status);
 
 /* One iteration of fit's loop (forward_pass.jl:162-175) for every trajectory
- * whose status is ILQR_TRAJ_OK, fused in one launch: backward, forward, the
- * convergence test. Reads (x, u), writes (x_new, u_new); prev_cost is read and
- * updated in place; du2 (batch) receives Σ(ū_new − u)²; trajectories whose
- * status is non-zero are skipped. The bench "step". */
+ * whose status is ILQR_TRAJ_OK: backward, forward with line search, the
+ * convergence test. Reads (x, u), writes (x_new, u_new). prev_cost (batch) is
+ * the cost to beat (NULL = +Inf, fit's first iteration, forward_pass.jl:159);
+ * new_cost (batch, may alias prev_cost) receives the accepted cost; du2 (batch,
+ * may be NULL) receives Σ(ū_new − u)²; status is read (non-zero = skip) and
+ * set to CONVERGED / LS_EXHAUSTED / NAN. Asynchronous. The bench "step". */
 ilqr_status ilqr_iterate(ilqr_handle* h, const ilqr_problem* p, const ilqr_options* o,
                          const double* x, const double* u, const double* x_traj,
-                         double* x_new, double* u_new, double* prev_cost, double* du2,
-                         int32_t* trials, int32_t* status);
+                         double* x_new, double* u_new, const double* prev_cost,
+                         double* new_cost, double* du2, int32_t* trials, int32_t* status);
 
 /* iLQR.fit (forward_pass.jl:148-179) for the whole batch. x_init/u_init are
  * the starting trajectories; x_out/u_out receive the result, which — like the
