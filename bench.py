@@ -110,10 +110,19 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = world > 1
+    # one process per GPU; ILQR_DIST_BACKEND=gloo rehearses the multi-rank path on a
+    # box with fewer GPUs than ranks (ranks then share devices round-robin)
+    backend = os.environ.get("ILQR_DIST_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()
+    gpu = local % max(ndev, 1) if backend != "nccl" else local
     if dist:
         import torch.distributed as tdist
-        torch.cuda.set_device(local)
-        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        torch.cuda.set_device(gpu)
+        if backend == "nccl":
+            tdist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+        else:
+            tdist.init_process_group(backend)
+    local = gpu
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -156,8 +165,8 @@ def main():
     ms = e0.elapsed_time(e1) / args.steps
     ms_wall = wall * 1000.0 / args.steps
     ms_step = max(ms, ms_wall)
-    if dist:
-        tt = torch.tensor([ms_step], dtype=torch.float64, device=dev)
+    if dist:  # max over ranks
+        tt = torch.tensor([ms_step], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         tdist.all_reduce(tt, op=tdist.ReduceOp.MAX)
         ms_step = float(tt.item())
     mean_trials = float(trials.double().mean().item())
@@ -180,14 +189,18 @@ def main():
 
     # result exchange (fit output): all-gather the per-trajectory costs over RCCL
     gather_ms = None
+    gathered = None
     if dist:
-        out = [torch.empty_like(pc) for _ in range(world)]
+        from ilqr_amd.dist import gather_fit_results
         tdist.barrier()
         torch.cuda.synchronize()
         g0 = time.perf_counter()
-        tdist.all_gather(out, pc)
+        src_c, src_s = (pc, st) if backend == "nccl" else (pc.cpu(), st.cpu())
+        gc, gs = gather_fit_results(src_c, src_s)
         torch.cuda.synchronize()
         gather_ms = (time.perf_counter() - g0) * 1000.0
+        gathered = {"trajectories": int(gc.numel()), "finite_costs": int(torch.isfinite(gc).sum().item()),
+                    "status_ok": int((gs == 0).sum().item())}
 
     cnt = algorithmic_counts(T)
     bw_flops = cnt["bw_flops"] * B
@@ -230,6 +243,7 @@ def main():
                       "mean_line_search_trials": mean_trials, "all_ok": ok,
                       "event_ms": ms, "wall_ms": ms_wall},
         "allgather_costs_ms": gather_ms,
+        "allgather_check": gathered,
         "cpu_baseline": None,
     }
     if rank == 0 and not args.no_cpu:

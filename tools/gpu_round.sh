@@ -21,6 +21,7 @@ case $WHAT in
   bench) step bench 300 python bench.py --steps 20 --warmup 3 ;;
   prof) step rocprof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu ;;
   ablate) step ablate 120 ./tools/ablate_bw ;;
+  dist2) ILQR_DIST_BACKEND=gloo step dist2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 2 --steps 5 --warmup 1 --no-cpu ;;
   pmc) step pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- python bench.py --steps 5 --warmup 1 --no-cpu
        step pmc_write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run -- python bench.py --steps 5 --warmup 1 --no-cpu
        python profiles/collect_pmc.py gpurun_out/pmc_fetch gpurun_out/pmc_write gpurun_out/pmc.json > gpurun_out/pmc_summary.log 2>&1 ;;
