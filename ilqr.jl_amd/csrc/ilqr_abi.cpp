@@ -27,6 +27,8 @@ struct ilqr_handle {
   int32_t* status = nullptr;
   int32_t* res_parity = nullptr;
   int32_t* iters = nullptr;
+  // 2-link arm: per-step linearisation workspace J = [A|B] (T × 24 × batch)
+  double* J = nullptr;
   // pipelining: the batch is split into `nchunks` chunks; chunk i's forward pass
   // runs on `side` while chunk i+1's backward runs on `stream`
   hipStream_t side = nullptr;
@@ -57,11 +59,21 @@ ilqr::LQParams lq_params(const ilqr_problem* p) {
 
 ilqr_status check_problem(const ilqr_handle* h, const ilqr_problem* p) {
   if (!h || !p) return ILQR_ERR_BAD_ARG;
-  if (p->kind != ILQR_PROBLEM_LQ) return ILQR_ERR_UNSUPPORTED;
-  if (!p->A || !p->B || !p->Q || !p->R || !p->Qf) return ILQR_ERR_BAD_ARG;
-  if (!ilqr::lq_supported(h->nx, h->nu)) return ILQR_ERR_UNSUPPORTED;
-  return ILQR_OK;
+  if (p->kind == ILQR_PROBLEM_LQ) {
+    if (!p->A || !p->B || !p->Q || !p->R || !p->Qf) return ILQR_ERR_BAD_ARG;
+    if (!ilqr::lq_supported(h->nx, h->nu)) return ILQR_ERR_UNSUPPORTED;
+    return ILQR_OK;
+  }
+  if (p->kind == ILQR_PROBLEM_TWO_LINK) {
+    // the arm is fully defined by the reference script: no per-instance data
+    if (p->A || p->B || p->Q || p->R || p->Qf) return ILQR_ERR_BAD_ARG;
+    if (!ilqr::tl_supported(h->nx, h->nu) || !h->J) return ILQR_ERR_UNSUPPORTED;
+    return ILQR_OK;
+  }
+  return ILQR_ERR_UNSUPPORTED;
 }
+
+bool two_link(const ilqr_problem* p) { return p->kind == ILQR_PROBLEM_TWO_LINK; }
 
 ilqr::LSParams ls_params(const ilqr_options* o) {
   ilqr_options def;
@@ -70,12 +82,20 @@ ilqr::LSParams ls_params(const ilqr_options* o) {
   return ilqr::LSParams{o->mu, o->alpha0, o->shrink, o->tol, o->max_trials};
 }
 
+ilqr_status join(ilqr_handle* h, const ilqr_problem* p);
+
 // Enqueue one fit iteration for the whole batch: backward(c) on the handle's
 // stream, forward(c) on the side stream after it. With `chain`, backward(c) first
 // waits for the previous iteration's forward(c) (same trajectories); otherwise the
 // call ends by making the handle's stream wait for every forward (join).
-ilqr_status enqueue_iteration(ilqr_handle* h, const ilqr::LQParams& P, const ilqr::IterArgs& a,
+ilqr_status enqueue_iteration(ilqr_handle* h, const ilqr_problem* p, const ilqr::IterArgs& a,
                               const ilqr::LSParams& ls, bool chain) {
+  if (two_link(p)) {  // one stream: linearise, backward, forward
+    HIP_TRY(ilqr::launch_tl_iteration(ilqr::two_link_params(), h->batch, h->T, a, h->J, ls,
+                                      h->stream));
+    return ILQR_OK;
+  }
+  const ilqr::LQParams P = lq_params(p);
   for (int c = 0; c < h->nchunks; ++c) {
     const int b0 = h->bound[c], b1 = h->bound[c + 1];
     if (chain) HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_fw[c], 0));
@@ -85,13 +105,12 @@ ilqr_status enqueue_iteration(ilqr_handle* h, const ilqr::LQParams& P, const ilq
     HIP_TRY(ilqr::launch_lq_iter_forward(h->nx, h->nu, P, b0, b1, h->T, a, ls, h->side));
     HIP_TRY(hipEventRecord(h->ev_fw[c], h->side));
   }
-  if (!chain) {
-    for (int c = 0; c < h->nchunks; ++c) HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_fw[c], 0));
-  }
+  if (!chain) return join(h, p);
   return ILQR_OK;
 }
 
-ilqr_status join(ilqr_handle* h) {
+ilqr_status join(ilqr_handle* h, const ilqr_problem* p) {
+  if (two_link(p)) return ILQR_OK;
   for (int c = 0; c < h->nchunks; ++c) HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_fw[c], 0));
   return ILQR_OK;
 }
@@ -150,7 +169,9 @@ void ilqr_default_options(ilqr_options* o) {
 }
 
 int ilqr_supported(int32_t kind, int nx, int nu) {
-  return kind == ILQR_PROBLEM_LQ && ilqr::lq_supported(nx, nu) ? 1 : 0;
+  if (kind == ILQR_PROBLEM_LQ) return ilqr::lq_supported(nx, nu) ? 1 : 0;
+  if (kind == ILQR_PROBLEM_TWO_LINK) return ilqr::tl_supported(nx, nu) ? 1 : 0;
+  return 0;
 }
 
 ilqr_status ilqr_create(ilqr_handle** out, int device, int nx, int nu, int T, int batch) {
@@ -178,6 +199,8 @@ ilqr_status ilqr_create(ilqr_handle** out, int device, int nx, int nu, int T, in
   if (e == hipSuccess) e = hipMalloc(&h->status, sizeof(int32_t) * B);
   if (e == hipSuccess) e = hipMalloc(&h->res_parity, sizeof(int32_t) * B);
   if (e == hipSuccess) e = hipMalloc(&h->iters, sizeof(int32_t) * B);
+  if (e == hipSuccess && ilqr::tl_supported(nx, nu))
+    e = hipMalloc(&h->J, sizeof(double) * ilqr::tl_workspace_doubles(batch, T));
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking);
   for (int c = 0; c < 2 && e == hipSuccess; ++c) {
     e = hipEventCreateWithFlags(&h->ev_bw[c], hipEventDisableTiming);
@@ -219,6 +242,7 @@ ilqr_status ilqr_destroy(ilqr_handle* h) {
   (void)hipFree(h->status);
   (void)hipFree(h->res_parity);
   (void)hipFree(h->iters);
+  (void)hipFree(h->J);
   for (int c = 0; c < 2; ++c) {
     if (h->ev_bw[c]) (void)hipEventDestroy(h->ev_bw[c]);
     if (h->ev_fw[c]) (void)hipEventDestroy(h->ev_fw[c]);
@@ -248,8 +272,12 @@ ilqr_status ilqr_backward(ilqr_handle* h, const ilqr_problem* p, const ilqr_opti
   if ((st = check_options(o)) != ILQR_OK) return st;
   if (!x || !u || !d || !K) return ILQR_ERR_BAD_ARG;
   HIP_TRY(hipSetDevice(h->device));
-  HIP_TRY(ilqr::launch_lq_backward(h->nx, h->nu, lq_params(p), h->batch, h->T, x, u, d, K, status,
-                                   ls_params(o).mu, h->stream));
+  if (two_link(p))
+    HIP_TRY(ilqr::launch_tl_backward(ilqr::two_link_params(), h->batch, h->T, x, u, h->J, d, K,
+                                     status, ls_params(o).mu, h->stream));
+  else
+    HIP_TRY(ilqr::launch_lq_backward(h->nx, h->nu, lq_params(p), h->batch, h->T, x, u, d, K,
+                                     status, ls_params(o).mu, h->stream));
   return status ? fold_status(h, status) : ILQR_OK;
 }
 
@@ -263,9 +291,14 @@ ilqr_status ilqr_forward(ilqr_handle* h, const ilqr_problem* p, const ilqr_optio
   if ((st = check_options(o)) != ILQR_OK) return st;
   if (!x || !u || !d || !K || !prev_cost || !x_new || !u_new || !new_cost) return ILQR_ERR_BAD_ARG;
   HIP_TRY(hipSetDevice(h->device));
-  HIP_TRY(ilqr::launch_lq_forward(h->nx, h->nu, lq_params(p), h->batch, h->T, x, u, x_traj, d, K,
-                                  prev_cost, x_new, u_new, new_cost, trials, status, ls_params(o),
-                                  h->stream));
+  if (two_link(p))
+    HIP_TRY(ilqr::launch_tl_forward(ilqr::two_link_params(), h->batch, h->T, x, u, x_traj, d, K,
+                                    prev_cost, x_new, u_new, new_cost, trials, status,
+                                    ls_params(o), h->stream));
+  else
+    HIP_TRY(ilqr::launch_lq_forward(h->nx, h->nu, lq_params(p), h->batch, h->T, x, u, x_traj, d,
+                                    K, prev_cost, x_new, u_new, new_cost, trials, status,
+                                    ls_params(o), h->stream));
   return status ? fold_status(h, status) : ILQR_OK;
 }
 
@@ -296,7 +329,7 @@ ilqr_status ilqr_iterate(ilqr_handle* h, const ilqr_problem* p, const ilqr_optio
   a.iters = nullptr;
   a.parity = 0;
   a.iter = 0;
-  return enqueue_iteration(h, lq_params(p), a, ls_params(o), /*chain=*/false);
+  return enqueue_iteration(h, p, a, ls_params(o), /*chain=*/false);
 }
 
 ilqr_status ilqr_fit(ilqr_handle* h, const ilqr_problem* p, const ilqr_options* o,
@@ -342,12 +375,12 @@ ilqr_status ilqr_fit(ilqr_handle* h, const ilqr_problem* p, const ilqr_options* 
     a.parity = par;
     a.iter = it;
     // iterations chain per chunk: chunk 0's next backward overlaps chunk 1's forward
-    const ilqr_status st = enqueue_iteration(h, lq_params(p), a, ls, /*chain=*/true);
+    const ilqr_status st = enqueue_iteration(h, p, a, ls, /*chain=*/true);
     if (st != ILQR_OK) return st;
     par ^= 1;  // x̄ⁱ, ūⁱ = x̄ⁱ⁺¹, ūⁱ⁺¹ (:174-175)
   }
   {
-    const ilqr_status st = join(h);
+    const ilqr_status st = join(h, p);
     if (st != ILQR_OK) return st;
   }
   // still-running trajectories (max_iter reached) return the last accepted iterate

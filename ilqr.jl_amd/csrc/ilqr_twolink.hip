@@ -1,0 +1,624 @@
+// MI355X (gfx950) kernels for the 2-link arm problem family (ILQR_PROBLEM_TWO_LINK):
+// the reference's only runnable nonlinear example, test/2_link_example/
+// 2_link_helper_functions.jl:1-108 (configs 1-2 of BASELINE.json), nx = 4, nu = 2.
+//
+// What replaces what:
+//  * dynamicsf (RK4 of continuous_dynamics, :49-79) is a device functor templated on
+//    the scalar type: `double` for the forward rollout, Dual<6> (forward-mode AD with
+//    the 4 state + 2 input directions carried together) for linearize_dynamics
+//    (src/backward_pass.jl:25-40, two ForwardDiff.jacobian calls). The CoriolisMatrix
+//    quirk (:36-47: `for k in length(θ)` visits k = 2 only; the nested
+//    jacobian(InertiaMatrix) is restated by its closed-form derivative ∂M/∂θ₂ — the
+//    value ForwardDiff produces) is reproduced term by term.
+//  * immediate_cost / final_cost (:82-108) are quadratic in (θ, u): their
+//    ForwardDiff gradient/Hessian (src/backward_pass.jl:81-153) are the exact
+//    constants lxx = diag(2,2,0,0), luu = 2I, lux = 0, lx = 2(θ-θ*), lu = 2u.
+//
+// Mapping:
+//  * tl_linearize: one lane per (trajectory, time step) — the only part of the
+//    backward pass that is parallel in time, and the FLOP-heavy one (≈3 kFLOP/step).
+//    Writes J = [A | B] in a [t][24][b] workspace so the sequential pass reads it
+//    coalesced across trajectories.
+//  * tl_backward: one lane per trajectory, the Riccati recursion in registers with
+//    the same exact step_back rewrite as the LQ kernels
+//    ([S s] = [Qxx | lx+Aᵀs] − Kᵀ((H+2μI)[K|d]); S computed as its upper triangle
+//    and mirrored, so it is symmetric by construction).
+//  * tl_forward: one lane per trajectory, RK4 rollout + α-halving line search
+//    (src/forward_pass.jl:55-93), inputs of step t+1 prefetched during step t.
+// The sequential passes are latency-bound (one RK4 or one Riccati step per step per
+// lane); with B = 1024 the chip is far from full — see DESIGN.md for the measured
+// numbers and what would change that.
+#include <hip/hip_runtime.h>
+#include <math.h>
+
+#include "ilqr_internal.h"
+#include "../../include/ilqr.h"
+
+namespace ilqr {
+namespace {
+
+constexpr int TL_NX = 4;
+constexpr int TL_NU = 2;
+constexpr int TL_NJ = TL_NX * (TL_NX + TL_NU);  // 24 entries of [A | B] per step
+
+// ---------------------------------------------------------------------------
+// Forward-mode dual numbers: value + N partials (ForwardDiff.Dual restated).
+// ---------------------------------------------------------------------------
+template <int N>
+struct Dual {
+  double v;
+  double d[N];
+  Dual() = default;
+  __device__ __forceinline__ Dual(double c) : v(c) {  // a constant: zero partials
+#pragma unroll
+    for (int i = 0; i < N; ++i) d[i] = 0.0;
+  }
+};
+
+template <int N>
+__device__ __forceinline__ Dual<N> operator+(const Dual<N>& a, const Dual<N>& b) {
+  Dual<N> r;
+  r.v = a.v + b.v;
+#pragma unroll
+  for (int i = 0; i < N; ++i) r.d[i] = a.d[i] + b.d[i];
+  return r;
+}
+template <int N>
+__device__ __forceinline__ Dual<N> operator-(const Dual<N>& a, const Dual<N>& b) {
+  Dual<N> r;
+  r.v = a.v - b.v;
+#pragma unroll
+  for (int i = 0; i < N; ++i) r.d[i] = a.d[i] - b.d[i];
+  return r;
+}
+template <int N>
+__device__ __forceinline__ Dual<N> operator-(const Dual<N>& a) {
+  Dual<N> r;
+  r.v = -a.v;
+#pragma unroll
+  for (int i = 0; i < N; ++i) r.d[i] = -a.d[i];
+  return r;
+}
+template <int N>
+__device__ __forceinline__ Dual<N> operator*(const Dual<N>& a, const Dual<N>& b) {
+  Dual<N> r;  // (ab)' = a'b + ab'
+  r.v = a.v * b.v;
+#pragma unroll
+  for (int i = 0; i < N; ++i) r.d[i] = a.d[i] * b.v + a.v * b.d[i];
+  return r;
+}
+template <int N>
+__device__ __forceinline__ Dual<N> operator*(double a, const Dual<N>& b) {
+  Dual<N> r;
+  r.v = a * b.v;
+#pragma unroll
+  for (int i = 0; i < N; ++i) r.d[i] = a * b.d[i];
+  return r;
+}
+template <int N>
+__device__ __forceinline__ Dual<N> operator/(const Dual<N>& a, const Dual<N>& b) {
+  Dual<N> r;  // (a/b)' = (a'b − ab') / b²
+  r.v = a.v / b.v;
+  const double b2 = b.v * b.v;
+#pragma unroll
+  for (int i = 0; i < N; ++i) r.d[i] = (a.d[i] * b.v - a.v * b.d[i]) / b2;
+  return r;
+}
+template <int N>
+__device__ __forceinline__ Dual<N> operator/(double a, const Dual<N>& b) {
+  Dual<N> r;  // (a/b)' = −a b' / b²
+  r.v = a / b.v;
+  const double b2 = b.v * b.v;
+#pragma unroll
+  for (int i = 0; i < N; ++i) r.d[i] = -(a * b.d[i]) / b2;
+  return r;
+}
+template <int N>
+__device__ __forceinline__ Dual<N> operator+(double a, const Dual<N>& b) {
+  Dual<N> r = b;
+  r.v = a + b.v;
+  return r;
+}
+template <int N>
+__device__ __forceinline__ void sin_cos(const Dual<N>& a, Dual<N>& s, Dual<N>& c) {
+  double sv, cv;
+  sincos(a.v, &sv, &cv);
+  s.v = sv;
+  c.v = cv;
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    s.d[i] = cv * a.d[i];
+    c.d[i] = -sv * a.d[i];
+  }
+}
+__device__ __forceinline__ void sin_cos(double a, double& s, double& c) { sincos(a, &s, &c); }
+
+template <int N>
+__device__ __forceinline__ Dual<N> seed(double v, int dir) {
+  Dual<N> r;
+  r.v = v;
+#pragma unroll
+  for (int i = 0; i < N; ++i) r.d[i] = i == dir ? 1.0 : 0.0;
+  return r;
+}
+
+// ---------------------------------------------------------------------------
+// dynamicsf of test/2_link_example/2_link_helper_functions.jl:49-79, generic in S.
+// ---------------------------------------------------------------------------
+template <class S>
+__device__ __forceinline__ void continuous_dynamics(const TwoLinkParams& P, const S (&x)[4],
+                                                    const S (&u)[2], S (&xd)[4]) {
+  // InertiaMatrix (:29-33): M = [α+2βc₂  δ+βc₂; δ+βc₂  δ]
+  S s2, c2;
+  sin_cos(x[1], s2, c2);
+  const S m00 = P.alpha + (2.0 * P.beta) * c2;
+  const S m01 = P.delta + P.beta * c2;  // = m10
+  // ∂M/∂θ₂ (the nested jacobian at :37): d/dθ₂ cos θ₂ = −sin θ₂; ∂M/∂θ₁ = 0, ∂M₂₂ = 0
+  const S ns2 = -s2;
+  const S dm00 = (2.0 * P.beta) * ns2;
+  const S dm01 = P.beta * ns2;
+  // CoriolisMatrix (:42-44) with k = 2 only: C[i,j] = ½(∇M[2,i,j] + ∇M[j,i,2] − ∇M[i,2,j])·θ̇₂
+  // → C₁₁ = ½∂M₁₁θ̇₂, C₁₂ = ½((∂M₂₁ + ∂M₂₁) − ∂M₁₂)θ̇₂ = ½∂M₁₂θ̇₂, C₂₁ = ½∂M₁₂θ̇₂, C₂₂ = 0
+  const S c00 = (0.5 * dm00) * x[3];
+  const S c01 = (0.5 * dm01) * x[3];
+  // inv(M) (:63) and M\C (:61) for the 2×2 M (δ = M₂₂ is a constant)
+  const S det = P.delta * m00 - m01 * m01;
+  const S i00 = P.delta / det;
+  const S i01 = -(m01 / det);
+  const S i11 = m00 / det;
+  // MC = M⁻¹C, C = [c00 c01; c01 0]
+  const S mc00 = i00 * c00 + i01 * c01;
+  const S mc01 = i00 * c01;
+  const S mc10 = i01 * c00 + i11 * c01;
+  const S mc11 = i01 * c01;
+  // state_dot = [θ̇; −(M\C)θ̇ + M⁻¹u] (:56-66)
+  xd[0] = x[2];
+  xd[1] = x[3];
+  xd[2] = -(mc00 * x[2] + mc01 * x[3]) + (i00 * u[0] + i01 * u[1]);
+  xd[3] = -(mc10 * x[2] + mc11 * x[3]) + (i01 * u[0] + i11 * u[1]);
+}
+
+// RK4 (:71-78): k_i = Δt·f(·); x' = x + (1/6)(k1 + 2k2 + 2k3 + k4)
+template <class S>
+__device__ __forceinline__ void rk4(const TwoLinkParams& P, const S (&x)[4], const S (&u)[2],
+                                    S (&out)[4]) {
+  S k1[4], k2[4], k3[4], k4[4], y[4];
+  continuous_dynamics(P, x, u, k1);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    k1[i] = P.dt * k1[i];
+    y[i] = x[i] + 0.5 * k1[i];
+  }
+  continuous_dynamics(P, y, u, k2);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    k2[i] = P.dt * k2[i];
+    y[i] = x[i] + 0.5 * k2[i];
+  }
+  continuous_dynamics(P, y, u, k3);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    k3[i] = P.dt * k3[i];
+    y[i] = x[i] + k3[i];
+  }
+  continuous_dynamics(P, y, u, k4);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    k4[i] = P.dt * k4[i];
+    out[i] = x[i] + (1.0 / 6.0) * (((k1[i] + 2.0 * k2[i]) + 2.0 * k3[i]) + k4[i]);
+  }
+}
+
+
+// ---------------------------------------------------------------------------
+// Linearisation: J_t = [A_t | B_t] = ∂f/∂(x,u) at (x_t, u_t), one lane per (b, t).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void tl_linearize_kernel(TwoLinkParams P, int B, int T,
+                                                           const double* __restrict__ x,
+                                                           const double* __restrict__ u,
+                                                           const int32_t* __restrict__ status,
+                                                           double* __restrict__ J) {
+  const int b = blockIdx.x * 256 + threadIdx.x;
+  const int t = blockIdx.y;
+  if (b >= B || (status && status[b] != ILQR_TRAJ_OK)) return;
+  const double* xb = x + ((size_t)b * (T + 1) + t) * TL_NX;
+  const double* ub = u + ((size_t)b * T + t) * TL_NU;
+  Dual<6> xs[4], us[2], out[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) xs[i] = seed<6>(xb[i], i);
+#pragma unroll
+  for (int i = 0; i < 2; ++i) us[i] = seed<6>(ub[i], 4 + i);
+  rk4(P, xs, us, out);
+  double* Jt = J + (size_t)t * TL_NJ * B + b;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int k = 0; k < 6; ++k) Jt[(size_t)(i * 6 + k) * B] = out[i].d[k];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Riccati recursion (src/backward_pass.jl:324-357), one lane per trajectory.
+// Returns true if δu or K holds a NaN (the reference's @assert at :353-354).
+// ---------------------------------------------------------------------------
+__device__ bool tl_backward_lane(const TwoLinkParams& P, int b, int B, int T,
+                                 const double* __restrict__ x, const double* __restrict__ u,
+                                 const double* __restrict__ J, double* __restrict__ dg,
+                                 double* __restrict__ Kg, double mu) {
+  const double* xb = x + (size_t)b * (T + 1) * TL_NX;
+  const double* ub = u + (size_t)b * T * TL_NU;
+  // final_cost_quadratization (:134-153): ∇ℓ_f = [2(θ−θ*), 0, 0], ∇²ℓ_f = diag(2,2,0,0)
+  double S[4][4] = {};
+  double s[4];
+  S[0][0] = 2.0;
+  S[1][1] = 2.0;
+  s[0] = -2.0 * (P.tgt0 - xb[(size_t)T * TL_NX + 0]);
+  s[1] = -2.0 * (P.tgt1 - xb[(size_t)T * TL_NX + 1]);
+  s[2] = 0.0;
+  s[3] = 0.0;
+  bool bad = false;
+
+  double F[TL_NJ];  // [A | B] of the step being processed, row-major 4×6
+  auto loadJ = [&](int t, double (&f)[TL_NJ]) {
+    const double* Jt = J + (size_t)t * TL_NJ * B + b;
+#pragma unroll
+    for (int k = 0; k < TL_NJ; ++k) f[k] = Jt[(size_t)k * B];
+  };
+  loadJ(T - 1, F);
+  for (int t = T - 1; t >= 0; --t) {
+    double Fn[TL_NJ];
+    loadJ(t > 0 ? t - 1 : 0, Fn);  // prefetch the next (earlier) step
+    const double th0 = xb[(size_t)t * TL_NX + 0], th1 = xb[(size_t)t * TL_NX + 1];
+    const double u0 = ub[(size_t)t * TL_NU + 0], u1 = ub[(size_t)t * TL_NU + 1];
+    // immediate_cost_quadratization (:81-109): lx = [2(θ−θ*), 0, 0], lu = 2u,
+    // lxx = diag(2,2,0,0), luu = 2I, lux = 0
+    // Y = S·F (4×6) and sF = sᵀF (1×6)
+    double Y[4][6], sF[6];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int k = 0; k < 6; ++k) {
+        double acc = 0.0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc = fma(S[i][j], F[j * 6 + k], acc);
+        Y[i][k] = acc;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+      double acc = 0.0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc = fma(s[j], F[j * 6 + k], acc);
+      sF[k] = acc;
+    }
+    // Z = FᵀY: Qxx = lxx + AᵀSA (upper), G = BᵀSA (2×4), H = luu + BᵀSB (2×2)
+    auto Z = [&](int a, int c) {
+      double acc = 0.0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc = fma(F[j * 6 + a], Y[j][c], acc);
+      return acc;
+    };
+    double G[2][4], H[2][2], g[2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) G[a][c] = Z(4 + a, c);
+    }
+    H[0][0] = 2.0 + Z(4, 4);
+    H[0][1] = Z(4, 5);
+    H[1][1] = 2.0 + Z(5, 5);
+    H[1][0] = H[0][1];
+    g[0] = 2.0 * u0 + sF[4];  // optimal_controller_param (:181): g = lu + Bᵀs
+    g[1] = 2.0 * u1 + sF[5];
+    // feedback_parameters (:207-218): (H + μI)⁻¹ by LDLᵀ; δu = −H⁻¹g, K = −H⁻¹G
+    const double h00 = H[0][0] + mu, h01 = H[0][1], h11 = H[1][1] + mu;
+    const double D0 = h00;
+    const double l10 = h01 / D0;
+    const double D1 = h11 - l10 * h01;
+    auto solve = [&](double r0, double r1, double& z0, double& z1) {  // z = −(H+μI)⁻¹ r
+      const double w1 = (r1 - l10 * r0) / D1;
+      z1 = -w1;
+      z0 = -(r0 / D0 - l10 * w1);
+    };
+    double K[2][4], d[2];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) solve(G[0][c], G[1][c], K[0][c], K[1][c]);
+    solve(g[0], g[1], d[0], d[1]);
+    double* Kt = Kg + ((size_t)b * T + t) * TL_NU * TL_NX;
+    double* dt = dg + ((size_t)b * T + t) * TL_NU;
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      dt[a] = d[a];
+      bad |= d[a] != d[a];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        Kt[a * 4 + c] = K[a][c];
+        bad |= K[a][c] != K[a][c];
+      }
+    }
+    // step_back (:262-273), exact rewrite: with W = (H+2μI)[K|d] = −[G|g] + μ[K|d],
+    //   S = lxx + AᵀSA − KᵀW_K,   s = lx + Aᵀs − KᵀW_d
+    double WK[2][4], Wd[2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) WK[a][c] = fma(mu, K[a][c], -G[a][c]);
+      Wd[a] = fma(mu, d[a], -g[a]);
+    }
+    double Sn[4][4], sn[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int j = i; j < 4; ++j) {
+        double acc = Z(i, j);
+        if (i == j && i < 2) acc += 2.0;
+        acc = fma(-K[0][i], WK[0][j], acc);
+        acc = fma(-K[1][i], WK[1][j], acc);
+        Sn[i][j] = acc;
+        Sn[j][i] = acc;
+      }
+      double acc = sF[i];
+      if (i == 0) acc += -2.0 * (P.tgt0 - th0);
+      if (i == 1) acc += -2.0 * (P.tgt1 - th1);
+      acc = fma(-K[0][i], Wd[0], acc);
+      acc = fma(-K[1][i], Wd[1], acc);
+      sn[i] = acc;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      s[i] = sn[i];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) S[i][j] = Sn[i][j];
+    }
+#pragma unroll
+    for (int k = 0; k < TL_NJ; ++k) F[k] = Fn[k];
+  }
+  return bad;
+}
+
+// ---------------------------------------------------------------------------
+// Forward rollout + line search (src/forward_pass.jl:55-93), one lane per trajectory.
+// ---------------------------------------------------------------------------
+struct TLFwdOut {
+  double cost;
+  int trials;
+  int accepted;
+};
+
+struct TLStepIn {
+  double x[4], xt[4], u[2], d[2], K[8];
+};
+
+__device__ TLFwdOut tl_forward_lane(const TwoLinkParams& P, int b, int T,
+                                    const double* __restrict__ x, const double* __restrict__ u,
+                                    const double* __restrict__ xtraj,
+                                    const double* __restrict__ dg, const double* __restrict__ Kg,
+                                    double prev_cost, double* __restrict__ xnew,
+                                    double* __restrict__ unew, double* du2_out,
+                                    const LSParams& ls) {
+  const double* xb0 = x + (size_t)b * (T + 1) * TL_NX;
+  const double* ub0 = u + (size_t)b * T * TL_NU;
+  const double* xt0 = (xtraj ? xtraj : x) + (size_t)b * (T + 1) * TL_NX;
+  const double xtw = xtraj ? 1.0 : 0.0;  // x_traj = NULL means zeros (forward_pass.jl:151)
+  const double* d0 = dg + (size_t)b * T * TL_NU;
+  const double* K0 = Kg + (size_t)b * T * TL_NU * TL_NX;
+  double* xo = xnew + (size_t)b * (T + 1) * TL_NX;
+  double* uo = unew + (size_t)b * T * TL_NU;
+
+  auto load = [&](int t, TLStepIn& in) {
+    const int tt = t < T ? t : T - 1;
+    const double4 xv = *reinterpret_cast<const double4*>(xb0 + (size_t)tt * TL_NX);
+    const double4 tv = *reinterpret_cast<const double4*>(xt0 + (size_t)tt * TL_NX);
+    in.x[0] = xv.x; in.x[1] = xv.y; in.x[2] = xv.z; in.x[3] = xv.w;
+    in.xt[0] = tv.x; in.xt[1] = tv.y; in.xt[2] = tv.z; in.xt[3] = tv.w;
+    const double2 uv = *reinterpret_cast<const double2*>(ub0 + (size_t)tt * TL_NU);
+    const double2 dv = *reinterpret_cast<const double2*>(d0 + (size_t)tt * TL_NU);
+    in.u[0] = uv.x; in.u[1] = uv.y;
+    in.d[0] = dv.x; in.d[1] = dv.y;
+    const double4* kv = reinterpret_cast<const double4*>(K0 + (size_t)tt * TL_NU * TL_NX);
+    const double4 k0 = kv[0], k1 = kv[1];
+    in.K[0] = k0.x; in.K[1] = k0.y; in.K[2] = k0.z; in.K[3] = k0.w;
+    in.K[4] = k1.x; in.K[5] = k1.y; in.K[6] = k1.z; in.K[7] = k1.w;
+  };
+
+  double alpha = ls.alpha0;
+  TLFwdOut out{0.0, 0, 0};
+  double du2 = 0.0;
+  for (int trial = 1; trial <= ls.max_trials; ++trial) {
+    double xb[4];
+    {
+      const double4 xv = *reinterpret_cast<const double4*>(xb0);  // x̄₁ = x₁ (:65)
+      xb[0] = xv.x; xb[1] = xv.y; xb[2] = xv.z; xb[3] = xv.w;
+    }
+    double cost = 0.0;
+    du2 = 0.0;
+    TLStepIn in;
+    load(0, in);
+    for (int t = 0; t < T; ++t) {
+      TLStepIn nx_in;
+      load(t + 1, nx_in);
+      // δx = x̄ₖ − xₖ (:72); ūₖ = uₖ + α δuₖ + Kₖ δx (:73)
+      double dx[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) dx[i] = xb[i] - in.x[i];
+      double ubar[2];
+#pragma unroll
+      for (int a = 0; a < 2; ++a) {
+        double kdx = 0.0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) kdx = fma(in.K[a * 4 + i], dx[i], kdx);
+        ubar[a] = fma(alpha, in.d[a], in.u[a]) + kdx;
+      }
+      // ℓ(x̄ₖ − x_trajₖ, ūₖ) (:187-190; 2_link_helper_functions.jl:82-97)
+      const double e0 = P.tgt0 - fma(-xtw, in.xt[0], xb[0]);
+      const double e1 = P.tgt1 - fma(-xtw, in.xt[1], xb[1]);
+      cost += (e0 * e0 + e1 * e1) + (ubar[0] * ubar[0] + ubar[1] * ubar[1]);
+      *reinterpret_cast<double4*>(xo + (size_t)t * TL_NX) = make_double4(xb[0], xb[1], xb[2], xb[3]);
+      *reinterpret_cast<double2*>(uo + (size_t)t * TL_NU) = make_double2(ubar[0], ubar[1]);
+      const double du0 = ubar[0] - in.u[0], du1 = ubar[1] - in.u[1];
+      du2 = fma(du0, du0, fma(du1, du1, du2));
+      // x̄ₖ₊₁ = f(x̄ₖ, ūₖ) (:74)
+      double xn[4];
+      rk4(P, xb, ubar, xn);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) xb[i] = xn[i];
+      in = nx_in;
+    }
+    *reinterpret_cast<double4*>(xo + (size_t)T * TL_NX) = make_double4(xb[0], xb[1], xb[2], xb[3]);
+    // final_cost(x̄_N) on the raw state (:192; 2_link_helper_functions.jl:100-108)
+    const double f0 = P.tgt0 - xb[0], f1 = P.tgt1 - xb[1];
+    cost += f0 * f0 + f1 * f1;
+    out.trials = trial;
+    out.cost = cost;
+    if (prev_cost - cost > 0.0) {  // (:77-80); NaN compares false → keep searching
+      out.accepted = 1;
+      break;
+    }
+    alpha *= ls.shrink;  // (:82)
+  }
+  if (du2_out) *du2_out = du2;
+  return out;
+}
+
+// ---------------------------------------------------------------------------
+// Kernels
+// ---------------------------------------------------------------------------
+constexpr int TL_WG = 64;  // one wave per workgroup: B = 1024 spreads over 16 CUs
+
+__global__ __launch_bounds__(TL_WG) void tl_backward_kernel(TwoLinkParams P, int B, int T,
+                                                            const double* __restrict__ x,
+                                                            const double* __restrict__ u,
+                                                            const double* __restrict__ J,
+                                                            double* __restrict__ d,
+                                                            double* __restrict__ K,
+                                                            int32_t* __restrict__ status,
+                                                            double mu) {
+  const int b = blockIdx.x * TL_WG + threadIdx.x;
+  if (b >= B) return;
+  const bool nan = tl_backward_lane(P, b, B, T, x, u, J, d, K, mu);
+  if (status) status[b] = nan ? ILQR_TRAJ_NAN : ILQR_TRAJ_OK;
+}
+
+__global__ __launch_bounds__(TL_WG) void tl_forward_kernel(
+    TwoLinkParams P, int B, int T, const double* __restrict__ x, const double* __restrict__ u,
+    const double* __restrict__ xtraj, const double* __restrict__ d, const double* __restrict__ K,
+    const double* __restrict__ prev_cost, double* __restrict__ xnew, double* __restrict__ unew,
+    double* __restrict__ new_cost, int32_t* __restrict__ trials, int32_t* __restrict__ status,
+    LSParams ls) {
+  const int b = blockIdx.x * TL_WG + threadIdx.x;
+  if (b >= B) return;
+  const double pc = prev_cost ? prev_cost[b] : INFINITY;
+  const TLFwdOut r = tl_forward_lane(P, b, T, x, u, xtraj, d, K, pc, xnew, unew, nullptr, ls);
+  if (!r.accepted) {  // exhausted (the reference would loop forever): return the inputs
+    for (int i = 0; i < (T + 1) * TL_NX; ++i) xnew[(size_t)b * (T + 1) * TL_NX + i] = x[(size_t)b * (T + 1) * TL_NX + i];
+    for (int i = 0; i < T * TL_NU; ++i) unew[(size_t)b * T * TL_NU + i] = u[(size_t)b * T * TL_NU + i];
+  }
+  new_cost[b] = r.cost;
+  if (trials) trials[b] = r.trials;
+  if (status) status[b] = r.accepted ? ILQR_TRAJ_OK
+                                     : (r.cost != r.cost ? ILQR_TRAJ_NAN : ILQR_TRAJ_LS_EXHAUSTED);
+}
+
+// One fit iteration (forward_pass.jl:161-176): backward part (after tl_linearize).
+__global__ __launch_bounds__(TL_WG) void tl_iter_backward_kernel(TwoLinkParams P, int B, int T,
+                                                                 IterArgs a, const double* J,
+                                                                 double mu) {
+  const int b = blockIdx.x * TL_WG + threadIdx.x;
+  if (b >= B || a.status[b] != ILQR_TRAJ_OK) return;
+  if (tl_backward_lane(P, b, B, T, a.x, a.u, J, a.d, a.K, mu)) {
+    a.status[b] = ILQR_TRAJ_NAN;  // reference: AssertionError at backward_pass.jl:353
+    if (a.res_parity) a.res_parity[b] = a.parity;
+  }
+}
+
+// Forward part + the convergence test (:163-175).
+__global__ __launch_bounds__(TL_WG) void tl_iter_forward_kernel(TwoLinkParams P, int B, int T,
+                                                                IterArgs a, LSParams ls) {
+  const int b = blockIdx.x * TL_WG + threadIdx.x;
+  if (b >= B || a.status[b] != ILQR_TRAJ_OK) return;
+  double du2 = 0.0;
+  const double pc = a.prev_cost ? a.prev_cost[b] : INFINITY;
+  const TLFwdOut r = tl_forward_lane(P, b, T, a.x, a.u, a.xtraj, a.d, a.K, pc, a.xnew, a.unew,
+                                     &du2, ls);
+  if (a.trials) a.trials[b] = r.trials;
+  if (a.du2) a.du2[b] = du2;
+  if (a.iters) a.iters[b] = a.iter;
+  if (!r.accepted) {
+    a.status[b] = (r.cost != r.cost) ? ILQR_TRAJ_NAN : ILQR_TRAJ_LS_EXHAUSTED;
+    if (a.res_parity) a.res_parity[b] = a.parity;
+  } else {
+    a.new_cost[b] = r.cost;  // prev_cost = new_cost (:168)
+    if (du2 <= ls.tol) {      // (:171) break BEFORE the update → result is the input iterate
+      a.status[b] = ILQR_TRAJ_CONVERGED;
+      if (a.res_parity) a.res_parity[b] = a.parity;
+    }
+  }
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// Host side
+// ---------------------------------------------------------------------------
+TwoLinkParams two_link_params() {
+#pragma clang fp contract(off)
+  // test/2_link_example/2_link_helper_functions.jl:4-26, same expression order
+  const double l1 = sqrt(2.) / 2., l2 = sqrt(2.) / 2.;
+  const double r1 = 0.5 * l1, r2 = 0.5 * l2;
+  const double m1 = 1.0, m2 = 1.0;
+  const double Iz1 = 1.0 / 12.0 * m1 * (l1 * l1), Iz2 = 1.0 / 12.0 * m2 * (l2 * l2);
+  TwoLinkParams P;
+  P.alpha = Iz1 + Iz2 + m1 * (r1 * r1) + m2 * (l1 * l1 + r2 * r2);
+  P.beta = m2 * l1 * r2;
+  P.delta = Iz2 + m2 * (r2 * r2);
+  P.dt = 0.01;
+  const double tx = 0.6, ty = -0.5;  // target_tool_loc (:16)
+  const double q2 = acos((tx * tx + ty * ty - l1 * l1 - l2 * l2) / (2 * l1 * l2));
+  const double q1 = atan2(ty, tx) - atan2(l2 * sin(q2), l1 + l2 * cos(q2));
+  P.tgt0 = q1;
+  P.tgt1 = q2;
+  return P;
+}
+
+bool tl_supported(int nx, int nu) { return nx == TL_NX && nu == TL_NU; }
+
+size_t tl_workspace_doubles(int B, int T) { return (size_t)T * TL_NJ * B; }
+
+static hipError_t launch_linearize(const TwoLinkParams& P, int B, int T, const double* x,
+                                   const double* u, const int32_t* status, double* J,
+                                   hipStream_t s) {
+  tl_linearize_kernel<<<dim3((B + 255) / 256, T), 256, 0, s>>>(P, B, T, x, u, status, J);
+  return hipGetLastError();
+}
+
+hipError_t launch_tl_backward(const TwoLinkParams& P, int B, int T, const double* x,
+                              const double* u, double* J, double* d, double* K, int32_t* status,
+                              double mu, hipStream_t s) {
+  hipError_t e = launch_linearize(P, B, T, x, u, nullptr, J, s);
+  if (e != hipSuccess) return e;
+  tl_backward_kernel<<<(B + TL_WG - 1) / TL_WG, TL_WG, 0, s>>>(P, B, T, x, u, J, d, K, status, mu);
+  return hipGetLastError();
+}
+
+hipError_t launch_tl_forward(const TwoLinkParams& P, int B, int T, const double* x,
+                             const double* u, const double* xtraj, const double* d,
+                             const double* K, const double* prev_cost, double* xnew,
+                             double* unew, double* new_cost, int32_t* trials, int32_t* status,
+                             const LSParams& ls, hipStream_t s) {
+  tl_forward_kernel<<<(B + TL_WG - 1) / TL_WG, TL_WG, 0, s>>>(P, B, T, x, u, xtraj, d, K,
+                                                              prev_cost, xnew, unew, new_cost,
+                                                              trials, status, ls);
+  return hipGetLastError();
+}
+
+hipError_t launch_tl_iteration(const TwoLinkParams& P, int B, int T, const IterArgs& a, double* J,
+                               const LSParams& ls, hipStream_t s) {
+  hipError_t e = launch_linearize(P, B, T, a.x, a.u, a.status, J, s);
+  if (e != hipSuccess) return e;
+  tl_iter_backward_kernel<<<(B + TL_WG - 1) / TL_WG, TL_WG, 0, s>>>(P, B, T, a, J, ls.mu);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  tl_iter_forward_kernel<<<(B + TL_WG - 1) / TL_WG, TL_WG, 0, s>>>(P, B, T, a, ls);
+  return hipGetLastError();
+}
+
+}  // namespace ilqr

@@ -29,6 +29,7 @@ TRAJ_LS_EXHAUSTED = 3
 TRAJ_NAN = 4
 
 PROBLEM_LQ = 1
+PROBLEM_TWO_LINK = 2
 
 
 class Problem(C.Structure):

@@ -28,7 +28,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from .problems import lq_from_closures
+from .problems import is_two_link, lq_from_closures
 from .solver import Solver
 
 
@@ -67,6 +67,10 @@ def _solver(xb, ub, dynamicsf, immediate_cost, final_cost):
     _, M, nu = ub.shape
     assert N == M + 1, "size(x)[1] == size(u)[1] + 1"   # backward_pass.jl:329
     assert ub.shape[0] == nb, "batch sizes differ"
+    if is_two_link(dynamicsf, immediate_cost, final_cost):
+        if (nx, nu) != (4, 2):
+            raise AssertionError(f"the 2-link arm is (4, 2) but x/u are ({nx}, {nu})")
+        return Solver(nx, nu, M, nb, device=_device(), kind=_lib.PROBLEM_TWO_LINK)
     lq = lq_from_closures(dynamicsf, immediate_cost, final_cost, nb)
     if (lq.nx, lq.nu) != (nx, nu):
         raise AssertionError(f"problem is ({lq.nx}, {lq.nu}) but x/u are ({nx}, {nu})")

@@ -11,11 +11,16 @@ to the GPU instead of calling them.
 Family ILQR_PROBLEM_LQ: f(x,u) = A x + B u, ℓ(x,u) = xᵀQx + uᵀRu, ℓ_f(x) = xᵀQf x,
 with per-trajectory (batched) A, B, Q, R, Qf.
 
+Family ILQR_PROBLEM_TWO_LINK: the reference's 2-link arm
+(test/2_link_example/2_link_helper_functions.jl), fixed constants, nx=4, nu=2.
+
 `quadrotor_batch` builds the headline benchmark instance: a
 hover-linearised quadrotor, per-instance randomised with
 numpy.random.default_rng(seed=b).
 """
 from __future__ import annotations
+
+import math
 
 import numpy as np
 
@@ -201,3 +206,91 @@ def random_lq_batch(batch: int, nx: int, nu: int, T: int, seed: int = 0, dense: 
     for t in range(T):
         x[:, t + 1] = np.einsum("bij,bj->bi", A, x[:, t]) + np.einsum("bij,bj->bi", B, u[:, t])
     return LQBatch(A, B, Q, R, Qf), x, u
+
+
+# -- family ILQR_PROBLEM_TWO_LINK: the reference's 2-link arm ---------------------
+class TwoLinkArm:
+    """Constants of test/2_link_example/2_link_helper_functions.jl:4-26 (same
+    expression order as the script). The device kernels compute the same numbers
+    on the host side of the C ABI; they are repeated here for host-side use."""
+    n_links = 2
+    l1 = l2 = math.sqrt(2.0) / 2.0
+    r1, r2 = 0.5 * l1, 0.5 * l2
+    m1 = m2 = 1.0
+    Iz1 = 1.0 / 12.0 * m1 * l1 ** 2
+    Iz2 = 1.0 / 12.0 * m2 * l2 ** 2
+    alpha = Iz1 + Iz2 + m1 * r1 ** 2 + m2 * (l1 ** 2 + r2 ** 2)
+    beta = m2 * l1 * r2
+    delta = Iz2 + m2 * r2 ** 2
+    dt = 0.01
+    target_tool_loc = (0.6, -0.5)
+    nx, nu = 4, 2
+
+    @classmethod
+    def inverse_kinematics(cls, target=None):
+        """InverseKinematics (:19-26) → θ* (2,)."""
+        x, y = cls.target_tool_loc if target is None else target
+        q2 = math.acos((x ** 2 + y ** 2 - cls.l1 ** 2 - cls.l2 ** 2) / (2 * cls.l1 * cls.l2))
+        q1 = math.atan2(y, x) - math.atan2(cls.l2 * math.sin(q2), cls.l1 + cls.l2 * math.cos(q2))
+        return np.array([q1, q2])
+
+
+class TwoLinkDynamics:
+    """dynamicsf(x, u) of the 2-link arm (:49-79): one RK4 step of
+    [θ̇; −(M\\C)θ̇ + M⁻¹u], with the script's CoriolisMatrix (k = 2 term only).
+    Host evaluation (float64 numpy) for callers that roll the model out on the
+    CPU; the device path never calls it — it runs its own kernel functor."""
+    nx, nu = 4, 2
+
+    @staticmethod
+    def _f(x, u):
+        P = TwoLinkArm
+        s2, c2 = math.sin(x[1]), math.cos(x[1])
+        m00 = P.alpha + 2 * P.beta * c2
+        m01 = P.delta + P.beta * c2
+        dm00, dm01 = 2 * P.beta * -s2, P.beta * -s2
+        C = np.array([[0.5 * dm00 * x[3], 0.5 * dm01 * x[3]], [0.5 * dm01 * x[3], 0.0]])
+        M = np.array([[m00, m01], [m01, P.delta]])
+        acc = -np.linalg.solve(M, C) @ x[2:4] + np.linalg.solve(M, np.asarray(u, float))
+        return np.array([x[2], x[3], acc[0], acc[1]])
+
+    def __call__(self, x, u):
+        x = np.asarray(x, dtype=np.float64)
+        dt = TwoLinkArm.dt
+        k1 = dt * self._f(x, u)
+        k2 = dt * self._f(x + k1 / 2, u)
+        k3 = dt * self._f(x + k2 / 2, u)
+        k4 = dt * self._f(x + k3, u)
+        return x + (1 / 6) * (k1 + 2 * k2 + 2 * k3 + k4)
+
+
+class TwoLinkCost:
+    """immediate_cost(x, u) = |θ* − θ|² + |u|² (:82-97; the velocity penalty is dead code)."""
+
+    def __call__(self, x, u):
+        e = TwoLinkArm.inverse_kinematics() - np.asarray(x[:2], float)
+        return float(np.sum(e ** 2) * 1.0 + np.sum(np.asarray(u, float) ** 2) * 1.0)
+
+
+class TwoLinkFinalCost:
+    """final_cost(x) = |θ* − θ|² (:100-108)."""
+
+    def __call__(self, x):
+        e = TwoLinkArm.inverse_kinematics() - np.asarray(x[:2], float)
+        return float(np.sum(e ** 2) * 1.0)
+
+
+def two_link_closures():
+    """(dynamicsf, immediate_cost, final_cost) of test/2_link_example."""
+    return TwoLinkDynamics(), TwoLinkCost(), TwoLinkFinalCost()
+
+
+def is_two_link(dynamicsf, immediate_cost, final_cost) -> bool:
+    return (isinstance(dynamicsf, TwoLinkDynamics) and isinstance(immediate_cost, TwoLinkCost)
+            and isinstance(final_cost, TwoLinkFinalCost))
+
+
+def two_link_initial_states(batch: int, seed0: int = 0):
+    """Config 2's x₀ batch: x₀[b] = rand(4) from numpy.random.default_rng(seed0 + b)
+    (test_iLQR.jl:8 draws rand(4) unseeded; SURVEY.md §8 fixes the seeds)."""
+    return np.stack([np.random.default_rng(seed0 + b).random(4) for b in range(batch)])

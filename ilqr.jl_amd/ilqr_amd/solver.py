@@ -43,17 +43,25 @@ class FitResult:
 
 
 class Solver:
-    def __init__(self, nx: int, nu: int, T: int, batch: int, device: int = 0):
+    """kind = _lib.PROBLEM_LQ (call set_problem with the per-instance data) or
+    _lib.PROBLEM_TWO_LINK (the reference's 2-link arm; nothing to set)."""
+
+    def __init__(self, nx: int, nu: int, T: int, batch: int, device: int = 0,
+                 kind: int = _lib.PROBLEM_LQ):
         self.lib = _lib.load()
-        if not self.lib.ilqr_supported(_lib.PROBLEM_LQ, nx, nu):
-            raise NotImplementedError(f"(nx, nu) = ({nx}, {nu}) has no compiled kernel")
+        if not self.lib.ilqr_supported(kind, nx, nu):
+            raise NotImplementedError(f"(nx, nu) = ({nx}, {nu}) has no compiled kernel for "
+                                      f"problem kind {kind}")
         self.nx, self.nu, self.T, self.batch, self.device = nx, nu, T, batch, device
+        self.kind = kind
         self.dev = torch.device("cuda", device)
         h = C.c_void_p()
         _lib.check(self.lib.ilqr_create(C.byref(h), device, nx, nu, T, batch), "ilqr_create")
         self.h = h
         self._problem = None
         self._keep = ()
+        if kind == _lib.PROBLEM_TWO_LINK:
+            self._problem = _lib.Problem(_lib.PROBLEM_TWO_LINK, 0, None, None, None, None, None)
 
     # -- setup ---------------------------------------------------------------------
     def close(self):
@@ -74,6 +82,8 @@ class Solver:
     def set_problem(self, lq):
         """lq: LQBatch (host numpy, copied to the device) or a dict of CUDA tensors
         A (B,nx,nx), B (B,nx,nu), Q (B,nx,nx), R (B,nu,nu), Qf (B,nx,nx)."""
+        if self.kind != _lib.PROBLEM_LQ:
+            raise TypeError("set_problem: only the LQ family has per-instance data")
         nb, nx, nu = self.batch, self.nx, self.nu
         if isinstance(lq, LQBatch):
             t = {k: torch.from_numpy(getattr(lq, k)).to(self.dev) for k in ("A", "B", "Q", "R", "Qf")}
@@ -136,6 +146,21 @@ class Solver:
                                    _ptr(cost), _ptr(trials), _ptr(st))
         _lib.check(rc, "ilqr_forward", allow=(_lib.ERR_NAN, _lib.ERR_LS_EXHAUSTED))
         return xn, un, cost, trials, st
+
+    def rollout(self, x0, u):
+        """Open-loop rollout x[t+1] = dynamicsf(x[t], u[t]) from x0 (B, nx) —
+        animate_2_link.jl:11-16's x_init — as forward_pass with δu = K = 0 (its
+        first trial at prev_cost = Inf is exactly that rollout). Synchronises."""
+        B, T, nx, nu = self.batch, self.T, self.nx, self.nu
+        _req(x0, torch.float64, (B, nx), "x0")
+        _req(u, torch.float64, (B, T, nu), "u")
+        x = torch.zeros((B, T + 1, nx), dtype=torch.float64, device=self.dev)
+        x[:, 0] = x0
+        d = torch.zeros((B, T, nu), dtype=torch.float64, device=self.dev)
+        K = torch.zeros((B, T, nu, nx), dtype=torch.float64, device=self.dev)
+        pc = torch.full((B,), float("inf"), dtype=torch.float64, device=self.dev)
+        xn, _, _, _, _ = self.forward(x, u, d, K, pc)
+        return xn
 
     def iterate(self, x, u, x_new, u_new, prev_cost, status, du2=None, trials=None,
                 x_traj=None, options=None, new_cost=None):

@@ -19,7 +19,12 @@
  *   dynamicsf(x,u)      = A x + B u
  *   immediate_cost(x,u) = xᵀ Q x + uᵀ R u
  *   final_cost(x)       = xᵀ Qf x
- * with per-instance (per-trajectory) A, B, Q, R, Qf.
+ * with per-instance (per-trajectory) A, B, Q, R, Qf. ILQR_PROBLEM_TWO_LINK is the
+ * reference's 2-link arm, test/2_link_example/2_link_helper_functions.jl:1-108
+ * (nx = 4, nu = 2): RK4 (Δt = 0.01) of the arm dynamics with its CoriolisMatrix,
+ * ℓ(x,u) = |θ* − θ|² + |u|², ℓ_f(x) = |θ* − θ|², θ* = InverseKinematics([0.6, −0.5]);
+ * it has no per-instance data (A..Qf must be NULL) and is linearised on the
+ * device by forward-mode dual numbers (what ForwardDiff does in the reference).
  *
  * Data layout (all arrays are DEVICE pointers, fp64, C row-major, trajectory
  * slowest; the same memory is a Julia column-major Array with the dimension
@@ -72,12 +77,12 @@ enum {
   ILQR_TRAJ_NAN = 4
 };
 
-typedef enum { ILQR_PROBLEM_LQ = 1 } ilqr_problem_kind;
+typedef enum { ILQR_PROBLEM_LQ = 1, ILQR_PROBLEM_TWO_LINK = 2 } ilqr_problem_kind;
 
 typedef struct {
   int32_t kind;        /* ilqr_problem_kind */
   int32_t reserved;
-  const double* A;     /* (batch, nx, nx) */
+  const double* A;     /* (batch, nx, nx); LQ only, NULL for TWO_LINK */
   const double* B;     /* (batch, nx, nu) */
   const double* Q;     /* (batch, nx, nx) */
   const double* R;     /* (batch, nu, nu) */

@@ -47,6 +47,16 @@ def test_supported_shapes():
     assert lib.ilqr_supported(_lib.PROBLEM_LQ, 12, 4) == 1
     assert lib.ilqr_supported(_lib.PROBLEM_LQ, 5, 3) == 0
     assert lib.ilqr_supported(99, 12, 4) == 0
+    assert lib.ilqr_supported(_lib.PROBLEM_TWO_LINK, 4, 2) == 1
+    assert lib.ilqr_supported(_lib.PROBLEM_TWO_LINK, 12, 4) == 0
+    assert lib.ilqr_supported(_lib.PROBLEM_LQ, 4, 2) == 0
+
+
+def test_header_problem_kinds_match_binding():
+    import re
+    hdr = open(os.path.join(ROOT, "include", "ilqr.h")).read()
+    kinds = dict(re.findall(r"ILQR_PROBLEM_(\w+) = (\d+)", hdr))
+    assert int(kinds["LQ"]) == _lib.PROBLEM_LQ and int(kinds["TWO_LINK"]) == _lib.PROBLEM_TWO_LINK
 
 
 def test_argument_validation_needs_no_gpu():

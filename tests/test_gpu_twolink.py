@@ -1,0 +1,199 @@
+"""GPU parity tests of the 2-link arm family (ILQR_PROBLEM_TWO_LINK) through the C ABI.
+
+Reference: test/2_link_example/2_link_helper_functions.jl (dynamics, costs) driven
+by src/backward_pass.jl / src/forward_pass.jl. Oracle: oracle.ilqr_oracle.TwoLink
+(literal restatement, ForwardDiff restated by oracle.dual), frozen in
+tests/golden/twolink_t50.npz (make_golden.py).
+
+Tolerances (fp64): the device evaluates RK4 with FMA contraction, sincos from the
+device math library, an LDLᵀ 2×2 solve and the exact step_back rewrite, so it
+agrees with the oracle to rounding: rollouts rel 1e-12, gains rel 1e-10, costs rel
+1e-12, fit iterates rel 1e-9 (after up to 7 Newton-like iterations), iteration
+counts exactly.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from ilqr_amd import _lib
+from ilqr_amd.problems import TwoLinkArm, two_link_closures, two_link_initial_states
+from ilqr_amd.solver import Solver
+from oracle import ilqr_oracle as O
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+TOL_ROLL = 1e-12
+TOL_GAIN = 1e-10
+TOL_COST = 1e-12
+TOL_FIT = 1e-9
+
+
+def rel(a, b):
+    a = a.cpu().numpy() if isinstance(a, torch.Tensor) else np.asarray(a)
+    b = b.cpu().numpy() if isinstance(b, torch.Tensor) else np.asarray(b)
+    return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-300))
+
+
+def dev(a, dtype=torch.float64):
+    return torch.as_tensor(np.ascontiguousarray(a)).to("cuda", dtype).contiguous()
+
+
+@pytest.fixture(scope="module")
+def g():
+    z = np.load(os.path.join(GOLD, "twolink_t50.npz"), allow_pickle=False)
+    return {k: z[k] for k in z.files}
+
+
+def tl_solver(T, B):
+    return Solver(4, 2, T, B, kind=_lib.PROBLEM_TWO_LINK)
+
+
+def test_tl_rollout(gpu, g):
+    """dynamicsf (RK4 functor) rollout from x₀ with u = 0 (animate_2_link.jl:11-16)."""
+    nb, T = g["u"].shape[:2]
+    s = tl_solver(T, nb)
+    x = s.rollout(dev(g["x"][:, 0]), dev(g["u"]))
+    assert rel(x, g["x"]) < TOL_ROLL
+
+
+def test_tl_backward(gpu, g):
+    nb, T = g["u"].shape[:2]
+    s = tl_solver(T, nb)
+    d, K, st = s.backward(dev(g["x"]), dev(g["u"]))
+    assert (st.cpu().numpy() == _lib.TRAJ_OK).all()
+    for b in range(nb):
+        assert rel(d[b], g["d"][b]) < TOL_GAIN, b
+        assert rel(K[b], g["K"][b]) < TOL_GAIN, b
+
+
+def test_tl_forward(gpu, g):
+    nb, T = g["u"].shape[:2]
+    s = tl_solver(T, nb)
+    pc = torch.full((nb,), float("inf"), dtype=torch.float64, device="cuda")
+    xn, un, cost, trials, st = s.forward(dev(g["x"]), dev(g["u"]), dev(g["d"]), dev(g["K"]), pc)
+    assert (st.cpu().numpy() == _lib.TRAJ_OK).all()
+    assert (trials.cpu().numpy() == 1).all()
+    assert rel(xn, g["fw_x"]) < TOL_ROLL * 10
+    assert rel(un, g["fw_u"]) < TOL_ROLL * 10
+    assert rel(cost, g["fw_cost"]) < TOL_COST
+
+
+def test_tl_forward_line_search_shrinks(gpu, g):
+    """prev_cost just above the α=1 cost of a doubled step forces α-halving
+    (forward_pass.jl:77-82); the accepted rollout equals the oracle's at that α."""
+    nb, T = g["u"].shape[:2]
+    x, u = g["x"][:1], g["u"][:1]
+    d2 = 6.0 * g["d"][:1]  # overshoot: α = 1 increases the cost
+    K = g["K"][:1]
+    TL = O.TwoLink
+    c0 = O.total_cost_generator(np.zeros_like(x[0]), TL.immediate_cost, TL.final_cost)(x[0], u[0])
+    st = {}
+    xo, uo, co = O.forward_pass(x[0], u[0], np.zeros_like(x[0]), d2[0], K[0], c0, TL.dynamicsf,
+                                TL.immediate_cost, TL.final_cost, max_trials=64, stats=st)
+    assert st["trials"] > 1
+    s = tl_solver(T, 1)
+    xn, un, cost, trials, sts = s.forward(dev(x), dev(u), dev(d2), dev(K),
+                                          torch.tensor([c0], dtype=torch.float64, device="cuda"))
+    assert int(trials[0]) == st["trials"]
+    assert rel(xn[0], xo) < 1e-11 and rel(un[0], uo) < 1e-11
+    assert abs(float(cost[0]) - co) / co < TOL_COST
+
+
+def test_tl_x_traj(gpu, g):
+    """x_traj enters only the line-search objective (forward_pass.jl:187-190)."""
+    nb, T = g["u"].shape[:2]
+    xt = 0.05 * np.random.default_rng(3).standard_normal(g["x"].shape)
+    s = tl_solver(T, nb)
+    pc = torch.full((nb,), float("inf"), dtype=torch.float64, device="cuda")
+    xn, un, cost, _, _ = s.forward(dev(g["x"]), dev(g["u"]), dev(g["d"]), dev(g["K"]), pc,
+                                   x_traj=dev(xt))
+    TL = O.TwoLink
+    for b in range(nb):
+        ref = O.total_cost_generator(xt[b], TL.immediate_cost, TL.final_cost)(g["fw_x"][b], g["fw_u"][b])
+        assert abs(float(cost[b]) - ref) / ref < 1e-11
+    assert rel(xn, g["fw_x"]) < TOL_ROLL * 10  # the rollout itself is unchanged
+
+
+def test_tl_fit(gpu, g):
+    nb, T = g["u"].shape[:2]
+    s = tl_solver(T, nb)
+    r = s.fit(dev(g["x"]), dev(g["u"]), max_iter=40, tol=1e-6)
+    st = r.status.cpu().numpy()
+    assert (st == _lib.TRAJ_CONVERGED).all(), st
+    assert (r.iters.cpu().numpy() == g["fit_iters"]).all()
+    for b in range(nb):
+        assert rel(r.x[b], g["fit_x"][b]) < TOL_FIT, b
+        assert rel(r.u[b], g["fit_u"][b]) < TOL_FIT, b
+        it = int(g["fit_iters"][b])
+        assert abs(float(r.cost[b]) - g["fit_cost"][b, it - 1]) / g["fit_cost"][b, it - 1] < 1e-11
+
+
+def test_tl_api_mirror(gpu, g):
+    """iLQR.fit / backward_pass / forward_pass called with the 2-link closures."""
+    from ilqr_amd import api
+    f, l, lf = two_link_closures()
+    d, K = api.backward_pass(g["x"][0], g["u"][0], f, l, lf)
+    assert rel(d, g["d"][0]) < TOL_GAIN and rel(K, g["K"][0]) < TOL_GAIN
+    xn, un, c = api.forward_pass(g["x"][0], g["u"][0], None, g["d"][0], g["K"][0], np.inf, f, l, lf)
+    assert rel(xn, g["fw_x"][0]) < TOL_ROLL * 10 and abs(c - g["fw_cost"][0]) / g["fw_cost"][0] < TOL_COST
+    xf, uf = api.fit(g["x"][0], g["u"][0], f, l, lf, max_iter=40, tol=1e-6)
+    assert rel(xf, g["fit_x"][0]) < TOL_FIT
+
+
+def test_tl_config2_batch(gpu):
+    """BASELINE config 2: B = 1024 random x₀ (default_rng(b).random(4)), u₀ = 0, T = 50.
+    Every trajectory converges with monotone cost; three sampled trajectories match
+    the oracle's fit; the device rollout matches the host dynamics."""
+    B, T = 1024, 50
+    x0 = two_link_initial_states(B)
+    s = tl_solver(T, B)
+    u0 = torch.zeros((B, T, 2), dtype=torch.float64, device="cuda")
+    x = s.rollout(dev(x0), u0)
+    f, l, lf = two_link_closures()
+    for b in (0, 517):
+        assert rel(x[b], O.rollout(x0[b], np.zeros((T, 2)), f)) < TOL_ROLL
+    r = s.fit(x, u0, max_iter=100, tol=1e-6)
+    st = r.status.cpu().numpy()
+    assert (st == _lib.TRAJ_CONVERGED).all(), np.unique(st, return_counts=True)
+    xs, us = x.cpu().numpy(), u0.cpu().numpy()
+    TL = O.TwoLink
+    for b in (0, 517, 1023):
+        h = []
+        fx, fu = O.fit(xs[b], us[b], TL.dynamicsf, TL.immediate_cost, TL.final_cost, max_iter=100,
+                       tol=1e-6, max_trials=64, history=h)
+        assert int(r.iters[b]) == len(h), b
+        assert rel(r.x[b], fx) < TOL_FIT and rel(r.u[b], fu) < TOL_FIT, b
+        assert abs(float(r.cost[b]) - h[-1]["cost"]) / h[-1]["cost"] < 1e-11
+
+
+def test_tl_long_horizon_reaches_target(gpu):
+    """The reference's end-to-end example (animate_2_link.jl:7-25: x₀ = [.1,-.1,0,0],
+    u₀ = 0, T = 900, tol = 1e-6) and the repaired check of test_iLQR.jl:19:
+    final_cost(x̄_N) < 0.01. Parity here is a property, not a fixture: the oracle
+    is too slow at T = 900."""
+    T = 900
+    s = tl_solver(T, 1)
+    u0 = torch.zeros((1, T, 2), dtype=torch.float64, device="cuda")
+    x = s.rollout(dev(np.array([[0.1, -0.1, 0.0, 0.0]])), u0)
+    r = s.fit(x, u0, max_iter=1000, tol=1e-6)
+    assert int(r.status[0]) == _lib.TRAJ_CONVERGED
+    th = TwoLinkArm.inverse_kinematics()
+    xN = r.x[0, -1].cpu().numpy()
+    assert float(np.sum((th - xN[:2]) ** 2)) < 0.01
+
+
+def test_tl_bad_problem_args(gpu):
+    """A TWO_LINK descriptor carrying LQ matrices is rejected (ILQR_ERR_BAD_ARG)."""
+    import ctypes as C
+    s = tl_solver(10, 2)
+    junk = torch.zeros(64, dtype=torch.float64, device="cuda")
+    p = _lib.Problem(_lib.PROBLEM_TWO_LINK, 0, junk.data_ptr(), None, None, None, None)
+    x = torch.zeros((2, 11, 4), dtype=torch.float64, device="cuda")
+    u = torch.zeros((2, 10, 2), dtype=torch.float64, device="cuda")
+    d = torch.empty((2, 10, 2), dtype=torch.float64, device="cuda")
+    K = torch.empty((2, 10, 2, 4), dtype=torch.float64, device="cuda")
+    rc = s.lib.ilqr_backward(s.h, C.byref(p), None, C.c_void_p(x.data_ptr()), C.c_void_p(u.data_ptr()),
+                             C.c_void_p(d.data_ptr()), C.c_void_p(K.data_ptr()), None)
+    assert rc == _lib.ERR_BAD_ARG
