@@ -1,5 +1,5 @@
-"""ctypes wrapper of oracle/ilqr_ref.c (C restatement of the reference's LQ hot
-path) — TEST INFRASTRUCTURE ONLY: the checker for large parity tests and the
+"""ctypes wrapper of oracle/ilqr_ref.c (C restatement of the reference's hot
+path for the LQ family and the 2-link arm) — TEST INFRASTRUCTURE ONLY: the checker for large parity tests and the
 bench's cpu_baseline leg. Build with `make -C oracle`."""
 from __future__ import annotations
 
@@ -92,3 +92,72 @@ def lq_fit(lq, x_init, u_init, x_traj=None, max_iter=100, tol=1e-6, mu=0.01, max
                       _p(ui), _p(xt), max_iter, C.c_double(tol), C.c_double(mu), int(symmetrize), max_trials,
                       _p(xo), _p(uo), _p(cost), _p(iters), _p(st), nthreads)
     return xo, uo, cost, iters, st
+
+
+# -- 2-link arm (test/2_link_example) ---------------------------------------------
+def tl_backward(x, u, mu=0.01, symmetrize=False, nthreads=0):
+    lib = load()
+    x, u = _f64(x), _f64(u)
+    nb, T = u.shape[:2]
+    d = np.empty((nb, T, 2))
+    K = np.empty((nb, T, 2, 4))
+    st = np.empty(nb, dtype=np.int32)
+    lib.oracle_tl_backward(nb, T, _p(x), _p(u), C.c_double(mu), int(symmetrize), _p(d), _p(K),
+                           _p(st), nthreads)
+    return d, K, st
+
+
+def tl_forward(x, u, x_traj, d, K, prev_cost, max_trials=64, alpha0=1.0, shrink=0.5, nthreads=0):
+    lib = load()
+    x, u, d, K = _f64(x), _f64(u), _f64(d), _f64(K)
+    nb, T = u.shape[:2]
+    xt = None if x_traj is None else _f64(x_traj)
+    pc = _f64(np.broadcast_to(np.asarray(prev_cost, dtype=np.float64), (nb,)))
+    xn = np.empty((nb, T + 1, 4))
+    un = np.empty((nb, T, 2))
+    cost = np.empty(nb)
+    tr = np.empty(nb, dtype=np.int32)
+    lib.oracle_tl_forward(nb, T, _p(x), _p(u), _p(xt), _p(d), _p(K), _p(pc), _p(xn), _p(un),
+                          _p(cost), _p(tr), max_trials, C.c_double(alpha0), C.c_double(shrink),
+                          nthreads)
+    return xn, un, cost, tr
+
+
+def tl_fit(x_init, u_init, x_traj=None, max_iter=100, tol=1e-6, mu=0.01, max_trials=64,
+           symmetrize=False, nthreads=0):
+    lib = load()
+    xi, ui = _f64(x_init), _f64(u_init)
+    nb, T = ui.shape[:2]
+    xt = None if x_traj is None else _f64(x_traj)
+    xo = np.empty((nb, T + 1, 4))
+    uo = np.empty((nb, T, 2))
+    cost = np.empty(nb)
+    iters = np.empty(nb, dtype=np.int32)
+    st = np.empty(nb, dtype=np.int32)
+    lib.oracle_tl_fit(nb, T, _p(xi), _p(ui), _p(xt), max_iter, C.c_double(tol), C.c_double(mu),
+                      int(symmetrize), max_trials, _p(xo), _p(uo), _p(cost), _p(iters), _p(st),
+                      nthreads)
+    return xo, uo, cost, iters, st
+
+
+def twolink_cpu_baseline(x, u, batch, budget_s):
+    """bench_twolink's cpu_baseline leg: one cold-start iteration (backward +
+    forward) per trajectory of the 2-link workload, OpenMP over trajectories."""
+    import time
+    threads = min(16, os.cpu_count() or 1)
+    n = 64
+    while True:
+        idx = np.arange(n) % x.shape[0]
+        t0 = time.perf_counter()
+        d, K, _ = tl_backward(x[idx], u[idx], nthreads=threads)
+        tl_forward(x[idx], u[idx], None, d, K, np.inf, nthreads=threads)
+        el = time.perf_counter() - t0
+        if el > budget_s / 4 or n >= 1 << 18:
+            break
+        n *= 2
+    rate = n / el
+    return {"value": rate / batch, "unit": f"batched iterations/s (batch={batch})", "cores": threads,
+            "kind": "port",
+            "sample": f"{n} trajectories x 1 cold-start iteration (C restatement oracle/ilqr_ref.c, "
+                      f"dual-number linearisation, OpenMP {threads} threads), {el:.2f} s; "
+                      f"trajectory-iterations/s={rate:.1f}"}

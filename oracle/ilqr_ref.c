@@ -17,6 +17,8 @@
  *   forward_pass                  (src/forward_pass.jl:55-93)    α halving, α on δu only
  *   total_cost                    (src/forward_pass.jl:182-196)  sequential sum, ℓ_f on raw x̄_N
  *   fit                           (src/forward_pass.jl:148-179)  prev_cost=Inf, break before update
+ * The same algorithm runs the 2-link arm of test/2_link_example (oracle_tl_*),
+ * its derivatives by dual-number forward-mode AD.
  * The reference's unbounded line search is capped at max_trials (status 3).
  * Layout: the ABI's (include/ilqr.h) row-major, trajectory-slowest arrays.
  * OpenMP parallelises over independent trajectories only.
@@ -97,40 +99,248 @@ static int lu_solve(int m, double* M, int c, double* Y) {
   return 1;
 }
 
-typedef struct {
+/* One trajectory's problem: the reference's three callbacks (dynamicsf,
+ * immediate_cost, final_cost) and the derivatives ForwardDiff takes of them
+ * (linearize_dynamics / immediate_cost_quadratization / final_cost_quadratization). */
+typedef struct prob_s prob_t;
+struct prob_s {
   int n, m, T;
-  const double *A, *B, *Q, *R, *Qf; /* this trajectory's instance */
-} lq_t;
+  const double *A, *B, *Q, *R, *Qf; /* LQ family: this trajectory's instance */
+  void (*lin)(const prob_t*, const double* x, const double* u, double* A, double* B);
+  /* 𝐪 (n), 𝐫 (m), 𝐐 (n×n), 𝐏 (m×n), 𝐑 (m×m) */
+  void (*quad)(const prob_t*, const double* x, const double* u, double* qv, double* r, double* Q,
+               double* P, double* R);
+  void (*fquad)(const prob_t*, const double* x, double* s, double* S);
+  void (*dyn)(const prob_t*, const double* x, const double* u, double* xn);
+  double (*cost)(const prob_t*, const double* x, const double* u);
+  double (*fcost)(const prob_t*, const double* x);
+};
 
-/* backward_pass (backward_pass.jl:324-357) for one trajectory. Returns 1 if NaN. */
-static int backward_one(const lq_t* P, const double* x, const double* u, double mu, int sym,
-                        double* d, double* K) {
-  const int n = P->n, m = P->m, T = P->T;
-  double S[NMAX * NMAX], s[NMAX], Qs[NMAX * NMAX], Rs[MMAX * MMAX];
-  double qv[NMAX], r[MMAX], g[MMAX], G[MMAX * NMAX], H[MMAX * MMAX], Hreg[MMAX * MMAX];
-  double BtS[MMAX * NMAX], AtS[NMAX * NMAX], t1[NMAX * NMAX], t2[NMAX], du[MMAX], Ki[MMAX * NMAX];
-  double HK[MMAX * NMAX], Hdu[MMAX], Snew[NMAX * NMAX], snew[NMAX];
-  int nan = 0;
+/* -- LQ family: f = Ax + Bu, ℓ = xᵀQx + uᵀRu, ℓ_f = xᵀQf x (exact derivatives) -- */
+static void lq_lin(const prob_t* P, const double* x, const double* u, double* A, double* B) {
+  (void)x; (void)u;
+  memcpy(A, P->A, sizeof(double) * P->n * P->n);
+  memcpy(B, P->B, sizeof(double) * P->n * P->m);
+}
+static void lq_quad(const prob_t* P, const double* x, const double* u, double* qv, double* r,
+                    double* Qs, double* Pm, double* Rs) {
+  const int n = P->n, m = P->m;
   for (int i = 0; i < n; ++i)
     for (int j = 0; j < n; ++j) Qs[i * n + j] = P->Q[i * n + j] + P->Q[j * n + i];
   for (int i = 0; i < m; ++i)
     for (int j = 0; j < m; ++j) Rs[i * m + j] = P->R[i * m + j] + P->R[j * m + i];
-  /* final_cost_quadratization (:134-153) */
+  memset(Pm, 0, sizeof(double) * m * n);
+  matvec(n, n, Qs, x, qv);
+  matvec(m, m, Rs, u, r);
+}
+static void lq_fquad(const prob_t* P, const double* x, double* s, double* S) {
+  const int n = P->n;
   for (int i = 0; i < n; ++i)
     for (int j = 0; j < n; ++j) S[i * n + j] = P->Qf[i * n + j] + P->Qf[j * n + i];
-  matvec(n, n, S, x + (size_t)T * n, s);
+  matvec(n, n, S, x, s);
+}
+static void lq_dyn(const prob_t* P, const double* x, const double* u, double* xn) {
+  double t1[NMAX], t2[NMAX];
+  matvec(P->n, P->n, P->A, x, t1);
+  matvec(P->n, P->m, P->B, u, t2);
+  for (int i = 0; i < P->n; ++i) xn[i] = t1[i] + t2[i];
+}
+static double lq_cost(const prob_t* P, const double* x, const double* u) {
+  double t[NMAX];
+  double c = 0.0;
+  matvec(P->n, P->n, P->Q, x, t);
+  for (int i = 0; i < P->n; ++i) c += x[i] * t[i];
+  matvec(P->m, P->m, P->R, u, t);
+  double cu = 0.0;
+  for (int i = 0; i < P->m; ++i) cu += u[i] * t[i];
+  return c + cu;
+}
+static double lq_fcost(const prob_t* P, const double* x) {
+  double t[NMAX];
+  double c = 0.0;
+  matvec(P->n, P->n, P->Qf, x, t);
+  for (int i = 0; i < P->n; ++i) c += x[i] * t[i];
+  return c;
+}
+
+/* -- 2-link arm: test/2_link_example/2_link_helper_functions.jl:1-108 ----------------
+ * Restates oracle/ilqr_oracle.py's TwoLink (literal, quirks included): RK4 of
+ * [θ̇; −(M⁻¹C)θ̇ + M⁻¹u] with the script's CoriolisMatrix (k = 2 term only), the
+ * 2×2 inverse by cofactors (ilqr_oracle._inv2). linearize_dynamics is forward-mode
+ * AD with the 6 directions (x, u) carried together — ForwardDiff's arithmetic. */
+typedef struct { double v, d[6]; } dual6;
+static dual6 dc(double v) { dual6 r; r.v = v; for (int i = 0; i < 6; ++i) r.d[i] = 0.0; return r; }
+static dual6 dadd(dual6 a, dual6 b) { dual6 r; r.v = a.v + b.v; for (int i = 0; i < 6; ++i) r.d[i] = a.d[i] + b.d[i]; return r; }
+static dual6 dsub(dual6 a, dual6 b) { dual6 r; r.v = a.v - b.v; for (int i = 0; i < 6; ++i) r.d[i] = a.d[i] - b.d[i]; return r; }
+static dual6 dneg(dual6 a) { dual6 r; r.v = -a.v; for (int i = 0; i < 6; ++i) r.d[i] = -a.d[i]; return r; }
+static dual6 dmul(dual6 a, dual6 b) { dual6 r; r.v = a.v * b.v; for (int i = 0; i < 6; ++i) r.d[i] = a.d[i] * b.v + a.v * b.d[i]; return r; }
+static dual6 dscale(double a, dual6 b) { dual6 r; r.v = a * b.v; for (int i = 0; i < 6; ++i) r.d[i] = a * b.d[i]; return r; }
+static dual6 ddiv(dual6 a, dual6 b) {
+  dual6 r; r.v = a.v / b.v;
+  for (int i = 0; i < 6; ++i) r.d[i] = (a.d[i] * b.v - a.v * b.d[i]) / (b.v * b.v);
+  return r;
+}
+static dual6 dsin(dual6 a) { dual6 r; r.v = sin(a.v); const double c = cos(a.v); for (int i = 0; i < 6; ++i) r.d[i] = c * a.d[i]; return r; }
+static dual6 dcos(dual6 a) { dual6 r; r.v = cos(a.v); const double s = -sin(a.v); for (int i = 0; i < 6; ++i) r.d[i] = s * a.d[i]; return r; }
+
+typedef struct { double alpha, beta, delta, dt, tgt0, tgt1; } tl_consts;
+static tl_consts TL;
+static void tl_init(void) {
+  static int done = 0;
+  if (done) return;
+  const double l1 = sqrt(2.) / 2., l2 = sqrt(2.) / 2., r2 = 0.5 * l2, r1 = 0.5 * l1;
+  const double m1 = 1.0, m2 = 1.0;
+  const double Iz1 = 1.0 / 12.0 * m1 * (l1 * l1), Iz2 = 1.0 / 12.0 * m2 * (l2 * l2);
+  TL.alpha = Iz1 + Iz2 + m1 * (r1 * r1) + m2 * (l1 * l1 + r2 * r2);   /* :11 */
+  TL.beta = m2 * l1 * r2;                                              /* :12 */
+  TL.delta = Iz2 + m2 * (r2 * r2);                                     /* :13 */
+  TL.dt = 0.01;                                                        /* :14 */
+  const double x = 0.6, y = -0.5;                                      /* :16 */
+  const double q2 = acos((x * x + y * y - l1 * l1 - l2 * l2) / (2 * l1 * l2));  /* :22-23 */
+  TL.tgt0 = atan2(y, x) - atan2(l2 * sin(q2), l1 + l2 * cos(q2));
+  TL.tgt1 = q2;
+  done = 1;
+}
+
+/* continuous_dynamics (:51-69) on duals */
+static void tl_cd_dual(const dual6* x, const dual6* u, dual6* xd) {
+  const dual6 c2 = dcos(x[1]), s2 = dsin(x[1]);
+  const dual6 m00 = dadd(dc(TL.alpha), dscale(2 * TL.beta, c2));
+  const dual6 m01 = dadd(dc(TL.delta), dscale(TL.beta, c2));
+  const dual6 dm00 = dscale(2 * TL.beta, dneg(s2)), dm01 = dscale(TL.beta, dneg(s2));
+  const dual6 zero = dc(0.0);
+  /* C[i,j] = ½(∇M[k,i,j] + ∇M[j,i,k] − ∇M[i,k,j])·θ̇[k], k = 2 only (:42-44) */
+  const dual6 c00 = dmul(dscale(0.5, dsub(dadd(zero, dm00), zero)), x[3]);
+  const dual6 c01 = dmul(dscale(0.5, dsub(dadd(dm01, dm01), dm01)), x[3]);
+  const dual6 c10 = dmul(dscale(0.5, dsub(dadd(zero, dm01), zero)), x[3]);
+  const dual6 c11 = dmul(dscale(0.5, dsub(dadd(zero, zero), zero)), x[3]);
+  const dual6 det = dsub(dmul(m00, dc(TL.delta)), dmul(m01, m01));
+  const dual6 i00 = ddiv(dc(TL.delta), det), i01 = ddiv(dneg(m01), det);
+  const dual6 i10 = ddiv(dneg(m01), det), i11 = ddiv(m00, det);
+  const dual6 mc00 = dadd(dmul(i00, c00), dmul(i01, c10)), mc01 = dadd(dmul(i00, c01), dmul(i01, c11));
+  const dual6 mc10 = dadd(dmul(i10, c00), dmul(i11, c10)), mc11 = dadd(dmul(i10, c01), dmul(i11, c11));
+  xd[0] = x[2];
+  xd[1] = x[3];
+  xd[2] = dadd(dneg(dadd(dmul(mc00, x[2]), dmul(mc01, x[3]))), dadd(dmul(i00, u[0]), dmul(i01, u[1])));
+  xd[3] = dadd(dneg(dadd(dmul(mc10, x[2]), dmul(mc11, x[3]))), dadd(dmul(i10, u[0]), dmul(i11, u[1])));
+}
+/* the same on doubles (forward rollout) */
+static void tl_cd(const double* x, const double* u, double* xd) {
+  const double c2 = cos(x[1]), s2 = sin(x[1]);
+  const double m00 = TL.alpha + 2 * TL.beta * c2, m01 = TL.delta + TL.beta * c2;
+  const double dm00 = 2 * TL.beta * -s2, dm01 = TL.beta * -s2;
+  const double c00 = 0.5 * dm00 * x[3], c01 = 0.5 * ((dm01 + dm01) - dm01) * x[3];
+  const double c10 = 0.5 * dm01 * x[3], c11 = 0.0 * x[3];
+  const double det = m00 * TL.delta - m01 * m01;
+  const double i00 = TL.delta / det, i01 = -m01 / det, i10 = -m01 / det, i11 = m00 / det;
+  const double mc00 = i00 * c00 + i01 * c10, mc01 = i00 * c01 + i01 * c11;
+  const double mc10 = i10 * c00 + i11 * c10, mc11 = i10 * c01 + i11 * c11;
+  xd[0] = x[2];
+  xd[1] = x[3];
+  xd[2] = -(mc00 * x[2] + mc01 * x[3]) + (i00 * u[0] + i01 * u[1]);
+  xd[3] = -(mc10 * x[2] + mc11 * x[3]) + (i10 * u[0] + i11 * u[1]);
+}
+/* RK4 (:71-78) */
+static void tl_rk4(const double* x, const double* u, double* xn) {
+  double k1[4], k2[4], k3[4], k4[4], y[4];
+  tl_cd(x, u, k1);
+  for (int i = 0; i < 4; ++i) { k1[i] *= TL.dt; y[i] = x[i] + k1[i] / 2; }
+  tl_cd(y, u, k2);
+  for (int i = 0; i < 4; ++i) { k2[i] *= TL.dt; y[i] = x[i] + k2[i] / 2; }
+  tl_cd(y, u, k3);
+  for (int i = 0; i < 4; ++i) { k3[i] *= TL.dt; y[i] = x[i] + k3[i]; }
+  tl_cd(y, u, k4);
+  for (int i = 0; i < 4; ++i) { k4[i] *= TL.dt; xn[i] = x[i] + (1.0 / 6.0) * (k1[i] + 2 * k2[i] + 2 * k3[i] + k4[i]); }
+}
+static void tl_rk4_dual(const dual6* x, const dual6* u, dual6* xn) {
+  dual6 k1[4], k2[4], k3[4], k4[4], y[4];
+  tl_cd_dual(x, u, k1);
+  for (int i = 0; i < 4; ++i) { k1[i] = dscale(TL.dt, k1[i]); y[i] = dadd(x[i], dscale(0.5, k1[i])); }
+  tl_cd_dual(y, u, k2);
+  for (int i = 0; i < 4; ++i) { k2[i] = dscale(TL.dt, k2[i]); y[i] = dadd(x[i], dscale(0.5, k2[i])); }
+  tl_cd_dual(y, u, k3);
+  for (int i = 0; i < 4; ++i) { k3[i] = dscale(TL.dt, k3[i]); y[i] = dadd(x[i], k3[i]); }
+  tl_cd_dual(y, u, k4);
+  for (int i = 0; i < 4; ++i) {
+    k4[i] = dscale(TL.dt, k4[i]);
+    xn[i] = dadd(x[i], dscale(1.0 / 6.0, dadd(dadd(dadd(k1[i], dscale(2, k2[i])), dscale(2, k3[i])), k4[i])));
+  }
+}
+static void tl_lin(const prob_t* P, const double* x, const double* u, double* A, double* B) {
+  (void)P;
+  dual6 xs[4], us[2], out[4];
+  for (int i = 0; i < 4; ++i) { xs[i] = dc(x[i]); xs[i].d[i] = 1.0; }
+  for (int i = 0; i < 2; ++i) { us[i] = dc(u[i]); us[i].d[4 + i] = 1.0; }
+  tl_rk4_dual(xs, us, out);
+  for (int i = 0; i < 4; ++i) {
+    for (int k = 0; k < 4; ++k) A[i * 4 + k] = out[i].d[k];
+    for (int k = 0; k < 2; ++k) B[i * 2 + k] = out[i].d[4 + k];
+  }
+}
+/* ℓ = Σ(θ*−θ)²·1 + Σu²·1 (:82-97): exact gradient/Hessian */
+static void tl_quad(const prob_t* P, const double* x, const double* u, double* qv, double* r,
+                    double* Q, double* Pm, double* R) {
+  (void)P;
+  memset(Q, 0, sizeof(double) * 16);
+  memset(Pm, 0, sizeof(double) * 8);
+  memset(R, 0, sizeof(double) * 4);
+  qv[0] = 2 * (TL.tgt0 - x[0]) * -1.0;
+  qv[1] = 2 * (TL.tgt1 - x[1]) * -1.0;
+  qv[2] = qv[3] = 0.0;
+  Q[0] = Q[5] = 2.0;
+  r[0] = 2 * u[0];
+  r[1] = 2 * u[1];
+  R[0] = R[3] = 2.0;
+}
+static void tl_fquad(const prob_t* P, const double* x, double* s, double* S) {
+  (void)P;
+  memset(S, 0, sizeof(double) * 16);
+  s[0] = 2 * (TL.tgt0 - x[0]) * -1.0;
+  s[1] = 2 * (TL.tgt1 - x[1]) * -1.0;
+  s[2] = s[3] = 0.0;
+  S[0] = S[5] = 2.0;
+}
+static void tl_dyn(const prob_t* P, const double* x, const double* u, double* xn) { (void)P; tl_rk4(x, u, xn); }
+static double tl_cost(const prob_t* P, const double* x, const double* u) {
+  (void)P;
+  const double e0 = TL.tgt0 - x[0], e1 = TL.tgt1 - x[1];
+  return (e0 * e0 + e1 * e1) * 1.0 + (u[0] * u[0] + u[1] * u[1]) * 1.0;
+}
+static double tl_fcost(const prob_t* P, const double* x) {
+  (void)P;
+  const double e0 = TL.tgt0 - x[0], e1 = TL.tgt1 - x[1];
+  return (e0 * e0 + e1 * e1) * 1.0;
+}
+static prob_t tl_problem(int T) {
+  tl_init();
+  prob_t P = {4, 2, T, NULL, NULL, NULL, NULL, NULL, tl_lin, tl_quad, tl_fquad, tl_dyn, tl_cost, tl_fcost};
+  return P;
+}
+
+/* backward_pass (backward_pass.jl:324-357) for one trajectory. Returns 1 if NaN. */
+static int backward_one(const prob_t* P, const double* x, const double* u, double mu, int sym,
+                        double* d, double* K) {
+  const int n = P->n, m = P->m, T = P->T;
+  double S[NMAX * NMAX], s[NMAX], Qs[NMAX * NMAX], Rs[MMAX * MMAX], Pm[MMAX * NMAX];
+  double A[NMAX * NMAX], Bm[NMAX * MMAX];
+  double qv[NMAX], r[MMAX], g[MMAX], G[MMAX * NMAX], H[MMAX * MMAX], Hreg[MMAX * MMAX];
+  double BtS[MMAX * NMAX], AtS[NMAX * NMAX], t1[NMAX * NMAX], t2[NMAX], du[MMAX], Ki[MMAX * NMAX];
+  double HK[MMAX * NMAX], Hdu[MMAX], Snew[NMAX * NMAX], snew[NMAX];
+  int nan = 0;
+  /* final_cost_quadratization (:134-153) */
+  P->fquad(P, x + (size_t)T * n, s, S);
   for (int t = T - 1; t >= 0; --t) { /* :339 */
     const double* xt = x + (size_t)t * n;
     const double* ut = u + (size_t)t * m;
-    /* immediate_cost_quadratization (:81-109) */
-    matvec(n, n, Qs, xt, qv);
-    matvec(m, m, Rs, ut, r);
+    P->lin(P, xt, ut, A, Bm);                 /* linearize_dynamics (:25-40) */
+    P->quad(P, xt, ut, qv, r, Qs, Pm, Rs);     /* immediate_cost_quadratization (:81-109) */
     /* optimal_controller_param (:177-186) */
-    matTvec(n, m, P->B, s, g);                 /* Bᵀ s */
+    matTvec(n, m, Bm, s, g);                   /* Bᵀ s */
     for (int i = 0; i < m; ++i) g[i] += r[i];  /* g = r + Bᵀ s */
-    matTmul(n, m, n, P->B, S, BtS);            /* Bᵀ S */
-    matmul(m, n, n, BtS, P->A, G);             /* G = P + (BᵀS)A, P = 0 */
-    matmul(m, n, m, BtS, P->B, H);             /* (BᵀS)B */
+    matTmul(n, m, n, Bm, S, BtS);              /* Bᵀ S */
+    matmul(m, n, n, BtS, A, G);                /* (BᵀS)A */
+    for (int i = 0; i < m * n; ++i) G[i] += Pm[i]; /* G = P + (BᵀS)A */
+    matmul(m, n, m, BtS, Bm, H);               /* (BᵀS)B */
     for (int i = 0; i < m * m; ++i) H[i] += Rs[i];
     /* feedback_parameters (:207-218) */
     memcpy(Hreg, H, sizeof(double) * m * m);
@@ -148,7 +358,7 @@ static int backward_one(const lq_t* P, const double* x, const double* u, double 
     for (int i = 0; i < m * n; ++i) K[(size_t)t * m * n + i] = Ki[i];
     /* step_back (:262-273), unregularised H */
     matvec(m, m, H, du, Hdu);
-    matTvec(n, n, P->A, s, snew);               /* Aᵀ s' */
+    matTvec(n, n, A, s, snew);                  /* Aᵀ s' */
     for (int i = 0; i < n; ++i) snew[i] += qv[i];
     matTvec(m, n, Ki, Hdu, t2);                 /* Kᵀ H δu */
     for (int i = 0; i < n; ++i) snew[i] += t2[i];
@@ -156,8 +366,8 @@ static int backward_one(const lq_t* P, const double* x, const double* u, double 
     for (int i = 0; i < n; ++i) snew[i] += t2[i];
     matTvec(m, n, G, du, t2);                   /* Gᵀ δu */
     for (int i = 0; i < n; ++i) snew[i] += t2[i];
-    matTmul(n, n, n, P->A, S, AtS);             /* Aᵀ S' */
-    matmul(n, n, n, AtS, P->A, Snew);           /* Aᵀ S' A */
+    matTmul(n, n, n, A, S, AtS);                /* Aᵀ S' */
+    matmul(n, n, n, AtS, A, Snew);              /* Aᵀ S' A */
     for (int i = 0; i < n * n; ++i) Snew[i] += Qs[i];
     matmul(m, m, n, H, Ki, HK);
     matTmul(m, n, n, Ki, HK, t1);               /* Kᵀ H K */
@@ -180,33 +390,14 @@ static int backward_one(const lq_t* P, const double* x, const double* u, double 
   return nan;
 }
 
-static double stage_cost(const lq_t* P, const double* x, const double* u) {
-  double t[NMAX];
-  double c = 0.0;
-  matvec(P->n, P->n, P->Q, x, t);
-  for (int i = 0; i < P->n; ++i) c += x[i] * t[i];
-  matvec(P->m, P->m, P->R, u, t);
-  double cu = 0.0;
-  for (int i = 0; i < P->m; ++i) cu += u[i] * t[i];
-  return c + cu;
-}
-
-static double final_cost(const lq_t* P, const double* x) {
-  double t[NMAX];
-  double c = 0.0;
-  matvec(P->n, P->n, P->Qf, x, t);
-  for (int i = 0; i < P->n; ++i) c += x[i] * t[i];
-  return c;
-}
-
 /* forward_pass (forward_pass.jl:55-93). Returns trials (>0 accepted, <0 exhausted). */
-static int forward_one(const lq_t* P, const double* x, const double* u, const double* xtraj,
+static int forward_one(const prob_t* P, const double* x, const double* u, const double* xtraj,
                        const double* d, const double* K, double prev_cost, double* xb,
                        double* ub, double* cost_out, int max_trials, double alpha0,
                        double shrink) {
   const int n = P->n, m = P->m, T = P->T;
   double alpha = alpha0;
-  double dx[NMAX], e[NMAX], Kdx[MMAX], t1[NMAX], t2[NMAX];
+  double dx[NMAX], e[NMAX], Kdx[MMAX];
   double new_cost = 0.0;
   for (int trial = 1; trial <= max_trials; ++trial) {
     memcpy(xb, x, sizeof(double) * n); /* :65 */
@@ -215,17 +406,15 @@ static int forward_one(const lq_t* P, const double* x, const double* u, const do
       matvec(m, n, K + (size_t)k * m * n, dx, Kdx);
       for (int i = 0; i < m; ++i)      /* :73 */
         ub[(size_t)k * m + i] = (u[(size_t)k * m + i] + alpha * d[(size_t)k * m + i]) + Kdx[i];
-      matvec(n, n, P->A, xb + (size_t)k * n, t1); /* :74 dynamicsf */
-      matvec(n, m, P->B, ub + (size_t)k * m, t2);
-      for (int i = 0; i < n; ++i) xb[(size_t)(k + 1) * n + i] = t1[i] + t2[i];
+      P->dyn(P, xb + (size_t)k * n, ub + (size_t)k * m, xb + (size_t)(k + 1) * n); /* :74 */
     }
     /* total_cost (:185-193) */
     double acc = 0.0;
     for (int k = 0; k < T; ++k) {
       for (int i = 0; i < n; ++i) e[i] = xb[(size_t)k * n + i] - (xtraj ? xtraj[(size_t)k * n + i] : 0.0);
-      acc += stage_cost(P, e, ub + (size_t)k * m);
+      acc += P->cost(P, e, ub + (size_t)k * m);
     }
-    acc += final_cost(P, xb + (size_t)T * n);
+    acc += P->fcost(P, xb + (size_t)T * n);
     new_cost = acc;
     *cost_out = new_cost;
     if (prev_cost - new_cost > 0) return trial; /* :77-80 */
@@ -234,10 +423,11 @@ static int forward_one(const lq_t* P, const double* x, const double* u, const do
   return -max_trials;
 }
 
-static lq_t instance(int b, int n, int m, int T, const double* A, const double* Bm, const double* Q,
-                     const double* R, const double* Qf) {
-  lq_t P = {n, m, T, A + (size_t)b * n * n, Bm + (size_t)b * n * m, Q + (size_t)b * n * n,
-            R + (size_t)b * m * m, Qf + (size_t)b * n * n};
+static prob_t instance(int b, int n, int m, int T, const double* A, const double* Bm,
+                       const double* Q, const double* R, const double* Qf) {
+  prob_t P = {n, m, T, A + (size_t)b * n * n, Bm + (size_t)b * n * m, Q + (size_t)b * n * n,
+              R + (size_t)b * m * m, Qf + (size_t)b * n * n,
+              lq_lin, lq_quad, lq_fquad, lq_dyn, lq_cost, lq_fcost};
   return P;
 }
 
@@ -267,7 +457,7 @@ int oracle_lq_backward(int Bn, int T, int n, int m, const double* A, const doubl
   int nans = 0;
 #pragma omp parallel for schedule(static) reduction(+ : nans)
   for (int b = 0; b < Bn; ++b) {
-    const lq_t P = instance(b, n, m, T, A, Bm, Q, R, Qf);
+    const prob_t P = instance(b, n, m, T, A, Bm, Q, R, Qf);
     const int bad = backward_one(&P, x + (size_t)b * (T + 1) * n, u + (size_t)b * T * m, mu, sym,
                                  d + (size_t)b * T * m, K + (size_t)b * T * m * n);
     if (status) status[b] = bad ? 4 : 0;
@@ -286,7 +476,7 @@ int oracle_lq_forward(int Bn, int T, int n, int m, const double* A, const double
   int fails = 0;
 #pragma omp parallel for schedule(static) reduction(+ : fails)
   for (int b = 0; b < Bn; ++b) {
-    const lq_t P = instance(b, n, m, T, A, Bm, Q, R, Qf);
+    const prob_t P = instance(b, n, m, T, A, Bm, Q, R, Qf);
     const int tr = forward_one(&P, x + (size_t)b * (T + 1) * n, u + (size_t)b * T * m,
                                xtraj ? xtraj + (size_t)b * (T + 1) * n : NULL,
                                d + (size_t)b * T * m, K + (size_t)b * T * m * n, prev_cost[b],
@@ -298,7 +488,40 @@ int oracle_lq_forward(int Bn, int T, int n, int m, const double* A, const double
   return fails;
 }
 
-/* fit (forward_pass.jl:148-179). status: 1 converged, 2 max_iter, 3 LS exhausted, 4 NaN. */
+/* fit (forward_pass.jl:148-179) for one trajectory.
+ * status: 1 converged, 2 max_iter, 3 LS exhausted, 4 NaN. */
+static void fit_one(const prob_t* P, const double* x_init, const double* u_init,
+                    const double* xtraj, int max_iter, double tol, double mu, int sym,
+                    int max_trials, double* x_out, double* u_out, double* cost, int* iters,
+                    int* status) {
+  const int n = P->n, m = P->m, T = P->T;
+  const size_t xs = (size_t)(T + 1) * n, us = (size_t)T * m;
+  double* buf = (double*)malloc(sizeof(double) * (2 * xs + 2 * us + us + us * n));
+  double *xi = buf, *ui = xi + xs, *xn = ui + us, *un = xn + xs, *d = un + us, *K = d + us;
+  memcpy(xi, x_init, sizeof(double) * xs);
+  memcpy(ui, u_init, sizeof(double) * us);
+  double prev_cost = INFINITY; /* :159 */
+  int st = 2, it;
+  for (it = 1; it <= max_iter; ++it) { /* :161 */
+    if (backward_one(P, xi, ui, mu, sym, d, K)) { st = 4; break; }
+    double nc = NAN;
+    const int tr = forward_one(P, xi, ui, xtraj, d, K, prev_cost, xn, un, &nc, max_trials, 1.0, 0.5);
+    if (tr < 0) { st = (nc != nc) ? 4 : 3; break; }
+    prev_cost = nc; /* :168 */
+    double du2 = 0.0;
+    for (size_t i = 0; i < us; ++i) du2 += (un[i] - ui[i]) * (un[i] - ui[i]);
+    if (du2 <= tol) { st = 1; break; } /* :171 — break before the update */
+    memcpy(xi, xn, sizeof(double) * xs); /* :174-175 */
+    memcpy(ui, un, sizeof(double) * us);
+  }
+  memcpy(x_out, xi, sizeof(double) * xs);
+  memcpy(u_out, ui, sizeof(double) * us);
+  *cost = prev_cost;
+  if (iters) *iters = it > max_iter ? max_iter : it;
+  if (status) *status = st;
+  free(buf);
+}
+
 int oracle_lq_fit(int Bn, int T, int n, int m, const double* A, const double* Bm, const double* Q,
                   const double* R, const double* Qf, const double* x_init, const double* u_init,
                   const double* xtraj, int max_iter, double tol, double mu, int sym, int max_trials,
@@ -306,35 +529,62 @@ int oracle_lq_fit(int Bn, int T, int n, int m, const double* A, const double* Bm
                   int nthreads) {
   if (n > NMAX || m > MMAX) return -1;
   set_threads(nthreads);
+  const size_t xs = (size_t)(T + 1) * n, us = (size_t)T * m;
 #pragma omp parallel for schedule(dynamic, 4)
   for (int b = 0; b < Bn; ++b) {
-    const lq_t P = instance(b, n, m, T, A, Bm, Q, R, Qf);
-    const size_t xs = (size_t)(T + 1) * n, us = (size_t)T * m;
-    double* buf = (double*)malloc(sizeof(double) * (2 * xs + 2 * us + us + us * n));
-    double *xi = buf, *ui = xi + xs, *xn = ui + us, *un = xn + xs, *d = un + us, *K = d + us;
-    memcpy(xi, x_init + b * xs, sizeof(double) * xs);
-    memcpy(ui, u_init + b * us, sizeof(double) * us);
-    double prev_cost = INFINITY; /* :159 */
-    int st = 2, it;
-    for (it = 1; it <= max_iter; ++it) { /* :161 */
-      if (backward_one(&P, xi, ui, mu, sym, d, K)) { st = 4; break; }
-      double nc;
-      const int tr = forward_one(&P, xi, ui, xtraj ? xtraj + b * xs : NULL, d, K, prev_cost, xn,
-                                 un, &nc, max_trials, 1.0, 0.5);
-      if (tr < 0) { st = (nc != nc) ? 4 : 3; break; }
-      prev_cost = nc; /* :168 */
-      double du2 = 0.0;
-      for (size_t i = 0; i < us; ++i) du2 += (un[i] - ui[i]) * (un[i] - ui[i]);
-      if (du2 <= tol) { st = 1; break; } /* :171 — break before the update */
-      memcpy(xi, xn, sizeof(double) * xs); /* :174-175 */
-      memcpy(ui, un, sizeof(double) * us);
-    }
-    memcpy(x_out + b * xs, xi, sizeof(double) * xs);
-    memcpy(u_out + b * us, ui, sizeof(double) * us);
-    cost[b] = prev_cost;
-    if (iters) iters[b] = it > max_iter ? max_iter : it;
-    if (status) status[b] = st;
-    free(buf);
+    const prob_t P = instance(b, n, m, T, A, Bm, Q, R, Qf);
+    fit_one(&P, x_init + b * xs, u_init + b * us, xtraj ? xtraj + b * xs : NULL, max_iter, tol, mu,
+            sym, max_trials, x_out + b * xs, u_out + b * us, &cost[b], iters ? &iters[b] : NULL,
+            status ? &status[b] : NULL);
   }
+  return 0;
+}
+
+/* -- 2-link arm entry points (same conventions as the LQ ones) -- */
+int oracle_tl_backward(int Bn, int T, const double* x, const double* u, double mu, int sym,
+                       double* d, double* K, int* status, int nthreads) {
+  set_threads(nthreads);
+  const prob_t P = tl_problem(T);
+  int nans = 0;
+#pragma omp parallel for schedule(static) reduction(+ : nans)
+  for (int b = 0; b < Bn; ++b) {
+    const int bad = backward_one(&P, x + (size_t)b * (T + 1) * 4, u + (size_t)b * T * 2, mu, sym,
+                                 d + (size_t)b * T * 2, K + (size_t)b * T * 8);
+    if (status) status[b] = bad ? 4 : 0;
+    nans += bad;
+  }
+  return nans;
+}
+
+int oracle_tl_forward(int Bn, int T, const double* x, const double* u, const double* xtraj,
+                      const double* d, const double* K, const double* prev_cost, double* xnew,
+                      double* unew, double* cost, int* trials, int max_trials, double alpha0,
+                      double shrink, int nthreads) {
+  set_threads(nthreads);
+  const prob_t P = tl_problem(T);
+  int fails = 0;
+#pragma omp parallel for schedule(static) reduction(+ : fails)
+  for (int b = 0; b < Bn; ++b) {
+    const int tr = forward_one(&P, x + (size_t)b * (T + 1) * 4, u + (size_t)b * T * 2,
+                               xtraj ? xtraj + (size_t)b * (T + 1) * 4 : NULL, d + (size_t)b * T * 2,
+                               K + (size_t)b * T * 8, prev_cost[b], xnew + (size_t)b * (T + 1) * 4,
+                               unew + (size_t)b * T * 2, &cost[b], max_trials, alpha0, shrink);
+    if (trials) trials[b] = tr;
+    fails += tr < 0;
+  }
+  return fails;
+}
+
+int oracle_tl_fit(int Bn, int T, const double* x_init, const double* u_init, const double* xtraj,
+                  int max_iter, double tol, double mu, int sym, int max_trials, double* x_out,
+                  double* u_out, double* cost, int* iters, int* status, int nthreads) {
+  set_threads(nthreads);
+  const prob_t P = tl_problem(T);
+  const size_t xs = (size_t)(T + 1) * 4, us = (size_t)T * 2;
+#pragma omp parallel for schedule(dynamic, 4)
+  for (int b = 0; b < Bn; ++b)
+    fit_one(&P, x_init + b * xs, u_init + b * us, xtraj ? xtraj + b * xs : NULL, max_iter, tol, mu,
+            sym, max_trials, x_out + b * xs, u_out + b * us, &cost[b], iters ? &iters[b] : NULL,
+            status ? &status[b] : NULL);
   return 0;
 }

@@ -208,3 +208,17 @@ def test_golden_twolink_reproduces():
     TL = O.TwoLink
     d, K = O.backward_pass(g["x"][0], g["u"][0], TL.dynamicsf, TL.immediate_cost, TL.final_cost)
     assert rel(K, g["K"][0]) < 1e-12 and rel(d, g["d"][0]) < 1e-12
+
+
+def test_c_oracle_twolink_agrees_with_golden():
+    """The C restatement's 2-link path (dual-number AD, oracle/ilqr_ref.c) against
+    the Python oracle's frozen fixture: backward, forward and fit."""
+    g = _load("twolink_t50")
+    d, K, st = cref.tl_backward(g["x"], g["u"])
+    assert (st == 0).all() and rel(d, g["d"]) < 1e-12 and rel(K, g["K"]) < 1e-12
+    xn, un, c, tr = cref.tl_forward(g["x"], g["u"], None, g["d"], g["K"], np.inf)
+    assert (tr == 1).all() and rel(xn, g["fw_x"]) < 1e-13 and rel(un, g["fw_u"]) < 1e-13
+    assert rel(c, g["fw_cost"]) < 1e-14
+    xo, uo, co, it, st = cref.tl_fit(g["x"], g["u"], max_iter=40)
+    assert np.array_equal(it, g["fit_iters"]) and (st == 1).all()
+    assert rel(xo, g["fit_x"]) < 1e-12 and rel(uo, g["fit_u"]) < 1e-12
