@@ -171,6 +171,7 @@ void ilqr_default_options(ilqr_options* o) {
 int ilqr_supported(int32_t kind, int nx, int nu) {
   if (kind == ILQR_PROBLEM_LQ) return ilqr::lq_supported(nx, nu) ? 1 : 0;
   if (kind == ILQR_PROBLEM_TWO_LINK) return ilqr::tl_supported(nx, nu) ? 1 : 0;
+  if (kind == ILQR_PROBLEM_TILES) return ilqr::tiles_supported(nx, nu) ? 1 : 0;
   return 0;
 }
 
@@ -278,6 +279,22 @@ ilqr_status ilqr_backward(ilqr_handle* h, const ilqr_problem* p, const ilqr_opti
   else
     HIP_TRY(ilqr::launch_lq_backward(h->nx, h->nu, lq_params(p), h->batch, h->T, x, u, d, K,
                                      status, ls_params(o).mu, h->stream));
+  return status ? fold_status(h, status) : ILQR_OK;
+}
+
+ilqr_status ilqr_backward_tiles(ilqr_handle* h, const ilqr_tiles* tl, const ilqr_options* o,
+                                double* d, double* K, int32_t* status) {
+  if (!h || !tl) return ILQR_ERR_BAD_ARG;
+  ilqr_status st = check_options(o);
+  if (st != ILQR_OK) return st;
+  if (!ilqr::tiles_supported(h->nx, h->nu)) return ILQR_ERR_UNSUPPORTED;
+  if (!tl->A || !tl->B || !tl->lx || !tl->lu || !tl->lxx || !tl->luu || !tl->lfx || !tl->lfxx ||
+      !d || !K)
+    return ILQR_ERR_BAD_ARG;
+  HIP_TRY(hipSetDevice(h->device));
+  const ilqr::TileParams P{tl->A, tl->B, tl->lx, tl->lu, tl->lxx, tl->lux, tl->luu, tl->lfx, tl->lfxx};
+  HIP_TRY(ilqr::launch_tiles_backward(h->nx, h->nu, P, h->batch, h->T, d, K, status,
+                                      ls_params(o).mu, h->stream));
   return status ? fold_status(h, status) : ILQR_OK;
 }
 

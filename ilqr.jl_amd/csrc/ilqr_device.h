@@ -1,0 +1,111 @@
+// Device helpers shared by the HIP translation units (gfx950 only). Private header.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace ilqr {
+namespace {
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+typedef unsigned u2v __attribute__((ext_vector_type(2)));
+
+constexpr int WAVES_PER_WG = 4;   // trajectories per workgroup
+constexpr int BW_LDS = 96 + 16 * 17;  // doubles of backward scratch per wave: [G|H] rows, g row, zero, S tile
+constexpr int SYM_EVERY = 4;          // symmetrise S every this many steps
+
+__device__ __forceinline__ d4 mfma(double a, double b, d4 c) {
+  return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
+// all-reduce over lanes {l, l^16} with v_permlane16_swap (gfx950): one instruction
+// per dword gives every lane both its own and its partner row's value.
+__device__ __forceinline__ double xor16_sum(double v) {
+  u2v p = __builtin_bit_cast(u2v, v);
+  auto lo = __builtin_amdgcn_permlane16_swap(p.x, p.x, false, false);
+  auto hi = __builtin_amdgcn_permlane16_swap(p.y, p.y, false, false);
+  u2v a = {lo[0], hi[0]};
+  u2v b = {lo[1], hi[1]};
+  return __builtin_bit_cast(double, a) + __builtin_bit_cast(double, b);
+}
+__device__ __forceinline__ double xor32_sum(double v) {
+  u2v p = __builtin_bit_cast(u2v, v);
+  auto lo = __builtin_amdgcn_permlane32_swap(p.x, p.x, false, false);
+  auto hi = __builtin_amdgcn_permlane32_swap(p.y, p.y, false, false);
+  u2v a = {lo[0], hi[0]};
+  u2v b = {lo[1], hi[1]};
+  return __builtin_bit_cast(double, a) + __builtin_bit_cast(double, b);
+}
+// sum over the four lanes {c, c+16, c+32, c+48} of a column
+__device__ __forceinline__ double colsum4(double v) { return xor32_sum(xor16_sum(v)); }
+
+// sum over the 16 lanes of a row (one forward group)
+__device__ __forceinline__ double rowsum16(double v) {
+#pragma unroll
+  for (int m = 8; m >= 1; m >>= 1) v += __shfl_xor(v, m, 16);
+  return v;
+}
+
+// Cross-lane LDS hand-off inside one wave: DS ops of a wave execute in order, so
+// only the compiler must be kept from moving LDS accesses across this point.
+__device__ __forceinline__ void wave_lds_fence() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// 1/x: v_rcp_f64 (≈2^-24 relative on gfx950) + two Newton steps. Measured by
+// tools/rcp_test.hip: 0 steps 2.5e8 ulp, 1 step 11 ulp, 2 steps 0 ulp.
+__device__ __forceinline__ double rcp(double x) {
+  double r = __builtin_amdgcn_rcp(x);
+  double e = fma(-x, r, 1.0);
+  r = fma(r, e, r);
+  e = fma(-x, r, 1.0);
+  return fma(r, e, r);
+}
+
+// Load-or-zero without a branch: the address is clamped to `safe` when !ok so
+// the load is unconditional (no exec-masked load + vmcnt(0) per element).
+__device__ __forceinline__ double ldz(bool ok, const double* p, const double* safe) {
+  const double v = *(ok ? p : safe);
+  return ok ? v : 0.0;
+}
+
+// (H + μI) = L D Lᵀ (no pivoting; H symmetric, lower triangle read) and a solve
+// with a d4 right-hand side; NU ≤ 4, entries ≥ NU unused.
+template <int NU>
+struct LDLT {
+  double l[NU][NU];
+  double dinv[NU];
+  __device__ __forceinline__ void factor(const double (&h)[NU][NU], double mu) {
+    double t[NU][NU];  // t[i][k] = L[i][k] · D[k]
+#pragma unroll
+    for (int k = 0; k < NU; ++k) {
+      double dk = h[k][k] + mu;
+#pragma unroll
+      for (int p = 0; p < k; ++p) dk = fma(-l[k][p], t[k][p], dk);
+      dinv[k] = rcp(dk);
+#pragma unroll
+      for (int i = k + 1; i < NU; ++i) {
+        double v = h[i][k];
+#pragma unroll
+        for (int p = 0; p < k; ++p) v = fma(-l[i][p], t[k][p], v);
+        t[i][k] = v;
+        l[i][k] = v * dinv[k];
+      }
+    }
+  }
+  __device__ __forceinline__ d4 solve(d4 x) const {
+#pragma unroll
+    for (int i = 0; i < NU; ++i)
+#pragma unroll
+      for (int p = 0; p < i; ++p) x[i] = fma(-l[i][p], x[p], x[i]);
+#pragma unroll
+    for (int i = 0; i < NU; ++i) x[i] *= dinv[i];
+#pragma unroll
+    for (int i = NU - 1; i >= 0; --i)
+#pragma unroll
+      for (int p = i + 1; p < NU; ++p) x[i] = fma(-l[p][i], x[p], x[i]);
+    return x;
+  }
+};
+
+}  // namespace
+}  // namespace ilqr

@@ -67,6 +67,14 @@ hipError_t launch_fill_i32(int32_t* p, int n, int32_t v, hipStream_t s);
 hipError_t launch_fill_f64(double* p, int n, double v, hipStream_t s);
 bool lq_supported(int nx, int nu);
 
+// Caller-supplied derivative tiles (ilqr_tiles in include/ilqr.h), device pointers.
+struct TileParams {
+  const double *A, *B, *lx, *lu, *lxx, *lux, *luu, *lfx, *lfxx;  // lux may be null (zeros)
+};
+bool tiles_supported(int nx, int nu);
+hipError_t launch_tiles_backward(int nx, int nu, const TileParams& p, int B, int T, double* d,
+                                 double* K, int32_t* status, double mu, hipStream_t s);
+
 // 2-link arm (ILQR_PROBLEM_TWO_LINK, test/2_link_example/2_link_helper_functions.jl):
 // the constants of the reference script, computed on the host in its expression order.
 struct TwoLinkParams {

@@ -30,12 +30,17 @@ TRAJ_NAN = 4
 
 PROBLEM_LQ = 1
 PROBLEM_TWO_LINK = 2
+PROBLEM_TILES = 3
 
 
 class Problem(C.Structure):
     _fields_ = [("kind", C.c_int32), ("reserved", C.c_int32),
                 ("A", C.c_void_p), ("B", C.c_void_p), ("Q", C.c_void_p),
                 ("R", C.c_void_p), ("Qf", C.c_void_p)]
+
+
+class Tiles(C.Structure):
+    _fields_ = [(n, C.c_void_p) for n in ("A", "B", "lx", "lu", "lxx", "lux", "luu", "lfx", "lfxx")]
 
 
 class Options(C.Structure):
@@ -56,6 +61,7 @@ SIGNATURES = {
     "ilqr_set_stream": (C.c_int, [P, P]),
     "ilqr_sync": (C.c_int, [P]),
     "ilqr_backward": (C.c_int, [P, C.POINTER(Problem), C.POINTER(Options), P, P, P, P, P]),
+    "ilqr_backward_tiles": (C.c_int, [P, C.POINTER(Tiles), C.POINTER(Options), P, P, P]),
     "ilqr_forward": (C.c_int, [P, C.POINTER(Problem), C.POINTER(Options), P, P, P, P, P, P,
                                P, P, P, P, P]),
     "ilqr_iterate": (C.c_int, [P, C.POINTER(Problem), C.POINTER(Options), P, P, P, P, P, P,

@@ -13,6 +13,12 @@ steps, u: (T, nu), δu: (T, nu), K: (T, nu, nx)); a leading batch dimension
 solves many independent problems at once. numpy inputs are copied to the GPU
 and results copied back; torch CUDA inputs stay on the device.
 
+Problem families: LinearDynamics/QuadraticCost/QuadraticFinalCost and the 2-link
+arm closures run fused device kernels; ANY other closures (written with torch ops
+on 1-D tensors) take the generic path — derivative tiles by torch.func on the
+device (ForwardDiff's role), the Riccati recursion in the HIP kernel behind
+ilqr_backward_tiles, and forward_pass rolling the user's dynamics out with torch.
+
 Errors mirror the reference: AssertionError for N ≠ M+1 (backward_pass.jl:329,
 forward_pass.jl:62,156) and for NaNs (backward_pass.jl:353-354,
 forward_pass.jl:89-90), TypeError for a non-integer max_iter
@@ -28,7 +34,9 @@ import numpy as np
 import torch
 
 from . import _lib
-from .problems import is_two_link, lq_from_closures
+from . import tiles as _tiles
+from .problems import (LinearDynamics, QuadraticCost, QuadraticFinalCost, is_two_link,
+                       lq_from_closures)
 from .solver import Solver
 
 
@@ -62,6 +70,24 @@ def _out(t, batched, as_torch):
     return t if as_torch else t.cpu().numpy()
 
 
+def _family(dynamicsf, immediate_cost, final_cost):
+    """'two_link', 'lq' (recognised problem families with fused device kernels) or
+    'closures' (arbitrary torch closures: derivative tiles + ilqr_backward_tiles)."""
+    if is_two_link(dynamicsf, immediate_cost, final_cost):
+        return "two_link"
+    if (isinstance(dynamicsf, LinearDynamics) and isinstance(immediate_cost, QuadraticCost)
+            and isinstance(final_cost, QuadraticFinalCost)):
+        return "lq"
+    return "closures"
+
+
+def _tiles_solver(xb, ub):
+    nb, N, nx = xb.shape
+    _, M, nu = ub.shape
+    assert N == M + 1, "size(x)[1] == size(u)[1] + 1"   # backward_pass.jl:329
+    return Solver(nx, nu, M, nb, device=_device(), kind=_lib.PROBLEM_TILES)
+
+
 def _solver(xb, ub, dynamicsf, immediate_cost, final_cost):
     nb, N, nx = xb.shape
     _, M, nu = ub.shape
@@ -83,8 +109,13 @@ def backward_pass(x, u, dynamicsf, immediate_cost, final_cost):
     """→ (δu, K) exactly like iLQR.backward_pass (backward_pass.jl:324-357)."""
     xb, batched, is_t = _as_batch(x, "x", 2)
     ub, _, _ = _as_batch(u, "u", 2)
-    s = _solver(xb, ub, dynamicsf, immediate_cost, final_cost)
-    d, K, st = s.backward(xb, ub)
+    if _family(dynamicsf, immediate_cost, final_cost) == "closures":
+        s = _tiles_solver(xb, ub)
+        tl = _tiles.derivative_tiles(xb, ub, dynamicsf, immediate_cost, final_cost)
+        d, K, st = s.backward_tiles(tl)
+    else:
+        s = _solver(xb, ub, dynamicsf, immediate_cost, final_cost)
+        d, K, st = s.backward(xb, ub)
     s.close()
     if bool((st == _lib.TRAJ_NAN).any()):
         raise AssertionError("!any(isnan, δu/K) failed")   # backward_pass.jl:353-354
@@ -105,9 +136,16 @@ def forward_pass(x, u, x_traj, du, K, prev_cost, dynamicsf, immediate_cost, fina
     pc = torch.as_tensor(np.broadcast_to(np.asarray(prev_cost, dtype=np.float64), (nb,)).copy()
                          if not isinstance(prev_cost, torch.Tensor) else prev_cost,
                          dtype=torch.float64).reshape(nb).to(xb.device).contiguous()
-    s = _solver(xb, ub, dynamicsf, immediate_cost, final_cost)
-    xn, un, cost, trials, st = s.forward(xb, ub, db, Kb, pc, x_traj=xt, max_trials=max_trials)
-    s.close()
+    if _family(dynamicsf, immediate_cost, final_cost) == "closures":
+        xn, un, cost, trials, ok = _tiles.rollout_forward(
+            xb, ub, xt, db, Kb, pc, dynamicsf, immediate_cost, final_cost,
+            max_trials=max_trials or _lib.default_options().max_trials)
+        st = torch.where(ok, 0, torch.where(torch.isnan(cost), _lib.TRAJ_NAN,
+                                            _lib.TRAJ_LS_EXHAUSTED)).to(torch.int32)
+    else:
+        s = _solver(xb, ub, dynamicsf, immediate_cost, final_cost)
+        xn, un, cost, trials, st = s.forward(xb, ub, db, Kb, pc, x_traj=xt, max_trials=max_trials)
+        s.close()
     if bool((st == _lib.TRAJ_NAN).any()):
         raise AssertionError("!any(isnan, ū/x̄) failed")   # forward_pass.jl:89-90
     if bool((st == _lib.TRAJ_LS_EXHAUSTED).any()):
@@ -129,9 +167,13 @@ def fit(x_init, u_init, dynamicsf, immediate_cost, final_cost, *, x_traj=None,
     xt = None
     if x_traj is not None:
         xt, _, _ = _as_batch(x_traj, "x_traj", 2)
-    s = _solver(xb, ub, dynamicsf, immediate_cost, final_cost)
-    r = s.fit(xb, ub, x_traj=xt, max_iter=int(max_iter), tol=float(tol))
-    s.close()
+    if _family(dynamicsf, immediate_cost, final_cost) == "closures":
+        r = _fit_closures(xb, ub, xt, dynamicsf, immediate_cost, final_cost, int(max_iter),
+                          float(tol))
+    else:
+        s = _solver(xb, ub, dynamicsf, immediate_cost, final_cost)
+        r = s.fit(xb, ub, x_traj=xt, max_iter=int(max_iter), tol=float(tol))
+        s.close()
     st = r.status.cpu().numpy()
     if (st == _lib.TRAJ_NAN).any():
         raise AssertionError("NaN in a trajectory (reference: AssertionError)")
@@ -143,6 +185,47 @@ def fit(x_init, u_init, dynamicsf, immediate_cost, final_cost, *, x_traj=None,
         info = {"cost": r.cost.cpu().numpy(), "iters": r.iters.cpu().numpy(), "status": st}
         return out + (info,)
     return out
+
+
+def _fit_closures(xb, ub, xt, dynamicsf, immediate_cost, final_cost, max_iter, tol):
+    """fit (forward_pass.jl:148-179) for arbitrary torch closures: per iteration,
+    derivative tiles (torch.func on the device) → ilqr_backward_tiles (HIP) →
+    forward_pass rollout of the user dynamics (torch on the device). Trajectories
+    that converge, exhaust their line search or hit NaN stop; the rest continue."""
+    from .solver import FitResult
+    nb = xb.shape[0]
+    s = _tiles_solver(xb, ub)
+    dev = xb.device
+    xi, ui = xb.clone(), ub.clone()
+    prev = torch.full((nb,), float("inf"), dtype=torch.float64, device=dev)   # :159
+    status = torch.zeros(nb, dtype=torch.int32, device=dev)
+    iters = torch.zeros(nb, dtype=torch.int32, device=dev)
+    max_trials = _lib.default_options().max_trials
+    for it in range(1, max_iter + 1):                                            # :161
+        run = status == _lib.TRAJ_OK
+        if not bool(run.any()):
+            break
+        tl = _tiles.derivative_tiles(xi, ui, dynamicsf, immediate_cost, final_cost)
+        d, K, bst = s.backward_tiles(tl)                                          # :162
+        status = torch.where(run & (bst == _lib.TRAJ_NAN), _lib.TRAJ_NAN, status).to(torch.int32)
+        run = status == _lib.TRAJ_OK
+        xn, un, c, _, ok = _tiles.rollout_forward(xi, ui, xt, d, K, prev, dynamicsf,
+                                                  immediate_cost, final_cost, max_trials)  # :163-166
+        iters = torch.where(run, it, iters).to(torch.int32)
+        bad = run & ~ok
+        status = torch.where(bad, torch.where(torch.isnan(c), _lib.TRAJ_NAN, _lib.TRAJ_LS_EXHAUSTED),
+                             status).to(torch.int32)
+        acc = run & ok
+        prev = torch.where(acc, c, prev)                                          # :168
+        du2 = ((un - ui) ** 2).sum(dim=(1, 2))
+        conv = acc & (du2 <= tol)                                                 # :171
+        status = torch.where(conv, _lib.TRAJ_CONVERGED, status).to(torch.int32)
+        step = acc & ~conv
+        xi = torch.where(step[:, None, None], xn, xi)                            # :174-175
+        ui = torch.where(step[:, None, None], un, ui)
+    s.close()
+    status = torch.where(status == _lib.TRAJ_OK, _lib.TRAJ_MAX_ITER, status).to(torch.int32)
+    return FitResult(xi, ui, prev, iters, status, _lib.OK)
 
 
 __all__ = ["fit", "backward_pass", "forward_pass", "LineSearchExhausted"]

@@ -123,6 +123,28 @@ class Solver:
         _lib.check(rc, "ilqr_backward", allow=(_lib.ERR_NAN,))
         return d, K, st
 
+    def backward_tiles(self, tiles, mu=None):
+        """iLQR.backward_pass on caller-supplied derivative tiles (ilqr_backward_tiles):
+        `tiles` maps ilqr_tiles' field names to CUDA float64 tensors (lux may be None)
+        → (d, K, status). Synchronises."""
+        B, T, nx, nu = self.batch, self.T, self.nx, self.nu
+        shapes = {"A": (B, T, nx, nx), "B": (B, T, nx, nu), "lx": (B, T, nx), "lu": (B, T, nu),
+                  "lxx": (B, T, nx, nx), "lux": (B, T, nu, nx), "luu": (B, T, nu, nu),
+                  "lfx": (B, nx), "lfxx": (B, nx, nx)}
+        for k, shp in shapes.items():
+            if k == "lux" and tiles.get(k) is None:
+                continue
+            _req(tiles[k], torch.float64, shp, k)
+        tl = _lib.Tiles(*(None if tiles.get(k) is None else tiles[k].data_ptr() for k in shapes))
+        d = torch.empty((B, T, nu), dtype=torch.float64, device=self.dev)
+        K = torch.empty((B, T, nu, nx), dtype=torch.float64, device=self.dev)
+        st = torch.empty((B,), dtype=torch.int32, device=self.dev)
+        self._bind_stream()
+        o = _lib.default_options(mu=mu)
+        rc = self.lib.ilqr_backward_tiles(self.h, C.byref(tl), C.byref(o), _ptr(d), _ptr(K), _ptr(st))
+        _lib.check(rc, "ilqr_backward_tiles", allow=(_lib.ERR_NAN,))
+        return d, K, st
+
     def forward(self, x, u, d, K, prev_cost, x_traj=None, alpha0=None, shrink=None,
                 max_trials=None):
         """iLQR.forward_pass for the batch → (x_new, u_new, new_cost, trials, status).

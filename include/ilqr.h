@@ -77,7 +77,11 @@ enum {
   ILQR_TRAJ_NAN = 4
 };
 
-typedef enum { ILQR_PROBLEM_LQ = 1, ILQR_PROBLEM_TWO_LINK = 2 } ilqr_problem_kind;
+typedef enum {
+  ILQR_PROBLEM_LQ = 1,
+  ILQR_PROBLEM_TWO_LINK = 2,
+  ILQR_PROBLEM_TILES = 3  /* ilqr_backward_tiles only (caller-supplied derivatives) */
+} ilqr_problem_kind;
 
 typedef struct {
   int32_t kind;        /* ilqr_problem_kind */
@@ -88,6 +92,23 @@ typedef struct {
   const double* R;     /* (batch, nu, nu) */
   const double* Qf;    /* (batch, nx, nx) */
 } ilqr_problem;
+
+/* Per-step derivative tiles of an ARBITRARY problem along (x, u): what the
+ * reference's derivative calls return — linearize_dynamics (backward_pass.jl:25-40),
+ * immediate_cost_quadratization (:81-109), final_cost_quadratization (:134-153) —
+ * evaluated by the caller (e.g. ForwardDiff on the host, as the reference does).
+ * Device pointers, fp64, row-major, trajectory slowest. */
+typedef struct {
+  const double* A;     /* (batch, T, nx, nx)  ∂f/∂x at (x_t, u_t)          */
+  const double* B;     /* (batch, T, nx, nu)  ∂f/∂u                         */
+  const double* lx;    /* (batch, T, nx)      𝐪 = ∇ₓℓ                       */
+  const double* lu;    /* (batch, T, nu)      𝐫 = ∇ᵤℓ                       */
+  const double* lxx;   /* (batch, T, nx, nx)  𝐐 = ∇²ₓₓℓ                     */
+  const double* lux;   /* (batch, T, nu, nx)  𝐏 = ∂(∇ᵤℓ)/∂x, NULL = zeros   */
+  const double* luu;   /* (batch, T, nu, nu)  𝐑 = ∇²ᵤᵤℓ                     */
+  const double* lfx;   /* (batch, nx)         ∇ℓ_f(x_N)                     */
+  const double* lfxx;  /* (batch, nx, nx)     ∇²ℓ_f(x_N)                    */
+} ilqr_tiles;
 
 typedef struct {
   int32_t max_iter;    /* fit: forward_pass.jl:152 default 100                         */
@@ -130,6 +151,13 @@ ilqr_status ilqr_backward(ilqr_handle* h, const ilqr_problem* p, const ilqr_opti
  * trajectory whose search exhausts max_trials gets x_new = x, u_new = u.
  * x_traj may be NULL (zeros); trials may be NULL. status as for ilqr_backward
  * (synchronising when given; ILQR_ERR_LS_EXHAUSTED / ILQR_ERR_NAN). */
+/* iLQR.backward_pass for arbitrary closures: the Riccati recursion of
+ * backward_pass.jl:335-357 (optimal_controller_param, feedback_parameters,
+ * step_back) on caller-supplied derivative tiles (ilqr_tiles); same outputs and
+ * status behaviour as ilqr_backward. Shapes: ilqr_supported(ILQR_PROBLEM_TILES, nx, nu). */
+ilqr_status ilqr_backward_tiles(ilqr_handle* h, const ilqr_tiles* tiles, const ilqr_options* o,
+                                double* d, double* K, int32_t* status);
+
 ilqr_status ilqr_forward(ilqr_handle* h, const ilqr_problem* p, const ilqr_options* o,
                          const double* x, const double* u, const double* x_traj,
                          const double* d, const double* K, const double* prev_cost,

@@ -161,3 +161,21 @@ def twolink_cpu_baseline(x, u, batch, budget_s):
             "sample": f"{n} trajectories x 1 cold-start iteration (C restatement oracle/ilqr_ref.c, "
                       f"dual-number linearisation, OpenMP {threads} threads), {el:.2f} s; "
                       f"trajectory-iterations/s={rate:.1f}"}
+
+
+# -- caller-supplied tiles (ilqr_backward_tiles) ------------------------------------
+TILE_NAMES = ("A", "B", "lx", "lu", "lxx", "lux", "luu", "lfx", "lfxx")
+
+
+def tiles_backward(tiles, mu=0.01, symmetrize=False, nthreads=0):
+    """tiles: dict of arrays with ilqr_tiles' shapes (lux may be None) → (d, K, status)."""
+    lib = load()
+    t = {k: (None if tiles.get(k) is None else _f64(tiles[k])) for k in TILE_NAMES}
+    nb, T, n, m = t["B"].shape
+    d = np.empty((nb, T, m))
+    K = np.empty((nb, T, m, n))
+    st = np.empty(nb, dtype=np.int32)
+    rc = lib.oracle_tiles_backward(nb, T, n, m, *(_p(t[k]) for k in TILE_NAMES), C.c_double(mu),
+                                   int(symmetrize), _p(d), _p(K), _p(st), nthreads)
+    assert rc >= 0
+    return d, K, st

@@ -106,10 +106,11 @@ typedef struct prob_s prob_t;
 struct prob_s {
   int n, m, T;
   const double *A, *B, *Q, *R, *Qf; /* LQ family: this trajectory's instance */
-  void (*lin)(const prob_t*, const double* x, const double* u, double* A, double* B);
+  const double* const* tiles;        /* TILES family: caller-supplied derivatives */
+  void (*lin)(const prob_t*, int t, const double* x, const double* u, double* A, double* B);
   /* 𝐪 (n), 𝐫 (m), 𝐐 (n×n), 𝐏 (m×n), 𝐑 (m×m) */
-  void (*quad)(const prob_t*, const double* x, const double* u, double* qv, double* r, double* Q,
-               double* P, double* R);
+  void (*quad)(const prob_t*, int t, const double* x, const double* u, double* qv, double* r,
+               double* Q, double* P, double* R);
   void (*fquad)(const prob_t*, const double* x, double* s, double* S);
   void (*dyn)(const prob_t*, const double* x, const double* u, double* xn);
   double (*cost)(const prob_t*, const double* x, const double* u);
@@ -117,13 +118,14 @@ struct prob_s {
 };
 
 /* -- LQ family: f = Ax + Bu, ℓ = xᵀQx + uᵀRu, ℓ_f = xᵀQf x (exact derivatives) -- */
-static void lq_lin(const prob_t* P, const double* x, const double* u, double* A, double* B) {
-  (void)x; (void)u;
+static void lq_lin(const prob_t* P, int t, const double* x, const double* u, double* A, double* B) {
+  (void)t; (void)x; (void)u;
   memcpy(A, P->A, sizeof(double) * P->n * P->n);
   memcpy(B, P->B, sizeof(double) * P->n * P->m);
 }
-static void lq_quad(const prob_t* P, const double* x, const double* u, double* qv, double* r,
-                    double* Qs, double* Pm, double* Rs) {
+static void lq_quad(const prob_t* P, int t, const double* x, const double* u, double* qv,
+                    double* r, double* Qs, double* Pm, double* Rs) {
+  (void)t;
   const int n = P->n, m = P->m;
   for (int i = 0; i < n; ++i)
     for (int j = 0; j < n; ++j) Qs[i * n + j] = P->Q[i * n + j] + P->Q[j * n + i];
@@ -266,8 +268,8 @@ static void tl_rk4_dual(const dual6* x, const dual6* u, dual6* xn) {
     xn[i] = dadd(x[i], dscale(1.0 / 6.0, dadd(dadd(dadd(k1[i], dscale(2, k2[i])), dscale(2, k3[i])), k4[i])));
   }
 }
-static void tl_lin(const prob_t* P, const double* x, const double* u, double* A, double* B) {
-  (void)P;
+static void tl_lin(const prob_t* P, int t, const double* x, const double* u, double* A, double* B) {
+  (void)P; (void)t;
   dual6 xs[4], us[2], out[4];
   for (int i = 0; i < 4; ++i) { xs[i] = dc(x[i]); xs[i].d[i] = 1.0; }
   for (int i = 0; i < 2; ++i) { us[i] = dc(u[i]); us[i].d[4 + i] = 1.0; }
@@ -278,9 +280,9 @@ static void tl_lin(const prob_t* P, const double* x, const double* u, double* A,
   }
 }
 /* ℓ = Σ(θ*−θ)²·1 + Σu²·1 (:82-97): exact gradient/Hessian */
-static void tl_quad(const prob_t* P, const double* x, const double* u, double* qv, double* r,
-                    double* Q, double* Pm, double* R) {
-  (void)P;
+static void tl_quad(const prob_t* P, int t, const double* x, const double* u, double* qv,
+                    double* r, double* Q, double* Pm, double* R) {
+  (void)P; (void)t;
   memset(Q, 0, sizeof(double) * 16);
   memset(Pm, 0, sizeof(double) * 8);
   memset(R, 0, sizeof(double) * 4);
@@ -313,8 +315,34 @@ static double tl_fcost(const prob_t* P, const double* x) {
 }
 static prob_t tl_problem(int T) {
   tl_init();
-  prob_t P = {4, 2, T, NULL, NULL, NULL, NULL, NULL, tl_lin, tl_quad, tl_fquad, tl_dyn, tl_cost, tl_fcost};
+  prob_t P = {4, 2, T, NULL, NULL, NULL, NULL, NULL, NULL, tl_lin, tl_quad, tl_fquad, tl_dyn, tl_cost, tl_fcost};
   return P;
+}
+
+/* -- TILES family: the derivative calls' results supplied per step by the caller --
+ * tiles[0..8] = A (T,n,n), B (T,n,m), lx (T,n), lu (T,m), lxx (T,n,n), lux (T,m,n) or
+ * NULL, luu (T,m,m), lfx (n), lfxx (n,n) of this trajectory. */
+static void tiles_lin(const prob_t* P, int t, const double* x, const double* u, double* A, double* B) {
+  (void)x; (void)u;
+  const int n = P->n, m = P->m;
+  memcpy(A, P->tiles[0] + (size_t)t * n * n, sizeof(double) * n * n);
+  memcpy(B, P->tiles[1] + (size_t)t * n * m, sizeof(double) * n * m);
+}
+static void tiles_quad(const prob_t* P, int t, const double* x, const double* u, double* qv,
+                       double* r, double* Q, double* Pm, double* R) {
+  (void)x; (void)u;
+  const int n = P->n, m = P->m;
+  memcpy(qv, P->tiles[2] + (size_t)t * n, sizeof(double) * n);
+  memcpy(r, P->tiles[3] + (size_t)t * m, sizeof(double) * m);
+  memcpy(Q, P->tiles[4] + (size_t)t * n * n, sizeof(double) * n * n);
+  if (P->tiles[5]) memcpy(Pm, P->tiles[5] + (size_t)t * m * n, sizeof(double) * m * n);
+  else memset(Pm, 0, sizeof(double) * m * n);
+  memcpy(R, P->tiles[6] + (size_t)t * m * m, sizeof(double) * m * m);
+}
+static void tiles_fquad(const prob_t* P, const double* x, double* s, double* S) {
+  (void)x;
+  memcpy(s, P->tiles[7], sizeof(double) * P->n);
+  memcpy(S, P->tiles[8], sizeof(double) * P->n * P->n);
 }
 
 /* backward_pass (backward_pass.jl:324-357) for one trajectory. Returns 1 if NaN. */
@@ -332,8 +360,8 @@ static int backward_one(const prob_t* P, const double* x, const double* u, doubl
   for (int t = T - 1; t >= 0; --t) { /* :339 */
     const double* xt = x + (size_t)t * n;
     const double* ut = u + (size_t)t * m;
-    P->lin(P, xt, ut, A, Bm);                 /* linearize_dynamics (:25-40) */
-    P->quad(P, xt, ut, qv, r, Qs, Pm, Rs);     /* immediate_cost_quadratization (:81-109) */
+    P->lin(P, t, xt, ut, A, Bm);              /* linearize_dynamics (:25-40) */
+    P->quad(P, t, xt, ut, qv, r, Qs, Pm, Rs);  /* immediate_cost_quadratization (:81-109) */
     /* optimal_controller_param (:177-186) */
     matTvec(n, m, Bm, s, g);                   /* Bᵀ s */
     for (int i = 0; i < m; ++i) g[i] += r[i];  /* g = r + Bᵀ s */
@@ -426,7 +454,7 @@ static int forward_one(const prob_t* P, const double* x, const double* u, const 
 static prob_t instance(int b, int n, int m, int T, const double* A, const double* Bm,
                        const double* Q, const double* R, const double* Qf) {
   prob_t P = {n, m, T, A + (size_t)b * n * n, Bm + (size_t)b * n * m, Q + (size_t)b * n * n,
-              R + (size_t)b * m * m, Qf + (size_t)b * n * n,
+              R + (size_t)b * m * m, Qf + (size_t)b * n * n, NULL,
               lq_lin, lq_quad, lq_fquad, lq_dyn, lq_cost, lq_fcost};
   return P;
 }
@@ -587,4 +615,30 @@ int oracle_tl_fit(int Bn, int T, const double* x_init, const double* u_init, con
             sym, max_trials, x_out + b * xs, u_out + b * us, &cost[b], iters ? &iters[b] : NULL,
             status ? &status[b] : NULL);
   return 0;
+}
+
+/* backward_pass on caller-supplied tiles (ilqr_backward_tiles' checker). x/u are
+ * only used for their shapes; the tiles carry everything. */
+int oracle_tiles_backward(int Bn, int T, int n, int m, const double* A, const double* Bm,
+                          const double* lx, const double* lu, const double* lxx, const double* lux,
+                          const double* luu, const double* lfx, const double* lfxx, double mu,
+                          int sym, double* d, double* K, int* status, int nthreads) {
+  if (n > NMAX || m > MMAX) return -1;
+  set_threads(nthreads);
+  int nans = 0;
+  double* dummy = (double*)calloc((size_t)(T + 1) * (n > m ? n : m), sizeof(double));
+#pragma omp parallel for schedule(static) reduction(+ : nans)
+  for (int b = 0; b < Bn; ++b) {
+    const size_t bt = (size_t)b * T;
+    const double* tl[9] = {A + bt * n * n, Bm + bt * n * m, lx + bt * n, lu + bt * m,
+                           lxx + bt * n * n, lux ? lux + bt * m * n : NULL, luu + bt * m * m,
+                           lfx + (size_t)b * n, lfxx + (size_t)b * n * n};
+    prob_t P = {n, m, T, NULL, NULL, NULL, NULL, NULL, tl, tiles_lin, tiles_quad, tiles_fquad,
+                NULL, NULL, NULL};
+    const int bad = backward_one(&P, dummy, dummy, mu, sym, d + bt * m, K + bt * m * n);
+    if (status) status[b] = bad ? 4 : 0;
+    nans += bad;
+  }
+  free(dummy);
+  return nans;
 }

@@ -26,6 +26,7 @@ case $WHAT in
        step pmc_write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run -- python bench.py --steps 5 --warmup 1 --no-cpu
        python profiles/collect_pmc.py gpurun_out/pmc_fetch gpurun_out/pmc_write gpurun_out/pmc.json > gpurun_out/pmc_summary.log 2>&1 ;;
   tl) step pytest_twolink 600 python -m pytest tests/test_gpu_twolink.py -x -q ;;
+  tiles) step pytest_tiles 600 python -m pytest tests/test_gpu_tiles.py -x -q ;;
   tlbench) step bench_twolink 300 python tools/bench_twolink.py ;;
   tlprof) step rocprof_twolink 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_tl -o run --output-format csv -- python tools/bench_twolink.py --steps 20 --warmup 2 --no-cpu ;;
   rcp) step rcp 60 ./tools/rcp_test ;;
