@@ -17,8 +17,8 @@
 // Mapping:
 //  * tl_linearize: one lane per (trajectory, time step) — the only part of the
 //    backward pass that is parallel in time, and the FLOP-heavy one (≈3 kFLOP/step).
-//    Writes J = [A | B] to a [b][t][24] workspace: each lane of the sequential pass
-//    then reads its step's 192 contiguous bytes with six 16-byte loads.
+//    Writes J = [A | B] (+ θ, u) to a [b][t][28] workspace: each lane of the
+//    sequential pass then reads its step's 224 contiguous bytes with 16-byte loads.
 //  * tl_backward: one lane per trajectory, the Riccati recursion in registers with
 //    the same exact step_back rewrite as the LQ kernels
 //    ([S s] = [Qxx | lx+Aᵀs] − Kᵀ((H+2μI)[K|d]); S computed as its upper triangle
@@ -40,6 +40,9 @@ namespace {
 constexpr int TL_NX = 4;
 constexpr int TL_NU = 2;
 constexpr int TL_NJ = TL_NX * (TL_NX + TL_NU);  // 24 entries of [A | B] per step
+constexpr int TL_NJR = TL_NJ + 4;                // + θ₁, θ₂, u₁, u₂: the backward's whole input
+constexpr int TL_BW_PF = 2;                      // backward prefetch depth (steps)
+constexpr int TL_FW_PF = 2;                      // forward prefetch depth (steps)
 
 // ---------------------------------------------------------------------------
 // sin and cos together: Cody-Waite reduction by π/2 (three-part constant, exact
@@ -271,16 +274,22 @@ __global__ __launch_bounds__(256) void tl_linearize_kernel(TwoLinkParams P, int 
 #pragma unroll
   for (int i = 0; i < 2; ++i) us[i] = seed<6>(ub[i], 4 + i);
   rk4(P, xs, us, out);
-  double2* Jt = reinterpret_cast<double2*>(J + ((size_t)b * T + t) * TL_NJ);
+  double2* Jt = reinterpret_cast<double2*>(J + ((size_t)b * T + t) * TL_NJR);
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
 #pragma unroll
     for (int k = 0; k < 6; k += 2) Jt[(i * 6 + k) / 2] = make_double2(out[i].d[k], out[i].d[k + 1]);
   }
+  Jt[TL_NJ / 2] = make_double2(xb[0], xb[1]);
+  Jt[TL_NJ / 2 + 1] = make_double2(ub[0], ub[1]);
 }
 
 // ---------------------------------------------------------------------------
 // Riccati recursion (src/backward_pass.jl:324-357), one lane per trajectory.
+struct TLBwIn {
+  double F[TL_NJ];  // [A | B], row-major 4×6
+  double th0, th1, u0, u1;
+};
 // Returns true if δu or K holds a NaN (the reference's @assert at :353-354).
 // ---------------------------------------------------------------------------
 __device__ bool tl_backward_lane(const TwoLinkParams& P, int b, int B, int T,
@@ -288,7 +297,6 @@ __device__ bool tl_backward_lane(const TwoLinkParams& P, int b, int B, int T,
                                  const double* __restrict__ J, double* __restrict__ dg,
                                  double* __restrict__ Kg, double mu) {
   const double* xb = x + (size_t)b * (T + 1) * TL_NX;
-  const double* ub = u + (size_t)b * T * TL_NU;
   // final_cost_quadratization (:134-153): ∇ℓ_f = [2(θ−θ*), 0, 0], ∇²ℓ_f = diag(2,2,0,0)
   double S[4][4] = {};
   double s[4];
@@ -300,23 +308,23 @@ __device__ bool tl_backward_lane(const TwoLinkParams& P, int b, int B, int T,
   s[3] = 0.0;
   bool bad = false;
 
-  double F[TL_NJ];  // [A | B] of the step being processed, row-major 4×6
-  const double* Jb = J + (size_t)b * T * TL_NJ;
-  auto loadJ = [&](int t, double (&f)[TL_NJ]) {
-    const double2* Jt = reinterpret_cast<const double2*>(Jb + (size_t)t * TL_NJ);
+  const double* Jb = J + (size_t)b * T * TL_NJR;
+  // one step's record: [A | B] (24) then θ₁, θ₂, u₁, u₂ — 14 16-byte loads
+  auto load = [&](int t, TLBwIn& in) {
+    const double2* Jt = reinterpret_cast<const double2*>(Jb + (size_t)(t > 0 ? t : 0) * TL_NJR);
 #pragma unroll
     for (int k = 0; k < TL_NJ / 2; ++k) {
       const double2 v = Jt[k];
-      f[2 * k] = v.x;
-      f[2 * k + 1] = v.y;
+      in.F[2 * k] = v.x;
+      in.F[2 * k + 1] = v.y;
     }
+    const double2 th = Jt[TL_NJ / 2], uu = Jt[TL_NJ / 2 + 1];
+    in.th0 = th.x;
+    in.th1 = th.y;
+    in.u0 = uu.x;
+    in.u1 = uu.y;
   };
-  loadJ(T - 1, F);
-  for (int t = T - 1; t >= 0; --t) {
-    double Fn[TL_NJ];
-    loadJ(t > 0 ? t - 1 : 0, Fn);  // prefetch the next (earlier) step
-    const double th0 = xb[(size_t)t * TL_NX + 0], th1 = xb[(size_t)t * TL_NX + 1];
-    const double u0 = ub[(size_t)t * TL_NU + 0], u1 = ub[(size_t)t * TL_NU + 1];
+  auto step = [&](int t, const TLBwIn& in) {
     // immediate_cost_quadratization (:81-109): lx = [2(θ−θ*), 0, 0], lu = 2u,
     // lxx = diag(2,2,0,0), luu = 2I, lux = 0
     // Y = S·F (4×6) and sF = sᵀF (1×6)
@@ -327,7 +335,7 @@ __device__ bool tl_backward_lane(const TwoLinkParams& P, int b, int B, int T,
       for (int k = 0; k < 6; ++k) {
         double acc = 0.0;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc = fma(S[i][j], F[j * 6 + k], acc);
+        for (int j = 0; j < 4; ++j) acc = fma(S[i][j], in.F[j * 6 + k], acc);
         Y[i][k] = acc;
       }
     }
@@ -335,14 +343,14 @@ __device__ bool tl_backward_lane(const TwoLinkParams& P, int b, int B, int T,
     for (int k = 0; k < 6; ++k) {
       double acc = 0.0;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc = fma(s[j], F[j * 6 + k], acc);
+      for (int j = 0; j < 4; ++j) acc = fma(s[j], in.F[j * 6 + k], acc);
       sF[k] = acc;
     }
     // Z = FᵀY: Qxx = lxx + AᵀSA (upper), G = BᵀSA (2×4), H = luu + BᵀSB (2×2)
     auto Z = [&](int a, int c) {
       double acc = 0.0;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc = fma(F[j * 6 + a], Y[j][c], acc);
+      for (int j = 0; j < 4; ++j) acc = fma(in.F[j * 6 + a], Y[j][c], acc);
       return acc;
     };
     double G[2][4], H[2][2], g[2];
@@ -355,8 +363,8 @@ __device__ bool tl_backward_lane(const TwoLinkParams& P, int b, int B, int T,
     H[0][1] = Z(4, 5);
     H[1][1] = 2.0 + Z(5, 5);
     H[1][0] = H[0][1];
-    g[0] = 2.0 * u0 + sF[4];  // optimal_controller_param (:181): g = lu + Bᵀs
-    g[1] = 2.0 * u1 + sF[5];
+    g[0] = 2.0 * in.u0 + sF[4];  // optimal_controller_param (:181): g = lu + Bᵀs
+    g[1] = 2.0 * in.u1 + sF[5];
     // feedback_parameters (:207-218): (H + μI)⁻¹ by LDLᵀ; δu = −H⁻¹g, K = −H⁻¹G
     const double h00 = H[0][0] + mu, h01 = H[0][1], h11 = H[1][1] + mu;
     const double iD0 = 1.0 / h00;
@@ -405,8 +413,8 @@ __device__ bool tl_backward_lane(const TwoLinkParams& P, int b, int B, int T,
         Sn[j][i] = acc;
       }
       double acc = sF[i];
-      if (i == 0) acc += -2.0 * (P.tgt0 - th0);
-      if (i == 1) acc += -2.0 * (P.tgt1 - th1);
+      if (i == 0) acc += -2.0 * (P.tgt0 - in.th0);
+      if (i == 1) acc += -2.0 * (P.tgt1 - in.th1);
       acc = fma(-K[0][i], Wd[0], acc);
       acc = fma(-K[1][i], Wd[1], acc);
       sn[i] = acc;
@@ -417,9 +425,22 @@ __device__ bool tl_backward_lane(const TwoLinkParams& P, int b, int B, int T,
 #pragma unroll
       for (int j = 0; j < 4; ++j) S[i][j] = Sn[i][j];
     }
+  };
+  // inputs of the next TL_BW_PF steps in flight (HBM latency ≈ one step's compute)
+  TLBwIn ring[TL_BW_PF];
 #pragma unroll
-    for (int k = 0; k < TL_NJ; ++k) F[k] = Fn[k];
+  for (int k = 0; k < TL_BW_PF; ++k) load(T - 1 - k, ring[k]);
+  int t = T - 1;
+  for (; t >= TL_BW_PF - 1; t -= TL_BW_PF) {
+#pragma unroll
+    for (int k = 0; k < TL_BW_PF; ++k) {
+      step(t - k, ring[k]);
+      load(t - k - TL_BW_PF, ring[k]);
+    }
   }
+#pragma unroll
+  for (int k = 0; k < TL_BW_PF - 1; ++k)
+    if (t - k >= 0) step(t - k, ring[k]);
   return bad;
 }
 
@@ -479,11 +500,7 @@ __device__ TLFwdOut tl_forward_lane(const TwoLinkParams& P, int b, int T,
     }
     double cost = 0.0;
     du2 = 0.0;
-    TLStepIn in;
-    load(0, in);
-    for (int t = 0; t < T; ++t) {
-      TLStepIn nx_in;
-      load(t + 1, nx_in);
+    auto step = [&](int t, const TLStepIn& in) {
       // δx = x̄ₖ − xₖ (:72); ūₖ = uₖ + α δuₖ + Kₖ δx (:73)
       double dx[4];
 #pragma unroll
@@ -509,8 +526,22 @@ __device__ TLFwdOut tl_forward_lane(const TwoLinkParams& P, int b, int T,
       rk4(P, xb, ubar, xn);
 #pragma unroll
       for (int i = 0; i < 4; ++i) xb[i] = xn[i];
-      in = nx_in;
+    };
+    // inputs of the next TL_FW_PF steps in flight (HBM latency ≈ one RK4 step)
+    TLStepIn ring[TL_FW_PF];
+#pragma unroll
+    for (int k = 0; k < TL_FW_PF; ++k) load(k, ring[k]);
+    int t = 0;
+    for (; t + TL_FW_PF <= T; t += TL_FW_PF) {
+#pragma unroll
+      for (int k = 0; k < TL_FW_PF; ++k) {
+        step(t + k, ring[k]);
+        load(t + k + TL_FW_PF, ring[k]);
+      }
     }
+#pragma unroll
+    for (int k = 0; k < TL_FW_PF - 1; ++k)
+      if (t + k < T) step(t + k, ring[k]);
     *reinterpret_cast<double4*>(xo + (size_t)T * TL_NX) = make_double4(xb[0], xb[1], xb[2], xb[3]);
     // final_cost(x̄_N) on the raw state (:192; 2_link_helper_functions.jl:100-108)
     const double f0 = P.tgt0 - xb[0], f1 = P.tgt1 - xb[1];
@@ -629,7 +660,7 @@ TwoLinkParams two_link_params() {
 
 bool tl_supported(int nx, int nu) { return nx == TL_NX && nu == TL_NU; }
 
-size_t tl_workspace_doubles(int B, int T) { return (size_t)T * TL_NJ * B; }
+size_t tl_workspace_doubles(int B, int T) { return (size_t)T * TL_NJR * B; }
 
 static hipError_t launch_linearize(const TwoLinkParams& P, int B, int T, const double* x,
                                    const double* u, const int32_t* status, double* J,
