@@ -96,6 +96,11 @@ ilqr_status enqueue_iteration(ilqr_handle* h, const ilqr_problem* p, const ilqr:
     return ILQR_OK;
   }
   const ilqr::LQParams P = lq_params(p);
+  if (h->nchunks == 1) {  // one stream, no cross-stream events (each hand-off costs ~10 µs)
+    HIP_TRY(ilqr::launch_lq_iter_backward(h->nx, h->nu, P, 0, h->batch, h->T, a, ls.mu, h->stream));
+    HIP_TRY(ilqr::launch_lq_iter_forward(h->nx, h->nu, P, 0, h->batch, h->T, a, ls, h->stream));
+    return ILQR_OK;
+  }
   for (int c = 0; c < h->nchunks; ++c) {
     const int b0 = h->bound[c], b1 = h->bound[c + 1];
     if (chain) HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_fw[c], 0));
@@ -110,7 +115,7 @@ ilqr_status enqueue_iteration(ilqr_handle* h, const ilqr_problem* p, const ilqr:
 }
 
 ilqr_status join(ilqr_handle* h, const ilqr_problem* p) {
-  if (two_link(p)) return ILQR_OK;
+  if (two_link(p) || h->nchunks == 1) return ILQR_OK;
   for (int c = 0; c < h->nchunks; ++c) HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_fw[c], 0));
   return ILQR_OK;
 }

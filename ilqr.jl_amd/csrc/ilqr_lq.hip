@@ -45,7 +45,10 @@ namespace {
 // ---------------------------------------------------------------------------
 // ABL: ablation bits for tools/ablate_bw.hip only (0 in the product): 1 skip the
 // factor/solve, 2 skip symmetrisation, 4 skip the LDS hand-off, 8 skip gain stores,
-// 16 skip the gradient reduction. Ablated variants compute wrong gains.
+// 16 skip the gradient reduction (ablated variants compute wrong gains); variant
+// bits (correct gains): 32 two Newton steps per reciprocal (product: one), 64
+// symmetrise every SYM_EVERY/2 steps, 128 Schur-complement 2×2-block solve instead
+// of LDLᵀ (NU = 4).
 template <int NX, int NU, int ABL = 0>
 __device__ bool lq_backward_wave(const LQParams& P, int b, int T, const double* __restrict__ x,
                                  const double* __restrict__ u, double* __restrict__ d_out,
@@ -213,8 +216,12 @@ __device__ bool lq_backward_wave(const LQParams& P, int b, int T, const double* 
     if constexpr ((ABL & 1) != 0) {
       asm volatile("" ::"v"(h[0][0]), "v"(h[1][0]), "v"(h[2][1]), "v"(h[3][3]));
       xs = col * 1e-3;
+    } else if constexpr ((ABL & 128) != 0 && NU == 4) {
+      Schur4 f;
+      f.factor<(ABL & 32) ? 2 : 1>(h, mu);
+      xs = f.solve(col);
     } else {
-      LDLT<NU> f;
+      LDLT<NU, (ABL & 32) ? 2 : 1> f;
       f.factor(h, mu);
       xs = f.solve(col);
     }
@@ -242,7 +249,7 @@ __device__ bool lq_backward_wave(const LQParams& P, int b, int T, const double* 
     // accumulator tile feeds the next Y MFMA as its own transpose, so rounding
     // asymmetry E evolves as E ← −AᵀEA and grows like ρ(A)^2t on unstable A;
     // a periodic projection bounds it at negligible cost.
-    if ((ABL & 2) == 0 && (t % SYM_EVERY) == 0) {
+    if ((ABL & 2) == 0 && (t % ((ABL & 64) ? SYM_EVERY / 2 : SYM_EVERY)) == 0) {
       double* tile = lds + 96;  // 16 × 17 (padded) doubles
 #pragma unroll
       for (int r = 0; r < 4; ++r) tile[(q + 4 * r) * 17 + c] = Sp[r];

@@ -25,6 +25,15 @@ import math
 import numpy as np
 
 
+def _like(M, x):
+    """M as a tensor on x's device when x is a torch tensor (the callables then also
+    serve the generic closure path, which differentiates them with torch.func)."""
+    if type(x).__module__.startswith("torch"):
+        import torch
+        return torch.as_tensor(M, dtype=x.dtype, device=x.device)
+    return M
+
+
 class LinearDynamics:
     """dynamicsf(x, u) = A x + B u.  A: (nx,nx) or (batch,nx,nx); B likewise."""
 
@@ -35,7 +44,7 @@ class LinearDynamics:
     def __call__(self, x, u):
         if self.A.ndim == 3:
             raise TypeError("batched LinearDynamics: select an instance with .instance(b)")
-        return self.A @ x + self.B @ u
+        return _like(self.A, x) @ x + _like(self.B, x) @ u
 
     def instance(self, b):
         return LinearDynamics(self.A[b], self.B[b]) if self.A.ndim == 3 else self
@@ -59,7 +68,7 @@ class QuadraticCost:
     def __call__(self, x, u):
         if self.Q.ndim == 3:
             raise TypeError("batched QuadraticCost: select an instance with .instance(b)")
-        return x @ (self.Q @ x) + u @ (self.R @ u)
+        return x @ (_like(self.Q, x) @ x) + u @ (_like(self.R, x) @ u)
 
     def instance(self, b):
         return QuadraticCost(self.Q[b], self.R[b]) if self.Q.ndim == 3 else self
@@ -74,7 +83,7 @@ class QuadraticFinalCost:
     def __call__(self, x):
         if self.Qf.ndim == 3:
             raise TypeError("batched QuadraticFinalCost: select an instance with .instance(b)")
-        return x @ (self.Qf @ x)
+        return x @ (_like(self.Qf, x) @ x)
 
     def instance(self, b):
         return QuadraticFinalCost(self.Qf[b]) if self.Qf.ndim == 3 else self

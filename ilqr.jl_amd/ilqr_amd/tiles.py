@@ -27,6 +27,15 @@ def derivative_tiles(x, u, dynamicsf, immediate_cost, final_cost):
     from torch.func import jacfwd, vmap
     nb, N, nx = x.shape
     T, nu = u.shape[1], u.shape[2]
+    try:
+        return _tiles(x, u, dynamicsf, immediate_cost, final_cost, jacfwd, vmap, nb, nx, T, nu)
+    except (TypeError, RuntimeError, ValueError) as e:
+        raise NotImplementedError(
+            "generic closures must be written with torch operations on 1-D tensors "
+            f"(torch.func could not differentiate them: {e})") from e
+
+
+def _tiles(x, u, dynamicsf, immediate_cost, final_cost, jacfwd, vmap, nb, nx, T, nu):
     xs = x[:, :T].reshape(-1, nx)
     us = u.reshape(-1, nu)
     A = vmap(jacfwd(dynamicsf, argnums=0))(xs, us)                      # :32

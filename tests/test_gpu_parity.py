@@ -131,8 +131,12 @@ def test_reference_api_errors(gpu):
         ilqr_amd.backward_pass(g["x"][0][:-1], g["u"][0], f, l, lf)
     with pytest.raises(TypeError):                            # forward_pass.jl:152
         ilqr_amd.fit(g["x"][0], g["u"][0], f, l, lf, max_iter=1e5)
-    with pytest.raises(NotImplementedError):                  # arbitrary closures: no kernel
-        ilqr_amd.backward_pass(g["x"][0], g["u"][0], lambda x, u: x, l, lf)
+    with pytest.raises(NotImplementedError):                  # closures torch.func cannot differentiate
+        ilqr_amd.backward_pass(g["x"][0], g["u"][0], lambda x, u: np.asarray(x), l, lf)
+    # a mixed triple (non-family dynamics, family costs) takes the generic tiles path
+    d, K = ilqr_amd.backward_pass(g["x"][0], g["u"][0], lambda x, u: f(x, u), l, lf)
+    dr, Kr = ilqr_amd.backward_pass(g["x"][0], g["u"][0], f, l, lf)
+    assert rel(d, dr) < 1e-12 and rel(K, Kr) < 1e-12
     with pytest.raises(AssertionError):                       # NaN → AssertionError (:353)
         xbad = g["x"][0].copy()
         xbad[5, 3] = np.nan

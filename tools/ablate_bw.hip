@@ -5,15 +5,22 @@
 #include <cstdio>
 #include <vector>
 #include <random>
+#include <cmath>
 using namespace ilqr;
 template <int ABL>
-__global__ __launch_bounds__(256) void abl_kernel(LQParams P, int B, int T, const double* x, const double* u,
+__global__ __launch_bounds__(256, 4) void abl_kernel(LQParams P, int B, int T, const double* x, const double* u,
                                                   double* d, double* K, int* flag) {
   __shared__ __attribute__((aligned(16))) double lds[WAVES_PER_WG * BW_LDS];
   const int w = threadIdx.x >> 6;
   const int b = blockIdx.x * WAVES_PER_WG + w;
   if (b >= B) return;
-  bool nan = lq_backward_wave<12, 4, ABL>(P, b, T, x, u, d, K, 0.01, lds + w * BW_LDS);
+  // phase-offset experiment (harness only): stagger the 4 waves of a SIMD
+  // (WGs sharing a SIMD are ~256 block indices apart: one wave per SIMD per WG)
+  const int gen = (blockIdx.x >> 8) & 3;
+  if constexpr ((ABL & 256) != 0) { if (gen & 1) __builtin_amdgcn_s_sleep(8); }
+  if constexpr ((ABL & 512) != 0) { if (gen & 1) __builtin_amdgcn_s_sleep(16); }
+  if constexpr ((ABL & 1024) != 0) { for (int i = 0; i < gen; ++i) __builtin_amdgcn_s_sleep(8); }
+  bool nan = lq_backward_wave<12, 4, (ABL & 255)>(P, b, T, x, u, d, K, 0.01, lds + w * BW_LDS);
   if (nan && (threadIdx.x & 63) == 0) atomicAdd(flag, 1);
 }
 #define CK(x) do { hipError_t e=(x); if(e!=hipSuccess){printf("err %s line %d\n",hipGetErrorString(e),__LINE__); return 1;} } while(0)
@@ -43,13 +50,28 @@ int main() {
   LQParams P{up(A), up(Bm), up(Q), up(R), up(Qf)};
   double *xd = up(x), *ud = up(u), *d, *K; int* flag;
   CK(hipMalloc(&d, (size_t)B * T * m * 8)); CK(hipMalloc(&K, (size_t)B * T * m * n * 8)); CK(hipMalloc(&flag, 4));
-  run<0>("full", P, B, T, xd, ud, d, K, flag);
-  run<1>("no factor/solve", P, B, T, xd, ud, d, K, flag);
-  run<2>("no symmetrisation", P, B, T, xd, ud, d, K, flag);
-  run<4>("no LDS hand-off", P, B, T, xd, ud, d, K, flag);
-  run<8>("no K/d stores", P, B, T, xd, ud, d, K, flag);
-  run<16>("no gradient reduction", P, B, T, xd, ud, d, K, flag);
-  run<31>("MFMA chain + selects only", P, B, T, xd, ud, d, K, flag);
-  run<0>("full (again)", P, B, T, xd, ud, d, K, flag);
+  std::vector<double> Kref((size_t)B * T * m * n), Kv(Kref.size());
+  auto diff = [&](const char* name) {
+    CK(hipMemcpy(Kv.data(), K, Kv.size() * 8, hipMemcpyDeviceToHost));
+    double mx = 0, ref = 0;
+    for (size_t i = 0; i < Kv.size(); ++i) { mx = fmax(mx, fabs(Kv[i] - Kref[i])); ref = fmax(ref, fabs(Kref[i])); }
+    printf("%-40s rel diff vs full %.3e\n", name, mx / ref);
+    return 0;
+  };
+  run<0>("product (1 Newton, sym every 8)", P, B, T, xd, ud, d, K, flag);
+  CK(hipMemcpy(Kref.data(), K, Kref.size() * 8, hipMemcpyDeviceToHost));
+  run<96>("2 Newton, sym every 4 (round-1 v4)", P, B, T, xd, ud, d, K, flag); diff("2 Newton, sym every 4");
+  run<128>("Schur block solve", P, B, T, xd, ud, d, K, flag); diff("Schur block solve");
+  for (int rep = 0; rep < 2; ++rep) {
+    printf("-- round %d\n", rep);
+    run<0>("product", P, B, T, xd, ud, d, K, flag);
+    run<96>("2 Newton, sym every 4", P, B, T, xd, ud, d, K, flag);
+    run<1>("no factor/solve", P, B, T, xd, ud, d, K, flag);
+    run<2>("no symmetrisation", P, B, T, xd, ud, d, K, flag);
+    run<4>("no LDS hand-off", P, B, T, xd, ud, d, K, flag);
+    run<8>("no K/d stores", P, B, T, xd, ud, d, K, flag);
+    run<16>("no gradient reduction", P, B, T, xd, ud, d, K, flag);
+    run<31>("MFMA chain + selects only", P, B, T, xd, ud, d, K, flag);
+  }
   return 0;
 }
