@@ -98,8 +98,8 @@ def cpu_baseline(lq, x, u, budget_s):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=300, help="untimed steps: the GPU clock settles after ~0.1 s of load (tools/ablate_bw)")
     ap.add_argument("--batch", type=int, default=4096, help="trajectories per GPU")
     ap.add_argument("--T", type=int, default=100)
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds for the CPU baseline sample")

@@ -9,7 +9,7 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 typedef unsigned u2v __attribute__((ext_vector_type(2)));
 
 constexpr int WAVES_PER_WG = 4;   // trajectories per workgroup
-constexpr int BW_LDS = 96 + 16 * 17;  // doubles of backward scratch per wave: [G|H] rows, g row, zero, S tile
+constexpr int BW_LDS = 96 + 16 * 17 + 64;  // doubles of backward scratch per wave: [G|H] rows, g row, zero, S tile, junk row
 constexpr int SYM_EVERY = 8;          // symmetrise S every this many steps
 
 __device__ __forceinline__ d4 mfma(double a, double b, d4 c) {
@@ -55,6 +55,18 @@ __device__ __forceinline__ void wave_lds_fence() {
 // tools/rcp_test.hip: 0 steps 2.5e8 ulp, 1 step 11 ulp, 2 steps 0 ulp. The LQ
 // backward's pivots use one step (11 ulp ≈ 2.4e-15 relative: far inside the parity
 // tolerances; the factorisation is the kernel's critical path, tools/ablate_bw).
+// 64-bit global store without an exec branch: a raw buffer store whose offset is
+// pushed out of range (dropped by the hardware bounds check) on inactive lanes.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buffer_rsrc(void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(base, 0, (int)bytes, 0x00020000);  // gfx9 dword3
+}
+__device__ __forceinline__ void store_or_drop(double v, __amdgpu_buffer_rsrc_t r, bool ok,
+                                              uint32_t byte_off) {
+  typedef unsigned u2v_ __attribute__((ext_vector_type(2)));
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v_, v), r,
+                                        ok ? byte_off : 0x80000000u, 0, 0);
+}
+
 template <int NEWTON = 2>
 __device__ __forceinline__ double rcp(double x) {
   double r = __builtin_amdgcn_rcp(x);

@@ -48,7 +48,8 @@ namespace {
 // 16 skip the gradient reduction (ablated variants compute wrong gains); variant
 // bits (correct gains): 32 two Newton steps per reciprocal (product: one), 64
 // symmetrise every SYM_EVERY/2 steps, 128 Schur-complement 2×2-block solve instead
-// of LDLᵀ (NU = 4).
+// of LDLᵀ (NU = 4), 256 round-1 gradient (one 4-lane reduction of Lz + Fᵀs after
+// the MFMAs), 512 round-1 gain stores (exec-masked branch).
 template <int NX, int NU, int ABL = 0>
 __device__ bool lq_backward_wave(const LQParams& P, int b, int T, const double* __restrict__ x,
                                  const double* __restrict__ u, double* __restrict__ d_out,
@@ -56,6 +57,7 @@ __device__ bool lq_backward_wave(const LQParams& P, int b, int T, const double* 
   static_assert(NX + NU <= 16 && NX < 16 && NU <= 4, "MFMA tile mapping needs nx+nu <= 16, nu <= 4");
   constexpr int KS = (NX + 3) / 4;  // k-steps of 4 over the state dimension
   constexpr int SROW = NX;          // row/column of Sp holding s
+  b = __builtin_amdgcn_readfirstlane(b);  // one trajectory per wave: keep its pointers scalar
   const int l = threadIdx.x & 63;
   const int c = l & 15;
   const int q = l >> 4;
@@ -154,6 +156,10 @@ __device__ bool lq_backward_wave(const LQParams& P, int b, int T, const double* 
   d4 zc = load_z(T - 1);
   double* Kb = K_out + (size_t)b * T * NU * NX;
   double* db = d_out + (size_t)b * T * NU;
+  // gains go out through raw buffer stores (inactive lanes dropped, no exec branch)
+  const auto rK = buffer_rsrc(Kb, (uint32_t)(T * NU * NX * 8));
+  const auto rD = buffer_rsrc(db, (uint32_t)(T * NU * 8));
+  constexpr int JUNK = 96 + 16 * 17;  // LDS row the lanes without a g value write to
 
   for (int t = T - 1; t >= 0; --t) {
     const d4 zn = load_z(t > 0 ? t - 1 : 0);
@@ -167,14 +173,25 @@ __device__ bool lq_backward_wave(const LQParams& P, int b, int T, const double* 
 #pragma unroll
     for (int kk = 0; kk < KS; ++kk) Z = mfma(fB[kk], Y[kk], Z);
 
-    // gq[c] = (L z)[c] + (Fᵀ s)[c]: lx + Aᵀs (c < NX), g = lu + Bᵀs (c ≥ NX)  (:181, :269)
-    double part = 0.0;
+    // gq[c] = (L z)[c] + (Fᵀ s)[c]: lx + Aᵀs (c < NX), g = lu + Bᵀs (c ≥ NX)  (:181, :269).
+    // (L z)[c] does not depend on the recursion: its 4-lane reduction overlaps the
+    // MFMAs; (Fᵀ s)[c] = Y[SROW][c] sits in lane q = SROW%4 only, which alone
+    // publishes g (the other lanes write a junk LDS row), so no reduction waits on Y.
+    double gq;
+    if constexpr ((ABL & 256) != 0) {
+      double part = 0.0;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      part = fma(Lc[r], zc[r], part);
-      if (r == SROW / 4) part += (q == SROW % 4) ? Y[r] : 0.0;
+      for (int r = 0; r < 4; ++r) {
+        part = fma(Lc[r], zc[r], part);
+        if (r == SROW / 4) part += (q == SROW % 4) ? Y[r] : 0.0;
+      }
+      gq = (ABL & 16) ? part : colsum4(part);
+    } else {
+      double part = 0.0;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) part = fma(Lc[r], zc[r], part);
+      gq = ((ABL & 16) ? part : colsum4(part)) + Y[SROW / 4];  // exact in lane q = SROW%4
     }
-    const double gq = (ABL & 16) ? part : colsum4(part);
 
     // hand the NU rows [G | H] and g to every lane
 #pragma unroll
@@ -182,7 +199,10 @@ __device__ bool lq_backward_wave(const LQParams& P, int b, int T, const double* 
       const int i = q + 4 * r;
       if (i >= NX && i < NX + NU) Gl[(i - NX) * 16 + c] = Z[r];
     }
-    gl[c] = gq;  // the four lanes of column c hold the same value
+    if constexpr ((ABL & 256) != 0)
+      gl[c] = gq;  // the four lanes of column c hold the same value
+    else
+      lds[(q == SROW % 4) ? 64 + c : JUNK + l] = gq;
     double h[NU][NU];
     d4 col = {0.0, 0.0, 0.0, 0.0};
     double colq;
@@ -229,9 +249,13 @@ __device__ bool lq_backward_wave(const LQParams& P, int b, int T, const double* 
     const double wk = (q < NU) ? fma(mu, kq, -colq) : 0.0;   // ((H + 2μI) K_aug)[q][c]
     nan |= __builtin_isnan(kq);
 
-    if constexpr ((ABL & 8) == 0) {
+    if constexpr ((ABL & 8) != 0) {
+    } else if constexpr ((ABL & 512) != 0) {
       double* dst = cx ? Kb + ((size_t)t * NU + qq) * NX + c : db + (size_t)t * NU + qq;
       if (q < NU && c <= SROW) *dst = kq;
+    } else {
+      store_or_drop(kq, rK, q < NU && cx, (uint32_t)(((t * NU + qq) * NX + ci) * 8));
+      store_or_drop(kq, rD, q < NU && c == SROW, (uint32_t)((t * NU + qq) * 8));
     }
 
     // step_back (:269-270): Sp ← [Qxx | lx + Aᵀs] − K_augᵀ (H + 2μI) K_aug

@@ -17,10 +17,8 @@ __global__ __launch_bounds__(256, 4) void abl_kernel(LQParams P, int B, int T, c
   // phase-offset experiment (harness only): stagger the 4 waves of a SIMD
   // (WGs sharing a SIMD are ~256 block indices apart: one wave per SIMD per WG)
   const int gen = (blockIdx.x >> 8) & 3;
-  if constexpr ((ABL & 256) != 0) { if (gen & 1) __builtin_amdgcn_s_sleep(8); }
-  if constexpr ((ABL & 512) != 0) { if (gen & 1) __builtin_amdgcn_s_sleep(16); }
-  if constexpr ((ABL & 1024) != 0) { for (int i = 0; i < gen; ++i) __builtin_amdgcn_s_sleep(8); }
-  bool nan = lq_backward_wave<12, 4, (ABL & 255)>(P, b, T, x, u, d, K, 0.01, lds + w * BW_LDS);
+  if constexpr ((ABL & 4096) != 0) { for (int i = 0; i < gen; ++i) __builtin_amdgcn_s_sleep(8); }
+  bool nan = lq_backward_wave<12, 4, (ABL & 4095)>(P, b, T, x, u, d, K, 0.01, lds + w * BW_LDS);
   if (nan && (threadIdx.x & 63) == 0) atomicAdd(flag, 1);
 }
 #define CK(x) do { hipError_t e=(x); if(e!=hipSuccess){printf("err %s line %d\n",hipGetErrorString(e),__LINE__); return 1;} } while(0)
@@ -58,14 +56,17 @@ int main() {
     printf("%-40s rel diff vs full %.3e\n", name, mx / ref);
     return 0;
   };
-  run<0>("product (1 Newton, sym every 8)", P, B, T, xd, ud, d, K, flag);
+  run<0>("product", P, B, T, xd, ud, d, K, flag);
   CK(hipMemcpy(Kref.data(), K, Kref.size() * 8, hipMemcpyDeviceToHost));
-  run<96>("2 Newton, sym every 4 (round-1 v4)", P, B, T, xd, ud, d, K, flag); diff("2 Newton, sym every 4");
-  run<128>("Schur block solve", P, B, T, xd, ud, d, K, flag); diff("Schur block solve");
+  run<768>("round-1 gradient + stores", P, B, T, xd, ud, d, K, flag); diff("round-1 gradient + stores");
+  run<768 + 96>("round-1 v4 (2 Newton, sym 4)", P, B, T, xd, ud, d, K, flag); diff("round-1 v4");
   for (int rep = 0; rep < 2; ++rep) {
     printf("-- round %d\n", rep);
     run<0>("product", P, B, T, xd, ud, d, K, flag);
-    run<96>("2 Newton, sym every 4", P, B, T, xd, ud, d, K, flag);
+    run<256>("round-1 gradient", P, B, T, xd, ud, d, K, flag);
+    run<512>("round-1 stores", P, B, T, xd, ud, d, K, flag);
+    run<768>("round-1 gradient + stores", P, B, T, xd, ud, d, K, flag);
+    run<768 + 96>("round-1 v4 (2 Newton, sym 4)", P, B, T, xd, ud, d, K, flag);
     run<1>("no factor/solve", P, B, T, xd, ud, d, K, flag);
     run<2>("no symmetrisation", P, B, T, xd, ud, d, K, flag);
     run<4>("no LDS hand-off", P, B, T, xd, ud, d, K, flag);

@@ -36,8 +36,8 @@ def timed(fn, n, stream):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=500)
     ap.add_argument("--batch", type=int, default=1024)
     ap.add_argument("--T", type=int, default=50)
     ap.add_argument("--cpu-budget", type=float, default=10.0)

@@ -18,8 +18,8 @@ for WHAT in "$@"; do
 case $WHAT in
   test) step pytest_gpu 600 python -m pytest tests -m gpu -x -q
         step smoke 180 python -c "import __graft_entry__ as g; g.smoke()" ;;
-  bench) step bench 300 python bench.py --steps 20 --warmup 3 ;;
-  prof) step rocprof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu ;;
+  bench) step bench 300 python bench.py ;;
+  prof) step rocprof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 50 --warmup 300 --no-cpu ;;
   ablate) step ablate 120 ./tools/ablate_bw ;;
   dist2) ILQR_DIST_BACKEND=gloo step dist2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 2 --steps 5 --warmup 1 --no-cpu ;;
   pmc) step pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- python bench.py --steps 5 --warmup 1 --no-cpu
