@@ -177,6 +177,7 @@ int ilqr_supported(int32_t kind, int nx, int nu) {
   if (kind == ILQR_PROBLEM_LQ) return ilqr::lq_supported(nx, nu) ? 1 : 0;
   if (kind == ILQR_PROBLEM_TWO_LINK) return ilqr::tl_supported(nx, nu) ? 1 : 0;
   if (kind == ILQR_PROBLEM_TILES) return ilqr::tiles_supported(nx, nu) ? 1 : 0;
+  if (kind == ILQR_PROBLEM_CHAIN) return (nx % 2 == 0) ? ilqr_chain_supported(nx / 2, nu) : 0;
   return 0;
 }
 

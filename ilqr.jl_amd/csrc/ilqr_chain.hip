@@ -1,0 +1,1305 @@
+// MI355X (gfx950) kernels + C ABI of the RBD problem family (ILQR_PROBLEM_CHAIN):
+// a fixed-base serial chain of revolute joints described by a URDF — the
+// reference's RigidBodyDynamics.jl example (test/RBD_2_link_example/
+// RBD_helper_functions.jl:48-116 on test/urdf/2Dof_arm.urdf; BASELINE.json
+// config 5) with a fixed base.
+//
+// What replaces what:
+//  * dynamicsf (:48-79): RK4 of v̇ = M(q) \ (τ − dynamics_bias(q, v)), q̇ = v. The
+//    device functor is Featherstone's recursive Newton-Euler (the published
+//    algorithm behind RBD.jl's dynamics_bias) for the bias, and M's columns from the
+//    same recursion with unit accelerations; everything templated on the scalar
+//    (float / double / DualT<N, ·>).
+//  * linearize_dynamics (src/backward_pass.jl:25-40, ForwardDiff): forward-mode dual
+//    numbers (ILQR_LINEARIZE_DUAL, exact like the reference) or central finite
+//    differences (ILQR_LINEARIZE_CENTRAL_FD, what BASELINE config 5 names), one lane
+//    per (trajectory, step).
+//  * immediate_cost / final_cost (:85-116) on the joint rows: Σ qwᵢ(θ*ᵢ−θᵢ)² + Σ rwₖuₖ²
+//    and Σ qfwᵢ(θ*ᵢ−θᵢ)²; their derivatives are the exact constants.
+//  * backward_pass / forward_pass / fit: lane-per-trajectory Riccati recursion and
+//    RK4 rollout + α-halving line search, in the handle's dtype (fp32 or fp64).
+// Layout as the other families (include/ilqr.h): x (B, T+1, nx), u/d (B, T, nu),
+// K (B, T, nu, nx), trajectory slowest, nx = 2·n_joints.
+#include <hip/hip_runtime.h>
+#include <math.h>
+
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <type_traits>
+#include <vector>
+
+#include "../../include/ilqr.h"
+#include "ilqr_internal.h"
+#include "ilqr_math.h"
+
+namespace ilqr {
+namespace {
+
+// ---------------------------------------------------------------------------
+// scalar helpers
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void vsincos(float x, float& s, float& c) { fast_sincosf(x, s, c); }
+__device__ __forceinline__ void vsincos(double x, double& s, double& c) { fast_sincos(x, s, c); }
+
+// Forward-mode dual number over value type V (ForwardDiff.Dual restated).
+template <int N, class V>
+struct DualT {
+  V v;
+  V d[N];
+  DualT() = default;
+  __device__ __forceinline__ DualT(V c) : v(c) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) d[i] = V(0);
+  }
+};
+template <int N, class V>
+__device__ __forceinline__ DualT<N, V> operator+(const DualT<N, V>& a, const DualT<N, V>& b) {
+  DualT<N, V> r;
+  r.v = a.v + b.v;
+#pragma unroll
+  for (int i = 0; i < N; ++i) r.d[i] = a.d[i] + b.d[i];
+  return r;
+}
+template <int N, class V>
+__device__ __forceinline__ DualT<N, V> operator-(const DualT<N, V>& a, const DualT<N, V>& b) {
+  DualT<N, V> r;
+  r.v = a.v - b.v;
+#pragma unroll
+  for (int i = 0; i < N; ++i) r.d[i] = a.d[i] - b.d[i];
+  return r;
+}
+template <int N, class V>
+__device__ __forceinline__ DualT<N, V> operator-(const DualT<N, V>& a) {
+  DualT<N, V> r;
+  r.v = -a.v;
+#pragma unroll
+  for (int i = 0; i < N; ++i) r.d[i] = -a.d[i];
+  return r;
+}
+template <int N, class V>
+__device__ __forceinline__ DualT<N, V> operator*(const DualT<N, V>& a, const DualT<N, V>& b) {
+  DualT<N, V> r;
+  r.v = a.v * b.v;
+#pragma unroll
+  for (int i = 0; i < N; ++i) r.d[i] = a.d[i] * b.v + a.v * b.d[i];
+  return r;
+}
+template <int N, class V>
+__device__ __forceinline__ DualT<N, V> operator*(V a, const DualT<N, V>& b) {
+  DualT<N, V> r;
+  r.v = a * b.v;
+#pragma unroll
+  for (int i = 0; i < N; ++i) r.d[i] = a * b.d[i];
+  return r;
+}
+template <int N, class V>
+__device__ __forceinline__ DualT<N, V> operator*(const DualT<N, V>& b, V a) { return a * b; }
+template <int N, class V>
+__device__ __forceinline__ DualT<N, V> operator+(V a, const DualT<N, V>& b) {
+  DualT<N, V> r = b;
+  r.v = a + b.v;
+  return r;
+}
+template <int N, class V>
+__device__ __forceinline__ DualT<N, V> operator-(V a, const DualT<N, V>& b) {
+  DualT<N, V> r = -b;
+  r.v = a - b.v;
+  return r;
+}
+template <int N, class V>
+__device__ __forceinline__ DualT<N, V> operator/(V a, const DualT<N, V>& b) {
+  DualT<N, V> r;  // (a/b)' = −(a/b) b'/b
+  r.v = a / b.v;
+  const V k = -r.v / b.v;
+#pragma unroll
+  for (int i = 0; i < N; ++i) r.d[i] = k * b.d[i];
+  return r;
+}
+template <int N, class V>
+__device__ __forceinline__ void scs(const DualT<N, V>& a, DualT<N, V>& s, DualT<N, V>& c) {
+  V sv, cv;
+  vsincos(a.v, sv, cv);
+  s.v = sv;
+  c.v = cv;
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    s.d[i] = cv * a.d[i];
+    c.d[i] = -sv * a.d[i];
+  }
+}
+__device__ __forceinline__ void scs(float a, float& s, float& c) { vsincos(a, s, c); }
+__device__ __forceinline__ void scs(double a, double& s, double& c) { vsincos(a, s, c); }
+
+template <class S> struct ValueOf { using type = S; };
+template <int N, class V> struct ValueOf<DualT<N, V>> { using type = V; };
+
+// ---------------------------------------------------------------------------
+// Chain constants in the kernel's value type (converted from ilqr_chain on the host)
+// ---------------------------------------------------------------------------
+template <class V, int NJ>
+struct ChainK {
+  V R0[NJ][9];  // joint frame → parent body frame, row-major
+  V p[NJ][3];   // joint origin in the parent body frame
+  V ax[NJ][3];  // unit axis (joint = child frame)
+  V m[NJ];
+  V mc[NJ][3];  // m · COM
+  V Io[NJ][9];  // rotational inertia about the body origin
+  V g[3];       // gravity
+  V dt;
+  V tgt[NJ], qw[NJ], rw[NJ], qfw[NJ];  // joint-space cost (RBD_helper_functions.jl:85-116)
+};
+
+template <class S>
+__device__ __forceinline__ void cross3(const S (&a)[3], const S (&b)[3], S (&o)[3]) {
+  o[0] = a[1] * b[2] - a[2] * b[1];
+  o[1] = a[2] * b[0] - a[0] * b[2];
+  o[2] = a[0] * b[1] - a[1] * b[0];
+}
+// a × b with a constant
+template <class S, class V>
+__device__ __forceinline__ void crossc(const V (&a)[3], const S (&b)[3], S (&o)[3]) {
+  o[0] = a[1] * b[2] - a[2] * b[1];
+  o[1] = a[2] * b[0] - a[0] * b[2];
+  o[2] = a[0] * b[1] - a[1] * b[0];
+}
+
+// parent → child coordinates of joint i: w_c = Rot(a, q)ᵀ R0ᵀ w_p (Rodrigues with −sin)
+template <class S, class V, int NJ>
+__device__ __forceinline__ void to_child(const ChainK<V, NJ>& P, int i, const S& c, const S& s,
+                                         const S (&w)[3], S (&o)[3]) {
+  S y[3];
+#pragma unroll
+  for (int r = 0; r < 3; ++r) y[r] = P.R0[i][r] * w[0] + P.R0[i][3 + r] * w[1] + P.R0[i][6 + r] * w[2];
+  S axy[3];
+  crossc(P.ax[i], y, axy);
+  const S ady = P.ax[i][0] * y[0] + P.ax[i][1] * y[1] + P.ax[i][2] * y[2];
+  const S k = (V(1) - c) * ady;
+#pragma unroll
+  for (int r = 0; r < 3; ++r) o[r] = c * y[r] - s * axy[r] + P.ax[i][r] * k;
+}
+// child → parent: w_p = R0 Rot(a, q) w_c
+template <class S, class V, int NJ>
+__device__ __forceinline__ void to_parent(const ChainK<V, NJ>& P, int i, const S& c, const S& s,
+                                          const S (&w)[3], S (&o)[3]) {
+  S axw[3];
+  crossc(P.ax[i], w, axw);
+  const S adw = P.ax[i][0] * w[0] + P.ax[i][1] * w[1] + P.ax[i][2] * w[2];
+  const S k = (V(1) - c) * adw;
+  S y[3];
+#pragma unroll
+  for (int r = 0; r < 3; ++r) y[r] = c * w[r] + s * axw[r] + P.ax[i][r] * k;
+#pragma unroll
+  for (int r = 0; r < 3; ++r) o[r] = P.R0[i][3 * r] * y[0] + P.R0[i][3 * r + 1] * y[1] + P.R0[i][3 * r + 2] * y[2];
+}
+
+// Recursive Newton-Euler: τ = M(q) q̈ + [VEL] C(q, q̇)q̇ + [GRAV] g(q).
+// qd is read only when VEL; qdd[i] is the joint acceleration.
+template <bool VEL, bool GRAV, int NJ, class S, class V>
+__device__ __forceinline__ void rnea(const ChainK<V, NJ>& P, const S (&c)[NJ], const S (&s)[NJ],
+                                     const S (&qd)[NJ], const S (&qdd)[NJ], S (&tau)[NJ]) {
+  S w[3], v[3], al[3], ac[3];
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+    w[r] = S(V(0));
+    v[r] = S(V(0));
+    al[r] = S(V(0));
+    ac[r] = S(GRAV ? -P.g[r] : V(0));  // fictitious base acceleration −g
+  }
+  S fn[NJ][3], ff[NJ][3];
+#pragma unroll
+  for (int i = 0; i < NJ; ++i) {
+    S t[3], u3[3];
+    // spatial motion transform to body i: ω_i = X ω, v_i = X (v − p × ω) (same for accel)
+    S wi[3], vi[3], ali[3], aci[3];
+    to_child(P, i, c[i], s[i], w, wi);
+    crossc(P.p[i], w, t);
+#pragma unroll
+    for (int r = 0; r < 3; ++r) u3[r] = v[r] - t[r];
+    to_child(P, i, c[i], s[i], u3, vi);
+    to_child(P, i, c[i], s[i], al, ali);
+    crossc(P.p[i], al, t);
+#pragma unroll
+    for (int r = 0; r < 3; ++r) u3[r] = ac[r] - t[r];
+    to_child(P, i, c[i], s[i], u3, aci);
+    if constexpr (VEL) {
+      S sq[3];
+#pragma unroll
+      for (int r = 0; r < 3; ++r) sq[r] = P.ax[i][r] * qd[i];  // S q̇
+#pragma unroll
+      for (int r = 0; r < 3; ++r) wi[r] = wi[r] + sq[r];
+      cross3(wi, sq, t);  // (v ×m S q̇): angular part ω × Sq̇, linear part v × Sq̇
+#pragma unroll
+      for (int r = 0; r < 3; ++r) ali[r] = ali[r] + t[r];
+      cross3(vi, sq, t);
+#pragma unroll
+      for (int r = 0; r < 3; ++r) aci[r] = aci[r] + t[r];
+    }
+#pragma unroll
+    for (int r = 0; r < 3; ++r) ali[r] = ali[r] + P.ax[i][r] * qdd[i];
+    // f = I a + v ×f (I v),  I·(α, a) = (Io α + mc × a, m a − mc × α)
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+      fn[i][r] = P.Io[i][3 * r] * ali[0] + P.Io[i][3 * r + 1] * ali[1] + P.Io[i][3 * r + 2] * ali[2];
+    crossc(P.mc[i], aci, t);
+#pragma unroll
+    for (int r = 0; r < 3; ++r) fn[i][r] = fn[i][r] + t[r];
+    crossc(P.mc[i], ali, t);
+#pragma unroll
+    for (int r = 0; r < 3; ++r) ff[i][r] = P.m[i] * aci[r] - t[r];
+    if constexpr (VEL) {
+      S hn[3], hf[3];
+#pragma unroll
+      for (int r = 0; r < 3; ++r)
+        hn[r] = P.Io[i][3 * r] * wi[0] + P.Io[i][3 * r + 1] * wi[1] + P.Io[i][3 * r + 2] * wi[2];
+      crossc(P.mc[i], vi, t);
+#pragma unroll
+      for (int r = 0; r < 3; ++r) hn[r] = hn[r] + t[r];
+      crossc(P.mc[i], wi, t);
+#pragma unroll
+      for (int r = 0; r < 3; ++r) hf[r] = P.m[i] * vi[r] - t[r];
+      cross3(wi, hn, t);
+#pragma unroll
+      for (int r = 0; r < 3; ++r) fn[i][r] = fn[i][r] + t[r];
+      cross3(vi, hf, t);
+#pragma unroll
+      for (int r = 0; r < 3; ++r) fn[i][r] = fn[i][r] + t[r];
+      cross3(wi, hf, t);
+#pragma unroll
+      for (int r = 0; r < 3; ++r) ff[i][r] = ff[i][r] + t[r];
+    }
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      w[r] = wi[r];
+      v[r] = vi[r];
+      al[r] = ali[r];
+      ac[r] = aci[r];
+    }
+  }
+#pragma unroll
+  for (int i = NJ - 1; i >= 0; --i) {
+    tau[i] = P.ax[i][0] * fn[i][0] + P.ax[i][1] * fn[i][1] + P.ax[i][2] * fn[i][2];
+    if (i > 0) {
+      S pf[3], pn[3], t[3];
+      to_parent(P, i, c[i], s[i], ff[i], pf);
+      to_parent(P, i, c[i], s[i], fn[i], pn);
+      crossc(P.p[i], pf, t);
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        fn[i - 1][r] = fn[i - 1][r] + (pn[r] + t[r]);
+        ff[i - 1][r] = ff[i - 1][r] + pf[r];
+      }
+    }
+  }
+}
+
+// [q̇; v̇] with v̇ = M \ (τ − bias)  (RBD_helper_functions.jl:61-66).
+// nu = NJ drives every joint; nu = 1 drives joint 1 only.
+template <int NJ, int NU, class S, class V>
+__device__ __forceinline__ void chain_xdot(const ChainK<V, NJ>& P, const S (&x)[2 * NJ],
+                                           const S (&u)[NU], S (&xd)[2 * NJ]) {
+  S c[NJ], s[NJ];
+#pragma unroll
+  for (int i = 0; i < NJ; ++i) scs(x[i], s[i], c[i]);
+  S zero[NJ], qd[NJ], b[NJ];
+#pragma unroll
+  for (int i = 0; i < NJ; ++i) {
+    zero[i] = S(V(0));
+    qd[i] = x[NJ + i];
+  }
+  rnea<true, true>(P, c, s, qd, zero, b);  // dynamics_bias
+  S M[NJ][NJ];
+#pragma unroll
+  for (int k = 0; k < NJ; ++k) {  // mass_matrix, column k = RNEA(q, 0, e_k)
+    S e[NJ], col[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) e[j] = S(V(j == k ? 1 : 0));
+    rnea<false, false>(P, c, s, zero, e, col);
+#pragma unroll
+    for (int i = 0; i < NJ; ++i) M[i][k] = col[i];
+  }
+  S r[NJ];
+#pragma unroll
+  for (int i = 0; i < NJ; ++i) r[i] = (i < NU ? u[i < NU ? i : 0] : S(V(0))) - b[i];
+  // Gaussian elimination (M is SPD: no pivoting)
+#pragma unroll
+  for (int k = 0; k < NJ; ++k) {
+    const S inv = V(1) / M[k][k];
+#pragma unroll
+    for (int i = k + 1; i < NJ; ++i) {
+      const S l = M[i][k] * inv;
+#pragma unroll
+      for (int j = k + 1; j < NJ; ++j) M[i][j] = M[i][j] - l * M[k][j];
+      r[i] = r[i] - l * r[k];
+    }
+  }
+  S qdd[NJ];
+#pragma unroll
+  for (int i = NJ - 1; i >= 0; --i) {
+    S acc = r[i];
+#pragma unroll
+    for (int j = i + 1; j < NJ; ++j) acc = acc - M[i][j] * qdd[j];
+    qdd[i] = acc * (V(1) / M[i][i]);
+  }
+#pragma unroll
+  for (int i = 0; i < NJ; ++i) {
+    xd[i] = x[NJ + i];
+    xd[NJ + i] = qdd[i];
+  }
+}
+
+// RK4 (RBD_helper_functions.jl:70-78)
+template <int NJ, int NU, class S, class V>
+__device__ __forceinline__ void chain_rk4(const ChainK<V, NJ>& P, const S (&x)[2 * NJ],
+                                          const S (&u)[NU], S (&out)[2 * NJ]) {
+  constexpr int NX = 2 * NJ;
+  S k1[NX], k2[NX], k3[NX], k4[NX], y[NX];
+  const V h = V(0.5);
+  chain_xdot<NJ, NU>(P, x, u, k1);
+#pragma unroll
+  for (int i = 0; i < NX; ++i) {
+    k1[i] = P.dt * k1[i];
+    y[i] = x[i] + h * k1[i];
+  }
+  chain_xdot<NJ, NU>(P, y, u, k2);
+#pragma unroll
+  for (int i = 0; i < NX; ++i) {
+    k2[i] = P.dt * k2[i];
+    y[i] = x[i] + h * k2[i];
+  }
+  chain_xdot<NJ, NU>(P, y, u, k3);
+#pragma unroll
+  for (int i = 0; i < NX; ++i) {
+    k3[i] = P.dt * k3[i];
+    y[i] = x[i] + k3[i];
+  }
+  chain_xdot<NJ, NU>(P, y, u, k4);
+#pragma unroll
+  for (int i = 0; i < NX; ++i) {
+    k4[i] = P.dt * k4[i];
+    out[i] = x[i] + (V(1) / V(6)) * (((k1[i] + V(2) * k2[i]) + V(2) * k3[i]) + k4[i]);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// f(x, u) for n points (a rollout primitive and the dynamics parity test)
+// ---------------------------------------------------------------------------
+template <class V, int NJ, int NU>
+__global__ __launch_bounds__(256) void chain_dynamics_kernel(ChainK<V, NJ> P, int n,
+                                                             const V* __restrict__ x,
+                                                             const V* __restrict__ u,
+                                                             V* __restrict__ xo) {
+  constexpr int NX = 2 * NJ;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  V xs[NX], us[NU], o[NX];
+#pragma unroll
+  for (int k = 0; k < NX; ++k) xs[k] = x[(size_t)i * NX + k];
+#pragma unroll
+  for (int k = 0; k < NU; ++k) us[k] = u[(size_t)i * NU + k];
+  chain_rk4<NJ, NU>(P, xs, us, o);
+#pragma unroll
+  for (int k = 0; k < NX; ++k) xo[(size_t)i * NX + k] = o[k];
+}
+
+// ---------------------------------------------------------------------------
+// Linearisation record per (b, t): [A | B] (NX × (NX+NU), row-major), x_t, u_t
+// ---------------------------------------------------------------------------
+template <int NJ, int NU>
+struct Rec {
+  static constexpr int NX = 2 * NJ;
+  static constexpr int NJAC = NX * (NX + NU);
+  static constexpr int N = NJAC + NX + NU;
+};
+
+template <class V, int NJ, int NU, int LIN>
+__global__ __launch_bounds__(256) void chain_linearize_kernel(ChainK<V, NJ> P, int B, int T,
+                                                              const V* __restrict__ x,
+                                                              const V* __restrict__ u,
+                                                              const int32_t* __restrict__ status,
+                                                              V* __restrict__ J) {
+  constexpr int NX = 2 * NJ, ND = NX + NU, NR = Rec<NJ, NU>::N;
+  const int b = blockIdx.x * 256 + threadIdx.x;
+  const int t = blockIdx.y;
+  if (b >= B || (status && status[b] != ILQR_TRAJ_OK)) return;
+  const V* xb = x + ((size_t)b * (T + 1) + t) * NX;
+  const V* ub = u + ((size_t)b * T + t) * NU;
+  V* Jt = J + ((size_t)b * T + t) * NR;
+  V z[ND];
+#pragma unroll
+  for (int k = 0; k < NX; ++k) z[k] = xb[k];
+#pragma unroll
+  for (int k = 0; k < NU; ++k) z[NX + k] = ub[k];
+  if constexpr (LIN == ILQR_LINEARIZE_DUAL) {
+    // the reference's two ForwardDiff.jacobian calls, two directions per pass (a pass
+    // carrying all ND directions would spill: ≈4.6 KB of scratch per lane)
+    constexpr int DC = 1;
+    using D = DualT<DC, V>;
+#pragma unroll 1
+    for (int k0 = 0; k0 < ND; k0 += DC) {
+      D xs[NX], us[NU], o[NX];
+#pragma unroll
+      for (int k = 0; k < ND; ++k) {
+        D v(z[k]);
+#pragma unroll
+        for (int c = 0; c < DC; ++c) v.d[c] = (k == k0 + c) ? V(1) : V(0);
+        if (k < NX) xs[k] = v; else us[k - NX] = v;
+      }
+      chain_rk4<NJ, NU>(P, xs, us, o);
+#pragma unroll
+      for (int i = 0; i < NX; ++i)
+#pragma unroll
+        for (int c = 0; c < DC; ++c)
+          if (k0 + c < ND) Jt[i * ND + k0 + c] = o[i].d[c];
+    }
+  } else {
+    // central differences, step h = ε^(1/3)·max(1, |z_k|), divided by the step actually taken
+    const V cbe = sizeof(V) == 4 ? V(4.921566e-3) : V(6.0554544523933395e-6);
+#pragma unroll 1
+    for (int k = 0; k < ND; ++k) {
+      const V h = cbe * fmax(V(1), fabs(z[k]));
+      V xp[NX], up[NU], xm[NX], um[NU], fp[NX], fm[NX];
+#pragma unroll
+      for (int j = 0; j < NX; ++j) xp[j] = xm[j] = z[j];
+#pragma unroll
+      for (int j = 0; j < NU; ++j) up[j] = um[j] = z[NX + j];
+      V zp = z[k] + h, zm = z[k] - h;
+#pragma unroll
+      for (int j = 0; j < NX; ++j)
+        if (j == k) { xp[j] = zp; xm[j] = zm; }
+#pragma unroll
+      for (int j = 0; j < NU; ++j)
+        if (NX + j == k) { up[j] = zp; um[j] = zm; }
+      chain_rk4<NJ, NU>(P, xp, up, fp);
+      chain_rk4<NJ, NU>(P, xm, um, fm);
+      const V inv = V(1) / (zp - zm);
+#pragma unroll
+      for (int i = 0; i < NX; ++i) Jt[i * ND + k] = (fp[i] - fm[i]) * inv;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < ND; ++k) Jt[Rec<NJ, NU>::NJAC + k] = z[k];
+}
+
+// record → separate A (B,T,NX,NX), B (B,T,NX,NU) tiles (ilqr_chain_linearize)
+template <class V, int NJ, int NU>
+__global__ __launch_bounds__(256) void chain_unpack_kernel(int B, int T, const V* __restrict__ J,
+                                                           V* __restrict__ A, V* __restrict__ Bm) {
+  constexpr int NX = 2 * NJ, ND = NX + NU, NR = Rec<NJ, NU>::N;
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (size_t)B * T) return;
+  const V* Jt = J + i * NR;
+#pragma unroll
+  for (int r = 0; r < NX; ++r) {
+#pragma unroll
+    for (int k = 0; k < NX; ++k) A[i * NX * NX + r * NX + k] = Jt[r * ND + k];
+#pragma unroll
+    for (int k = 0; k < NU; ++k) Bm[i * NX * NU + r * NU + k] = Jt[r * ND + NX + k];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Riccati recursion (src/backward_pass.jl:324-357), one lane per trajectory
+// ---------------------------------------------------------------------------
+template <class V, int NJ, int NU>
+__device__ bool chain_backward_lane(const ChainK<V, NJ>& P, int b, int T, const V* __restrict__ x,
+                                    const V* __restrict__ J, V* __restrict__ dg,
+                                    V* __restrict__ Kg, V mu) {
+  constexpr int NX = 2 * NJ, ND = NX + NU, NR = Rec<NJ, NU>::N, NJAC = Rec<NJ, NU>::NJAC;
+  const V* xN = x + ((size_t)b * (T + 1) + T) * NX;
+  // final_cost_quadratization (:134-153): ∇ℓ_f = −2 qfw (θ* − θ), ∇²ℓ_f = diag(2 qfw, 0)
+  V S[NX][NX], s[NX];
+#pragma unroll
+  for (int i = 0; i < NX; ++i) {
+#pragma unroll
+    for (int j = 0; j < NX; ++j) S[i][j] = V(0);
+    s[i] = V(0);
+  }
+#pragma unroll
+  for (int i = 0; i < NJ; ++i) {
+    S[i][i] = V(2) * P.qfw[i];
+    s[i] = V(-2) * P.qfw[i] * (P.tgt[i] - xN[i]);
+  }
+  bool bad = false;
+  const V* Jb = J + (size_t)b * T * NR;
+  V rec[2][NR];
+  auto load = [&](int t, V (&r)[NR]) {
+    const V* Jt = Jb + (size_t)(t > 0 ? t : 0) * NR;
+#pragma unroll
+    for (int k = 0; k < NR; ++k) r[k] = Jt[k];
+  };
+  auto step = [&](int t, const V (&F)[NR]) {
+    // Y = S F, sF = sᵀF  (optimal_controller_param :181-183)
+    V Y[NX][ND], sF[ND];
+#pragma unroll
+    for (int i = 0; i < NX; ++i)
+#pragma unroll
+      for (int k = 0; k < ND; ++k) {
+        V acc = V(0);
+#pragma unroll
+        for (int j = 0; j < NX; ++j) acc = fma(S[i][j], F[j * ND + k], acc);
+        Y[i][k] = acc;
+      }
+#pragma unroll
+    for (int k = 0; k < ND; ++k) {
+      V acc = V(0);
+#pragma unroll
+      for (int j = 0; j < NX; ++j) acc = fma(s[j], F[j * ND + k], acc);
+      sF[k] = acc;
+    }
+    auto Z = [&](int a, int c) {
+      V acc = V(0);
+#pragma unroll
+      for (int j = 0; j < NX; ++j) acc = fma(F[j * ND + a], Y[j][c], acc);
+      return acc;
+    };
+    // immediate_cost_quadratization (:81-109): lx = −2qw(θ*−θ), lu = 2 rw u,
+    // lxx = diag(2qw, 0), luu = diag(2rw), lux = 0
+    V G[NU][NX], H[NU][NU], g[NU];
+#pragma unroll
+    for (int a = 0; a < NU; ++a) {
+#pragma unroll
+      for (int c = 0; c < NX; ++c) G[a][c] = Z(NX + a, c);
+#pragma unroll
+      for (int c = 0; c < NU; ++c) H[a][c] = Z(NX + a, NX + c) + (a == c ? V(2) * P.rw[a] : V(0));
+      g[a] = V(2) * P.rw[a] * F[NJAC + NX + a] + sF[NX + a];
+    }
+    // feedback_parameters (:207-218): H + μI = L D Lᵀ (unit lower L); δu = −H⁻¹g, K = −H⁻¹G
+    V L[NU][NU], D[NU], iD[NU];
+#pragma unroll
+    for (int i = 0; i < NU; ++i) {
+#pragma unroll
+      for (int j = 0; j < i; ++j) {
+        V acc = H[i][j];
+#pragma unroll
+        for (int k = 0; k < j; ++k) acc = acc - L[i][k] * L[j][k] * D[k];
+        L[i][j] = acc * iD[j];
+      }
+      V acc = H[i][i] + mu;
+#pragma unroll
+      for (int k = 0; k < i; ++k) acc = acc - L[i][k] * L[i][k] * D[k];
+      D[i] = acc;
+      iD[i] = V(1) / acc;
+    }
+    auto solve = [&](const V (&r)[NU], V (&z)[NU]) {  // z = −(H + μI)⁻¹ r
+      V y[NU], w[NU];
+#pragma unroll
+      for (int i = 0; i < NU; ++i) {
+        V acc = r[i];
+#pragma unroll
+        for (int k = 0; k < i; ++k) acc = acc - L[i][k] * y[k];
+        y[i] = acc;
+      }
+#pragma unroll
+      for (int i = NU - 1; i >= 0; --i) {
+        V acc = y[i] * iD[i];
+#pragma unroll
+        for (int k = i + 1; k < NU; ++k) acc = acc - L[k][i] * w[k];
+        w[i] = acc;
+      }
+#pragma unroll
+      for (int i = 0; i < NU; ++i) z[i] = -w[i];
+    };
+    V K[NU][NX], d[NU];
+#pragma unroll
+    for (int c = 0; c < NX; ++c) {
+      V r[NU], z[NU];
+#pragma unroll
+      for (int a = 0; a < NU; ++a) r[a] = G[a][c];
+      solve(r, z);
+#pragma unroll
+      for (int a = 0; a < NU; ++a) K[a][c] = z[a];
+    }
+    solve(g, d);
+    V* Kt = Kg + ((size_t)b * T + t) * NU * NX;
+    V* dt = dg + ((size_t)b * T + t) * NU;
+#pragma unroll
+    for (int a = 0; a < NU; ++a) {
+      dt[a] = d[a];
+      bad |= d[a] != d[a];
+#pragma unroll
+      for (int c = 0; c < NX; ++c) {
+        Kt[a * NX + c] = K[a][c];
+        bad |= K[a][c] != K[a][c];
+      }
+    }
+    // step_back (:262-273), exact rewrite with W = (H+2μI)[K|d] = −[G|g] + μ[K|d]
+    V WK[NU][NX], Wd[NU];
+#pragma unroll
+    for (int a = 0; a < NU; ++a) {
+#pragma unroll
+      for (int c = 0; c < NX; ++c) WK[a][c] = fma(mu, K[a][c], -G[a][c]);
+      Wd[a] = fma(mu, d[a], -g[a]);
+    }
+    V Sn[NX][NX], sn[NX];
+#pragma unroll
+    for (int i = 0; i < NX; ++i) {
+#pragma unroll
+      for (int j = i; j < NX; ++j) {
+        V acc = Z(i, j);
+        if (i == j && i < NJ) acc += V(2) * P.qw[i];
+#pragma unroll
+        for (int a = 0; a < NU; ++a) acc = fma(-K[a][i], WK[a][j], acc);
+        Sn[i][j] = acc;
+        Sn[j][i] = acc;
+      }
+      V acc = sF[i];
+      if (i < NJ) acc += V(-2) * P.qw[i] * (P.tgt[i] - F[NJAC + i]);
+#pragma unroll
+      for (int a = 0; a < NU; ++a) acc = fma(-K[a][i], Wd[a], acc);
+      sn[i] = acc;
+    }
+#pragma unroll
+    for (int i = 0; i < NX; ++i) {
+      s[i] = sn[i];
+#pragma unroll
+      for (int j = 0; j < NX; ++j) S[i][j] = Sn[i][j];
+    }
+  };
+  load(T - 1, rec[0]);
+  int t = T - 1;
+  for (; t >= 1; t -= 2) {  // one step of prefetch
+    load(t - 1, rec[1]);
+    step(t, rec[0]);
+    load(t - 2, rec[0]);
+    step(t - 1, rec[1]);
+  }
+  if (t == 0) step(0, rec[0]);
+  return bad;
+}
+
+// ---------------------------------------------------------------------------
+// Forward rollout + line search (src/forward_pass.jl:55-93), one lane per trajectory
+// ---------------------------------------------------------------------------
+template <class V>
+struct ChainFwdOut {
+  V cost;
+  int trials;
+  int accepted;
+};
+
+template <class V, int NJ, int NU>
+__device__ ChainFwdOut<V> chain_forward_lane(const ChainK<V, NJ>& P, int b, int T,
+                                             const V* __restrict__ x, const V* __restrict__ u,
+                                             const V* __restrict__ xtraj, const V* __restrict__ dg,
+                                             const V* __restrict__ Kg, V prev_cost,
+                                             V* __restrict__ xnew, V* __restrict__ unew, V* du2_out,
+                                             const LSParams& ls) {
+  constexpr int NX = 2 * NJ;
+  const V* xb0 = x + (size_t)b * (T + 1) * NX;
+  const V* ub0 = u + (size_t)b * T * NU;
+  const V* xt0 = (xtraj ? xtraj : x) + (size_t)b * (T + 1) * NX;
+  const V xtw = xtraj ? V(1) : V(0);  // x_traj = NULL means zeros (forward_pass.jl:151)
+  const V* d0 = dg + (size_t)b * T * NU;
+  const V* K0 = Kg + (size_t)b * T * NU * NX;
+  V* xo = xnew + (size_t)b * (T + 1) * NX;
+  V* uo = unew + (size_t)b * T * NU;
+
+  V alpha = V(ls.alpha0);
+  ChainFwdOut<V> out{V(0), 0, 0};
+  V du2 = V(0);
+  for (int trial = 1; trial <= ls.max_trials; ++trial) {
+    V xb[NX];
+#pragma unroll
+    for (int i = 0; i < NX; ++i) xb[i] = xb0[i];  // x̄₁ = x₁ (:65)
+    V cost = V(0);
+    du2 = V(0);
+    for (int t = 0; t < T; ++t) {
+      const V* xk = xb0 + (size_t)t * NX;
+      const V* xtk = xt0 + (size_t)t * NX;
+      V dx[NX];
+#pragma unroll
+      for (int i = 0; i < NX; ++i) dx[i] = xb[i] - xk[i];  // δx (:72)
+      V ubar[NU];
+#pragma unroll
+      for (int a = 0; a < NU; ++a) {  // ūₖ = uₖ + α δuₖ + Kₖ δx (:73)
+        V kdx = V(0);
+#pragma unroll
+        for (int i = 0; i < NX; ++i) kdx = fma(K0[((size_t)t * NU + a) * NX + i], dx[i], kdx);
+        const V uk = ub0[(size_t)t * NU + a];
+        ubar[a] = fma(alpha, d0[(size_t)t * NU + a], uk) + kdx;
+        const V e = ubar[a] - uk;
+        du2 = fma(e, e, du2);
+      }
+      // ℓ(x̄ₖ − x_trajₖ, ūₖ) (:187-190; RBD_helper_functions.jl:85-99 on the joints)
+      V lk = V(0);
+#pragma unroll
+      for (int i = 0; i < NJ; ++i) {
+        const V e = P.tgt[i] - fma(-xtw, xtk[i], xb[i]);
+        lk = fma(P.qw[i] * e, e, lk);
+      }
+#pragma unroll
+      for (int a = 0; a < NU; ++a) lk = fma(P.rw[a] * ubar[a], ubar[a], lk);
+      cost += lk;
+#pragma unroll
+      for (int i = 0; i < NX; ++i) xo[(size_t)t * NX + i] = xb[i];
+#pragma unroll
+      for (int a = 0; a < NU; ++a) uo[(size_t)t * NU + a] = ubar[a];
+      V xn[NX];
+      chain_rk4<NJ, NU>(P, xb, ubar, xn);  // x̄ₖ₊₁ = f(x̄ₖ, ūₖ) (:74)
+#pragma unroll
+      for (int i = 0; i < NX; ++i) xb[i] = xn[i];
+    }
+#pragma unroll
+    for (int i = 0; i < NX; ++i) xo[(size_t)T * NX + i] = xb[i];
+    // final_cost(x̄_N) on the raw state (:192; RBD_helper_functions.jl:105-116)
+    V lf = V(0);
+#pragma unroll
+    for (int i = 0; i < NJ; ++i) {
+      const V e = P.tgt[i] - xb[i];
+      lf = fma(P.qfw[i] * e, e, lf);
+    }
+    cost += lf;
+    out.trials = trial;
+    out.cost = cost;
+    if (prev_cost - cost > V(0)) {  // (:77-80); NaN compares false → keep searching
+      out.accepted = 1;
+      break;
+    }
+    alpha *= V(ls.shrink);  // (:82)
+  }
+  if (du2_out) *du2_out = du2;
+  return out;
+}
+
+template <class V>
+struct ChainIter {
+  const V* x;
+  const V* u;
+  const V* xtraj;
+  V* xnew;
+  V* unew;
+  V* K;
+  V* d;
+  const V* prev_cost;
+  V* new_cost;
+  V* du2;
+  int32_t* trials;
+  int32_t* status;
+  int32_t* res_parity;
+  int32_t* iters;
+  int parity;
+  int iter;
+};
+
+constexpr int CH_WG = 64;
+
+template <class V, int NJ, int NU>
+__global__ __launch_bounds__(CH_WG) void chain_backward_kernel(ChainK<V, NJ> P, int B, int T,
+                                                               const V* __restrict__ x,
+                                                               const V* __restrict__ J,
+                                                               V* __restrict__ d, V* __restrict__ K,
+                                                               int32_t* __restrict__ status, V mu) {
+  const int b = blockIdx.x * CH_WG + threadIdx.x;
+  if (b >= B) return;
+  const bool nan = chain_backward_lane<V, NJ, NU>(P, b, T, x, J, d, K, mu);
+  if (status) status[b] = nan ? ILQR_TRAJ_NAN : ILQR_TRAJ_OK;
+}
+
+template <class V, int NJ, int NU>
+__global__ __launch_bounds__(CH_WG) void chain_forward_kernel(
+    ChainK<V, NJ> P, int B, int T, const V* __restrict__ x, const V* __restrict__ u,
+    const V* __restrict__ xtraj, const V* __restrict__ d, const V* __restrict__ K,
+    const V* __restrict__ prev_cost, V* __restrict__ xnew, V* __restrict__ unew,
+    V* __restrict__ new_cost, int32_t* __restrict__ trials, int32_t* __restrict__ status,
+    LSParams ls) {
+  constexpr int NX = 2 * NJ;
+  const int b = blockIdx.x * CH_WG + threadIdx.x;
+  if (b >= B) return;
+  const V pc = prev_cost ? prev_cost[b] : V(INFINITY);
+  const ChainFwdOut<V> r =
+      chain_forward_lane<V, NJ, NU>(P, b, T, x, u, xtraj, d, K, pc, xnew, unew, nullptr, ls);
+  if (!r.accepted) {  // exhausted (the reference would loop forever): return the inputs
+    for (int i = 0; i < (T + 1) * NX; ++i) xnew[(size_t)b * (T + 1) * NX + i] = x[(size_t)b * (T + 1) * NX + i];
+    for (int i = 0; i < T * NU; ++i) unew[(size_t)b * T * NU + i] = u[(size_t)b * T * NU + i];
+  }
+  new_cost[b] = r.cost;
+  if (trials) trials[b] = r.trials;
+  if (status) status[b] = r.accepted ? ILQR_TRAJ_OK
+                                     : (r.cost != r.cost ? ILQR_TRAJ_NAN : ILQR_TRAJ_LS_EXHAUSTED);
+}
+
+template <class V, int NJ, int NU>
+__global__ __launch_bounds__(CH_WG) void chain_iter_backward_kernel(ChainK<V, NJ> P, int B, int T,
+                                                                    ChainIter<V> a, const V* J, V mu) {
+  const int b = blockIdx.x * CH_WG + threadIdx.x;
+  if (b >= B || a.status[b] != ILQR_TRAJ_OK) return;
+  if (chain_backward_lane<V, NJ, NU>(P, b, T, a.x, J, a.d, a.K, mu)) {
+    a.status[b] = ILQR_TRAJ_NAN;  // reference: AssertionError at backward_pass.jl:353
+    if (a.res_parity) a.res_parity[b] = a.parity;
+  }
+}
+
+template <class V, int NJ, int NU>
+__global__ __launch_bounds__(CH_WG) void chain_iter_forward_kernel(ChainK<V, NJ> P, int B, int T,
+                                                                   ChainIter<V> a, LSParams ls) {
+  const int b = blockIdx.x * CH_WG + threadIdx.x;
+  if (b >= B || a.status[b] != ILQR_TRAJ_OK) return;
+  V du2 = V(0);
+  const V pc = a.prev_cost ? a.prev_cost[b] : V(INFINITY);
+  const ChainFwdOut<V> r = chain_forward_lane<V, NJ, NU>(P, b, T, a.x, a.u, a.xtraj, a.d, a.K, pc,
+                                                         a.xnew, a.unew, &du2, ls);
+  if (a.trials) a.trials[b] = r.trials;
+  if (a.du2) a.du2[b] = du2;
+  if (a.iters) a.iters[b] = a.iter;
+  if (!r.accepted) {
+    a.status[b] = (r.cost != r.cost) ? ILQR_TRAJ_NAN : ILQR_TRAJ_LS_EXHAUSTED;
+    if (a.res_parity) a.res_parity[b] = a.parity;
+  } else {
+    a.new_cost[b] = r.cost;                // prev_cost = new_cost (:168)
+    if ((double)du2 <= ls.tol) {           // (:171) break BEFORE the update
+      a.status[b] = ILQR_TRAJ_CONVERGED;
+      if (a.res_parity) a.res_parity[b] = a.parity;
+    }
+  }
+}
+
+// x_out[b] = (res_parity[b] ? x1 : x0)[b]; still-running trajectories → MAX_ITER
+template <class V>
+__global__ __launch_bounds__(256) void chain_gather_kernel(int B, int nxe, int nue, const V* x0,
+                                                           const V* u0, const V* x1, const V* u1,
+                                                           const int32_t* res_parity,
+                                                           int32_t* status, int final_parity,
+                                                           V* x_out, V* u_out) {
+  const int b = blockIdx.y;
+  if (b >= B) return;
+  const bool running = status[b] == ILQR_TRAJ_OK;
+  const int par = running ? final_parity : res_parity[b];
+  const V* xs = (par ? x1 : x0) + (size_t)b * nxe;
+  const V* us = (par ? u1 : u0) + (size_t)b * nue;
+  for (int i = threadIdx.x; i < nxe + nue; i += 256) {  // one block per trajectory: status is
+                                                         // read by all threads before it is set
+    if (i < nxe) x_out[(size_t)b * nxe + i] = xs[i];
+    else u_out[(size_t)b * nue + (i - nxe)] = us[i - nxe];
+  }
+  __syncthreads();
+  if (running && threadIdx.x == 0) status[b] = ILQR_TRAJ_MAX_ITER;
+}
+
+template <class V>
+__global__ void chain_fill_kernel(V* p, int n, V v) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < n) p[i] = v;
+}
+
+}  // namespace
+}  // namespace ilqr
+
+// ---------------------------------------------------------------------------
+// Host side: the chain handle and its C ABI (include/ilqr.h, ilqr_chain_*)
+// ---------------------------------------------------------------------------
+struct ilqr_chain_handle {
+  int device = 0;
+  int nj = 0, nu = 0, T = 0, batch = 0;
+  int dtype = ILQR_F64;
+  int lin = ILQR_LINEARIZE_DUAL;
+  ilqr_chain chain{};
+  hipStream_t stream = nullptr;
+  void* xbuf[2] = {nullptr, nullptr};
+  void* ubuf[2] = {nullptr, nullptr};
+  void* K = nullptr;
+  void* d = nullptr;
+  void* J = nullptr;
+  void* prev_cost = nullptr;
+  void* du2 = nullptr;
+  int32_t* trials = nullptr;
+  int32_t* status = nullptr;
+  int32_t* res_parity = nullptr;
+  int32_t* iters = nullptr;
+};
+
+namespace {
+
+thread_local std::string g_chain_error;
+
+ilqr_status chain_hip_fail(hipError_t e, const char* what) {
+  g_chain_error = std::string(what) + ": " + hipGetErrorString(e);
+  return ILQR_ERR_HIP;
+}
+
+#define CH_TRY(expr)                                         \
+  do {                                                       \
+    hipError_t e_ = (expr);                                  \
+    if (e_ != hipSuccess) return chain_hip_fail(e_, #expr);  \
+  } while (0)
+
+template <class V, int NJ>
+ilqr::ChainK<V, NJ> chain_consts(const ilqr_chain& c) {
+  ilqr::ChainK<V, NJ> P{};
+  for (int i = 0; i < NJ; ++i) {
+    for (int k = 0; k < 9; ++k) P.R0[i][k] = (V)c.joint_rot[i][k];
+    for (int k = 0; k < 3; ++k) {
+      P.p[i][k] = (V)c.joint_pos[i][k];
+      P.ax[i][k] = (V)c.axis[i][k];
+      P.mc[i][k] = (V)(c.mass[i] * c.com[i][k]);
+    }
+    P.m[i] = (V)c.mass[i];
+    // Io = Ic + m(|c|²1 − c cᵀ): rotational inertia about the body origin (fp64 first)
+    const double* cm = c.com[i];
+    const double cc = cm[0] * cm[0] + cm[1] * cm[1] + cm[2] * cm[2];
+    for (int r = 0; r < 3; ++r)
+      for (int k = 0; k < 3; ++k)
+        P.Io[i][3 * r + k] =
+            (V)(c.inertia[i][3 * r + k] + c.mass[i] * ((r == k ? cc : 0.0) - cm[r] * cm[k]));
+    P.tgt[i] = (V)c.target[i];
+    P.qw[i] = (V)c.q_weight[i];
+    P.rw[i] = (V)c.r_weight[i];
+    P.qfw[i] = (V)c.qf_weight[i];
+  }
+  for (int k = 0; k < 3; ++k) P.g[k] = (V)c.gravity[k];
+  P.dt = (V)c.dt;
+  return P;
+}
+
+ilqr::LSParams chain_ls(const ilqr_options* o) {
+  ilqr_options def;
+  ilqr_default_options(&def);
+  if (!o) o = &def;
+  return ilqr::LSParams{o->mu, o->alpha0, o->shrink, o->tol, o->max_trials};
+}
+
+ilqr_status chain_check_options(const ilqr_options* o) {
+  if (!o) return ILQR_OK;
+  if (o->max_trials < 1 || o->max_iter < 0) return ILQR_ERR_BAD_ARG;
+  if (!(o->shrink > 0.0 && o->shrink < 1.0) || !(o->alpha0 > 0.0) || std::isnan(o->mu))
+    return ILQR_ERR_BAD_ARG;
+  return ILQR_OK;
+}
+
+size_t vsize(const ilqr_chain_handle* h) { return h->dtype == ILQR_F32 ? 4 : 8; }
+
+// Typed operations of one (V, NJ, NU) instantiation.
+template <class V, int NJ, int NU>
+struct ChainOps {
+  static constexpr int NX = 2 * NJ;
+  using Value = V;
+  using Iter = ilqr::ChainIter<V>;
+
+  static hipError_t linearize(ilqr_chain_handle* h, const V* x, const V* u, const int32_t* st) {
+    const auto P = chain_consts<V, NJ>(h->chain);
+    const dim3 grid((h->batch + 255) / 256, h->T);
+    if (h->lin == ILQR_LINEARIZE_DUAL)
+      ilqr::chain_linearize_kernel<V, NJ, NU, ILQR_LINEARIZE_DUAL>
+          <<<grid, 256, 0, h->stream>>>(P, h->batch, h->T, x, u, st, (V*)h->J);
+    else
+      ilqr::chain_linearize_kernel<V, NJ, NU, ILQR_LINEARIZE_CENTRAL_FD>
+          <<<grid, 256, 0, h->stream>>>(P, h->batch, h->T, x, u, st, (V*)h->J);
+    return hipGetLastError();
+  }
+  static hipError_t unpack(ilqr_chain_handle* h, V* A, V* Bm) {
+    const size_t n = (size_t)h->batch * h->T;
+    ilqr::chain_unpack_kernel<V, NJ, NU><<<(unsigned)((n + 255) / 256), 256, 0, h->stream>>>(
+        h->batch, h->T, (const V*)h->J, A, Bm);
+    return hipGetLastError();
+  }
+  static hipError_t backward(ilqr_chain_handle* h, const V* x, const V* u, V* d, V* K,
+                             int32_t* st, double mu) {
+    hipError_t e = linearize(h, x, u, nullptr);
+    if (e != hipSuccess) return e;
+    const auto P = chain_consts<V, NJ>(h->chain);
+    ilqr::chain_backward_kernel<V, NJ, NU><<<(h->batch + ilqr::CH_WG - 1) / ilqr::CH_WG, ilqr::CH_WG,
+                                             0, h->stream>>>(P, h->batch, h->T, x, (const V*)h->J,
+                                                             d, K, st, (V)mu);
+    return hipGetLastError();
+  }
+  static hipError_t forward(ilqr_chain_handle* h, const V* x, const V* u, const V* xt, const V* d,
+                            const V* K, const V* pc, V* xn, V* un, V* nc, int32_t* tr,
+                            int32_t* st, const ilqr::LSParams& ls) {
+    const auto P = chain_consts<V, NJ>(h->chain);
+    ilqr::chain_forward_kernel<V, NJ, NU><<<(h->batch + ilqr::CH_WG - 1) / ilqr::CH_WG, ilqr::CH_WG,
+                                            0, h->stream>>>(P, h->batch, h->T, x, u, xt, d, K, pc,
+                                                            xn, un, nc, tr, st, ls);
+    return hipGetLastError();
+  }
+  static hipError_t iteration(ilqr_chain_handle* h, const Iter& a, const ilqr::LSParams& ls) {
+    hipError_t e = linearize(h, a.x, a.u, a.status);
+    if (e != hipSuccess) return e;
+    const auto P = chain_consts<V, NJ>(h->chain);
+    const int g = (h->batch + ilqr::CH_WG - 1) / ilqr::CH_WG;
+    ilqr::chain_iter_backward_kernel<V, NJ, NU>
+        <<<g, ilqr::CH_WG, 0, h->stream>>>(P, h->batch, h->T, a, (const V*)h->J, (V)ls.mu);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    ilqr::chain_iter_forward_kernel<V, NJ, NU><<<g, ilqr::CH_WG, 0, h->stream>>>(P, h->batch, h->T,
+                                                                                a, ls);
+    return hipGetLastError();
+  }
+  static hipError_t dynamics(ilqr_chain_handle* h, const V* x, const V* u, V* xo, int n) {
+    const auto P = chain_consts<V, NJ>(h->chain);
+    ilqr::chain_dynamics_kernel<V, NJ, NU><<<(n + 255) / 256, 256, 0, h->stream>>>(P, n, x, u, xo);
+    return hipGetLastError();
+  }
+};
+
+// (n_joints, nu) shapes with compiled kernels: the iLQR iteration for the 2-DoF arm
+// (nu = 2 every joint driven, nu = 1 joint 1 only); dynamics also for the 6-DoF arm.
+bool iter_supported(int nj, int nu) { return nj == 2 && (nu == 1 || nu == 2); }
+bool dyn_supported(int nj, int nu) { return iter_supported(nj, nu) || (nj == 6 && nu == 6); }
+
+template <class V, class Fn>
+hipError_t dispatch(const ilqr_chain_handle* h, Fn&& fn) {
+  if (h->nj == 2 && h->nu == 2) return fn(ChainOps<V, 2, 2>{});
+  if (h->nj == 2 && h->nu == 1) return fn(ChainOps<V, 2, 1>{});
+  return hipErrorInvalidValue;
+}
+template <class Fn>
+hipError_t dispatch_any(const ilqr_chain_handle* h, Fn&& fn) {
+  if (h->dtype == ILQR_F32) return dispatch<float>(h, fn);
+  return dispatch<double>(h, fn);
+}
+
+template <class V>
+ilqr::ChainIter<V> iter_args(const ilqr_chain_handle* h, const void* x, const void* u,
+                             const void* xt, void* xn, void* un, const void* pc, void* nc,
+                             void* du2, int32_t* tr, int32_t* st) {
+  ilqr::ChainIter<V> a{};
+  a.x = (const V*)x;
+  a.u = (const V*)u;
+  a.xtraj = (const V*)xt;
+  a.xnew = (V*)xn;
+  a.unew = (V*)un;
+  a.K = (V*)h->K;
+  a.d = (V*)h->d;
+  a.prev_cost = (const V*)pc;
+  a.new_cost = (V*)nc;
+  a.du2 = (V*)du2;
+  a.trials = tr;
+  a.status = st;
+  return a;
+}
+
+ilqr_status chain_fold_status(ilqr_chain_handle* h, const int32_t* dev_status) {
+  std::vector<int32_t> st(h->batch);
+  CH_TRY(hipMemcpyAsync(st.data(), dev_status, sizeof(int32_t) * h->batch, hipMemcpyDeviceToHost,
+                        h->stream));
+  CH_TRY(hipStreamSynchronize(h->stream));
+  bool nan = false, ls = false;
+  for (int32_t s : st) {
+    nan |= s == ILQR_TRAJ_NAN;
+    ls |= s == ILQR_TRAJ_LS_EXHAUSTED;
+  }
+  return nan ? ILQR_ERR_NAN : (ls ? ILQR_ERR_LS_EXHAUSTED : ILQR_OK);
+}
+
+template <class V>
+ilqr_status chain_fit_t(ilqr_chain_handle* h, const ilqr_options* o, const void* x_init,
+                        const void* u_init, const void* x_traj, void* x_out, void* u_out,
+                        void* cost, int32_t* iters, int32_t* status) {
+  const size_t B = (size_t)h->batch, nx = 2 * (size_t)h->nj;
+  const size_t nxe = (h->T + 1) * nx, nue = (size_t)h->T * h->nu;
+  hipStream_t s = h->stream;
+  CH_TRY(hipMemcpyAsync(h->xbuf[0], x_init, sizeof(V) * B * nxe, hipMemcpyDeviceToDevice, s));
+  CH_TRY(hipMemcpyAsync(h->ubuf[0], u_init, sizeof(V) * B * nue, hipMemcpyDeviceToDevice, s));
+  const unsigned g = (unsigned)((B + 255) / 256);
+  ilqr::chain_fill_kernel<V><<<g, 256, 0, s>>>((V*)h->prev_cost, h->batch, V(INFINITY));  // :159
+  ilqr::chain_fill_kernel<int32_t><<<g, 256, 0, s>>>(h->status, h->batch, ILQR_TRAJ_OK);
+  ilqr::chain_fill_kernel<int32_t><<<g, 256, 0, s>>>(h->res_parity, h->batch, 0);
+  ilqr::chain_fill_kernel<int32_t><<<g, 256, 0, s>>>(h->iters, h->batch, 0);
+  CH_TRY(hipGetLastError());
+  const ilqr::LSParams ls = chain_ls(o);
+  const int max_iter = o ? o->max_iter : 100;
+  int par = 0;
+  for (int it = 1; it <= max_iter; ++it) {  // forward_pass.jl:161
+    auto a = iter_args<V>(h, h->xbuf[par], h->ubuf[par], x_traj, h->xbuf[par ^ 1], h->ubuf[par ^ 1],
+                          h->prev_cost, h->prev_cost, h->du2, h->trials, h->status);
+    a.res_parity = h->res_parity;
+    a.iters = h->iters;
+    a.parity = par;
+    a.iter = it;
+    CH_TRY(dispatch<V>(h, [&](auto ops) { return decltype(ops)::iteration(h, a, ls); }));
+    par ^= 1;  // x̄ⁱ, ūⁱ = x̄ⁱ⁺¹, ūⁱ⁺¹ (:174-175)
+  }
+  ilqr::chain_gather_kernel<V><<<dim3(1, h->batch), 256, 0, s>>>(
+      h->batch, (int)nxe, (int)nue, (const V*)h->xbuf[0], (const V*)h->ubuf[0],
+      (const V*)h->xbuf[1], (const V*)h->ubuf[1], h->res_parity, h->status, par, (V*)x_out,
+      (V*)u_out);
+  CH_TRY(hipGetLastError());
+  if (cost) CH_TRY(hipMemcpyAsync(cost, h->prev_cost, sizeof(V) * B, hipMemcpyDeviceToDevice, s));
+  if (iters) CH_TRY(hipMemcpyAsync(iters, h->iters, sizeof(int32_t) * B, hipMemcpyDeviceToDevice, s));
+  if (status) CH_TRY(hipMemcpyAsync(status, h->status, sizeof(int32_t) * B, hipMemcpyDeviceToDevice, s));
+  return chain_fold_status(h, h->status);
+}
+
+}  // namespace
+
+extern "C" {
+
+int ilqr_chain_supported(int n_joints, int nu) { return iter_supported(n_joints, nu) ? 1 : 0; }
+
+const char* ilqr_chain_last_error(void) { return g_chain_error.c_str(); }
+
+ilqr_status ilqr_chain_create(ilqr_chain_handle** out, int device, const ilqr_chain* chain, int T,
+                              int batch, int32_t dtype, int32_t linearization) {
+  if (!out || !chain) return ILQR_ERR_BAD_ARG;
+  *out = nullptr;
+  if (T <= 0 || batch <= 0 || chain->n_joints <= 0 || chain->nu <= 0) return ILQR_ERR_BAD_DIMS;
+  if (chain->n_joints > ILQR_CHAIN_MAX_JOINTS || !(chain->nu == chain->n_joints || chain->nu == 1))
+    return ILQR_ERR_BAD_DIMS;
+  if (dtype != ILQR_F32 && dtype != ILQR_F64) return ILQR_ERR_BAD_ARG;
+  if (linearization != ILQR_LINEARIZE_DUAL && linearization != ILQR_LINEARIZE_CENTRAL_FD)
+    return ILQR_ERR_BAD_ARG;
+  if (!(chain->dt > 0.0)) return ILQR_ERR_BAD_ARG;
+  if (!dyn_supported(chain->n_joints, chain->nu)) return ILQR_ERR_UNSUPPORTED;
+  CH_TRY(hipSetDevice(device));
+  auto* h = new ilqr_chain_handle;
+  h->device = device;
+  h->nj = chain->n_joints;
+  h->nu = chain->nu;
+  h->T = T;
+  h->batch = batch;
+  h->dtype = dtype;
+  h->lin = linearization;
+  h->chain = *chain;
+  const size_t w = vsize(h), B = (size_t)batch, nx = 2 * (size_t)h->nj, nu = (size_t)h->nu;
+  hipError_t e = hipSuccess;
+  if (iter_supported(h->nj, h->nu)) {  // dynamics-only shapes need no workspace
+    for (int i = 0; i < 2 && e == hipSuccess; ++i) {
+      e = hipMalloc(&h->xbuf[i], w * B * (T + 1) * nx);
+      if (e == hipSuccess) e = hipMalloc(&h->ubuf[i], w * B * T * nu);
+    }
+    if (e == hipSuccess) e = hipMalloc(&h->K, w * B * T * nu * nx);
+    if (e == hipSuccess) e = hipMalloc(&h->d, w * B * T * nu);
+    if (e == hipSuccess) e = hipMalloc(&h->J, w * B * T * (nx * (nx + nu) + nx + nu));
+    if (e == hipSuccess) e = hipMalloc(&h->prev_cost, w * B);
+    if (e == hipSuccess) e = hipMalloc(&h->du2, w * B);
+    if (e == hipSuccess) e = hipMalloc(&h->trials, sizeof(int32_t) * B);
+    if (e == hipSuccess) e = hipMalloc(&h->status, sizeof(int32_t) * B);
+    if (e == hipSuccess) e = hipMalloc(&h->res_parity, sizeof(int32_t) * B);
+    if (e == hipSuccess) e = hipMalloc(&h->iters, sizeof(int32_t) * B);
+  }
+  if (e != hipSuccess) {
+    ilqr_chain_destroy(h);
+    return chain_hip_fail(e, "ilqr_chain_create: hipMalloc");
+  }
+  *out = h;
+  return ILQR_OK;
+}
+
+ilqr_status ilqr_chain_destroy(ilqr_chain_handle* h) {
+  if (!h) return ILQR_OK;
+  (void)hipSetDevice(h->device);
+  for (int i = 0; i < 2; ++i) {
+    (void)hipFree(h->xbuf[i]);
+    (void)hipFree(h->ubuf[i]);
+  }
+  for (void* p : {h->K, h->d, h->J, h->prev_cost, h->du2}) (void)hipFree(p);
+  for (int32_t* p : {h->trials, h->status, h->res_parity, h->iters}) (void)hipFree(p);
+  delete h;
+  return ILQR_OK;
+}
+
+ilqr_status ilqr_chain_set_stream(ilqr_chain_handle* h, void* s) {
+  if (!h) return ILQR_ERR_BAD_ARG;
+  h->stream = (hipStream_t)s;
+  return ILQR_OK;
+}
+
+ilqr_status ilqr_chain_dynamics(ilqr_chain_handle* h, const void* x, const void* u, void* x_next,
+                                int n) {
+  if (!h || !x || !u || !x_next) return ILQR_ERR_BAD_ARG;
+  if (n <= 0) return ILQR_ERR_BAD_DIMS;
+  CH_TRY(hipSetDevice(h->device));
+  auto fn = [&](auto ops) {
+    using O = decltype(ops);
+    using V = typename O::Value;
+    return O::dynamics(h, (const V*)x, (const V*)u, (V*)x_next, n);
+  };
+  hipError_t e;
+  if (h->nj == 6) {
+    e = h->dtype == ILQR_F32 ? fn(ChainOps<float, 6, 6>{}) : fn(ChainOps<double, 6, 6>{});
+  } else {
+    e = dispatch_any(h, fn);
+  }
+  CH_TRY(e);
+  return ILQR_OK;
+}
+
+ilqr_status ilqr_chain_linearize(ilqr_chain_handle* h, const void* x, const void* u, void* A,
+                                 void* B) {
+  if (!h || !x || !u || !A || !B) return ILQR_ERR_BAD_ARG;
+  if (!iter_supported(h->nj, h->nu)) return ILQR_ERR_UNSUPPORTED;
+  CH_TRY(hipSetDevice(h->device));
+  CH_TRY(dispatch_any(h, [&](auto ops) {
+    using O = decltype(ops);
+    using V = typename O::Value;
+    hipError_t e = O::linearize(h, (const V*)x, (const V*)u, nullptr);
+    return e != hipSuccess ? e : O::unpack(h, (V*)A, (V*)B);
+  }));
+  return ILQR_OK;
+}
+
+ilqr_status ilqr_chain_backward(ilqr_chain_handle* h, const ilqr_options* o, const void* x,
+                                const void* u, void* d, void* K, int32_t* status) {
+  if (!h || !x || !u || !d || !K) return ILQR_ERR_BAD_ARG;
+  if (!iter_supported(h->nj, h->nu)) return ILQR_ERR_UNSUPPORTED;
+  ilqr_status st = chain_check_options(o);
+  if (st != ILQR_OK) return st;
+  CH_TRY(hipSetDevice(h->device));
+  const double mu = chain_ls(o).mu;
+  CH_TRY(dispatch_any(h, [&](auto ops) {
+    using O = decltype(ops);
+    using V = typename O::Value;
+    return O::backward(h, (const V*)x, (const V*)u, (V*)d, (V*)K, status, mu);
+  }));
+  return status ? chain_fold_status(h, status) : ILQR_OK;
+}
+
+ilqr_status ilqr_chain_forward(ilqr_chain_handle* h, const ilqr_options* o, const void* x,
+                               const void* u, const void* x_traj, const void* d, const void* K,
+                               const void* prev_cost, void* x_new, void* u_new, void* new_cost,
+                               int32_t* trials, int32_t* status) {
+  if (!h || !x || !u || !d || !K || !prev_cost || !x_new || !u_new || !new_cost)
+    return ILQR_ERR_BAD_ARG;
+  if (!iter_supported(h->nj, h->nu)) return ILQR_ERR_UNSUPPORTED;
+  ilqr_status st = chain_check_options(o);
+  if (st != ILQR_OK) return st;
+  CH_TRY(hipSetDevice(h->device));
+  const ilqr::LSParams ls = chain_ls(o);
+  CH_TRY(dispatch_any(h, [&](auto ops) {
+    using O = decltype(ops);
+    using V = typename O::Value;
+    return O::forward(h, (const V*)x, (const V*)u, (const V*)x_traj, (const V*)d, (const V*)K,
+                      (const V*)prev_cost, (V*)x_new, (V*)u_new, (V*)new_cost, trials, status, ls);
+  }));
+  return status ? chain_fold_status(h, status) : ILQR_OK;
+}
+
+ilqr_status ilqr_chain_iterate(ilqr_chain_handle* h, const ilqr_options* o, const void* x,
+                               const void* u, const void* x_traj, void* x_new, void* u_new,
+                               const void* prev_cost, void* new_cost, void* du2, int32_t* trials,
+                               int32_t* status) {
+  if (!h || !x || !u || !x_new || !u_new || !new_cost || !status) return ILQR_ERR_BAD_ARG;
+  if (!iter_supported(h->nj, h->nu)) return ILQR_ERR_UNSUPPORTED;
+  ilqr_status st = chain_check_options(o);
+  if (st != ILQR_OK) return st;
+  CH_TRY(hipSetDevice(h->device));
+  const ilqr::LSParams ls = chain_ls(o);
+  CH_TRY(dispatch_any(h, [&](auto ops) {
+    using O = decltype(ops);
+    using V = typename O::Value;
+    const auto a = iter_args<V>(h, x, u, x_traj, x_new, u_new, prev_cost, new_cost, du2, trials,
+                                status);
+    return O::iteration(h, a, ls);
+  }));
+  return ILQR_OK;
+}
+
+ilqr_status ilqr_chain_fit(ilqr_chain_handle* h, const ilqr_options* o, const void* x_init,
+                           const void* u_init, const void* x_traj, void* x_out, void* u_out,
+                           void* cost, int32_t* iters, int32_t* status) {
+  if (!h || !x_init || !u_init || !x_out || !u_out) return ILQR_ERR_BAD_ARG;
+  if (!iter_supported(h->nj, h->nu)) return ILQR_ERR_UNSUPPORTED;
+  ilqr_status st = chain_check_options(o);
+  if (st != ILQR_OK) return st;
+  CH_TRY(hipSetDevice(h->device));
+  if (h->dtype == ILQR_F32)
+    return chain_fit_t<float>(h, o, x_init, u_init, x_traj, x_out, u_out, cost, iters, status);
+  return chain_fit_t<double>(h, o, x_init, u_init, x_traj, x_out, u_out, cost, iters, status);
+}
+
+ilqr_status ilqr_chain_sync(ilqr_chain_handle* h) {
+  if (!h) return ILQR_ERR_BAD_ARG;
+  CH_TRY(hipStreamSynchronize(h->stream));
+  return ILQR_OK;
+}
+
+}  // extern "C"

@@ -8,7 +8,9 @@ from .problems import (LinearDynamics, LQBatch, QuadraticCost, QuadraticFinalCos
 __all__ = ["LinearDynamics", "QuadraticCost", "QuadraticFinalCost", "LQBatch",
            "lq_from_closures", "TwoLinkArm", "TwoLinkDynamics", "TwoLinkCost",
            "TwoLinkFinalCost", "two_link_closures", "two_link_initial_states", "quadrotor_batch", "quadrotor_instance", "random_lq_batch",
-           "fit", "backward_pass", "forward_pass", "Solver", "selftest", "LineSearchExhausted"]
+           "fit", "backward_pass", "forward_pass", "Solver", "selftest", "LineSearchExhausted",
+           "ChainSolver", "ChainProblem", "rbd_2dof_problem", "chain_closures", "load_robot",
+           "rbd_initial_states"]
 
 
 def __getattr__(name):
@@ -17,6 +19,10 @@ def __getattr__(name):
     if name in ("fit", "backward_pass", "forward_pass", "LineSearchExhausted"):
         from . import api
         return getattr(api, name)
+    if name in ("ChainSolver", "ChainProblem", "rbd_2dof_problem", "chain_closures", "load_robot",
+                "rbd_initial_states"):
+        from . import chain
+        return getattr(chain, name)
     if name in ("Solver", "selftest", "FitResult"):
         from . import solver
         return getattr(solver, name)

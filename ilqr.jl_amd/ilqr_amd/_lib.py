@@ -31,6 +31,14 @@ TRAJ_NAN = 4
 PROBLEM_LQ = 1
 PROBLEM_TWO_LINK = 2
 PROBLEM_TILES = 3
+PROBLEM_CHAIN = 4
+
+# ilqr_dtype / ilqr_linearization (chain family)
+F64 = 0
+F32 = 1
+LINEARIZE_DUAL = 0
+LINEARIZE_CENTRAL_FD = 1
+CHAIN_MAX_JOINTS = 8
 
 
 class Problem(C.Structure):
@@ -46,6 +54,18 @@ class Tiles(C.Structure):
 class Options(C.Structure):
     _fields_ = [("max_iter", C.c_int32), ("max_trials", C.c_int32), ("tol", C.c_double),
                 ("mu", C.c_double), ("alpha0", C.c_double), ("shrink", C.c_double)]
+
+
+class ChainStruct(C.Structure):
+    """ilqr_chain (include/ilqr.h)."""
+    J = CHAIN_MAX_JOINTS
+    _fields_ = [("n_joints", C.c_int32), ("nu", C.c_int32), ("dt", C.c_double),
+                ("gravity", C.c_double * 3),
+                ("joint_rot", (C.c_double * 9) * J), ("joint_pos", (C.c_double * 3) * J),
+                ("axis", (C.c_double * 3) * J), ("mass", C.c_double * J),
+                ("com", (C.c_double * 3) * J), ("inertia", (C.c_double * 9) * J),
+                ("target", C.c_double * J), ("q_weight", C.c_double * J),
+                ("r_weight", C.c_double * J), ("qf_weight", C.c_double * J)]
 
 
 # every symbol declared in include/ilqr.h, with its ctypes signature
@@ -72,6 +92,19 @@ SIGNATURES = {
     "ilqr_memcpy_h2d": (C.c_int, [P, P, P, C.c_size_t]),
     "ilqr_memcpy_d2h": (C.c_int, [P, P, P, C.c_size_t]),
     "ilqr_selftest": (C.c_int, [C.c_int, C.POINTER(C.c_int32)]),
+    "ilqr_chain_supported": (C.c_int, [C.c_int, C.c_int]),
+    "ilqr_chain_last_error": (C.c_char_p, []),
+    "ilqr_chain_create": (C.c_int, [C.POINTER(P), C.c_int, C.POINTER(ChainStruct), C.c_int,
+                                    C.c_int, C.c_int32, C.c_int32]),
+    "ilqr_chain_destroy": (C.c_int, [P]),
+    "ilqr_chain_set_stream": (C.c_int, [P, P]),
+    "ilqr_chain_sync": (C.c_int, [P]),
+    "ilqr_chain_dynamics": (C.c_int, [P, P, P, P, C.c_int]),
+    "ilqr_chain_linearize": (C.c_int, [P, P, P, P, P]),
+    "ilqr_chain_backward": (C.c_int, [P, C.POINTER(Options), P, P, P, P, P]),
+    "ilqr_chain_forward": (C.c_int, [P, C.POINTER(Options), P, P, P, P, P, P, P, P, P, P, P]),
+    "ilqr_chain_iterate": (C.c_int, [P, C.POINTER(Options), P, P, P, P, P, P, P, P, P, P]),
+    "ilqr_chain_fit": (C.c_int, [P, C.POINTER(Options), P, P, P, P, P, P, P, P]),
 }
 
 _lib = None
@@ -101,7 +134,7 @@ class IlqrError(RuntimeError):
     def __init__(self, status: int, where: str):
         lib = load()
         msg = lib.ilqr_status_string(status).decode()
-        extra = lib.ilqr_last_error().decode()
+        extra = lib.ilqr_last_error().decode() or lib.ilqr_chain_last_error().decode()
         super().__init__(f"{where}: {msg}" + (f" ({extra})" if extra and status == ERR_HIP else ""))
         self.status = status
 

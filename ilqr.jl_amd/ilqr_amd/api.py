@@ -35,6 +35,7 @@ import torch
 
 from . import _lib
 from . import tiles as _tiles
+from .chain import ChainSolver, chain_problem_of
 from .problems import (LinearDynamics, QuadraticCost, QuadraticFinalCost, is_two_link,
                        lq_from_closures)
 from .solver import Solver
@@ -71,14 +72,32 @@ def _out(t, batched, as_torch):
 
 
 def _family(dynamicsf, immediate_cost, final_cost):
-    """'two_link', 'lq' (recognised problem families with fused device kernels) or
-    'closures' (arbitrary torch closures: derivative tiles + ilqr_backward_tiles)."""
+    """'two_link', 'lq', 'chain' (recognised problem families with fused device kernels)
+    or 'closures' (arbitrary torch closures: derivative tiles + ilqr_backward_tiles)."""
     if is_two_link(dynamicsf, immediate_cost, final_cost):
         return "two_link"
+    if chain_problem_of(dynamicsf, immediate_cost, final_cost) is not None:
+        return "chain"
     if (isinstance(dynamicsf, LinearDynamics) and isinstance(immediate_cost, QuadraticCost)
             and isinstance(final_cost, QuadraticFinalCost)):
         return "lq"
     return "closures"
+
+
+def _eltype(a):
+    """The reference is generic in the element type (Julia): Float32 inputs solve in fp32."""
+    dt = a.dtype if isinstance(a, (torch.Tensor, np.ndarray)) else None
+    return torch.float32 if dt in (torch.float32, np.float32) else torch.float64
+
+
+def _chain_solver(xb, ub, dynamicsf, immediate_cost, final_cost, dtype):
+    nb, N, nx = xb.shape
+    _, M, nu = ub.shape
+    assert N == M + 1, "size(x)[1] == size(u)[1] + 1"   # backward_pass.jl:329
+    p = chain_problem_of(dynamicsf, immediate_cost, final_cost)
+    if (p.nx, p.nu) != (nx, nu):
+        raise AssertionError(f"problem is ({p.nx}, {p.nu}) but x/u are ({nx}, {nu})")
+    return ChainSolver(p, M, nb, dtype=dtype, device=_device())
 
 
 def _tiles_solver(xb, ub):
@@ -109,10 +128,16 @@ def backward_pass(x, u, dynamicsf, immediate_cost, final_cost):
     """→ (δu, K) exactly like iLQR.backward_pass (backward_pass.jl:324-357)."""
     xb, batched, is_t = _as_batch(x, "x", 2)
     ub, _, _ = _as_batch(u, "u", 2)
-    if _family(dynamicsf, immediate_cost, final_cost) == "closures":
+    fam = _family(dynamicsf, immediate_cost, final_cost)
+    if fam == "closures":
         s = _tiles_solver(xb, ub)
         tl = _tiles.derivative_tiles(xb, ub, dynamicsf, immediate_cost, final_cost)
         d, K, st = s.backward_tiles(tl)
+    elif fam == "chain":
+        dt = _eltype(x)
+        xb, ub = xb.to(dt), ub.to(dt)
+        s = _chain_solver(xb, ub, dynamicsf, immediate_cost, final_cost, dt)
+        d, K, st = s.backward(xb, ub)
     else:
         s = _solver(xb, ub, dynamicsf, immediate_cost, final_cost)
         d, K, st = s.backward(xb, ub)
@@ -136,7 +161,15 @@ def forward_pass(x, u, x_traj, du, K, prev_cost, dynamicsf, immediate_cost, fina
     pc = torch.as_tensor(np.broadcast_to(np.asarray(prev_cost, dtype=np.float64), (nb,)).copy()
                          if not isinstance(prev_cost, torch.Tensor) else prev_cost,
                          dtype=torch.float64).reshape(nb).to(xb.device).contiguous()
-    if _family(dynamicsf, immediate_cost, final_cost) == "closures":
+    fam = _family(dynamicsf, immediate_cost, final_cost)
+    if fam == "chain":
+        dt = _eltype(x)
+        s = _chain_solver(xb, ub, dynamicsf, immediate_cost, final_cost, dt)
+        o = _lib.default_options(max_trials=max_trials)
+        xn, un, cost, trials, st = s.forward(xb.to(dt), ub.to(dt), db.to(dt), Kb.to(dt),
+                                             pc.to(dt), x_traj=xt.to(dt), options=o)
+        s.close()
+    elif fam == "closures":
         xn, un, cost, trials, ok = _tiles.rollout_forward(
             xb, ub, xt, db, Kb, pc, dynamicsf, immediate_cost, final_cost,
             max_trials=max_trials or _lib.default_options().max_trials)
@@ -167,9 +200,16 @@ def fit(x_init, u_init, dynamicsf, immediate_cost, final_cost, *, x_traj=None,
     xt = None
     if x_traj is not None:
         xt, _, _ = _as_batch(x_traj, "x_traj", 2)
-    if _family(dynamicsf, immediate_cost, final_cost) == "closures":
+    fam = _family(dynamicsf, immediate_cost, final_cost)
+    if fam == "closures":
         r = _fit_closures(xb, ub, xt, dynamicsf, immediate_cost, final_cost, int(max_iter),
                           float(tol))
+    elif fam == "chain":
+        dt = _eltype(x_init)
+        s = _chain_solver(xb, ub, dynamicsf, immediate_cost, final_cost, dt)
+        r = s.fit(xb.to(dt), ub.to(dt), x_traj=None if xt is None else xt.to(dt),
+                  max_iter=int(max_iter), tol=float(tol))
+        s.close()
     else:
         s = _solver(xb, ub, dynamicsf, immediate_cost, final_cost)
         r = s.fit(xb, ub, x_traj=xt, max_iter=int(max_iter), tol=float(tol))

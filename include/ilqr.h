@@ -80,7 +80,8 @@ enum {
 typedef enum {
   ILQR_PROBLEM_LQ = 1,
   ILQR_PROBLEM_TWO_LINK = 2,
-  ILQR_PROBLEM_TILES = 3  /* ilqr_backward_tiles only (caller-supplied derivatives) */
+  ILQR_PROBLEM_TILES = 3, /* ilqr_backward_tiles only (caller-supplied derivatives) */
+  ILQR_PROBLEM_CHAIN = 4  /* URDF serial chain: the ilqr_chain_* entry points below   */
 } ilqr_problem_kind;
 
 typedef struct {
@@ -187,6 +188,77 @@ ilqr_status ilqr_fit(ilqr_handle* h, const ilqr_problem* p, const ilqr_options* 
                      const double* x_init, const double* u_init, const double* x_traj,
                      double* x_out, double* u_out, double* cost, int32_t* iters,
                      int32_t* status);
+
+/* ---------------------------------------------------------------------------
+ * RBD problem family (ILQR_PROBLEM_CHAIN): a fixed-base serial chain of revolute
+ * joints described by a URDF — the reference's RigidBodyDynamics.jl example,
+ * test/RBD_2_link_example/RBD_helper_functions.jl:48-116 on test/urdf/2Dof_arm.urdf
+ * (BASELINE.json config 5), with the base fixed. nx = 2·n_joints (q, q̇), and
+ *   dynamicsf(x, u)     = RK4(dt) of [q̇; M(q) \ (τ − dynamics_bias(q, q̇))]      (:48-79)
+ *   immediate_cost(x,u) = Σ q_weightᵢ (targetᵢ − qᵢ)² + Σ r_weightₖ uₖ²         (:85-99)
+ *   final_cost(x)       = Σ qf_weightᵢ (targetᵢ − qᵢ)²                          (:105-116)
+ * with τ = u (nu = n_joints) or τ = [u₁, 0, …] (nu = 1). Arrays use the layout
+ * above in the handle's dtype (ILQR_F32 or ILQR_F64), costs included; the
+ * derivatives of dynamicsf are forward-mode duals (ForwardDiff's algorithm,
+ * ILQR_LINEARIZE_DUAL) or central differences (ILQR_LINEARIZE_CENTRAL_FD).
+ * Compiled shapes: ilqr_chain_supported(); ilqr_chain_dynamics also takes the
+ * 6-DoF arm (n_joints = nu = 6).
+ * --------------------------------------------------------------------------- */
+#define ILQR_CHAIN_MAX_JOINTS 8
+
+typedef enum { ILQR_F64 = 0, ILQR_F32 = 1 } ilqr_dtype;
+typedef enum { ILQR_LINEARIZE_DUAL = 0, ILQR_LINEARIZE_CENTRAL_FD = 1 } ilqr_linearization;
+
+typedef struct {
+  int32_t n_joints;    /* revolute joints, root to tip (ilqr_amd.urdf.parse_urdf)          */
+  int32_t nu;          /* n_joints (every joint driven) or 1 (joint 1 only)               */
+  double dt;           /* RK4 step (Δt = 0.01 in the reference script)                    */
+  double gravity[3];   /* base-frame gravity (the reference parses with zero gravity)     */
+  double joint_rot[ILQR_CHAIN_MAX_JOINTS][9];  /* joint frame → parent body frame, row-major */
+  double joint_pos[ILQR_CHAIN_MAX_JOINTS][3];  /* joint origin in the parent body frame      */
+  double axis[ILQR_CHAIN_MAX_JOINTS][3];       /* unit axis, joint (= child body) frame     */
+  double mass[ILQR_CHAIN_MAX_JOINTS];
+  double com[ILQR_CHAIN_MAX_JOINTS][3];        /* COM in the body frame                     */
+  double inertia[ILQR_CHAIN_MAX_JOINTS][9];    /* about the COM, body axes, row-major       */
+  double target[ILQR_CHAIN_MAX_JOINTS];        /* θ* (target_pose's joint rows)             */
+  double q_weight[ILQR_CHAIN_MAX_JOINTS];
+  double r_weight[ILQR_CHAIN_MAX_JOINTS];
+  double qf_weight[ILQR_CHAIN_MAX_JOINTS];
+} ilqr_chain;
+
+typedef struct ilqr_chain_handle ilqr_chain_handle;
+
+/* 1 if the iLQR kernels are compiled for (n_joints, nu) */
+int ilqr_chain_supported(int n_joints, int nu);
+const char* ilqr_chain_last_error(void);
+ilqr_status ilqr_chain_create(ilqr_chain_handle** out, int device, const ilqr_chain* chain, int T,
+                              int batch, int32_t dtype, int32_t linearization);
+ilqr_status ilqr_chain_destroy(ilqr_chain_handle* h);
+ilqr_status ilqr_chain_set_stream(ilqr_chain_handle* h, void* hip_stream);
+ilqr_status ilqr_chain_sync(ilqr_chain_handle* h);
+/* dynamicsf for n independent (x, u) pairs: x (n, nx), u (n, nu) → x_next (n, nx) */
+ilqr_status ilqr_chain_dynamics(ilqr_chain_handle* h, const void* x, const void* u, void* x_next,
+                                int n);
+/* linearize_dynamics (backward_pass.jl:25-40) at every (b, t): A (batch, T, nx, nx),
+ * B (batch, T, nx, nu) */
+ilqr_status ilqr_chain_linearize(ilqr_chain_handle* h, const void* x, const void* u, void* A,
+                                 void* B);
+/* iLQR.backward_pass / forward_pass / one fit iteration / fit for the chain family;
+ * arguments, status and return semantics as ilqr_backward / ilqr_forward /
+ * ilqr_iterate / ilqr_fit. */
+ilqr_status ilqr_chain_backward(ilqr_chain_handle* h, const ilqr_options* o, const void* x,
+                                const void* u, void* d, void* K, int32_t* status);
+ilqr_status ilqr_chain_forward(ilqr_chain_handle* h, const ilqr_options* o, const void* x,
+                               const void* u, const void* x_traj, const void* d, const void* K,
+                               const void* prev_cost, void* x_new, void* u_new, void* new_cost,
+                               int32_t* trials, int32_t* status);
+ilqr_status ilqr_chain_iterate(ilqr_chain_handle* h, const ilqr_options* o, const void* x,
+                               const void* u, const void* x_traj, void* x_new, void* u_new,
+                               const void* prev_cost, void* new_cost, void* du2, int32_t* trials,
+                               int32_t* status);
+ilqr_status ilqr_chain_fit(ilqr_chain_handle* h, const ilqr_options* o, const void* x_init,
+                           const void* u_init, const void* x_traj, void* x_out, void* u_out,
+                           void* cost, int32_t* iters, int32_t* status);
 
 /* Device memory helpers so a host-language shim (Julia ccall) needs no GPU package. */
 ilqr_status ilqr_malloc(ilqr_handle* h, size_t bytes, void** ptr);

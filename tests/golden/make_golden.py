@@ -19,8 +19,10 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(os.path.dirname(HERE))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "ilqr.jl_amd")]
 
+from ilqr_amd.chain import load_robot, rbd_2dof_problem, rbd_initial_states  # noqa: E402
 from ilqr_amd.problems import quadrotor_batch, random_lq_batch  # noqa: E402
 from oracle import ilqr_oracle as O  # noqa: E402
+from oracle import rbd as RBD  # noqa: E402
 
 MAX_TRIALS = 60
 
@@ -93,7 +95,79 @@ def twolink_case(name, x0s, T, fit_iters=40, tol=1e-6):
     print(name, "fit iters", fiters.tolist())
 
 
-def main():
+def chain_case(name, nu, x0s, T, fit_iters=20, tol=1e-6):
+    """RBD family (ILQR_PROBLEM_CHAIN) on the fixed-base 2Dof_arm: oracle.rbd dynamics
+    (RNEA + RK4, exact Jacobians by forward-mode AD) through the generic oracle passes."""
+    pr = rbd_2dof_problem(nu)
+    model = RBD.ChainModel(pr.chain, pr.dt)
+    cost = RBD.ChainCost(pr.target, pr.q_weight, pr.r_weight, pr.qf_weight)
+    f, l, lf = RBD.chain_closures(model, cost)
+    nb, nx = len(x0s), pr.nx
+    u = np.zeros((nb, T, nu))
+    x = np.empty((nb, T + 1, nx))
+    x[:, 0] = x0s
+    for t in range(T):
+        x[:, t + 1] = model.step(x[:, t], u[:, t])
+    A, Bm = model.linearize(x[:, :T].reshape(-1, nx), u.reshape(-1, nu))
+    d, K = np.empty_like(u), np.empty((nb, T, nu, nx))
+    xn, un, fwc = np.empty_like(x), np.empty_like(u), np.empty(nb)
+    fx, fu = np.empty_like(x), np.empty_like(u)
+    fcost = np.full((nb, fit_iters), np.nan)
+    fiters = np.empty(nb, dtype=np.int32)
+    fstatus = np.empty(nb, dtype=np.int32)  # ILQR_TRAJ_*: 1 converged, 2 max_iter, 3 exhausted
+    for b in range(nb):
+        d[b], K[b] = O.backward_pass(x[b], u[b], f, l, lf)
+        ds, Ks = O.backward_pass(x[b], u[b], f, l, lf, symmetrize=True)
+        assert np.abs(K[b] - Ks).max() <= 1e-9 * np.abs(Ks).max(), name
+        xn[b], un[b], fwc[b] = O.forward_pass(x[b], u[b], np.zeros_like(x[b]), d[b], K[b], np.inf,
+                                              f, l, lf, max_trials=MAX_TRIALS)
+        hist = []
+        try:
+            fx[b], fu[b] = O.fit(x[b], u[b], f, l, lf, max_iter=fit_iters, tol=tol,
+                                 max_trials=MAX_TRIALS, history=hist)
+            fiters[b] = len(hist)
+            fstatus[b] = 1 if hist[-1]["du2"] <= tol else 2
+        except O.LineSearchExhausted:
+            # the reference would loop forever; the device stops this trajectory at the
+            # iterate its failing iteration started from (len(hist) accepted updates)
+            fx[b], fu[b] = O.fit(x[b], u[b], f, l, lf, max_iter=len(hist), tol=-1.0,
+                                 max_trials=MAX_TRIALS)
+            fiters[b] = len(hist) + 1
+            fstatus[b] = 3
+        fcost[b, :len(hist)] = [h["cost"] for h in hist]
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), x=x, u=u,
+                        A=A.reshape(nb, T, nx, nx), B=Bm.reshape(nb, T, nx, nu), d=d, K=K,
+                        fw_x=xn, fw_u=un, fw_cost=fwc, fit_x=fx, fit_u=fu, fit_cost=fcost,
+                        fit_iters=fiters, fit_status=fstatus,
+                        meta=np.array(json.dumps({"T": T, "nu": nu, "fit_max_iter": fit_iters,
+                                                  "tol": tol, "robot": "2dof_arm"})))
+    print(name, "fit iters", fiters.tolist(), "status", fstatus.tolist())
+
+
+def chain6_dynamics_case(name, n=24, seed=5):
+    """One RK4 step of the coupled 6-DoF arm (test/urdf/6Dof_arm.urdf) at random states."""
+    ch = load_robot("6dof_arm")
+    model = RBD.ChainModel(ch, 0.01)
+    rng = np.random.default_rng(seed)
+    x = np.concatenate([rng.uniform(-2, 2, (n, 6)), rng.uniform(-1, 1, (n, 6))], axis=1)
+    u = rng.uniform(-5, 5, (n, 6))
+    M = np.stack([model.mass_matrix_np(q) for q in x[:, :6]])
+    bias = np.stack([model.bias_np(q, qd) for q, qd in zip(x[:, :6], x[:, 6:])])
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), x=x, u=u, x_next=model.step(x, u),
+                        M=M, bias=bias)
+    print(name, "points", n)
+
+
+def main(only=()):
+    def want(n):
+        return not only or n in only
+    if want("chain2"):
+        # RBD family, fixed-base 2Dof_arm (BASELINE config 5 shape: T = 100)
+        chain_case("chain2_t100", 2, rbd_initial_states(3, 2, seed0=0), T=100)
+        chain_case("chain2_nu1_t50", 1, rbd_initial_states(2, 2, seed0=10), T=50)
+        chain6_dynamics_case("chain6_dynamics")
+    if only:
+        return
     # headline family, short horizon: the literal recursion is healthy for T ≲ 16 (rounding asymmetry grows ~3×/step)
     lq, x, u = quadrotor_batch(4, T=16, seed0=0)
     lq_case("quad_t16", lq, x, u)
@@ -123,4 +197,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    main(tuple(sys.argv[1:]))

@@ -1,0 +1,175 @@
+"""CPU tests pinning the RBD-family oracle (oracle/rbd.py) and its host plumbing.
+
+RigidBodyDynamics.jl (the reference's dynamics library for
+test/RBD_2_link_example) is absent, so the restatement is pinned by known answers:
+  * the fixed-base 2Dof_arm.urdf has COMs on the joint origins and isotropic link
+    inertias (0.5·I), with zero gravity as the reference parses it
+    (RBD_helper_functions.jl:7): M(q) = diag(0.5 + 0.5 + 3·1², 0.5) = diag(4, 0.5)
+    for every q and dynamics_bias ≡ 0;
+  * on the coupled 6Dof_arm.urdf, M from the recursive Newton-Euler columns equals an
+    independent formulation Σ mJ_vᵀJ_v + J_ωᵀ I J_ω, is symmetric positive definite,
+    and RNEA(q, q̇, M⁻¹(τ − b)) = τ;
+  * the unforced rollout conserves kinetic energy (RK4 error only);
+  * the exact (forward-mode) Jacobians match central differences; the cost
+    derivatives match oracle.dual (the ForwardDiff restatement).
+"""
+import os
+
+import numpy as np
+import pytest
+
+from ilqr_amd import _lib
+from ilqr_amd.chain import (ChainProblem, chain_closures, load_robot, rbd_2dof_problem,
+                            rbd_initial_states)
+from ilqr_amd.urdf import parse_urdf, rpy_matrix
+from oracle import dual
+from oracle import rbd as RBD
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+REF_URDF = "/root/reference/test/urdf"
+
+
+@pytest.fixture(scope="module")
+def arm2():
+    return RBD.ChainModel(load_robot("2dof_arm"))
+
+
+@pytest.fixture(scope="module")
+def arm6():
+    return RBD.ChainModel(load_robot("6dof_arm"))
+
+
+def test_two_dof_closed_form(arm2):
+    rng = np.random.default_rng(0)
+    for _ in range(5):
+        q, qd = rng.uniform(-3, 3, 2), rng.uniform(-2, 2, 2)
+        assert np.allclose(arm2.mass_matrix_np(q), np.diag([4.0, 0.5]), atol=1e-14)
+        assert np.abs(arm2.bias_np(q, qd)).max() < 1e-14
+
+
+def test_six_dof_mass_matrix_independent_formulation(arm6):
+    rng = np.random.default_rng(1)
+    for _ in range(5):
+        q = rng.uniform(-3, 3, 6)
+        M = arm6.mass_matrix_np(q)
+        Mj = RBD.mass_matrix_jacobian(arm6.ch, q)
+        assert np.abs(M - Mj).max() < 1e-12 * np.abs(Mj).max()
+        assert np.abs(M - M.T).max() < 1e-12 * np.abs(M).max()
+        assert np.linalg.eigvalsh(M).min() > 0
+        # genuinely coupled (unlike the 2-DoF arm)
+        assert np.abs(M - np.diag(np.diag(M))).max() > 0.1
+
+
+def test_six_dof_rnea_inverts_forward_dynamics(arm6):
+    rng = np.random.default_rng(2)
+    q, qd, tau = rng.uniform(-2, 2, 6), rng.uniform(-1, 1, 6), rng.uniform(-3, 3, 6)
+    qdd = np.linalg.solve(arm6.mass_matrix_np(q), tau - arm6.bias_np(q, qd))
+    back = arm6.rnea([np.array([v]) for v in q], [np.array([v]) for v in qd],
+                     [np.array([v]) for v in qdd])
+    assert np.abs(np.array([v[0] for v in back]) - tau).max() < 1e-12
+
+
+def test_six_dof_energy_conservation(arm6):
+    rng = np.random.default_rng(3)
+    x = np.concatenate([rng.uniform(-1, 1, 6), rng.uniform(-1, 1, 6)])[None]
+    u = np.zeros((1, 6))
+    ke = lambda x: 0.5 * x[0, 6:] @ arm6.mass_matrix_np(x[0, :6]) @ x[0, 6:]
+    e0 = ke(x)
+    for _ in range(100):
+        x = arm6.step(x, u)
+    assert abs(ke(x) - e0) < 1e-8 * e0
+
+
+def test_exact_jacobians_match_central_differences(arm6):
+    rng = np.random.default_rng(4)
+    X, U = rng.uniform(-1, 1, (3, 12)), rng.uniform(-1, 1, (3, 6))
+    A, B = arm6.linearize(X, U)
+    h = 1e-6
+    Afd = np.stack([(arm6.step(X + h * np.eye(12)[k], U) - arm6.step(X - h * np.eye(12)[k], U)) / (2 * h)
+                    for k in range(12)], axis=2)
+    Bfd = np.stack([(arm6.step(X, U + h * np.eye(6)[k]) - arm6.step(X, U - h * np.eye(6)[k])) / (2 * h)
+                    for k in range(6)], axis=2)
+    assert np.abs(A - Afd).max() < 1e-8 and np.abs(B - Bfd).max() < 1e-8
+
+
+def test_cost_derivatives_match_forwarddiff_restatement():
+    pr = rbd_2dof_problem(2)
+    cost = RBD.ChainCost(pr.target, pr.q_weight, pr.r_weight, pr.qf_weight)
+    x, u = np.array([0.3, -0.2, 0.1, 0.05]), np.array([1.5, -0.7])
+    _, qv, r, Q, P, R = cost.quad(x, u)
+    assert np.allclose(qv, dual.gradient(lambda z: cost.immediate(z, u), x))
+    assert np.allclose(r, dual.gradient(lambda z: cost.immediate(x, z), u))
+    assert np.allclose(Q, dual.hessian(lambda z: cost.immediate(z, u), x))
+    assert np.allclose(R, dual.hessian(lambda z: cost.immediate(x, z), u))
+    _, g, H = cost.fquad(x)
+    assert np.allclose(g, dual.gradient(cost.final, x)) and np.allclose(H, dual.hessian(cost.final, x))
+    # nu = 1: only joint 1's torque is penalised
+    c1 = RBD.ChainCost(pr.target, pr.q_weight, pr.r_weight, pr.qf_weight)
+    assert c1.immediate(x, u[:1]) == pytest.approx(
+        np.sum(pr.q_weight * (pr.target - x[:2]) ** 2) + pr.r_weight[0] * u[0] ** 2)
+
+
+def test_reference_costs_restated():
+    """RBD_helper_functions.jl:85-116 on the joint rows and animate_RBD_2_link.jl:8-10."""
+    pr = rbd_2dof_problem(2)
+    assert pr.dt == 0.01 and tuple(pr.target) == (1.0, 0.3)
+    assert (pr.q_weight == 100.0).all() and (pr.r_weight == 10.0).all() and (pr.qf_weight == 1e6).all()
+    dyn, cost, fcost = chain_closures(pr)
+    x, u = np.array([0.5, 0.1, 0.0, 0.0]), np.array([1.0, 2.0])
+    assert cost(x, u) == pytest.approx(10.0 * (10 * 0.5 ** 2 + 10 * 0.2 ** 2) + (10 * 1 + 10 * 4))
+    assert fcost(x) == pytest.approx(1e5 * (10 * 0.5 ** 2 + 10 * 0.2 ** 2))
+
+
+@pytest.mark.skipif(not os.path.isdir(REF_URDF), reason="reference URDFs only in the build container")
+@pytest.mark.parametrize("name", ["2Dof_arm", "6Dof_arm"])
+def test_shipped_robots_match_the_reference_urdfs(name):
+    a, b = parse_urdf(os.path.join(REF_URDF, name + ".urdf")), load_robot(name.lower())
+    for f in ("R0", "p", "axis", "mass", "com", "Ic"):
+        assert np.array_equal(getattr(a, f), getattr(b, f)), f
+
+
+def test_urdf_conventions():
+    assert np.allclose(rpy_matrix([0, 0, np.pi / 2]) @ [1, 0, 0], [0, 1, 0])
+    assert np.allclose(rpy_matrix([np.pi / 2, 0, 0]) @ [0, 1, 0], [0, 0, 1])
+    ch = load_robot("2dof_arm")
+    assert ch.names == ["joint_1", "joint_2"]
+    assert np.allclose(ch.axis, [[0, 0, 1], [0, 1, 0]]) and np.allclose(ch.p, [[0.5, 0.5, 0], [1, 0, 0]])
+    # the massless tool link of the 6-DoF arm merges into link_6 without changing it
+    ch6 = load_robot("6dof_arm")
+    assert ch6.n == 6 and np.allclose(ch6.mass, 3.0)
+
+
+def test_golden_fixtures_consistent(arm2):
+    """Spot-check the frozen chain2 fixture against the oracle (same seeds)."""
+    z = np.load(os.path.join(GOLD, "chain2_t100.npz"), allow_pickle=False)
+    assert np.allclose(z["x"][:, 0], rbd_initial_states(3, 2, seed0=0))
+    A, B = arm2.linearize(z["x"][:, 5], z["u"][:, 5])
+    assert np.allclose(A, z["A"][:, 5], rtol=0, atol=1e-14) and np.allclose(B, z["B"][:, 5], atol=1e-14)
+    # the fixed-base arm is linear: A = block RK4 of a double integrator
+    assert np.allclose(A[0, :2, 2:], 0.01 * np.eye(2))
+
+
+def test_chain_struct_packing():
+    pr = rbd_2dof_problem(1)
+    s = pr.struct()
+    assert (s.n_joints, s.nu, s.dt) == (2, 1, 0.01)
+    assert list(s.axis[0]) == [0.0, 0.0, 1.0] and s.mass[1] == 3.0
+    assert s.qf_weight[0] == 1e6 and s.target[1] == 0.3
+    with pytest.raises(ValueError):
+        ChainProblem(load_robot("2dof_arm"), nu=3)
+
+
+def test_chain_abi_validates_without_gpu():
+    """Argument checks of ilqr_chain_create happen before any HIP call."""
+    import ctypes as C
+    lib = _lib.load()
+    s = rbd_2dof_problem(2).struct()
+    h = C.c_void_p()
+    assert lib.ilqr_chain_create(C.byref(h), 0, C.byref(s), 0, 8, _lib.F32, 0) == _lib.ERR_BAD_DIMS
+    assert lib.ilqr_chain_create(C.byref(h), 0, C.byref(s), 10, 8, 7, 0) == _lib.ERR_BAD_ARG
+    assert lib.ilqr_chain_create(C.byref(h), 0, C.byref(s), 10, 8, _lib.F32, 9) == _lib.ERR_BAD_ARG
+    s.nu = 3
+    assert lib.ilqr_chain_create(C.byref(h), 0, C.byref(s), 10, 8, _lib.F32, 0) == _lib.ERR_BAD_DIMS
+    assert lib.ilqr_chain_supported(2, 2) == 1 and lib.ilqr_chain_supported(2, 1) == 1
+    assert lib.ilqr_chain_supported(6, 6) == 0
+    assert lib.ilqr_supported(_lib.PROBLEM_CHAIN, 4, 2) == 1

@@ -1,0 +1,179 @@
+"""GPU parity tests of the RBD family (ILQR_PROBLEM_CHAIN) through the C ABI.
+
+Reference: test/RBD_2_link_example/RBD_helper_functions.jl (RK4 of
+v̇ = M \\ (−dynamics_bias + u), weighted joint costs) on test/urdf/2Dof_arm.urdf with a
+fixed base (BASELINE config 5), driven by src/backward_pass.jl / src/forward_pass.jl.
+Oracle: oracle.rbd (recursive Newton-Euler + RK4, exact Jacobians by forward-mode
+AD) through oracle.ilqr_oracle, frozen in tests/golden/chain2_*.npz and
+chain6_dynamics.npz (make_golden.py). RigidBodyDynamics.jl itself cannot run here:
+the oracle is pinned by known answers (tests/test_chain_oracle.py) — parity against
+the executed reference is unpinned.
+
+Tolerances, written per dtype and linearisation:
+  fp64, dual numbers: rollout 1e-12, A/B 1e-11, gains 1e-9, forward 1e-10, fit 1e-8
+    (the device uses FMA contraction and its own sincos: rounding-level differences);
+  fp64, central differences: A/B 1e-7 (truncation O(h²) with h = ε^⅓·max(1,|z|)),
+    gains 1e-6;
+  fp32 (BASELINE config 5), dual: rollout 2e-5, A/B 5e-5, gains 5e-4, forward 5e-4;
+  fp32, central differences: A/B 2e-2 (ε_f32^⅔ ≈ 2.4e-5 relative to the largest
+    entry, but entries of size ~dt² carry absolute error ~1e-5·max), gains 5e-3.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from ilqr_amd import _lib
+from ilqr_amd.chain import (ChainSolver, chain_closures, load_robot, rbd_2dof_problem,
+                            ChainProblem)
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def rel(a, b):
+    a = a.double().cpu().numpy() if isinstance(a, torch.Tensor) else np.asarray(a, float)
+    b = b.double().cpu().numpy() if isinstance(b, torch.Tensor) else np.asarray(b, float)
+    return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-300))
+
+
+def dev(a, dtype):
+    return torch.as_tensor(np.ascontiguousarray(a)).to("cuda", dtype).contiguous()
+
+
+def load(name):
+    z = np.load(os.path.join(GOLD, name + ".npz"), allow_pickle=False)
+    return {k: z[k] for k in z.files}
+
+
+@pytest.fixture(scope="module")
+def g2():
+    return load("chain2_t100")
+
+
+@pytest.fixture(scope="module")
+def g1():
+    return load("chain2_nu1_t50")
+
+
+TOL = {  # (dtype, linearisation) → tolerances
+    (torch.float64, "dual"): dict(roll=1e-12, AB=1e-11, gain=1e-9, fw=1e-10),
+    (torch.float64, "fd"): dict(roll=1e-12, AB=1e-7, gain=1e-6, fw=1e-6),
+    (torch.float32, "dual"): dict(roll=2e-5, AB=5e-5, gain=5e-4, fw=5e-4),
+    (torch.float32, "fd"): dict(roll=2e-5, AB=2e-2, gain=5e-3, fw=5e-3),
+}
+CASES = list(TOL)
+
+
+def solver(g, dtype, lin, nu=2):
+    nb, T = g["u"].shape[:2]
+    return ChainSolver(rbd_2dof_problem(nu), T, nb, dtype=dtype, linearization=lin)
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_chain_rollout(gpu, g2, dtype):
+    """dynamicsf (RNEA + RK4 functor) rollout from x₀ with u = 0."""
+    s = solver(g2, dtype, "dual")
+    x = s.rollout(dev(g2["x"][:, 0], dtype), dev(g2["u"], dtype))
+    assert rel(x, g2["x"]) < TOL[(dtype, "dual")]["roll"]
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_chain6_dynamics(gpu, dtype):
+    """One RK4 step of the coupled 6-DoF arm (test/urdf/6Dof_arm.urdf) vs the oracle."""
+    g = load("chain6_dynamics")
+    pr = ChainProblem(load_robot("6dof_arm"), 6, 0.01)
+    s = ChainSolver(pr, 1, 1, dtype=dtype)
+    xn = s.dynamics(dev(g["x"], dtype), dev(g["u"], dtype))
+    assert rel(xn, g["x_next"]) < (1e-12 if dtype == torch.float64 else 5e-5)
+    # the state moved: a wrong M or bias would show in the velocity rows
+    assert rel(xn[:, 6:], g["x_next"][:, 6:]) < (1e-12 if dtype == torch.float64 else 5e-5)
+
+
+@pytest.mark.parametrize("dtype,lin", CASES)
+def test_chain_linearize(gpu, g2, dtype, lin):
+    """linearize_dynamics (backward_pass.jl:25-40) at every (b, t)."""
+    s = solver(g2, dtype, lin)
+    A, B = s.linearize(dev(g2["x"], dtype), dev(g2["u"], dtype))
+    t = TOL[(dtype, lin)]["AB"]
+    assert rel(A, g2["A"]) < t and rel(B, g2["B"]) < t, (rel(A, g2["A"]), rel(B, g2["B"]))
+
+
+@pytest.mark.parametrize("dtype,lin", CASES)
+def test_chain_backward(gpu, g2, dtype, lin):
+    """backward_pass (backward_pass.jl:324-357) gains vs the oracle."""
+    s = solver(g2, dtype, lin)
+    d, K, st = s.backward(dev(g2["x"], dtype), dev(g2["u"], dtype))
+    assert (st.cpu().numpy() == 0).all()
+    t = TOL[(dtype, lin)]["gain"]
+    assert rel(K, g2["K"]) < t and rel(d, g2["d"]) < t, (rel(K, g2["K"]), rel(d, g2["d"]))
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_chain_forward(gpu, g2, dtype):
+    """forward_pass (forward_pass.jl:55-93) from the oracle's gains, prev_cost = Inf."""
+    s = solver(g2, dtype, "dual")
+    nb = g2["u"].shape[0]
+    pc = torch.full((nb,), float("inf"), dtype=dtype, device="cuda")
+    xn, un, c, tr, st = s.forward(dev(g2["x"], dtype), dev(g2["u"], dtype), dev(g2["d"], dtype),
+                                  dev(g2["K"], dtype), pc)
+    t = TOL[(dtype, "dual")]["fw"]
+    assert (tr.cpu().numpy() == 1).all() and (st.cpu().numpy() == 0).all()
+    assert rel(xn, g2["fw_x"]) < t and rel(un, g2["fw_u"]) < t and rel(c, g2["fw_cost"]) < t
+
+
+def test_chain_fit_f64(gpu, g2):
+    """fit (forward_pass.jl:148-179): same iteration counts, iterates and costs."""
+    s = solver(g2, torch.float64, "dual")
+    r = s.fit(dev(g2["x"], torch.float64), dev(g2["u"], torch.float64), max_iter=20, tol=1e-6)
+    assert np.array_equal(r.iters.cpu().numpy(), g2["fit_iters"])
+    assert (r.status.cpu().numpy() == g2["fit_status"]).all()
+    assert rel(r.x, g2["fit_x"]) < 1e-8 and rel(r.u, g2["fit_u"]) < 1e-8
+    last = g2["fit_cost"][np.arange(len(g2["fit_iters"])), g2["fit_iters"] - 1]
+    assert rel(r.cost, last) < 1e-10
+
+
+@pytest.mark.parametrize("lin", ["dual", "fd"])
+def test_chain_fit_f32(gpu, g2, lin):
+    """BASELINE config 5 precision (fp32): the fit reaches the oracle's optimum."""
+    s = solver(g2, torch.float32, lin)
+    r = s.fit(dev(g2["x"], torch.float32), dev(g2["u"], torch.float32), max_iter=20, tol=1e-6)
+    st = r.status.cpu().numpy()
+    assert set(st.tolist()) <= {_lib.TRAJ_CONVERGED, _lib.TRAJ_LS_EXHAUSTED}, st
+    last = g2["fit_cost"][np.arange(len(g2["fit_iters"])), g2["fit_iters"] - 1]
+    assert rel(r.cost, last) < 1e-4
+    assert rel(r.u, g2["fit_u"]) < 2e-3
+
+
+def test_chain_nu1(gpu, g1):
+    """nu = 1 (joint 1 driven only): gains, forward pass and the fit iterate (fp64).
+    The oracle's trajectory 0 reaches a stationary point where the reference's line
+    search would loop forever; either stop (converged / exhausted) returns the same
+    iterate."""
+    s = solver(g1, torch.float64, "dual", nu=1)
+    x, u = dev(g1["x"], torch.float64), dev(g1["u"], torch.float64)
+    d, K, _ = s.backward(x, u)
+    assert rel(K, g1["K"]) < 1e-9 and rel(d, g1["d"]) < 1e-9
+    nb = u.shape[0]
+    pc = torch.full((nb,), float("inf"), dtype=torch.float64, device="cuda")
+    xn, un, c, _, _ = s.forward(x, u, dev(g1["d"], torch.float64), dev(g1["K"], torch.float64), pc)
+    assert rel(xn, g1["fw_x"]) < 1e-10 and rel(c, g1["fw_cost"]) < 1e-10
+    r = s.fit(x, u, max_iter=20, tol=1e-6)
+    assert set(r.status.cpu().numpy().tolist()) <= {_lib.TRAJ_CONVERGED, _lib.TRAJ_LS_EXHAUSTED}
+    assert rel(r.x, g1["fit_x"]) < 1e-8 and rel(r.u, g1["fit_u"]) < 1e-8
+
+
+def test_chain_api_mirror_keeps_eltype(gpu, g2):
+    """ilqr_amd.fit with the chain closures: Float32 inputs solve in fp32 (the reference
+    is generic in the element type), Float64 in fp64."""
+    import ilqr_amd
+    dyn, cost, fcost = chain_closures(rbd_2dof_problem(2))
+    x32 = g2["x"][0].astype(np.float32)
+    u32 = g2["u"][0].astype(np.float32)
+    xo, uo = ilqr_amd.fit(x32, u32, dyn, cost, fcost, max_iter=20, tol=1e-6)
+    assert uo.dtype == np.float32 and rel(uo, g2["fit_u"][0]) < 2e-3
+    xo, uo = ilqr_amd.fit(g2["x"][0], g2["u"][0], dyn, cost, fcost, max_iter=20, tol=1e-6)
+    assert uo.dtype == np.float64 and rel(uo, g2["fit_u"][0]) < 1e-8
+    d, K = ilqr_amd.backward_pass(g2["x"][0], g2["u"][0], dyn, cost, fcost)
+    assert rel(K, g2["K"][0]) < 1e-9

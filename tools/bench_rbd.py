@@ -1,0 +1,120 @@
+"""Secondary benchmark: BASELINE config 5 — the RBD example (RigidBodyDynamics-style
+dynamics of test/urdf/2Dof_arm.urdf, fixed base: nx = 4, nu = 2 or 1), T = 100,
+batch 2048 random x₀, fp32, linearised on the device by central finite differences
+(BASELINE's wording) or dual numbers (the reference's ForwardDiff). Same step as
+bench.py: one cold-start fit iteration over the batch (linearise + backward +
+forward with line search), timed with HIP events on torch's current stream.
+Prints one JSON line per linearisation. The CPU baseline is the oracle
+(oracle/rbd.py, numpy, 1 core) on a bounded sample — a port, not the reference.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "ilqr.jl_amd")]
+
+from ilqr_amd import _lib  # noqa: E402
+from ilqr_amd.chain import ChainSolver, rbd_2dof_problem, rbd_initial_states  # noqa: E402
+
+
+def timed(fn, n, stream):
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(n):
+        fn()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / n
+
+
+def cpu_baseline(pr, x, u, budget_s):
+    """oracle/rbd.py + oracle/ilqr_oracle.py: one cold-start iteration per trajectory."""
+    from oracle import ilqr_oracle as O
+    from oracle import rbd as RBD
+    model = RBD.ChainModel(pr.chain, pr.dt)
+    cost = RBD.ChainCost(pr.target, pr.q_weight, pr.r_weight, pr.qf_weight)
+    f, l, lf = RBD.chain_closures(model, cost)
+    n, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < budget_s and n < x.shape[0]:
+        d, K = O.backward_pass(x[n], u[n], f, l, lf)
+        O.forward_pass(x[n], u[n], np.zeros_like(x[n]), d, K, np.inf, f, l, lf, max_trials=60)
+        n += 1
+    el = time.perf_counter() - t0
+    return {"value": n / el / x.shape[0], "unit": f"batched iterations/s (batch={x.shape[0]})",
+            "cores": 1, "kind": "port",
+            "sample": f"{n} trajectories x 1 cold-start iteration (numpy oracle oracle/rbd.py, fp64, "
+                      f"1 core), {el:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=100)
+    ap.add_argument("--batch", type=int, default=2048)
+    ap.add_argument("--T", type=int, default=100)
+    ap.add_argument("--nu", type=int, default=2)
+    ap.add_argument("--dtype", default="f32", choices=["f32", "f64"])
+    ap.add_argument("--lin", default="fd,dual")
+    ap.add_argument("--cpu-budget", type=float, default=10.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+    B, T = args.batch, args.T
+    dt = torch.float32 if args.dtype == "f32" else torch.float64
+    dev = torch.device("cuda", 0)
+    pr = rbd_2dof_problem(args.nu)
+    x0 = rbd_initial_states(B, 2)
+    base = None
+    for lin in args.lin.split(","):
+        s = ChainSolver(pr, T, B, dtype=dt, linearization=lin)
+        u = torch.zeros((B, T, pr.nu), dtype=dt, device=dev)
+        x = s.rollout(torch.from_numpy(x0).to(dev, dt), u)
+        xn, un = torch.empty_like(x), torch.empty_like(u)
+        pc = torch.empty((B,), dtype=dt, device=dev)
+        st = torch.zeros((B,), dtype=torch.int32, device=dev)
+        trials = torch.empty((B,), dtype=torch.int32, device=dev)
+        opts = _lib.default_options(tol=-1.0)
+        stream = torch.cuda.current_stream(dev)
+        s._bind()
+
+        def step():
+            s.iterate(x, u, xn, un, None, st, pc, trials=trials, options=opts)
+
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ms_ev = timed(step, args.steps, stream)
+        ms = max(ms_ev, (time.perf_counter() - t0) * 1000.0 / args.steps)
+        ok = bool((st == 0).all().item())
+        res = {"metric": f"batched iLQR iterations/sec (fwd+bwd pass), RBD 2-DoF arm fixed base, "
+                         f"nx=4 nu={pr.nu} T={T}",
+               "value": 1000.0 / ms, "unit": f"batched iterations/s (batch={B})", "n_gpus": 1,
+               "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms,
+               "higher_is_better": True, "dtype": args.dtype, "data": "synthetic x0 ~ U(-1,1)",
+               "config": {"workload": "BASELINE config 5 (RBD_2_link_example, fixed base)",
+                          "batch": B, "T": T, "linearization": lin},
+               "traj_iters_per_s": B * 1000.0 / ms,
+               "mean_line_search_trials": float(trials.double().mean().item()), "all_ok": ok,
+               "cpu_baseline": None}
+        if not args.no_cpu:
+            if base is None:
+                xs = x[: min(B, 64)].double().cpu().numpy()
+                us = u[: min(B, 64)].double().cpu().numpy()
+                base = cpu_baseline(pr, xs, us, args.cpu_budget)
+                base["unit"] = f"batched iterations/s (batch={B})"
+                base["value"] = base["value"] * min(B, 64) / B
+            res["cpu_baseline"] = base
+        print(json.dumps(res), flush=True)
+        s.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -29,6 +29,9 @@ case $WHAT in
   tiles) step pytest_tiles 600 python -m pytest tests/test_gpu_tiles.py -x -q ;;
   tlbench) step bench_twolink 300 python tools/bench_twolink.py ;;
   tlprof) step rocprof_twolink 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_tl -o run --output-format csv -- python tools/bench_twolink.py --steps 20 --warmup 2 --no-cpu ;;
+  chain) step pytest_chain 600 python -u -m pytest tests/test_gpu_chain.py -x -v --timeout 120 --timeout-method thread ;;
+  rbdbench) step bench_rbd 300 python tools/bench_rbd.py ;;
+  rbdprof) step rocprof_rbd 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_rbd -o run --output-format csv -- python tools/bench_rbd.py --steps 20 --warmup 5 --no-cpu ;;
   rcp) step rcp 60 ./tools/rcp_test ;;
   ubench) step ubench 120 ./tools/ubench_f64 ;;
 esac
