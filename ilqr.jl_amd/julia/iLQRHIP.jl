@@ -178,4 +178,50 @@ function solve!(prob::iLQRProblem; max_iter::Int64=100, tol::Float64=1e-6)
     return prob
 end
 
+# -- RBD family (ILQR_PROBLEM_CHAIN): test/RBD_2_link_example with a fixed base --------
+const ILQR_F64 = Int32(0)
+const ILQR_F32 = Int32(1)
+const ILQR_LINEARIZE_DUAL = Int32(0)
+const ILQR_LINEARIZE_CENTRAL_FD = Int32(1)
+
+struct Chain                 # ilqr_chain (include/ilqr.h), ILQR_CHAIN_MAX_JOINTS = 8
+    n_joints::Int32; nu::Int32; dt::Float64; gravity::NTuple{3,Float64}
+    joint_rot::NTuple{72,Float64}; joint_pos::NTuple{24,Float64}; axis::NTuple{24,Float64}
+    mass::NTuple{8,Float64}; com::NTuple{24,Float64}; inertia::NTuple{72,Float64}
+    target::NTuple{8,Float64}; q_weight::NTuple{8,Float64}; r_weight::NTuple{8,Float64}
+    qf_weight::NTuple{8,Float64}
+end
+
+"""chain_fit(chain, x_init, u_init; max_iter, tol, linearization) → (x̄, ū, status)
+
+Batched fit of the chain family; x_init (nx, T+1, batch), u_init (nu, T, batch) as
+Array{Float32,3} (fp32, BASELINE config 5) or Array{Float64,3}: the element type picks
+the device precision, as the reference's generic Julia code would."""
+function chain_fit(c::Chain, x_init::Array{E,3}, u_init::Array{E,3}; max_iter::Int64=100,
+                   tol::Float64=1e-6, linearization=ILQR_LINEARIZE_DUAL) where {E<:Union{Float32,Float64}}
+    nx, N, nb = size(x_init); nu = size(u_init, 1); M = N - 1
+    @assert(size(u_init, 2) == M)
+    r = Ref{Ptr{Cvoid}}(C_NULL)
+    dt = E === Float32 ? ILQR_F32 : ILQR_F64
+    check(ccall((:ilqr_chain_create, libilqr), Cint,
+                (Ref{Ptr{Cvoid}}, Cint, Ref{Chain}, Cint, Cint, Int32, Int32),
+                r, 0, c, M, nb, dt, linearization), "ilqr_chain_create")
+    h = Handle(nx, nu, M, 1)                 # device-memory helper only
+    dev(a) = (p = alloc(h, E, length(a));
+              check(ccall((:ilqr_memcpy_h2d, libilqr), Cint, (Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Csize_t),
+                          h.ptr, p, a, sizeof(a)), "ilqr_memcpy_h2d"); p)
+    xi = dev(x_init); ui = dev(u_init)
+    xo = alloc(h, E, length(x_init)); uo = alloc(h, E, length(u_init)); sd = alloc(h, Int32, nb)
+    o = default_options(); o.max_iter = max_iter; o.tol = tol
+    st = ccall((:ilqr_chain_fit, libilqr), Cint,
+               (Ptr{Cvoid}, Ref{Options}, Ptr{E}, Ptr{E}, Ptr{E}, Ptr{E}, Ptr{E}, Ptr{E}, Ptr{Int32}, Ptr{Int32}),
+               r[], o, xi, ui, C_NULL, xo, uo, C_NULL, C_NULL, sd)
+    st == ILQR_ERR_NAN && throw(AssertionError("!any(isnan, ...)"))
+    st == ILQR_ERR_LS_EXHAUSTED || check(st, "ilqr_chain_fit")
+    x = download!(h, similar(x_init), xo); u = download!(h, similar(u_init), uo)
+    status = download!(h, zeros(Int32, nb), sd)
+    ccall((:ilqr_chain_destroy, libilqr), Cint, (Ptr{Cvoid},), r[])
+    return x, u, status
+end
+
 end # module
