@@ -33,6 +33,11 @@ struct ilqr_handle {
   // runs on `side` while chunk i+1's backward runs on `stream`
   hipStream_t side = nullptr;
   int nchunks = 1;
+  // LQ family schedule (ilqr_set_schedule): fit through the pipelined kernel (forward
+  // of half the workgroups overlapping the backward of the other half), and the
+  // forward of sequential iterations through the LDS-ring kernel
+  bool pipelined = false;
+  bool fw_ring = true;
   int bound[3] = {0, 0, 0};
   hipEvent_t ev_bw[2] = {nullptr, nullptr};
   hipEvent_t ev_fw[2] = {nullptr, nullptr};
@@ -98,7 +103,7 @@ ilqr_status enqueue_iteration(ilqr_handle* h, const ilqr_problem* p, const ilqr:
   const ilqr::LQParams P = lq_params(p);
   if (h->nchunks == 1) {  // one stream, no cross-stream events (each hand-off costs ~10 µs)
     HIP_TRY(ilqr::launch_lq_iter_backward(h->nx, h->nu, P, 0, h->batch, h->T, a, ls.mu, h->stream));
-    HIP_TRY(ilqr::launch_lq_iter_forward(h->nx, h->nu, P, 0, h->batch, h->T, a, ls, h->stream));
+    HIP_TRY(ilqr::launch_lq_iter_forward(h->nx, h->nu, P, 0, h->batch, h->T, a, ls, h->stream, h->fw_ring));
     return ILQR_OK;
   }
   for (int c = 0; c < h->nchunks; ++c) {
@@ -265,6 +270,13 @@ ilqr_status ilqr_set_stream(ilqr_handle* h, void* s) {
   return ILQR_OK;
 }
 
+ilqr_status ilqr_set_schedule(ilqr_handle* h, int flags) {
+  if (!h || (flags & ~(ILQR_SCHED_PIPELINED | ILQR_SCHED_RING_FORWARD)) != 0) return ILQR_ERR_BAD_ARG;
+  h->pipelined = (flags & ILQR_SCHED_PIPELINED) != 0;
+  h->fw_ring = (flags & ILQR_SCHED_RING_FORWARD) != 0;
+  return ILQR_OK;
+}
+
 ilqr_status ilqr_sync(ilqr_handle* h) {
   if (!h) return ILQR_ERR_BAD_ARG;
   HIP_TRY(hipStreamSynchronize(h->stream));
@@ -378,8 +390,7 @@ ilqr_status ilqr_fit(ilqr_handle* h, const ilqr_problem* p, const ilqr_options* 
   HIP_TRY(ilqr::launch_fill_i32(h->res_parity, h->batch, 0, s));
   HIP_TRY(ilqr::launch_fill_i32(h->iters, h->batch, 0, s));
   const ilqr::LSParams ls = ls_params(o);
-  int par = 0;
-  for (int it = 1; it <= o->max_iter; ++it) {  // forward_pass.jl:161
+  auto iter_args = [&](int it, int par) {
     ilqr::IterArgs a{};
     a.x = h->xbuf[par];
     a.u = h->ubuf[par];
@@ -397,8 +408,27 @@ ilqr_status ilqr_fit(ilqr_handle* h, const ilqr_problem* p, const ilqr_options* 
     a.iters = h->iters;
     a.parity = par;
     a.iter = it;
+    return a;
+  };
+  int par = 0;
+  if (!two_link(p) && h->pipelined) {
+    // iteration `it` reads buffer parity (it−1)&1. Launch `it` runs iteration it for
+    // role-B workgroups and forward(it−1) + backward(it) for role A; launch
+    // max_iter+1 drains A's last forward.
+    for (int it = 1; it <= o->max_iter + 1; ++it) {
+      int flags = 0;
+      if (it <= o->max_iter) flags |= ilqr::PIPE_A_BW_FLAG | ilqr::PIPE_B_FLAG;
+      if (it >= 2) flags |= ilqr::PIPE_A_FW_FLAG;
+      if (!flags) continue;
+      HIP_TRY(ilqr::launch_lq_iter_pipe(h->nx, h->nu, lq_params(p), h->batch, h->T,
+                                        iter_args(it, (it - 1) & 1), iter_args(it - 1, it & 1), ls,
+                                        flags, s));
+    }
+    par = o->max_iter & 1;
+  }
+  for (int it = 1; (two_link(p) || !h->pipelined) && it <= o->max_iter; ++it) {  // forward_pass.jl:161
     // iterations chain per chunk: chunk 0's next backward overlaps chunk 1's forward
-    const ilqr_status st = enqueue_iteration(h, p, a, ls, /*chain=*/true);
+    const ilqr_status st = enqueue_iteration(h, p, iter_args(it, par), ls, /*chain=*/true);
     if (st != ILQR_OK) return st;
     par ^= 1;  // x̄ⁱ, ūⁱ = x̄ⁱ⁺¹, ūⁱ⁺¹ (:174-175)
   }

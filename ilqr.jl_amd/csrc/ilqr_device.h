@@ -9,7 +9,8 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 typedef unsigned u2v __attribute__((ext_vector_type(2)));
 
 constexpr int WAVES_PER_WG = 4;   // trajectories per workgroup
-constexpr int BW_LDS = 96 + 16 * 17 + 64;  // doubles of backward scratch per wave: [G|H] rows, g row, zero, S tile, junk row
+constexpr int YT_OFF = 96 + 16 * 17 + 64;  // Y all-gather tile (VALU products): 16 columns × 14
+constexpr int BW_LDS = YT_OFF + 16 * 14;   // doubles of backward scratch per wave: [G|H] rows, g row, zero, S tile, junk row, Y tile
 constexpr int SYM_EVERY = 8;          // symmetrise S every this many steps
 
 __device__ __forceinline__ d4 mfma(double a, double b, d4 c) {

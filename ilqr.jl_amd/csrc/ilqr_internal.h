@@ -57,7 +57,14 @@ hipError_t launch_lq_forward(int nx, int nu, const LQParams& p, int B, int T, co
 hipError_t launch_lq_iter_backward(int nx, int nu, const LQParams& p, int b0, int b1, int T,
                                    const IterArgs& a, double mu, hipStream_t s);
 hipError_t launch_lq_iter_forward(int nx, int nu, const LQParams& p, int b0, int b1, int T,
-                                  const IterArgs& a, const LSParams& ls, hipStream_t s);
+                                  const IterArgs& a, const LSParams& ls, hipStream_t s,
+                                  bool ring = false);
+// Pipelined fit iteration (DESIGN.md §fit driver): role-B workgroups run iteration
+// `cur` (backward then forward), role-A workgroups the forward of iteration `prev`
+// then the backward of `cur`; flags select the phases (PIPE_* below).
+constexpr int PIPE_A_FW_FLAG = 1, PIPE_A_BW_FLAG = 2, PIPE_B_FLAG = 4;
+hipError_t launch_lq_iter_pipe(int nx, int nu, const LQParams& p, int B, int T, const IterArgs& cur,
+                               const IterArgs& prev, const LSParams& ls, int flags, hipStream_t s);
 // x_out[b] = (res_parity[b] ? x1 : x0)[b] (and u); status MAX_ITER for still-running ones.
 hipError_t launch_gather_result(int B, int T, int nx, int nu, const double* x0, const double* u0,
                                 const double* x1, const double* u1, const int32_t* res_parity,

@@ -38,6 +38,128 @@
 namespace ilqr {
 namespace {
 
+// VALU replacement of the Y = Sp·F and Z = L + FᵀY MFMAs:
+// on gfx950 f64 VALU FMAs with a DPP64 row broadcast sustain 58 TF/s at 4 waves/SIMD
+// against 42 TF/s for v_mfma_f64_16x16x4 (profiles/r01/ubench_{f64,dpp}.log).
+// y[r] += Σ_k bcast_k(s[r]) · f[k]: lane (q, c) holds Sp[q+4r][c] in s[r] and
+// F[k][c] in f[k], so y[r] = (Sp F)[q+4r][c] — the MFMA accumulator layout.
+// The leading s_nops give the f64 MFMA that produced s[] its VALU-read wait states.
+[[maybe_unused]] __device__ __forceinline__ void dpp_sf4(double& y0, double& y1, double& y2, double& y3, double s0,
+                                        double s1, double s2, double s3, const double (&f)[12]) {
+  asm volatile(
+      "s_nop 7\n\t"
+      "s_nop 7\n\t"
+      "s_nop 4\n\t"
+      "v_fmac_f64_dpp %[y0], %[s0], %[f0] row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[y1], %[s1], %[f0] row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[y2], %[s2], %[f0] row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[y3], %[s3], %[f0] row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[y0], %[s0], %[f1] row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[y1], %[s1], %[f1] row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[y2], %[s2], %[f1] row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[y3], %[s3], %[f1] row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[y0], %[s0], %[f2] row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[y1], %[s1], %[f2] row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[y2], %[s2], %[f2] row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[y3], %[s3], %[f2] row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[y0], %[s0], %[f3] row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[y1], %[s1], %[f3] row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[y2], %[s2], %[f3] row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[y3], %[s3], %[f3] row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[y0], %[s0], %[f4] row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[y1], %[s1], %[f4] row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[y2], %[s2], %[f4] row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[y3], %[s3], %[f4] row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[y0], %[s0], %[f5] row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[y1], %[s1], %[f5] row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[y2], %[s2], %[f5] row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[y3], %[s3], %[f5] row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[y0], %[s0], %[f6] row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[y1], %[s1], %[f6] row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[y2], %[s2], %[f6] row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[y3], %[s3], %[f6] row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[y0], %[s0], %[f7] row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[y1], %[s1], %[f7] row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[y2], %[s2], %[f7] row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[y3], %[s3], %[f7] row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[y0], %[s0], %[f8] row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[y1], %[s1], %[f8] row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[y2], %[s2], %[f8] row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[y3], %[s3], %[f8] row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[y0], %[s0], %[f9] row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[y1], %[s1], %[f9] row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[y2], %[s2], %[f9] row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[y3], %[s3], %[f9] row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[y0], %[s0], %[f10] row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[y1], %[s1], %[f10] row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[y2], %[s2], %[f10] row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[y3], %[s3], %[f10] row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[y0], %[s0], %[f11] row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[y1], %[s1], %[f11] row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[y2], %[s2], %[f11] row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[y3], %[s3], %[f11] row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+      : [y0] "+v"(y0), [y1] "+v"(y1), [y2] "+v"(y2), [y3] "+v"(y3)
+      : [s0] "v"(s0), [s1] "v"(s1), [s2] "v"(s2), [s3] "v"(s3), [f0] "v"(f[0]), [f1] "v"(f[1]), [f2] "v"(f[2]), [f3] "v"(f[3]), [f4] "v"(f[4]), [f5] "v"(f[5]), [f6] "v"(f[6]), [f7] "v"(f[7]), [f8] "v"(f[8]), [f9] "v"(f[9]), [f10] "v"(f[10]), [f11] "v"(f[11]));
+}
+// z[r] += Σ_k bcast_{4r}(p[k]) · f[k] where lane (q, m) holds column (m + q) mod 16 of Y
+// in p[] (so lane 4r of row q holds column q + 4r) and F[k][c] in f[k]:
+// z[r] = (FᵀY)[c][q+4r] = Z[q+4r][c] by the symmetry of Z = FᵀSF (rounding aside).
+[[maybe_unused]] __device__ __forceinline__ void dpp_fy4(double& z0, double& z1, double& z2, double& z3,
+                                        const double (&p)[12], const double (&f)[12]) {
+  asm volatile(
+      "s_nop 4\n\t"
+      "v_fmac_f64_dpp %[z0], %[p0], %[f0] row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[z1], %[p0], %[f0] row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[z2], %[p0], %[f0] row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[z3], %[p0], %[f0] row_newbcast:12 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[z0], %[p1], %[f1] row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[z1], %[p1], %[f1] row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[z2], %[p1], %[f1] row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[z3], %[p1], %[f1] row_newbcast:12 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[z0], %[p2], %[f2] row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[z1], %[p2], %[f2] row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[z2], %[p2], %[f2] row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[z3], %[p2], %[f2] row_newbcast:12 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[z0], %[p3], %[f3] row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[z1], %[p3], %[f3] row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[z2], %[p3], %[f3] row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[z3], %[p3], %[f3] row_newbcast:12 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[z0], %[p4], %[f4] row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[z1], %[p4], %[f4] row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[z2], %[p4], %[f4] row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[z3], %[p4], %[f4] row_newbcast:12 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[z0], %[p5], %[f5] row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[z1], %[p5], %[f5] row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[z2], %[p5], %[f5] row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[z3], %[p5], %[f5] row_newbcast:12 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[z0], %[p6], %[f6] row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[z1], %[p6], %[f6] row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[z2], %[p6], %[f6] row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[z3], %[p6], %[f6] row_newbcast:12 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[z0], %[p7], %[f7] row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[z1], %[p7], %[f7] row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[z2], %[p7], %[f7] row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[z3], %[p7], %[f7] row_newbcast:12 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[z0], %[p8], %[f8] row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[z1], %[p8], %[f8] row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[z2], %[p8], %[f8] row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[z3], %[p8], %[f8] row_newbcast:12 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[z0], %[p9], %[f9] row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[z1], %[p9], %[f9] row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[z2], %[p9], %[f9] row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[z3], %[p9], %[f9] row_newbcast:12 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[z0], %[p10], %[f10] row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[z1], %[p10], %[f10] row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[z2], %[p10], %[f10] row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[z3], %[p10], %[f10] row_newbcast:12 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[z0], %[p11], %[f11] row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[z1], %[p11], %[f11] row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[z2], %[p11], %[f11] row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[z3], %[p11], %[f11] row_newbcast:12 row_mask:0xf bank_mask:0xf\n\t"
+      : [z0] "+v"(z0), [z1] "+v"(z1), [z2] "+v"(z2), [z3] "+v"(z3)
+      : [p0] "v"(p[0]), [p1] "v"(p[1]), [p2] "v"(p[2]), [p3] "v"(p[3]), [p4] "v"(p[4]), [p5] "v"(p[5]), [p6] "v"(p[6]), [p7] "v"(p[7]), [p8] "v"(p[8]), [p9] "v"(p[9]), [p10] "v"(p[10]), [p11] "v"(p[11]), [f0] "v"(f[0]), [f1] "v"(f[1]), [f2] "v"(f[2]), [f3] "v"(f[3]), [f4] "v"(f[4]), [f5] "v"(f[5]), [f6] "v"(f[6]), [f7] "v"(f[7]), [f8] "v"(f[8]), [f9] "v"(f[9]), [f10] "v"(f[10]), [f11] "v"(f[11]));
+}
+
 // ---------------------------------------------------------------------------
 // Backward pass of one trajectory by one wave (backward_pass.jl:324-357).
 // Writes d (T,NU) and K (T,NU,NX) of trajectory b. Returns true if any gain is NaN
@@ -82,6 +204,19 @@ __device__ bool lq_backward_wave(const LQParams& P, int b, int T, const double* 
     const double a = ldz(ri && cx, Ab + ii * NX + ci, Ab);
     const double bb = ldz(ri && cu, Bb + ii * NU + cj, Bb);
     fB[kk] = a + bb;
+  }
+  // VYZ (ABL bit 1024): the Y and Z products on the VALU (dpp_sf4 / dpp_fy4); this
+  // lane keeps its whole column of F, Fo[k] = F[k][c]
+  constexpr bool VYZ = (ABL & 1024) != 0;
+  static_assert(!VYZ || NX == 12, "dpp_sf4/dpp_fy4 are written for nx = 12");
+  double Fo[VYZ ? NX : 1];
+  if constexpr (VYZ) {
+#pragma unroll
+    for (int k = 0; k < NX; ++k) {
+      const double a = ldz(cx, Ab + k * NX + ci, Ab);
+      const double bb = ldz(cu, Bb + k * NU + cj, Bb);
+      Fo[k] = a + bb;
+    }
   }
   // Cost Hessian L = blockdiag(Q+Qᵀ, R+Rᵀ) in accumulator layout: Lc[r] = L[q+4r][c]
   // (immediate_cost_quadratization :101-106 of ℓ = xᵀQx + uᵀRu: 𝐐 = Q+Qᵀ, 𝐑 = R+Rᵀ, 𝐏 = 0)
@@ -165,13 +300,39 @@ __device__ bool lq_backward_wave(const LQParams& P, int b, int T, const double* 
     const d4 zn = load_z(t > 0 ? t - 1 : 0);
 
     // Y = Sp · F (optimal_controller_param's S'A, S'B and the row sᵀF)
-    d4 Y = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-    for (int kk = 0; kk < KS; ++kk) Y = mfma(Sp[kk], fB[kk], Y);
     // Z = L + Fᵀ Y = [[lxx + AᵀSA, AᵀSB], [BᵀSA, luu + BᵀSB]]  (:182-183, first terms of :270)
+    d4 Y = {0.0, 0.0, 0.0, 0.0};
     d4 Z = Lc;
+    if constexpr (VYZ) {
+      double y0 = 0.0, y1 = 0.0, y2 = 0.0, y3 = 0.0;
+      dpp_sf4(y0, y1, y2, y3, Sp[0], Sp[1], Sp[2], Sp[3], Fo);
+      Y = d4{y0, y1, y2, y3};
+      // all-gather Y's columns through LDS: column-major, stride 14 (16-B aligned rows
+      // 0..12 + one junk slot taking the nonexistent rows 13..15)
+      double* yt = lds + YT_OFF;
 #pragma unroll
-    for (int kk = 0; kk < KS; ++kk) Z = mfma(fB[kk], Y[kk], Z);
+      for (int r = 0; r < 4; ++r) {
+        const int i = q + 4 * r;
+        yt[c * 14 + (i <= SROW ? i : 13)] = Y[r];
+      }
+      wave_lds_fence();
+      const double2* col = reinterpret_cast<const double2*>(yt + ((c + q) & 15) * 14);
+      double Yp[NX];
+#pragma unroll
+      for (int k = 0; k < NX / 2; ++k) {
+        const double2 v = col[k];
+        Yp[2 * k] = v.x;
+        Yp[2 * k + 1] = v.y;
+      }
+      double z0 = Lc[0], z1 = Lc[1], z2 = Lc[2], z3 = Lc[3];
+      dpp_fy4(z0, z1, z2, z3, Yp, Fo);
+      Z = d4{z0, z1, z2, z3};
+    } else {
+#pragma unroll
+      for (int kk = 0; kk < KS; ++kk) Y = mfma(Sp[kk], fB[kk], Y);
+#pragma unroll
+      for (int kk = 0; kk < KS; ++kk) Z = mfma(fB[kk], Y[kk], Z);
+    }
 
     // gq[c] = (L z)[c] + (Fᵀ s)[c]: lx + Aᵀs (c < NX), g = lu + Bᵀs (c ≥ NX)  (:181, :269).
     // (L z)[c] does not depend on the recursion: its 4-lane reduction overlaps the
@@ -341,6 +502,34 @@ __device__ __forceinline__ double dpp_dot12(double src, const double (&c)[12]) {
   return (a0 + a1) + (a2 + a3);
 }
 
+// dpp_dot16 for a block-diagonal row held in 12 registers: lanes 0..11 of each row
+// (banks 0-2) take Σ_k<12 bcast_k(src)·c[k], lanes 12..15 (bank 3) Σ_m<4
+// bcast_{12+m}(src)·c[m] — the same accumulators and order as dpp_dot16 on the
+// zero-padded row [c[0..11] | 0] resp. [0 | c[0..3]].
+__device__ __forceinline__ double dpp_dot16_bd(double src, const double (&c)[12]) {
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+  asm("s_nop 4\n\t"
+      "v_fmac_f64_dpp %[a0], %[s], %[c0] row_newbcast:0 row_mask:0xf bank_mask:0x7\n\t"
+      "v_fmac_f64_dpp %[a1], %[s], %[c1] row_newbcast:1 row_mask:0xf bank_mask:0x7\n\t"
+      "v_fmac_f64_dpp %[a2], %[s], %[c2] row_newbcast:2 row_mask:0xf bank_mask:0x7\n\t"
+      "v_fmac_f64_dpp %[a3], %[s], %[c3] row_newbcast:3 row_mask:0xf bank_mask:0x7\n\t"
+      "v_fmac_f64_dpp %[a0], %[s], %[c4] row_newbcast:4 row_mask:0xf bank_mask:0x7\n\t"
+      "v_fmac_f64_dpp %[a1], %[s], %[c5] row_newbcast:5 row_mask:0xf bank_mask:0x7\n\t"
+      "v_fmac_f64_dpp %[a2], %[s], %[c6] row_newbcast:6 row_mask:0xf bank_mask:0x7\n\t"
+      "v_fmac_f64_dpp %[a3], %[s], %[c7] row_newbcast:7 row_mask:0xf bank_mask:0x7\n\t"
+      "v_fmac_f64_dpp %[a0], %[s], %[c8] row_newbcast:8 row_mask:0xf bank_mask:0x7\n\t"
+      "v_fmac_f64_dpp %[a1], %[s], %[c9] row_newbcast:9 row_mask:0xf bank_mask:0x7\n\t"
+      "v_fmac_f64_dpp %[a2], %[s], %[c10] row_newbcast:10 row_mask:0xf bank_mask:0x7\n\t"
+      "v_fmac_f64_dpp %[a3], %[s], %[c11] row_newbcast:11 row_mask:0xf bank_mask:0x7\n\t"
+      "v_fmac_f64_dpp %[a0], %[s], %[c0] row_newbcast:12 row_mask:0xf bank_mask:0x8\n\t"
+      "v_fmac_f64_dpp %[a1], %[s], %[c1] row_newbcast:13 row_mask:0xf bank_mask:0x8\n\t"
+      "v_fmac_f64_dpp %[a2], %[s], %[c2] row_newbcast:14 row_mask:0xf bank_mask:0x8\n\t"
+      "v_fmac_f64_dpp %[a3], %[s], %[c3] row_newbcast:15 row_mask:0xf bank_mask:0x8\n\t"
+      : [a0] "+v"(a0), [a1] "+v"(a1), [a2] "+v"(a2), [a3] "+v"(a3)
+      : [s] "v"(src), [c0] "v"(c[0]), [c1] "v"(c[1]), [c2] "v"(c[2]), [c3] "v"(c[3]), [c4] "v"(c[4]), [c5] "v"(c[5]), [c6] "v"(c[6]), [c7] "v"(c[7]), [c8] "v"(c[8]), [c9] "v"(c[9]), [c10] "v"(c[10]), [c11] "v"(c[11]));
+  return (a0 + a1) + (a2 + a3);
+}
+
 // ---------------------------------------------------------------------------
 // Forward pass of up to 4 trajectories by one wave, 16 lanes each — one DPP row
 // per trajectory (forward_pass.jl:55-93, total_cost :182-196). Lane j < nx owns
@@ -359,7 +548,7 @@ struct FwdStepIn {
   double Kr[NX];           // row of Kₖ (u lanes)
 };
 
-template <int NX, int NU>
+template <int NX, int NU, int PF = 2>  // PF: prefetch distance (steps)
 __device__ FwdOut lq_forward_group(const LQParams& P, int b, int T, const double* __restrict__ x,
                                    const double* __restrict__ u, const double* __restrict__ xtraj,
                                    const double* __restrict__ dg, const double* __restrict__ Kg,
@@ -368,7 +557,6 @@ __device__ FwdOut lq_forward_group(const LQParams& P, int b, int T, const double
                                    const LSParams& ls) {
   static_assert(NX + NU == 16, "one 16-lane DPP row per trajectory: nx + nu == 16");
   static_assert(NX == 12, "dpp_dot12 is the K·δx product");
-  constexpr int PF = 2;  // prefetch distance (steps)
   const int j = threadIdx.x & 15;
   const bool is_x = j < NX;
   const bool is_u = !is_x;
@@ -475,6 +663,213 @@ __device__ FwdOut lq_forward_group(const LQParams& P, int b, int T, const double
   return out;
 }
 
+// Forward pass of a wave's four trajectories b0 .. b0+3 (contiguous) with the per-step
+// inputs streamed HBM → LDS by the wave itself (global_load_lds_dwordx4, no VGPRs
+// held in flight) PF steps ahead into a ring of R slots. Same lane roles and the
+// same arithmetic in the same order as lq_forward_group — bit-identical results —
+// but ≈100 VGPRs instead of ≈250 and a deeper prefetch: it runs inside kernels that
+// also run the backward pass (128 VGPRs at 4 waves/SIMD). Called by the WHOLE wave
+// (every lane produces a slice of every group's inputs); `active` masks the groups
+// that compute, and the line-search loop is uniform (a group that accepted stops
+// storing). One slot (3 KB): K rows [0,192), x [192,240), u [240,256), x_traj
+// [256,304), δu [304,320) doubles; group g at K + 48g, x/x_traj + 12g, u/δu + 4g.
+constexpr int RING_SLOT = 384;  // doubles per ring slot
+constexpr int RING_LAREA = 4 * 160 + 16;  // Q, R of the wave's 4 trajectories (+ read overhang)
+
+template <int NX, int NU, int R, int PF>
+__device__ FwdOut lq_forward_wave_ring(const LQParams& P, int b0, int B, int T, bool active,
+                                       const double* __restrict__ x, const double* __restrict__ u,
+                                       const double* __restrict__ xtraj, const double* __restrict__ dg,
+                                       const double* __restrict__ Kg, double prev_cost,
+                                       double* __restrict__ xnew, double* __restrict__ unew,
+                                       double* du2_out, const LSParams& ls, double* ring) {
+  static_assert(NX == 12 && NU == 4, "slot layout and lane map are written for nx = 12, nu = 4");
+  static_assert(R > PF && PF >= 1, "the slot being refilled must not be the one being read");
+  constexpr uint32_t OOR = 0x80000000u;
+  const int l = threadIdx.x & 63;
+  const int g = l >> 4;
+  const int j = l & 15;
+  const bool is_x = j < NX;
+  const bool is_u = !is_x;
+  const int iu = is_u ? j - NX : 0;
+  const int jx = is_x ? j : 0;
+  const int nt = B - b0 < 4 ? B - b0 : 4;  // trajectories present in this wave
+  const int b = b0 + (g < nt ? g : 0);     // absent groups alias trajectory b0 (never stored)
+
+  const double* Ab = P.A + (size_t)b * NX * NX;
+  const double* Bb = P.B + (size_t)b * NX * NU;
+  const double* Qfb = P.Qf + (size_t)b * NX * NX;
+  double Fr[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const double a = ldz(is_x && k < NX, Ab + jx * NX + (k < NX ? k : 0), Ab);
+    const double bb = ldz(is_x && k >= NX, Bb + jx * NU + (k >= NX ? k - NX : 0), Bb);
+    Fr[k] = a + bb;
+  }
+  // the cost Hessian rows live in LDS after the ring (re-read every step: registers
+  // are the scarce resource): trajectory g's Q at 160g, R at 160g + 144
+  double* const Ls = ring + R * RING_SLOT;
+  for (int i = l; i < 4 * 160; i += 64) {
+    const int gg = i / 160, e = i % 160;
+    const size_t bt = (size_t)b0 + (gg < nt ? gg : 0);
+    Ls[i] = e < NX * NX ? P.Q[bt * NX * NX + e] : P.R[bt * NU * NU + (e < NX * NX ? 0 : e - NX * NX)];
+  }
+  const int la = is_x ? g * 160 + jx * NX : g * 160 + NX * NX + iu * NU;  // this lane's L row
+  wave_lds_fence();
+
+  // producer: lane l moves 16 B per instruction; three instructions fill one slot
+  //   #1: K chunk l (of 96)   #2: K chunk 64+l | x chunk l−32 | u chunk l−56
+  //   #3: x_traj chunk l | δu chunk l−24 | (lanes 32..63 repeat lanes 0..31)
+  auto tr = [&](int gg) { return (size_t)(b0 + (gg < nt ? gg : 0)); };
+  const double* xt0 = xtraj ? xtraj : x;  // x_traj = NULL: read x with weight 0
+  const double xtw = xtraj ? 1.0 : 0.0;
+  const char *p1, *p2, *p3;
+  uint32_t s1, s2, s3;  // bytes per step
+  {
+    const int c = l;
+    p1 = reinterpret_cast<const char*>(Kg + tr(c / 24) * T * NU * NX + 2 * (c % 24));
+    s1 = NU * NX * 8;
+    if (l < 32) {
+      const int c2 = 64 + l;
+      p2 = reinterpret_cast<const char*>(Kg + tr(c2 / 24) * T * NU * NX + 2 * (c2 % 24));
+      s2 = NU * NX * 8;
+    } else if (l < 56) {
+      const int m = l - 32;
+      p2 = reinterpret_cast<const char*>(x + tr(m / 6) * (T + 1) * NX + 2 * (m % 6));
+      s2 = NX * 8;
+    } else {
+      const int m = l - 56;
+      p2 = reinterpret_cast<const char*>(u + tr(m / 2) * T * NU + 2 * (m % 2));
+      s2 = NU * 8;
+    }
+    const int l3 = l & 31;
+    if (l3 < 24) {
+      p3 = reinterpret_cast<const char*>(xt0 + tr(l3 / 6) * (T + 1) * NX + 2 * (l3 % 6));
+      s3 = NX * 8;
+    } else {
+      const int m = l3 - 24;
+      p3 = reinterpret_cast<const char*>(dg + tr(m / 2) * T * NU + 2 * (m % 2));
+      s3 = NU * 8;
+    }
+  }
+  const uint32_t ring_lds = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) double*)ring;
+  auto produce = [&](int t) {
+    uint32_t tt = (uint32_t)(t < T ? t : T - 1);  // clamped: loaded, never read
+    asm volatile("" : "+s"(tt));  // no hoisting of the prologue's addresses out of the trial loop
+    const uint32_t m0 = ring_lds + (uint32_t)((t % R) * RING_SLOT * 8);
+    asm volatile("global_load_lds_dwordx4 %0, off" ::"v"(p1 + (size_t)tt * s1), "{m0}"(m0) : "memory");
+    asm volatile("global_load_lds_dwordx4 %0, off" ::"v"(p2 + (size_t)tt * s2), "{m0}"(m0 + 1024) : "memory");
+    asm volatile("global_load_lds_dwordx4 %0, off" ::"v"(p3 + (size_t)tt * s3), "{m0}"(m0 + 2048) : "memory");
+  };
+  // vmcnt immediates (gfx9: vmcnt[3:0] | expcnt 7 << 4 | lgkmcnt 15 << 8 | vmcnt[5:4] << 14):
+  // per step the wave issues 3 slot loads then 2 result stores, so slot t is
+  // complete once ≤ 5·PF − 3 ops are outstanding (≤ 3·PF − 3 while the prologue
+  // loads are the newest)
+  constexpr int N_SS = 5 * PF - 3, N_PRO = 3 * PF - 3;
+  auto wait_slot = [](auto n) {
+    constexpr int v = decltype(n)::value;
+    static_assert(v >= 0 && v < 64, "vmcnt is 6 bits");
+    __builtin_amdgcn_s_waitcnt((v & 15) | (7 << 4) | (15 << 8) | ((v >> 4) << 14));
+    asm volatile("" ::: "memory");
+  };
+
+  const int ka = g * 48 + iu * NX;                                 // K row of (g, iu)
+  const int va = is_x ? 192 + g * 12 + jx : 240 + g * 4 + iu;      // x (x lanes) / u (u lanes)
+  const int vb = is_x ? 256 + g * 12 + jx : 304 + g * 4 + iu;      // x_traj / δu
+  const auto rXN = buffer_rsrc(xnew + (size_t)b0 * (T + 1) * NX, (uint32_t)nt * (T + 1) * NX * 8);
+  const auto rUN = buffer_rsrc(unew + (size_t)b0 * T * NU, (uint32_t)nt * T * NU * 8);
+  const uint32_t oxs = is_x ? (uint32_t)(g * (T + 1) * NX + jx) * 8 : OOR;
+  const uint32_t ous = is_u ? (uint32_t)(g * T * NU + iu) * 8 : OOR;
+
+  double alpha = ls.alpha0;
+  FwdOut out{INFINITY, 0, 0};
+  bool open = active;  // still line-searching
+  double du2_acc = 0.0;
+  for (int trial = 1; trial <= ls.max_trials && __any(open); ++trial) {
+#pragma unroll
+    for (int t = 0; t < PF; ++t) produce(t);
+    double xb = 0.0;  // x̄₁ = x₁ (:65), taken from slot 0 once it has landed
+    double cost = 0.0, du2 = 0.0;
+    const uint32_t ox = open ? oxs : OOR, ou = open ? ous : OOR;  // closed groups store nothing
+    auto step = [&](int t) {
+      const double* sl = ring + (t % R) * RING_SLOT;
+      const double a = sl[va], bq = sl[vb];
+      if (t == 0) xb = is_x ? a : 0.0;
+      double Kr[NX];
+      const double2* kr = reinterpret_cast<const double2*>(sl + ka);
+#pragma unroll
+      for (int k = 0; k < NX / 2; ++k) {
+        const double2 v = kr[k];
+        Kr[2 * k] = v.x;
+        Kr[2 * k + 1] = v.y;
+      }
+      // δx = x̄ₖ − xₖ (:72); ūₖ = uₖ + α δuₖ + Kₖ δx (:73)
+      const double dx = is_x ? xb - a : 0.0;
+      const double kdx = dpp_dot12(dx, Kr);
+      const double ub = fma(alpha, bq, a) + kdx;
+      const double z = is_x ? xb : ub;
+      const double v = is_x ? fma(-xtw, bq, xb) : ub;
+      const double e = is_x ? 0.0 : ub - a;
+      produce(t + PF);  // slot (t+PF)%R was last read at step t+PF−R < t
+      double Lr[NX];  // Q row (x lanes); R row in slots 0..NU-1 (u lanes), rest unused
+      const double2* lr = reinterpret_cast<const double2*>(Ls + la);
+#pragma unroll
+      for (int k = 0; k < NX / 2; ++k) {
+        const double2 q = lr[k];
+        Lr[2 * k] = q.x;
+        Lr[2 * k + 1] = q.y;
+      }
+      const double lv = dpp_dot16_bd(v, Lr);
+      const double xn = dpp_dot16(z, Fr);
+      cost = fma(v, lv, cost);
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, z), rXN, ox, (uint32_t)t * NX * 8, 0);
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, z), rUN, ou, (uint32_t)t * NU * 8, 0);
+      du2 = fma(e, e, du2);
+      xb = xn;
+    };
+    const int tp = T < PF ? T : PF;
+    for (int t = 0; t < tp; ++t) {
+      wait_slot(std::integral_constant<int, N_PRO>{});
+      step(t);
+    }
+    for (int t = tp; t < T; ++t) {
+      wait_slot(std::integral_constant<int, N_SS>{});
+      step(t);
+    }
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, xb), rXN, ox, (uint32_t)T * NX * 8, 0);
+    // Qf row (x lanes; u lanes read row 0 and zero it): one base address, 6 × 16 B
+    const double2* qrow = reinterpret_cast<const double2*>(Qfb + jx * NX);
+    asm volatile("" : "+v"(qrow));  // keep the row address from being hoisted as 12 pointers
+    double Qfr[NX];
+#pragma unroll
+    for (int k = 0; k < NX / 2; ++k) {
+      const double2 q = qrow[k];
+      Qfr[2 * k] = is_x ? q.x : 0.0;
+      Qfr[2 * k + 1] = is_x ? q.y : 0.0;
+    }
+    const double lf = dpp_dot12(is_x ? xb : 0.0, Qfr);
+    cost = fma(is_x ? xb : 0.0, lf, cost);
+    cost = rowsum16(cost);
+    du2 = rowsum16(du2);
+    if (open) {
+      out.trials = trial;
+      out.cost = cost;
+      du2_acc = du2;
+      if (prev_cost - cost > 0.0) {  // (:77-80); NaN compares false → keep searching
+        out.accepted = 1;
+        open = false;
+      }
+    }
+    alpha *= ls.shrink;  // (:82); unused by closed groups
+    // the loads of the clamped steps past the horizon are still in flight: drain them
+    // before the next trial's prologue reuses the slots
+    __builtin_amdgcn_s_waitcnt((0) | (7 << 4) | (15 << 8));
+    asm volatile("" ::: "memory");
+  }
+  if (du2_out) *du2_out = du2_acc;
+  return out;
+}
+
 // ---------------------------------------------------------------------------
 // Kernels
 // ---------------------------------------------------------------------------
@@ -567,6 +962,100 @@ __global__ __launch_bounds__(64) void lq_iter_forward_kernel(LQParams P, int B, 
   }
 }
 
+// ---------------------------------------------------------------------------
+// Pipelined fit iteration (DESIGN.md §fit driver): the backward pass is bound by the
+// FP64 pipe and the forward pass by HBM, so one launch runs both at once on
+// different trajectories. Workgroups (4 trajectories each) have one of two roles:
+//   role B: backward(iteration i) → barrier → wave 0: forward(iteration i)
+//   role A: wave 0: forward(iteration i−1) → barrier → backward(iteration i)
+// so while B's waves run Riccati recursions, A's first waves stream their forward
+// passes, and vice versa at the end of the launch. `cur` describes iteration i
+// (B, and A's backward), `prev` iteration i−1 (A's forward, which reads the gains
+// A's backward wrote in the previous launch). fit runs max_iter + 1 launches: the
+// first without A's forward, the last with A's forward only.
+// ---------------------------------------------------------------------------
+// forward ring inside the pipe kernel: the workgroup's backward scratch holds R slots
+constexpr int PIPE_R = 8, PIPE_PF = 7;
+constexpr int PIPE_LDS = (PIPE_R * RING_SLOT + RING_LAREA > WAVES_PER_WG * BW_LDS)
+                             ? PIPE_R * RING_SLOT + RING_LAREA : WAVES_PER_WG * BW_LDS;
+enum : int { PIPE_A_FW = PIPE_A_FW_FLAG, PIPE_A_BW = PIPE_A_BW_FLAG, PIPE_B = PIPE_B_FLAG };
+
+// role of workgroup g: two of the four workgroups each CU hosts at B = 4096 are A,
+// whether the dispatcher spreads consecutive workgroups of an XCD over its CUs
+// (CU mates g, g+256, g+512, g+768) or packs them (g, g+8, g+16, g+24)
+__device__ __forceinline__ bool pipe_role_a(int g) { return (((g >> 8) ^ (g >> 3)) & 1) != 0; }
+
+// forward pass + convergence test (:163-175) of the wave's trajectories b0 .. b0+3;
+// called by the whole wave, groups whose status is not OK (or past B) sit out
+template <int NX, int NU>
+__device__ __forceinline__ void iter_forward_wave(const LQParams& P, int b0, int B, int T,
+                                                  const IterArgs& a, const LSParams& ls,
+                                                  double* ring) {
+  const int j = threadIdx.x & 15;
+  const int b = b0 + ((threadIdx.x & 63) >> 4);
+  const bool active = b < B && a.status[b < B ? b : b0] == ILQR_TRAJ_OK;
+  double du2 = 0.0;
+  const double pc = (a.prev_cost && active) ? a.prev_cost[b] : INFINITY;
+  const FwdOut r = lq_forward_wave_ring<NX, NU, PIPE_R, PIPE_PF>(P, b0, B, T, active, a.x, a.u,
+                                                                 a.xtraj, a.d, a.K, pc, a.xnew,
+                                                                 a.unew, &du2, ls, ring);
+  if (j == 0 && active) {
+    if (a.trials) a.trials[b] = r.trials;
+    if (a.du2) a.du2[b] = du2;
+    if (a.iters) a.iters[b] = a.iter;
+    if (!r.accepted) {
+      a.status[b] = (r.cost != r.cost) ? ILQR_TRAJ_NAN : ILQR_TRAJ_LS_EXHAUSTED;
+      if (a.res_parity) a.res_parity[b] = a.parity;
+    } else {
+      a.new_cost[b] = r.cost;
+      if (du2 <= ls.tol) {
+        a.status[b] = ILQR_TRAJ_CONVERGED;
+        if (a.res_parity) a.res_parity[b] = a.parity;
+      }
+    }
+  }
+}
+
+// Part 2 with the LDS-ring forward (one wave, four trajectories per workgroup).
+template <int NX, int NU>
+__global__ __launch_bounds__(64) void lq_iter_forward_ring_kernel(LQParams P, int B, int T, IterArgs a,
+                                                                  LSParams ls) {
+  __shared__ __attribute__((aligned(16))) double ring[PIPE_R * RING_SLOT + RING_LAREA];
+  iter_forward_wave<NX, NU>(P, blockIdx.x * 4, B, T, a, ls, ring);
+}
+
+template <int NX, int NU>
+__global__ __launch_bounds__(256, 4) void lq_iter_pipe_kernel(LQParams P, int B, int T,
+                                                              IterArgs cur, IterArgs prev,
+                                                              LSParams ls, int flags) {
+  __shared__ __attribute__((aligned(16))) double lds[PIPE_LDS];
+  const int w = threadIdx.x >> 6;
+  const int b0 = blockIdx.x * WAVES_PER_WG;
+  const bool role_a = pipe_role_a(blockIdx.x);
+  auto forward4 = [&](const IterArgs& a) {  // wave 0: the workgroup's 4 trajectories
+    if (w == 0) iter_forward_wave<NX, NU>(P, b0, B, T, a, ls, lds);  // ring: the whole WG's scratch
+  };
+  auto backward = [&](const IterArgs& a) {
+    const int b = b0 + w;
+    if (b < B && a.status[b] == ILQR_TRAJ_OK) {
+      const bool nan = lq_backward_wave<NX, NU>(P, b, T, a.x, a.u, a.d, a.K, ls.mu, lds + w * BW_LDS);
+      if (nan && (threadIdx.x & 63) == 0) {
+        a.status[b] = ILQR_TRAJ_NAN;  // reference: AssertionError at backward_pass.jl:353
+        if (a.res_parity) a.res_parity[b] = a.parity;
+      }
+    }
+  };
+  if (role_a) {
+    if (flags & PIPE_A_FW) forward4(prev);
+    __syncthreads();  // x̄, ū and the status of iteration i−1 are visible to the workgroup
+    if (flags & PIPE_A_BW) backward(cur);
+  } else if (flags & PIPE_B) {
+    backward(cur);
+    __syncthreads();  // the gains of iteration i are visible to wave 0
+    forward4(cur);
+  }
+}
+
 __global__ void gather_kernel(int B, int T, int nx, int nu, const double* x0, const double* u0,
                               const double* x1, const double* u1, const int32_t* res_parity,
                               int32_t* status, int final_parity, double* x_out, double* u_out) {
@@ -578,6 +1067,7 @@ __global__ void gather_kernel(int B, int T, int nx, int nu, const double* x0, co
   const double* us = (par ? u1 : u0) + (size_t)b * T * nu;
   for (int i = threadIdx.x; i < (T + 1) * nx; i += blockDim.x) x_out[(size_t)b * (T + 1) * nx + i] = xs[i];
   for (int i = threadIdx.x; i < T * nu; i += blockDim.x) u_out[(size_t)b * T * nu + i] = us[i];
+  __syncthreads();  // every wave of the block has read status[b] before it changes
   if (threadIdx.x == 0 && running) status[b] = ILQR_TRAJ_MAX_ITER;
 }
 
@@ -695,12 +1185,23 @@ hipError_t launch_lq_iter_backward(int nx, int nu, const LQParams& p, int b0, in
 }
 
 hipError_t launch_lq_iter_forward(int nx, int nu, const LQParams& p, int b0, int b1, int T,
-                                  const IterArgs& a, const LSParams& ls, hipStream_t s) {
+                                  const IterArgs& a, const LSParams& ls, hipStream_t s, bool ring) {
   const int B = b1 - b0;
   if (B <= 0) return hipSuccess;
   const LQParams ps = shift(p, nx, nu, b0);
   const IterArgs as = shift(a, nx, nu, T, b0);
+  if (ring) {
+    ILQR_DISPATCH(12, 4, (lq_iter_forward_ring_kernel<NX_, NU_><<<(B + 3) / 4, 64, 0, s>>>(ps, B, T, as, ls)));
+  }
   ILQR_DISPATCH(12, 4, (lq_iter_forward_kernel<NX_, NU_><<<(B + 3) / 4, 64, 0, s>>>(ps, B, T, as, ls)));
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_lq_iter_pipe(int nx, int nu, const LQParams& p, int B, int T, const IterArgs& cur,
+                               const IterArgs& prev, const LSParams& ls, int flags, hipStream_t s) {
+  if (B <= 0) return hipSuccess;
+  const int grid = (B + WAVES_PER_WG - 1) / WAVES_PER_WG;
+  ILQR_DISPATCH(12, 4, (lq_iter_pipe_kernel<NX_, NU_><<<grid, 256, 0, s>>>(p, B, T, cur, prev, ls, flags)));
   return hipErrorInvalidValue;
 }
 

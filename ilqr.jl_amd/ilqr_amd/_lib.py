@@ -28,6 +28,10 @@ TRAJ_MAX_ITER = 2
 TRAJ_LS_EXHAUSTED = 3
 TRAJ_NAN = 4
 
+# ilqr_set_schedule flags (LQ family)
+SCHED_PIPELINED = 1
+SCHED_RING_FORWARD = 2
+
 PROBLEM_LQ = 1
 PROBLEM_TWO_LINK = 2
 PROBLEM_TILES = 3
@@ -80,6 +84,7 @@ SIGNATURES = {
     "ilqr_destroy": (C.c_int, [P]),
     "ilqr_set_stream": (C.c_int, [P, P]),
     "ilqr_sync": (C.c_int, [P]),
+    "ilqr_set_schedule": (C.c_int, [P, C.c_int]),
     "ilqr_backward": (C.c_int, [P, C.POINTER(Problem), C.POINTER(Options), P, P, P, P, P]),
     "ilqr_backward_tiles": (C.c_int, [P, C.POINTER(Tiles), C.POINTER(Options), P, P, P]),
     "ilqr_forward": (C.c_int, [P, C.POINTER(Problem), C.POINTER(Options), P, P, P, P, P, P,

@@ -138,6 +138,17 @@ ilqr_status ilqr_destroy(ilqr_handle* h);
 /* HIP stream (hipStream_t) the handle launches on; NULL = the null stream. */
 ilqr_status ilqr_set_stream(ilqr_handle* h, void* hip_stream);
 ilqr_status ilqr_sync(ilqr_handle* h);
+/* Launch schedule of ilqr_iterate / ilqr_fit for the LQ family (bit flags; every
+ * schedule returns the same bits):
+ *   ILQR_SCHED_RING_FORWARD  the forward pass streams its per-step inputs HBM → LDS
+ *                            ahead of use (default on);
+ *   ILQR_SCHED_PIPELINED     fit runs one kernel per iteration in which half of the
+ *                            workgroups do forward(i-1) then backward(i) while the
+ *                            other half do backward(i) then forward(i) (default off).
+ * Unknown bits → ILQR_ERR_BAD_ARG. */
+#define ILQR_SCHED_PIPELINED 1
+#define ILQR_SCHED_RING_FORWARD 2
+ilqr_status ilqr_set_schedule(ilqr_handle* h, int flags);
 
 /* iLQR.backward_pass (backward_pass.jl:324-357): gains d (batch,T,nu) and
  * K (batch,T,nu,nx) for every trajectory. With a status array (batch) the call

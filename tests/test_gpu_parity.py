@@ -256,3 +256,74 @@ def test_headline_iterate_matches_backward_plus_forward(gpu, headline):
     s.iterate(xi, ui, xn, un, pc, st, options=_lib.default_options(tol=-1.0))
     torch.cuda.synchronize()
     assert torch.equal(xn, xf) and torch.equal(un, uf) and torch.equal(pc, cf)
+
+
+# -- launch schedules (ilqr_set_schedule) ----------------------------------------------
+def _fit_both(s, x, u, **kw):
+    s.set_schedule(pipelined=False)
+    a = s.fit(x, u, **kw)
+    s.set_schedule(pipelined=True)
+    b = s.fit(x, u, **kw)
+    torch.cuda.synchronize()
+    s.set_schedule()
+    return a, b
+
+
+def _same(a, b):
+    assert a.call_status == b.call_status
+    for f in ("x", "u", "cost", "iters", "status"):  # bitwise, NaN == NaN
+        torch.testing.assert_close(getattr(a, f), getattr(b, f), rtol=0, atol=0, equal_nan=True,
+                                   msg=f)
+
+
+def test_pipelined_fit_equals_sequential_headline(gpu, headline):
+    """Role A/B workgroups run forward(i−1) ∥ backward(i): same results, bit for bit,
+    through convergence (tol), max_iter and the final gather."""
+    s, lq, x, u = headline
+    for kw in (dict(max_iter=1, tol=-1.0), dict(max_iter=5, tol=-1.0), dict(max_iter=40, tol=1e-9)):
+        a, b = _fit_both(s, dev(x), dev(u), **kw)
+        _same(a, b)
+
+
+@pytest.mark.parametrize("nb,T", [(1, 5), (5, 3), (37, 17), (1029, 9)])
+def test_pipelined_fit_ragged(gpu, nb, T):
+    lq, x, u = random_lq_batch(nb, 12, 4, T, seed=nb + 7 * T)
+    x[nb // 2, 1, 0] = np.nan  # one NaN trajectory leaves the batch in iteration 1
+    s = Solver(12, 4, T, nb)
+    s.set_problem(lq)
+    a, b = _fit_both(s, dev(x), dev(u), max_iter=12, tol=1e-8)
+    _same(a, b)
+    st = b.status.cpu().numpy()
+    assert st[nb // 2] == _lib.TRAJ_NAN
+    xo, uo, co, it, sto = cref.lq_fit(LQBatch(lq.A, lq.B, lq.Q, lq.R, lq.Qf), x, u, max_iter=12,
+                                      tol=1e-8, symmetrize=True)
+    ok = np.arange(nb) != nb // 2
+    if ok.any():
+        assert np.array_equal(b.iters.cpu().numpy()[ok], it[ok])
+        assert rel(b.u.cpu().numpy()[ok], uo[ok]) < 1e-8
+
+
+@pytest.mark.parametrize("nb,T", [(4096, 100), (37, 17), (5, 3)])
+def test_ring_forward_iterate_equals_standard(gpu, nb, T):
+    """The LDS-ring forward kernel (ILQR_SCHED_RING_FORWARD) returns the register-ring
+    forward's bits, line-search trials included."""
+    lq, x, u = (quadrotor_batch(nb, T=T, seed0=0) if nb == 4096
+                else random_lq_batch(nb, 12, 4, T, seed=nb * 3 + T))
+    s = Solver(12, 4, T, nb)
+    s.set_problem(lq)
+    xi, ui = dev(x), dev(u)
+    outs = []
+    for ring in (False, True):
+        s.set_schedule(ring_forward=ring)
+        xn, un = torch.empty_like(xi), torch.empty_like(ui)
+        pc = torch.full((nb,), float("inf"), dtype=torch.float64, device="cuda")
+        st = torch.zeros((nb,), dtype=torch.int32, device="cuda")
+        tr = torch.zeros((nb,), dtype=torch.int32, device="cuda")
+        xa, ua = xi.clone(), ui.clone()
+        for _ in range(3):  # cold start, then line searches against finite costs
+            s.iterate(xa, ua, xn, un, pc, st, trials=tr, options=_lib.default_options(tol=-1.0))
+            xa, xn, ua, un = xn, xa, un, ua
+        torch.cuda.synchronize()
+        outs.append((xa, ua, pc, st, tr))
+    for a, b in zip(*outs):
+        torch.testing.assert_close(a, b, rtol=0, atol=0, equal_nan=True)

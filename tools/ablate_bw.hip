@@ -58,9 +58,16 @@ int main() {
   };
   run<0>("product", P, B, T, xd, ud, d, K, flag);
   CK(hipMemcpy(Kref.data(), K, Kref.size() * 8, hipMemcpyDeviceToHost));
-  run<768>("round-1 gradient + stores", P, B, T, xd, ud, d, K, flag); diff("round-1 gradient + stores");
-  run<768 + 96>("round-1 v4 (2 Newton, sym 4)", P, B, T, xd, ud, d, K, flag); diff("round-1 v4");
+  run<1024>("VALU Y/Z (dpp)", P, B, T, xd, ud, d, K, flag); diff("VALU Y/Z (dpp)");
   for (int rep = 0; rep < 2; ++rep) {
+    printf("-- VALU products, round %d\n", rep);
+    run<0>("product (MFMA Y/Z)", P, B, T, xd, ud, d, K, flag);
+    run<1024>("VALU Y/Z (dpp)", P, B, T, xd, ud, d, K, flag);
+    run<1024 + 1>("VALU Y/Z, no factor/solve", P, B, T, xd, ud, d, K, flag);
+    run<1024 + 8>("VALU Y/Z, no K/d stores", P, B, T, xd, ud, d, K, flag);
+    run<1024 + 31>("VALU Y/Z chain + selects only", P, B, T, xd, ud, d, K, flag);
+  }
+  for (int rep = 0; rep < 1; ++rep) {
     printf("-- round %d\n", rep);
     run<0>("product", P, B, T, xd, ud, d, K, flag);
     run<256>("round-1 gradient", P, B, T, xd, ud, d, K, flag);

@@ -16,7 +16,7 @@ step() {  # step <name> <timeout> <cmd...>
 }
 for WHAT in "$@"; do
 case $WHAT in
-  test) step pytest_gpu 600 python -m pytest tests -m gpu -x -q
+  test) step pytest_gpu 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
         step smoke 180 python -c "import __graft_entry__ as g; g.smoke()" ;;
   bench) step bench 300 python bench.py ;;
   prof) step rocprof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 50 --warmup 300 --no-cpu ;;
