@@ -983,7 +983,7 @@ enum : int { PIPE_A_FW = PIPE_A_FW_FLAG, PIPE_A_BW = PIPE_A_BW_FLAG, PIPE_B = PI
 // role of workgroup g: two of the four workgroups each CU hosts at B = 4096 are A,
 // whether the dispatcher spreads consecutive workgroups of an XCD over its CUs
 // (CU mates g, g+256, g+512, g+768) or packs them (g, g+8, g+16, g+24)
-__device__ __forceinline__ bool pipe_role_a(int g) { return (((g >> 8) ^ (g >> 3)) & 1) != 0; }
+__host__ __device__ __forceinline__ bool pipe_role_a(int g) { return (((g >> 8) ^ (g >> 3)) & 1) != 0; }
 
 // forward pass + convergence test (:163-175) of the wave's trajectories b0 .. b0+3;
 // called by the whole wave, groups whose status is not OK (or past B) sit out

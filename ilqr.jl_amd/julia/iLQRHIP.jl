@@ -77,6 +77,12 @@ function Handle(nx, nu, T, batch; device=0)
     return h
 end
 
+# launch schedule of the LQ family (include/ilqr.h: ILQR_SCHED_*); same bits either way
+const ILQR_SCHED_PIPELINED = Int32(1)
+const ILQR_SCHED_RING_FORWARD = Int32(2)
+set_schedule!(h::Handle, flags::Integer) =
+    check(ccall((:ilqr_set_schedule, libilqr), Cint, (Ptr{Cvoid}, Cint), h.ptr, flags), "ilqr_set_schedule")
+
 function upload(h::Handle, a::Array{Float64})
     p = Ref{Ptr{Cvoid}}(C_NULL)
     check(ccall((:ilqr_malloc, libilqr), Cint, (Ptr{Cvoid}, Csize_t, Ref{Ptr{Cvoid}}), h.ptr, sizeof(a), p), "ilqr_malloc")
