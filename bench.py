@@ -72,27 +72,33 @@ def load_pmc_traffic(profiles_dir):
 
 def cpu_baseline(lq, x, u, budget_s):
     """Time the C restatement (oracle/, kind 'port') on a bounded sample of the
-    same workload: one cold-start iteration (backward + forward) per trajectory."""
+    same workload: one cold-start iteration (backward + forward) per trajectory, on
+    all host threads (≤16, the box's CPU share) and on one core."""
     from oracle import cref
+
+    def rate(threads, budget):
+        n = 32
+        while True:
+            idx = np.arange(n) % lq.batch
+            sub = type(lq)(lq.A[idx], lq.B[idx], lq.Q[idx], lq.R[idx], lq.Qf[idx])
+            t0 = time.perf_counter()
+            d, K, _ = cref.lq_backward(sub, x[idx], u[idx], symmetrize=True, nthreads=threads)
+            cref.lq_forward(sub, x[idx], u[idx], None, d, K, np.inf, nthreads=threads)
+            elapsed = time.perf_counter() - t0
+            if elapsed > budget or n >= 1 << 16:
+                return n, elapsed, n / elapsed  # trajectory-iterations / s
+            n *= 2
+
     threads = min(16, os.cpu_count() or 1)
-    n = 32
-    elapsed = 0.0
-    while True:
-        idx = np.arange(n) % lq.batch
-        sub = type(lq)(lq.A[idx], lq.B[idx], lq.Q[idx], lq.R[idx], lq.Qf[idx])
-        t0 = time.perf_counter()
-        d, K, _ = cref.lq_backward(sub, x[idx], u[idx], symmetrize=True, nthreads=threads)
-        cref.lq_forward(sub, x[idx], u[idx], None, d, K, np.inf, nthreads=threads)
-        elapsed = time.perf_counter() - t0
-        if elapsed > budget_s / 4 or n >= 1 << 16:
-            break
-        n *= 2
-    rate = n / elapsed  # trajectory-iterations / s
-    return {"value": rate / lq.batch, "unit": "batched iterations/s (batch=4096)", "cores": threads,
+    n, elapsed, r = rate(threads, budget_s / 4)
+    n1, elapsed1, r1 = rate(1, budget_s / 8)
+    return {"value": r / lq.batch, "unit": "batched iterations/s (batch=4096)", "cores": threads,
             "kind": "port",
+            "value_1core": r1 / lq.batch,
             "sample": f"{n} trajectories x 1 cold-start iteration (C restatement oracle/ilqr_ref.c, "
                       f"OpenMP {threads} threads, -O3), {elapsed:.2f} s; trajectory-iterations/s="
-                      f"{rate:.1f}"}
+                      f"{r:.1f}; 1 core: {n1} trajectories in {elapsed1:.2f} s, "
+                      f"trajectory-iterations/s={r1:.1f}"}
 
 
 def main():
