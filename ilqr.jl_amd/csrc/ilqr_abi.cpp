@@ -27,6 +27,7 @@ struct ilqr_handle {
   int32_t* status = nullptr;
   int32_t* res_parity = nullptr;
   int32_t* iters = nullptr;
+  int32_t* host_status = nullptr;  // pinned host copy of a status array (fold_status)
   // 2-link arm: per-step linearisation workspace J = [A|B] (T × 24 × batch)
   double* J = nullptr;
   // pipelining: the batch is split into `nchunks` chunks; chunk i's forward pass
@@ -135,14 +136,13 @@ ilqr_status check_options(const ilqr_options* o) {
 
 // Reduce per-trajectory status to the call status (host copy, synchronising).
 ilqr_status fold_status(ilqr_handle* h, const int32_t* dev_status) {
-  std::vector<int32_t> st(h->batch);
-  HIP_TRY(hipMemcpyAsync(st.data(), dev_status, sizeof(int32_t) * h->batch, hipMemcpyDeviceToHost,
-                         h->stream));
+  int32_t* st = h->host_status;  // pinned: one DMA, no staging copy
+  HIP_TRY(hipMemcpyAsync(st, dev_status, sizeof(int32_t) * h->batch, hipMemcpyDeviceToHost, h->stream));
   HIP_TRY(hipStreamSynchronize(h->stream));
   bool nan = false, ls = false;
-  for (int32_t s : st) {
-    nan |= s == ILQR_TRAJ_NAN;
-    ls |= s == ILQR_TRAJ_LS_EXHAUSTED;
+  for (int b = 0; b < h->batch; ++b) {
+    nan |= st[b] == ILQR_TRAJ_NAN;
+    ls |= st[b] == ILQR_TRAJ_LS_EXHAUSTED;
   }
   return nan ? ILQR_ERR_NAN : (ls ? ILQR_ERR_LS_EXHAUSTED : ILQR_OK);
 }
@@ -211,6 +211,7 @@ ilqr_status ilqr_create(ilqr_handle** out, int device, int nx, int nu, int T, in
   if (e == hipSuccess) e = hipMalloc(&h->status, sizeof(int32_t) * B);
   if (e == hipSuccess) e = hipMalloc(&h->res_parity, sizeof(int32_t) * B);
   if (e == hipSuccess) e = hipMalloc(&h->iters, sizeof(int32_t) * B);
+  if (e == hipSuccess) e = hipHostMalloc(&h->host_status, sizeof(int32_t) * B, hipHostMallocDefault);
   if (e == hipSuccess && ilqr::tl_supported(nx, nu))
     e = hipMalloc(&h->J, sizeof(double) * ilqr::tl_workspace_doubles(batch, T));
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking);
@@ -254,6 +255,7 @@ ilqr_status ilqr_destroy(ilqr_handle* h) {
   (void)hipFree(h->status);
   (void)hipFree(h->res_parity);
   (void)hipFree(h->iters);
+  if (h->host_status) (void)hipHostFree(h->host_status);
   (void)hipFree(h->J);
   for (int c = 0; c < 2; ++c) {
     if (h->ev_bw[c]) (void)hipEventDestroy(h->ev_bw[c]);
@@ -379,21 +381,19 @@ ilqr_status ilqr_fit(ilqr_handle* h, const ilqr_problem* p, const ilqr_options* 
   ilqr_default_options(&def);
   if (!o) o = &def;
   HIP_TRY(hipSetDevice(h->device));
-  const size_t B = (size_t)h->batch;
-  const size_t xbytes = sizeof(double) * B * (h->T + 1) * h->nx;
-  const size_t ubytes = sizeof(double) * B * h->T * h->nu;
   hipStream_t s = h->stream;
-  HIP_TRY(hipMemcpyAsync(h->xbuf[0], x_init, xbytes, hipMemcpyDeviceToDevice, s));
-  HIP_TRY(hipMemcpyAsync(h->ubuf[0], u_init, ubytes, hipMemcpyDeviceToDevice, s));
-  HIP_TRY(ilqr::launch_fill_f64(h->prev_cost, h->batch, INFINITY, s));  // forward_pass.jl:159
-  HIP_TRY(ilqr::launch_fill_i32(h->status, h->batch, ILQR_TRAJ_OK, s));
-  HIP_TRY(ilqr::launch_fill_i32(h->res_parity, h->batch, 0, s));
-  HIP_TRY(ilqr::launch_fill_i32(h->iters, h->batch, 0, s));
+  // prev_cost = Inf (forward_pass.jl:159), status OK, result "the input", iters 0
+  HIP_TRY(ilqr::launch_fit_init(h->batch, h->prev_cost, h->status, h->res_parity, h->iters, s));
   const ilqr::LSParams ls = ls_params(o);
-  auto iter_args = [&](int it, int par) {
+  // Iteration `it` reads x̄ⁱ (the caller's x_init/u_init for it = 1, no copy; else
+  // the handle's buffer (it−1)&1) and writes buffer it&1 (x̄ⁱ, ūⁱ = x̄ⁱ⁺¹, ūⁱ⁺¹,
+  // :174-175). `parity` records where a trajectory's result lies when it stops:
+  // ilqr::PARITY_INPUT for the caller's buffers.
+  auto iter_args = [&](int it) {
+    const int par = (it - 1) & 1;
     ilqr::IterArgs a{};
-    a.x = h->xbuf[par];
-    a.u = h->ubuf[par];
+    a.x = it == 1 ? x_init : h->xbuf[par];
+    a.u = it == 1 ? u_init : h->ubuf[par];
     a.xtraj = x_traj;
     a.xnew = h->xbuf[par ^ 1];
     a.unew = h->ubuf[par ^ 1];
@@ -406,43 +406,38 @@ ilqr_status ilqr_fit(ilqr_handle* h, const ilqr_problem* p, const ilqr_options* 
     a.status = h->status;
     a.res_parity = h->res_parity;
     a.iters = h->iters;
-    a.parity = par;
+    a.parity = it == 1 ? ilqr::PARITY_INPUT : par;
     a.iter = it;
     return a;
   };
-  int par = 0;
   if (!two_link(p) && h->pipelined) {
-    // iteration `it` reads buffer parity (it−1)&1. Launch `it` runs iteration it for
-    // role-B workgroups and forward(it−1) + backward(it) for role A; launch
-    // max_iter+1 drains A's last forward.
+    // Launch `it` runs iteration it for role-B workgroups and forward(it−1) +
+    // backward(it) for role A; launch max_iter+1 drains A's last forward.
     for (int it = 1; it <= o->max_iter + 1; ++it) {
       int flags = 0;
       if (it <= o->max_iter) flags |= ilqr::PIPE_A_BW_FLAG | ilqr::PIPE_B_FLAG;
       if (it >= 2) flags |= ilqr::PIPE_A_FW_FLAG;
       if (!flags) continue;
-      HIP_TRY(ilqr::launch_lq_iter_pipe(h->nx, h->nu, lq_params(p), h->batch, h->T,
-                                        iter_args(it, (it - 1) & 1), iter_args(it - 1, it & 1), ls,
-                                        flags, s));
+      HIP_TRY(ilqr::launch_lq_iter_pipe(h->nx, h->nu, lq_params(p), h->batch, h->T, iter_args(it),
+                                        iter_args(it - 1), ls, flags, s));
     }
-    par = o->max_iter & 1;
   }
   for (int it = 1; (two_link(p) || !h->pipelined) && it <= o->max_iter; ++it) {  // forward_pass.jl:161
     // iterations chain per chunk: chunk 0's next backward overlaps chunk 1's forward
-    const ilqr_status st = enqueue_iteration(h, p, iter_args(it, par), ls, /*chain=*/true);
+    const ilqr_status st = enqueue_iteration(h, p, iter_args(it), ls, /*chain=*/true);
     if (st != ILQR_OK) return st;
-    par ^= 1;  // x̄ⁱ, ūⁱ = x̄ⁱ⁺¹, ūⁱ⁺¹ (:174-175)
   }
   {
     const ilqr_status st = join(h, p);
     if (st != ILQR_OK) return st;
   }
-  // still-running trajectories (max_iter reached) return the last accepted iterate
-  HIP_TRY(ilqr::launch_gather_result(h->batch, h->T, h->nx, h->nu, h->xbuf[0], h->ubuf[0],
-                                     h->xbuf[1], h->ubuf[1], h->res_parity, h->status, par, x_out,
-                                     u_out, s));
-  if (cost) HIP_TRY(hipMemcpyAsync(cost, h->prev_cost, sizeof(double) * B, hipMemcpyDeviceToDevice, s));
-  if (iters) HIP_TRY(hipMemcpyAsync(iters, h->iters, sizeof(int32_t) * B, hipMemcpyDeviceToDevice, s));
-  if (status) HIP_TRY(hipMemcpyAsync(status, h->status, sizeof(int32_t) * B, hipMemcpyDeviceToDevice, s));
+  // still-running trajectories (max_iter reached) return the last accepted iterate,
+  // the one the last iteration wrote (the input when max_iter = 0)
+  const int last = o->max_iter == 0 ? ilqr::PARITY_INPUT : (o->max_iter & 1);
+  HIP_TRY(ilqr::launch_gather_result(h->batch, h->T, h->nx, h->nu, x_init, u_init, h->xbuf[0],
+                                     h->ubuf[0], h->xbuf[1], h->ubuf[1], h->res_parity, h->status,
+                                     last, h->prev_cost, h->iters, x_out, u_out, cost, iters,
+                                     status, s));
   return fold_status(h, h->status);
 }
 

@@ -65,11 +65,21 @@ hipError_t launch_lq_iter_forward(int nx, int nu, const LQParams& p, int b0, int
 constexpr int PIPE_A_FW_FLAG = 1, PIPE_A_BW_FLAG = 2, PIPE_B_FLAG = 4;
 hipError_t launch_lq_iter_pipe(int nx, int nu, const LQParams& p, int B, int T, const IterArgs& cur,
                                const IterArgs& prev, const LSParams& ls, int flags, hipStream_t s);
-// x_out[b] = (res_parity[b] ? x1 : x0)[b] (and u); status MAX_ITER for still-running ones.
-hipError_t launch_gather_result(int B, int T, int nx, int nu, const double* x0, const double* u0,
-                                const double* x1, const double* u1, const int32_t* res_parity,
-                                int32_t* status, int final_parity, double* x_out, double* u_out,
-                                hipStream_t s);
+// Result buffer codes of the fit ping-pong: 0 / 1 the handle's buffers, PARITY_INPUT
+// the caller's x_init / u_init (iteration 1 reads them in place).
+constexpr int PARITY_INPUT = 2;
+// fit's per-trajectory state: prev_cost = +Inf, status OK, res_parity INPUT, iters 0.
+hipError_t launch_fit_init(int B, double* prev_cost, int32_t* status, int32_t* res_parity,
+                           int32_t* iters, hipStream_t s);
+// x_out[b] = the buffer res_parity[b] names (final_parity for still-running ones,
+// whose status becomes MAX_ITER), and u; cost/iters/status copied out (each may be
+// null).
+hipError_t launch_gather_result(int B, int T, int nx, int nu, const double* xin, const double* uin,
+                                const double* x0, const double* u0, const double* x1,
+                                const double* u1, const int32_t* res_parity, int32_t* status,
+                                int final_parity, const double* fit_cost, const int32_t* fit_iters,
+                                double* x_out, double* u_out, double* cost_out,
+                                int32_t* iters_out, int32_t* status_out, hipStream_t s);
 hipError_t launch_fill_i32(int32_t* p, int n, int32_t v, hipStream_t s);
 hipError_t launch_fill_f64(double* p, int n, double v, hipStream_t s);
 bool lq_supported(int nx, int nu);

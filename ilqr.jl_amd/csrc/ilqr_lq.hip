@@ -1056,19 +1056,38 @@ __global__ __launch_bounds__(256, 4) void lq_iter_pipe_kernel(LQParams P, int B,
   }
 }
 
-__global__ void gather_kernel(int B, int T, int nx, int nu, const double* x0, const double* u0,
-                              const double* x1, const double* u1, const int32_t* res_parity,
-                              int32_t* status, int final_parity, double* x_out, double* u_out) {
+__global__ void gather_kernel(int B, int T, int nx, int nu, const double* xin, const double* uin,
+                              const double* x0, const double* u0, const double* x1,
+                              const double* u1, const int32_t* res_parity, int32_t* status,
+                              int final_parity, const double* fit_cost, const int32_t* fit_iters,
+                              double* x_out, double* u_out, double* cost_out, int32_t* iters_out,
+                              int32_t* status_out) {
   const int b = blockIdx.x;
   if (b >= B) return;
   const bool running = status[b] == ILQR_TRAJ_OK;
   const int par = running ? final_parity : res_parity[b];
-  const double* xs = (par ? x1 : x0) + (size_t)b * (T + 1) * nx;
-  const double* us = (par ? u1 : u0) + (size_t)b * T * nu;
+  const double* xs = (par == PARITY_INPUT ? xin : (par ? x1 : x0)) + (size_t)b * (T + 1) * nx;
+  const double* us = (par == PARITY_INPUT ? uin : (par ? u1 : u0)) + (size_t)b * T * nu;
   for (int i = threadIdx.x; i < (T + 1) * nx; i += blockDim.x) x_out[(size_t)b * (T + 1) * nx + i] = xs[i];
   for (int i = threadIdx.x; i < T * nu; i += blockDim.x) u_out[(size_t)b * T * nu + i] = us[i];
   __syncthreads();  // every wave of the block has read status[b] before it changes
-  if (threadIdx.x == 0 && running) status[b] = ILQR_TRAJ_MAX_ITER;
+  if (threadIdx.x == 0) {
+    const int32_t st = running ? ILQR_TRAJ_MAX_ITER : status[b];
+    status[b] = st;
+    if (status_out) status_out[b] = st;
+    if (cost_out) cost_out[b] = fit_cost[b];
+    if (iters_out) iters_out[b] = fit_iters[b];
+  }
+}
+
+__global__ void fit_init_kernel(int B, double* prev_cost, int32_t* status, int32_t* res_parity,
+                                int32_t* iters) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  prev_cost[b] = INFINITY;
+  status[b] = ILQR_TRAJ_OK;
+  res_parity[b] = PARITY_INPUT;
+  iters[b] = 0;
 }
 
 __global__ void fill_i32_kernel(int32_t* p, int n, int32_t v) {
@@ -1205,12 +1224,23 @@ hipError_t launch_lq_iter_pipe(int nx, int nu, const LQParams& p, int B, int T, 
   return hipErrorInvalidValue;
 }
 
-hipError_t launch_gather_result(int B, int T, int nx, int nu, const double* x0, const double* u0,
-                                const double* x1, const double* u1, const int32_t* res_parity,
-                                int32_t* status, int final_parity, double* x_out, double* u_out,
-                                hipStream_t s) {
-  gather_kernel<<<B, 256, 0, s>>>(B, T, nx, nu, x0, u0, x1, u1, res_parity, status, final_parity,
-                                  x_out, u_out);
+hipError_t launch_gather_result(int B, int T, int nx, int nu, const double* xin, const double* uin,
+                                const double* x0, const double* u0, const double* x1,
+                                const double* u1, const int32_t* res_parity, int32_t* status,
+                                int final_parity, const double* fit_cost, const int32_t* fit_iters,
+                                double* x_out, double* u_out, double* cost_out,
+                                int32_t* iters_out, int32_t* status_out, hipStream_t s) {
+  if (B <= 0) return hipSuccess;
+  gather_kernel<<<B, 256, 0, s>>>(B, T, nx, nu, xin, uin, x0, u0, x1, u1, res_parity, status,
+                                  final_parity, fit_cost, fit_iters, x_out, u_out, cost_out,
+                                  iters_out, status_out);
+  return hipGetLastError();
+}
+
+hipError_t launch_fit_init(int B, double* prev_cost, int32_t* status, int32_t* res_parity,
+                           int32_t* iters, hipStream_t s) {
+  if (B <= 0) return hipSuccess;
+  fit_init_kernel<<<(B + 255) / 256, 256, 0, s>>>(B, prev_cost, status, res_parity, iters);
   return hipGetLastError();
 }
 

@@ -327,3 +327,22 @@ def test_ring_forward_iterate_equals_standard(gpu, nb, T):
         outs.append((xa, ua, pc, st, tr))
     for a, b in zip(*outs):
         torch.testing.assert_close(a, b, rtol=0, atol=0, equal_nan=True)
+
+
+@pytest.mark.parametrize("pipelined", [False, True])
+def test_fit_zero_iterations_returns_inputs(gpu, pipelined):
+    """for iter = 1:0 runs nothing (forward_pass.jl:161): fit returns x_init, u_init
+    (the fit driver reads the caller's buffers in place; the gather copies them out)."""
+    lq, x, u = random_lq_batch(6, 12, 4, 9, seed=11)
+    s = Solver(12, 4, 9, 6)
+    s.set_problem(lq)
+    s.set_schedule(pipelined=pipelined)
+    xi, ui = dev(x), dev(u)
+    r = s.fit(xi, ui, max_iter=0)
+    assert torch.equal(r.x, xi) and torch.equal(r.u, ui)
+    assert (r.iters.cpu().numpy() == 0).all()
+    assert (r.status.cpu().numpy() == _lib.TRAJ_MAX_ITER).all()
+    assert torch.isinf(r.cost).all()
+    # the inputs are never written (ownership rule, backward_pass.jl:332-333)
+    r = s.fit(xi, ui, max_iter=5)
+    assert torch.equal(xi.cpu(), torch.from_numpy(x)) and torch.equal(ui.cpu(), torch.from_numpy(u))
