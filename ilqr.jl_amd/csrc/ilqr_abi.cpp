@@ -28,6 +28,13 @@ struct ilqr_handle {
   int32_t* res_parity = nullptr;
   int32_t* iters = nullptr;
   int32_t* host_status = nullptr;  // pinned host copy of a status array (fold_status)
+  // LQ problems of another shape (nx ≤ 12, nu ≤ 4) run zero-padded on an inner
+  // (12, 4) handle (created on the first such call): zero rows/columns of A, B, Q, R,
+  // Qf, x, u decouple exactly, so the real entries are the (12, 4) kernels' bits.
+  ilqr_handle* pad = nullptr;
+  double *pA = nullptr, *pB = nullptr, *pQ = nullptr, *pR = nullptr, *pQf = nullptr;
+  double *px = nullptr, *pu = nullptr, *pxt = nullptr, *pxn = nullptr, *pun = nullptr;
+  double *pd = nullptr, *pK = nullptr;
   // 2-link arm: per-step linearisation workspace J = [A|B] (T × 24 × batch)
   double* J = nullptr;
   // pipelining: the batch is split into `nchunks` chunks; chunk i's forward pass
@@ -63,11 +70,18 @@ ilqr::LQParams lq_params(const ilqr_problem* p) {
   return ilqr::LQParams{p->A, p->B, p->Q, p->R, p->Qf};
 }
 
+constexpr int PAD_NX = 12, PAD_NU = 4;  // the compiled LQ shape padded problems run at
+
+bool lq_paddable(int nx, int nu) {
+  return !ilqr::lq_supported(nx, nu) && nx <= PAD_NX && nu <= PAD_NU &&
+         ilqr::lq_supported(PAD_NX, PAD_NU);
+}
+
 ilqr_status check_problem(const ilqr_handle* h, const ilqr_problem* p) {
   if (!h || !p) return ILQR_ERR_BAD_ARG;
   if (p->kind == ILQR_PROBLEM_LQ) {
     if (!p->A || !p->B || !p->Q || !p->R || !p->Qf) return ILQR_ERR_BAD_ARG;
-    if (!ilqr::lq_supported(h->nx, h->nu)) return ILQR_ERR_UNSUPPORTED;
+    if (!ilqr::lq_supported(h->nx, h->nu) && !lq_paddable(h->nx, h->nu)) return ILQR_ERR_UNSUPPORTED;
     return ILQR_OK;
   }
   if (p->kind == ILQR_PROBLEM_TWO_LINK) {
@@ -80,6 +94,10 @@ ilqr_status check_problem(const ilqr_handle* h, const ilqr_problem* p) {
 }
 
 bool two_link(const ilqr_problem* p) { return p->kind == ILQR_PROBLEM_TWO_LINK; }
+
+bool padded(const ilqr_handle* h, const ilqr_problem* p) {
+  return p->kind == ILQR_PROBLEM_LQ && lq_paddable(h->nx, h->nu);
+}
 
 ilqr::LSParams ls_params(const ilqr_options* o) {
   ilqr_options def;
@@ -147,6 +165,84 @@ ilqr_status fold_status(ilqr_handle* h, const int32_t* dev_status) {
   return nan ? ILQR_ERR_NAN : (ls ? ILQR_ERR_LS_EXHAUSTED : ILQR_OK);
 }
 
+// Inner (12, 4) handle and padded scratch, created on the first padded call (the
+// only allocation outside ilqr_create); stream and schedule follow the outer handle.
+ilqr_status ensure_pad(ilqr_handle* h) {
+  if (!h->pad) {
+    ilqr_handle* in = nullptr;
+    const ilqr_status st = ilqr_create(&in, h->device, PAD_NX, PAD_NU, h->T, h->batch);
+    if (st != ILQR_OK) return st;
+    h->pad = in;
+    const size_t B = (size_t)h->batch, T = (size_t)h->T;
+    hipError_t e = hipSuccess;
+    auto al = [&](double** q, size_t n) { if (e == hipSuccess) e = hipMalloc(q, sizeof(double) * n); };
+    al(&h->pA, B * PAD_NX * PAD_NX);
+    al(&h->pB, B * PAD_NX * PAD_NU);
+    al(&h->pQ, B * PAD_NX * PAD_NX);
+    al(&h->pR, B * PAD_NU * PAD_NU);
+    al(&h->pQf, B * PAD_NX * PAD_NX);
+    al(&h->px, B * (T + 1) * PAD_NX);
+    al(&h->pxt, B * (T + 1) * PAD_NX);
+    al(&h->pxn, B * (T + 1) * PAD_NX);
+    al(&h->pu, B * T * PAD_NU);
+    al(&h->pun, B * T * PAD_NU);
+    al(&h->pd, B * T * PAD_NU);
+    al(&h->pK, B * T * PAD_NU * PAD_NX);
+    if (e != hipSuccess) return hip_fail(e, "ilqr: padded workspace");
+  }
+  h->pad->stream = h->stream;
+  h->pad->pipelined = h->pipelined;
+  h->pad->fw_ring = h->fw_ring;
+  return ILQR_OK;
+}
+
+// (N, R, C) → (N, R2, C2) zero-padded, and back
+ilqr_status pad3(ilqr_handle* h, const double* src, double* dst, size_t N, int R, int C, int R2, int C2) {
+  HIP_TRY(ilqr::launch_pad3(src, dst, N, R, C, R2, C2, h->stream));
+  return ILQR_OK;
+}
+ilqr_status unpad3(ilqr_handle* h, const double* src, double* dst, size_t N, int R, int C, int R2, int C2) {
+  HIP_TRY(ilqr::launch_unpad3(src, dst, N, R, C, R2, C2, h->stream));
+  return ILQR_OK;
+}
+
+#define ILQR_TRY(expr)                    \
+  do {                                    \
+    const ilqr_status s_ = (expr);        \
+    if (s_ != ILQR_OK) return s_;         \
+  } while (0)
+
+// pad the LQ problem data into the scratch and describe it
+ilqr_status pad_problem(ilqr_handle* h, const ilqr_problem* p, ilqr_problem* pp) {
+  const size_t B = (size_t)h->batch;
+  const int n = h->nx, m = h->nu;
+  ILQR_TRY(pad3(h, p->A, h->pA, B, n, n, PAD_NX, PAD_NX));
+  ILQR_TRY(pad3(h, p->B, h->pB, B, n, m, PAD_NX, PAD_NU));
+  ILQR_TRY(pad3(h, p->Q, h->pQ, B, n, n, PAD_NX, PAD_NX));
+  ILQR_TRY(pad3(h, p->R, h->pR, B, m, m, PAD_NU, PAD_NU));
+  ILQR_TRY(pad3(h, p->Qf, h->pQf, B, n, n, PAD_NX, PAD_NX));
+  *pp = *p;
+  pp->A = h->pA;
+  pp->B = h->pB;
+  pp->Q = h->pQ;
+  pp->R = h->pR;
+  pp->Qf = h->pQf;
+  return ILQR_OK;
+}
+// trajectories: x-like (B, T+1, nx), u-like (B, T, nu), gains K (B·T, nu, nx)
+ilqr_status pad_x(ilqr_handle* h, const double* x, double* px) {
+  return pad3(h, x, px, (size_t)h->batch, h->T + 1, h->nx, h->T + 1, PAD_NX);
+}
+ilqr_status pad_u(ilqr_handle* h, const double* u, double* pu) {
+  return pad3(h, u, pu, (size_t)h->batch, h->T, h->nu, h->T, PAD_NU);
+}
+ilqr_status unpad_x(ilqr_handle* h, const double* px, double* x) {
+  return unpad3(h, px, x, (size_t)h->batch, h->T + 1, h->nx, h->T + 1, PAD_NX);
+}
+ilqr_status unpad_u(ilqr_handle* h, const double* pu, double* u) {
+  return unpad3(h, pu, u, (size_t)h->batch, h->T, h->nu, h->T, PAD_NU);
+}
+
 }  // namespace
 
 extern "C" {
@@ -179,7 +275,7 @@ void ilqr_default_options(ilqr_options* o) {
 }
 
 int ilqr_supported(int32_t kind, int nx, int nu) {
-  if (kind == ILQR_PROBLEM_LQ) return ilqr::lq_supported(nx, nu) ? 1 : 0;
+  if (kind == ILQR_PROBLEM_LQ) return (ilqr::lq_supported(nx, nu) || lq_paddable(nx, nu)) ? 1 : 0;
   if (kind == ILQR_PROBLEM_TWO_LINK) return ilqr::tl_supported(nx, nu) ? 1 : 0;
   if (kind == ILQR_PROBLEM_TILES) return ilqr::tiles_supported(nx, nu) ? 1 : 0;
   if (kind == ILQR_PROBLEM_CHAIN) return (nx % 2 == 0) ? ilqr_chain_supported(nx / 2, nu) : 0;
@@ -256,6 +352,11 @@ ilqr_status ilqr_destroy(ilqr_handle* h) {
   (void)hipFree(h->res_parity);
   (void)hipFree(h->iters);
   if (h->host_status) (void)hipHostFree(h->host_status);
+  if (h->pad) {
+    (void)ilqr_destroy(h->pad);
+    for (double* q : {h->pA, h->pB, h->pQ, h->pR, h->pQf, h->px, h->pu, h->pxt, h->pxn, h->pun, h->pd, h->pK})
+      (void)hipFree(q);
+  }
   (void)hipFree(h->J);
   for (int c = 0; c < 2; ++c) {
     if (h->ev_bw[c]) (void)hipEventDestroy(h->ev_bw[c]);
@@ -293,6 +394,20 @@ ilqr_status ilqr_backward(ilqr_handle* h, const ilqr_problem* p, const ilqr_opti
   if ((st = check_options(o)) != ILQR_OK) return st;
   if (!x || !u || !d || !K) return ILQR_ERR_BAD_ARG;
   HIP_TRY(hipSetDevice(h->device));
+  if (padded(h, p)) {
+    ILQR_TRY(ensure_pad(h));
+    ilqr_problem pp;
+    ILQR_TRY(pad_problem(h, p, &pp));
+    ILQR_TRY(pad_x(h, x, h->px));
+    ILQR_TRY(pad_u(h, u, h->pu));
+    // with a status array the inner call folds it (and synchronises)
+    const ilqr_status bst = ilqr_backward(h->pad, &pp, o, h->px, h->pu, h->pd, h->pK, status);
+    if (bst != ILQR_OK && bst != ILQR_ERR_NAN) return bst;
+    ILQR_TRY(unpad_u(h, h->pd, d));
+    ILQR_TRY(unpad3(h, h->pK, K, (size_t)h->batch * h->T, h->nu, h->nx, PAD_NU, PAD_NX));
+    if (status) HIP_TRY(hipStreamSynchronize(h->stream));
+    return bst;
+  }
   if (two_link(p))
     HIP_TRY(ilqr::launch_tl_backward(ilqr::two_link_params(), h->batch, h->T, x, u, h->J, d, K,
                                      status, ls_params(o).mu, h->stream));
@@ -328,6 +443,24 @@ ilqr_status ilqr_forward(ilqr_handle* h, const ilqr_problem* p, const ilqr_optio
   if ((st = check_options(o)) != ILQR_OK) return st;
   if (!x || !u || !d || !K || !prev_cost || !x_new || !u_new || !new_cost) return ILQR_ERR_BAD_ARG;
   HIP_TRY(hipSetDevice(h->device));
+  if (padded(h, p)) {
+    ILQR_TRY(ensure_pad(h));
+    ilqr_problem pp;
+    ILQR_TRY(pad_problem(h, p, &pp));
+    ILQR_TRY(pad_x(h, x, h->px));
+    ILQR_TRY(pad_u(h, u, h->pu));
+    if (x_traj) ILQR_TRY(pad_x(h, x_traj, h->pxt));
+    ILQR_TRY(pad_u(h, d, h->pd));
+    ILQR_TRY(pad3(h, K, h->pK, (size_t)h->batch * h->T, h->nu, h->nx, PAD_NU, PAD_NX));
+    const ilqr_status fst = ilqr_forward(h->pad, &pp, o, h->px, h->pu, x_traj ? h->pxt : nullptr,
+                                         h->pd, h->pK, prev_cost, h->pxn, h->pun, new_cost, trials,
+                                         status);
+    if (fst != ILQR_OK && fst != ILQR_ERR_NAN && fst != ILQR_ERR_LS_EXHAUSTED) return fst;
+    ILQR_TRY(unpad_x(h, h->pxn, x_new));
+    ILQR_TRY(unpad_u(h, h->pun, u_new));
+    if (status) HIP_TRY(hipStreamSynchronize(h->stream));
+    return fst;
+  }
   if (two_link(p))
     HIP_TRY(ilqr::launch_tl_forward(ilqr::two_link_params(), h->batch, h->T, x, u, x_traj, d, K,
                                     prev_cost, x_new, u_new, new_cost, trials, status,
@@ -349,6 +482,18 @@ ilqr_status ilqr_iterate(ilqr_handle* h, const ilqr_problem* p, const ilqr_optio
   if ((st = check_options(o)) != ILQR_OK) return st;
   if (!x || !u || !x_new || !u_new || !new_cost || !status) return ILQR_ERR_BAD_ARG;
   HIP_TRY(hipSetDevice(h->device));
+  if (padded(h, p)) {
+    ILQR_TRY(ensure_pad(h));
+    ilqr_problem pp;
+    ILQR_TRY(pad_problem(h, p, &pp));
+    ILQR_TRY(pad_x(h, x, h->px));
+    ILQR_TRY(pad_u(h, u, h->pu));
+    if (x_traj) ILQR_TRY(pad_x(h, x_traj, h->pxt));
+    ILQR_TRY(ilqr_iterate(h->pad, &pp, o, h->px, h->pu, x_traj ? h->pxt : nullptr, h->pxn, h->pun,
+                          prev_cost, new_cost, du2, trials, status));
+    ILQR_TRY(unpad_x(h, h->pxn, x_new));
+    return unpad_u(h, h->pun, u_new);
+  }
   ilqr::IterArgs a{};
   a.x = x;
   a.u = u;
@@ -381,6 +526,21 @@ ilqr_status ilqr_fit(ilqr_handle* h, const ilqr_problem* p, const ilqr_options* 
   ilqr_default_options(&def);
   if (!o) o = &def;
   HIP_TRY(hipSetDevice(h->device));
+  if (padded(h, p)) {
+    ILQR_TRY(ensure_pad(h));
+    ilqr_problem pp;
+    ILQR_TRY(pad_problem(h, p, &pp));
+    ILQR_TRY(pad_x(h, x_init, h->px));
+    ILQR_TRY(pad_u(h, u_init, h->pu));
+    if (x_traj) ILQR_TRY(pad_x(h, x_traj, h->pxt));
+    const ilqr_status fst = ilqr_fit(h->pad, &pp, o, h->px, h->pu, x_traj ? h->pxt : nullptr,
+                                     h->pxn, h->pun, cost, iters, status);
+    if (fst != ILQR_OK && fst != ILQR_ERR_NAN && fst != ILQR_ERR_LS_EXHAUSTED) return fst;
+    ILQR_TRY(unpad_x(h, h->pxn, x_out));
+    ILQR_TRY(unpad_u(h, h->pun, u_out));
+    HIP_TRY(hipStreamSynchronize(h->stream));  // fit returns with its outputs written
+    return fst;
+  }
   hipStream_t s = h->stream;
   // prev_cost = Inf (forward_pass.jl:159), status OK, result "the input", iters 0
   HIP_TRY(ilqr::launch_fit_init(h->batch, h->prev_cost, h->status, h->res_parity, h->iters, s));

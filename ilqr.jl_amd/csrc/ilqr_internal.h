@@ -80,6 +80,11 @@ hipError_t launch_gather_result(int B, int T, int nx, int nu, const double* xin,
                                 int final_parity, const double* fit_cost, const int32_t* fit_iters,
                                 double* x_out, double* u_out, double* cost_out,
                                 int32_t* iters_out, int32_t* status_out, hipStream_t s);
+// (N, R, C) row-major → (N, R2, C2) zero-padded (R2 ≥ R, C2 ≥ C), and back.
+hipError_t launch_pad3(const double* src, double* dst, size_t N, int R, int C, int R2, int C2,
+                       hipStream_t s);
+hipError_t launch_unpad3(const double* src, double* dst, size_t N, int R, int C, int R2, int C2,
+                         hipStream_t s);
 hipError_t launch_fill_i32(int32_t* p, int n, int32_t v, hipStream_t s);
 hipError_t launch_fill_f64(double* p, int n, double v, hipStream_t s);
 bool lq_supported(int nx, int nu);

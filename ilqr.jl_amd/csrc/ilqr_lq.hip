@@ -1090,6 +1090,28 @@ __global__ void fit_init_kernel(int B, double* prev_cost, int32_t* status, int32
   iters[b] = 0;
 }
 
+// one thread per destination element; consecutive threads → consecutive elements
+__global__ void pad3_kernel(const double* __restrict__ src, double* __restrict__ dst, size_t total,
+                            int R, int C, int R2, int C2) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int c = (int)(i % C2);
+  const size_t rr = i / C2;
+  const int r = (int)(rr % R2);
+  const size_t n = rr / R2;
+  dst[i] = (r < R && c < C) ? src[(n * R + r) * C + c] : 0.0;
+}
+__global__ void unpad3_kernel(const double* __restrict__ src, double* __restrict__ dst, size_t total,
+                              int R, int C, int R2, int C2) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int c = (int)(i % C);
+  const size_t rr = i / C;
+  const int r = (int)(rr % R);
+  const size_t n = rr / R;
+  dst[i] = src[(n * R2 + r) * C2 + c];
+}
+
 __global__ void fill_i32_kernel(int32_t* p, int n, int32_t v) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) p[i] = v;
@@ -1241,6 +1263,21 @@ hipError_t launch_fit_init(int B, double* prev_cost, int32_t* status, int32_t* r
                            int32_t* iters, hipStream_t s) {
   if (B <= 0) return hipSuccess;
   fit_init_kernel<<<(B + 255) / 256, 256, 0, s>>>(B, prev_cost, status, res_parity, iters);
+  return hipGetLastError();
+}
+
+hipError_t launch_pad3(const double* src, double* dst, size_t N, int R, int C, int R2, int C2,
+                       hipStream_t s) {
+  const size_t total = N * R2 * C2;
+  if (total == 0) return hipSuccess;
+  pad3_kernel<<<(unsigned)((total + 255) / 256), 256, 0, s>>>(src, dst, total, R, C, R2, C2);
+  return hipGetLastError();
+}
+hipError_t launch_unpad3(const double* src, double* dst, size_t N, int R, int C, int R2, int C2,
+                         hipStream_t s) {
+  const size_t total = N * R * C;
+  if (total == 0) return hipSuccess;
+  unpad3_kernel<<<(unsigned)((total + 255) / 256), 256, 0, s>>>(src, dst, total, R, C, R2, C2);
   return hipGetLastError();
 }
 

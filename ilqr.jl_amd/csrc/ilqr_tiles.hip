@@ -214,9 +214,8 @@ __global__ __launch_bounds__(256) void tiles_backward_kernel(TileParams P, int B
 
 }  // namespace
 
-bool tiles_supported(int nx, int nu) {
-  return (nx == 12 && nu == 4) || (nx == 4 && nu == 2) || (nx == 4 && nu == 1);
-}
+// every state dimension 1..12 with 1..4 inputs (nx + nu ≤ 16, nu ≤ 4: one MFMA tile)
+bool tiles_supported(int nx, int nu) { return nx >= 1 && nx <= 12 && nu >= 1 && nu <= 4; }
 
 hipError_t launch_tiles_backward(int nx, int nu, const TileParams& p, int B, int T, double* d,
                                  double* K, int32_t* status, double mu, hipStream_t s) {
@@ -226,9 +225,10 @@ hipError_t launch_tiles_backward(int nx, int nu, const TileParams& p, int B, int
     tiles_backward_kernel<NXV, NUV><<<grid, 256, 0, s>>>(p, B, T, d, K, status, mu);          \
     return hipGetLastError();                                                                  \
   }
-  ILQR_TILES_CASE(12, 4)
-  ILQR_TILES_CASE(4, 2)
-  ILQR_TILES_CASE(4, 1)
+#define ILQR_TILES_NU(NXV) ILQR_TILES_CASE(NXV, 1) ILQR_TILES_CASE(NXV, 2) ILQR_TILES_CASE(NXV, 3) ILQR_TILES_CASE(NXV, 4)
+  ILQR_TILES_NU(1) ILQR_TILES_NU(2) ILQR_TILES_NU(3) ILQR_TILES_NU(4) ILQR_TILES_NU(5) ILQR_TILES_NU(6)
+  ILQR_TILES_NU(7) ILQR_TILES_NU(8) ILQR_TILES_NU(9) ILQR_TILES_NU(10) ILQR_TILES_NU(11) ILQR_TILES_NU(12)
+#undef ILQR_TILES_NU
 #undef ILQR_TILES_CASE
   return hipErrorInvalidValue;
 }

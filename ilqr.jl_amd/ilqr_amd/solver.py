@@ -10,6 +10,7 @@ from __future__ import annotations
 import ctypes as C
 from dataclasses import dataclass
 
+import numpy as np
 import torch
 
 from . import _lib
@@ -94,7 +95,8 @@ class Solver:
             raise TypeError("set_problem: only the LQ family has per-instance data")
         nb, nx, nu = self.batch, self.nx, self.nu
         if isinstance(lq, LQBatch):
-            t = {k: torch.from_numpy(getattr(lq, k)).to(self.dev) for k in ("A", "B", "Q", "R", "Qf")}
+            t = {k: torch.from_numpy(np.require(getattr(lq, k), np.float64, ("C", "W"))).to(self.dev)
+                 for k in ("A", "B", "Q", "R", "Qf")}
         else:
             t = dict(lq)
         shapes = {"A": (nb, nx, nx), "B": (nb, nx, nu), "Q": (nb, nx, nx), "R": (nb, nu, nu),

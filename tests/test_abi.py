@@ -45,11 +45,15 @@ def test_status_strings_and_defaults():
 def test_supported_shapes():
     lib = _lib.load()
     assert lib.ilqr_supported(_lib.PROBLEM_LQ, 12, 4) == 1
-    assert lib.ilqr_supported(_lib.PROBLEM_LQ, 5, 3) == 0
+    assert lib.ilqr_supported(_lib.PROBLEM_LQ, 5, 3) == 1   # zero-padded onto (12, 4)
+    assert lib.ilqr_supported(_lib.PROBLEM_LQ, 13, 3) == 0
+    assert lib.ilqr_supported(_lib.PROBLEM_LQ, 12, 5) == 0
     assert lib.ilqr_supported(99, 12, 4) == 0
     assert lib.ilqr_supported(_lib.PROBLEM_TWO_LINK, 4, 2) == 1
     assert lib.ilqr_supported(_lib.PROBLEM_TWO_LINK, 12, 4) == 0
-    assert lib.ilqr_supported(_lib.PROBLEM_LQ, 4, 2) == 0
+    assert lib.ilqr_supported(_lib.PROBLEM_LQ, 4, 2) == 1
+    assert lib.ilqr_supported(_lib.PROBLEM_TILES, 7, 3) == 1
+    assert lib.ilqr_supported(_lib.PROBLEM_TILES, 13, 1) == 0
 
 
 def test_header_problem_kinds_match_binding():

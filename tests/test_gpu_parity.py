@@ -346,3 +346,49 @@ def test_fit_zero_iterations_returns_inputs(gpu, pipelined):
     # the inputs are never written (ownership rule, backward_pass.jl:332-333)
     r = s.fit(xi, ui, max_iter=5)
     assert torch.equal(xi.cpu(), torch.from_numpy(x)) and torch.equal(ui.cpu(), torch.from_numpy(u))
+
+
+# -- LQ problems of other shapes: zero-padded onto the (12, 4) kernels ---------------
+PAD_SHAPES = [(1, 1), (3, 2), (4, 1), (4, 2), (6, 2), (8, 3), (10, 4), (12, 1), (12, 3)]
+
+
+@pytest.mark.parametrize("nx,nu", PAD_SHAPES)
+def test_lq_padded_shapes_vs_oracle(gpu, nx, nu):
+    """Any nx ≤ 12, nu ≤ 4 runs on the (12, 4) kernels with zero rows/columns
+    (exactly decoupled): backward, forward, iterate and fit against the C oracle."""
+    nb, T = 9, 25
+    lq, x, u = random_lq_batch(nb, nx, nu, T, seed=17 * nx + nu)
+    assert _lib.load().ilqr_supported(_lib.PROBLEM_LQ, nx, nu) == 1
+    s = Solver(nx, nu, T, nb)
+    s.set_problem(lq)
+    xi, ui = dev(x), dev(u)
+    d, K, st = s.backward(xi, ui)
+    assert d.shape == (nb, T, nu) and K.shape == (nb, T, nu, nx)
+    dc, Kc, _ = cref.lq_backward(lq, x, u, symmetrize=True)
+    assert (st.cpu().numpy() == 0).all()
+    assert rel(K, Kc) < TOL_GAIN_SYM and rel(d, dc) < TOL_GAIN_SYM
+    pc = torch.full((nb,), float("inf"), dtype=torch.float64, device="cuda")
+    xn, un, c, tr, st = s.forward(xi, ui, d, K, pc)
+    xo, uo, co, tro = cref.lq_forward(lq, x, u, None, d.cpu().numpy(), K.cpu().numpy(), np.inf)
+    assert rel(xn, xo) < TOL_ROLL and rel(un, uo) < TOL_ROLL and rel(c, co) < TOL_COST
+    assert np.array_equal(tr.cpu().numpy(), tro)
+    # iterate = backward + forward, bit for bit
+    xn2, un2 = torch.empty_like(xi), torch.empty_like(ui)
+    pc2 = torch.full((nb,), float("inf"), dtype=torch.float64, device="cuda")
+    st2 = torch.zeros((nb,), dtype=torch.int32, device="cuda")
+    s.iterate(xi, ui, xn2, un2, pc2, st2, options=_lib.default_options(tol=-1.0))
+    torch.cuda.synchronize()
+    assert torch.equal(xn2, xn) and torch.equal(un2, un) and torch.equal(pc2, c)
+    r = s.fit(xi, ui, max_iter=15, tol=1e-8)
+    xf, uf, cf, itf, stf = cref.lq_fit(lq, x, u, max_iter=15, tol=1e-8, symmetrize=True)
+    assert r.x.shape == (nb, T + 1, nx) and r.u.shape == (nb, T, nu)
+    assert np.array_equal(r.iters.cpu().numpy(), itf)
+    assert rel(r.u, uf) < 1e-8 and rel(r.x, xf) < 1e-8
+
+
+def test_lq_unsupported_shapes_raise(gpu):
+    lib = _lib.load()
+    for nx, nu in ((13, 1), (12, 5), (16, 4)):
+        assert lib.ilqr_supported(_lib.PROBLEM_LQ, nx, nu) == 0
+        with pytest.raises(NotImplementedError):
+            Solver(nx, nu, 10, 4)

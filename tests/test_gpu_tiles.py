@@ -65,9 +65,37 @@ def lq_tiles(lq, x, u):
 
 def test_tiles_supported_shapes(gpu):
     lib = _lib.load()
-    for nx, nu in ((12, 4), (4, 2), (4, 1)):
-        assert lib.ilqr_supported(_lib.PROBLEM_TILES, nx, nu) == 1
-    assert lib.ilqr_supported(_lib.PROBLEM_TILES, 7, 3) == 0
+    for nx in range(1, 13):
+        for nu in range(1, 5):
+            assert lib.ilqr_supported(_lib.PROBLEM_TILES, nx, nu) == 1
+    for nx, nu in ((13, 1), (12, 5), (0, 1), (4, 0)):
+        assert lib.ilqr_supported(_lib.PROBLEM_TILES, nx, nu) == 0
+
+
+def random_tiles(nb, T, n, m, seed):
+    rng = np.random.default_rng(seed)
+    A = np.eye(n) + 0.03 * rng.standard_normal((nb, T, n, n))
+    Bm = 0.2 * rng.standard_normal((nb, T, n, m))
+    Mq = rng.standard_normal((nb, T, n, n))
+    lxx = 0.1 * np.einsum("btij,btkj->btik", Mq, Mq) / n + np.eye(n)
+    Mr = rng.standard_normal((nb, T, m, m))
+    luu = 0.05 * np.einsum("btij,btkj->btik", Mr, Mr) / m + 0.2 * np.eye(m)
+    Mf = rng.standard_normal((nb, n, n))
+    return {"A": A, "B": Bm, "lx": rng.standard_normal((nb, T, n)), "lu": rng.standard_normal((nb, T, m)),
+            "lxx": lxx, "lux": 0.05 * rng.standard_normal((nb, T, m, n)), "luu": luu,
+            "lfx": rng.standard_normal((nb, n)), "lfxx": 0.1 * np.einsum("bij,bkj->bik", Mf, Mf) + 2 * np.eye(n)}
+
+
+@pytest.mark.parametrize("n,m", [(1, 1), (2, 1), (3, 2), (5, 3), (6, 4), (7, 4), (9, 2), (11, 3), (12, 1)])
+def test_tiles_every_shape_vs_oracle(gpu, n, m):
+    """ilqr_backward_tiles is compiled for every nx ≤ 12, nu ≤ 4 (one MFMA tile)."""
+    nb, T = 9, 40
+    tl = random_tiles(nb, T, n, m, seed=100 * n + m)
+    s = Solver(n, m, T, nb, kind=_lib.PROBLEM_TILES)
+    d, K, st = s.backward_tiles(to_dev(tl))
+    assert (st.cpu().numpy() == 0).all()
+    dr, Kr, _ = cref.tiles_backward(tl, symmetrize=True)
+    assert rel(d, dr) < 1e-10 and rel(K, Kr) < 1e-10
 
 
 def test_tiles_pendula_vs_oracle(gpu):
