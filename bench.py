@@ -147,6 +147,16 @@ def main():
     s._bind_stream()
 
     st.zero_()  # stays 0: from a cold start no trajectory converges or exhausts
+    # the roofline leg's buffers, allocated and first touched before any timing (a
+    # 157 MB first touch between the legs would idle the GPU and drop its clock)
+    d = torch.empty((B, T, NU), dtype=torch.float64, device=dev)
+    K = torch.empty((B, T, NU, NX), dtype=torch.float64, device=dev)
+    o = _lib.default_options()
+
+    def backward_only():
+        s.lib.ilqr_backward(s.h, s._p(), C.byref(o), _ptr(x), _ptr(u), _ptr(d), _ptr(K), None)
+
+    backward_only()
 
     def step():  # cold start: prev_cost = +Inf (NULL), the new cost lands in pc
         s.iterate(x, u, xn, un, None, st, trials=trials, options=opts, new_cost=pc)
@@ -175,23 +185,21 @@ def main():
         tt = torch.tensor([ms_step], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         tdist.all_reduce(tt, op=tdist.ReduceOp.MAX)
         ms_step = float(tt.item())
-    mean_trials = float(trials.double().mean().item())
-    ok = bool((st == 0).all().item())
-
-    # dominant kernel: the backward pass, timed alone on the same stream
-    d = torch.empty((B, T, NU), dtype=torch.float64, device=dev)
-    K = torch.empty((B, T, NU, NX), dtype=torch.float64, device=dev)
-    o = _lib.default_options()
-    nrep = max(5, args.steps)
-    for _ in range(2):
-        s.lib.ilqr_backward(s.h, s._p(), C.byref(o), _ptr(x), _ptr(u), _ptr(d), _ptr(K), None)
+    # dominant kernel: the backward pass, timed alone on the same stream right after
+    # the timed loop (GPU still at its loaded clock), after a short untimed run-in
+    nrep = max(50, args.steps)
+    for _ in range(20):
+        backward_only()
     b0, b1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     b0.record(stream)
     for _ in range(nrep):
-        s.lib.ilqr_backward(s.h, s._p(), C.byref(o), _ptr(x), _ptr(u), _ptr(d), _ptr(K), None)
+        backward_only()
     b1.record(stream)
     torch.cuda.synchronize()
     bw_ms = b0.elapsed_time(b1) / nrep
+    # result checks only now: their first torch reductions load kernels (~0.1 s idle)
+    mean_trials = float(trials.double().mean().item())
+    ok = bool((st == 0).all().item())
 
     # result exchange (fit output): all-gather the per-trajectory costs over RCCL
     gather_ms = None
