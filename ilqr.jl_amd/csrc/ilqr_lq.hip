@@ -160,6 +160,20 @@ namespace {
       : [p0] "v"(p[0]), [p1] "v"(p[1]), [p2] "v"(p[2]), [p3] "v"(p[3]), [p4] "v"(p[4]), [p5] "v"(p[5]), [p6] "v"(p[6]), [p7] "v"(p[7]), [p8] "v"(p[8]), [p9] "v"(p[9]), [p10] "v"(p[10]), [p11] "v"(p[11]), [f0] "v"(f[0]), [f1] "v"(f[1]), [f2] "v"(f[2]), [f3] "v"(f[3]), [f4] "v"(f[4]), [f5] "v"(f[5]), [f6] "v"(f[6]), [f7] "v"(f[7]), [f8] "v"(f[8]), [f9] "v"(f[9]), [f10] "v"(f[10]), [f11] "v"(f[11]));
 }
 
+// Σ_j<4 bcast_j(src)·c[j]: src broadcast from lane j of each 16-lane row, two
+// accumulators. `s_nop 4` covers the VALU→DPP read hazard.
+__device__ __forceinline__ double dpp_dot4(double src, double c0, double c1, double c2, double c3) {
+  double a0 = 0.0, a1 = 0.0;
+  asm("s_nop 4\n\t"
+      "v_fmac_f64_dpp %[a0], %[s], %[c0] row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[a1], %[s], %[c1] row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[a0], %[s], %[c2] row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[a1], %[s], %[c3] row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+      : [a0] "+v"(a0), [a1] "+v"(a1)
+      : [s] "v"(src), [c0] "v"(c0), [c1] "v"(c1), [c2] "v"(c2), [c3] "v"(c3));
+  return a0 + a1;
+}
+
 // ---------------------------------------------------------------------------
 // Backward pass of one trajectory by one wave (backward_pass.jl:324-357).
 // Writes d (T,NU) and K (T,NU,NX) of trajectory b. Returns true if any gain is NaN
@@ -171,7 +185,9 @@ namespace {
 // bits (correct gains): 32 two Newton steps per reciprocal (product: one), 64
 // symmetrise every SYM_EVERY/2 steps, 128 Schur-complement 2×2-block solve instead
 // of LDLᵀ (NU = 4), 256 round-1 gradient (one 4-lane reduction of Lz + Fᵀs after
-// the MFMAs), 512 round-1 gain stores (exec-masked branch).
+// the MFMAs), 512 round-1 gain stores (exec-masked branch), 2048 the gain solve by
+// cofactors spread over the lanes (COF) instead of the redundant LDLᵀ per lane,
+// 8192 COF without its refinement step.
 template <int NX, int NU, int ABL = 0>
 __device__ bool lq_backward_wave(const LQParams& P, int b, int T, const double* __restrict__ x,
                                  const double* __restrict__ u, double* __restrict__ d_out,
@@ -244,6 +260,30 @@ __device__ bool lq_backward_wave(const LQParams& P, int b, int T, const double* 
   int qv_at[KS];
 #pragma unroll
   for (int r = 0; r < KS; ++r) qv_at[r] = (c == SROW && q + 4 * r < NX) ? 64 + q + 4 * r : ZERO;
+  // COF: lane (q, c) forms the cofactor C[q][c&3] of H_reg = H + μI (stored in LDS
+  // with μ on its diagonal) from the 3×3 minor without row q and column c&3, read
+  // from the lower triangle; row q of H_reg feeds the determinant.
+  constexpr bool COF = NU == 4 && (ABL & 2048) != 0;  // ablation variant
+  int m_at[COF ? 9 : 1], hrow_at[COF ? 4 : 1];
+  double csign = 1.0;
+  if constexpr (COF) {
+    const int bq = c & 3;
+    int rr[3], cc[3];
+#pragma unroll
+    for (int k = 0, n = 0; k < 4; ++k)
+      if (k != q) rr[n++] = k;
+#pragma unroll
+    for (int k = 0, n = 0; k < 4; ++k)
+      if (k != bq) cc[n++] = k;
+    auto at = [](int i, int j) { return (i > j ? i : j) * 16 + NX + (i > j ? j : i); };
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int j = 0; j < 3; ++j) m_at[3 * i + j] = at(rr[i], cc[j]);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) hrow_at[j] = at(q, j);
+    csign = ((q + bq) & 1) ? -1.0 : 1.0;
+  }
 
   // Terminal value function (final_cost_quadratization :134-153, ℓ_f = xᵀQf x):
   // S = Qf+Qfᵀ, s = (Qf+Qfᵀ) x_N.
@@ -358,13 +398,14 @@ __device__ bool lq_backward_wave(const LQParams& P, int b, int T, const double* 
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int i = q + 4 * r;
-      if (i >= NX && i < NX + NU) Gl[(i - NX) * 16 + c] = Z[r];
+      if (i >= NX && i < NX + NU) Gl[(i - NX) * 16 + c] = COF && c == i ? Z[r] + mu : Z[r];
     }
     if constexpr ((ABL & 256) != 0)
       gl[c] = gq;  // the four lanes of column c hold the same value
     else
       lds[(q == SROW % 4) ? 64 + c : JUNK + l] = gq;
     double h[NU][NU];
+    double mn[COF ? 9 : 1], hr[COF ? 4 : 1];
     d4 col = {0.0, 0.0, 0.0, 0.0};
     double colq;
     double qv[KS];
@@ -380,10 +421,17 @@ __device__ bool lq_backward_wave(const LQParams& P, int b, int T, const double* 
       for (int r = 0; r < KS; ++r) qv[r] = gq;
     } else {
       wave_lds_fence();
+      if constexpr (COF) {
 #pragma unroll
-      for (int i = 0; i < NU; ++i)
+        for (int k = 0; k < 9; ++k) mn[k] = lds[m_at[k]];
 #pragma unroll
-        for (int k = 0; k <= i; ++k) h[i][k] = Gl[i * 16 + NX + k];
+        for (int j = 0; j < 4; ++j) hr[j] = lds[hrow_at[j]];
+      } else {
+#pragma unroll
+        for (int i = 0; i < NU; ++i)
+#pragma unroll
+          for (int k = 0; k <= i; ++k) h[i][k] = Gl[i * 16 + NX + k];
+      }
 #pragma unroll
       for (int j = 0; j < NU; ++j) col[j] = lds[col_at[j]];     // [G | g][j][c], 0 for c > NX
       colq = lds[colq_at];                                      // [G | g][q][c]
@@ -393,20 +441,60 @@ __device__ bool lq_backward_wave(const LQParams& P, int b, int T, const double* 
     }
 
     // feedback_parameters (:207-218): K_aug[:,c] = -(H + μI)⁻¹ [G | g][:,c]
-    d4 xs;
+    double sol;  // ((H + μI)⁻¹ [G | g])[q][c]
     if constexpr ((ABL & 1) != 0) {
       asm volatile("" ::"v"(h[0][0]), "v"(h[1][0]), "v"(h[2][1]), "v"(h[3][3]));
-      xs = col * 1e-3;
+      sol = col[qq] * 1e-3;
+    } else if constexpr (COF) {
+      // C[q][c&3] = ±det(minor), det(H_reg) by row q's expansion (lane (q, j) holds
+      // C[q][j]), (H_reg)⁻¹[q][j] = C[q][j] / det (symmetric), then the row times
+      // [G | g][:, c] with the inverse row broadcast from lanes (q, 0..3)
+      double t0 = mn[4] * mn[8];
+      t0 = fma(-mn[5], mn[7], t0);
+      double t1 = mn[3] * mn[8];
+      t1 = fma(-mn[5], mn[6], t1);
+      double t2 = mn[3] * mn[7];
+      t2 = fma(-mn[4], mn[6], t2);
+      double cf = mn[0] * t0;
+      cf = fma(-mn[1], t1, cf);
+      cf = fma(mn[2], t2, cf);
+      cf *= csign;
+      const double det = dpp_dot4(cf, hr[0], hr[1], hr[2], hr[3]);
+      const double hinv = cf * rcp<(ABL & 32) ? 2 : 1>(det);
+      sol = dpp_dot4(hinv, col[0], col[1], col[2], col[3]);
+      if constexpr ((ABL & 8192) == 0) {
+        // one step of iterative refinement: cofactors of a near-rank-1 H lose ~2
+        // digits (3e-12 per step against 5e-14 for LDLᵀ on the quadrotor H, which
+        // the recursion amplifies); r = [G|g] − H_reg·sol, sol += (H_reg)⁻¹ r. The
+        // columns of sol and r cross rows, so they go through LDS (column-major,
+        // the symmetrisation tile, free at this point of the step)
+        double* xc = lds + 96;
+        xc[c * 4 + q] = sol;
+        wave_lds_fence();
+        const double2 s01 = reinterpret_cast<const double2*>(xc + c * 4)[0];
+        const double2 s23 = reinterpret_cast<const double2*>(xc + c * 4)[1];
+        double r = colq;
+        r = fma(-hr[0], s01.x, r);
+        r = fma(-hr[1], s01.y, r);
+        r = fma(-hr[2], s23.x, r);
+        r = fma(-hr[3], s23.y, r);
+        xc[64 + c * 4 + q] = r;
+        wave_lds_fence();
+        const double2 r01 = reinterpret_cast<const double2*>(xc + 64 + c * 4)[0];
+        const double2 r23 = reinterpret_cast<const double2*>(xc + 64 + c * 4)[1];
+        sol += dpp_dot4(hinv, r01.x, r01.y, r23.x, r23.y);
+        wave_lds_fence();
+      }
     } else if constexpr ((ABL & 128) != 0 && NU == 4) {
       Schur4 f;
       f.factor<(ABL & 32) ? 2 : 1>(h, mu);
-      xs = f.solve(col);
+      sol = f.solve(col)[qq];
     } else {
       LDLT<NU, (ABL & 32) ? 2 : 1> f;
       f.factor(h, mu);
-      xs = f.solve(col);
+      sol = f.solve(col)[qq];
     }
-    const double kq = (q < NU) ? -xs[qq] : 0.0;              // K_aug[q][c]
+    const double kq = (q < NU) ? -sol : 0.0;              // K_aug[q][c]
     const double wk = (q < NU) ? fma(mu, kq, -colq) : 0.0;   // ((H + 2μI) K_aug)[q][c]
     nan |= __builtin_isnan(kq);
 

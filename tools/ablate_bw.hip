@@ -17,8 +17,8 @@ __global__ __launch_bounds__(256, 4) void abl_kernel(LQParams P, int B, int T, c
   // phase-offset experiment (harness only): stagger the 4 waves of a SIMD
   // (WGs sharing a SIMD are ~256 block indices apart: one wave per SIMD per WG)
   const int gen = (blockIdx.x >> 8) & 3;
-  if constexpr ((ABL & 4096) != 0) { for (int i = 0; i < gen; ++i) __builtin_amdgcn_s_sleep(8); }
-  bool nan = lq_backward_wave<12, 4, (ABL & 4095)>(P, b, T, x, u, d, K, 0.01, lds + w * BW_LDS);
+  if constexpr ((ABL & (1 << 14)) != 0) { for (int i = 0; i < gen; ++i) __builtin_amdgcn_s_sleep(8); }
+  bool nan = lq_backward_wave<12, 4, (ABL & ((1 << 14) - 1))>(P, b, T, x, u, d, K, 0.01, lds + w * BW_LDS);
   if (nan && (threadIdx.x & 63) == 0) atomicAdd(flag, 1);
 }
 #define CK(x) do { hipError_t e=(x); if(e!=hipSuccess){printf("err %s line %d\n",hipGetErrorString(e),__LINE__); return 1;} } while(0)
@@ -26,7 +26,7 @@ template <int ABL>
 int run(const char* name, LQParams P, int B, int T, double* x, double* u, double* d, double* K, int* flag) {
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   int grid = (B + 3) / 4;
-  for (int i = 0; i < 3; ++i) abl_kernel<ABL><<<grid, 256>>>(P, B, T, x, u, d, K, flag);
+  for (int i = 0; i < 150; ++i) abl_kernel<ABL><<<grid, 256>>>(P, B, T, x, u, d, K, flag);  // clock run-in
   CK(hipDeviceSynchronize());
   const int R = 20;
   CK(hipEventRecord(e0));
@@ -58,6 +58,15 @@ int main() {
   };
   run<0>("product", P, B, T, xd, ud, d, K, flag);
   CK(hipMemcpy(Kref.data(), K, Kref.size() * 8, hipMemcpyDeviceToHost));
+  run<2048>("cofactor solve + refinement", P, B, T, xd, ud, d, K, flag); diff("cofactor + refinement");
+  run<2048 + 8192>("cofactor solve, no refinement", P, B, T, xd, ud, d, K, flag); diff("cofactor, no refinement");
+  run<128>("Schur4 solve", P, B, T, xd, ud, d, K, flag); diff("Schur4 solve");
+  for (int rep = 0; rep < 2; ++rep) {
+    printf("-- cofactor, round %d\n", rep);
+    run<0>("product (LDLT solve)", P, B, T, xd, ud, d, K, flag);
+    run<2048>("cofactor solve + refinement", P, B, T, xd, ud, d, K, flag);
+    run<2048 + 8192>("cofactor solve, no refinement", P, B, T, xd, ud, d, K, flag);
+  }
   run<1024>("VALU Y/Z (dpp)", P, B, T, xd, ud, d, K, flag); diff("VALU Y/Z (dpp)");
   for (int rep = 0; rep < 2; ++rep) {
     printf("-- VALU products, round %d\n", rep);
