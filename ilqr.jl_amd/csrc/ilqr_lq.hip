@@ -162,7 +162,7 @@ namespace {
 
 // Σ_j<4 bcast_j(src)·c[j]: src broadcast from lane j of each 16-lane row, two
 // accumulators. `s_nop 4` covers the VALU→DPP read hazard.
-__device__ __forceinline__ double dpp_dot4(double src, double c0, double c1, double c2, double c3) {
+[[maybe_unused]] __device__ __forceinline__ double dpp_dot4(double src, double c0, double c1, double c2, double c3) {
   double a0 = 0.0, a1 = 0.0;
   asm("s_nop 4\n\t"
       "v_fmac_f64_dpp %[a0], %[s], %[c0] row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"

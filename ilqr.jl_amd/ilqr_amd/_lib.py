@@ -85,6 +85,11 @@ SIGNATURES = {
     "ilqr_set_stream": (C.c_int, [P, P]),
     "ilqr_sync": (C.c_int, [P]),
     "ilqr_set_schedule": (C.c_int, [P, C.c_int]),
+    "ilqr_multi_create": (C.c_int, [P, P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int]),
+    "ilqr_multi_destroy": (C.c_int, [P]),
+    "ilqr_multi_set_schedule": (C.c_int, [P, C.c_int]),
+    "ilqr_multi_devices": (C.c_int, [P]),
+    "ilqr_multi_fit": (C.c_int, [P, C.POINTER(Problem), C.POINTER(Options), P, P, P, P, P, P, P, P]),
     "ilqr_backward": (C.c_int, [P, C.POINTER(Problem), C.POINTER(Options), P, P, P, P, P]),
     "ilqr_backward_tiles": (C.c_int, [P, C.POINTER(Tiles), C.POINTER(Options), P, P, P]),
     "ilqr_forward": (C.c_int, [P, C.POINTER(Problem), C.POINTER(Options), P, P, P, P, P, P,

@@ -1,0 +1,70 @@
+"""Single-process multi-GPU fit (ilqr_multi_* in include/ilqr.h):
+the batch is sharded in contiguous blocks over the given devices, each shard runs
+ilqr_fit concurrently on its own device (one host thread per device inside the
+library). Host numpy in, host numpy out — what a single-process host (the Julia
+shim's fit_multi) hands over. The one-process-per-GPU path with torch.distributed
+is ilqr_amd.dist."""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+from .problems import LQBatch
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+def _host(a, dtype=np.float64):
+    return np.require(a, dtype, ("C", "W"))
+
+
+class MultiSolver:
+    def __init__(self, devices, nx: int, nu: int, T: int, batch: int):
+        self.lib = _lib.load()
+        self.nx, self.nu, self.T, self.batch = nx, nu, T, batch
+        devs = (C.c_int * len(devices))(*devices)
+        h = C.c_void_p()
+        _lib.check(self.lib.ilqr_multi_create(C.byref(h), devs, len(devices), nx, nu, T, batch),
+                   "ilqr_multi_create")
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.ilqr_multi_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_schedule(self, pipelined: bool = False, ring_forward: bool = True):
+        flags = (_lib.SCHED_PIPELINED if pipelined else 0) | (_lib.SCHED_RING_FORWARD if ring_forward else 0)
+        _lib.check(self.lib.ilqr_multi_set_schedule(self.h, flags), "ilqr_multi_set_schedule")
+
+    def fit(self, lq: LQBatch, x_init, u_init, x_traj=None, max_iter=100, tol=1e-6, mu=None,
+            max_trials=None):
+        """→ (x, u, cost, iters, status, call_status), numpy, whole batch."""
+        if not isinstance(max_iter, int):
+            raise TypeError("max_iter::Int64")  # forward_pass.jl:152
+        B, T, nx, nu = self.batch, self.T, self.nx, self.nu
+        x_init, u_init = _host(x_init), _host(u_init)
+        if x_init.shape != (B, T + 1, nx) or u_init.shape != (B, T, nu):
+            raise AssertionError("size(x_init)[2] == size(u_init)[1] + 1")  # forward_pass.jl:156
+        arrs = {k: _host(getattr(lq, k)) for k in ("A", "B", "Q", "R", "Qf")}
+        prob = _lib.Problem(_lib.PROBLEM_LQ, 0, *(arrs[k].ctypes.data for k in ("A", "B", "Q", "R", "Qf")))
+        xt = None if x_traj is None else _host(x_traj)
+        xo, uo = np.empty_like(x_init), np.empty_like(u_init)
+        cost = np.empty(B)
+        iters = np.empty(B, dtype=np.int32)
+        st = np.empty(B, dtype=np.int32)
+        o = _lib.default_options(max_iter=max_iter, tol=float(tol), mu=mu, max_trials=max_trials)
+        rc = self.lib.ilqr_multi_fit(self.h, C.byref(prob), C.byref(o), _ptr(x_init), _ptr(u_init),
+                                     _ptr(xt), _ptr(xo), _ptr(uo), _ptr(cost), _ptr(iters), _ptr(st))
+        _lib.check(rc, "ilqr_multi_fit", allow=(_lib.ERR_NAN, _lib.ERR_LS_EXHAUSTED))
+        return xo, uo, cost, iters, st, rc

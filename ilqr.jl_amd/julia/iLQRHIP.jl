@@ -184,6 +184,34 @@ function solve!(prob::iLQRProblem; max_iter::Int64=100, tol::Float64=1e-6)
     return prob
 end
 
+"""solve!(prob, devices; …): the same over several GPUs of this node in one process
+(ilqr_multi_fit: contiguous blocks of instances per device, host arrays in and out)."""
+function solve!(prob::iLQRProblem, devices::Vector{Int}; max_iter::Int64=100, tol::Float64=1e-6)
+    nx, N, nb = size(prob.x); nu = size(prob.u, 1); M = N - 1
+    r = Ref{Ptr{Cvoid}}(C_NULL)
+    check(ccall((:ilqr_multi_create, libilqr), Cint,
+                (Ref{Ptr{Cvoid}}, Ptr{Cint}, Cint, Cint, Cint, Cint, Cint),
+                r, Cint.(devices), length(devices), nx, nu, M, nb), "ilqr_multi_create")
+    tr(a) = Array{Float64}(permutedims(a, (2, 1, 3)))
+    A, B, Q, R, Qf = tr(prob.A), tr(prob.B), tr(prob.Q), tr(prob.R), tr(prob.Qf)
+    try
+        GC.@preserve A B Q R Qf begin
+            p = Ref(Problem(ILQR_PROBLEM_LQ, 0, pointer(A), pointer(B), pointer(Q), pointer(R), pointer(Qf)))
+            o = default_options(); o.max_iter = max_iter; o.tol = tol
+            xo = similar(prob.x); uo = similar(prob.u)
+            st = ccall((:ilqr_multi_fit, libilqr), Cint,
+                       (Ptr{Cvoid}, Ref{Problem}, Ref{Options}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64},
+                        Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Int32}, Ptr{Int32}),
+                       r[], p, o, prob.x, prob.u, C_NULL, xo, uo, C_NULL, C_NULL, C_NULL)
+            st in (ILQR_OK, ILQR_ERR_LS_EXHAUSTED) || check(st, "ilqr_multi_fit")
+            prob.x .= xo; prob.u .= uo
+        end
+    finally
+        ccall((:ilqr_multi_destroy, libilqr), Cint, (Ptr{Cvoid},), r[])
+    end
+    return prob
+end
+
 # -- RBD family (ILQR_PROBLEM_CHAIN): test/RBD_2_link_example with a fixed base --------
 const ILQR_F64 = Int32(0)
 const ILQR_F32 = Int32(1)

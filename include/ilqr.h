@@ -271,6 +271,25 @@ ilqr_status ilqr_chain_fit(ilqr_chain_handle* h, const ilqr_options* o, const vo
                            const void* u_init, const void* x_traj, void* x_out, void* u_out,
                            void* cost, int32_t* iters, int32_t* status);
 
+/* Multi-GPU fit in one process (what a single-process Julia host
+ * uses): the batch is split into contiguous blocks over `devices` (block i holds
+ * trajectories [i·batch/n, (i+1)·batch/n)); each device owns a handle and its
+ * shard's buffers (allocated at create) and the shards run concurrently, one host
+ * thread per device. ilqr_multi_fit takes HOST pointers with the whole batch in
+ * the layout above (problem arrays included) and writes the host outputs; the
+ * returned status is the most severe shard status (hard errors, then NAN, then
+ * LS_EXHAUSTED). Trajectories are independent: no device-to-device traffic. */
+typedef struct ilqr_multi ilqr_multi;
+ilqr_status ilqr_multi_create(ilqr_multi** out, const int* devices, int n_devices, int nx, int nu,
+                              int T, int batch);
+ilqr_status ilqr_multi_destroy(ilqr_multi* m);
+ilqr_status ilqr_multi_set_schedule(ilqr_multi* m, int flags);
+int ilqr_multi_devices(const ilqr_multi* m);
+ilqr_status ilqr_multi_fit(ilqr_multi* m, const ilqr_problem* host_problem, const ilqr_options* o,
+                           const double* x_init, const double* u_init, const double* x_traj,
+                           double* x_out, double* u_out, double* cost, int32_t* iters,
+                           int32_t* status);
+
 /* Device memory helpers so a host-language shim (Julia ccall) needs no GPU package. */
 ilqr_status ilqr_malloc(ilqr_handle* h, size_t bytes, void** ptr);
 ilqr_status ilqr_free(ilqr_handle* h, void* ptr);

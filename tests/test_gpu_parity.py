@@ -392,3 +392,35 @@ def test_lq_unsupported_shapes_raise(gpu):
         assert lib.ilqr_supported(_lib.PROBLEM_LQ, nx, nu) == 0
         with pytest.raises(NotImplementedError):
             Solver(nx, nu, 10, 4)
+
+
+# -- single-process multi-GPU fit (ilqr_multi_*) --------------------------------------
+@pytest.mark.parametrize("devices", [[0], [0, 0], [0, 0, 0]])
+def test_multi_fit_equals_single_handle(gpu, devices):
+    """Shards (here several on one GPU: each shard has its own handle and stream,
+    one host thread each) return exactly the single-handle fit, ragged splits too."""
+    from ilqr_amd.multi import MultiSolver
+    nb, T = 37, 20
+    lq, x, u = random_lq_batch(nb, 12, 4, T, seed=5)
+    x[7, 3, 1] = np.nan  # one NaN trajectory: reported, the others unaffected
+    ms = MultiSolver(devices, 12, 4, T, nb)
+    xo, uo, co, it, st, rc = ms.fit(lq, x, u, max_iter=12, tol=1e-8)
+    s = Solver(12, 4, T, nb)
+    s.set_problem(lq)
+    r = s.fit(dev(x), dev(u), max_iter=12, tol=1e-8)
+    assert rc == r.call_status == _lib.ERR_NAN
+    np.testing.assert_array_equal(xo, r.x.cpu().numpy())
+    np.testing.assert_array_equal(uo, r.u.cpu().numpy())
+    np.testing.assert_array_equal(co, r.cost.cpu().numpy())
+    np.testing.assert_array_equal(it, r.iters.cpu().numpy())
+    np.testing.assert_array_equal(st, r.status.cpu().numpy())
+    ms.close()
+
+
+def test_multi_fit_padded_shape(gpu):
+    from ilqr_amd.multi import MultiSolver
+    nb, T = 10, 15
+    lq, x, u = random_lq_batch(nb, 6, 2, T, seed=6)
+    xo, uo, co, it, st, rc = MultiSolver([0, 0], 6, 2, T, nb).fit(lq, x, u, max_iter=10, tol=1e-8)
+    xf, uf, cf, itf, stf = cref.lq_fit(lq, x, u, max_iter=10, tol=1e-8, symmetrize=True)
+    assert np.array_equal(it, itf) and rel(uo, uf) < 1e-8 and rel(xo, xf) < 1e-8
