@@ -224,9 +224,12 @@ __device__ bool lq_backward_wave(const LQParams& P, int b, int T, const double* 
   // VYZ (ABL bit 1024): the Y and Z products on the VALU (dpp_sf4 / dpp_fy4); this
   // lane keeps its whole column of F, Fo[k] = F[k][c]
   constexpr bool VYZ = (ABL & 1024) != 0;
-  static_assert(!VYZ || NX == 12, "dpp_sf4/dpp_fy4 are written for nx = 12");
-  double Fo[VYZ ? NX : 1];
-  if constexpr (VYZ) {
+  // VY (ABL bit 4096): only Y = Sp·F on the VALU (row-local: lane (q, k) holds
+  // Sp[q+4r][k]), Z = L + FᵀY stays on the MFMA, reading Y as its B operand
+  constexpr bool VY = (ABL & 4096) != 0 && !VYZ;
+  static_assert(!(VYZ || VY) || NX == 12, "dpp_sf4/dpp_fy4 are written for nx = 12");
+  double Fo[(VYZ || VY) ? NX : 1];
+  if constexpr (VYZ || VY) {
 #pragma unroll
     for (int k = 0; k < NX; ++k) {
       const double a = ldz(cx, Ab + k * NX + ci, Ab);
@@ -367,6 +370,13 @@ __device__ bool lq_backward_wave(const LQParams& P, int b, int T, const double* 
       double z0 = Lc[0], z1 = Lc[1], z2 = Lc[2], z3 = Lc[3];
       dpp_fy4(z0, z1, z2, z3, Yp, Fo);
       Z = d4{z0, z1, z2, z3};
+    } else if constexpr (VY) {
+      double y0 = 0.0, y1 = 0.0, y2 = 0.0, y3 = 0.0;
+      dpp_sf4(y0, y1, y2, y3, Sp[0], Sp[1], Sp[2], Sp[3], Fo);
+      asm volatile("s_nop 4" ::: );  // VALU write → MFMA operand read
+      Y = d4{y0, y1, y2, y3};
+#pragma unroll
+      for (int kk = 0; kk < KS; ++kk) Z = mfma(fB[kk], Y[kk], Z);
     } else {
 #pragma unroll
       for (int kk = 0; kk < KS; ++kk) Y = mfma(Sp[kk], fB[kk], Y);

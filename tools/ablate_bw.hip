@@ -58,6 +58,11 @@ int main() {
   };
   run<0>("product", P, B, T, xd, ud, d, K, flag);
   CK(hipMemcpy(Kref.data(), K, Kref.size() * 8, hipMemcpyDeviceToHost));
+  run<4096>("Y on VALU (dpp), Z on MFMA", P, B, T, xd, ud, d, K, flag); diff("Y on VALU, Z on MFMA");
+  for (int rep = 0; rep < 2; ++rep) {
+    run<0>("product", P, B, T, xd, ud, d, K, flag);
+    run<4096>("Y on VALU (dpp), Z on MFMA", P, B, T, xd, ud, d, K, flag);
+  }
   run<2048>("cofactor solve + refinement", P, B, T, xd, ud, d, K, flag); diff("cofactor + refinement");
   run<2048 + 8192>("cofactor solve, no refinement", P, B, T, xd, ud, d, K, flag); diff("cofactor, no refinement");
   run<128>("Schur4 solve", P, B, T, xd, ud, d, K, flag); diff("Schur4 solve");
