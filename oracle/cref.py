@@ -179,3 +179,45 @@ def tiles_backward(tiles, mu=0.01, symmetrize=False, nthreads=0):
                                    int(symmetrize), _p(d), _p(K), _p(st), nthreads)
     assert rc >= 0
     return d, K, st
+
+
+# -- RBD chain (ILQR_PROBLEM_CHAIN, BASELINE config 5) ------------------------------
+def _chain_args(pr):
+    """ChainProblem (ilqr_amd.chain) → the C restatement's chain arguments."""
+    ch = pr.chain
+    arrs = [_f64(ch.R0), _f64(ch.p), _f64(ch.axis), _f64(ch.mass), _f64(ch.com), _f64(ch.Ic),
+            _f64(ch.gravity)]
+    tail = [_f64(pr.target), _f64(pr.q_weight), _f64(pr.r_weight), _f64(pr.qf_weight)]
+    args = [ch.n, pr.nu] + [_p(a) for a in arrs] + [C.c_double(pr.dt)] + [_p(a) for a in tail]
+    return args, arrs + tail  # keep the arrays alive for the call
+
+
+def chain_dynamics(pr, x, u):
+    """One RK4 step of the chain for n points: x (n, 2nj), u (n, nu) → (n, 2nj)."""
+    lib = load()
+    x, u = _f64(x), _f64(u)
+    out = np.empty_like(x)
+    args, keep = _chain_args(pr)
+    rc = lib.oracle_chain_dynamics(x.shape[0], *args, _p(x), _p(u), _p(out))
+    assert rc == 0, "oracle_chain_dynamics: bad chain"
+    return out
+
+
+def chain_iterate(pr, x, u, mu=0.01, symmetrize=True, max_trials=64, nthreads=0):
+    """One cold-start iteration per trajectory (central-difference linearisation,
+    backward_pass, forward_pass) → (d, K, x_new, u_new, cost, trials)."""
+    lib = load()
+    x, u = _f64(x), _f64(u)
+    nb, T, m = u.shape
+    n = x.shape[2]
+    d = np.empty((nb, T, m))
+    K = np.empty((nb, T, m, n))
+    xn, un = np.empty_like(x), np.empty_like(u)
+    cost = np.empty(nb)
+    trials = np.empty(nb, dtype=np.int32)
+    args, keep = _chain_args(pr)
+    rc = lib.oracle_chain_iterate(nb, T, *args, _p(x), _p(u), C.c_double(mu), int(symmetrize),
+                                  max_trials, _p(d), _p(K), _p(xn), _p(un), _p(cost), _p(trials),
+                                  nthreads)
+    assert rc >= 0, "oracle_chain_iterate: bad chain"
+    return d, K, xn, un, cost, trials

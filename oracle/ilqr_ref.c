@@ -115,6 +115,7 @@ struct prob_s {
   void (*dyn)(const prob_t*, const double* x, const double* u, double* xn);
   double (*cost)(const prob_t*, const double* x, const double* u);
   double (*fcost)(const prob_t*, const double* x);
+  const void* ext; /* CHAIN family: the chain's constants (chain_t) */
 };
 
 /* -- LQ family: f = Ax + Bu, ℓ = xᵀQx + uᵀRu, ℓ_f = xᵀQf x (exact derivatives) -- */
@@ -451,6 +452,264 @@ static int forward_one(const prob_t* P, const double* x, const double* u, const 
   return -max_trials;
 }
 
+/* -- RBD fixed-base serial chain (test/RBD_2_link_example, BASELINE config 5) ---------
+ * Restates oracle/rbd.py's ChainModel / ChainCost (the numpy oracle of the device's
+ * ILQR_PROBLEM_CHAIN): recursive Newton-Euler for the bias, M's columns by unit
+ * accelerations without gravity, Gaussian elimination, RK4 with dt; linearised by
+ * central differences h = ε^⅓·max(1, |z_k|) divided by the step actually taken (the
+ * device's ILQR_LINEARIZE_CENTRAL_FD); cost Σ qwᵢ(θ*ᵢ−θᵢ)² + Σ rwₖuₖ², final
+ * Σ qfwᵢ(θ*ᵢ−θᵢ)² (RBD_helper_functions.jl:48-116). */
+#define NJMAX 8
+typedef struct {
+  int nj, nu;
+  double R0[NJMAX][9], p[NJMAX][3], ax[NJMAX][3], m[NJMAX], mc[NJMAX][3], Io[NJMAX][9], g[3], dt;
+  double tgt[NJMAX], qw[NJMAX], rw[NJMAX], qfw[NJMAX];
+} chain_t;
+
+static void ch_rod(const double* a, double c, double s, const double* w, double* o) {
+  const double axw[3] = {a[1] * w[2] - a[2] * w[1], a[2] * w[0] - a[0] * w[2], a[0] * w[1] - a[1] * w[0]};
+  const double k = (1.0 - c) * (a[0] * w[0] + a[1] * w[1] + a[2] * w[2]);
+  for (int r = 0; r < 3; ++r) o[r] = c * w[r] + s * axw[r] + k * a[r];
+}
+static void ch_cross(const double* a, const double* b, double* o) {
+  o[0] = a[1] * b[2] - a[2] * b[1];
+  o[1] = a[2] * b[0] - a[0] * b[2];
+  o[2] = a[0] * b[1] - a[1] * b[0];
+}
+static void ch_to_child(const chain_t* C, int i, double c, double s, const double* w, double* o) {
+  double y[3];
+  for (int r = 0; r < 3; ++r) y[r] = C->R0[i][r] * w[0] + C->R0[i][3 + r] * w[1] + C->R0[i][6 + r] * w[2];
+  ch_rod(C->ax[i], c, -s, y, o);
+}
+static void ch_to_parent(const chain_t* C, int i, double c, double s, const double* w, double* o) {
+  double y[3];
+  ch_rod(C->ax[i], c, s, w, y);
+  for (int r = 0; r < 3; ++r) o[r] = C->R0[i][3 * r] * y[0] + C->R0[i][3 * r + 1] * y[1] + C->R0[i][3 * r + 2] * y[2];
+}
+/* τ = M(q)q̈ + [qd] C(q,q̇)q̇ + [grav] g(q); qd may be NULL (zero velocity) */
+static void ch_rnea(const chain_t* C, const double* cq, const double* sq, const double* qd,
+                    const double* qdd, int grav, double* tau) {
+  const int n = C->nj;
+  double w[3] = {0, 0, 0}, v[3] = {0, 0, 0}, al[3] = {0, 0, 0}, ac[3];
+  for (int r = 0; r < 3; ++r) ac[r] = grav ? -C->g[r] : 0.0;
+  double fn[NJMAX][3], ff[NJMAX][3];
+  for (int i = 0; i < n; ++i) {
+    double t[3], u3[3], wi[3], vi[3], ali[3], aci[3];
+    ch_to_child(C, i, cq[i], sq[i], w, wi);
+    ch_cross(C->p[i], w, t);
+    for (int r = 0; r < 3; ++r) u3[r] = v[r] - t[r];
+    ch_to_child(C, i, cq[i], sq[i], u3, vi);
+    ch_to_child(C, i, cq[i], sq[i], al, ali);
+    ch_cross(C->p[i], al, t);
+    for (int r = 0; r < 3; ++r) u3[r] = ac[r] - t[r];
+    ch_to_child(C, i, cq[i], sq[i], u3, aci);
+    if (qd) {
+      double sqd[3];
+      for (int r = 0; r < 3; ++r) sqd[r] = C->ax[i][r] * qd[i];
+      for (int r = 0; r < 3; ++r) wi[r] += sqd[r];
+      ch_cross(wi, sqd, t);
+      for (int r = 0; r < 3; ++r) ali[r] += t[r];
+      ch_cross(vi, sqd, t);
+      for (int r = 0; r < 3; ++r) aci[r] += t[r];
+    }
+    for (int r = 0; r < 3; ++r) ali[r] += C->ax[i][r] * qdd[i];
+    for (int r = 0; r < 3; ++r)
+      fn[i][r] = C->Io[i][3 * r] * ali[0] + C->Io[i][3 * r + 1] * ali[1] + C->Io[i][3 * r + 2] * ali[2];
+    ch_cross(C->mc[i], aci, t);
+    for (int r = 0; r < 3; ++r) fn[i][r] += t[r];
+    ch_cross(C->mc[i], ali, t);
+    for (int r = 0; r < 3; ++r) ff[i][r] = C->m[i] * aci[r] - t[r];
+    if (qd) {
+      double hn[3], hf[3];
+      for (int r = 0; r < 3; ++r)
+        hn[r] = C->Io[i][3 * r] * wi[0] + C->Io[i][3 * r + 1] * wi[1] + C->Io[i][3 * r + 2] * wi[2];
+      ch_cross(C->mc[i], vi, t);
+      for (int r = 0; r < 3; ++r) hn[r] += t[r];
+      ch_cross(C->mc[i], wi, t);
+      for (int r = 0; r < 3; ++r) hf[r] = C->m[i] * vi[r] - t[r];
+      ch_cross(wi, hn, t);
+      for (int r = 0; r < 3; ++r) fn[i][r] += t[r];
+      ch_cross(vi, hf, t);
+      for (int r = 0; r < 3; ++r) fn[i][r] += t[r];
+      ch_cross(wi, hf, t);
+      for (int r = 0; r < 3; ++r) ff[i][r] += t[r];
+    }
+    memcpy(w, wi, sizeof w);
+    memcpy(v, vi, sizeof v);
+    memcpy(al, ali, sizeof al);
+    memcpy(ac, aci, sizeof ac);
+  }
+  for (int i = n - 1; i >= 0; --i) {
+    tau[i] = C->ax[i][0] * fn[i][0] + C->ax[i][1] * fn[i][1] + C->ax[i][2] * fn[i][2];
+    if (i > 0) {
+      double pf[3], pn[3], t[3];
+      ch_to_parent(C, i, cq[i], sq[i], ff[i], pf);
+      ch_to_parent(C, i, cq[i], sq[i], fn[i], pn);
+      ch_cross(C->p[i], pf, t);
+      for (int r = 0; r < 3; ++r) {
+        fn[i - 1][r] += pn[r] + t[r];
+        ff[i - 1][r] += pf[r];
+      }
+    }
+  }
+}
+/* [q̇; v̇], v̇ = M \ (τ − bias) (RBD_helper_functions.jl:61-66) */
+static void ch_xdot(const chain_t* C, const double* x, const double* u, double* xd) {
+  const int n = C->nj;
+  double cq[NJMAX], sq[NJMAX], zero[NJMAX], b[NJMAX], M[NJMAX][NJMAX], r[NJMAX], qdd[NJMAX];
+  for (int i = 0; i < n; ++i) {
+    cq[i] = cos(x[i]);
+    sq[i] = sin(x[i]);
+    zero[i] = 0.0;
+  }
+  ch_rnea(C, cq, sq, x + n, zero, 1, b);
+  for (int k = 0; k < n; ++k) {
+    double e[NJMAX], col[NJMAX];
+    for (int j = 0; j < n; ++j) e[j] = j == k ? 1.0 : 0.0;
+    ch_rnea(C, cq, sq, NULL, e, 0, col);
+    for (int i = 0; i < n; ++i) M[i][k] = col[i];
+  }
+  for (int i = 0; i < n; ++i) r[i] = (i < C->nu ? u[i] : 0.0) - b[i];
+  for (int k = 0; k < n; ++k) { /* Gaussian elimination, no pivoting (M SPD) */
+    const double inv = 1.0 / M[k][k];
+    for (int i = k + 1; i < n; ++i) {
+      const double l = M[i][k] * inv;
+      for (int j = k + 1; j < n; ++j) M[i][j] -= l * M[k][j];
+      r[i] -= l * r[k];
+    }
+  }
+  for (int i = n - 1; i >= 0; --i) {
+    double acc = r[i];
+    for (int j = i + 1; j < n; ++j) acc -= M[i][j] * qdd[j];
+    qdd[i] = acc / M[i][i];
+  }
+  for (int i = 0; i < n; ++i) {
+    xd[i] = x[n + i];
+    xd[n + i] = qdd[i];
+  }
+}
+static void ch_rk4(const chain_t* C, const double* x, const double* u, double* xn) {
+  const int nx = 2 * C->nj;
+  double k1[2 * NJMAX], k2[2 * NJMAX], k3[2 * NJMAX], k4[2 * NJMAX], y[2 * NJMAX] = {0};
+  ch_xdot(C, x, u, k1);
+  for (int i = 0; i < nx; ++i) { k1[i] *= C->dt; y[i] = x[i] + 0.5 * k1[i]; }
+  ch_xdot(C, y, u, k2);
+  for (int i = 0; i < nx; ++i) { k2[i] *= C->dt; y[i] = x[i] + 0.5 * k2[i]; }
+  ch_xdot(C, y, u, k3);
+  for (int i = 0; i < nx; ++i) { k3[i] *= C->dt; y[i] = x[i] + k3[i]; }
+  ch_xdot(C, y, u, k4);
+  for (int i = 0; i < nx; ++i) {
+    k4[i] *= C->dt;
+    xn[i] = x[i] + (1.0 / 6.0) * (((k1[i] + 2.0 * k2[i]) + 2.0 * k3[i]) + k4[i]);
+  }
+}
+static void ch_dyn(const prob_t* P, const double* x, const double* u, double* xn) {
+  ch_rk4((const chain_t*)P->ext, x, u, xn);
+}
+static void ch_lin(const prob_t* P, int t, const double* x, const double* u, double* A, double* B) {
+  (void)t;
+  const chain_t* C = (const chain_t*)P->ext;
+  const int nx = P->n, nu = P->m, nd = nx + nu;
+  const double cbe = 6.0554544523933395e-6; /* ε^⅓, fp64 */
+  double z[2 * NJMAX + NJMAX], fp[2 * NJMAX], fm[2 * NJMAX];
+  for (int i = 0; i < nx; ++i) z[i] = x[i];
+  for (int i = 0; i < nu; ++i) z[nx + i] = u[i];
+  for (int k = 0; k < nd; ++k) {
+    const double h = cbe * fmax(1.0, fabs(z[k]));
+    double zp[2 * NJMAX + NJMAX], zm[2 * NJMAX + NJMAX];
+    memcpy(zp, z, sizeof(double) * nd);
+    memcpy(zm, z, sizeof(double) * nd);
+    zp[k] = z[k] + h;
+    zm[k] = z[k] - h;
+    ch_rk4(C, zp, zp + nx, fp);
+    ch_rk4(C, zm, zm + nx, fm);
+    const double inv = 1.0 / (zp[k] - zm[k]);
+    for (int i = 0; i < nx; ++i) {
+      const double dv = (fp[i] - fm[i]) * inv;
+      if (k < nx) A[i * nx + k] = dv; else B[i * nu + (k - nx)] = dv;
+    }
+  }
+}
+static void ch_quad(const prob_t* P, int t, const double* x, const double* u, double* qv, double* r,
+                    double* Q, double* Pm, double* R) {
+  (void)t;
+  const chain_t* C = (const chain_t*)P->ext;
+  const int n = C->nj, nx = P->n, nu = P->m;
+  memset(qv, 0, sizeof(double) * nx);
+  memset(Q, 0, sizeof(double) * nx * nx);
+  memset(Pm, 0, sizeof(double) * nu * nx);
+  memset(R, 0, sizeof(double) * nu * nu);
+  for (int i = 0; i < n; ++i) {
+    qv[i] = -2.0 * C->qw[i] * (C->tgt[i] - x[i]);
+    Q[i * nx + i] = 2.0 * C->qw[i];
+  }
+  for (int k = 0; k < nu; ++k) {
+    r[k] = 2.0 * C->rw[k] * u[k];
+    R[k * nu + k] = 2.0 * C->rw[k];
+  }
+}
+static void ch_fquad(const prob_t* P, const double* x, double* s, double* S) {
+  const chain_t* C = (const chain_t*)P->ext;
+  const int n = C->nj, nx = P->n;
+  memset(s, 0, sizeof(double) * nx);
+  memset(S, 0, sizeof(double) * nx * nx);
+  for (int i = 0; i < n; ++i) {
+    s[i] = -2.0 * C->qfw[i] * (C->tgt[i] - x[i]);
+    S[i * nx + i] = 2.0 * C->qfw[i];
+  }
+}
+static double ch_cost(const prob_t* P, const double* x, const double* u) {
+  const chain_t* C = (const chain_t*)P->ext;
+  double acc = 0.0;
+  for (int i = 0; i < C->nj; ++i) {
+    const double e = C->tgt[i] - x[i];
+    acc = acc + C->qw[i] * e * e;
+  }
+  for (int k = 0; k < P->m; ++k) acc = acc + C->rw[k] * u[k] * u[k];
+  return acc;
+}
+static double ch_fcost(const prob_t* P, const double* x) {
+  const chain_t* C = (const chain_t*)P->ext;
+  double acc = 0.0;
+  for (int i = 0; i < C->nj; ++i) {
+    const double e = C->tgt[i] - x[i];
+    acc = acc + C->qfw[i] * e * e;
+  }
+  return acc;
+}
+/* chain constants from the URDF-derived arrays (ilqr_amd.urdf.Chain): rotational
+ * inertia about the body origin Io = Ic + m(|c|²I − ccᵀ), first moment mc = m·c */
+static int ch_init(chain_t* C, int nj, int nu, const double* R0, const double* p, const double* ax,
+                   const double* mass, const double* com, const double* Ic, const double* grav,
+                   double dt, const double* tgt, const double* qw, const double* rw,
+                   const double* qfw) {
+  if (nj < 1 || nj > NJMAX || nu < 1 || nu > nj || 2 * nj > NMAX) return -1;
+  memset(C, 0, sizeof *C);
+  C->nj = nj;
+  C->nu = nu;
+  C->dt = dt;
+  for (int r = 0; r < 3; ++r) C->g[r] = grav[r];
+  for (int i = 0; i < nj; ++i) {
+    const double* c = com + 3 * i;
+    const double cc = c[0] * c[0] + c[1] * c[1] + c[2] * c[2];
+    for (int k = 0; k < 9; ++k) C->R0[i][k] = R0[9 * i + k];
+    for (int r = 0; r < 3; ++r) {
+      C->p[i][r] = p[3 * i + r];
+      C->ax[i][r] = ax[3 * i + r];
+      C->mc[i][r] = mass[i] * c[r];
+    }
+    C->m[i] = mass[i];
+    for (int r = 0; r < 3; ++r)
+      for (int k = 0; k < 3; ++k)
+        C->Io[i][3 * r + k] = Ic[9 * i + 3 * r + k] + mass[i] * ((r == k ? cc : 0.0) - c[r] * c[k]);
+    C->tgt[i] = tgt[i];
+    C->qw[i] = qw[i];
+    C->qfw[i] = qfw[i];
+  }
+  for (int k = 0; k < nu; ++k) C->rw[k] = rw[k];
+  return 0;
+}
+
 static prob_t instance(int b, int n, int m, int T, const double* A, const double* Bm,
                        const double* Q, const double* R, const double* Qf) {
   prob_t P = {n, m, T, A + (size_t)b * n * n, Bm + (size_t)b * n * m, Q + (size_t)b * n * n,
@@ -640,5 +899,44 @@ int oracle_tiles_backward(int Bn, int T, int n, int m, const double* A, const do
     nans += bad;
   }
   free(dummy);
+  return nans;
+}
+
+/* -- chain family exports (config 5 checker and CPU baseline) ------------------------ */
+#define CH_ARGS                                                                                 \
+  int nj, int nu, const double *R0, const double *p, const double *ax, const double *mass,      \
+      const double *com, const double *Ic, const double *grav, double dt, const double *tgt,    \
+      const double *qw, const double *rw, const double *qfw
+#define CH_PASS nj, nu, R0, p, ax, mass, com, Ic, grav, dt, tgt, qw, rw, qfw
+
+/* one RK4 step for n points: x (n, 2nj), u (n, nu) → xn (n, 2nj) */
+int oracle_chain_dynamics(int npts, CH_ARGS, const double* x, const double* u, double* xn) {
+  chain_t C;
+  if (ch_init(&C, CH_PASS) != 0) return -1;
+  for (int i = 0; i < npts; ++i) ch_rk4(&C, x + (size_t)i * 2 * nj, u + (size_t)i * nu, xn + (size_t)i * 2 * nj);
+  return 0;
+}
+
+/* one cold-start fit iteration per trajectory (prev_cost = +Inf): backward_pass on the
+ * central-difference linearisation, then forward_pass with the line search. */
+int oracle_chain_iterate(int Bn, int T, CH_ARGS, const double* x, const double* u, double mu,
+                         int sym, int max_trials, double* d, double* K, double* xn, double* un,
+                         double* cost, int* trials, int nthreads) {
+  chain_t C;
+  if (ch_init(&C, CH_PASS) != 0) return -1;
+  set_threads(nthreads);
+  const int n = 2 * nj, m = nu;
+  const size_t xs = (size_t)(T + 1) * n, us = (size_t)T * m;
+  int nans = 0;
+#pragma omp parallel for schedule(dynamic, 1) reduction(+ : nans)
+  for (int b = 0; b < Bn; ++b) {
+    prob_t P = {n, m, T, NULL, NULL, NULL, NULL, NULL, NULL, ch_lin, ch_quad, ch_fquad,
+                ch_dyn, ch_cost, ch_fcost, &C};
+    const int bad = backward_one(&P, x + b * xs, u + b * us, mu, sym, d + b * us, K + b * us * n);
+    nans += bad;
+    const int tr = forward_one(&P, x + b * xs, u + b * us, NULL, d + b * us, K + b * us * n, INFINITY,
+                               xn + b * xs, un + b * us, &cost[b], max_trials, 1.0, 0.5);
+    if (trials) trials[b] = tr;
+  }
   return nans;
 }

@@ -173,3 +173,50 @@ def test_chain_abi_validates_without_gpu():
     assert lib.ilqr_chain_supported(2, 2) == 1 and lib.ilqr_chain_supported(2, 1) == 1
     assert lib.ilqr_chain_supported(6, 6) == 0
     assert lib.ilqr_supported(_lib.PROBLEM_CHAIN, 4, 2) == 1
+
+
+# -- the C restatement of the chain family (oracle/ilqr_ref.c, CPU baseline of config 5)
+@pytest.mark.parametrize("robot,nu", [("2dof_arm", 2), ("2dof_arm", 1), ("6dof_arm", 6)])
+def test_c_chain_dynamics_matches_numpy_oracle(robot, nu):
+    """Two restatements of the same published algorithms (RNEA bias, unit-acceleration
+    mass-matrix columns, Gaussian elimination, RK4): C vs numpy agree to rounding."""
+    import copy
+    from oracle import cref
+    ch = copy.deepcopy(load_robot(robot))
+    pr = ChainProblem(ch, nu, 0.01, np.full(ch.n, 0.3), np.full(ch.n, 2.0), np.full(ch.n, 0.5),
+                      np.full(ch.n, 7.0))
+    if robot == "6dof_arm":  # exercise gravity too (the reference parses the URDF without it)
+        ch.gravity = np.array([0.0, 0.0, -9.81])
+    rng = np.random.default_rng(3)
+    X = rng.uniform(-1.5, 1.5, (40, 2 * ch.n))
+    U = rng.uniform(-2.0, 2.0, (40, nu))
+    ref = RBD.ChainModel(ch, 0.01).step(X, U)
+    out = cref.chain_dynamics(pr, X, U)
+    assert np.abs(out - ref).max() <= 1e-12 * max(1.0, np.abs(ref).max())
+
+
+def test_c_chain_iteration_matches_numpy_oracle():
+    """One cold-start iteration (C: central differences; numpy: exact Jacobians):
+    gains within the differencing error, rollouts and costs of the same gains exactly."""
+    from oracle import cref
+    from oracle import ilqr_oracle as O
+    pr = rbd_2dof_problem(2)
+    T, nb = 30, 3
+    x0 = rbd_initial_states(nb, 2)
+    model = RBD.ChainModel(pr.chain, pr.dt)
+    cost = RBD.ChainCost(pr.target, pr.q_weight, pr.r_weight, pr.qf_weight)
+    f, l, lf = RBD.chain_closures(model, cost)
+    u = np.zeros((nb, T, 2))
+    x = np.zeros((nb, T + 1, 4))
+    x[:, 0] = x0
+    for t in range(T):
+        x[:, t + 1] = model.step(x[:, t], u[:, t])
+    d, K, xn, un, c, tr = cref.chain_iterate(pr, x, u)
+    assert (tr == 1).all()
+    for b in range(nb):
+        do, Ko = O.backward_pass(x[b], u[b], f, l, lf, symmetrize=True)
+        assert np.abs(K[b] - Ko).max() <= 1e-6 * np.abs(Ko).max()
+        assert np.abs(d[b] - do).max() <= 1e-6 * np.abs(do).max()
+        xo, uo, co = O.forward_pass(x[b], u[b], np.zeros_like(x[b]), d[b], K[b], np.inf, f, l, lf)
+        assert np.abs(xn[b] - xo).max() <= 1e-12 * np.abs(xo).max()
+        assert abs(c[b] - co) <= 1e-12 * abs(co)

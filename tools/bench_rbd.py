@@ -4,8 +4,8 @@ batch 2048 random x₀, fp32, linearised on the device by central finite differe
 (BASELINE's wording) or dual numbers (the reference's ForwardDiff). Same step as
 bench.py: one cold-start fit iteration over the batch (linearise + backward +
 forward with line search), timed with HIP events on torch's current stream.
-Prints one JSON line per linearisation. The CPU baseline is the oracle
-(oracle/rbd.py, numpy, 1 core) on a bounded sample — a port, not the reference.
+Prints one JSON line per linearisation. The CPU baseline is the C restatement
+(oracle/ilqr_ref.c, fp64, OpenMP) on a bounded sample — a port, not the reference.
 """
 from __future__ import annotations
 
@@ -36,22 +36,24 @@ def timed(fn, n, stream):
 
 
 def cpu_baseline(pr, x, u, budget_s):
-    """oracle/rbd.py + oracle/ilqr_oracle.py: one cold-start iteration per trajectory."""
-    from oracle import ilqr_oracle as O
-    from oracle import rbd as RBD
-    model = RBD.ChainModel(pr.chain, pr.dt)
-    cost = RBD.ChainCost(pr.target, pr.q_weight, pr.r_weight, pr.qf_weight)
-    f, l, lf = RBD.chain_closures(model, cost)
-    n, t0 = 0, time.perf_counter()
-    while time.perf_counter() - t0 < budget_s and n < x.shape[0]:
-        d, K = O.backward_pass(x[n], u[n], f, l, lf)
-        O.forward_pass(x[n], u[n], np.zeros_like(x[n]), d, K, np.inf, f, l, lf, max_trials=60)
-        n += 1
-    el = time.perf_counter() - t0
-    return {"value": n / el / x.shape[0], "unit": f"batched iterations/s (batch={x.shape[0]})",
-            "cores": 1, "kind": "port",
-            "sample": f"{n} trajectories x 1 cold-start iteration (numpy oracle oracle/rbd.py, fp64, "
-                      f"1 core), {el:.1f} s"}
+    """The C restatement of the chain family (oracle/ilqr_ref.c: oracle_chain_iterate,
+    fp64, central differences, OpenMP over trajectories) on a bounded sample: one
+    cold-start iteration per trajectory."""
+    from oracle import cref
+    threads = min(16, os.cpu_count() or 1)
+    n = 16
+    while True:
+        idx = np.arange(n) % x.shape[0]
+        t0 = time.perf_counter()
+        cref.chain_iterate(pr, x[idx], u[idx], nthreads=threads)
+        el = time.perf_counter() - t0
+        if el > budget_s / 2 or n >= 1 << 15:
+            break
+        n *= 2
+    return {"value": n / el, "unit": "trajectory-iterations/s", "cores": threads, "kind": "port",
+            "sample": f"{n} trajectories x 1 cold-start iteration (C restatement oracle/ilqr_ref.c "
+                      f"oracle_chain_iterate, fp64, central differences, OpenMP {threads} threads, -O3), "
+                      f"{el:.2f} s"}
 
 
 def main():
@@ -106,11 +108,11 @@ def main():
                "cpu_baseline": None}
         if not args.no_cpu:
             if base is None:
-                xs = x[: min(B, 64)].double().cpu().numpy()
-                us = u[: min(B, 64)].double().cpu().numpy()
+                xs = x[: min(B, 256)].double().cpu().numpy()
+                us = u[: min(B, 256)].double().cpu().numpy()
                 base = cpu_baseline(pr, xs, us, args.cpu_budget)
+                base["value"] = base["value"] / B  # trajectory-iterations/s → batched it/s
                 base["unit"] = f"batched iterations/s (batch={B})"
-                base["value"] = base["value"] * min(B, 64) / B
             res["cpu_baseline"] = base
         print(json.dumps(res), flush=True)
         s.close()
