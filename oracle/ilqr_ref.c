@@ -1,6 +1,6 @@
 /*
  * ilqr_ref.c — C restatement of aabouman/iLQR.jl's hot path (LQ, 2-link arm, caller tiles and RBD chain families)
- * family — TEST INFRASTRUCTURE ONLY (checker for the GPU parity tests and the
+ * — TEST INFRASTRUCTURE ONLY (checker for the GPU parity tests and the
  * bench's cpu_baseline leg; never linked into the product).
  *
  * The reference is pure Julia (not buildable here: no Julia toolchain), so this
