@@ -468,7 +468,7 @@ ilqr_status ilqr_forward(ilqr_handle* h, const ilqr_problem* p, const ilqr_optio
   else
     HIP_TRY(ilqr::launch_lq_forward(h->nx, h->nu, lq_params(p), h->batch, h->T, x, u, x_traj, d,
                                     K, prev_cost, x_new, u_new, new_cost, trials, status,
-                                    ls_params(o), h->stream));
+                                    ls_params(o), h->stream, h->fw_ring));
   return status ? fold_status(h, status) : ILQR_OK;
 }
 

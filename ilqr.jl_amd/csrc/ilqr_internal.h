@@ -51,7 +51,7 @@ hipError_t launch_lq_forward(int nx, int nu, const LQParams& p, int B, int T, co
                              const double* u, const double* xtraj, const double* d,
                              const double* K, const double* prev_cost, double* xnew,
                              double* unew, double* new_cost, int32_t* trials, int32_t* status,
-                             const LSParams& ls, hipStream_t s);
+                             const LSParams& ls, hipStream_t s, bool ring = false);
 // The two halves of one fit iteration over trajectories [b0, b1) (pointers in
 // `a` and `p` address the whole batch).
 hipError_t launch_lq_iter_backward(int nx, int nu, const LQParams& p, int b0, int b1, int T,

@@ -1114,6 +1114,36 @@ __device__ __forceinline__ void iter_forward_wave(const LQParams& P, int b0, int
   }
 }
 
+// forward_pass (the ilqr_forward entry) with the LDS-ring forward: every trajectory
+// runs; an exhausted line search returns the inputs (as lq_forward_kernel).
+template <int NX, int NU>
+__global__ __launch_bounds__(64) void lq_forward_ring_kernel(
+    LQParams P, int B, int T, const double* __restrict__ x, const double* __restrict__ u,
+    const double* __restrict__ xtraj, const double* __restrict__ d, const double* __restrict__ K,
+    const double* __restrict__ prev_cost, double* __restrict__ xnew, double* __restrict__ unew,
+    double* __restrict__ new_cost, int32_t* __restrict__ trials, int32_t* __restrict__ status,
+    LSParams ls) {
+  __shared__ __attribute__((aligned(16))) double ring[PIPE_R * RING_SLOT + RING_LAREA];
+  const int b0 = blockIdx.x * 4;
+  const int j = threadIdx.x & 15;
+  const int b = b0 + (threadIdx.x >> 4);
+  const bool active = b < B;
+  const double pc = (prev_cost && active) ? prev_cost[b] : INFINITY;
+  const FwdOut r = lq_forward_wave_ring<NX, NU, PIPE_R, PIPE_PF>(P, b0, B, T, active, x, u, xtraj, d,
+                                                                 K, pc, xnew, unew, nullptr, ls, ring);
+  if (!active) return;
+  if (!r.accepted) {
+    for (int i = j; i < (T + 1) * NX; i += 16) xnew[(size_t)b * (T + 1) * NX + i] = x[(size_t)b * (T + 1) * NX + i];
+    for (int i = j; i < T * NU; i += 16) unew[(size_t)b * T * NU + i] = u[(size_t)b * T * NU + i];
+  }
+  if (j == 0) {
+    new_cost[b] = r.cost;
+    if (trials) trials[b] = r.trials;
+    if (status) status[b] = r.accepted ? ILQR_TRAJ_OK
+                                       : (r.cost != r.cost ? ILQR_TRAJ_NAN : ILQR_TRAJ_LS_EXHAUSTED);
+  }
+}
+
 // Part 2 with the LDS-ring forward (one wave, four trajectories per workgroup).
 template <int NX, int NU>
 __global__ __launch_bounds__(64) void lq_iter_forward_ring_kernel(LQParams P, int B, int T, IterArgs a,
@@ -1278,8 +1308,11 @@ hipError_t launch_lq_forward(int nx, int nu, const LQParams& p, int B, int T, co
                              const double* u, const double* xtraj, const double* d,
                              const double* K, const double* prev_cost, double* xnew,
                              double* unew, double* new_cost, int32_t* trials, int32_t* status,
-                             const LSParams& ls, hipStream_t s) {
+                             const LSParams& ls, hipStream_t s, bool ring) {
   const int grid = (B + 3) / 4;
+  if (ring) {
+    ILQR_DISPATCH(12, 4, (lq_forward_ring_kernel<NX_, NU_><<<grid, 64, 0, s>>>(p, B, T, x, u, xtraj, d, K, prev_cost, xnew, unew, new_cost, trials, status, ls)));
+  }
   ILQR_DISPATCH(12, 4, (lq_forward_kernel<NX_, NU_><<<grid, 64, 0, s>>>(p, B, T, x, u, xtraj, d, K, prev_cost, xnew, unew, new_cost, trials, status, ls)));
   return hipErrorInvalidValue;
 }

@@ -424,3 +424,24 @@ def test_multi_fit_padded_shape(gpu):
     xo, uo, co, it, st, rc = MultiSolver([0, 0], 6, 2, T, nb).fit(lq, x, u, max_iter=10, tol=1e-8)
     xf, uf, cf, itf, stf = cref.lq_fit(lq, x, u, max_iter=10, tol=1e-8, symmetrize=True)
     assert np.array_equal(it, itf) and rel(uo, uf) < 1e-8 and rel(xo, xf) < 1e-8
+
+
+@pytest.mark.parametrize("nb,T", [(4096, 100), (13, 9)])
+def test_ring_forward_pass_api_equals_register_ring(gpu, nb, T):
+    """ilqr_forward (forward_pass) through either forward kernel: same bits, including
+    exhausted line searches (prev_cost = -Inf → inputs returned, max_trials trials)."""
+    lq, x, u = (quadrotor_batch(nb, T=T, seed0=1) if nb == 4096
+                else random_lq_batch(nb, 12, 4, T, seed=nb + T))
+    s = Solver(12, 4, T, nb)
+    s.set_problem(lq)
+    xi, ui = dev(x), dev(u)
+    d, K, _ = s.backward(xi, ui)
+    pcs = torch.full((nb,), float("inf"), dtype=torch.float64, device="cuda")
+    pcs[::3] = -float("inf")
+    outs = []
+    for ring in (False, True):
+        s.set_schedule(ring_forward=ring)
+        outs.append(s.forward(xi, ui, d, K, pcs, max_trials=5))
+    for a, b in zip(*outs):
+        torch.testing.assert_close(a, b, rtol=0, atol=0, equal_nan=True)
+    assert (outs[1][4][::3].cpu().numpy() == _lib.TRAJ_LS_EXHAUSTED).all()
