@@ -877,11 +877,15 @@ __global__ __launch_bounds__(CH_WG) void chain_forward_kernel(
     V* __restrict__ new_cost, int32_t* __restrict__ trials, int32_t* __restrict__ status,
     LSParams ls) {
   constexpr int NX = 2 * NJ;
+  __shared__ ChainK<V, NJ> Ps;  // constants in LDS (see chain_iter_forward_kernel)
+  for (int i = threadIdx.x; i < (int)(sizeof(ChainK<V, NJ>) / 4); i += CH_WG)
+    reinterpret_cast<uint32_t*>(&Ps)[i] = reinterpret_cast<const uint32_t*>(&P)[i];
+  __syncthreads();
   const int b = (blockIdx.x * CH_WG + threadIdx.x) / CH_FW_LANES;
   if (b >= B) return;  // the whole lane group
   const V pc = prev_cost ? prev_cost[b] : V(INFINITY);
   const ChainFwdOut<V> r =
-      chain_forward_lane<V, NJ, NU, true>(P, b, T, x, u, xtraj, d, K, pc, xnew, unew, nullptr, ls);
+      chain_forward_lane<V, NJ, NU, true>(Ps, b, T, x, u, xtraj, d, K, pc, xnew, unew, nullptr, ls);
   if ((threadIdx.x & 3) != 0) return;
   if (!r.accepted) {  // exhausted (the reference would loop forever): return the inputs
     for (int i = 0; i < (T + 1) * NX; ++i) xnew[(size_t)b * (T + 1) * NX + i] = x[(size_t)b * (T + 1) * NX + i];
@@ -907,11 +911,18 @@ __global__ __launch_bounds__(CH_WG) void chain_iter_backward_kernel(ChainK<V, NJ
 template <class V, int NJ, int NU>
 __global__ __launch_bounds__(CH_WG) void chain_iter_forward_kernel(ChainK<V, NJ> P, int B, int T,
                                                                    ChainIter<V> a, LSParams ls) {
+  // the chain constants go to LDS: as a kernel argument they overflow the SGPR file
+  // (~210 SGPRs spilled to VGPR lanes at every use)
+  __shared__ ChainK<V, NJ> Ps;
+  static_assert(sizeof(ChainK<V, NJ>) % 4 == 0, "dword copy");
+  for (int i = threadIdx.x; i < (int)(sizeof(ChainK<V, NJ>) / 4); i += CH_WG)
+    reinterpret_cast<uint32_t*>(&Ps)[i] = reinterpret_cast<const uint32_t*>(&P)[i];
+  __syncthreads();
   const int b = (blockIdx.x * CH_WG + threadIdx.x) / CH_FW_LANES;
   if (b >= B || a.status[b] != ILQR_TRAJ_OK) return;  // the whole lane group
   V du2 = V(0);
   const V pc = a.prev_cost ? a.prev_cost[b] : V(INFINITY);
-  const ChainFwdOut<V> r = chain_forward_lane<V, NJ, NU, true>(P, b, T, a.x, a.u, a.xtraj, a.d,
+  const ChainFwdOut<V> r = chain_forward_lane<V, NJ, NU, true>(Ps, b, T, a.x, a.u, a.xtraj, a.d,
                                                                a.K, pc, a.xnew, a.unew, &du2, ls);
   if ((threadIdx.x & 3) != 0) return;
   if (a.trials) a.trials[b] = r.trials;
