@@ -19,7 +19,17 @@ __global__ __launch_bounds__(256) void kern(double* out, long long* cyc, int ite
   long long t0 = __builtin_amdgcn_s_memtime();
   double res = 0;
   bool do_mfma = (MODE == 0) || (MODE == 2 && (wid & 1) == 0);
-  if (do_mfma) {
+  if (MODE == 3) {  // v_mfma_f64_4x4x4_4b: four independent 4×4×4 blocks per instruction
+    double acc[NACC];
+#pragma unroll
+    for (int i = 0; i < NACC; ++i) acc[i] = 0.0;
+    for (int it = 0; it < iters; ++it) {
+#pragma unroll
+      for (int i = 0; i < NACC; ++i) acc[i] = __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, acc[i], 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < NACC; ++i) res += acc[i];
+  } else if (do_mfma) {
     d4 acc[NACC];
 #pragma unroll
     for (int i = 0; i < NACC; ++i) acc[i] = d4{0, 0, 0, 0};
@@ -66,7 +76,7 @@ int run(const char* name, int blocks, int iters) {
   double waves_per_simd = blocks * 4.0 / 1024.0;
   long long nops = (long long)iters * NACC * (MODE == 1 ? 8 : 1);
   // flops: MFMA 16x16x4 = 2048 flop per wave-instr; VALU fma wave64 = 128 flop
-  double flop_per = (MODE == 1) ? 128.0 : 2048.0;
+  double flop_per = (MODE == 1) ? 128.0 : (MODE == 3 ? 512.0 : 2048.0);
   double tflops;
   if (MODE == 2) tflops = (blocks * 2.0 * nops * 2048.0 + blocks * 2.0 * (double)iters * NACC * 8 * 128.0) / (ms * 1e-3) / 1e12;
   else tflops = blocks * 4.0 * nops * flop_per / (ms * 1e-3) / 1e12;
@@ -90,5 +100,10 @@ int main() {
   run<1, 1>("valu fma_f64 8 chains", 2048, it);
   run<2, 4>("mixed mfma(4acc)|valu(4x8)", 512, it / 4);
   run<2, 4>("mixed mfma(4acc)|valu(4x8)", 1024, it / 4);
+  run<3, 1>("mfma_f64 4x4x4_4b 1 acc", 256, it);
+  run<3, 4>("mfma_f64 4x4x4_4b 4 acc", 256, it / 4);
+  run<3, 4>("mfma_f64 4x4x4_4b 4 acc", 1024, it / 4);
+  run<3, 8>("mfma_f64 4x4x4_4b 8 acc", 1024, it / 8);
+  run<0, 4>("mfma_f64 16x16x4 4 acc (again)", 1024, it / 4);
   return 0;
 }
