@@ -243,7 +243,7 @@ def main():
         "config": {"workload": "quadrotor-style LQ fit iteration (cold start)", "nx": NX, "nu": NU,
                    "T": T, "batch_per_gpu": B, "global_batch": B * world,
                    "parallelism": f"independent trajectories, {world} rank(s), no data-path collective"},
-        "roofline": {"bound": "mfma", "kernel": "lq_backward (backward_pass, v_mfma_f64_16x16x4_f64)",
+        "roofline": {"bound": "mfma", "kernel": "lq_iter_backward4 (backward_pass, 4 trajectories per wave, v_mfma_f64_4x4x4_4b)",
                      "achieved": achieved_tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved_tf / FP64_PEAK_TFLOPS, "traffic": traffic,
                      "avg_launch_ms": bw_ms, "algorithmic_flops_per_launch": bw_flops,

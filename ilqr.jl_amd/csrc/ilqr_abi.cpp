@@ -46,6 +46,7 @@ struct ilqr_handle {
   // forward of sequential iterations through the LDS-ring kernel
   bool pipelined = false;
   bool fw_ring = true;
+  bool bw_wave = false;  // ILQR_SCHED_BACKWARD_WAVE (implied by pipelined)
   int bound[3] = {0, 0, 0};
   hipEvent_t ev_bw[2] = {nullptr, nullptr};
   hipEvent_t ev_fw[2] = {nullptr, nullptr};
@@ -121,14 +122,14 @@ ilqr_status enqueue_iteration(ilqr_handle* h, const ilqr_problem* p, const ilqr:
   }
   const ilqr::LQParams P = lq_params(p);
   if (h->nchunks == 1) {  // one stream, no cross-stream events (each hand-off costs ~10 µs)
-    HIP_TRY(ilqr::launch_lq_iter_backward(h->nx, h->nu, P, 0, h->batch, h->T, a, ls.mu, h->stream));
+    HIP_TRY(ilqr::launch_lq_iter_backward(h->nx, h->nu, P, 0, h->batch, h->T, a, ls.mu, h->stream, h->bw_wave));
     HIP_TRY(ilqr::launch_lq_iter_forward(h->nx, h->nu, P, 0, h->batch, h->T, a, ls, h->stream, h->fw_ring));
     return ILQR_OK;
   }
   for (int c = 0; c < h->nchunks; ++c) {
     const int b0 = h->bound[c], b1 = h->bound[c + 1];
     if (chain) HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_fw[c], 0));
-    HIP_TRY(ilqr::launch_lq_iter_backward(h->nx, h->nu, P, b0, b1, h->T, a, ls.mu, h->stream));
+    HIP_TRY(ilqr::launch_lq_iter_backward(h->nx, h->nu, P, b0, b1, h->T, a, ls.mu, h->stream, h->bw_wave));
     HIP_TRY(hipEventRecord(h->ev_bw[c], h->stream));
     HIP_TRY(hipStreamWaitEvent(h->side, h->ev_bw[c], 0));
     HIP_TRY(ilqr::launch_lq_iter_forward(h->nx, h->nu, P, b0, b1, h->T, a, ls, h->side));
@@ -193,6 +194,7 @@ ilqr_status ensure_pad(ilqr_handle* h) {
   h->pad->stream = h->stream;
   h->pad->pipelined = h->pipelined;
   h->pad->fw_ring = h->fw_ring;
+  h->pad->bw_wave = h->bw_wave;
   return ILQR_OK;
 }
 
@@ -374,9 +376,16 @@ ilqr_status ilqr_set_stream(ilqr_handle* h, void* s) {
 }
 
 ilqr_status ilqr_set_schedule(ilqr_handle* h, int flags) {
-  if (!h || (flags & ~(ILQR_SCHED_PIPELINED | ILQR_SCHED_RING_FORWARD)) != 0) return ILQR_ERR_BAD_ARG;
+  if (!h || (flags & ~(ILQR_SCHED_PIPELINED | ILQR_SCHED_RING_FORWARD | ILQR_SCHED_BACKWARD_WAVE)) != 0)
+    return ILQR_ERR_BAD_ARG;
   h->pipelined = (flags & ILQR_SCHED_PIPELINED) != 0;
   h->fw_ring = (flags & ILQR_SCHED_RING_FORWARD) != 0;
+  h->bw_wave = (flags & (ILQR_SCHED_BACKWARD_WAVE | ILQR_SCHED_PIPELINED)) != 0;
+  if (h->pad) {
+    h->pad->pipelined = h->pipelined;
+    h->pad->fw_ring = h->fw_ring;
+    h->pad->bw_wave = h->bw_wave;
+  }
   return ILQR_OK;
 }
 
@@ -413,7 +422,7 @@ ilqr_status ilqr_backward(ilqr_handle* h, const ilqr_problem* p, const ilqr_opti
                                      status, ls_params(o).mu, h->stream));
   else
     HIP_TRY(ilqr::launch_lq_backward(h->nx, h->nu, lq_params(p), h->batch, h->T, x, u, d, K,
-                                     status, ls_params(o).mu, h->stream));
+                                     status, ls_params(o).mu, h->stream, h->bw_wave));
   return status ? fold_status(h, status) : ILQR_OK;
 }
 

@@ -1,0 +1,422 @@
+// Backward pass of the LQ family with FOUR trajectories per wave on the 4-block
+// f64 MFMA, v_mfma_f64_4x4x4f64 (backward v7).
+//
+// Reference path: backward_pass (aabouman/iLQR.jl src/backward_pass.jl:324-357) —
+// the same recursion as lq_backward_wave in ilqr_lq.hip, re-tiled:
+//  * the 4-block MFMA computes four independent 4×4×4 products per instruction
+//    (one per trajectory slot β) at 63-66 TF/s against 42-44 TF/s for the 16×16×4
+//    tile (profiles/r01/ubench_f64_4x4.log), and its 4×4 blocks fit the 12-state,
+//    4-input shape exactly: no zero padding of the 13×16 augmented tile;
+//  * the 4×4 gain solve runs once per slot (16 lanes) instead of once per wave,
+//    so the VALU share is amortised over four trajectories.
+//
+// Lane layout (measured by tools/mfma4_probe.hip): lane l = 16ρ + 4β + κ holds
+// element [ρ][κ] of slot β's 4×4 block ("D layout"). The instruction computes
+//     mf4(a, b, c) = c + aᵀ·b      for D-layout blocks a, b, c
+// i.e. a D-layout register is the B operand as is and the A operand transposed.
+// Vectors are kept "replicated": block register v[I] holds v[4I+ρ] in every κ.
+//
+// Per step (nx = 12 → 3 blocks, nu = 4 → 1 block; F = [A | B] = F[K][J], K < 3, J < 4):
+//   Y[I][J]  = Σ_K mf4(S[K][I], F[K][J])                 S·F            36 MFMAs
+//   Z[I][J]  = L[I][J] + Σ_K mf4(F[K][I], Y[K][J])       FᵀSF, I ≤ J    30 MFMAs
+//   gv[I]    = Σ_K mf4(L[K][I], z[K]) + Σ_K mf4(F[K][I], s[K])
+//            = [lx + Aᵀs | lu + Bᵀs]                                     22 MFMAs
+//   H_reg = Z[3][3] + μI = L D Lᵀ (every lane of the slot, VALU), M = L⁻¹:
+//   P[J]     = Mᵀ D⁻¹ M [G | g][J]  = (H + μI)⁻¹[G | g]   (K_aug = −P)   8 MFMAs
+//   W        = (H + 2μI) K_aug = −([G | g] + μP)
+//   S[I][J]  = mf4(P[I], W[J], Z[I][J])  (I ≤ J < 3),  s[I] = mf4(P[I], W[3], gv[I])
+//            = [Qxx | lx + Aᵀs] − K_augᵀ(H + 2μI)K_aug   (step_back :268-270)
+//   S[J][I]  = S[I][J]ᵀ by a lane permutation (ds_bpermute), diagonal blocks
+//              symmetrised every SYM_EVERY steps as in the 16×16 kernel.
+// The solve is LDLᵀ as in the one-trajectory kernel, applied as the triangular
+// factors' explicit inverses on the MFMA (M = L⁻¹ has six entries).
+#include <hip/hip_runtime.h>
+#include <math.h>
+
+#include "ilqr_internal.h"
+#include "ilqr_device.h"
+#include "../../include/ilqr.h"
+
+namespace ilqr {
+namespace {
+
+constexpr int BW4_SLOTS = 4;          // trajectories per wave
+constexpr int BW4_WAVES = 4;          // waves per workgroup
+constexpr int BW4_LDS = 64;           // doubles of LDS per wave: the four H tiles
+
+__device__ __forceinline__ double mf4(double a, double b, double c) {
+  return __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c, 0, 0, 0);
+}
+
+// v from lane `src_byte / 4` (ds_bpermute, both dwords)
+__device__ __forceinline__ double lane_perm(double v, int src_byte) {
+  u2v p = __builtin_bit_cast(u2v, v);
+  p.x = (unsigned)__builtin_amdgcn_ds_bpermute(src_byte, (int)p.x);
+  p.y = (unsigned)__builtin_amdgcn_ds_bpermute(src_byte, (int)p.y);
+  return __builtin_bit_cast(double, p);
+}
+
+// lanes of slot β: bits [3:2] of the lane index
+__device__ __forceinline__ unsigned long long slot_lanes(int beta) {
+  return (0xFull << (4 * beta)) * 0x0001000100010001ull;
+}
+
+// mf4 with a negated A operand (the f64 MFMA's neg modifier, blgp bit 0)
+__device__ __forceinline__ double mf4n(double a, double b, double c) {
+  return __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c, 0, 0, 1);
+}
+
+__device__ __forceinline__ double buf_ld(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0));
+}
+__device__ __forceinline__ void buf_st(double v, __amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, v), r, voff, soff, 0);
+}
+
+// ABL: bits for tools/bw4_probe.hip only (0 in the product). Ablations (wrong
+// gains): 1 no factorisation, 2 no transposes, 4 no gradient, 8 no gain stores,
+// 64 no z loads. Variants (correct gains): 16 the explicit (H + μI)⁻¹ instead of
+// the two triangular sweeps, 32 L z per step instead of four steps per MFMA.
+//
+// Backward pass of trajectories b0 .. b0+3 (slots with active bit clear, or past B,
+// compute on clamped data and store nothing). Returns the slots whose gains hold a
+// NaN (bit β): the reference's @assert !any(isnan, ...) (:353-354). A NaN in any K_t
+// or d_t reaches K_0 or d_0 (S and s carry it down the recursion; no step compares,
+// selects or clamps), so the test reads the last step's gains only.
+template <int ABL = 0>
+__device__ unsigned lq_backward4_wave(const LQParams& P, int b0, int B, unsigned active, int T,
+                                      const double* __restrict__ x, const double* __restrict__ u,
+                                      double* __restrict__ d_out, double* __restrict__ K_out,
+                                      double mu, double* lds) {
+  constexpr int NX = 12, NU = 4;
+  b0 = __builtin_amdgcn_readfirstlane(b0);
+  const int l = threadIdx.x & 63;
+  const int rho = l >> 4;
+  const int beta = (l >> 2) & 3;
+  const int kap = l & 3;
+  const int b = b0 + beta;
+  const bool live = b < B && ((active >> beta) & 1u);
+  const int bc = b < B ? b : B - 1;  // clamped: every load stays in bounds
+  const int nslot = B - b0 < 4 ? B - b0 : 4;
+
+  const double* Ab = P.A + (size_t)bc * NX * NX;
+  const double* Bb = P.B + (size_t)bc * NX * NU;
+  const double* Qb = P.Q + (size_t)bc * NX * NX;
+  const double* Rb = P.R + (size_t)bc * NU * NU;
+  const double* Qfb = P.Qf + (size_t)bc * NX * NX;
+
+  // F = [A | B] blocks, L = Q + Qᵀ blocks (immediate_cost_quadratization :101-106)
+  double F[3][4], L[3][3];
+#pragma unroll
+  for (int K = 0; K < 3; ++K) {
+    const int r = 4 * K + rho;
+#pragma unroll
+    for (int J = 0; J < 3; ++J) F[K][J] = Ab[r * NX + 4 * J + kap];
+    F[K][3] = Bb[r * NU + kap];
+#pragma unroll
+    for (int I = 0; I < 3; ++I) L[K][I] = Qb[r * NX + 4 * I + kap] + Qb[(4 * I + kap) * NX + r];
+  }
+  const double LR = Rb[rho * NU + kap] + Rb[kap * NU + rho];
+
+  // the lane permutation ρ ↔ κ (block transpose within each slot)
+  const int tr_src = (16 * kap + 4 * beta + rho) * 4;
+
+  // terminal value function (final_cost_quadratization :134-153): S = Qf + Qfᵀ, s = S x_N
+  double S[3][3], s[3];
+  {
+    const double* xN = x + ((size_t)bc * (T + 1) + T) * NX;
+    double xr[3];
+#pragma unroll
+    for (int K = 0; K < 3; ++K) {
+      const int r = 4 * K + rho;
+      xr[K] = xN[r];
+#pragma unroll
+      for (int I = 0; I < 3; ++I) S[K][I] = Qfb[r * NX + 4 * I + kap] + Qfb[(4 * I + kap) * NX + r];
+    }
+#pragma unroll
+    for (int I = 0; I < 3; ++I) {
+      double v = 0.0;
+#pragma unroll
+      for (int K = 0; K < 3; ++K) v = mf4(S[K][I], xr[K], v);
+      s[I] = v;
+    }
+  }
+
+  // the wave's x, u, K, d through buffer resources over its slots (records end at
+  // slot nslot: loads past it read 0, stores are dropped); per-lane offsets are
+  // loop constants, the step enters as the scalar offset
+  const auto rX = buffer_rsrc(const_cast<double*>(x) + (size_t)b0 * (T + 1) * NX, (uint32_t)(nslot * (T + 1) * NX * 8));
+  const auto rU = buffer_rsrc(const_cast<double*>(u) + (size_t)b0 * T * NU, (uint32_t)(nslot * T * NU * 8));
+  const auto rK = buffer_rsrc(K_out + (size_t)b0 * T * NU * NX, (uint32_t)(nslot * T * NU * NX * 8));
+  const auto rD = buffer_rsrc(d_out + (size_t)b0 * T * NU, (uint32_t)(nslot * T * NU * 8));
+  const uint32_t DEAD = 0x80000000u;  // beyond every record count
+  const uint32_t kv = live ? (uint32_t)((beta * T * NU * NX + rho * NX + kap) * 8) : DEAD;
+  const uint32_t dv = (live && kap == 0) ? (uint32_t)((beta * T * NU + rho) * 8) : DEAD;
+
+  // z_t = [x_t; u_t] (cost gradient L z, :101-106). LZ4: one MFMA set gives L z for
+  // steps t0 .. t0-3 (column κ = step t0-κ); each step permutes its column out.
+  constexpr bool LZ4 = (ABL & 32) == 0;
+  double Lzq[4] = {0.0, 0.0, 0.0, 0.0}, zq[4], zc[4], zn[4];
+  auto load_zq = [&](int t0) {  // clamped at step 0
+    const int tz = t0 - kap > 0 ? t0 - kap : 0;
+    const uint32_t xo = (uint32_t)(((beta * (T + 1) + tz) * NX + rho) * 8);
+    const uint32_t uo = (uint32_t)(((beta * T + tz) * NU + rho) * 8);
+#pragma unroll
+    for (int K = 0; K < 3; ++K) zq[K] = buf_ld(rX, xo + 32 * K, 0);
+    zq[3] = buf_ld(rU, uo, 0);
+  };
+  const uint32_t zxo = (uint32_t)((beta * (T + 1) * NX + rho) * 8), zuo = (uint32_t)((beta * T * NU + rho) * 8);
+  auto load_z = [&](int t, double (&z)[4]) {
+#pragma unroll
+    for (int K = 0; K < 3; ++K) z[K] = buf_ld(rX, zxo + 32 * K, (uint32_t)(t * NX * 8));
+    z[3] = buf_ld(rU, zuo, (uint32_t)(t * NU * 8));
+  };
+  if constexpr (LZ4) load_zq(T - 1);
+  else load_z(T - 1, zc);
+
+  double* Hl = lds + beta * 16;
+  double Klast[4];
+  // every load of the prologue lands here, so the loop's waits only count the loop's
+  // own loads
+  __builtin_amdgcn_s_waitcnt(0);
+
+  for (int t = T - 1; t >= 0; --t) {
+    if constexpr ((ABL & 64) != 0) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) zn[k] = zc[k] * 0.5;
+    } else if constexpr (!LZ4) {
+      load_z(t > 0 ? t - 1 : 0, zn);
+    }
+
+    // Y = S·F, column block 3 (B) first: H needs it
+    double Y[3][4];
+#pragma unroll
+    for (int J = 3; J >= 0; --J)
+#pragma unroll
+      for (int I = 0; I < 3; ++I) {
+        double v = 0.0;
+#pragma unroll
+        for (int K = 0; K < 3; ++K) v = mf4(S[K][I], F[K][J], v);
+        Y[I][J] = v;
+      }
+    // H = R + Rᵀ + BᵀSB → LDS, read back whole by the slot's lanes
+    double H = LR;
+#pragma unroll
+    for (int K = 0; K < 3; ++K) H = mf4(F[K][3], Y[K][3], H);
+    Hl[rho * 4 + kap] = H;
+
+    // gradient [lx + Aᵀs | lu + Bᵀs] (:181, :269)
+    double gv[4];
+    if constexpr (LZ4) {
+      const int j = (T - 1 - t) & 3;
+      if (j == 0) {  // L z for steps t .. t-3, then the next four steps' z
+#pragma unroll
+        for (int I = 0; I < 3; ++I) {
+          double v = 0.0;
+#pragma unroll
+          for (int K = 0; K < 3; ++K) v = mf4(L[K][I], zq[K], v);
+          Lzq[I] = v;
+        }
+        Lzq[3] = mf4(LR, zq[3], 0.0);
+        load_zq(t - 4);
+      }
+      const int src = ((l & ~3) | j) * 4;
+#pragma unroll
+      for (int I = 0; I < 4; ++I) {
+        double v = lane_perm(Lzq[I], src);
+#pragma unroll
+        for (int K = 0; K < 3; ++K) v = mf4(F[K][I], s[K], v);
+        gv[I] = v;
+      }
+    } else if constexpr ((ABL & 4) != 0) {
+#pragma unroll
+      for (int I = 0; I < 4; ++I) gv[I] = I < 3 ? s[I] + zc[I] : zc[3];
+    } else {
+#pragma unroll
+      for (int I = 0; I < 4; ++I) {
+        double v = 0.0;
+        if (I < 3) {
+#pragma unroll
+          for (int K = 0; K < 3; ++K) v = mf4(L[K][I], zc[K], v);
+        } else {
+          v = mf4(LR, zc[3], v);
+        }
+#pragma unroll
+        for (int K = 0; K < 3; ++K) v = mf4(F[K][I], s[K], v);
+        gv[I] = v;
+      }
+    }
+    // G = BᵀSA (lux = 0) and Qxx = lxx + AᵀSA (upper blocks)
+    double G[3], Z[3][3];
+#pragma unroll
+    for (int J = 0; J < 3; ++J) {
+      double v = 0.0;
+#pragma unroll
+      for (int K = 0; K < 3; ++K) v = mf4(F[K][3], Y[K][J], v);
+      G[J] = v;
+    }
+#pragma unroll
+    for (int I = 0; I < 3; ++I)
+#pragma unroll
+      for (int J = I; J < 3; ++J) {
+        double v = L[I][J];
+#pragma unroll
+        for (int K = 0; K < 3; ++K) v = mf4(F[K][I], Y[K][J], v);
+        Z[I][J] = v;
+      }
+
+    // (H + μI) = L D Lᵀ in every lane of the slot (feedback_parameters :207-218)
+    wave_lds_fence();
+    double h[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int k = 0; k <= i; ++k) h[i][k] = Hl[i * 4 + k];
+    wave_lds_fence();
+    LDLT<4, 1> f;
+    if constexpr ((ABL & 1) != 0) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        f.dinv[i] = h[i][i];
+#pragma unroll
+        for (int k = 0; k < i; ++k) f.l[i][k] = h[i][k] * 1e-3;
+      }
+    } else {
+      f.factor(h, mu);
+    }
+    // M = L⁻¹ (unit lower)
+    double Mf[4][4];
+    Mf[1][0] = -f.l[1][0];
+    Mf[2][1] = -f.l[2][1];
+    Mf[2][0] = fma(f.l[2][1], f.l[1][0], -f.l[2][0]);
+    Mf[3][2] = -f.l[3][2];
+    Mf[3][1] = fma(f.l[3][2], f.l[2][1], -f.l[3][1]);
+    Mf[3][0] = fma(-f.l[3][2], Mf[2][0], fma(-f.l[3][1], Mf[1][0], -f.l[3][0]));
+    // this lane's entries: Mn = M[ρ][κ], D⁻¹[ρ]
+    double Mn = rho == kap ? 1.0 : 0.0;
+#pragma unroll
+    for (int i = 1; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < i; ++j) Mn = (rho == i && kap == j) ? Mf[i][j] : Mn;
+    double dsel = f.dinv[0];
+#pragma unroll
+    for (int i = 1; i < 4; ++i) dsel = rho == i ? f.dinv[i] : dsel;
+
+    // K_aug = −(H + μI)⁻¹ [G | g] = −(D⁻¹M)ᵀ (M [G | g]): the LDLᵀ solve's two
+    // triangular sweeps as two MFMA stages. A operands: M·  wants M[κ][ρ] (the
+    // transpose of Mn, by the lane permutation), (D⁻¹M)ᵀ· wants D⁻¹[ρ] M[ρ][κ].
+    // (Forming (H + μI)⁻¹ = Mᵀ D⁻¹ M explicitly instead — ablation bit 16 — costs
+    // two digits on the headline's near-rank-1 H: 2e-11 against the oracle where
+    // the sweeps give 1.7e-13, profiles/r01/bw4_quad.txt.)
+    double Kg[4];
+    if constexpr ((ABL & 16) != 0) {
+      const double Hi = mf4(Mn, Mn * dsel, 0.0);
+#pragma unroll
+      for (int J = 0; J < 4; ++J) Kg[J] = mf4n(Hi, J < 3 ? G[J] : gv[3], 0.0);
+    } else {
+      const double Mt = lane_perm(Mn, tr_src), Mnd = Mn * dsel;
+#pragma unroll
+      for (int J = 0; J < 4; ++J) Kg[J] = mf4n(Mnd, mf4(Mt, J < 3 ? G[J] : gv[3], 0.0), 0.0);
+    }
+    if constexpr ((ABL & 8) == 0) {
+#pragma unroll
+      for (int J = 0; J < 3; ++J) buf_st(Kg[J], rK, kv + 32 * J, (uint32_t)(t * NU * NX * 8));
+      buf_st(Kg[3], rD, dv, (uint32_t)(t * NU * 8));
+    }
+
+    // step_back (:268-270): W = (H + 2μI) K_aug = μ K_aug − [G | g],
+    // [S | s] = [Qxx | lx + Aᵀs] − K_augᵀ W
+    double W[4];
+#pragma unroll
+    for (int J = 0; J < 3; ++J) W[J] = fma(mu, Kg[J], -G[J]);
+    W[3] = fma(mu, Kg[3], -gv[3]);
+#pragma unroll
+    for (int I = 0; I < 3; ++I) {
+#pragma unroll
+      for (int J = I; J < 3; ++J) S[I][J] = mf4n(Kg[I], W[J], Z[I][J]);
+      s[I] = mf4n(Kg[I], W[3], gv[I]);
+    }
+    if ((t % SYM_EVERY) == 0) {
+#pragma unroll
+      for (int I = 0; I < 3; ++I) S[I][I] = 0.5 * (S[I][I] + lane_perm(S[I][I], tr_src));
+    }
+#pragma unroll
+    for (int I = 0; I < 3; ++I)
+#pragma unroll
+      for (int J = I + 1; J < 3; ++J) S[J][I] = (ABL & 2) ? S[I][J] : lane_perm(S[I][J], tr_src);
+    if constexpr (!LZ4) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) zc[k] = zn[k];
+    }
+#pragma unroll
+    for (int J = 0; J < 4; ++J) Klast[J] = Kg[J];
+  }
+  bool nan = false;
+#pragma unroll
+  for (int J = 0; J < 4; ++J) nan |= __builtin_isnan(Klast[J]);
+  const unsigned long long nb = __ballot(nan);
+  unsigned r = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) r |= (nb & slot_lanes(q)) ? (1u << q) : 0u;
+  return r;
+}
+
+template <int ABL = 0>
+__global__ __launch_bounds__(256) void lq_backward4_kernel(LQParams P, int B, int T,
+                                                           const double* __restrict__ x,
+                                                           const double* __restrict__ u,
+                                                           double* __restrict__ d,
+                                                           double* __restrict__ K,
+                                                           int32_t* __restrict__ status, double mu) {
+  __shared__ __attribute__((aligned(16))) double lds[BW4_WAVES * BW4_LDS];
+  const int w = threadIdx.x >> 6;
+  const int b0 = (blockIdx.x * BW4_WAVES + w) * BW4_SLOTS;
+  if (b0 >= B) return;
+  const unsigned nan = lq_backward4_wave<ABL>(P, b0, B, 0xFu, T, x, u, d, K, mu, lds + w * BW4_LDS);
+  const int l = threadIdx.x & 63;
+  if (status && l < BW4_SLOTS && b0 + l < B) status[b0 + l] = ((nan >> l) & 1u) ? ILQR_TRAJ_NAN : ILQR_TRAJ_OK;
+}
+
+// fit iteration, part 1 (see lq_iter_backward_kernel): slots whose status is not OK
+// are skipped (computed on, never stored)
+__global__ __launch_bounds__(256) void lq_iter_backward4_kernel(LQParams P, int B, int T, IterArgs a,
+                                                                double mu) {
+  __shared__ __attribute__((aligned(16))) double lds[BW4_WAVES * BW4_LDS];
+  const int w = threadIdx.x >> 6;
+  const int b0 = (blockIdx.x * BW4_WAVES + w) * BW4_SLOTS;
+  if (b0 >= B) return;
+  unsigned active = 0;
+#pragma unroll
+  for (int q = 0; q < BW4_SLOTS; ++q)
+    if (b0 + q < B && a.status[b0 + q] == ILQR_TRAJ_OK) active |= 1u << q;
+  if (active == 0) return;
+  const unsigned nan = lq_backward4_wave(P, b0, B, active, T, a.x, a.u, a.d, a.K, mu, lds + w * BW4_LDS) & active;
+  const int l = threadIdx.x & 63;
+  if (l < BW4_SLOTS && ((nan >> l) & 1u)) {
+    a.status[b0 + l] = ILQR_TRAJ_NAN;  // reference: AssertionError at backward_pass.jl:353
+    if (a.res_parity) a.res_parity[b0 + l] = a.parity;
+  }
+}
+
+}  // namespace
+
+int bw4_grid(int B) {
+  const int per_wg = BW4_WAVES * BW4_SLOTS;
+  return (B + per_wg - 1) / per_wg;
+}
+
+hipError_t launch_lq_backward4(const LQParams& p, int B, int T, const double* x, const double* u,
+                               double* d, double* K, int32_t* status, double mu, hipStream_t s) {
+  if (B <= 0) return hipSuccess;
+  lq_backward4_kernel<0><<<bw4_grid(B), 256, 0, s>>>(p, B, T, x, u, d, K, status, mu);
+  return hipGetLastError();
+}
+
+hipError_t launch_lq_iter_backward4(const LQParams& p, int B, int T, const IterArgs& a, double mu,
+                                    hipStream_t s) {
+  if (B <= 0) return hipSuccess;
+  lq_iter_backward4_kernel<<<bw4_grid(B), 256, 0, s>>>(p, B, T, a, mu);
+  return hipGetLastError();
+}
+
+}  // namespace ilqr

@@ -46,7 +46,17 @@ struct IterArgs {
 // Returns hipSuccess or the launch error. All launches are asynchronous on `s`.
 hipError_t launch_lq_backward(int nx, int nu, const LQParams& p, int B, int T, const double* x,
                               const double* u, double* d, double* K, int32_t* status, double mu,
-                              hipStream_t s);
+                              hipStream_t s, bool wave = false);
+// (12, 4) goes to the four-trajectories-per-wave kernel (ilqr_bw4.hip) unless
+// `wave` (ILQR_SCHED_BACKWARD_WAVE) selects the one-trajectory-per-wave kernel
+// (launch_lq_backward_v6), which the pipelined schedule's fused kernel also runs.
+hipError_t launch_lq_backward4(const LQParams& p, int B, int T, const double* x, const double* u,
+                               double* d, double* K, int32_t* status, double mu, hipStream_t s);
+hipError_t launch_lq_iter_backward4(const LQParams& p, int B, int T, const IterArgs& a, double mu,
+                                    hipStream_t s);
+hipError_t launch_lq_backward_v6(int nx, int nu, const LQParams& p, int B, int T, const double* x,
+                                 const double* u, double* d, double* K, int32_t* status, double mu,
+                                 hipStream_t s);
 hipError_t launch_lq_forward(int nx, int nu, const LQParams& p, int B, int T, const double* x,
                              const double* u, const double* xtraj, const double* d,
                              const double* K, const double* prev_cost, double* xnew,
@@ -55,7 +65,7 @@ hipError_t launch_lq_forward(int nx, int nu, const LQParams& p, int B, int T, co
 // The two halves of one fit iteration over trajectories [b0, b1) (pointers in
 // `a` and `p` address the whole batch).
 hipError_t launch_lq_iter_backward(int nx, int nu, const LQParams& p, int b0, int b1, int T,
-                                   const IterArgs& a, double mu, hipStream_t s);
+                                   const IterArgs& a, double mu, hipStream_t s, bool wave = false);
 hipError_t launch_lq_iter_forward(int nx, int nu, const LQParams& p, int b0, int b1, int T,
                                   const IterArgs& a, const LSParams& ls, hipStream_t s,
                                   bool ring = false);

@@ -1298,7 +1298,15 @@ bool lq_supported(int nx, int nu) { return nx == 12 && nu == 4; }
 
 hipError_t launch_lq_backward(int nx, int nu, const LQParams& p, int B, int T, const double* x,
                               const double* u, double* d, double* K, int32_t* status, double mu,
-                              hipStream_t s) {
+                              hipStream_t s, bool wave) {
+  if (wave) return launch_lq_backward_v6(nx, nu, p, B, T, x, u, d, K, status, mu, s);
+  if (nx == 12 && nu == 4) return launch_lq_backward4(p, B, T, x, u, d, K, status, mu, s);
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_lq_backward_v6(int nx, int nu, const LQParams& p, int B, int T, const double* x,
+                                 const double* u, double* d, double* K, int32_t* status, double mu,
+                                 hipStream_t s) {
   const int grid = (B + WAVES_PER_WG - 1) / WAVES_PER_WG;
   ILQR_DISPATCH(12, 4, (lq_backward_kernel<NX_, NU_><<<grid, 256, 0, s>>>(p, B, T, x, u, d, K, status, mu)));
   return hipErrorInvalidValue;
@@ -1346,13 +1354,17 @@ IterArgs shift(const IterArgs& a, int nx, int nu, int T, int b0) {
 }  // namespace
 
 hipError_t launch_lq_iter_backward(int nx, int nu, const LQParams& p, int b0, int b1, int T,
-                                   const IterArgs& a, double mu, hipStream_t s) {
+                                   const IterArgs& a, double mu, hipStream_t s, bool wave) {
   const int B = b1 - b0;
   if (B <= 0) return hipSuccess;
-  const int grid = (B + WAVES_PER_WG - 1) / WAVES_PER_WG;
   const LQParams ps = shift(p, nx, nu, b0);
   const IterArgs as = shift(a, nx, nu, T, b0);
-  ILQR_DISPATCH(12, 4, (lq_iter_backward_kernel<NX_, NU_><<<grid, 256, 0, s>>>(ps, B, T, as, mu)));
+  if (wave) {
+    const int grid = (B + WAVES_PER_WG - 1) / WAVES_PER_WG;
+    ILQR_DISPATCH(12, 4, (lq_iter_backward_kernel<NX_, NU_><<<grid, 256, 0, s>>>(ps, B, T, as, mu)));
+    return hipErrorInvalidValue;
+  }
+  if (nx == 12 && nu == 4) return launch_lq_iter_backward4(ps, B, T, as, mu, s);
   return hipErrorInvalidValue;
 }
 

@@ -31,6 +31,7 @@ TRAJ_NAN = 4
 # ilqr_set_schedule flags (LQ family)
 SCHED_PIPELINED = 1
 SCHED_RING_FORWARD = 2
+SCHED_BACKWARD_WAVE = 4
 
 PROBLEM_LQ = 1
 PROBLEM_TWO_LINK = 2

@@ -80,12 +80,16 @@ class Solver:
         s = torch.cuda.current_stream(self.dev).cuda_stream
         _lib.check(self.lib.ilqr_set_stream(self.h, C.c_void_p(s)), "ilqr_set_stream")
 
-    def set_schedule(self, pipelined: bool = False, ring_forward: bool = True):
-        """LQ launch schedule (ilqr_set_schedule); every schedule returns the same bits.
-        pipelined: fit overlaps half of the workgroups' forward passes with the other
-        half's backward passes; ring_forward: the forward pass streams its inputs
-        HBM → LDS ahead of use."""
-        flags = (_lib.SCHED_PIPELINED if pipelined else 0) | (_lib.SCHED_RING_FORWARD if ring_forward else 0)
+    def set_schedule(self, pipelined: bool = False, ring_forward: bool = True,
+                     backward_wave: bool = False):
+        """LQ launch schedule (ilqr_set_schedule). pipelined: fit overlaps half of the
+        workgroups' forward passes with the other half's backward passes (implies
+        backward_wave); ring_forward: the forward pass streams its inputs HBM → LDS
+        ahead of use; backward_wave: one trajectory per wave in the backward pass
+        (16x16x4 MFMA) instead of four (4x4x4 4-block MFMA). Schedules with the same
+        backward kernel return the same bits."""
+        flags = ((_lib.SCHED_PIPELINED if pipelined else 0) | (_lib.SCHED_RING_FORWARD if ring_forward else 0)
+                 | (_lib.SCHED_BACKWARD_WAVE if backward_wave else 0))
         _lib.check(self.lib.ilqr_set_schedule(self.h, flags), "ilqr_set_schedule")
 
     def set_problem(self, lq):

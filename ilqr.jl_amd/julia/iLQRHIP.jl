@@ -77,9 +77,10 @@ function Handle(nx, nu, T, batch; device=0)
     return h
 end
 
-# launch schedule of the LQ family (include/ilqr.h: ILQR_SCHED_*); same bits either way
+# launch schedule of the LQ family (include/ilqr.h: ILQR_SCHED_*)
 const ILQR_SCHED_PIPELINED = Int32(1)
 const ILQR_SCHED_RING_FORWARD = Int32(2)
+const ILQR_SCHED_BACKWARD_WAVE = Int32(4)
 set_schedule!(h::Handle, flags::Integer) =
     check(ccall((:ilqr_set_schedule, libilqr), Cint, (Ptr{Cvoid}, Cint), h.ptr, flags), "ilqr_set_schedule")
 

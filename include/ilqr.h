@@ -138,16 +138,23 @@ ilqr_status ilqr_destroy(ilqr_handle* h);
 /* HIP stream (hipStream_t) the handle launches on; NULL = the null stream. */
 ilqr_status ilqr_set_stream(ilqr_handle* h, void* hip_stream);
 ilqr_status ilqr_sync(ilqr_handle* h);
-/* Launch schedule of ilqr_iterate / ilqr_fit for the LQ family (bit flags; every
- * schedule returns the same bits):
+/* Launch schedule of ilqr_backward / ilqr_iterate / ilqr_fit for the LQ family (bit
+ * flags):
  *   ILQR_SCHED_RING_FORWARD  the forward pass streams its per-step inputs HBM → LDS
  *                            ahead of use (default on);
+ *   ILQR_SCHED_BACKWARD_WAVE the backward pass runs one trajectory per wave on the
+ *                            16x16x4 MFMA tile (the v6 kernel) instead of four
+ *                            trajectories per wave on the 4x4x4 4-block MFMA (default
+ *                            off; faster below ~2048 trajectories, slower above);
  *   ILQR_SCHED_PIPELINED     fit runs one kernel per iteration in which half of the
  *                            workgroups do forward(i-1) then backward(i) while the
- *                            other half do backward(i) then forward(i) (default off).
- * Unknown bits → ILQR_ERR_BAD_ARG. */
+ *                            other half do backward(i) then forward(i) (default off;
+ *                            implies ILQR_SCHED_BACKWARD_WAVE).
+ * Schedules with the same backward kernel return the same bits; the two backward
+ * kernels agree to rounding. Unknown bits → ILQR_ERR_BAD_ARG. */
 #define ILQR_SCHED_PIPELINED 1
 #define ILQR_SCHED_RING_FORWARD 2
+#define ILQR_SCHED_BACKWARD_WAVE 4
 ilqr_status ilqr_set_schedule(ilqr_handle* h, int flags);
 
 /* iLQR.backward_pass (backward_pass.jl:324-357): gains d (batch,T,nu) and

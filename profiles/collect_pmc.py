@@ -29,7 +29,7 @@ def read(d, counter):
             name = r["Kernel_Name"]
             key = ("backward" if "lq_iter_backward" in name else
                    "forward" if "lq_iter_forward" in name else
-                   "backward_api" if "lq_backward_kernel" in name else None)
+                   "backward_api" if "lq_backward" in name else None)
             if key:
                 vals[key].append(float(r["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in vals.items() if v}

@@ -215,6 +215,42 @@ def test_headline_backward_vs_c_oracle(gpu, headline):
     assert rel(K.cpu().numpy()[idx], Kc) < TOL_GAIN_SYM and rel(d.cpu().numpy()[idx], dc) < TOL_GAIN_SYM
 
 
+def test_backward_kernels_agree_headline(gpu, headline):
+    """The two backward kernels (4 trajectories / wave on the 4-block MFMA, the
+    default; 1 trajectory / wave on the 16x16x4 tile, ILQR_SCHED_BACKWARD_WAVE) agree
+    to rounding: both sit within 2e-13 of the symmetrised oracle on these fixtures."""
+    s, lq, x, u = headline
+    d4_, K4_, st4 = s.backward(dev(x), dev(u))
+    s.set_schedule(backward_wave=True)
+    try:
+        dw, Kw, stw = s.backward(dev(x), dev(u))
+    finally:
+        s.set_schedule()
+    assert (st4.cpu().numpy() == 0).all() and (stw.cpu().numpy() == 0).all()
+    assert rel(K4_, Kw) < 1e-12 and rel(d4_, dw) < 1e-12
+
+
+@pytest.mark.parametrize("nb", [1, 3, 5, 17, 1030])
+def test_backward4_ragged_batch_and_nan_slot(gpu, nb):
+    """Batches that leave a wave's last slots empty, and a NaN trajectory sharing its
+    wave with clean ones: the clean slots' gains match the oracle, the NaN slot alone
+    is flagged."""
+    T = 13
+    lq, x, u = random_lq_batch(nb, 12, 4, T, seed=nb + 101)
+    bad = nb // 2
+    x[bad, 4, 2] = np.nan
+    s = Solver(12, 4, T, nb)
+    s.set_problem(lq)
+    d, K, st = s.backward(dev(x), dev(u))
+    st = st.cpu().numpy()
+    assert st[bad] == _lib.TRAJ_NAN and (np.delete(st, bad) == 0).all()
+    ok = np.arange(nb) != bad
+    dc, Kc, _ = cref.lq_backward(LQBatch(lq.A[ok], lq.B[ok], lq.Q[ok], lq.R[ok], lq.Qf[ok]), x[ok], u[ok],
+                                 symmetrize=True)
+    if ok.any():
+        assert rel(K.cpu().numpy()[ok], Kc) < TOL_GAIN_SYM and rel(d.cpu().numpy()[ok], dc) < TOL_GAIN_SYM
+
+
 def test_headline_fit_reaches_kkt_and_cost_is_monotone(gpu, headline):
     s, lq, x, u = headline
     # three iterations with tol disabled: every trajectory improves (α = 1 from cold,
@@ -260,7 +296,7 @@ def test_headline_iterate_matches_backward_plus_forward(gpu, headline):
 
 # -- launch schedules (ilqr_set_schedule) ----------------------------------------------
 def _fit_both(s, x, u, **kw):
-    s.set_schedule(pipelined=False)
+    s.set_schedule(pipelined=False, backward_wave=True)  # the pipelined kernel's backward
     a = s.fit(x, u, **kw)
     s.set_schedule(pipelined=True)
     b = s.fit(x, u, **kw)

@@ -19,7 +19,22 @@ __global__ __launch_bounds__(256) void kern(double* out, long long* cyc, int ite
   long long t0 = __builtin_amdgcn_s_memtime();
   double res = 0;
   bool do_mfma = (MODE == 0) || (MODE == 2 && (wid & 1) == 0);
-  if (MODE == 3) {  // v_mfma_f64_4x4x4_4b: four independent 4×4×4 blocks per instruction
+  if (MODE == 4) {  // one wave: 8-acc 4x4x4_4b MFMAs with NACC dependent VALU fmas after each
+    double acc[8], c = 0.5 + lane;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[i] = 0.0;
+    for (int it = 0; it < iters; ++it) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        acc[i] = __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, acc[i], 0, 0, 0);
+#pragma unroll
+        for (int r = 0; r < NACC - 1; ++r) c = __builtin_fma(c, a, b);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) res += acc[i];
+    res += c;
+  } else if (MODE == 3) {  // v_mfma_f64_4x4x4_4b: four independent 4×4×4 blocks per instruction
     double acc[NACC];
 #pragma unroll
     for (int i = 0; i < NACC; ++i) acc[i] = 0.0;
@@ -105,5 +120,13 @@ int main() {
   run<3, 4>("mfma_f64 4x4x4_4b 4 acc", 1024, it / 4);
   run<3, 8>("mfma_f64 4x4x4_4b 8 acc", 1024, it / 8);
   run<0, 4>("mfma_f64 16x16x4 4 acc (again)", 1024, it / 4);
+  run<3, 8>("mfma_f64 4x4x4_4b 8 acc", 256, it / 8);
+  run<3, 16>("mfma_f64 4x4x4_4b 16 acc", 256, it / 16);
+  run<3, 8>("mfma_f64 4x4x4_4b 8 acc", 512, it / 8);
+  run<3, 16>("mfma_f64 4x4x4_4b 16 acc", 512, it / 16);
+  run<4, 1>("4x4x4 8 acc, 0 valu/mfma", 256, it / 8);
+  run<4, 2>("4x4x4 8 acc + 1 dep valu/mfma", 256, it / 8);
+  run<4, 3>("4x4x4 8 acc + 2 dep valu/mfma", 256, it / 8);
+  run<4, 5>("4x4x4 8 acc + 4 dep valu/mfma", 256, it / 8);
   return 0;
 }
