@@ -42,7 +42,7 @@ namespace {
 
 constexpr int BW4_SLOTS = 4;          // trajectories per wave
 constexpr int BW4_WAVES = 4;          // waves per workgroup
-constexpr int BW4_LDS = 64;           // doubles of LDS per wave: the four H tiles
+constexpr int BW4_LDS = 64 + 256;     // doubles of LDS per wave: the four H tiles, L z columns
 
 __device__ __forceinline__ double mf4(double a, double b, double c) {
   return __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c, 0, 0, 0);
@@ -69,14 +69,16 @@ __device__ __forceinline__ double mf4n(double a, double b, double c) {
 __device__ __forceinline__ double buf_ld(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
   return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0));
 }
+template <int AUX = 0>
 __device__ __forceinline__ void buf_st(double v, __amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
-  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, v), r, voff, soff, 0);
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, v), r, voff, soff, AUX);
 }
 
 // ABL: bits for tools/bw4_probe.hip only (0 in the product). Ablations (wrong
 // gains): 1 no factorisation, 2 no transposes, 4 no gradient, 8 no gain stores,
-// 64 no z loads. Variants (correct gains): 16 the explicit (H + μI)⁻¹ instead of
-// the two triangular sweeps, 32 L z per step instead of four steps per MFMA.
+// 64 no z loads, 128 no diagonal-block symmetrisation. Variants (correct gains): 16 the explicit (H + μI)⁻¹ instead of
+// the two triangular sweeps, 32 L z per step instead of four steps per MFMA, 256
+// the L z columns through LDS instead of lane permutations.
 //
 // Backward pass of trajectories b0 .. b0+3 (slots with active bit clear, or past B,
 // compute on clamped data and store nothing). Returns the slots whose gains hold a
@@ -220,10 +222,26 @@ __device__ unsigned lq_backward4_wave(const LQParams& P, int b0, int B, unsigned
         Lzq[3] = mf4(LR, zq[3], 0.0);
         load_zq(t - 4);
       }
-      const int src = ((l & ~3) | j) * 4;
+      double lz[4];
+      if constexpr ((ABL & 256) != 0) {  // through LDS: column j of each block, replicated
+        double* Lzl = lds + 64 + beta * 64;
+        if (j == 0) {
+          double2* w = reinterpret_cast<double2*>(Lzl + (kap * 4 + rho) * 4);
+          w[0] = double2{Lzq[0], Lzq[1]};
+          w[1] = double2{Lzq[2], Lzq[3]};
+          wave_lds_fence();
+        }
+        const double2* rd = reinterpret_cast<const double2*>(Lzl + (j * 4 + rho) * 4);
+        const double2 a = rd[0], c = rd[1];
+        lz[0] = a.x; lz[1] = a.y; lz[2] = c.x; lz[3] = c.y;
+      } else {
+        const int src = ((l & ~3) | j) * 4;
+#pragma unroll
+        for (int I = 0; I < 4; ++I) lz[I] = lane_perm(Lzq[I], src);
+      }
 #pragma unroll
       for (int I = 0; I < 4; ++I) {
-        double v = lane_perm(Lzq[I], src);
+        double v = lz[I];
 #pragma unroll
         for (int K = 0; K < 3; ++K) v = mf4(F[K][I], s[K], v);
         gv[I] = v;
@@ -319,9 +337,10 @@ __device__ unsigned lq_backward4_wave(const LQParams& P, int b0, int B, unsigned
       for (int J = 0; J < 4; ++J) Kg[J] = mf4n(Mnd, mf4(Mt, J < 3 ? G[J] : gv[3], 0.0), 0.0);
     }
     if constexpr ((ABL & 8) == 0) {
+      constexpr int AUX = (ABL >> 9) & 7;  // probe only: cache-policy bits of the gain stores
 #pragma unroll
-      for (int J = 0; J < 3; ++J) buf_st(Kg[J], rK, kv + 32 * J, (uint32_t)(t * NU * NX * 8));
-      buf_st(Kg[3], rD, dv, (uint32_t)(t * NU * 8));
+      for (int J = 0; J < 3; ++J) buf_st<AUX>(Kg[J], rK, kv + 32 * J, (uint32_t)(t * NU * NX * 8));
+      buf_st<AUX>(Kg[3], rD, dv, (uint32_t)(t * NU * 8));
     }
 
     // step_back (:268-270): W = (H + 2μI) K_aug = μ K_aug − [G | g],
@@ -336,7 +355,7 @@ __device__ unsigned lq_backward4_wave(const LQParams& P, int b0, int B, unsigned
       for (int J = I; J < 3; ++J) S[I][J] = mf4n(Kg[I], W[J], Z[I][J]);
       s[I] = mf4n(Kg[I], W[3], gv[I]);
     }
-    if ((t % SYM_EVERY) == 0) {
+    if ((ABL & 128) == 0 && (t % SYM_EVERY) == 0) {
 #pragma unroll
       for (int I = 0; I < 3; ++I) S[I][I] = 0.5 * (S[I][I] + lane_perm(S[I][I], tr_src));
     }

@@ -83,15 +83,17 @@ int main(int argc, char** argv) {
       CK(hipMemcpy(Kv.data(), K, Kv.size() * 8, hipMemcpyDeviceToHost)); \
       CK(hipMemcpy(dv.data(), d, dv.size() * 8, hipMemcpyDeviceToHost)); \
       rel(Kv, Kref, "  K"); rel(dv, dref, "  d"); } } while (0)
+  if (argc > 2) {  // scan mode: default variant only
+    for (int rep = 0; rep < 2; ++rep) { if (time("product (1 trajectory / wave)", prod)) return 1; VAR(0, "bw4"); }
+    return 0;
+  }
   for (int rep = 0; rep < 2; ++rep) {
     if (time("product (1 trajectory / wave)", prod)) return 1;
     VAR(0, "bw4 (sweeps, Lz4)");
-    VAR(16, "bw4 explicit Hinv");
-    VAR(32, "bw4 Lz per step");
-    VAR(1, "bw4 -factor");
-    VAR(2, "bw4 -transposes");
+    VAR(512, "bw4 stores aux=1");
+    VAR(1024, "bw4 stores aux=2");
+    VAR(1536, "bw4 stores aux=3");
     VAR(8, "bw4 -stores");
-    VAR(11, "bw4 -factor -transposes -stores");
   }
   return 0;
 }
