@@ -12,6 +12,8 @@
 #include "../../include/ilqr.h"
 #include "ilqr_internal.h"
 
+constexpr int BW4_MIN_BATCH = 2048;  // default backward kernel switch (see bw_wave)
+
 struct ilqr_handle {
   int device = 0;
   int nx = 0, nu = 0, T = 0, batch = 0;
@@ -46,7 +48,12 @@ struct ilqr_handle {
   // forward of sequential iterations through the LDS-ring kernel
   bool pipelined = false;
   bool fw_ring = true;
-  bool bw_wave = false;  // ILQR_SCHED_BACKWARD_WAVE (implied by pipelined)
+  // backward kernel of the LQ family: ILQR_SCHED_BACKWARD_WAVE (or PIPELINED) forces
+  // one trajectory per wave, ILQR_SCHED_BACKWARD_BLOCK four per wave; by default four
+  // per wave from BW4_MIN_BATCH trajectories up (below it there are fewer waves than
+  // SIMDs and the shorter per-wave chain of the one-trajectory kernel wins:
+  // profiles/r01/bw4_scan.txt)
+  bool bw_wave = false;
   int bound[3] = {0, 0, 0};
   hipEvent_t ev_bw[2] = {nullptr, nullptr};
   hipEvent_t ev_fw[2] = {nullptr, nullptr};
@@ -295,6 +302,7 @@ ilqr_status ilqr_create(ilqr_handle** out, int device, int nx, int nu, int T, in
   h->nu = nu;
   h->T = T;
   h->batch = batch;
+  h->bw_wave = batch < BW4_MIN_BATCH;
   const size_t B = (size_t)batch;
   hipError_t e = hipSuccess;
   for (int i = 0; i < 2 && e == hipSuccess; ++i) {
@@ -376,11 +384,15 @@ ilqr_status ilqr_set_stream(ilqr_handle* h, void* s) {
 }
 
 ilqr_status ilqr_set_schedule(ilqr_handle* h, int flags) {
-  if (!h || (flags & ~(ILQR_SCHED_PIPELINED | ILQR_SCHED_RING_FORWARD | ILQR_SCHED_BACKWARD_WAVE)) != 0)
+  if (!h || (flags & ~(ILQR_SCHED_PIPELINED | ILQR_SCHED_RING_FORWARD | ILQR_SCHED_BACKWARD_WAVE |
+                      ILQR_SCHED_BACKWARD_BLOCK)) != 0)
     return ILQR_ERR_BAD_ARG;
   h->pipelined = (flags & ILQR_SCHED_PIPELINED) != 0;
   h->fw_ring = (flags & ILQR_SCHED_RING_FORWARD) != 0;
-  h->bw_wave = (flags & (ILQR_SCHED_BACKWARD_WAVE | ILQR_SCHED_PIPELINED)) != 0;
+  if ((flags & ILQR_SCHED_BACKWARD_BLOCK) && (flags & (ILQR_SCHED_BACKWARD_WAVE | ILQR_SCHED_PIPELINED)))
+    return ILQR_ERR_BAD_ARG;
+  h->bw_wave = (flags & (ILQR_SCHED_BACKWARD_WAVE | ILQR_SCHED_PIPELINED)) != 0 ||
+               (!(flags & ILQR_SCHED_BACKWARD_BLOCK) && h->batch < BW4_MIN_BATCH);
   if (h->pad) {
     h->pad->pipelined = h->pipelined;
     h->pad->fw_ring = h->fw_ring;

@@ -81,6 +81,7 @@ end
 const ILQR_SCHED_PIPELINED = Int32(1)
 const ILQR_SCHED_RING_FORWARD = Int32(2)
 const ILQR_SCHED_BACKWARD_WAVE = Int32(4)
+const ILQR_SCHED_BACKWARD_BLOCK = Int32(8)
 set_schedule!(h::Handle, flags::Integer) =
     check(ccall((:ilqr_set_schedule, libilqr), Cint, (Ptr{Cvoid}, Cint), h.ptr, flags), "ilqr_set_schedule")
 

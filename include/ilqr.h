@@ -143,18 +143,22 @@ ilqr_status ilqr_sync(ilqr_handle* h);
  *   ILQR_SCHED_RING_FORWARD  the forward pass streams its per-step inputs HBM → LDS
  *                            ahead of use (default on);
  *   ILQR_SCHED_BACKWARD_WAVE the backward pass runs one trajectory per wave on the
- *                            16x16x4 MFMA tile (the v6 kernel) instead of four
- *                            trajectories per wave on the 4x4x4 4-block MFMA (default
- *                            off; faster below ~2048 trajectories, slower above);
+ *                            16x16x4 MFMA tile (the v6 kernel);
+ *   ILQR_SCHED_BACKWARD_BLOCK the backward pass runs four trajectories per wave on
+ *                            the 4x4x4 4-block MFMA (the v7 kernel). With neither
+ *                            flag the handle picks BLOCK from 2048 trajectories up
+ *                            and WAVE below (fewer waves than SIMDs);
  *   ILQR_SCHED_PIPELINED     fit runs one kernel per iteration in which half of the
  *                            workgroups do forward(i-1) then backward(i) while the
  *                            other half do backward(i) then forward(i) (default off;
  *                            implies ILQR_SCHED_BACKWARD_WAVE).
  * Schedules with the same backward kernel return the same bits; the two backward
- * kernels agree to rounding. Unknown bits → ILQR_ERR_BAD_ARG. */
+ * kernels agree to rounding. Unknown bits, or BLOCK with WAVE or
+ * PIPELINED → ILQR_ERR_BAD_ARG. */
 #define ILQR_SCHED_PIPELINED 1
 #define ILQR_SCHED_RING_FORWARD 2
 #define ILQR_SCHED_BACKWARD_WAVE 4
+#define ILQR_SCHED_BACKWARD_BLOCK 8
 ilqr_status ilqr_set_schedule(ilqr_handle* h, int flags);
 
 /* iLQR.backward_pass (backward_pass.jl:324-357): gains d (batch,T,nu) and

@@ -221,7 +221,7 @@ def test_backward_kernels_agree_headline(gpu, headline):
     to rounding: both sit within 2e-13 of the symmetrised oracle on these fixtures."""
     s, lq, x, u = headline
     d4_, K4_, st4 = s.backward(dev(x), dev(u))
-    s.set_schedule(backward_wave=True)
+    s.set_schedule(backward="wave")
     try:
         dw, Kw, stw = s.backward(dev(x), dev(u))
     finally:
@@ -241,6 +241,7 @@ def test_backward4_ragged_batch_and_nan_slot(gpu, nb):
     x[bad, 4, 2] = np.nan
     s = Solver(12, 4, T, nb)
     s.set_problem(lq)
+    s.set_schedule(backward="block")  # small batches default to one trajectory per wave
     d, K, st = s.backward(dev(x), dev(u))
     st = st.cpu().numpy()
     assert st[bad] == _lib.TRAJ_NAN and (np.delete(st, bad) == 0).all()
@@ -296,7 +297,7 @@ def test_headline_iterate_matches_backward_plus_forward(gpu, headline):
 
 # -- launch schedules (ilqr_set_schedule) ----------------------------------------------
 def _fit_both(s, x, u, **kw):
-    s.set_schedule(pipelined=False, backward_wave=True)  # the pipelined kernel's backward
+    s.set_schedule(pipelined=False, backward="wave")  # the pipelined kernel's backward
     a = s.fit(x, u, **kw)
     s.set_schedule(pipelined=True)
     b = s.fit(x, u, **kw)
@@ -337,6 +338,25 @@ def test_pipelined_fit_ragged(gpu, nb, T):
     if ok.any():
         assert np.array_equal(b.iters.cpu().numpy()[ok], it[ok])
         assert rel(b.u.cpu().numpy()[ok], uo[ok]) < 1e-8
+
+
+@pytest.mark.parametrize("nb,T", [(5, 3), (37, 17), (1029, 9)])
+def test_fit_block_backward_ragged_vs_oracle(gpu, nb, T):
+    """fit through the four-trajectories-per-wave backward on ragged batches with a
+    NaN trajectory that leaves in iteration 1 (its wave's other slots keep going)."""
+    lq, x, u = random_lq_batch(nb, 12, 4, T, seed=nb + 7 * T)
+    x[nb // 2, 1, 0] = np.nan
+    s = Solver(12, 4, T, nb)
+    s.set_problem(lq)
+    s.set_schedule(backward="block")
+    r = s.fit(dev(x), dev(u), max_iter=12, tol=1e-8)
+    st = r.status.cpu().numpy()
+    assert st[nb // 2] == _lib.TRAJ_NAN
+    xo, uo, co, it, sto = cref.lq_fit(LQBatch(lq.A, lq.B, lq.Q, lq.R, lq.Qf), x, u, max_iter=12,
+                                      tol=1e-8, symmetrize=True)
+    ok = np.arange(nb) != nb // 2
+    assert np.array_equal(r.iters.cpu().numpy()[ok], it[ok])
+    assert rel(r.x.cpu().numpy()[ok], xo[ok]) < 1e-8 and rel(r.u.cpu().numpy()[ok], uo[ok]) < 1e-8
 
 
 @pytest.mark.parametrize("nb,T", [(4096, 100), (37, 17), (5, 3)])
@@ -388,15 +408,19 @@ def test_fit_zero_iterations_returns_inputs(gpu, pipelined):
 PAD_SHAPES = [(1, 1), (3, 2), (4, 1), (4, 2), (6, 2), (8, 3), (10, 4), (12, 1), (12, 3)]
 
 
+@pytest.mark.parametrize("backward", ["auto", "block"])
 @pytest.mark.parametrize("nx,nu", PAD_SHAPES)
-def test_lq_padded_shapes_vs_oracle(gpu, nx, nu):
+def test_lq_padded_shapes_vs_oracle(gpu, nx, nu, backward):
     """Any nx ≤ 12, nu ≤ 4 runs on the (12, 4) kernels with zero rows/columns
-    (exactly decoupled): backward, forward, iterate and fit against the C oracle."""
+    (exactly decoupled): backward, forward, iterate and fit against the C oracle,
+    with the default backward kernel (one trajectory per wave at this batch) and the
+    four-trajectories-per-wave one."""
     nb, T = 9, 25
     lq, x, u = random_lq_batch(nb, nx, nu, T, seed=17 * nx + nu)
     assert _lib.load().ilqr_supported(_lib.PROBLEM_LQ, nx, nu) == 1
     s = Solver(nx, nu, T, nb)
     s.set_problem(lq)
+    s.set_schedule(backward=backward)
     xi, ui = dev(x), dev(u)
     d, K, st = s.backward(xi, ui)
     assert d.shape == (nb, T, nu) and K.shape == (nb, T, nu, nx)
