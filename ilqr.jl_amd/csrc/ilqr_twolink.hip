@@ -19,10 +19,10 @@
 //    backward pass that is parallel in time, and the FLOP-heavy one (≈3 kFLOP/step).
 //    Writes J = [A | B] (+ θ, u) to a [b][t][28] workspace: each lane of the
 //    sequential pass then reads its step's 224 contiguous bytes with 16-byte loads.
-//  * tl_backward: one lane per trajectory, the Riccati recursion in registers with
-//    the same exact step_back rewrite as the LQ kernels
-//    ([S s] = [Qxx | lx+Aᵀs] − Kᵀ((H+2μI)[K|d]); S computed as its upper triangle
-//    and mirrored, so it is symmetric by construction).
+//  * tl_backward: four trajectories per wave on the 4-block f64 MFMA (the LQ
+//    family's ilqr_bw4.hip layout), the same exact step_back rewrite as the LQ
+//    kernels ([S s] = [Qxx | lx+Aᵀs] − Kᵀ((H+2μI)[K|d]); S's upper triangle
+//    mirrored, so it is symmetric by construction).
 //  * tl_forward: one lane per trajectory, RK4 rollout + α-halving line search
 //    (src/forward_pass.jl:55-93), inputs of step t+1 prefetched during step t.
 // The sequential passes are latency-bound (one RK4 or one Riccati step per step per
@@ -32,6 +32,7 @@
 #include <math.h>
 
 #include "ilqr_internal.h"
+#include "ilqr_device.h"
 #include "ilqr_math.h"
 #include "../../include/ilqr.h"
 
@@ -42,7 +43,6 @@ constexpr int TL_NX = 4;
 constexpr int TL_NU = 2;
 constexpr int TL_NJ = TL_NX * (TL_NX + TL_NU);  // 24 entries of [A | B] per step
 constexpr int TL_NJR = TL_NJ + 4;                // + θ₁, θ₂, u₁, u₂: the backward's whole input
-constexpr int TL_BW_PF = 2;                      // backward prefetch depth (steps)
 constexpr int TL_FW_PF = 2;                      // forward prefetch depth (steps)
 
 // ---------------------------------------------------------------------------
@@ -245,163 +245,117 @@ __global__ __launch_bounds__(256) void tl_linearize_kernel(TwoLinkParams P, int 
 }
 
 // ---------------------------------------------------------------------------
-// Riccati recursion (src/backward_pass.jl:324-357), one lane per trajectory.
-struct TLBwIn {
-  double F[TL_NJ];  // [A | B], row-major 4×6
-  double th0, th1, u0, u1;
-};
-// Returns true if δu or K holds a NaN (the reference's @assert at :353-354).
-// ---------------------------------------------------------------------------
-__device__ bool tl_backward_lane(const TwoLinkParams& P, int b, int B, int T,
-                                 const double* __restrict__ x, const double* __restrict__ u,
-                                 const double* __restrict__ J, double* __restrict__ dg,
-                                 double* __restrict__ Kg, double mu) {
-  const double* xb = x + (size_t)b * (T + 1) * TL_NX;
-  // final_cost_quadratization (:134-153): ∇ℓ_f = [2(θ−θ*), 0, 0], ∇²ℓ_f = diag(2,2,0,0)
-  double S[4][4] = {};
-  double s[4];
-  S[0][0] = 2.0;
-  S[1][1] = 2.0;
-  s[0] = -2.0 * (P.tgt0 - xb[(size_t)T * TL_NX + 0]);
-  s[1] = -2.0 * (P.tgt1 - xb[(size_t)T * TL_NX + 1]);
-  s[2] = 0.0;
-  s[3] = 0.0;
-  bool bad = false;
+// Riccati recursion on the 4-block f64 MFMA (v_mfma_f64_4x4x4f64), FOUR trajectories
+// per wave — the layout of the LQ family's ilqr_bw4.hip: lane
+// 16ρ + 4β + κ holds element [ρ][κ] of slot β's 4×4 block, mfa(a, b, c) = c + aᵀb,
+// vectors are replicated blocks (v[ρ] in every κ). nx = 4 is one block; B (4×2) is
+// zero-padded to a block, so rows/columns 2, 3 of the u-side blocks are 0 (G, g, K,
+// d) and H's padding never meets a nonzero right-hand side. Per step: 13 MFMAs
+// (S·A, S·B, AᵀSA + lxx, BᵀSA, BᵀSB + luu, the gradient's Aᵀs and Bᵀs, two triangular
+// sweeps for each of G and g, the update of S and s) against ≈260 f64 VALU ops per
+// trajectory in tl_backward_lane.
+__device__ __forceinline__ double mfa(double a, double b, double c) {
+  return __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ double mfa_n(double a, double b, double c) {  // −aᵀb + c
+  return __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c, 0, 0, 1);
+}
+__device__ __forceinline__ double lane_perm2(double v, int src_byte) {
+  u2v p = __builtin_bit_cast(u2v, v);
+  p.x = (unsigned)__builtin_amdgcn_ds_bpermute(src_byte, (int)p.x);
+  p.y = (unsigned)__builtin_amdgcn_ds_bpermute(src_byte, (int)p.y);
+  return __builtin_bit_cast(double, p);
+}
 
-  const double* Jb = J + (size_t)b * T * TL_NJR;
-  // one step's record: [A | B] (24) then θ₁, θ₂, u₁, u₂ — 14 16-byte loads
-  auto load = [&](int t, TLBwIn& in) {
-    const double2* Jt = reinterpret_cast<const double2*>(Jb + (size_t)(t > 0 ? t : 0) * TL_NJR);
-#pragma unroll
-    for (int k = 0; k < TL_NJ / 2; ++k) {
-      const double2 v = Jt[k];
-      in.F[2 * k] = v.x;
-      in.F[2 * k + 1] = v.y;
-    }
-    const double2 th = Jt[TL_NJ / 2], uu = Jt[TL_NJ / 2 + 1];
-    in.th0 = th.x;
-    in.th1 = th.y;
-    in.u0 = uu.x;
-    in.u1 = uu.y;
+// Slots whose bit in `active` is clear, or past B, compute on clamped data and store
+// nothing. Returns the NaN slots (bit β). As in ilqr_bw4.hip, a NaN in any K_t or d_t
+// reaches K_0 or d_0, so only the last step's gains are tested.
+__device__ unsigned tl_backward4_wave(const TwoLinkParams& P, int b0, int B, unsigned active, int T,
+                                      const double* __restrict__ x, const double* __restrict__ J,
+                                      double* __restrict__ dg, double* __restrict__ Kg, double mu,
+                                      double* lds) {
+  b0 = __builtin_amdgcn_readfirstlane(b0);
+  const int l = threadIdx.x & 63;
+  const int rho = l >> 4, beta = (l >> 2) & 3, kap = l & 3;
+  const int b = b0 + beta;
+  const bool live = b < B && ((active >> beta) & 1u);
+  const int bc = b < B ? b : B - 1;
+  const int nslot = B - b0 < 4 ? B - b0 : 4;
+  const bool ru = rho < TL_NU;  // a real u row
+  const double tg = rho == 0 ? P.tgt0 : P.tgt1;
+
+  // final_cost_quadratization (:134-153): ∇²ℓ_f = lxx = diag(2,2,0,0), ∇ℓ_f = [2(θ−θ*), 0, 0]
+  const double lxx = (rho == kap && rho < 2) ? 2.0 : 0.0;  // also luu (pad rows 0)
+  double S = lxx;
+  const double xT = x[((size_t)bc * (T + 1) + T) * TL_NX + (rho < 2 ? rho : 0)];
+  double s = rho < 2 ? -2.0 * (tg - xT) : 0.0;
+
+  // per-step record J[b][t] = [A|B] (4×6 row-major), θ₁, θ₂, u₁, u₂ via one buffer
+  // resource over the wave's slots; the step is the scalar offset
+  const auto rJ = buffer_rsrc(const_cast<double*>(J) + (size_t)b0 * T * TL_NJR,
+                              (uint32_t)(nslot * T * TL_NJR * 8));
+  const uint32_t base = (uint32_t)(beta * T * TL_NJR * 8);
+  const uint32_t oA = base + (uint32_t)((rho * 6 + kap) * 8);
+  const uint32_t oB = kap < TL_NU ? base + (uint32_t)((rho * 6 + 4 + kap) * 8) : 0x80000000u;
+  const uint32_t oT = rho < 2 ? base + (uint32_t)((TL_NJ + rho) * 8) : 0x80000000u;
+  const uint32_t oU = rho < 2 ? base + (uint32_t)((TL_NJ + 2 + rho) * 8) : 0x80000000u;
+  auto ld = [&](uint32_t off, int t) {
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rJ, off, (uint32_t)(t * TL_NJR * 8), 0));
   };
-  auto step = [&](int t, const TLBwIn& in) {
-    // immediate_cost_quadratization (:81-109): lx = [2(θ−θ*), 0, 0], lu = 2u,
-    // lxx = diag(2,2,0,0), luu = 2I, lux = 0
-    // Y = S·F (4×6) and sF = sᵀF (1×6)
-    double Y[4][6], sF[6];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-#pragma unroll
-      for (int k = 0; k < 6; ++k) {
-        double acc = 0.0;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc = fma(S[i][j], in.F[j * 6 + k], acc);
-        Y[i][k] = acc;
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < 6; ++k) {
-      double acc = 0.0;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc = fma(s[j], in.F[j * 6 + k], acc);
-      sF[k] = acc;
-    }
-    // Z = FᵀY: Qxx = lxx + AᵀSA (upper), G = BᵀSA (2×4), H = luu + BᵀSB (2×2)
-    auto Z = [&](int a, int c) {
-      double acc = 0.0;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc = fma(in.F[j * 6 + a], Y[j][c], acc);
-      return acc;
-    };
-    double G[2][4], H[2][2], g[2];
-#pragma unroll
-    for (int a = 0; a < 2; ++a) {
-#pragma unroll
-      for (int c = 0; c < 4; ++c) G[a][c] = Z(4 + a, c);
-    }
-    H[0][0] = 2.0 + Z(4, 4);
-    H[0][1] = Z(4, 5);
-    H[1][1] = 2.0 + Z(5, 5);
-    H[1][0] = H[0][1];
-    g[0] = 2.0 * in.u0 + sF[4];  // optimal_controller_param (:181): g = lu + Bᵀs
-    g[1] = 2.0 * in.u1 + sF[5];
-    // feedback_parameters (:207-218): (H + μI)⁻¹ by LDLᵀ; δu = −H⁻¹g, K = −H⁻¹G
-    const double h00 = H[0][0] + mu, h01 = H[0][1], h11 = H[1][1] + mu;
-    const double iD0 = 1.0 / h00;
-    const double l10 = h01 * iD0;
-    const double iD1 = 1.0 / (h11 - l10 * h01);
-    auto solve = [&](double r0, double r1, double& z0, double& z1) {  // z = −(H+μI)⁻¹ r
-      const double w1 = (r1 - l10 * r0) * iD1;
-      z1 = -w1;
-      z0 = -(r0 * iD0 - l10 * w1);
-    };
-    double K[2][4], d[2];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) solve(G[0][c], G[1][c], K[0][c], K[1][c]);
-    solve(g[0], g[1], d[0], d[1]);
-    double* Kt = Kg + ((size_t)b * T + t) * TL_NU * TL_NX;
-    double* dt = dg + ((size_t)b * T + t) * TL_NU;
-#pragma unroll
-    for (int a = 0; a < 2; ++a) {
-      dt[a] = d[a];
-      bad |= d[a] != d[a];
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        Kt[a * 4 + c] = K[a][c];
-        bad |= K[a][c] != K[a][c];
-      }
-    }
-    // step_back (:262-273), exact rewrite: with W = (H+2μI)[K|d] = −[G|g] + μ[K|d],
-    //   S = lxx + AᵀSA − KᵀW_K,   s = lx + Aᵀs − KᵀW_d
-    double WK[2][4], Wd[2];
-#pragma unroll
-    for (int a = 0; a < 2; ++a) {
-#pragma unroll
-      for (int c = 0; c < 4; ++c) WK[a][c] = fma(mu, K[a][c], -G[a][c]);
-      Wd[a] = fma(mu, d[a], -g[a]);
-    }
-    double Sn[4][4], sn[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-#pragma unroll
-      for (int j = i; j < 4; ++j) {
-        double acc = Z(i, j);
-        if (i == j && i < 2) acc += 2.0;
-        acc = fma(-K[0][i], WK[0][j], acc);
-        acc = fma(-K[1][i], WK[1][j], acc);
-        Sn[i][j] = acc;
-        Sn[j][i] = acc;
-      }
-      double acc = sF[i];
-      if (i == 0) acc += -2.0 * (P.tgt0 - in.th0);
-      if (i == 1) acc += -2.0 * (P.tgt1 - in.th1);
-      acc = fma(-K[0][i], Wd[0], acc);
-      acc = fma(-K[1][i], Wd[1], acc);
-      sn[i] = acc;
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      s[i] = sn[i];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) S[i][j] = Sn[i][j];
-    }
-  };
-  // inputs of the next TL_BW_PF steps in flight (HBM latency ≈ one step's compute)
-  TLBwIn ring[TL_BW_PF];
-#pragma unroll
-  for (int k = 0; k < TL_BW_PF; ++k) load(T - 1 - k, ring[k]);
-  int t = T - 1;
-  for (; t >= TL_BW_PF - 1; t -= TL_BW_PF) {
-#pragma unroll
-    for (int k = 0; k < TL_BW_PF; ++k) {
-      step(t - k, ring[k]);
-      load(t - k - TL_BW_PF, ring[k]);
-    }
+  const auto rK = buffer_rsrc(Kg + (size_t)b0 * T * TL_NU * TL_NX, (uint32_t)(nslot * T * TL_NU * TL_NX * 8));
+  const auto rD = buffer_rsrc(dg + (size_t)b0 * T * TL_NU, (uint32_t)(nslot * T * TL_NU * 8));
+  const uint32_t kv = (live && ru) ? (uint32_t)((beta * T * TL_NU * TL_NX + rho * TL_NX + kap) * 8) : 0x80000000u;
+  const uint32_t dv = (live && ru && kap == 0) ? (uint32_t)((beta * T * TL_NU + rho) * 8) : 0x80000000u;
+  const int tr_src = (16 * kap + 4 * beta + rho) * 4;  // lane of element [κ][ρ]
+  double* Hl = lds + beta * 16;
+
+  double A = ld(oA, T - 1), Bm = ld(oB, T - 1), th = ld(oT, T - 1), uu = ld(oU, T - 1);
+  __builtin_amdgcn_s_waitcnt(0);
+  double Kl = 0.0, dl = 0.0;
+  for (int t = T - 1; t >= 0; --t) {
+    const int tn = t > 0 ? t - 1 : 0;
+    const double An = ld(oA, tn), Bn = ld(oB, tn), thn = ld(oT, tn), un = ld(oU, tn);
+    // immediate_cost_quadratization (:81-109): lx = [2(θ−θ*), 0, 0], lu = 2u
+    const double lx = rho < 2 ? -2.0 * (tg - th) : 0.0;
+    const double lu = ru ? 2.0 * uu : 0.0;
+    const double Y0 = mfa(S, A, 0.0), Y1 = mfa(S, Bm, 0.0);      // S·A, S·B
+    const double H = mfa(Bm, Y1, lxx);                            // luu + BᵀSB
+    Hl[rho * 4 + kap] = H;
+    const double Z = mfa(A, Y0, lxx);                             // lxx + AᵀSA
+    const double G = mfa(Bm, Y0, 0.0);                            // BᵀSA (lux = 0)
+    const double gx = mfa(A, s, lx), gu = mfa(Bm, s, lu);         // lx + Aᵀs, lu + Bᵀs
+    // feedback_parameters (:207-218): (H + μI) = L D Lᵀ on the 2×2 block, in every lane
+    wave_lds_fence();
+    const double h00 = Hl[0], h10 = Hl[4], h11 = Hl[5];
+    wave_lds_fence();
+    const double iD0 = rcp<2>(h00 + mu);
+    const double l10 = h10 * iD0;
+    const double iD1 = rcp<2>(fma(-l10, h10, h11 + mu));
+    // M = L⁻¹ = I − l10 e₁e₀ᵀ; this lane's M[κ][ρ] (A operand of M·) and
+    // D⁻¹[ρ]M[ρ][κ] (of (D⁻¹M)ᵀ·); padded pivots get D⁻¹ = 0 (their rows are 0)
+    const double eye = rho == kap ? 1.0 : 0.0;
+    const double Mt = (kap == 1 && rho == 0) ? -l10 : eye;
+    const double dsel = rho == 0 ? iD0 : (rho == 1 ? iD1 : 0.0);
+    const double Mnd = ((rho == 1 && kap == 0) ? -l10 : eye) * dsel;
+    const double K = mfa_n(Mnd, mfa(Mt, G, 0.0), 0.0);            // −(H+μI)⁻¹ G
+    const double d = mfa_n(Mnd, mfa(Mt, gu, 0.0), 0.0);           // −(H+μI)⁻¹ g
+    store_or_drop(K, rK, kv != 0x80000000u, kv + (uint32_t)(t * TL_NU * TL_NX * 8));
+    store_or_drop(d, rD, dv != 0x80000000u, dv + (uint32_t)(t * TL_NU * 8));
+    // step_back (:262-273), exact rewrite: W = (H+2μI)[K|d] = μ[K|d] − [G|g]
+    const double W = fma(mu, K, -G), Wd = fma(mu, d, -gu);
+    const double Sf = mfa_n(K, W, Z);                             // Qxx − KᵀW_K
+    // S as the reference's symmetric matrix: the upper triangle, mirrored
+    const double Sm = lane_perm2(Sf, tr_src);
+    S = rho <= kap ? Sf : Sm;
+    s = mfa_n(K, Wd, gx);                                         // lx + Aᵀs − KᵀW_d
+    A = An; Bm = Bn; th = thn; uu = un;
+    Kl = K; dl = d;
   }
+  const unsigned long long nb = __ballot(__builtin_isnan(Kl) || __builtin_isnan(dl));
+  unsigned r = 0;
 #pragma unroll
-  for (int k = 0; k < TL_BW_PF - 1; ++k)
-    if (t - k >= 0) step(t - k, ring[k]);
-  return bad;
+  for (int q = 0; q < 4; ++q) r |= (nb & ((0xFull << (4 * q)) * 0x0001000100010001ull)) ? (1u << q) : 0u;
+  return r;
 }
 
 // ---------------------------------------------------------------------------
@@ -523,18 +477,22 @@ __device__ TLFwdOut tl_forward_lane(const TwoLinkParams& P, int b, int T,
 // ---------------------------------------------------------------------------
 constexpr int TL_WG = 64;  // one wave per workgroup: B = 1024 spreads over 16 CUs
 
-__global__ __launch_bounds__(TL_WG) void tl_backward_kernel(TwoLinkParams P, int B, int T,
-                                                            const double* __restrict__ x,
-                                                            const double* __restrict__ u,
-                                                            const double* __restrict__ J,
-                                                            double* __restrict__ d,
-                                                            double* __restrict__ K,
-                                                            int32_t* __restrict__ status,
-                                                            double mu) {
-  const int b = blockIdx.x * TL_WG + threadIdx.x;
-  if (b >= B) return;
-  const bool nan = tl_backward_lane(P, b, B, T, x, u, J, d, K, mu);
-  if (status) status[b] = nan ? ILQR_TRAJ_NAN : ILQR_TRAJ_OK;
+// four trajectories per wave, four waves per workgroup
+constexpr int TL_BW4_WAVES = 4;
+__global__ __launch_bounds__(64 * TL_BW4_WAVES) void tl_backward_kernel(TwoLinkParams P, int B, int T,
+                                                                      const double* __restrict__ x,
+                                                                      const double* __restrict__ J,
+                                                                      double* __restrict__ d,
+                                                                      double* __restrict__ K,
+                                                                      int32_t* __restrict__ status,
+                                                                      double mu) {
+  __shared__ double lds[TL_BW4_WAVES * 64];
+  const int w = threadIdx.x >> 6;
+  const int b0 = (blockIdx.x * TL_BW4_WAVES + w) * 4;
+  if (b0 >= B) return;
+  const unsigned nan = tl_backward4_wave(P, b0, B, 0xFu, T, x, J, d, K, mu, lds + w * 64);
+  const int l = threadIdx.x & 63;
+  if (status && l < 4 && b0 + l < B) status[b0 + l] = ((nan >> l) & 1u) ? ILQR_TRAJ_NAN : ILQR_TRAJ_OK;
 }
 
 __global__ __launch_bounds__(TL_WG) void tl_forward_kernel(
@@ -557,15 +515,24 @@ __global__ __launch_bounds__(TL_WG) void tl_forward_kernel(
                                      : (r.cost != r.cost ? ILQR_TRAJ_NAN : ILQR_TRAJ_LS_EXHAUSTED);
 }
 
-// One fit iteration (forward_pass.jl:161-176): backward part (after tl_linearize).
-__global__ __launch_bounds__(TL_WG) void tl_iter_backward_kernel(TwoLinkParams P, int B, int T,
-                                                                 IterArgs a, const double* J,
-                                                                 double mu) {
-  const int b = blockIdx.x * TL_WG + threadIdx.x;
-  if (b >= B || a.status[b] != ILQR_TRAJ_OK) return;
-  if (tl_backward_lane(P, b, B, T, a.x, a.u, J, a.d, a.K, mu)) {
-    a.status[b] = ILQR_TRAJ_NAN;  // reference: AssertionError at backward_pass.jl:353
-    if (a.res_parity) a.res_parity[b] = a.parity;
+// One fit iteration (forward_pass.jl:161-176): backward part (after tl_linearize),
+// slots whose status is not OK computed on and never stored.
+__global__ __launch_bounds__(64 * TL_BW4_WAVES) void tl_iter_backward_kernel(TwoLinkParams P, int B, int T,
+                                                                           IterArgs a, const double* J,
+                                                                           double mu) {
+  __shared__ double lds[TL_BW4_WAVES * 64];
+  const int w = threadIdx.x >> 6;
+  const int b0 = (blockIdx.x * TL_BW4_WAVES + w) * 4;
+  if (b0 >= B) return;
+  unsigned active = 0;
+  for (int q = 0; q < 4; ++q)
+    if (b0 + q < B && a.status[b0 + q] == ILQR_TRAJ_OK) active |= 1u << q;
+  if (active == 0) return;
+  const unsigned nan = tl_backward4_wave(P, b0, B, active, T, a.x, J, a.d, a.K, mu, lds + w * 64) & active;
+  const int l = threadIdx.x & 63;
+  if (l < 4 && ((nan >> l) & 1u)) {
+    a.status[b0 + l] = ILQR_TRAJ_NAN;  // reference: AssertionError at backward_pass.jl:353
+    if (a.res_parity) a.res_parity[b0 + l] = a.parity;
   }
 }
 
@@ -634,7 +601,8 @@ hipError_t launch_tl_backward(const TwoLinkParams& P, int B, int T, const double
                               double mu, hipStream_t s) {
   hipError_t e = launch_linearize(P, B, T, x, u, nullptr, J, s);
   if (e != hipSuccess) return e;
-  tl_backward_kernel<<<(B + TL_WG - 1) / TL_WG, TL_WG, 0, s>>>(P, B, T, x, u, J, d, K, status, mu);
+  const int per_wg = 4 * TL_BW4_WAVES;
+  tl_backward_kernel<<<(B + per_wg - 1) / per_wg, 64 * TL_BW4_WAVES, 0, s>>>(P, B, T, x, J, d, K, status, mu);
   return hipGetLastError();
 }
 
@@ -653,7 +621,8 @@ hipError_t launch_tl_iteration(const TwoLinkParams& P, int B, int T, const IterA
                                const LSParams& ls, hipStream_t s) {
   hipError_t e = launch_linearize(P, B, T, a.x, a.u, a.status, J, s);
   if (e != hipSuccess) return e;
-  tl_iter_backward_kernel<<<(B + TL_WG - 1) / TL_WG, TL_WG, 0, s>>>(P, B, T, a, J, ls.mu);
+  const int per_wg = 4 * TL_BW4_WAVES;
+  tl_iter_backward_kernel<<<(B + per_wg - 1) / per_wg, 64 * TL_BW4_WAVES, 0, s>>>(P, B, T, a, J, ls.mu);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   tl_iter_forward_kernel<<<(B + TL_WG - 1) / TL_WG, TL_WG, 0, s>>>(P, B, T, a, ls);
   return hipGetLastError();
