@@ -140,6 +140,8 @@ template <int N, class V> struct ValueOf<DualT<N, V>> { using type = V; };
 template <class V, int NJ>
 struct ChainK {
   V R0[NJ][9];  // joint frame → parent body frame, row-major
+  V R0x[NJ][9];  // R0·[a]×   } so that R0·Rot(a, q) = c·R0 + s·R0x + (1−c)·R0aa
+  V R0aa[NJ][9]; // R0·a·aᵀ   } (Rodrigues expanded over the constant factors)
   V p[NJ][3];   // joint origin in the parent body frame
   V ax[NJ][3];  // unit axis (joint = child frame)
   V m[NJ];
@@ -164,10 +166,36 @@ __device__ __forceinline__ void crossc(const V (&a)[3], const S (&b)[3], S (&o)[
   o[2] = a[0] * b[1] - a[1] * b[0];
 }
 
-// parent → child coordinates of joint i: w_c = Rot(a, q)ᵀ R0ᵀ w_p (Rodrigues with −sin)
+// The joint transform R_i = R0_i Rot(a_i, q_i) (joint frame → parent body frame),
+// built once per evaluation from (cos q, sin q): 9 × 3 ops, after which each of the
+// recursion's 6 coordinate changes per joint is a 3×3 product (9 ops) instead of an
+// in-place Rodrigues rotation (≈28). v7; the v6 form rotated every vector.
 template <class S, class V, int NJ>
-__device__ __forceinline__ void to_child(const ChainK<V, NJ>& P, int i, const S& c, const S& s,
-                                         const S (&w)[3], S (&o)[3]) {
+__device__ __forceinline__ void joint_rot(const ChainK<V, NJ>& P, int i, const S& c, const S& s,
+                                          S (&R)[9]) {
+  const S omc = V(1) - c;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) R[k] = c * P.R0[i][k] + s * P.R0x[i][k] + omc * P.R0aa[i][k];
+}
+// parent → child coordinates: w_c = R_iᵀ w_p
+template <class S>
+__device__ __forceinline__ void to_child(const S (&R)[9], const S (&w)[3], S (&o)[3]) {
+#pragma unroll
+  for (int r = 0; r < 3; ++r) o[r] = R[r] * w[0] + R[3 + r] * w[1] + R[6 + r] * w[2];
+}
+// child → parent: w_p = R_i w_c
+template <class S>
+__device__ __forceinline__ void to_parent(const S (&R)[9], const S (&w)[3], S (&o)[3]) {
+#pragma unroll
+  for (int r = 0; r < 3; ++r) o[r] = R[3 * r] * w[0] + R[3 * r + 1] * w[1] + R[3 * r + 2] * w[2];
+}
+
+// The same coordinate changes as in-place Rodrigues rotations (no R_i): fewer
+// constants live at once, which the central-difference linearisation needs (its
+// kernel reads the chain from SGPRs, and R0x/R0aa there spill ~90 of them).
+template <class S, class V, int NJ>
+__device__ __forceinline__ void rod_to_child(const ChainK<V, NJ>& P, int i, const S& c, const S& s,
+                                             const S (&w)[3], S (&o)[3]) {
   S y[3];
 #pragma unroll
   for (int r = 0; r < 3; ++r) y[r] = P.R0[i][r] * w[0] + P.R0[i][3 + r] * w[1] + P.R0[i][6 + r] * w[2];
@@ -178,10 +206,9 @@ __device__ __forceinline__ void to_child(const ChainK<V, NJ>& P, int i, const S&
 #pragma unroll
   for (int r = 0; r < 3; ++r) o[r] = c * y[r] - s * axy[r] + P.ax[i][r] * k;
 }
-// child → parent: w_p = R0 Rot(a, q) w_c
 template <class S, class V, int NJ>
-__device__ __forceinline__ void to_parent(const ChainK<V, NJ>& P, int i, const S& c, const S& s,
-                                          const S (&w)[3], S (&o)[3]) {
+__device__ __forceinline__ void rod_to_parent(const ChainK<V, NJ>& P, int i, const S& c, const S& s,
+                                              const S (&w)[3], S (&o)[3]) {
   S axw[3];
   crossc(P.ax[i], w, axw);
   const S adw = P.ax[i][0] * w[0] + P.ax[i][1] * w[1] + P.ax[i][2] * w[2];
@@ -197,7 +224,7 @@ __device__ __forceinline__ void to_parent(const ChainK<V, NJ>& P, int i, const S
 // qd is read only when VEL; qdd[i] is the joint acceleration.
 // gs scales gravity (the lane-split forward runs the bias and the mass-matrix
 // columns as one uniform pass with per-lane q̇, q̈ and gravity; 1 elsewhere, folded)
-template <bool VEL, bool GRAV, int NJ, class S, class V>
+template <bool VEL, bool GRAV, bool ROT, int NJ, class S, class V>
 __device__ __forceinline__ void rnea(const ChainK<V, NJ>& P, const S (&c)[NJ], const S (&s)[NJ],
                                      const S (&qd)[NJ], const S (&qdd)[NJ], S (&tau)[NJ],
                                      V gs = V(1)) {
@@ -209,22 +236,32 @@ __device__ __forceinline__ void rnea(const ChainK<V, NJ>& P, const S (&c)[NJ], c
     al[r] = S(V(0));
     ac[r] = S(GRAV ? -P.g[r] * gs : V(0));  // fictitious base acceleration −g
   }
-  S fn[NJ][3], ff[NJ][3];
+  S fn[NJ][3], ff[NJ][3], R[ROT ? NJ : 1][9];
+  if constexpr (ROT) {
+#pragma unroll
+    for (int i = 0; i < NJ; ++i) joint_rot(P, i, c[i], s[i], R[i]);
+  }
+  auto tc = [&](int i, const S (&w)[3], S (&o)[3]) {
+    if constexpr (ROT) to_child(R[i], w, o); else rod_to_child(P, i, c[i], s[i], w, o);
+  };
+  auto tp = [&](int i, const S (&w)[3], S (&o)[3]) {
+    if constexpr (ROT) to_parent(R[i], w, o); else rod_to_parent(P, i, c[i], s[i], w, o);
+  };
 #pragma unroll
   for (int i = 0; i < NJ; ++i) {
     S t[3], u3[3];
     // spatial motion transform to body i: ω_i = X ω, v_i = X (v − p × ω) (same for accel)
     S wi[3], vi[3], ali[3], aci[3];
-    to_child(P, i, c[i], s[i], w, wi);
+    tc(i, w, wi);
     crossc(P.p[i], w, t);
 #pragma unroll
     for (int r = 0; r < 3; ++r) u3[r] = v[r] - t[r];
-    to_child(P, i, c[i], s[i], u3, vi);
-    to_child(P, i, c[i], s[i], al, ali);
+    tc(i, u3, vi);
+    tc(i, al, ali);
     crossc(P.p[i], al, t);
 #pragma unroll
     for (int r = 0; r < 3; ++r) u3[r] = ac[r] - t[r];
-    to_child(P, i, c[i], s[i], u3, aci);
+    tc(i, u3, aci);
     if constexpr (VEL) {
       S sq[3];
 #pragma unroll
@@ -284,8 +321,8 @@ __device__ __forceinline__ void rnea(const ChainK<V, NJ>& P, const S (&c)[NJ], c
     tau[i] = P.ax[i][0] * fn[i][0] + P.ax[i][1] * fn[i][1] + P.ax[i][2] * fn[i][2];
     if (i > 0) {
       S pf[3], pn[3], t[3];
-      to_parent(P, i, c[i], s[i], ff[i], pf);
-      to_parent(P, i, c[i], s[i], fn[i], pn);
+      tp(i, ff[i], pf);
+      tp(i, fn[i], pn);
       crossc(P.p[i], pf, t);
 #pragma unroll
       for (int r = 0; r < 3; ++r) {
@@ -298,7 +335,7 @@ __device__ __forceinline__ void rnea(const ChainK<V, NJ>& P, const S (&c)[NJ], c
 
 // [q̇; v̇] with v̇ = M \ (τ − bias)  (RBD_helper_functions.jl:61-66).
 // nu = NJ drives every joint; nu = 1 drives joint 1 only.
-template <int NJ, int NU, class S, class V>
+template <int NJ, int NU, bool ROT = true, class S, class V>
 __device__ __forceinline__ void chain_xdot(const ChainK<V, NJ>& P, const S (&x)[2 * NJ],
                                            const S (&u)[NU], S (&xd)[2 * NJ]) {
   S c[NJ], s[NJ];
@@ -310,14 +347,14 @@ __device__ __forceinline__ void chain_xdot(const ChainK<V, NJ>& P, const S (&x)[
     zero[i] = S(V(0));
     qd[i] = x[NJ + i];
   }
-  rnea<true, true>(P, c, s, qd, zero, b);  // dynamics_bias
+  rnea<true, true, ROT>(P, c, s, qd, zero, b);  // dynamics_bias
   S M[NJ][NJ];
 #pragma unroll
   for (int k = 0; k < NJ; ++k) {  // mass_matrix, column k = RNEA(q, 0, e_k)
     S e[NJ], col[NJ];
 #pragma unroll
     for (int j = 0; j < NJ; ++j) e[j] = S(V(j == k ? 1 : 0));
-    rnea<false, false>(P, c, s, zero, e, col);
+    rnea<false, false, ROT>(P, c, s, zero, e, col);
 #pragma unroll
     for (int i = 0; i < NJ; ++i) M[i][k] = col[i];
   }
@@ -358,7 +395,7 @@ __device__ __forceinline__ void chain_xdot(const ChainK<V, NJ>& P, const S (&x)[
 // separate passes), then gathered with lane shuffles; every lane of the group then
 // holds the same [q̇; v̇]. The forward rollout is a dependent chain per trajectory:
 // this cuts its latency per step to about a third at 4× the lanes.
-template <int NJ, int NU, class S, class V>
+template <int NJ, int NU, bool ROT = true, class S, class V>
 __device__ __forceinline__ void chain_xdot_split(const ChainK<V, NJ>& P, const S (&x)[2 * NJ],
                                                  const S (&u)[NU], S (&xd)[2 * NJ]) {
   static_assert(NJ + 1 <= 4, "one lane per pass in a group of 4");
@@ -371,7 +408,7 @@ __device__ __forceinline__ void chain_xdot_split(const ChainK<V, NJ>& P, const S
     qd[i] = role == 0 ? x[NJ + i] : S(V(0));
     qdd[i] = S(V(role == i + 1 ? 1 : 0));
   }
-  rnea<true, true>(P, c, s, qd, qdd, tau, V(role == 0 ? 1 : 0));
+  rnea<true, true, ROT>(P, c, s, qd, qdd, tau, V(role == 0 ? 1 : 0));
   S b[NJ], M[NJ][NJ];
 #pragma unroll
   for (int i = 0; i < NJ; ++i) {
@@ -409,15 +446,15 @@ __device__ __forceinline__ void chain_xdot_split(const ChainK<V, NJ>& P, const S
 }
 
 // RK4 (RBD_helper_functions.jl:70-78)
-template <int NJ, int NU, bool SPLIT = false, class S, class V>
+template <int NJ, int NU, bool SPLIT = false, bool ROT = true, class S, class V>
 __device__ __forceinline__ void chain_rk4(const ChainK<V, NJ>& P, const S (&x)[2 * NJ],
                                           const S (&u)[NU], S (&out)[2 * NJ]) {
   constexpr int NX = 2 * NJ;
   auto xdot = [](const ChainK<V, NJ>& Pc, const S (&xx)[2 * NJ], const S (&uu)[NU], S (&o)[2 * NJ]) {
     if constexpr (SPLIT)
-      chain_xdot_split<NJ, NU>(Pc, xx, uu, o);
+      chain_xdot_split<NJ, NU, ROT>(Pc, xx, uu, o);
     else
-      chain_xdot<NJ, NU>(Pc, xx, uu, o);
+      chain_xdot<NJ, NU, ROT>(Pc, xx, uu, o);
   };
   S k1[NX], k2[NX], k3[NX], k4[NX], y[NX];
   const V h = V(0.5);
@@ -536,8 +573,8 @@ __global__ __launch_bounds__(256) void chain_linearize_kernel(ChainK<V, NJ> P, i
 #pragma unroll
       for (int j = 0; j < NU; ++j)
         if (NX + j == k) { up[j] = zp; um[j] = zm; }
-      chain_rk4<NJ, NU>(P, xp, up, fp);
-      chain_rk4<NJ, NU>(P, xm, um, fm);
+      chain_rk4<NJ, NU, false, false>(P, xp, up, fp);
+      chain_rk4<NJ, NU, false, false>(P, xm, um, fm);
       const V inv = V(1) / (zp - zm);
 #pragma unroll
       for (int i = 0; i < NX; ++i) Jt[i * ND + k] = (fp[i] - fm[i]) * inv;
@@ -1014,6 +1051,21 @@ ilqr::ChainK<V, NJ> chain_consts(const ilqr_chain& c) {
   ilqr::ChainK<V, NJ> P{};
   for (int i = 0; i < NJ; ++i) {
     for (int k = 0; k < 9; ++k) P.R0[i][k] = (V)c.joint_rot[i][k];
+    {  // R0·[a]× and R0·a·aᵀ in fp64, then rounded (joint_rot)
+      const double* R0 = c.joint_rot[i];
+      const double* a = c.axis[i];
+      const double ax[9] = {0.0, -a[2], a[1], a[2], 0.0, -a[0], -a[1], a[0], 0.0};
+      for (int r = 0; r < 3; ++r)
+        for (int k = 0; k < 3; ++k) {
+          double x = 0.0, y = 0.0;
+          for (int j = 0; j < 3; ++j) {
+            x += R0[3 * r + j] * ax[3 * j + k];
+            y += R0[3 * r + j] * a[j] * a[k];
+          }
+          P.R0x[i][3 * r + k] = (V)x;
+          P.R0aa[i][3 * r + k] = (V)y;
+        }
+    }
     for (int k = 0; k < 3; ++k) {
       P.p[i][k] = (V)c.joint_pos[i][k];
       P.ax[i][k] = (V)c.axis[i][k];
