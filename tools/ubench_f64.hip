@@ -19,7 +19,21 @@ __global__ __launch_bounds__(256) void kern(double* out, long long* cyc, int ite
   long long t0 = __builtin_amdgcn_s_memtime();
   double res = 0;
   bool do_mfma = (MODE == 0) || (MODE == 2 && (wid & 1) == 0);
-  if (MODE == 4) {  // one wave: 8-acc 4x4x4_4b MFMAs with NACC dependent VALU fmas after each
+  if (MODE == 5) {  // one wave: 8-acc 4x4x4_4b MFMAs, each followed by NACC-1 fmas on 8 independent chains
+    double acc[8], c[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { acc[i] = 0.0; c[i] = 0.5 + lane + i; }
+    for (int it = 0; it < iters; ++it) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        acc[i] = __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, acc[i], 0, 0, 0);
+#pragma unroll
+        for (int r = 0; r < NACC - 1; ++r) c[(i + r) & 7] = __builtin_fma(c[(i + r) & 7], a, b);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) res += acc[i] + c[i];
+  } else if (MODE == 4) {  // one wave: 8-acc 4x4x4_4b MFMAs with NACC dependent VALU fmas after each
     double acc[8], c = 0.5 + lane;
 #pragma unroll
     for (int i = 0; i < 8; ++i) acc[i] = 0.0;
@@ -128,5 +142,8 @@ int main() {
   run<4, 2>("4x4x4 8 acc + 1 dep valu/mfma", 256, it / 8);
   run<4, 3>("4x4x4 8 acc + 2 dep valu/mfma", 256, it / 8);
   run<4, 5>("4x4x4 8 acc + 4 dep valu/mfma", 256, it / 8);
+  run<5, 2>("4x4x4 8 acc + 1 indep valu/mfma", 256, it / 8);
+  run<5, 3>("4x4x4 8 acc + 2 indep valu/mfma", 256, it / 8);
+  run<5, 5>("4x4x4 8 acc + 4 indep valu/mfma", 256, it / 8);
   return 0;
 }
