@@ -63,10 +63,14 @@ def test_selftest_lane_maps(gpu):
     assert selftest(0) == 0
 
 
+@pytest.mark.parametrize("backward", ["auto", "block"])
 @pytest.mark.parametrize("name", LQ_FIXTURES)
-def test_backward_matches_golden(gpu, name):
+def test_backward_matches_golden(gpu, name, backward):
+    """Golden gains through the default backward kernel (one trajectory per wave at
+    these batch sizes) and the four-trajectories-per-wave one."""
     g = load(name)
     s, _ = solver_for(g)
+    s.set_schedule(backward=backward)
     d, K, st = s.backward(dev(g["x"]), dev(g["u"]))
     assert (st.cpu().numpy() == 0).all()
     assert rel(K, g["K"]) < tol_gain(g), rel(K, g["K"])
@@ -87,11 +91,13 @@ def test_forward_matches_golden(gpu, name):
     assert np.array_equal(tr.cpu().numpy(), g["fw_trials"])
 
 
+@pytest.mark.parametrize("backward", ["auto", "block"])
 @pytest.mark.parametrize("name", LQ_FIXTURES)
-def test_fit_matches_golden(gpu, name):
+def test_fit_matches_golden(gpu, name, backward):
     g = load(name)
     meta = json.loads(str(g["meta"]))
     s, _ = solver_for(g)
+    s.set_schedule(backward=backward)
     xt = dev(g["xtraj"]) if "xtraj" in g else None
     r = s.fit(dev(g["x"]), dev(g["u"]), x_traj=xt, max_iter=meta["fit_max_iter"], tol=meta["tol"])
     assert r.call_status == 0
