@@ -808,20 +808,38 @@ __device__ ChainFwdOut<V> chain_forward_lane(const ChainK<V, NJ>& P, int b, int 
     for (int i = 0; i < NX; ++i) xb[i] = xb0[i];  // x̄₁ = x₁ (:65)
     V cost = V(0);
     du2 = V(0);
+    // step t's inputs (x_t, x_traj_t, K_t, u_t, δu_t) are loaded during step t − 1: a
+    // step is a few µs of dependent dynamics, so the loads land off the critical path
+    struct In { V xk[NX], xtk[NJ], K[NU * NX], u[NU], d[NU]; };
+    auto load = [&](int t, In& in) {
+#pragma unroll
+      for (int i = 0; i < NX; ++i) in.xk[i] = xb0[(size_t)t * NX + i];
+#pragma unroll
+      for (int i = 0; i < NJ; ++i) in.xtk[i] = xt0[(size_t)t * NX + i];
+#pragma unroll
+      for (int k = 0; k < NU * NX; ++k) in.K[k] = K0[(size_t)t * NU * NX + k];
+#pragma unroll
+      for (int a = 0; a < NU; ++a) {
+        in.u[a] = ub0[(size_t)t * NU + a];
+        in.d[a] = d0[(size_t)t * NU + a];
+      }
+    };
+    In cur;
+    load(0, cur);
     for (int t = 0; t < T; ++t) {
-      const V* xk = xb0 + (size_t)t * NX;
-      const V* xtk = xt0 + (size_t)t * NX;
+      In nxt;
+      load(t + 1 < T ? t + 1 : t, nxt);
       V dx[NX];
 #pragma unroll
-      for (int i = 0; i < NX; ++i) dx[i] = xb[i] - xk[i];  // δx (:72)
+      for (int i = 0; i < NX; ++i) dx[i] = xb[i] - cur.xk[i];  // δx (:72)
       V ubar[NU];
 #pragma unroll
       for (int a = 0; a < NU; ++a) {  // ūₖ = uₖ + α δuₖ + Kₖ δx (:73)
         V kdx = V(0);
 #pragma unroll
-        for (int i = 0; i < NX; ++i) kdx = fma(K0[((size_t)t * NU + a) * NX + i], dx[i], kdx);
-        const V uk = ub0[(size_t)t * NU + a];
-        ubar[a] = fma(alpha, d0[(size_t)t * NU + a], uk) + kdx;
+        for (int i = 0; i < NX; ++i) kdx = fma(cur.K[a * NX + i], dx[i], kdx);
+        const V uk = cur.u[a];
+        ubar[a] = fma(alpha, cur.d[a], uk) + kdx;
         const V e = ubar[a] - uk;
         du2 = fma(e, e, du2);
       }
@@ -829,7 +847,7 @@ __device__ ChainFwdOut<V> chain_forward_lane(const ChainK<V, NJ>& P, int b, int 
       V lk = V(0);
 #pragma unroll
       for (int i = 0; i < NJ; ++i) {
-        const V e = P.tgt[i] - fma(-xtw, xtk[i], xb[i]);
+        const V e = P.tgt[i] - fma(-xtw, cur.xtk[i], xb[i]);
         lk = fma(P.qw[i] * e, e, lk);
       }
 #pragma unroll
@@ -845,6 +863,7 @@ __device__ ChainFwdOut<V> chain_forward_lane(const ChainK<V, NJ>& P, int b, int 
       chain_rk4<NJ, NU, SPLIT>(P, xb, ubar, xn);  // x̄ₖ₊₁ = f(x̄ₖ, ūₖ) (:74)
 #pragma unroll
       for (int i = 0; i < NX; ++i) xb[i] = xn[i];
+      cur = nxt;
     }
 #pragma unroll
     for (int i = 0; i < NX; ++i)
