@@ -31,6 +31,7 @@
 
 #include "../../include/ilqr.h"
 #include "ilqr_internal.h"
+#include "ilqr_device.h"
 #include "ilqr_math.h"
 
 namespace ilqr {
@@ -908,6 +909,129 @@ struct ChainIter {
   int iter;
 };
 
+// ---------------------------------------------------------------------------
+// Riccati recursion of the 2-joint chain (nx = 4, nu ≤ 2) on the 4-block f64 MFMA,
+// four trajectories per wave: the 2-link family's tl_backward4_wave (ilqr_twolink.hip,
+// DESIGN.md §4) with the chain's weighted joint-space cost (RBD_helper_functions.jl:
+// 85-116: lxx = diag(2qw, 0), luu = diag(2rw), lx = −2qw(θ* − θ), lu = 2rw·u, final
+// diag(2qfw, 0) and −2qfw(θ* − θ_N)). The recursion runs in f64 whatever V is (the
+// fp32 family's records and gains are converted at the load/store): one rounding of
+// the gains to fp32 instead of fp32 arithmetic throughout.
+template <class V>
+__device__ __forceinline__ double ch_ld(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+  if constexpr (sizeof(V) == 4)
+    return (double)__builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
+  else
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0));
+}
+template <class V>
+__device__ __forceinline__ void ch_st(double v, __amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+  if constexpr (sizeof(V) == 4)
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, (float)v), r, voff, soff, 0);
+  else
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, v), r, voff, soff, 0);
+}
+__device__ __forceinline__ double ch_mf(double a, double b, double c) {  // c + aᵀb
+  return __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ double ch_mfn(double a, double b, double c) {  // c − aᵀb
+  return __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c, 0, 0, 1);
+}
+constexpr int CH_BW4_PF = 4;  // record prefetch depth (steps)
+
+template <class V, int NU>
+__device__ unsigned chain_backward4_wave(const ChainK<V, 2>& P, int b0, int B, unsigned active, int T,
+                                         const V* __restrict__ x, const V* __restrict__ J,
+                                         V* __restrict__ dg, V* __restrict__ Kg, double mu,
+                                         double* lds) {
+  constexpr int NJ = 2, NX = 4, ND = NX + NU, NR = Rec<NJ, NU>::N, NJAC = Rec<NJ, NU>::NJAC;
+  constexpr uint32_t DEAD = 0x80000000u, W = sizeof(V);
+  b0 = __builtin_amdgcn_readfirstlane(b0);
+  const int l = threadIdx.x & 63;
+  const int rho = l >> 4, beta = (l >> 2) & 3, kap = l & 3;
+  const int b = b0 + beta;
+  const bool live = b < B && ((active >> beta) & 1u);
+  const int bc = b < B ? b : B - 1;
+  const int nslot = B - b0 < 4 ? B - b0 : 4;
+  const bool rj = rho < NJ, ru = rho < NU;
+  const int jr = rj ? rho : 0;
+  const double tg = (double)P.tgt[jr], qw2 = 2.0 * (double)P.qw[jr], qfw2 = 2.0 * (double)P.qfw[jr];
+  const double rw2 = ru ? 2.0 * (double)P.rw[rho < NU ? rho : 0] : 0.0;
+  const double lxx = (rho == kap && rj) ? qw2 : 0.0;
+  const double luu = (rho == kap && ru) ? rw2 : 0.0;
+  double S = (rho == kap && rj) ? qfw2 : 0.0;
+  const double xT = (double)x[((size_t)bc * (T + 1) + T) * NX + jr];
+  double s = rj ? -qfw2 * (tg - xT) : 0.0;
+
+  const auto rJ = buffer_rsrc(const_cast<V*>(J) + (size_t)b0 * T * NR, (uint32_t)(nslot * T * NR * W));
+  const uint32_t base = (uint32_t)(beta * T * NR * W);
+  const uint32_t oA = base + (uint32_t)((rho * ND + kap) * W);
+  const uint32_t oB = kap < NU ? base + (uint32_t)((rho * ND + NX + kap) * W) : DEAD;
+  const uint32_t oT = rj ? base + (uint32_t)((NJAC + rho) * W) : DEAD;
+  const uint32_t oU = ru ? base + (uint32_t)((NJAC + NX + rho) * W) : DEAD;
+  const auto rK = buffer_rsrc(Kg + (size_t)b0 * T * NU * NX, (uint32_t)(nslot * T * NU * NX * W));
+  const auto rD = buffer_rsrc(dg + (size_t)b0 * T * NU, (uint32_t)(nslot * T * NU * W));
+  const uint32_t kv = (live && ru) ? (uint32_t)((beta * T * NU * NX + rho * NX + kap) * W) : DEAD;
+  const uint32_t dv = (live && ru && kap == 0) ? (uint32_t)((beta * T * NU + rho) * W) : DEAD;
+  const int tr_src = (16 * kap + 4 * beta + rho) * 4;
+  double* Hl = lds + beta * 16;
+
+  constexpr int PF = CH_BW4_PF;
+  double rA[PF], rB[PF], rT[PF], rU[PF];
+  auto ld = [&](uint32_t off, int t) { return ch_ld<V>(rJ, off, (uint32_t)(t * NR * W)); };
+#pragma unroll
+  for (int k = 0; k < PF; ++k) {
+    const int tk = T - 1 - k > 0 ? T - 1 - k : 0;
+    rA[k] = ld(oA, tk); rB[k] = ld(oB, tk); rT[k] = ld(oT, tk); rU[k] = ld(oU, tk);
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+  double Kl = 0.0, dl = 0.0;
+  auto step = [&](int t, int k) {
+    const double A = rA[k], Bm = rB[k], th = rT[k], uu = rU[k];
+    const int tn = t - PF > 0 ? t - PF : 0;
+    rA[k] = ld(oA, tn); rB[k] = ld(oB, tn); rT[k] = ld(oT, tn); rU[k] = ld(oU, tn);
+    const double lx = rj ? -qw2 * (tg - th) : 0.0;
+    const double lu = rw2 * uu;
+    const double Y0 = ch_mf(S, A, 0.0), Y1 = ch_mf(S, Bm, 0.0);
+    const double H = ch_mf(Bm, Y1, luu);                          // luu + BᵀSB
+    Hl[rho * 4 + kap] = H;
+    const double Z = ch_mf(A, Y0, lxx);                           // lxx + AᵀSA
+    const double G = ch_mf(Bm, Y0, 0.0);                          // BᵀSA
+    const double gx = ch_mf(A, s, lx), gu = ch_mf(Bm, s, lu);     // lx + Aᵀs, lu + Bᵀs
+    wave_lds_fence();
+    const double h00 = Hl[0], h10 = Hl[4], h11 = Hl[5];
+    wave_lds_fence();
+    // (H + μI)⁻¹ on the (≤ 2) × (≤ 2) u block by its adjugate (H = luu + O(Δt²)BᵀSB)
+    const double a00 = h00 + mu, a11 = h11 + mu;
+    const double idet = rcp<2>(fma(a00, a11, -h10 * h10));
+    const bool in2 = rho < 2 && kap < 2;
+    const double Hi = !in2 ? 0.0 : (rho != kap ? -h10 : (rho == 0 ? a11 : a00)) * idet;
+    const double K = ch_mfn(Hi, G, 0.0), d = ch_mfn(Hi, gu, 0.0);
+    ch_st<V>(K, rK, kv, kv == DEAD ? 0u : (uint32_t)(t * NU * NX * W));
+    ch_st<V>(d, rD, dv, dv == DEAD ? 0u : (uint32_t)(t * NU * W));
+    const double Wk = fma(mu, K, -G), Wd = fma(mu, d, -gu);
+    const double Sf = ch_mfn(K, Wk, Z);
+    const double Sm = __builtin_bit_cast(double, u2v{(unsigned)__builtin_amdgcn_ds_bpermute(tr_src, (int)__builtin_bit_cast(u2v, Sf).x),
+                                                     (unsigned)__builtin_amdgcn_ds_bpermute(tr_src, (int)__builtin_bit_cast(u2v, Sf).y)});
+    S = rho <= kap ? Sf : Sm;                                      // upper triangle, mirrored
+    s = ch_mfn(K, Wd, gx);
+    Kl = K; dl = d;
+  };
+  int t = T - 1;
+  for (; t >= PF - 1; t -= PF) {
+#pragma unroll
+    for (int k = 0; k < PF; ++k) step(t - k, k);
+  }
+#pragma unroll
+  for (int k = 0; k < PF - 1; ++k)
+    if (t - k >= 0) step(t - k, k);
+  const unsigned long long nb = __ballot(__builtin_isnan(Kl) || __builtin_isnan(dl));
+  unsigned r = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) r |= (nb & ((0xFull << (4 * q)) * 0x0001000100010001ull)) ? (1u << q) : 0u;
+  return r;
+}
+
 constexpr int CH_WG = 64;
 
 template <class V, int NJ, int NU>
@@ -924,6 +1048,22 @@ __global__ __launch_bounds__(CH_WG) void chain_backward_kernel(ChainK<V, NJ> P, 
 
 // lanes per trajectory of the forward kernels: 4 with the lane-split dynamics
 constexpr int CH_FW_LANES = 4;
+
+// four trajectories per wave, four waves per workgroup (2-joint chains)
+template <class V, int NU>
+__global__ __launch_bounds__(256) void chain_backward4_kernel(ChainK<V, 2> P, int B, int T,
+                                                              const V* __restrict__ x,
+                                                              const V* __restrict__ J,
+                                                              V* __restrict__ d, V* __restrict__ K,
+                                                              int32_t* __restrict__ status, V mu) {
+  __shared__ double lds[4 * 64];
+  const int w = threadIdx.x >> 6;
+  const int b0 = (blockIdx.x * 4 + w) * 4;
+  if (b0 >= B) return;
+  const unsigned nan = chain_backward4_wave<V, NU>(P, b0, B, 0xFu, T, x, J, d, K, (double)mu, lds + w * 64);
+  const int l = threadIdx.x & 63;
+  if (status && l < 4 && b0 + l < B) status[b0 + l] = ((nan >> l) & 1u) ? ILQR_TRAJ_NAN : ILQR_TRAJ_OK;
+}
 
 template <class V, int NJ, int NU>
 __global__ __launch_bounds__(CH_WG) void chain_forward_kernel(
@@ -961,6 +1101,28 @@ __global__ __launch_bounds__(CH_WG) void chain_iter_backward_kernel(ChainK<V, NJ
   if (chain_backward_lane<V, NJ, NU>(P, b, T, a.x, J, a.d, a.K, mu)) {
     a.status[b] = ILQR_TRAJ_NAN;  // reference: AssertionError at backward_pass.jl:353
     if (a.res_parity) a.res_parity[b] = a.parity;
+  }
+}
+
+// fit iteration, backward part, 2-joint chains: slots whose status is not OK are
+// computed on and never stored
+template <class V, int NU>
+__global__ __launch_bounds__(256) void chain_iter_backward4_kernel(ChainK<V, 2> P, int B, int T,
+                                                                   ChainIter<V> a, const V* J, V mu) {
+  __shared__ double lds[4 * 64];
+  const int w = threadIdx.x >> 6;
+  const int b0 = (blockIdx.x * 4 + w) * 4;
+  if (b0 >= B) return;
+  unsigned active = 0;
+  for (int q = 0; q < 4; ++q)
+    if (b0 + q < B && a.status[b0 + q] == ILQR_TRAJ_OK) active |= 1u << q;
+  if (active == 0) return;
+  const unsigned nan =
+      chain_backward4_wave<V, NU>(P, b0, B, active, T, a.x, J, a.d, a.K, (double)mu, lds + w * 64) & active;
+  const int l = threadIdx.x & 63;
+  if (l < 4 && ((nan >> l) & 1u)) {
+    a.status[b0 + l] = ILQR_TRAJ_NAN;  // reference: AssertionError at backward_pass.jl:353
+    if (a.res_parity) a.res_parity[b0 + l] = a.parity;
   }
 }
 
@@ -1154,6 +1316,11 @@ struct ChainOps {
     hipError_t e = linearize(h, x, u, nullptr);
     if (e != hipSuccess) return e;
     const auto P = chain_consts<V, NJ>(h->chain);
+    if constexpr (NJ == 2) {  // four trajectories per wave on the f64 MFMA
+      ilqr::chain_backward4_kernel<V, NU><<<(h->batch + 15) / 16, 256, 0, h->stream>>>(
+          P, h->batch, h->T, x, (const V*)h->J, d, K, st, (V)mu);
+      return hipGetLastError();
+    }
     ilqr::chain_backward_kernel<V, NJ, NU><<<(h->batch + ilqr::CH_WG - 1) / ilqr::CH_WG, ilqr::CH_WG,
                                              0, h->stream>>>(P, h->batch, h->T, x, (const V*)h->J,
                                                              d, K, st, (V)mu);
@@ -1172,9 +1339,14 @@ struct ChainOps {
     hipError_t e = linearize(h, a.x, a.u, a.status);
     if (e != hipSuccess) return e;
     const auto P = chain_consts<V, NJ>(h->chain);
-    const int g = (h->batch + ilqr::CH_WG - 1) / ilqr::CH_WG;
-    ilqr::chain_iter_backward_kernel<V, NJ, NU>
-        <<<g, ilqr::CH_WG, 0, h->stream>>>(P, h->batch, h->T, a, (const V*)h->J, (V)ls.mu);
+    if constexpr (NJ == 2) {
+      ilqr::chain_iter_backward4_kernel<V, NU>
+          <<<(h->batch + 15) / 16, 256, 0, h->stream>>>(P, h->batch, h->T, a, (const V*)h->J, (V)ls.mu);
+    } else {
+      const int g = (h->batch + ilqr::CH_WG - 1) / ilqr::CH_WG;
+      ilqr::chain_iter_backward_kernel<V, NJ, NU>
+          <<<g, ilqr::CH_WG, 0, h->stream>>>(P, h->batch, h->T, a, (const V*)h->J, (V)ls.mu);
+    }
     if ((e = hipGetLastError()) != hipSuccess) return e;
     const int gf = (h->batch * ilqr::CH_FW_LANES + ilqr::CH_WG - 1) / ilqr::CH_WG;
     ilqr::chain_iter_forward_kernel<V, NJ, NU><<<gf, ilqr::CH_WG, 0, h->stream>>>(P, h->batch, h->T,
