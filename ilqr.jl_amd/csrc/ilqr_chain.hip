@@ -446,6 +446,156 @@ __device__ __forceinline__ void chain_xdot_split(const ChainK<V, NJ>& P, const S
   }
 }
 
+// ---------------------------------------------------------------------------
+// Component-parallel Newton-Euler (v7 forward): a 16-lane group per trajectory,
+// lane 4·role + c. The role picks the pass (0: bias with q̇ and gravity, k+1: M's
+// column k), c ∈ {0,1,2} holds component c of every 3-vector (lane 3 of each quad
+// computes a copy of component 0 and is never read). Cross products, rotations and
+// dot products reach the other components of the same quad through DPP quad
+// permutations, so each lane issues about a third of the scalar pass's arithmetic;
+// the arithmetic per component is the scalar pass's, in the same order up to the
+// association of three-term sums.
+// ---------------------------------------------------------------------------
+template <int CTRL, class V>
+__device__ __forceinline__ V qperm(V x) {  // quad_perm DPP move
+  if constexpr (sizeof(V) == 4) {
+    return __builtin_bit_cast(V, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), CTRL, 0xF, 0xF, false));
+  } else {
+    const u2v p = __builtin_bit_cast(u2v, x);
+    const u2v q = {(unsigned)__builtin_amdgcn_mov_dpp((int)p.x, CTRL, 0xF, 0xF, false),
+                   (unsigned)__builtin_amdgcn_mov_dpp((int)p.y, CTRL, 0xF, 0xF, false)};
+    return __builtin_bit_cast(V, q);
+  }
+}
+constexpr int QP_B0 = 0x00, QP_B1 = 0x55, QP_B2 = 0xAA;  // broadcast component k
+constexpr int QP_R1 = 0xC9, QP_R2 = 0xD2;                // component c+1 / c+2 (mod 3)
+template <class V> __device__ __forceinline__ V bc0(V x) { return qperm<QP_B0>(x); }
+template <class V> __device__ __forceinline__ V bc1(V x) { return qperm<QP_B1>(x); }
+template <class V> __device__ __forceinline__ V bc2(V x) { return qperm<QP_B2>(x); }
+template <class V> __device__ __forceinline__ V r1(V x) { return qperm<QP_R1>(x); }
+template <class V> __device__ __forceinline__ V r2(V x) { return qperm<QP_R2>(x); }
+// (a × b)_c = a_{c+1} b_{c+2} − a_{c+2} b_{c+1}
+template <class V> __device__ __forceinline__ V cv_cross(V a, V b) { return r1(a) * r2(b) - r2(a) * r1(b); }
+// constant a: the lane holds a1 = a_{c+1}, a2 = a_{c+2}
+template <class V> __device__ __forceinline__ V cv_crossc(V a1, V a2, V b) { return a1 * r2(b) - a2 * r1(b); }
+// Σ_k m_k w_k with m_k the lane's row (m[c][k]) or column entries
+template <class V> __device__ __forceinline__ V cv_mat(V m0, V m1, V m2, V w) {
+  return m0 * bc0(w) + m1 * bc1(w) + m2 * bc2(w);
+}
+
+template <bool VEL, bool GRAV, int NJ, class V>
+__device__ __forceinline__ void rnea_cv(const ChainK<V, NJ>& P, const V (&c)[NJ], const V (&s)[NJ],
+                                        const V (&qd)[NJ], const V (&qdd)[NJ], V (&tau)[NJ], V gs,
+                                        int cmp) {
+  const int c0 = cmp < 3 ? cmp : 0;
+  const int c1 = c0 == 2 ? 0 : c0 + 1, c2 = c0 == 0 ? 2 : c0 - 1;
+  V w = V(0), v = V(0), al = V(0), ac = GRAV ? -P.g[c0] * gs : V(0);
+  V fn[NJ], ff[NJ], Rr[NJ][3], Rc[NJ][3];
+#pragma unroll
+  for (int i = 0; i < NJ; ++i) {  // row c and column c of R_i = R0 Rot(a, q)
+    const V omc = V(1) - c[i];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      Rr[i][k] = c[i] * P.R0[i][3 * c0 + k] + s[i] * P.R0x[i][3 * c0 + k] + omc * P.R0aa[i][3 * c0 + k];
+      Rc[i][k] = c[i] * P.R0[i][3 * k + c0] + s[i] * P.R0x[i][3 * k + c0] + omc * P.R0aa[i][3 * k + c0];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < NJ; ++i) {
+    const V p1 = P.p[i][c1], p2 = P.p[i][c2], mc1 = P.mc[i][c1], mc2 = P.mc[i][c2];
+    const V axc = P.ax[i][c0];
+    // to_child: w_c = Σ_k R[k][c] w_k
+    V wi = cv_mat(Rc[i][0], Rc[i][1], Rc[i][2], w);
+    V vi = cv_mat(Rc[i][0], Rc[i][1], Rc[i][2], v - cv_crossc(p1, p2, w));
+    V ali = cv_mat(Rc[i][0], Rc[i][1], Rc[i][2], al);
+    V aci = cv_mat(Rc[i][0], Rc[i][1], Rc[i][2], ac - cv_crossc(p1, p2, al));
+    if constexpr (VEL) {
+      const V sq = axc * qd[i];
+      wi = wi + sq;
+      ali = ali + cv_cross(wi, sq);
+      aci = aci + cv_cross(vi, sq);
+    }
+    ali = ali + axc * qdd[i];
+    fn[i] = cv_mat(P.Io[i][3 * c0], P.Io[i][3 * c0 + 1], P.Io[i][3 * c0 + 2], ali) + cv_crossc(mc1, mc2, aci);
+    ff[i] = P.m[i] * aci - cv_crossc(mc1, mc2, ali);
+    if constexpr (VEL) {
+      const V hn = cv_mat(P.Io[i][3 * c0], P.Io[i][3 * c0 + 1], P.Io[i][3 * c0 + 2], wi) + cv_crossc(mc1, mc2, vi);
+      const V hf = P.m[i] * vi - cv_crossc(mc1, mc2, wi);
+      fn[i] = fn[i] + cv_cross(wi, hn);
+      fn[i] = fn[i] + cv_cross(vi, hf);
+      ff[i] = ff[i] + cv_cross(wi, hf);
+    }
+    w = wi;
+    v = vi;
+    al = ali;
+    ac = aci;
+  }
+#pragma unroll
+  for (int i = NJ - 1; i >= 0; --i) {
+    const V pr = P.ax[i][c0] * fn[i];  // S_iᵀ f_i over the three components
+    tau[i] = (bc0(pr) + bc1(pr)) + bc2(pr);
+    if (i > 0) {
+      const V pf = cv_mat(Rr[i][0], Rr[i][1], Rr[i][2], ff[i]);  // to_parent: Σ_k R[c][k] f_k
+      const V pn = cv_mat(Rr[i][0], Rr[i][1], Rr[i][2], fn[i]);
+      fn[i - 1] = fn[i - 1] + (pn + cv_crossc(P.p[i][c1], P.p[i][c2], pf));
+      ff[i - 1] = ff[i - 1] + pf;
+    }
+  }
+}
+
+// chain_xdot over a 16-lane group: role = pass, c = component (see rnea_cv); every
+// lane of the group ends with the same [q̇; v̇]
+template <int NJ, int NU, class V>
+__device__ __forceinline__ void chain_xdot_cv(const ChainK<V, NJ>& P, const V (&x)[2 * NJ],
+                                              const V (&u)[NU], V (&xd)[2 * NJ]) {
+  static_assert(NJ + 1 <= 4, "one role per pass in a group of 16");
+  const int l16 = threadIdx.x & 15;
+  const int role = l16 >> 2, cmp = l16 & 3;
+  const int base = (threadIdx.x & 63) & ~15;
+  V c[NJ], s[NJ], qd[NJ], qdd[NJ], tau[NJ];
+#pragma unroll
+  for (int i = 0; i < NJ; ++i) {
+    scs(x[i], s[i], c[i]);
+    qd[i] = role == 0 ? x[NJ + i] : V(0);
+    qdd[i] = V(role == i + 1 ? 1 : 0);
+  }
+  rnea_cv<true, true>(P, c, s, qd, qdd, tau, V(role == 0 ? 1 : 0), cmp);
+  V b[NJ], M[NJ][NJ];
+#pragma unroll
+  for (int i = 0; i < NJ; ++i) {
+    b[i] = __shfl(tau[i], base);
+#pragma unroll
+    for (int k = 0; k < NJ; ++k) M[i][k] = __shfl(tau[i], base + 4 * (1 + k));
+  }
+  V r[NJ];
+#pragma unroll
+  for (int i = 0; i < NJ; ++i) r[i] = (i < NU ? u[i < NU ? i : 0] : V(0)) - b[i];
+#pragma unroll
+  for (int k = 0; k < NJ; ++k) {
+    const V inv = V(1) / M[k][k];
+#pragma unroll
+    for (int i = k + 1; i < NJ; ++i) {
+      const V lk = M[i][k] * inv;
+#pragma unroll
+      for (int j = k + 1; j < NJ; ++j) M[i][j] = M[i][j] - lk * M[k][j];
+      r[i] = r[i] - lk * r[k];
+    }
+  }
+  V q2[NJ];
+#pragma unroll
+  for (int i = NJ - 1; i >= 0; --i) {
+    V acc = r[i];
+#pragma unroll
+    for (int j = i + 1; j < NJ; ++j) acc = acc - M[i][j] * q2[j];
+    q2[i] = acc * (V(1) / M[i][i]);
+  }
+#pragma unroll
+  for (int i = 0; i < NJ; ++i) {
+    xd[i] = x[NJ + i];
+    xd[NJ + i] = q2[i];
+  }
+}
+
 // RK4 (RBD_helper_functions.jl:70-78)
 template <int NJ, int NU, bool SPLIT = false, bool ROT = true, class S, class V>
 __device__ __forceinline__ void chain_rk4(const ChainK<V, NJ>& P, const S (&x)[2 * NJ],
@@ -453,7 +603,7 @@ __device__ __forceinline__ void chain_rk4(const ChainK<V, NJ>& P, const S (&x)[2
   constexpr int NX = 2 * NJ;
   auto xdot = [](const ChainK<V, NJ>& Pc, const S (&xx)[2 * NJ], const S (&uu)[NU], S (&o)[2 * NJ]) {
     if constexpr (SPLIT)
-      chain_xdot_split<NJ, NU, ROT>(Pc, xx, uu, o);
+      chain_xdot_cv<NJ, NU>(Pc, xx, uu, o);
     else
       chain_xdot<NJ, NU, ROT>(Pc, xx, uu, o);
   };
@@ -790,7 +940,7 @@ __device__ ChainFwdOut<V> chain_forward_lane(const ChainK<V, NJ>& P, int b, int 
                                              V* __restrict__ xnew, V* __restrict__ unew, V* du2_out,
                                              const LSParams& ls) {
   constexpr int NX = 2 * NJ;
-  const bool writer = !SPLIT || (threadIdx.x & 3) == 0;  // SPLIT: one lane of the group stores
+  const bool writer = !SPLIT || (threadIdx.x & 15) == 0;  // SPLIT: one lane of the group stores
   const V* xb0 = x + (size_t)b * (T + 1) * NX;
   const V* ub0 = u + (size_t)b * T * NU;
   const V* xt0 = (xtraj ? xtraj : x) + (size_t)b * (T + 1) * NX;
@@ -1047,7 +1197,7 @@ __global__ __launch_bounds__(CH_WG) void chain_backward_kernel(ChainK<V, NJ> P, 
 }
 
 // lanes per trajectory of the forward kernels: 4 with the lane-split dynamics
-constexpr int CH_FW_LANES = 4;
+constexpr int CH_FW_LANES = 16;  // lanes per trajectory in the forward (chain_xdot_cv)
 
 // four trajectories per wave, four waves per workgroup (2-joint chains)
 template <class V, int NU>
@@ -1082,7 +1232,7 @@ __global__ __launch_bounds__(CH_WG) void chain_forward_kernel(
   const V pc = prev_cost ? prev_cost[b] : V(INFINITY);
   const ChainFwdOut<V> r =
       chain_forward_lane<V, NJ, NU, true>(Ps, b, T, x, u, xtraj, d, K, pc, xnew, unew, nullptr, ls);
-  if ((threadIdx.x & 3) != 0) return;
+  if ((threadIdx.x & 15) != 0) return;
   if (!r.accepted) {  // exhausted (the reference would loop forever): return the inputs
     for (int i = 0; i < (T + 1) * NX; ++i) xnew[(size_t)b * (T + 1) * NX + i] = x[(size_t)b * (T + 1) * NX + i];
     for (int i = 0; i < T * NU; ++i) unew[(size_t)b * T * NU + i] = u[(size_t)b * T * NU + i];
@@ -1142,7 +1292,7 @@ __global__ __launch_bounds__(CH_WG) void chain_iter_forward_kernel(ChainK<V, NJ>
   const V pc = a.prev_cost ? a.prev_cost[b] : V(INFINITY);
   const ChainFwdOut<V> r = chain_forward_lane<V, NJ, NU, true>(Ps, b, T, a.x, a.u, a.xtraj, a.d,
                                                                a.K, pc, a.xnew, a.unew, &du2, ls);
-  if ((threadIdx.x & 3) != 0) return;
+  if ((threadIdx.x & 15) != 0) return;
   if (a.trials) a.trials[b] = r.trials;
   if (a.du2) a.du2[b] = du2;
   if (a.iters) a.iters[b] = a.iter;
