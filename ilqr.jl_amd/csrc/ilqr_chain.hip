@@ -666,16 +666,28 @@ struct Rec {
   static constexpr int N = NJAC + NX + NU;
 };
 
+// One lane per (b, t, direction k): lane g = (b·T + t)·ND + k, so a record's ND
+// columns come from ND adjacent lanes and a block writes a contiguous run of records.
+// (v7 ran one lane per (b, t) over all ND directions: 3,200 waves at B=2048, T=100 on a
+// 3-wave/SIMD occupancy — a second, nearly empty round on 32 CUs.)
+// occupancy asked of the central-difference linearisation: 4 waves/SIMD fits it in 128
+// VGPRs (a few spilled lanes); the dual kernel is left at the compiler's choice
+#ifndef ILQR_CHAIN_FD_WAVES
+#define ILQR_CHAIN_FD_WAVES 4
+#endif
 template <class V, int NJ, int NU, int LIN>
-__global__ __launch_bounds__(256) void chain_linearize_kernel(ChainK<V, NJ> P, int B, int T,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LIN == ILQR_LINEARIZE_CENTRAL_FD ? ILQR_CHAIN_FD_WAVES : 1))) void chain_linearize_kernel(ChainK<V, NJ> P, int B, int T,
                                                               const V* __restrict__ x,
                                                               const V* __restrict__ u,
                                                               const int32_t* __restrict__ status,
                                                               V* __restrict__ J) {
   constexpr int NX = 2 * NJ, ND = NX + NU, NR = Rec<NJ, NU>::N;
-  const int b = blockIdx.x * 256 + threadIdx.x;
-  const int t = blockIdx.y;
-  if (b >= B || (status && status[b] != ILQR_TRAJ_OK)) return;
+  const size_t g = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (g >= (size_t)B * T * ND) return;
+  const int bt = (int)(g / ND);
+  const int kd = (int)(g - (size_t)bt * ND);
+  const int b = bt / T, t = bt - b * T;
+  if (status && status[b] != ILQR_TRAJ_OK) return;
   const V* xb = x + ((size_t)b * (T + 1) + t) * NX;
   const V* ub = u + ((size_t)b * T + t) * NU;
   V* Jt = J + ((size_t)b * T + t) * NR;
@@ -689,8 +701,8 @@ __global__ __launch_bounds__(256) void chain_linearize_kernel(ChainK<V, NJ> P, i
     // carrying all ND directions would spill: ≈4.6 KB of scratch per lane)
     constexpr int DC = 1;
     using D = DualT<DC, V>;
-#pragma unroll 1
-    for (int k0 = 0; k0 < ND; k0 += DC) {
+    {
+      const int k0 = kd;
       D xs[NX], us[NU], o[NX];
 #pragma unroll
       for (int k = 0; k < ND; ++k) {
@@ -709,15 +721,19 @@ __global__ __launch_bounds__(256) void chain_linearize_kernel(ChainK<V, NJ> P, i
   } else {
     // central differences, step h = ε^(1/3)·max(1, |z_k|), divided by the step actually taken
     const V cbe = sizeof(V) == 4 ? V(4.921566e-3) : V(6.0554544523933395e-6);
-#pragma unroll 1
-    for (int k = 0; k < ND; ++k) {
-      const V h = cbe * fmax(V(1), fabs(z[k]));
+    {
+      const int k = kd;
+      V zk = z[0];
+#pragma unroll
+      for (int j = 1; j < ND; ++j)
+        if (j == k) zk = z[j];
+      const V h = cbe * fmax(V(1), fabs(zk));
       V xp[NX], up[NU], xm[NX], um[NU], fp[NX], fm[NX];
 #pragma unroll
       for (int j = 0; j < NX; ++j) xp[j] = xm[j] = z[j];
 #pragma unroll
       for (int j = 0; j < NU; ++j) up[j] = um[j] = z[NX + j];
-      V zp = z[k] + h, zm = z[k] - h;
+      V zp = zk + h, zm = zk - h;
 #pragma unroll
       for (int j = 0; j < NX; ++j)
         if (j == k) { xp[j] = zp; xm[j] = zm; }
@@ -731,8 +747,11 @@ __global__ __launch_bounds__(256) void chain_linearize_kernel(ChainK<V, NJ> P, i
       for (int i = 0; i < NX; ++i) Jt[i * ND + k] = (fp[i] - fm[i]) * inv;
     }
   }
+  V zd = z[0];
 #pragma unroll
-  for (int k = 0; k < ND; ++k) Jt[Rec<NJ, NU>::NJAC + k] = z[k];
+  for (int j = 1; j < ND; ++j)
+    if (j == kd) zd = z[j];
+  Jt[Rec<NJ, NU>::NJAC + kd] = zd;
 }
 
 // record → separate A (B,T,NX,NX), B (B,T,NX,NU) tiles (ilqr_chain_linearize)
@@ -1446,7 +1465,8 @@ struct ChainOps {
 
   static hipError_t linearize(ilqr_chain_handle* h, const V* x, const V* u, const int32_t* st) {
     const auto P = chain_consts<V, NJ>(h->chain);
-    const dim3 grid((h->batch + 255) / 256, h->T);
+    const size_t lanes = (size_t)h->batch * h->T * (NX + NU);
+    const dim3 grid((unsigned)((lanes + 255) / 256));
     if (h->lin == ILQR_LINEARIZE_DUAL)
       ilqr::chain_linearize_kernel<V, NJ, NU, ILQR_LINEARIZE_DUAL>
           <<<grid, 256, 0, h->stream>>>(P, h->batch, h->T, x, u, st, (V*)h->J);
