@@ -131,6 +131,16 @@ __device__ __forceinline__ void scs(const DualT<N, V>& a, DualT<N, V>& s, DualT<
 }
 __device__ __forceinline__ void scs(float a, float& s, float& c) { vsincos(a, s, c); }
 __device__ __forceinline__ void scs(double a, double& s, double& c) { vsincos(a, s, c); }
+// 1/x of the mass-matrix pivots: fp32 by v_rcp_f32 and one Newton step (within an
+// ulp of the IEEE quotient; the IEEE division's scale/fixup sequence sat on the
+// rollout's dependent chain), fp64 and duals by division
+__device__ __forceinline__ float crecip(float x) {
+  const float r = __builtin_amdgcn_rcpf(x);
+  return fmaf(fmaf(-x, r, 1.0f), r, r);
+}
+__device__ __forceinline__ double crecip(double x) { return 1.0 / x; }
+template <int N, class V>
+__device__ __forceinline__ DualT<N, V> crecip(const DualT<N, V>& x) { return V(1) / x; }
 
 template <class S> struct ValueOf { using type = S; };
 template <int N, class V> struct ValueOf<DualT<N, V>> { using type = V; };
@@ -365,7 +375,7 @@ __device__ __forceinline__ void chain_xdot(const ChainK<V, NJ>& P, const S (&x)[
   // Gaussian elimination (M is SPD: no pivoting)
 #pragma unroll
   for (int k = 0; k < NJ; ++k) {
-    const S inv = V(1) / M[k][k];
+    const S inv = crecip(M[k][k]);
 #pragma unroll
     for (int i = k + 1; i < NJ; ++i) {
       const S l = M[i][k] * inv;
@@ -380,7 +390,7 @@ __device__ __forceinline__ void chain_xdot(const ChainK<V, NJ>& P, const S (&x)[
     S acc = r[i];
 #pragma unroll
     for (int j = i + 1; j < NJ; ++j) acc = acc - M[i][j] * qdd[j];
-    qdd[i] = acc * (V(1) / M[i][i]);
+    qdd[i] = acc * crecip(M[i][i]);
   }
 #pragma unroll
   for (int i = 0; i < NJ; ++i) {
@@ -422,7 +432,7 @@ __device__ __forceinline__ void chain_xdot_split(const ChainK<V, NJ>& P, const S
   for (int i = 0; i < NJ; ++i) r[i] = (i < NU ? u[i < NU ? i : 0] : S(V(0))) - b[i];
 #pragma unroll
   for (int k = 0; k < NJ; ++k) {
-    const S inv = V(1) / M[k][k];
+    const S inv = crecip(M[k][k]);
 #pragma unroll
     for (int i = k + 1; i < NJ; ++i) {
       const S l = M[i][k] * inv;
@@ -437,7 +447,7 @@ __device__ __forceinline__ void chain_xdot_split(const ChainK<V, NJ>& P, const S
     S acc = r[i];
 #pragma unroll
     for (int j = i + 1; j < NJ; ++j) acc = acc - M[i][j] * q2[j];
-    q2[i] = acc * (V(1) / M[i][i]);
+    q2[i] = acc * crecip(M[i][i]);
   }
 #pragma unroll
   for (int i = 0; i < NJ; ++i) {
@@ -572,7 +582,7 @@ __device__ __forceinline__ void chain_xdot_cv(const ChainK<V, NJ>& P, const V (&
   for (int i = 0; i < NJ; ++i) r[i] = (i < NU ? u[i < NU ? i : 0] : V(0)) - b[i];
 #pragma unroll
   for (int k = 0; k < NJ; ++k) {
-    const V inv = V(1) / M[k][k];
+    const V inv = crecip(M[k][k]);
 #pragma unroll
     for (int i = k + 1; i < NJ; ++i) {
       const V lk = M[i][k] * inv;
@@ -587,7 +597,7 @@ __device__ __forceinline__ void chain_xdot_cv(const ChainK<V, NJ>& P, const V (&
     V acc = r[i];
 #pragma unroll
     for (int j = i + 1; j < NJ; ++j) acc = acc - M[i][j] * q2[j];
-    q2[i] = acc * (V(1) / M[i][i]);
+    q2[i] = acc * crecip(M[i][i]);
   }
 #pragma unroll
   for (int i = 0; i < NJ; ++i) {
