@@ -479,6 +479,11 @@ __device__ __forceinline__ V qperm(V x) {  // quad_perm DPP move
 }
 constexpr int QP_B0 = 0x00, QP_B1 = 0x55, QP_B2 = 0xAA;  // broadcast component k
 constexpr int QP_R1 = 0xC9, QP_R2 = 0xD2;                // component c+1 / c+2 (mod 3)
+constexpr int QP_ROWBC = 0x150;                         // row_newbcast:n = 0x150 + n
+// lane 4·role (component 0 of that pass) of the row, broadcast to the row
+template <class V> __device__ __forceinline__ V rowbc_role(V x, int role) {
+  return role == 1 ? qperm<QP_ROWBC + 4>(x) : role == 2 ? qperm<QP_ROWBC + 8>(x) : qperm<QP_ROWBC + 12>(x);
+}
 template <class V> __device__ __forceinline__ V bc0(V x) { return qperm<QP_B0>(x); }
 template <class V> __device__ __forceinline__ V bc1(V x) { return qperm<QP_B1>(x); }
 template <class V> __device__ __forceinline__ V bc2(V x) { return qperm<QP_B2>(x); }
@@ -561,7 +566,6 @@ __device__ __forceinline__ void chain_xdot_cv(const ChainK<V, NJ>& P, const V (&
   static_assert(NJ + 1 <= 4, "one role per pass in a group of 16");
   const int l16 = threadIdx.x & 15;
   const int role = l16 >> 2, cmp = l16 & 3;
-  const int base = (threadIdx.x & 63) & ~15;
   V c[NJ], s[NJ], qd[NJ], qdd[NJ], tau[NJ];
 #pragma unroll
   for (int i = 0; i < NJ; ++i) {
@@ -573,9 +577,11 @@ __device__ __forceinline__ void chain_xdot_cv(const ChainK<V, NJ>& P, const V (&
   V b[NJ], M[NJ][NJ];
 #pragma unroll
   for (int i = 0; i < NJ; ++i) {
-    b[i] = __shfl(tau[i], base);
+    // the group is a DPP row (16 lanes): row_newbcast:n (gfx90a+) hands lane n of the
+    // row to all of it on the VALU, off the LDS crossbar that ds_bpermute goes through
+    b[i] = qperm<QP_ROWBC + 0>(tau[i]);
 #pragma unroll
-    for (int k = 0; k < NJ; ++k) M[i][k] = __shfl(tau[i], base + 4 * (1 + k));
+    for (int k = 0; k < NJ; ++k) M[i][k] = rowbc_role(tau[i], 1 + k);
   }
   V r[NJ];
 #pragma unroll
