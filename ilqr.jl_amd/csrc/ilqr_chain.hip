@@ -688,6 +688,11 @@ struct Rec {
 // 3-wave/SIMD occupancy — a second, nearly empty round on 32 CUs.)
 // occupancy asked of the central-difference linearisation: 4 waves/SIMD fits it in 128
 // VGPRs (a few spilled lanes); the dual kernel is left at the compiler's choice
+// joint transforms of the central-difference linearisation: 0 = Rodrigues rotations in
+// place, 1 = 3×3 products of the per-evaluation R_i (the forward's form)
+#ifndef ILQR_CHAIN_FD_ROT
+#define ILQR_CHAIN_FD_ROT 1
+#endif
 #ifndef ILQR_CHAIN_FD_WAVES
 #define ILQR_CHAIN_FD_WAVES 4
 #endif
@@ -756,8 +761,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LIN == ILQR
 #pragma unroll
       for (int j = 0; j < NU; ++j)
         if (NX + j == k) { up[j] = zp; um[j] = zm; }
-      chain_rk4<NJ, NU, false, false>(P, xp, up, fp);
-      chain_rk4<NJ, NU, false, false>(P, xm, um, fm);
+      chain_rk4<NJ, NU, false, ILQR_CHAIN_FD_ROT>(P, xp, up, fp);
+      chain_rk4<NJ, NU, false, ILQR_CHAIN_FD_ROT>(P, xm, um, fm);
       const V inv = V(1) / (zp - zm);
 #pragma unroll
       for (int i = 0; i < NX; ++i) Jt[i * ND + k] = (fp[i] - fm[i]) * inv;
