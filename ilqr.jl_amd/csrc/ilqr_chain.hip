@@ -466,14 +466,17 @@ __device__ __forceinline__ void chain_xdot_split(const ChainK<V, NJ>& P, const S
 // the arithmetic per component is the scalar pass's, in the same order up to the
 // association of three-term sums.
 // ---------------------------------------------------------------------------
+// bound_ctrl set: every source lane of a quad_perm / row_newbcast is valid, so it
+// changes nothing but lets the compiler fold the move into a VOP2 consumer
+// (v_mul_f32_dpp, v_add_f32_dpp: forward 1,733 → 1,653 instructions)
 template <int CTRL, class V>
 __device__ __forceinline__ V qperm(V x) {  // quad_perm DPP move
   if constexpr (sizeof(V) == 4) {
-    return __builtin_bit_cast(V, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), CTRL, 0xF, 0xF, false));
+    return __builtin_bit_cast(V, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), CTRL, 0xF, 0xF, true));
   } else {
     const u2v p = __builtin_bit_cast(u2v, x);
-    const u2v q = {(unsigned)__builtin_amdgcn_mov_dpp((int)p.x, CTRL, 0xF, 0xF, false),
-                   (unsigned)__builtin_amdgcn_mov_dpp((int)p.y, CTRL, 0xF, 0xF, false)};
+    const u2v q = {(unsigned)__builtin_amdgcn_mov_dpp((int)p.x, CTRL, 0xF, 0xF, true),
+                   (unsigned)__builtin_amdgcn_mov_dpp((int)p.y, CTRL, 0xF, 0xF, true)};
     return __builtin_bit_cast(V, q);
   }
 }
@@ -686,18 +689,22 @@ struct Rec {
 // columns come from ND adjacent lanes and a block writes a contiguous run of records.
 // (v7 ran one lane per (b, t) over all ND directions: 3,200 waves at B=2048, T=100 on a
 // 3-wave/SIMD occupancy — a second, nearly empty round on 32 CUs.)
-// occupancy asked of the central-difference linearisation: 4 waves/SIMD fits it in 128
-// VGPRs (a few spilled lanes); the dual kernel is left at the compiler's choice
+// occupancy asked of the linearisation: central differences at 4 waves/SIMD fit in 128
+// VGPRs (a few spilled lanes); the dual kernel at 2 (256 VGPRs, ~150 spilled, still
+// faster than 1 wave with 300 registers: config 5 dual 1,710 → 1,908 it/s)
 // joint transforms of the central-difference linearisation: 0 = Rodrigues rotations in
 // place, 1 = 3×3 products of the per-evaluation R_i (the forward's form)
 #ifndef ILQR_CHAIN_FD_ROT
 #define ILQR_CHAIN_FD_ROT 1
 #endif
+#ifndef ILQR_CHAIN_DUAL_WAVES
+#define ILQR_CHAIN_DUAL_WAVES 2
+#endif
 #ifndef ILQR_CHAIN_FD_WAVES
 #define ILQR_CHAIN_FD_WAVES 4
 #endif
 template <class V, int NJ, int NU, int LIN>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LIN == ILQR_LINEARIZE_CENTRAL_FD ? ILQR_CHAIN_FD_WAVES : 1))) void chain_linearize_kernel(ChainK<V, NJ> P, int B, int T,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LIN == ILQR_LINEARIZE_CENTRAL_FD ? ILQR_CHAIN_FD_WAVES : ILQR_CHAIN_DUAL_WAVES))) void chain_linearize_kernel(ChainK<V, NJ> P, int B, int T,
                                                               const V* __restrict__ x,
                                                               const V* __restrict__ u,
                                                               const int32_t* __restrict__ status,
