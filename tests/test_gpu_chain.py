@@ -91,6 +91,26 @@ def test_chain6_dynamics(gpu, dtype):
     assert rel(xn[:, 6:], g["x_next"][:, 6:]) < (1e-12 if dtype == torch.float64 else 5e-5)
 
 
+@pytest.mark.parametrize("nu", [1, 2])
+@pytest.mark.parametrize("dtype,lin,tol", [(torch.float64, "dual", 1e-11), (torch.float64, "fd", 1e-7),
+                                           (torch.float32, "dual", 5e-5), (torch.float32, "fd", 2e-2)])
+def test_chain_linearize_ragged(gpu, dtype, lin, tol, nu):
+    """linearize_dynamics (backward_pass.jl:25-40), one lane per (b, t, direction), on a
+    ragged batch (37 × 5 points × 5 or 6 directions: partial last workgroup, records
+    straddling waves) at random states vs the oracle's exact forward-mode Jacobians."""
+    from oracle import rbd
+    pr = rbd_2dof_problem(nu)
+    nb, T = 37, 5
+    rng = np.random.default_rng(11 + nu)
+    x = np.concatenate([rng.uniform(-2, 2, (nb, T + 1, 2)), rng.uniform(-1, 1, (nb, T + 1, 2))], axis=2)
+    u = rng.uniform(-3, 3, (nb, T, nu))
+    Ar, Br = rbd.ChainModel(pr.chain, pr.dt).linearize(x[:, :T].reshape(-1, 4), u.reshape(-1, nu))
+    s = ChainSolver(pr, T, nb, dtype=dtype, linearization=lin)
+    A, B = s.linearize(dev(x, dtype), dev(u, dtype))
+    ea, eb = rel(A.reshape(-1, 4, 4), Ar), rel(B.reshape(-1, 4, nu), Br)
+    assert ea < tol and eb < tol, (ea, eb)
+
+
 @pytest.mark.parametrize("dtype,lin", CASES)
 def test_chain_linearize(gpu, g2, dtype, lin):
     """linearize_dynamics (backward_pass.jl:25-40) at every (b, t)."""
