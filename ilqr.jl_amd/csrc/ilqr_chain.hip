@@ -142,6 +142,23 @@ __device__ __forceinline__ double crecip(double x) { return 1.0 / x; }
 template <int N, class V>
 __device__ __forceinline__ DualT<N, V> crecip(const DualT<N, V>& x) { return V(1) / x; }
 
+// a pair of fp32 evaluations carried together (packed v_pk_* arithmetic)
+typedef float F2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void scs(F2 a, F2& s, F2& c) {
+  float s0, c0, s1, c1;
+  vsincos(a.x, s0, c0);
+  vsincos(a.y, s1, c1);
+  s = F2{s0, s1};
+  c = F2{c0, c1};
+}
+__device__ __forceinline__ F2 crecip(F2 x) {
+  const F2 r = F2{__builtin_amdgcn_rcpf(x.x), __builtin_amdgcn_rcpf(x.y)};
+  return (F2(1.0f) - x * r) * r + r;
+}
+#ifndef ILQR_CHAIN_FD_PAIR
+#define ILQR_CHAIN_FD_PAIR 1
+#endif
+
 template <class S> struct ValueOf { using type = S; };
 template <int N, class V> struct ValueOf<DualT<N, V>> { using type = V; };
 
@@ -689,9 +706,11 @@ struct Rec {
 // columns come from ND adjacent lanes and a block writes a contiguous run of records.
 // (v7 ran one lane per (b, t) over all ND directions: 3,200 waves at B=2048, T=100 on a
 // 3-wave/SIMD occupancy — a second, nearly empty round on 32 CUs.)
-// occupancy asked of the linearisation: central differences at 4 waves/SIMD fit in 128
-// VGPRs (a few spilled lanes); the dual kernel at 2 (256 VGPRs, ~150 spilled, still
-// faster than 1 wave with 300 registers: config 5 dual 1,710 → 1,908 it/s)
+// occupancy asked of the linearisation: central differences, the ±h pair packed
+// (ILQR_CHAIN_FD_PAIR), at 3 waves/SIMD (168 VGPRs; config 5 2,208 it/s against 2,175
+// at 2 waves, 1,962 at 4 where it spills, and 2,163 unpacked at 4 waves); the dual
+// kernel at 2 (256 VGPRs, ~150 spilled, still faster than 1 wave with 300 registers:
+// config 5 dual 1,710 → 1,908 it/s)
 // joint transforms of the central-difference linearisation: 0 = Rodrigues rotations in
 // place, 1 = 3×3 products of the per-evaluation R_i (the forward's form)
 #ifndef ILQR_CHAIN_FD_ROT
@@ -701,7 +720,7 @@ struct Rec {
 #define ILQR_CHAIN_DUAL_WAVES 2
 #endif
 #ifndef ILQR_CHAIN_FD_WAVES
-#define ILQR_CHAIN_FD_WAVES 4
+#define ILQR_CHAIN_FD_WAVES 3
 #endif
 template <class V, int NJ, int NU, int LIN>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LIN == ILQR_LINEARIZE_CENTRAL_FD ? ILQR_CHAIN_FD_WAVES : ILQR_CHAIN_DUAL_WAVES))) void chain_linearize_kernel(ChainK<V, NJ> P, int B, int T,
@@ -768,8 +787,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LIN == ILQR
 #pragma unroll
       for (int j = 0; j < NU; ++j)
         if (NX + j == k) { up[j] = zp; um[j] = zm; }
-      chain_rk4<NJ, NU, false, ILQR_CHAIN_FD_ROT>(P, xp, up, fp);
-      chain_rk4<NJ, NU, false, ILQR_CHAIN_FD_ROT>(P, xm, um, fm);
+#if ILQR_CHAIN_FD_PAIR
+      if constexpr (sizeof(V) == 4) {
+        // f(z + h e_k) and f(z − h e_k) run the same instruction stream: one packed
+        // evaluation (v_pk_* on the pair)
+        F2 x2[NX], u2[NU], f2[NX];
+#pragma unroll
+        for (int j = 0; j < NX; ++j) x2[j] = F2{(float)xp[j], (float)xm[j]};
+#pragma unroll
+        for (int j = 0; j < NU; ++j) u2[j] = F2{(float)up[j], (float)um[j]};
+        chain_rk4<NJ, NU, false, ILQR_CHAIN_FD_ROT>(P, x2, u2, f2);
+#pragma unroll
+        for (int j = 0; j < NX; ++j) { fp[j] = f2[j].x; fm[j] = f2[j].y; }
+      } else
+#endif
+      {
+        chain_rk4<NJ, NU, false, ILQR_CHAIN_FD_ROT>(P, xp, up, fp);
+        chain_rk4<NJ, NU, false, ILQR_CHAIN_FD_ROT>(P, xm, um, fm);
+      }
       const V inv = V(1) / (zp - zm);
 #pragma unroll
       for (int i = 0; i < NX; ++i) Jt[i * ND + k] = (fp[i] - fm[i]) * inv;
