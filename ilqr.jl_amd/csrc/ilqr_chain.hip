@@ -587,9 +587,19 @@ __device__ __forceinline__ void chain_xdot_cv(const ChainK<V, NJ>& P, const V (&
   const int l16 = threadIdx.x & 15;
   const int role = l16 >> 2, cmp = l16 & 3;
   V c[NJ], s[NJ], qd[NJ], qdd[NJ], tau[NJ];
+  // one sin/cos per lane: lane c of each quad evaluates joint min(c, NJ − 1), and the
+  // quad reads joint i's pair from its lane i by DPP quad broadcast (the same bits as
+  // evaluating every joint in every lane, at one polynomial pair per lane)
+  V ang = x[0];
+#pragma unroll
+  for (int i = 1; i < NJ; ++i)
+    if (cmp >= i) ang = x[i];
+  V so, co;
+  scs(ang, so, co);
 #pragma unroll
   for (int i = 0; i < NJ; ++i) {
-    scs(x[i], s[i], c[i]);
+    s[i] = i == 0 ? bc0(so) : i == 1 ? bc1(so) : bc2(so);
+    c[i] = i == 0 ? bc0(co) : i == 1 ? bc1(co) : bc2(co);
     qd[i] = role == 0 ? x[NJ + i] : V(0);
     qdd[i] = V(role == i + 1 ? 1 : 0);
   }
