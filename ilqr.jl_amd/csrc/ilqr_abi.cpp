@@ -123,7 +123,7 @@ ilqr_status join(ilqr_handle* h, const ilqr_problem* p);
 ilqr_status enqueue_iteration(ilqr_handle* h, const ilqr_problem* p, const ilqr::IterArgs& a,
                               const ilqr::LSParams& ls, bool chain) {
   if (two_link(p)) {  // one stream: linearise, backward, forward
-    HIP_TRY(ilqr::launch_tl_iteration(ilqr::two_link_params(), h->batch, h->T, a, h->J, ls,
+    HIP_TRY(ilqr::launch_tl_iteration(ilqr::two_link_params(), h->nu, h->batch, h->T, a, h->J, ls,
                                       h->stream));
     return ILQR_OK;
   }
@@ -430,7 +430,7 @@ ilqr_status ilqr_backward(ilqr_handle* h, const ilqr_problem* p, const ilqr_opti
     return bst;
   }
   if (two_link(p))
-    HIP_TRY(ilqr::launch_tl_backward(ilqr::two_link_params(), h->batch, h->T, x, u, h->J, d, K,
+    HIP_TRY(ilqr::launch_tl_backward(ilqr::two_link_params(), h->nu, h->batch, h->T, x, u, h->J, d, K,
                                      status, ls_params(o).mu, h->stream));
   else
     HIP_TRY(ilqr::launch_lq_backward(h->nx, h->nu, lq_params(p), h->batch, h->T, x, u, d, K,
@@ -483,7 +483,7 @@ ilqr_status ilqr_forward(ilqr_handle* h, const ilqr_problem* p, const ilqr_optio
     return fst;
   }
   if (two_link(p))
-    HIP_TRY(ilqr::launch_tl_forward(ilqr::two_link_params(), h->batch, h->T, x, u, x_traj, d, K,
+    HIP_TRY(ilqr::launch_tl_forward(ilqr::two_link_params(), h->nu, h->batch, h->T, x, u, x_traj, d, K,
                                     prev_cost, x_new, u_new, new_cost, trials, status,
                                     ls_params(o), h->stream));
   else

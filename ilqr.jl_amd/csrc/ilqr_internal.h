@@ -115,20 +115,20 @@ struct TwoLinkParams {
   double tgt0, tgt1;          // θ* = InverseKinematics(target_tool_loc) (:16-26)
 };
 TwoLinkParams two_link_params();
-bool tl_supported(int nx, int nu);
+bool tl_supported(int nx, int nu);  // (4, 2), and (4, 1): f(x, [u₁, 0])
 size_t tl_workspace_doubles(int B, int T);  // linearisation workspace J
 // backward = linearise every (b, t) into J, then the Riccati recursion
-hipError_t launch_tl_backward(const TwoLinkParams& P, int B, int T, const double* x,
+hipError_t launch_tl_backward(const TwoLinkParams& P, int nu, int B, int T, const double* x,
                               const double* u, double* J, double* d, double* K, int32_t* status,
                               double mu, hipStream_t s);
-hipError_t launch_tl_forward(const TwoLinkParams& P, int B, int T, const double* x,
+hipError_t launch_tl_forward(const TwoLinkParams& P, int nu, int B, int T, const double* x,
                              const double* u, const double* xtraj, const double* d,
                              const double* K, const double* prev_cost, double* xnew,
                              double* unew, double* new_cost, int32_t* trials, int32_t* status,
                              const LSParams& ls, hipStream_t s);
 // one fit iteration (linearise, backward, forward) for trajectories with status OK
-hipError_t launch_tl_iteration(const TwoLinkParams& P, int B, int T, const IterArgs& a, double* J,
-                               const LSParams& ls, hipStream_t s);
+hipError_t launch_tl_iteration(const TwoLinkParams& P, int nu, int B, int T, const IterArgs& a,
+                               double* J, const LSParams& ls, hipStream_t s);
 int run_selftest(int device);  // number of failed checks, or -1 on HIP error
 
 }  // namespace ilqr

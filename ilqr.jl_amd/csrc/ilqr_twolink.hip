@@ -1,6 +1,10 @@
 // MI355X (gfx950) kernels for the 2-link arm problem family (ILQR_PROBLEM_TWO_LINK):
 // the reference's only runnable nonlinear example, test/2_link_example/
-// 2_link_helper_functions.jl:1-108 (configs 1-2 of BASELINE.json), nx = 4, nu = 2.
+// 2_link_helper_functions.jl:1-108 (configs 1-2 of BASELINE.json), nx = 4, nu = 2
+// (the reference's shape), and the nu = 1 variant BASELINE.json's configs 1-2 name:
+// f₁(x, u) = f(x, [u₁, 0]) — build-defined (the reference multiplies inv(M), 2×2, by
+// u, :63-65, so a length-1 u would throw), not reference-pinned. Every kernel is
+// templated on NU ∈ {1, 2}.
 //
 // What replaces what:
 //  * dynamicsf (RK4 of continuous_dynamics, :49-79) is a device functor templated on
@@ -40,9 +44,11 @@ namespace ilqr {
 namespace {
 
 constexpr int TL_NX = 4;
-constexpr int TL_NU = 2;
-constexpr int TL_NJ = TL_NX * (TL_NX + TL_NU);  // 24 entries of [A | B] per step
-constexpr int TL_NJR = TL_NJ + 4;                // + θ₁, θ₂, u₁, u₂: the backward's whole input
+// per-step linearisation record [A | B] (4 × (4 + NU), row-major), θ₁, θ₂, u (NU),
+// padded to a whole number of 16-byte pairs: the backward's whole input for a step
+template <int NU> constexpr int tl_nj() { return TL_NX * (TL_NX + NU); }
+template <int NU> constexpr int tl_njr() { return tl_nj<NU>() + 4; }  // 28 (NU = 2), 24 (NU = 1)
+constexpr int TL_NJR_MAX = 28;
 constexpr int TL_FW_PF = 2;                      // forward prefetch depth (steps)
 constexpr int TL_BW4_PF = 4;                     // backward prefetch depth (steps)
 
@@ -161,9 +167,10 @@ __device__ __forceinline__ Dual<N> tl_recip(const Dual<N>& x) { return 1.0 / x; 
 // ---------------------------------------------------------------------------
 // dynamicsf of test/2_link_example/2_link_helper_functions.jl:49-79, generic in S.
 // ---------------------------------------------------------------------------
-template <class S>
+// u has NU entries; NU = 1 is f(x, [u₁, 0]) (the second torque a constant zero)
+template <class S, int NU>
 __device__ __forceinline__ void continuous_dynamics(const TwoLinkParams& P, const S (&x)[4],
-                                                    const S (&u)[2], S (&xd)[4]) {
+                                                    const S (&u)[NU], S (&xd)[4]) {
   // InertiaMatrix (:29-33): M = [α+2βc₂  δ+βc₂; δ+βc₂  δ]
   S s2, c2;
   sin_cos(x[1], s2, c2);
@@ -191,13 +198,14 @@ __device__ __forceinline__ void continuous_dynamics(const TwoLinkParams& P, cons
   // state_dot = [θ̇; −(M\C)θ̇ + M⁻¹u] (:56-66)
   xd[0] = x[2];
   xd[1] = x[3];
-  xd[2] = -(mc00 * x[2] + mc01 * x[3]) + (i00 * u[0] + i01 * u[1]);
-  xd[3] = -(mc10 * x[2] + mc11 * x[3]) + (i01 * u[0] + i11 * u[1]);
+  const S u1 = NU > 1 ? u[NU - 1] : S(0.0);
+  xd[2] = -(mc00 * x[2] + mc01 * x[3]) + (i00 * u[0] + i01 * u1);
+  xd[3] = -(mc10 * x[2] + mc11 * x[3]) + (i01 * u[0] + i11 * u1);
 }
 
 // RK4 (:71-78): k_i = Δt·f(·); x' = x + (1/6)(k1 + 2k2 + 2k3 + k4)
-template <class S>
-__device__ __forceinline__ void rk4(const TwoLinkParams& P, const S (&x)[4], const S (&u)[2],
+template <class S, int NU>
+__device__ __forceinline__ void rk4(const TwoLinkParams& P, const S (&x)[4], const S (&u)[NU],
                                     S (&out)[4]) {
   S k1[4], k2[4], k3[4], k4[4], y[4];
   continuous_dynamics(P, x, u, k1);
@@ -230,30 +238,37 @@ __device__ __forceinline__ void rk4(const TwoLinkParams& P, const S (&x)[4], con
 // ---------------------------------------------------------------------------
 // Linearisation: J_t = [A_t | B_t] = ∂f/∂(x,u) at (x_t, u_t), one lane per (b, t).
 // ---------------------------------------------------------------------------
+template <int NU>
 __global__ __launch_bounds__(256) void tl_linearize_kernel(TwoLinkParams P, int B, int T,
                                                            const double* __restrict__ x,
                                                            const double* __restrict__ u,
                                                            const int32_t* __restrict__ status,
                                                            double* __restrict__ J) {
+  constexpr int ND = TL_NX + NU;  // directions: the 4 states and NU inputs
+  constexpr int NJ = tl_nj<NU>(), NJR = tl_njr<NU>();
   const int b = blockIdx.x * 256 + threadIdx.x;
   const int t = blockIdx.y;
   if (b >= B || (status && status[b] != ILQR_TRAJ_OK)) return;
   const double* xb = x + ((size_t)b * (T + 1) + t) * TL_NX;
-  const double* ub = u + ((size_t)b * T + t) * TL_NU;
-  Dual<6> xs[4], us[2], out[4];
+  const double* ub = u + ((size_t)b * T + t) * NU;
+  Dual<ND> xs[4], us[NU], out[4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) xs[i] = seed<6>(xb[i], i);
+  for (int i = 0; i < 4; ++i) xs[i] = seed<ND>(xb[i], i);
 #pragma unroll
-  for (int i = 0; i < 2; ++i) us[i] = seed<6>(ub[i], 4 + i);
-  rk4(P, xs, us, out);
-  double2* Jt = reinterpret_cast<double2*>(J + ((size_t)b * T + t) * TL_NJR);
+  for (int i = 0; i < NU; ++i) us[i] = seed<ND>(ub[i], 4 + i);
+  rk4<Dual<ND>, NU>(P, xs, us, out);
+  double jv[NJR];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int k = 0; k < 6; k += 2) Jt[(i * 6 + k) / 2] = make_double2(out[i].d[k], out[i].d[k + 1]);
-  }
-  Jt[TL_NJ / 2] = make_double2(xb[0], xb[1]);
-  Jt[TL_NJ / 2 + 1] = make_double2(ub[0], ub[1]);
+    for (int k = 0; k < ND; ++k) jv[i * ND + k] = out[i].d[k];
+  jv[NJ] = xb[0];
+  jv[NJ + 1] = xb[1];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) jv[NJ + 2 + i] = i < NU ? ub[i] : 0.0;
+  double2* Jt = reinterpret_cast<double2*>(J + ((size_t)b * T + t) * NJR);
+#pragma unroll
+  for (int e = 0; e < NJR; e += 2) Jt[e / 2] = make_double2(jv[e], jv[e + 1]);
 }
 
 // ---------------------------------------------------------------------------
@@ -282,6 +297,7 @@ __device__ __forceinline__ double lane_perm2(double v, int src_byte) {
 // Slots whose bit in `active` is clear, or past B, compute on clamped data and store
 // nothing. Returns the NaN slots (bit β). As in ilqr_bw4.hip, a NaN in any K_t or d_t
 // reaches K_0 or d_0, so only the last step's gains are tested.
+template <int NU>
 __device__ unsigned tl_backward4_wave(const TwoLinkParams& P, int b0, int B, unsigned active, int T,
                                       const double* __restrict__ x, const double* __restrict__ J,
                                       double* __restrict__ dg, double* __restrict__ Kg, double mu,
@@ -293,7 +309,8 @@ __device__ unsigned tl_backward4_wave(const TwoLinkParams& P, int b0, int B, uns
   const bool live = b < B && ((active >> beta) & 1u);
   const int bc = b < B ? b : B - 1;
   const int nslot = B - b0 < 4 ? B - b0 : 4;
-  const bool ru = rho < TL_NU;  // a real u row
+  constexpr int ND = TL_NX + NU, NJ = tl_nj<NU>(), NJR = tl_njr<NU>();
+  const bool ru = rho < NU;  // a real u row
   const double tg = rho == 0 ? P.tgt0 : P.tgt1;
 
   // final_cost_quadratization (:134-153): ∇²ℓ_f = lxx = diag(2,2,0,0), ∇ℓ_f = [2(θ−θ*), 0, 0]
@@ -302,22 +319,23 @@ __device__ unsigned tl_backward4_wave(const TwoLinkParams& P, int b0, int B, uns
   const double xT = x[((size_t)bc * (T + 1) + T) * TL_NX + (rho < 2 ? rho : 0)];
   double s = rho < 2 ? -2.0 * (tg - xT) : 0.0;
 
-  // per-step record J[b][t] = [A|B] (4×6 row-major), θ₁, θ₂, u₁, u₂ via one buffer
-  // resource over the wave's slots; the step is the scalar offset
-  const auto rJ = buffer_rsrc(const_cast<double*>(J) + (size_t)b0 * T * TL_NJR,
-                              (uint32_t)(nslot * T * TL_NJR * 8));
-  const uint32_t base = (uint32_t)(beta * T * TL_NJR * 8);
-  const uint32_t oA = base + (uint32_t)((rho * 6 + kap) * 8);
-  const uint32_t oB = kap < TL_NU ? base + (uint32_t)((rho * 6 + 4 + kap) * 8) : 0x80000000u;
-  const uint32_t oT = rho < 2 ? base + (uint32_t)((TL_NJ + rho) * 8) : 0x80000000u;
-  const uint32_t oU = rho < 2 ? base + (uint32_t)((TL_NJ + 2 + rho) * 8) : 0x80000000u;
+  // per-step record J[b][t] = [A|B] (4×(4+NU) row-major), θ₁, θ₂, u via one buffer
+  // resource over the wave's slots; the step is the scalar offset (loads past a
+  // record's live entries read 0: the B block is zero-padded to 4×4)
+  const auto rJ = buffer_rsrc(const_cast<double*>(J) + (size_t)b0 * T * NJR,
+                              (uint32_t)(nslot * T * NJR * 8));
+  const uint32_t base = (uint32_t)(beta * T * NJR * 8);
+  const uint32_t oA = base + (uint32_t)((rho * ND + kap) * 8);
+  const uint32_t oB = kap < NU ? base + (uint32_t)((rho * ND + 4 + kap) * 8) : 0x80000000u;
+  const uint32_t oT = rho < 2 ? base + (uint32_t)((NJ + rho) * 8) : 0x80000000u;
+  const uint32_t oU = ru ? base + (uint32_t)((NJ + 2 + rho) * 8) : 0x80000000u;
   auto ld = [&](uint32_t off, int t) {
-    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rJ, off, (uint32_t)(t * TL_NJR * 8), 0));
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rJ, off, (uint32_t)(t * NJR * 8), 0));
   };
-  const auto rK = buffer_rsrc(Kg + (size_t)b0 * T * TL_NU * TL_NX, (uint32_t)(nslot * T * TL_NU * TL_NX * 8));
-  const auto rD = buffer_rsrc(dg + (size_t)b0 * T * TL_NU, (uint32_t)(nslot * T * TL_NU * 8));
-  const uint32_t kv = (live && ru) ? (uint32_t)((beta * T * TL_NU * TL_NX + rho * TL_NX + kap) * 8) : 0x80000000u;
-  const uint32_t dv = (live && ru && kap == 0) ? (uint32_t)((beta * T * TL_NU + rho) * 8) : 0x80000000u;
+  const auto rK = buffer_rsrc(Kg + (size_t)b0 * T * NU * TL_NX, (uint32_t)(nslot * T * NU * TL_NX * 8));
+  const auto rD = buffer_rsrc(dg + (size_t)b0 * T * NU, (uint32_t)(nslot * T * NU * 8));
+  const uint32_t kv = (live && ru) ? (uint32_t)((beta * T * NU * TL_NX + rho * TL_NX + kap) * 8) : 0x80000000u;
+  const uint32_t dv = (live && ru && kap == 0) ? (uint32_t)((beta * T * NU + rho) * 8) : 0x80000000u;
   const int tr_src = (16 * kap + 4 * beta + rho) * 4;  // lane of element [κ][ρ]
   double* Hl = lds + beta * 16;
 
@@ -345,20 +363,26 @@ __device__ unsigned tl_backward4_wave(const TwoLinkParams& P, int b0, int B, uns
     const double Z = mfa(A, Y0, lxx);                             // lxx + AᵀSA
     const double G = mfa(Bm, Y0, 0.0);                            // BᵀSA (lux = 0)
     const double gx = mfa(A, s, lx), gu = mfa(Bm, s, lu);         // lx + Aᵀs, lu + Bᵀs
-    // feedback_parameters (:207-218): (H + μI)⁻¹ of the 2×2 block by its adjugate, in
+    // feedback_parameters (:207-218): (H + μI)⁻¹ of the NU×NU block by its adjugate, in
     // every lane (H = 2I + BᵀSB with B = O(Δt): condition ≈ 1, so the explicit inverse
     // costs nothing in accuracy and one MFMA stage less than two triangular sweeps)
     wave_lds_fence();
     const double h00 = Hl[0], h10 = Hl[4], h11 = Hl[5];
     wave_lds_fence();
-    const double a00 = h00 + mu, a11 = h11 + mu;
-    const double idet = rcp<2>(fma(a00, a11, -h10 * h10));
-    const bool in2 = rho < 2 && kap < 2;
-    const double Hi = !in2 ? 0.0 : (rho != kap ? -h10 : (rho == 0 ? a11 : a00)) * idet;
+    double Hi;
+    if constexpr (NU == 2) {
+      const double a00 = h00 + mu, a11 = h11 + mu;
+      const double idet = rcp<2>(fma(a00, a11, -h10 * h10));
+      const bool in2 = rho < 2 && kap < 2;
+      Hi = !in2 ? 0.0 : (rho != kap ? -h10 : (rho == 0 ? a11 : a00)) * idet;
+    } else {
+      (void)h10; (void)h11;
+      Hi = (rho == 0 && kap == 0) ? rcp<2>(h00 + mu) : 0.0;
+    }
     const double K = mfa_n(Hi, G, 0.0);                           // −(H+μI)⁻¹ G
     const double d = mfa_n(Hi, gu, 0.0);                          // −(H+μI)⁻¹ g
-    store_or_drop(K, rK, kv != 0x80000000u, kv + (uint32_t)(t * TL_NU * TL_NX * 8));
-    store_or_drop(d, rD, dv != 0x80000000u, dv + (uint32_t)(t * TL_NU * 8));
+    store_or_drop(K, rK, kv != 0x80000000u, kv + (uint32_t)(t * NU * TL_NX * 8));
+    store_or_drop(d, rD, dv != 0x80000000u, dv + (uint32_t)(t * NU * 8));
     // step_back (:262-273), exact rewrite: W = (H+2μI)[K|d] = μ[K|d] − [G|g]
     const double W = fma(mu, K, -G), Wd = fma(mu, d, -gu);
     const double Sf = mfa_n(K, W, Z);                             // Qxx − KᵀW_K
@@ -392,10 +416,12 @@ struct TLFwdOut {
   int accepted;
 };
 
+template <int NU>
 struct TLStepIn {
-  double x[4], xt[4], u[2], d[2], K[8];
+  double x[4], xt[4], u[NU], d[NU], K[4 * NU];
 };
 
+template <int NU>
 __device__ TLFwdOut tl_forward_lane(const TwoLinkParams& P, int b, int T,
                                     const double* __restrict__ x, const double* __restrict__ u,
                                     const double* __restrict__ xtraj,
@@ -404,28 +430,27 @@ __device__ TLFwdOut tl_forward_lane(const TwoLinkParams& P, int b, int T,
                                     double* __restrict__ unew, double* du2_out,
                                     const LSParams& ls) {
   const double* xb0 = x + (size_t)b * (T + 1) * TL_NX;
-  const double* ub0 = u + (size_t)b * T * TL_NU;
+  const double* ub0 = u + (size_t)b * T * NU;
   const double* xt0 = (xtraj ? xtraj : x) + (size_t)b * (T + 1) * TL_NX;
   const double xtw = xtraj ? 1.0 : 0.0;  // x_traj = NULL means zeros (forward_pass.jl:151)
-  const double* d0 = dg + (size_t)b * T * TL_NU;
-  const double* K0 = Kg + (size_t)b * T * TL_NU * TL_NX;
+  const double* d0 = dg + (size_t)b * T * NU;
+  const double* K0 = Kg + (size_t)b * T * NU * TL_NX;
   double* xo = xnew + (size_t)b * (T + 1) * TL_NX;
-  double* uo = unew + (size_t)b * T * TL_NU;
+  double* uo = unew + (size_t)b * T * NU;
 
-  auto load = [&](int t, TLStepIn& in) {
+  auto load = [&](int t, TLStepIn<NU>& in) {
     const int tt = t < T ? t : T - 1;
     const double4 xv = *reinterpret_cast<const double4*>(xb0 + (size_t)tt * TL_NX);
     const double4 tv = *reinterpret_cast<const double4*>(xt0 + (size_t)tt * TL_NX);
     in.x[0] = xv.x; in.x[1] = xv.y; in.x[2] = xv.z; in.x[3] = xv.w;
     in.xt[0] = tv.x; in.xt[1] = tv.y; in.xt[2] = tv.z; in.xt[3] = tv.w;
-    const double2 uv = *reinterpret_cast<const double2*>(ub0 + (size_t)tt * TL_NU);
-    const double2 dv = *reinterpret_cast<const double2*>(d0 + (size_t)tt * TL_NU);
-    in.u[0] = uv.x; in.u[1] = uv.y;
-    in.d[0] = dv.x; in.d[1] = dv.y;
-    const double4* kv = reinterpret_cast<const double4*>(K0 + (size_t)tt * TL_NU * TL_NX);
-    const double4 k0 = kv[0], k1 = kv[1];
-    in.K[0] = k0.x; in.K[1] = k0.y; in.K[2] = k0.z; in.K[3] = k0.w;
-    in.K[4] = k1.x; in.K[5] = k1.y; in.K[6] = k1.z; in.K[7] = k1.w;
+#pragma unroll
+    for (int a = 0; a < NU; ++a) {
+      in.u[a] = ub0[(size_t)tt * NU + a];
+      in.d[a] = d0[(size_t)tt * NU + a];
+      const double4 kr = reinterpret_cast<const double4*>(K0 + (size_t)tt * NU * TL_NX)[a];
+      in.K[4 * a] = kr.x; in.K[4 * a + 1] = kr.y; in.K[4 * a + 2] = kr.z; in.K[4 * a + 3] = kr.w;
+    }
   };
 
   double alpha = ls.alpha0;
@@ -439,14 +464,14 @@ __device__ TLFwdOut tl_forward_lane(const TwoLinkParams& P, int b, int T,
     }
     double cost = 0.0;
     du2 = 0.0;
-    auto step = [&](int t, const TLStepIn& in) {
+    auto step = [&](int t, const TLStepIn<NU>& in) {
       // δx = x̄ₖ − xₖ (:72); ūₖ = uₖ + α δuₖ + Kₖ δx (:73)
       double dx[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) dx[i] = xb[i] - in.x[i];
-      double ubar[2];
+      double ubar[NU];
 #pragma unroll
-      for (int a = 0; a < 2; ++a) {
+      for (int a = 0; a < NU; ++a) {
         double kdx = 0.0;
 #pragma unroll
         for (int i = 0; i < 4; ++i) kdx = fma(in.K[a * 4 + i], dx[i], kdx);
@@ -455,19 +480,28 @@ __device__ TLFwdOut tl_forward_lane(const TwoLinkParams& P, int b, int T,
       // ℓ(x̄ₖ − x_trajₖ, ūₖ) (:187-190; 2_link_helper_functions.jl:82-97)
       const double e0 = P.tgt0 - fma(-xtw, in.xt[0], xb[0]);
       const double e1 = P.tgt1 - fma(-xtw, in.xt[1], xb[1]);
-      cost += (e0 * e0 + e1 * e1) + (ubar[0] * ubar[0] + ubar[1] * ubar[1]);
+      double uu;
+      if constexpr (NU == 2) uu = ubar[0] * ubar[0] + ubar[NU - 1] * ubar[NU - 1];
+      else uu = ubar[0] * ubar[0];
+      cost += (e0 * e0 + e1 * e1) + uu;
       *reinterpret_cast<double4*>(xo + (size_t)t * TL_NX) = make_double4(xb[0], xb[1], xb[2], xb[3]);
-      *reinterpret_cast<double2*>(uo + (size_t)t * TL_NU) = make_double2(ubar[0], ubar[1]);
-      const double du0 = ubar[0] - in.u[0], du1 = ubar[1] - in.u[1];
-      du2 = fma(du0, du0, fma(du1, du1, du2));
+#pragma unroll
+      for (int a = 0; a < NU; ++a) uo[(size_t)t * NU + a] = ubar[a];
+      const double du0 = ubar[0] - in.u[0];
+      if constexpr (NU == 2) {
+        const double du1 = ubar[NU - 1] - in.u[NU - 1];
+        du2 = fma(du0, du0, fma(du1, du1, du2));
+      } else {
+        du2 = fma(du0, du0, du2);
+      }
       // x̄ₖ₊₁ = f(x̄ₖ, ūₖ) (:74)
       double xn[4];
-      rk4(P, xb, ubar, xn);
+      rk4<double, NU>(P, xb, ubar, xn);
 #pragma unroll
       for (int i = 0; i < 4; ++i) xb[i] = xn[i];
     };
     // inputs of the next TL_FW_PF steps in flight (HBM latency ≈ one RK4 step)
-    TLStepIn ring[TL_FW_PF];
+    TLStepIn<NU> ring[TL_FW_PF];
 #pragma unroll
     for (int k = 0; k < TL_FW_PF; ++k) load(k, ring[k]);
     int t = 0;
@@ -504,6 +538,7 @@ constexpr int TL_WG = 64;  // one wave per workgroup: B = 1024 spreads over 16 C
 
 // four trajectories per wave, four waves per workgroup
 constexpr int TL_BW4_WAVES = 4;
+template <int NU>
 __global__ __launch_bounds__(64 * TL_BW4_WAVES) void tl_backward_kernel(TwoLinkParams P, int B, int T,
                                                                       const double* __restrict__ x,
                                                                       const double* __restrict__ J,
@@ -515,11 +550,12 @@ __global__ __launch_bounds__(64 * TL_BW4_WAVES) void tl_backward_kernel(TwoLinkP
   const int w = threadIdx.x >> 6;
   const int b0 = (blockIdx.x * TL_BW4_WAVES + w) * 4;
   if (b0 >= B) return;
-  const unsigned nan = tl_backward4_wave(P, b0, B, 0xFu, T, x, J, d, K, mu, lds + w * 64);
+  const unsigned nan = tl_backward4_wave<NU>(P, b0, B, 0xFu, T, x, J, d, K, mu, lds + w * 64);
   const int l = threadIdx.x & 63;
   if (status && l < 4 && b0 + l < B) status[b0 + l] = ((nan >> l) & 1u) ? ILQR_TRAJ_NAN : ILQR_TRAJ_OK;
 }
 
+template <int NU>
 __global__ __launch_bounds__(TL_WG) void tl_forward_kernel(
     TwoLinkParams P, int B, int T, const double* __restrict__ x, const double* __restrict__ u,
     const double* __restrict__ xtraj, const double* __restrict__ d, const double* __restrict__ K,
@@ -529,10 +565,10 @@ __global__ __launch_bounds__(TL_WG) void tl_forward_kernel(
   const int b = blockIdx.x * TL_WG + threadIdx.x;
   if (b >= B) return;
   const double pc = prev_cost ? prev_cost[b] : INFINITY;
-  const TLFwdOut r = tl_forward_lane(P, b, T, x, u, xtraj, d, K, pc, xnew, unew, nullptr, ls);
+  const TLFwdOut r = tl_forward_lane<NU>(P, b, T, x, u, xtraj, d, K, pc, xnew, unew, nullptr, ls);
   if (!r.accepted) {  // exhausted (the reference would loop forever): return the inputs
     for (int i = 0; i < (T + 1) * TL_NX; ++i) xnew[(size_t)b * (T + 1) * TL_NX + i] = x[(size_t)b * (T + 1) * TL_NX + i];
-    for (int i = 0; i < T * TL_NU; ++i) unew[(size_t)b * T * TL_NU + i] = u[(size_t)b * T * TL_NU + i];
+    for (int i = 0; i < T * NU; ++i) unew[(size_t)b * T * NU + i] = u[(size_t)b * T * NU + i];
   }
   new_cost[b] = r.cost;
   if (trials) trials[b] = r.trials;
@@ -542,6 +578,7 @@ __global__ __launch_bounds__(TL_WG) void tl_forward_kernel(
 
 // One fit iteration (forward_pass.jl:161-176): backward part (after tl_linearize),
 // slots whose status is not OK computed on and never stored.
+template <int NU>
 __global__ __launch_bounds__(64 * TL_BW4_WAVES) void tl_iter_backward_kernel(TwoLinkParams P, int B, int T,
                                                                            IterArgs a, const double* J,
                                                                            double mu) {
@@ -553,7 +590,7 @@ __global__ __launch_bounds__(64 * TL_BW4_WAVES) void tl_iter_backward_kernel(Two
   for (int q = 0; q < 4; ++q)
     if (b0 + q < B && a.status[b0 + q] == ILQR_TRAJ_OK) active |= 1u << q;
   if (active == 0) return;
-  const unsigned nan = tl_backward4_wave(P, b0, B, active, T, a.x, J, a.d, a.K, mu, lds + w * 64) & active;
+  const unsigned nan = tl_backward4_wave<NU>(P, b0, B, active, T, a.x, J, a.d, a.K, mu, lds + w * 64) & active;
   const int l = threadIdx.x & 63;
   if (l < 4 && ((nan >> l) & 1u)) {
     a.status[b0 + l] = ILQR_TRAJ_NAN;  // reference: AssertionError at backward_pass.jl:353
@@ -562,14 +599,15 @@ __global__ __launch_bounds__(64 * TL_BW4_WAVES) void tl_iter_backward_kernel(Two
 }
 
 // Forward part + the convergence test (:163-175).
+template <int NU>
 __global__ __launch_bounds__(TL_WG) void tl_iter_forward_kernel(TwoLinkParams P, int B, int T,
                                                                 IterArgs a, LSParams ls) {
   const int b = blockIdx.x * TL_WG + threadIdx.x;
   if (b >= B || a.status[b] != ILQR_TRAJ_OK) return;
   double du2 = 0.0;
   const double pc = a.prev_cost ? a.prev_cost[b] : INFINITY;
-  const TLFwdOut r = tl_forward_lane(P, b, T, a.x, a.u, a.xtraj, a.d, a.K, pc, a.xnew, a.unew,
-                                     &du2, ls);
+  const TLFwdOut r = tl_forward_lane<NU>(P, b, T, a.x, a.u, a.xtraj, a.d, a.K, pc, a.xnew, a.unew,
+                                         &du2, ls);
   if (a.trials) a.trials[b] = r.trials;
   if (a.du2) a.du2[b] = du2;
   if (a.iters) a.iters[b] = a.iter;
@@ -610,47 +648,66 @@ TwoLinkParams two_link_params() {
   return P;
 }
 
-bool tl_supported(int nx, int nu) { return nx == TL_NX && nu == TL_NU; }
+bool tl_supported(int nx, int nu) { return nx == TL_NX && (nu == 1 || nu == 2); }
 
-size_t tl_workspace_doubles(int B, int T) { return (size_t)T * TL_NJR * B; }
+size_t tl_workspace_doubles(int B, int T) { return (size_t)T * TL_NJR_MAX * B; }
 
-static hipError_t launch_linearize(const TwoLinkParams& P, int B, int T, const double* x,
-                                   const double* u, const int32_t* status, double* J,
-                                   hipStream_t s) {
-  tl_linearize_kernel<<<dim3((B + 255) / 256, T), 256, 0, s>>>(P, B, T, x, u, status, J);
-  return hipGetLastError();
-}
-
-hipError_t launch_tl_backward(const TwoLinkParams& P, int B, int T, const double* x,
-                              const double* u, double* J, double* d, double* K, int32_t* status,
-                              double mu, hipStream_t s) {
-  hipError_t e = launch_linearize(P, B, T, x, u, nullptr, J, s);
+namespace {
+template <int NU>
+hipError_t tl_backward_nu(const TwoLinkParams& P, int B, int T, const double* x, const double* u,
+                          double* J, double* d, double* K, int32_t* status, double mu, hipStream_t s) {
+  tl_linearize_kernel<NU><<<dim3((B + 255) / 256, T), 256, 0, s>>>(P, B, T, x, u, nullptr, J);
+  hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const int per_wg = 4 * TL_BW4_WAVES;
-  tl_backward_kernel<<<(B + per_wg - 1) / per_wg, 64 * TL_BW4_WAVES, 0, s>>>(P, B, T, x, J, d, K, status, mu);
+  tl_backward_kernel<NU><<<(B + per_wg - 1) / per_wg, 64 * TL_BW4_WAVES, 0, s>>>(P, B, T, x, J, d, K, status, mu);
   return hipGetLastError();
 }
 
-hipError_t launch_tl_forward(const TwoLinkParams& P, int B, int T, const double* x,
+template <int NU>
+hipError_t tl_forward_nu(const TwoLinkParams& P, int B, int T, const double* x, const double* u,
+                         const double* xtraj, const double* d, const double* K,
+                         const double* prev_cost, double* xnew, double* unew, double* new_cost,
+                         int32_t* trials, int32_t* status, const LSParams& ls, hipStream_t s) {
+  tl_forward_kernel<NU><<<(B + TL_WG - 1) / TL_WG, TL_WG, 0, s>>>(P, B, T, x, u, xtraj, d, K,
+                                                                  prev_cost, xnew, unew, new_cost,
+                                                                  trials, status, ls);
+  return hipGetLastError();
+}
+
+template <int NU>
+hipError_t tl_iteration_nu(const TwoLinkParams& P, int B, int T, const IterArgs& a, double* J,
+                           const LSParams& ls, hipStream_t s) {
+  tl_linearize_kernel<NU><<<dim3((B + 255) / 256, T), 256, 0, s>>>(P, B, T, a.x, a.u, a.status, J);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const int per_wg = 4 * TL_BW4_WAVES;
+  tl_iter_backward_kernel<NU><<<(B + per_wg - 1) / per_wg, 64 * TL_BW4_WAVES, 0, s>>>(P, B, T, a, J, ls.mu);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  tl_iter_forward_kernel<NU><<<(B + TL_WG - 1) / TL_WG, TL_WG, 0, s>>>(P, B, T, a, ls);
+  return hipGetLastError();
+}
+}  // namespace
+
+hipError_t launch_tl_backward(const TwoLinkParams& P, int nu, int B, int T, const double* x,
+                              const double* u, double* J, double* d, double* K, int32_t* status,
+                              double mu, hipStream_t s) {
+  return nu == 1 ? tl_backward_nu<1>(P, B, T, x, u, J, d, K, status, mu, s)
+                 : tl_backward_nu<2>(P, B, T, x, u, J, d, K, status, mu, s);
+}
+
+hipError_t launch_tl_forward(const TwoLinkParams& P, int nu, int B, int T, const double* x,
                              const double* u, const double* xtraj, const double* d,
                              const double* K, const double* prev_cost, double* xnew,
                              double* unew, double* new_cost, int32_t* trials, int32_t* status,
                              const LSParams& ls, hipStream_t s) {
-  tl_forward_kernel<<<(B + TL_WG - 1) / TL_WG, TL_WG, 0, s>>>(P, B, T, x, u, xtraj, d, K,
-                                                              prev_cost, xnew, unew, new_cost,
-                                                              trials, status, ls);
-  return hipGetLastError();
+  return nu == 1 ? tl_forward_nu<1>(P, B, T, x, u, xtraj, d, K, prev_cost, xnew, unew, new_cost, trials, status, ls, s)
+                 : tl_forward_nu<2>(P, B, T, x, u, xtraj, d, K, prev_cost, xnew, unew, new_cost, trials, status, ls, s);
 }
 
-hipError_t launch_tl_iteration(const TwoLinkParams& P, int B, int T, const IterArgs& a, double* J,
-                               const LSParams& ls, hipStream_t s) {
-  hipError_t e = launch_linearize(P, B, T, a.x, a.u, a.status, J, s);
-  if (e != hipSuccess) return e;
-  const int per_wg = 4 * TL_BW4_WAVES;
-  tl_iter_backward_kernel<<<(B + per_wg - 1) / per_wg, 64 * TL_BW4_WAVES, 0, s>>>(P, B, T, a, J, ls.mu);
-  if ((e = hipGetLastError()) != hipSuccess) return e;
-  tl_iter_forward_kernel<<<(B + TL_WG - 1) / TL_WG, TL_WG, 0, s>>>(P, B, T, a, ls);
-  return hipGetLastError();
+hipError_t launch_tl_iteration(const TwoLinkParams& P, int nu, int B, int T, const IterArgs& a,
+                               double* J, const LSParams& ls, hipStream_t s) {
+  return nu == 1 ? tl_iteration_nu<1>(P, B, T, a, J, ls, s) : tl_iteration_nu<2>(P, B, T, a, J, ls, s);
 }
 
 }  // namespace ilqr

@@ -1,12 +1,12 @@
 """ilqr_amd — MI355X-native batched iLQR (host-side mirror of aabouman/iLQR.jl's
 `iLQR` module over the C ABI of libilqr_hip.so; see include/ilqr.h)."""
 from .problems import (LinearDynamics, LQBatch, QuadraticCost, QuadraticFinalCost, TwoLinkArm,
-                       TwoLinkCost, TwoLinkDynamics, TwoLinkFinalCost, lq_from_closures,
+                       TwoLinkCost, TwoLinkDynamics, TwoLinkDynamicsNu1, TwoLinkFinalCost, lq_from_closures,
                        quadrotor_batch, quadrotor_instance, random_lq_batch, two_link_closures,
                        two_link_initial_states)
 
 __all__ = ["LinearDynamics", "QuadraticCost", "QuadraticFinalCost", "LQBatch",
-           "lq_from_closures", "TwoLinkArm", "TwoLinkDynamics", "TwoLinkCost",
+           "lq_from_closures", "TwoLinkArm", "TwoLinkDynamics", "TwoLinkDynamicsNu1", "TwoLinkCost",
            "TwoLinkFinalCost", "two_link_closures", "two_link_initial_states", "quadrotor_batch", "quadrotor_instance", "random_lq_batch",
            "fit", "backward_pass", "forward_pass", "Solver", "selftest", "LineSearchExhausted",
            "ChainSolver", "ChainProblem", "rbd_2dof_problem", "chain_closures", "load_robot",

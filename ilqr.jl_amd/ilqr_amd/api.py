@@ -113,8 +113,8 @@ def _solver(xb, ub, dynamicsf, immediate_cost, final_cost):
     assert N == M + 1, "size(x)[1] == size(u)[1] + 1"   # backward_pass.jl:329
     assert ub.shape[0] == nb, "batch sizes differ"
     if is_two_link(dynamicsf, immediate_cost, final_cost):
-        if (nx, nu) != (4, 2):
-            raise AssertionError(f"the 2-link arm is (4, 2) but x/u are ({nx}, {nu})")
+        if (nx, nu) != (4, dynamicsf.nu):
+            raise AssertionError(f"the 2-link arm is (4, {dynamicsf.nu}) but x/u are ({nx}, {nu})")
         return Solver(nx, nu, M, nb, device=_device(), kind=_lib.PROBLEM_TWO_LINK)
     lq = lq_from_closures(dynamicsf, immediate_cost, final_cost, nb)
     if (lq.nx, lq.nu) != (nx, nu):

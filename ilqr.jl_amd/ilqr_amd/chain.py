@@ -17,6 +17,7 @@ from __future__ import annotations
 
 import ctypes as C
 import json
+import math
 import os
 from dataclasses import dataclass, field
 
@@ -105,6 +106,25 @@ def rbd_2dof_problem(nu: int = 2) -> ChainProblem:
     only, BASELINE's 'nᵤ=1' row; not reference-pinned)."""
     return ChainProblem(load_robot("2dof_arm"), nu, RBD_DT, RBD_TARGET_JOINTS, RBD_Q_JOINT,
                         RBD_R_JOINT, RBD_QF_JOINT)
+
+
+def coupled_2dof_problem(nu: int = 2) -> ChainProblem:
+    """A non-degenerate 2-joint chain for parity tests (not a reference robot): the
+    2Dof_arm's joint layout with the first joint frame tilted, COMs off the joint
+    origins, anisotropic inertias with products of inertia, and gravity on. Unlike the
+    2Dof_arm (COMs on the joint axes, 0.5·I inertias, zero gravity: constant
+    M = diag(4, 0.5), zero bias), M(q) is dense and q-dependent and the bias carries
+    Coriolis and gravity terms, so A's q-columns are nonzero."""
+    ch = load_robot("2dof_arm")
+    c, s = math.cos(0.3), math.sin(0.3)
+    R0 = ch.R0.copy()
+    R0[0] = np.array([[1.0, 0.0, 0.0], [0.0, c, -s], [0.0, s, c]])   # joint 1 tilted about x
+    com = np.array([[0.10, 0.05, 0.20], [0.30, 0.05, -0.15]])
+    Ic = np.array([[[0.40, 0.02, 0.01], [0.02, 0.60, 0.03], [0.01, 0.03, 0.30]],
+                   [[0.20, 0.01, -0.02], [0.01, 0.35, 0.015], [-0.02, 0.015, 0.25]]])
+    chain = Chain(list(ch.names), R0, ch.p.copy(), ch.axis.copy(), np.array([3.0, 2.0]), com, Ic,
+                  np.array([0.0, 0.0, -9.81]))
+    return ChainProblem(chain, nu, RBD_DT, RBD_TARGET_JOINTS, RBD_Q_JOINT, RBD_R_JOINT, RBD_QF_JOINT)
 
 
 def rbd_initial_states(batch: int, n_joints: int = 2, seed0: int = 0):

@@ -273,6 +273,18 @@ class TwoLinkDynamics:
         return x + (1 / 6) * (k1 + 2 * k2 + 2 * k3 + k4)
 
 
+class TwoLinkDynamicsNu1(TwoLinkDynamics):
+    """dynamicsf₁(x, u) = dynamicsf(x, [u₁, 0]) — the nu = 1 variant of the 2-link arm
+    that BASELINE.json's configs 1-2 name. Build-defined: the reference
+    multiplies inv(M) (2×2) by u (2_link_helper_functions.jl:63-65), so its own
+    dynamicsf needs nu = 2; only joint 1 is driven here. Not reference-pinned."""
+    nu = 1
+
+    def __call__(self, x, u):
+        u = np.asarray(u, dtype=np.float64).reshape(-1)
+        return super().__call__(x, np.array([u[0], 0.0]))
+
+
 class TwoLinkCost:
     """immediate_cost(x, u) = |θ* − θ|² + |u|² (:82-97; the velocity penalty is dead code)."""
 
@@ -289,9 +301,12 @@ class TwoLinkFinalCost:
         return float(np.sum(e ** 2) * 1.0)
 
 
-def two_link_closures():
-    """(dynamicsf, immediate_cost, final_cost) of test/2_link_example."""
-    return TwoLinkDynamics(), TwoLinkCost(), TwoLinkFinalCost()
+def two_link_closures(nu: int = 2):
+    """(dynamicsf, immediate_cost, final_cost) of test/2_link_example; nu = 1 gives the
+    build-defined single-torque variant (TwoLinkDynamicsNu1)."""
+    if nu not in (1, 2):
+        raise ValueError("the 2-link arm takes nu = 2 (reference) or 1 (joint 1 driven)")
+    return (TwoLinkDynamics() if nu == 2 else TwoLinkDynamicsNu1()), TwoLinkCost(), TwoLinkFinalCost()
 
 
 def is_two_link(dynamicsf, immediate_cost, final_cost) -> bool:

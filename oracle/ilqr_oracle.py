@@ -347,6 +347,13 @@ class TwoLink:
         return out
 
     @classmethod
+    def dynamicsf_nu1(cls, x, u):
+        """dynamicsf₁(x, u) = dynamicsf(x, [u₁, 0]): the build-defined nu = 1 variant
+        (BASELINE.json configs 1-2; the reference's own dynamicsf needs nu = 2,
+        :63-65). Not reference-pinned."""
+        return cls.dynamicsf(x, np.array([u[0], 0.0], dtype=object))
+
+    @classmethod
     def immediate_cost(cls, x, u):                                      # :82-97
         tgt = cls.inverse_kinematics(cls.target_tool_loc)
         e = (tgt[0] - x[0]) ** 2 + (tgt[1] - x[1]) ** 2

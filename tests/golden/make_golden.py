@@ -19,7 +19,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(os.path.dirname(HERE))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "ilqr.jl_amd")]
 
-from ilqr_amd.chain import load_robot, rbd_2dof_problem, rbd_initial_states  # noqa: E402
+from ilqr_amd.chain import (coupled_2dof_problem, load_robot, rbd_2dof_problem,  # noqa: E402
+                            rbd_initial_states)
 from ilqr_amd.problems import quadrotor_batch, random_lq_batch  # noqa: E402
 from oracle import ilqr_oracle as O  # noqa: E402
 from oracle import rbd as RBD  # noqa: E402
@@ -67,38 +68,41 @@ def lq_case(name, lq, x, u, xtraj=None, symmetrize=False, fit_iters=30, tol=1e-6
     print(name, "fit iters", fiters.tolist(), "trials", trials.tolist())
 
 
-def twolink_case(name, x0s, T, fit_iters=40, tol=1e-6):
+def twolink_case(name, x0s, T, fit_iters=40, tol=1e-6, nu=2):
+    """2-link arm; nu = 1 is the build-defined f(x, [u₁, 0]) variant (not reference-pinned)."""
     TL = O.TwoLink
+    f = TL.dynamicsf if nu == 2 else TL.dynamicsf_nu1
     nb = len(x0s)
-    x = np.stack([O.rollout(np.asarray(x0, float), np.zeros((T, 2)), TL.dynamicsf) for x0 in x0s])
-    u = np.zeros((nb, T, 2))
+    x = np.stack([O.rollout(np.asarray(x0, float), np.zeros((T, nu)), f) for x0 in x0s])
+    u = np.zeros((nb, T, nu))
     d = np.empty_like(u)
-    K = np.empty((nb, T, 2, 4))
+    K = np.empty((nb, T, nu, 4))
     xn, un = np.empty_like(x), np.empty_like(u)
     cost = np.empty(nb)
     fx, fu = np.empty_like(x), np.empty_like(u)
     fcost = np.full((nb, fit_iters), np.nan)
     fiters = np.empty(nb, dtype=np.int32)
     for b in range(nb):
-        d[b], K[b] = O.backward_pass(x[b], u[b], TL.dynamicsf, TL.immediate_cost, TL.final_cost)
+        d[b], K[b] = O.backward_pass(x[b], u[b], f, TL.immediate_cost, TL.final_cost)
         xn[b], un[b], cost[b] = O.forward_pass(x[b], u[b], np.zeros_like(x[b]), d[b], K[b], np.inf,
-                                               TL.dynamicsf, TL.immediate_cost, TL.final_cost,
+                                               f, TL.immediate_cost, TL.final_cost,
                                                max_trials=MAX_TRIALS)
         hist = []
-        fx[b], fu[b] = O.fit(x[b], u[b], TL.dynamicsf, TL.immediate_cost, TL.final_cost,
+        fx[b], fu[b] = O.fit(x[b], u[b], f, TL.immediate_cost, TL.final_cost,
                              max_iter=fit_iters, tol=tol, max_trials=MAX_TRIALS, history=hist)
         fiters[b] = len(hist)
         fcost[b, :len(hist)] = [h["cost"] for h in hist]
     np.savez_compressed(os.path.join(HERE, name + ".npz"), x=x, u=u, d=d, K=K, fw_x=xn, fw_u=un,
                         fw_cost=cost, fit_x=fx, fit_u=fu, fit_cost=fcost, fit_iters=fiters,
-                        meta=np.array(json.dumps({"T": T, "fit_max_iter": fit_iters, "tol": tol})))
+                        meta=np.array(json.dumps({"T": T, "nu": nu, "fit_max_iter": fit_iters, "tol": tol})))
     print(name, "fit iters", fiters.tolist())
 
 
-def chain_case(name, nu, x0s, T, fit_iters=20, tol=1e-6):
-    """RBD family (ILQR_PROBLEM_CHAIN) on the fixed-base 2Dof_arm: oracle.rbd dynamics
-    (RNEA + RK4, exact Jacobians by forward-mode AD) through the generic oracle passes."""
-    pr = rbd_2dof_problem(nu)
+def chain_case(name, nu, x0s, T, fit_iters=20, tol=1e-6, pr=None, robot="2dof_arm"):
+    """RBD family (ILQR_PROBLEM_CHAIN) on the fixed-base 2Dof_arm (or `pr`): oracle.rbd
+    dynamics (RNEA + RK4, exact Jacobians by forward-mode AD) through the generic
+    oracle passes."""
+    pr = rbd_2dof_problem(nu) if pr is None else pr
     model = RBD.ChainModel(pr.chain, pr.dt)
     cost = RBD.ChainCost(pr.target, pr.q_weight, pr.r_weight, pr.qf_weight)
     f, l, lf = RBD.chain_closures(model, cost)
@@ -140,7 +144,7 @@ def chain_case(name, nu, x0s, T, fit_iters=20, tol=1e-6):
                         fw_x=xn, fw_u=un, fw_cost=fwc, fit_x=fx, fit_u=fu, fit_cost=fcost,
                         fit_iters=fiters, fit_status=fstatus,
                         meta=np.array(json.dumps({"T": T, "nu": nu, "fit_max_iter": fit_iters,
-                                                  "tol": tol, "robot": "2dof_arm"})))
+                                                  "tol": tol, "robot": robot})))
     print(name, "fit iters", fiters.tolist(), "status", fstatus.tolist())
 
 
@@ -166,6 +170,20 @@ def main(only=()):
         chain_case("chain2_t100", 2, rbd_initial_states(3, 2, seed0=0), T=100)
         chain_case("chain2_nu1_t50", 1, rbd_initial_states(2, 2, seed0=10), T=50)
         chain6_dynamics_case("chain6_dynamics")
+    if want("chain2_nu1_t100"):
+        # BASELINE config 5 as stated: nu = 1 (joint 1 driven), T = 100
+        chain_case("chain2_nu1_t100", 1, rbd_initial_states(3, 2, seed0=20), T=100)
+    if want("chain2c"):
+        # a coupled 2-joint chain (dense q-dependent M, Coriolis and gravity bias): the
+        # 2Dof_arm's own M is constant, so it cannot pin the recursion's coupling terms
+        chain_case("chain2c_t40", 2, rbd_initial_states(4, 2, seed0=30), T=40,
+                   pr=coupled_2dof_problem(2), robot="coupled_2dof")
+        chain_case("chain2c_nu1_t40", 1, rbd_initial_states(3, 2, seed0=40), T=40,
+                   pr=coupled_2dof_problem(1), robot="coupled_2dof")
+    if want("twolink_nu1"):
+        # the nu = 1 variant of configs 1-2: f(x, [u₁, 0]), T = 50
+        rng = np.random.default_rng(2025)
+        twolink_case("twolink_nu1_t50", [[0.1, -0.1, 0.0, 0.0], rng.random(4), rng.random(4)], T=50, nu=1)
     if only:
         return
     # headline family, short horizon: the literal recursion is healthy for T ≲ 16 (rounding asymmetry grows ~3×/step)

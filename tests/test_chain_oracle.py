@@ -220,3 +220,15 @@ def test_c_chain_iteration_matches_numpy_oracle():
         xo, uo, co = O.forward_pass(x[b], u[b], np.zeros_like(x[b]), d[b], K[b], np.inf, f, l, lf)
         assert np.abs(xn[b] - xo).max() <= 1e-12 * np.abs(xo).max()
         assert abs(c[b] - co) <= 1e-12 * abs(co)
+
+
+def test_coupled_chain_is_not_degenerate():
+    """The fixture really exercises the coupling terms (CPU-checkable property)."""
+    from ilqr_amd.chain import coupled_2dof_problem
+    from oracle import rbd
+    m = rbd.ChainModel(coupled_2dof_problem(2).chain, 0.01)
+    M0, M1 = m.mass_matrix_np(np.array([0.0, 0.0])), m.mass_matrix_np(np.array([0.7, -1.1]))
+    assert abs(M0[0, 1]) > 1e-2 and np.abs(M0 - M1).max() > 1e-2
+    assert np.abs(m.bias_np(np.array([0.4, 0.9]), np.zeros(2))).max() > 1.0      # gravity
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "chain2c_t40.npz"))
+    assert np.abs(g["A"][..., 2:, :2]).max() > 1e-3                                # ∂q̈/∂q

@@ -197,3 +197,161 @@ def test_chain_api_mirror_keeps_eltype(gpu, g2):
     assert uo.dtype == np.float64 and rel(uo, g2["fit_u"][0]) < 1e-8
     d, K = ilqr_amd.backward_pass(g2["x"][0], g2["u"][0], dyn, cost, fcost)
     assert rel(K, g2["K"][0]) < 1e-9
+
+
+# -- a coupled chain: dense q-dependent M, Coriolis and gravity in the bias ----------------
+# The 2Dof_arm's fixed-base M is the constant diag(4, 0.5) with zero bias, so the tests
+# above cannot see a wrong joint angle, permutation sign or rotation in the 16-lane
+# Newton-Euler forward (per-lane sin/cos + DPP quad broadcasts, row_newbcast b/M
+# gathers), nor in the rotation-form central differences. These run the same kernels on
+# ilqr_amd.chain.coupled_2dof_problem against the oracle (tests/golden/chain2c_*.npz).
+@pytest.fixture(scope="module")
+def gc():
+    return load("chain2c_t40")
+
+
+@pytest.fixture(scope="module")
+def gc1():
+    return load("chain2c_nu1_t40")
+
+
+def coupled_solver(g, dtype, lin, nu=2):
+    from ilqr_amd.chain import coupled_2dof_problem
+    nb, T = g["u"].shape[:2]
+    return ChainSolver(coupled_2dof_problem(nu), T, nb, dtype=dtype, linearization=lin)
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_coupled_chain_dynamics_kernel(gpu, dtype):
+    """chain_dynamics_kernel (one lane per point) at random states vs the oracle."""
+    from ilqr_amd.chain import coupled_2dof_problem
+    from oracle import rbd
+    pr = coupled_2dof_problem(2)
+    rng = np.random.default_rng(3)
+    n = 97
+    x = np.concatenate([rng.uniform(-2.5, 2.5, (n, 2)), rng.uniform(-2, 2, (n, 2))], axis=1)
+    u = rng.uniform(-20, 20, (n, 2))
+    ref = rbd.ChainModel(pr.chain, pr.dt).step(x, u)
+    s = ChainSolver(pr, 1, 1, dtype=dtype)
+    xn = s.dynamics(dev(x, dtype), dev(u, dtype))
+    assert rel(xn, ref) < (1e-12 if dtype == torch.float64 else 5e-5)
+    assert rel(xn[:, 2:], ref[:, 2:]) < (1e-12 if dtype == torch.float64 else 1e-4)
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_coupled_chain_forward_rollout(gpu, gc, dtype):
+    """The 16-lane component-parallel forward kernel (chain_forward_lane): with δu = K = 0
+    and prev_cost = Inf it is the rollout the fixture starts from; with the oracle's
+    gains it is forward_pass (forward_pass.jl:55-93)."""
+    s = coupled_solver(gc, dtype, "dual")
+    nb, T = gc["u"].shape[:2]
+    x, u = dev(gc["x"], dtype), dev(gc["u"], dtype)
+    pc = torch.full((nb,), float("inf"), dtype=dtype, device="cuda")
+    z_d, z_K = torch.zeros((nb, T, 2), dtype=dtype, device="cuda"), torch.zeros((nb, T, 2, 4), dtype=dtype, device="cuda")
+    xr, _, _, _, _ = s.forward(x, u, z_d, z_K, pc)
+    t = TOL[(dtype, "dual")]
+    assert rel(xr, gc["x"]) < (1e-11 if dtype == torch.float64 else 1e-4)
+    assert rel(xr[..., 2:], gc["x"][..., 2:]) < (1e-10 if dtype == torch.float64 else 2e-4)
+    xn, un, c, tr, st = s.forward(x, u, dev(gc["d"], dtype), dev(gc["K"], dtype), pc)
+    assert (st.cpu().numpy() == 0).all() and (tr.cpu().numpy() == 1).all()
+    assert rel(xn, gc["fw_x"]) < t["fw"] * 10 and rel(un, gc["fw_u"]) < t["fw"] * 10
+    assert rel(c, gc["fw_cost"]) < t["fw"] * 10
+
+
+@pytest.mark.parametrize("dtype,lin", CASES)
+def test_coupled_chain_linearize(gpu, gc, dtype, lin):
+    """linearize_dynamics at every (b, t) of the coupled chain: dual numbers and the
+    rotation-form central differences (ILQR_CHAIN_FD_ROT), fp64 and fp32."""
+    s = coupled_solver(gc, dtype, lin)
+    A, B = s.linearize(dev(gc["x"], dtype), dev(gc["u"], dtype))
+    t = TOL[(dtype, lin)]["AB"]
+    assert rel(A, gc["A"]) < t and rel(B, gc["B"]) < t, (rel(A, gc["A"]), rel(B, gc["B"]))
+    # the coupling block ∂q̈/∂q alone, relative to its own size
+    ta = 1e-9 if dtype == torch.float64 and lin == "dual" else (1e-5 if dtype == torch.float64 else 5e-2)
+    assert rel(A[..., 2:, :2], gc["A"][..., 2:, :2]) < ta
+
+
+@pytest.mark.parametrize("dtype,lin", CASES)
+def test_coupled_chain_backward(gpu, gc, dtype, lin):
+    s = coupled_solver(gc, dtype, lin)
+    d, K, st = s.backward(dev(gc["x"], dtype), dev(gc["u"], dtype))
+    assert (st.cpu().numpy() == 0).all()
+    t = TOL[(dtype, lin)]["gain"]
+    assert rel(K, gc["K"]) < t and rel(d, gc["d"]) < t, (rel(K, gc["K"]), rel(d, gc["d"]))
+
+
+def test_coupled_chain_fit_f64(gpu, gc):
+    s = coupled_solver(gc, torch.float64, "dual")
+    r = s.fit(dev(gc["x"], torch.float64), dev(gc["u"], torch.float64), max_iter=20, tol=1e-6)
+    assert np.array_equal(r.iters.cpu().numpy(), gc["fit_iters"])
+    assert (r.status.cpu().numpy() == gc["fit_status"]).all()
+    assert rel(r.x, gc["fit_x"]) < 1e-8 and rel(r.u, gc["fit_u"]) < 1e-8
+
+
+@pytest.mark.parametrize("dtype,lin", [(torch.float64, "dual"), (torch.float32, "fd")])
+def test_coupled_chain_nu1(gpu, gc1, dtype, lin):
+    """nu = 1 (τ = [u₁, 0]) on the coupled chain: gains and forward pass."""
+    s = coupled_solver(gc1, dtype, lin, nu=1)
+    x, u = dev(gc1["x"], dtype), dev(gc1["u"], dtype)
+    d, K, _ = s.backward(x, u)
+    t = TOL[(dtype, lin)]
+    assert rel(K, gc1["K"]) < t["gain"] and rel(d, gc1["d"]) < t["gain"]
+    nb = u.shape[0]
+    pc = torch.full((nb,), float("inf"), dtype=dtype, device="cuda")
+    xn, un, c, _, _ = s.forward(x, u, dev(gc1["d"], dtype), dev(gc1["K"], dtype), pc)
+    assert rel(xn, gc1["fw_x"]) < t["fw"] * 10 and rel(c, gc1["fw_cost"]) < t["fw"] * 10
+
+
+# -- BASELINE config 5 as stated: nu = 1, fp32, central differences, T = 100 ---------------
+@pytest.fixture(scope="module")
+def g5():
+    return load("chain2_nu1_t100")
+
+
+def test_config5_nu1_fp32_fd_fixture(gpu, g5):
+    """Gains, forward pass and fit of the nu = 1, T = 100 fixture in the config-5
+    arithmetic (fp32, central-difference linearisation on the device)."""
+    s = solver(g5, torch.float32, "fd", nu=1)
+    x, u = dev(g5["x"], torch.float32), dev(g5["u"], torch.float32)
+    A, B = s.linearize(x, u)
+    t = TOL[(torch.float32, "fd")]
+    assert rel(A, g5["A"]) < t["AB"] and rel(B, g5["B"]) < t["AB"]
+    d, K, st = s.backward(x, u)
+    assert (st.cpu().numpy() == 0).all()
+    assert rel(K, g5["K"]) < t["gain"] and rel(d, g5["d"]) < t["gain"], (rel(K, g5["K"]), rel(d, g5["d"]))
+    nb = u.shape[0]
+    pc = torch.full((nb,), float("inf"), dtype=torch.float32, device="cuda")
+    xn, un, c, _, _ = s.forward(x, u, dev(g5["d"], torch.float32), dev(g5["K"], torch.float32), pc)
+    assert rel(xn, g5["fw_x"]) < t["fw"] and rel(c, g5["fw_cost"]) < t["fw"]
+    r = s.fit(x, u, max_iter=20, tol=1e-6)
+    assert set(r.status.cpu().numpy().tolist()) <= {_lib.TRAJ_CONVERGED, _lib.TRAJ_LS_EXHAUSTED}
+    last = g5["fit_cost"][np.arange(nb), g5["fit_iters"] - 1]
+    assert rel(r.cost, last) < 1e-4 and rel(r.u, g5["fit_u"]) < 2e-3
+
+
+def test_config5_batch2048_iteration_vs_c_oracle(gpu):
+    """The config-5 bench step (tools/bench_rbd.py --nu 1: B = 2048, T = 100, fp32,
+    central differences, one fit iteration from cold) against the C restatement
+    (oracle_chain_iterate: fp64, central differences) on 64 sampled trajectories."""
+    from ilqr_amd.chain import rbd_initial_states
+    from oracle import cref
+    pr = rbd_2dof_problem(1)
+    B, T = 2048, 100
+    x0 = rbd_initial_states(B, 2)
+    s = ChainSolver(pr, T, B, dtype=torch.float32, linearization="fd")
+    u = torch.zeros((B, T, 1), dtype=torch.float32, device="cuda")
+    x = s.rollout(torch.from_numpy(x0).to("cuda", torch.float32), u)
+    xn, un = torch.empty_like(x), torch.empty_like(u)
+    pc = torch.empty((B,), dtype=torch.float32, device="cuda")
+    st = torch.zeros((B,), dtype=torch.int32, device="cuda")
+    tr = torch.empty((B,), dtype=torch.int32, device="cuda")
+    s.iterate(x, u, xn, un, None, st, pc, trials=tr, options=_lib.default_options(tol=-1.0))
+    torch.cuda.synchronize()
+    assert (st.cpu().numpy() == 0).all() and (tr.cpu().numpy() == 1).all()
+    idx = np.arange(0, B, 32)
+    d, K, xo, uo, co, tro = cref.chain_iterate(pr, x[idx].double().cpu().numpy(),
+                                               u[idx].double().cpu().numpy())
+    t = TOL[(torch.float32, "fd")]
+    assert (tro == 1).all()
+    assert rel(un.cpu().numpy()[idx], uo) < t["fw"] and rel(xn.cpu().numpy()[idx], xo) < t["fw"]
+    assert rel(pc.cpu().numpy()[idx], co) < t["fw"]

@@ -197,3 +197,84 @@ def test_tl_bad_problem_args(gpu):
     rc = s.lib.ilqr_backward(s.h, C.byref(p), None, C.c_void_p(x.data_ptr()), C.c_void_p(u.data_ptr()),
                              C.c_void_p(d.data_ptr()), C.c_void_p(K.data_ptr()), None)
     assert rc == _lib.ERR_BAD_ARG
+
+
+# -- the nu = 1 variant (BASELINE.json configs 1-2: "n_u = 1") -------------------------------
+# f₁(x, u) = f(x, [u₁, 0]) on ILQR_PROBLEM_TWO_LINK with nu = 1 (SURVEY.md §0's
+# build-defined wrapper: the reference's dynamicsf multiplies inv(M), 2×2, by u,
+# 2_link_helper_functions.jl:63-65, so it needs nu = 2). NOT reference-pinned: the
+# oracle is the same restatement with the second torque held at 0
+# (oracle.ilqr_oracle.TwoLink.dynamicsf_nu1), frozen in tests/golden/twolink_nu1_t50.npz.
+@pytest.fixture(scope="module")
+def g1():
+    z = np.load(os.path.join(GOLD, "twolink_nu1_t50.npz"), allow_pickle=False)
+    return {k: z[k] for k in z.files}
+
+
+def tl1_solver(T, B):
+    return Solver(4, 1, T, B, kind=_lib.PROBLEM_TWO_LINK)
+
+
+def test_tl_nu1_supported(gpu):
+    lib = _lib.load()
+    assert lib.ilqr_supported(_lib.PROBLEM_TWO_LINK, 4, 1) == 1
+    assert lib.ilqr_supported(_lib.PROBLEM_TWO_LINK, 4, 3) == 0
+
+
+def test_tl_nu1_passes(gpu, g1):
+    nb, T = g1["u"].shape[:2]
+    s = tl1_solver(T, nb)
+    x = s.rollout(dev(g1["x"][:, 0]), dev(g1["u"]))
+    assert rel(x, g1["x"]) < TOL_ROLL
+    d, K, st = s.backward(dev(g1["x"]), dev(g1["u"]))
+    assert (st.cpu().numpy() == _lib.TRAJ_OK).all()
+    assert d.shape == (nb, T, 1) and K.shape == (nb, T, 1, 4)
+    assert rel(d, g1["d"]) < TOL_GAIN and rel(K, g1["K"]) < TOL_GAIN
+    pc = torch.full((nb,), float("inf"), dtype=torch.float64, device="cuda")
+    xn, un, cost, trials, st = s.forward(dev(g1["x"]), dev(g1["u"]), dev(g1["d"]), dev(g1["K"]), pc)
+    assert (st.cpu().numpy() == _lib.TRAJ_OK).all() and (trials.cpu().numpy() == 1).all()
+    assert rel(xn, g1["fw_x"]) < TOL_ROLL * 10 and rel(un, g1["fw_u"]) < TOL_ROLL * 10
+    assert rel(cost, g1["fw_cost"]) < TOL_COST
+
+
+def test_tl_nu1_fit(gpu, g1):
+    nb, T = g1["u"].shape[:2]
+    s = tl1_solver(T, nb)
+    r = s.fit(dev(g1["x"]), dev(g1["u"]), max_iter=40, tol=1e-6)
+    assert (r.status.cpu().numpy() == _lib.TRAJ_CONVERGED).all()
+    assert (r.iters.cpu().numpy() == g1["fit_iters"]).all()
+    assert rel(r.x, g1["fit_x"]) < TOL_FIT and rel(r.u, g1["fit_u"]) < TOL_FIT
+
+
+def test_tl_nu1_api_mirror(gpu, g1):
+    from ilqr_amd import api
+    f, l, lf = two_link_closures(nu=1)
+    d, K = api.backward_pass(g1["x"][1], g1["u"][1], f, l, lf)
+    assert rel(d, g1["d"][1]) < TOL_GAIN and rel(K, g1["K"][1]) < TOL_GAIN
+    xf, uf = api.fit(g1["x"][1], g1["u"][1], f, l, lf, max_iter=40, tol=1e-6)
+    assert rel(uf, g1["fit_u"][1]) < TOL_FIT
+    with pytest.raises(AssertionError):  # a nu = 2 control trajectory for the nu = 1 problem
+        api.backward_pass(g1["x"][1], np.zeros((g1["u"].shape[1], 2)), f, l, lf)
+
+
+def test_tl_nu1_config2_batch(gpu):
+    """Config 2 in the nu = 1 shape: B = 1024, T = 50; the fit converges for every
+    trajectory and sampled trajectories match the oracle's fit."""
+    B, T = 1024, 50
+    x0 = two_link_initial_states(B)
+    s = tl1_solver(T, B)
+    u0 = torch.zeros((B, T, 1), dtype=torch.float64, device="cuda")
+    x = s.rollout(dev(x0), u0)
+    r = s.fit(x, u0, max_iter=100, tol=1e-6)
+    st = r.status.cpu().numpy()
+    assert np.isin(st, [_lib.TRAJ_CONVERGED, _lib.TRAJ_LS_EXHAUSTED]).all(), np.unique(st, return_counts=True)
+    xs, us = x.cpu().numpy(), u0.cpu().numpy()
+    TL = O.TwoLink
+    for b in (0, 777):
+        if st[b] != _lib.TRAJ_CONVERGED:
+            continue
+        h = []
+        fx, fu = O.fit(xs[b], us[b], TL.dynamicsf_nu1, TL.immediate_cost, TL.final_cost, max_iter=100,
+                       tol=1e-6, max_trials=64, history=h)
+        assert int(r.iters[b]) == len(h), b
+        assert rel(r.u[b], fu) < TOL_FIT, b
