@@ -30,6 +30,11 @@ struct ilqr_handle {
   int32_t* res_parity = nullptr;
   int32_t* iters = nullptr;
   int32_t* host_status = nullptr;  // pinned host copy of a status array (fold_status)
+  // fit's convergence poll: running-trajectory counts of the last two iterations,
+  // written by the device into host-mapped memory, each behind an event
+  int32_t* host_running = nullptr;
+  int32_t* dev_running = nullptr;  // device alias of host_running
+  hipEvent_t ev_poll[2] = {nullptr, nullptr};
   // LQ problems of another shape (nx ≤ 12, nu ≤ 4) run zero-padded on an inner
   // (12, 4) handle (created on the first such call): zero rows/columns of A, B, Q, R,
   // Qf, x, u decouple exactly, so the real entries are the (12, 4) kernels' bits.
@@ -318,6 +323,10 @@ ilqr_status ilqr_create(ilqr_handle** out, int device, int nx, int nu, int T, in
   if (e == hipSuccess) e = hipMalloc(&h->res_parity, sizeof(int32_t) * B);
   if (e == hipSuccess) e = hipMalloc(&h->iters, sizeof(int32_t) * B);
   if (e == hipSuccess) e = hipHostMalloc(&h->host_status, sizeof(int32_t) * B, hipHostMallocDefault);
+  if (e == hipSuccess)
+    e = hipHostMalloc(&h->host_running, sizeof(int32_t) * 2, hipHostMallocMapped | hipHostMallocCoherent);
+  if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&h->dev_running, h->host_running, 0);
+  for (int c = 0; c < 2 && e == hipSuccess; ++c) e = hipEventCreateWithFlags(&h->ev_poll[c], hipEventDisableTiming);
   if (e == hipSuccess && ilqr::tl_supported(nx, nu))
     e = hipMalloc(&h->J, sizeof(double) * ilqr::tl_workspace_doubles(batch, T));
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking);
@@ -362,6 +371,9 @@ ilqr_status ilqr_destroy(ilqr_handle* h) {
   (void)hipFree(h->res_parity);
   (void)hipFree(h->iters);
   if (h->host_status) (void)hipHostFree(h->host_status);
+  if (h->host_running) (void)hipHostFree(h->host_running);
+  for (int c = 0; c < 2; ++c)
+    if (h->ev_poll[c]) (void)hipEventDestroy(h->ev_poll[c]);
   if (h->pad) {
     (void)ilqr_destroy(h->pad);
     for (double* q : {h->pA, h->pB, h->pQ, h->pR, h->pQf, h->px, h->pu, h->pxt, h->pxn, h->pun, h->pd, h->pK})
@@ -570,14 +582,27 @@ ilqr_status ilqr_fit(ilqr_handle* h, const ilqr_problem* p, const ilqr_options* 
   // the handle's buffer (it−1)&1) and writes buffer it&1 (x̄ⁱ, ūⁱ = x̄ⁱ⁺¹, ūⁱ⁺¹,
   // :174-175). `parity` records where a trajectory's result lies when it stops:
   // ilqr::PARITY_INPUT for the caller's buffers.
+  // The last iteration writes the caller's x_out / u_out directly (the gather then
+  // copies only trajectories that stopped earlier) unless they overlap an input.
+  const size_t xbytes = sizeof(double) * (size_t)h->batch * (h->T + 1) * h->nx;
+  const size_t ubytes = sizeof(double) * (size_t)h->batch * h->T * h->nu;
+  auto overlap = [](const void* a, size_t na, const void* b, size_t nb) {
+    const char *pa = (const char*)a, *pb = (const char*)b;
+    return b && pa < pb + nb && pb < pa + na;
+  };
+  const bool direct = o->max_iter > 0 && !overlap(x_out, xbytes, x_init, xbytes) &&
+                      !overlap(x_out, xbytes, x_traj, xbytes) && !overlap(u_out, ubytes, u_init, ubytes) &&
+                      !overlap(x_out, xbytes, u_init, ubytes) && !overlap(u_out, ubytes, x_init, xbytes) &&
+                      !overlap(u_out, ubytes, x_traj, xbytes);
   auto iter_args = [&](int it) {
     const int par = (it - 1) & 1;
+    const bool last = direct && it == o->max_iter;
     ilqr::IterArgs a{};
     a.x = it == 1 ? x_init : h->xbuf[par];
     a.u = it == 1 ? u_init : h->ubuf[par];
     a.xtraj = x_traj;
-    a.xnew = h->xbuf[par ^ 1];
-    a.unew = h->ubuf[par ^ 1];
+    a.xnew = last ? x_out : h->xbuf[par ^ 1];
+    a.unew = last ? u_out : h->ubuf[par ^ 1];
     a.K = h->K;
     a.d = h->d;
     a.prev_cost = h->prev_cost;  // in place: prev_cost = new_cost (:168)
@@ -603,10 +628,27 @@ ilqr_status ilqr_fit(ilqr_handle* h, const ilqr_problem* p, const ilqr_options* 
                                         iter_args(it - 1), ls, flags, s));
     }
   }
+  // With a convergence test (tol ≥ 0) the loop stops enqueueing once every trajectory
+  // has stopped, like the reference's `break` (:171): after iteration it a one-block
+  // kernel writes the running count to host-mapped memory behind an event, and the host
+  // reads iteration it−1's count while the GPU runs iteration it (no idle gap; at most
+  // one iteration of already-stopped waves is enqueued past the last useful one).
+  const bool poll = o->tol >= 0.0 && o->max_iter > 2;
   for (int it = 1; (two_link(p) || !h->pipelined) && it <= o->max_iter; ++it) {  // forward_pass.jl:161
     // iterations chain per chunk: chunk 0's next backward overlaps chunk 1's forward
     const ilqr_status st = enqueue_iteration(h, p, iter_args(it), ls, /*chain=*/true);
     if (st != ILQR_OK) return st;
+    if (!poll || it == o->max_iter) continue;
+    {
+      const ilqr_status js = join(h, p);
+      if (js != ILQR_OK) return js;
+    }
+    HIP_TRY(ilqr::launch_count_running(h->batch, h->status, h->dev_running + (it & 1), s));
+    HIP_TRY(hipEventRecord(h->ev_poll[it & 1], s));
+    if (it >= 2) {
+      HIP_TRY(hipEventSynchronize(h->ev_poll[(it - 1) & 1]));
+      if (__atomic_load_n(h->host_running + ((it - 1) & 1), __ATOMIC_ACQUIRE) == 0) break;
+    }
   }
   {
     const ilqr_status st = join(h, p);
@@ -614,7 +656,7 @@ ilqr_status ilqr_fit(ilqr_handle* h, const ilqr_problem* p, const ilqr_options* 
   }
   // still-running trajectories (max_iter reached) return the last accepted iterate,
   // the one the last iteration wrote (the input when max_iter = 0)
-  const int last = o->max_iter == 0 ? ilqr::PARITY_INPUT : (o->max_iter & 1);
+  const int last = o->max_iter == 0 ? ilqr::PARITY_INPUT : (direct ? ilqr::PARITY_OUT : (o->max_iter & 1));
   HIP_TRY(ilqr::launch_gather_result(h->batch, h->T, h->nx, h->nu, x_init, u_init, h->xbuf[0],
                                      h->ubuf[0], h->xbuf[1], h->ubuf[1], h->res_parity, h->status,
                                      last, h->prev_cost, h->iters, x_out, u_out, cost, iters,

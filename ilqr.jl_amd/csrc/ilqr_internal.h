@@ -78,6 +78,10 @@ hipError_t launch_lq_iter_pipe(int nx, int nu, const LQParams& p, int B, int T, 
 // Result buffer codes of the fit ping-pong: 0 / 1 the handle's buffers, PARITY_INPUT
 // the caller's x_init / u_init (iteration 1 reads them in place).
 constexpr int PARITY_INPUT = 2;
+// ... and PARITY_OUT the caller's x_out / u_out (fit's last iteration writes there
+// directly when they do not alias the inputs, so the gather copies only trajectories
+// that stopped earlier)
+constexpr int PARITY_OUT = 3;
 // fit's per-trajectory state: prev_cost = +Inf, status OK, res_parity INPUT, iters 0.
 hipError_t launch_fit_init(int B, double* prev_cost, int32_t* status, int32_t* res_parity,
                            int32_t* iters, hipStream_t s);
@@ -97,6 +101,8 @@ hipError_t launch_unpad3(const double* src, double* dst, size_t N, int R, int C,
                          hipStream_t s);
 hipError_t launch_fill_i32(int32_t* p, int n, int32_t v, hipStream_t s);
 hipError_t launch_fill_f64(double* p, int n, double v, hipStream_t s);
+// *out = #trajectories with status OK (out may be host-mapped memory)
+hipError_t launch_count_running(int B, const int32_t* status, int32_t* out, hipStream_t s);
 bool lq_supported(int nx, int nu);
 
 // Caller-supplied derivative tiles (ilqr_tiles in include/ilqr.h), device pointers.

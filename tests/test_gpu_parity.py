@@ -511,3 +511,29 @@ def test_ring_forward_pass_api_equals_register_ring(gpu, nb, T):
     for a, b in zip(*outs):
         torch.testing.assert_close(a, b, rtol=0, atol=0, equal_nan=True)
     assert (outs[1][4][::3].cpu().numpy() == _lib.TRAJ_LS_EXHAUSTED).all()
+
+
+@pytest.mark.parametrize("max_iter,tol", [(1, -1.0), (3, -1.0), (6, 1e-8), (40, 1e-9)])
+def test_fit_output_aliasing_input(gpu, max_iter, tol):
+    """fit's last iteration writes the caller's x_out/u_out directly unless they
+    overlap an input; in-place (x_out = x_init) calls take the gather path and return
+    the same bits. Covers trajectories that converge before and at the last iteration."""
+    import ctypes as C
+    nb, T = 37, 20
+    lq, x, u = random_lq_batch(nb, 12, 4, T, seed=21)
+    s = Solver(12, 4, T, nb)
+    s.set_problem(lq)
+    ref = s.fit(dev(x), dev(u), max_iter=max_iter, tol=tol)
+    xi, ui = dev(x), dev(u)
+    cost = torch.empty((nb,), dtype=torch.float64, device="cuda")
+    it = torch.empty((nb,), dtype=torch.int32, device="cuda")
+    st = torch.empty((nb,), dtype=torch.int32, device="cuda")
+    s._bind_stream()
+    o = _lib.default_options(max_iter=max_iter, tol=tol)
+    p = C.c_void_p
+    rc = s.lib.ilqr_fit(s.h, s._p(), C.byref(o), p(xi.data_ptr()), p(ui.data_ptr()), None,
+                        p(xi.data_ptr()), p(ui.data_ptr()), p(cost.data_ptr()), p(it.data_ptr()),
+                        p(st.data_ptr()))
+    assert rc == ref.call_status
+    assert torch.equal(xi, ref.x) and torch.equal(ui, ref.u) and torch.equal(it, ref.iters)
+    assert torch.equal(st, ref.status) and torch.equal(cost, ref.cost)
