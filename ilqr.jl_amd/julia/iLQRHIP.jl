@@ -1,18 +1,32 @@
-# iLQRHIP.jl — Julia-side drop-in for aabouman/iLQR.jl's hot path over the C ABI
-# of libilqr_hip.so (include/ilqr.h). Not executable in this build environment (no
-# Julia toolchain); the same symbols and layouts are exercised from Python by
-# tests/test_gpu_parity.py and tests/test_abi.py.
+# iLQRHIP.jl — Julia-side drop-in for aabouman/iLQR.jl's hot path over the C ABI of
+# libilqr_hip.so (include/ilqr.h). Not executable in this build environment (no Julia
+# toolchain); every ccall below is exercised from Python with the same symbols and the
+# same memory layouts by tests/test_gpu_julia_layout.py (tests/julia_layout.py restates
+# this file's permutedims conventions on Fortran-ordered arrays).
 #
-# It keeps the reference's public signatures:
+# It keeps the reference's public signatures and error behaviour:
 #   fit(x_init, u_init, dynamicsf, immediate_cost, final_cost; x_traj, max_iter, tol)
-#                                                     (reference src/forward_pass.jl:148-179)
-#   backward_pass(x, u, dynamicsf, immediate_cost, final_cost) -> (δu, K)
-#                                                     (reference src/backward_pass.jl:324-357)
+#                                            -> (x̄, ū)          reference src/forward_pass.jl:148-179
+#   backward_pass(x, u, dynamicsf, immediate_cost, final_cost)
+#                                            -> (δu, K)         reference src/backward_pass.jl:324-357
 #   forward_pass(x, u, x_traj, δu, K, prev_cost, dynamicsf, immediate_cost, final_cost)
-#                                                     (reference src/forward_pass.jl:55-93)
-# for the LQ problem family, whose closures are the callable structs below, and
-# adds a batched `solve!(::iLQRProblem)`.
+#                                            -> (x̄, ū, cost)    reference src/forward_pass.jl:55-93
+# and dispatches on the closures:
+#   * LinearDynamics / QuadraticCost / QuadraticFinalCost  → ILQR_PROBLEM_LQ (all on the GPU);
+#   * TwoLinkDynamics{NU} / TwoLinkCost / TwoLinkFinalCost → ILQR_PROBLEM_TWO_LINK (all on the
+#     GPU; these callable structs evaluate test/2_link_example/2_link_helper_functions.jl
+#     on the host too, so they ARE the reference's closures);
+#   * any other Julia closures → ILQR_PROBLEM_TILES: ForwardDiff on the host produces the
+#     per-step derivative tiles exactly as the reference's backward_pass.jl:32-33, 95-99,
+#     142-143 do, the Riccati recursion runs on the GPU (ilqr_backward_tiles), and the
+#     forward pass rolls the user's closure out on the host (a Julia closure cannot run on
+#     the device; this is the reference's own forward_pass.jl:70-87 loop with the line
+#     search capped).
+# New API: `solve!(::iLQRProblem)` (batched LQ, one or several GPUs) and `chain_fit`
+# (the RBD family of BASELINE config 5).
 module iLQRHIP
+
+using ForwardDiff: gradient, jacobian, hessian   # as the reference (src/iLQR.jl:3)
 
 const libilqr = joinpath(@__DIR__, "..", "lib", "libilqr_hip.so")
 
@@ -21,6 +35,9 @@ const ILQR_ERR_BAD_DIMS = Int32(1)
 const ILQR_ERR_NAN = Int32(5)
 const ILQR_ERR_LS_EXHAUSTED = Int32(6)
 const ILQR_PROBLEM_LQ = Int32(1)
+const ILQR_PROBLEM_TWO_LINK = Int32(2)
+const ILQR_PROBLEM_TILES = Int32(3)
+const ILQR_TRAJ_NAN = Int32(4)
 
 struct Problem               # ilqr_problem
     kind::Int32
@@ -30,6 +47,11 @@ struct Problem               # ilqr_problem
     Q::Ptr{Float64}
     R::Ptr{Float64}
     Qf::Ptr{Float64}
+end
+
+struct Tiles                 # ilqr_tiles: per-step derivatives of an arbitrary problem
+    A::Ptr{Float64}; B::Ptr{Float64}; lx::Ptr{Float64}; lu::Ptr{Float64}; lxx::Ptr{Float64}
+    lux::Ptr{Float64}; luu::Ptr{Float64}; lfx::Ptr{Float64}; lfxx::Ptr{Float64}
 end
 
 mutable struct Options       # ilqr_options
@@ -47,6 +69,10 @@ function default_options()
     return o
 end
 
+"""The reference's line search (forward_pass.jl:70-87) loops forever when no step lowers
+the cost; the device stops after `max_trials` halvings and the shim throws this."""
+struct LineSearchExhausted <: Exception end
+
 # -- the reference's callbacks, as recognisable callable structs ------------------
 struct LinearDynamics{M<:AbstractMatrix}; A::M; B::M; end
 (f::LinearDynamics)(x, u) = f.A * x + f.B * u                      # dynamicsf(x, u)
@@ -55,11 +81,60 @@ struct QuadraticCost{M<:AbstractMatrix}; Q::M; R::M; end
 struct QuadraticFinalCost{M<:AbstractMatrix}; Qf::M; end
 (l::QuadraticFinalCost)(x) = x' * l.Qf * x                         # final_cost(x)
 
-check(st, what) = st == ILQR_OK ? nothing :
-    st == ILQR_ERR_BAD_DIMS ? throw(AssertionError("N == M+1")) :
-    error("$what: " * unsafe_string(ccall((:ilqr_status_string, libilqr), Cstring, (Cint,), st)))
+# test/2_link_example/2_link_helper_functions.jl:4-108 with the same expression order
+# (the CoriolisMatrix quirk `for k in length(θ)` → k = 2 only, :42-44). NU = 1 is the
+# build-defined f(x, [u₁, 0]) of BASELINE configs 1-2 (not reference-pinned).
+module TwoLinkConsts
+    const l₁ = sqrt(2.) / 2.; const l₂ = sqrt(2.) / 2.
+    const r₁ = 0.5 * l₁; const r₂ = 0.5 * l₂
+    const m₁ = 1.0; const m₂ = 1.0
+    const Iz1 = 1.0 / 12.0 * m₁ * l₁^2; const Iz2 = 1.0 / 12.0 * m₂ * l₂^2
+    const α = Iz1 + Iz2 + m₁ * r₁^2 + m₂ * (l₁^2 + r₂^2)
+    const β = m₂ * l₁ * r₂
+    const δ = Iz2 + m₂ * r₂^2
+    const Δt = 0.01
+    function ik(x, y)                                               # InverseKinematics (:19-26)
+        q₂ = acos((x^2 + y^2 - l₁^2 - l₂^2) / (2 * l₁ * l₂))
+        q₁ = atan(y, x) - atan(l₂ * sin(q₂), l₁ + l₂ * cos(q₂))
+        return [q₁, q₂]
+    end
+    const θstar = ik(0.6, -0.5)                                     # target_tool_loc (:16)
+end
 
-# device buffer owned by Julia (freed with the handle)
+struct TwoLinkDynamics{NU} end
+TwoLinkDynamics(nu::Integer=2) = (nu in (1, 2) || throw(ArgumentError("nu ∈ (1, 2)")); TwoLinkDynamics{nu}())
+function _tl_continuous(x, w)
+    C = TwoLinkConsts
+    c2 = cos(x[2]); s2 = sin(x[2])
+    M = [C.α+2*C.β*c2 C.δ+C.β*c2; C.δ+C.β*c2 C.δ]                 # InertiaMatrix (:29-33)
+    dM11 = 2 * C.β * -s2; dM12 = C.β * -s2                          # ∂M/∂θ₂ (the nested jacobian, :37)
+    Cm = [1/2*dM11*x[4] 1/2*dM12*x[4]; 1/2*dM12*x[4] zero(dM11)]   # CoriolisMatrix, k = 2 only
+    acc = -(M \ Cm) * x[3:4] + inv(M) * w                           # :56-66
+    return [x[3], x[4], acc[1], acc[2]]
+end
+function (f::TwoLinkDynamics{NU})(x, u) where {NU}                 # RK4 (:71-78)
+    w = NU == 2 ? u : [u[1], zero(eltype(u))]
+    Δt = TwoLinkConsts.Δt
+    k1 = Δt * _tl_continuous(x, w)
+    k2 = Δt * _tl_continuous(x + k1 / 2, w)
+    k3 = Δt * _tl_continuous(x + k2 / 2, w)
+    k4 = Δt * _tl_continuous(x + k3, w)
+    return x + (1 / 6) * (k1 + 2 * k2 + 2 * k3 + k4)
+end
+struct TwoLinkCost end                                              # immediate_cost (:82-97)
+(::TwoLinkCost)(x, u) = sum((TwoLinkConsts.θstar .- x[1:2]) .^ 2) * 1.0 + sum(u .^ 2) * 1.0
+struct TwoLinkFinalCost end                                         # final_cost (:100-108)
+(::TwoLinkFinalCost)(x) = sum((TwoLinkConsts.θstar .- x[1:2]) .^ 2) * 1.0
+
+function check(st, what)
+    st == ILQR_OK && return nothing
+    st == ILQR_ERR_BAD_DIMS && throw(AssertionError("N == M+1"))           # backward_pass.jl:329
+    st == ILQR_ERR_NAN && throw(AssertionError("!any(isnan, ...)"))        # backward_pass.jl:353, forward_pass.jl:89
+    st == ILQR_ERR_LS_EXHAUSTED && throw(LineSearchExhausted())
+    error("$what: " * unsafe_string(ccall((:ilqr_status_string, libilqr), Cstring, (Cint,), st)))
+end
+
+# a handle bound to device 0 plus the device buffers it owns (freed with it)
 mutable struct Handle
     ptr::Ptr{Cvoid}
     bufs::Vector{Ptr{Cvoid}}
@@ -85,20 +160,18 @@ const ILQR_SCHED_BACKWARD_BLOCK = Int32(8)
 set_schedule!(h::Handle, flags::Integer) =
     check(ccall((:ilqr_set_schedule, libilqr), Cint, (Ptr{Cvoid}, Cint), h.ptr, flags), "ilqr_set_schedule")
 
-function upload(h::Handle, a::Array{Float64})
-    p = Ref{Ptr{Cvoid}}(C_NULL)
-    check(ccall((:ilqr_malloc, libilqr), Cint, (Ptr{Cvoid}, Csize_t, Ref{Ptr{Cvoid}}), h.ptr, sizeof(a), p), "ilqr_malloc")
-    push!(h.bufs, p[])
-    check(ccall((:ilqr_memcpy_h2d, libilqr), Cint, (Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Csize_t),
-                h.ptr, p[], a, sizeof(a)), "ilqr_memcpy_h2d")
-    return Ptr{Float64}(p[])
-end
-
 function alloc(h::Handle, T::Type, n)
     p = Ref{Ptr{Cvoid}}(C_NULL)
-    check(ccall((:ilqr_malloc, libilqr), Cint, (Ptr{Cvoid}, Csize_t, Ref{Ptr{Cvoid}}), h.ptr, n * sizeof(T), p), "ilqr_malloc")
+    check(ccall((:ilqr_malloc, libilqr), Cint, (Ptr{Cvoid}, Csize_t, Ref{Ptr{Cvoid}}), h.ptr, max(n, 1) * sizeof(T), p), "ilqr_malloc")
     push!(h.bufs, p[])
     return Ptr{T}(p[])
+end
+
+function upload(h::Handle, a::Array{T}) where {T}
+    p = alloc(h, T, length(a))
+    check(ccall((:ilqr_memcpy_h2d, libilqr), Cint, (Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Csize_t),
+                h.ptr, p, a, sizeof(a)), "ilqr_memcpy_h2d")
+    return p
 end
 
 function download!(h::Handle, a::Array, p::Ptr)
@@ -107,26 +180,78 @@ function download!(h::Handle, a::Array, p::Ptr)
     return a
 end
 
-# Reference layout per trajectory: x (N × nx) rows = time steps. The ABI's
-# layout for one trajectory is (nx, N) column-major == permutedims(x).
+# -- layouts ------------------------------------------------------------------------
+# The reference's per-trajectory matrices are row-per-timestep (x::(N × nx), column-
+# major: time fastest). The ABI's trajectory is C row-major (N, nx) = Julia (nx, N):
+# permutedims for one trajectory, no copy for batched (nx, N, batch) arrays. A C
+# row-major (r, c) matrix is the Julia transpose; K (T, nu, nx) row-major comes back
+# as Julia (nx, nu, T) and is permuted to the reference's 𝐊s (T × nu × nx).
 to_abi(x::AbstractMatrix) = Array{Float64}(permutedims(x))
 from_abi(a::AbstractMatrix) = permutedims(a)
+gains_from_abi(K::Array{Float64,3}) = permutedims(K, (3, 2, 1))
+gains_to_abi(K::AbstractArray{<:Real,3}) = Array{Float64}(permutedims(K, (3, 2, 1)))
+rowmajor(M::AbstractMatrix) = Array{Float64}(permutedims(M))
+# batched per-instance matrices (r, c, batch) → C (batch, r, c): each matrix transposed
+rowmajor3(A::AbstractArray{<:Real,3}) = Array{Float64}(permutedims(A, (2, 1, 3)))
+
+# -- problem families -----------------------------------------------------------------
+const LQTriple = Tuple{LinearDynamics,QuadraticCost,QuadraticFinalCost}
+const TwoLinkTriple = Tuple{TwoLinkDynamics,TwoLinkCost,TwoLinkFinalCost}
+family(f, l, lf) = (f, l, lf) isa LQTriple ? :lq : (f, l, lf) isa TwoLinkTriple ? :two_link : :tiles
 
 function problem(h::Handle, f::LinearDynamics, l::QuadraticCost, lf::QuadraticFinalCost)
-    # C row-major (nx, nx) == Julia transpose
-    A = upload(h, Array{Float64}(permutedims(f.A))); B = upload(h, Array{Float64}(permutedims(f.B)))
-    Q = upload(h, Array{Float64}(permutedims(l.Q))); R = upload(h, Array{Float64}(permutedims(l.R)))
-    Qf = upload(h, Array{Float64}(permutedims(lf.Qf)))
-    return Problem(ILQR_PROBLEM_LQ, 0, A, B, Q, R, Qf)
+    return Problem(ILQR_PROBLEM_LQ, 0, upload(h, rowmajor(f.A)), upload(h, rowmajor(f.B)),
+                   upload(h, rowmajor(l.Q)), upload(h, rowmajor(l.R)), upload(h, rowmajor(lf.Qf)))
+end
+problem(h::Handle, f::TwoLinkDynamics, l::TwoLinkCost, lf::TwoLinkFinalCost) =
+    Problem(ILQR_PROBLEM_TWO_LINK, 0, C_NULL, C_NULL, C_NULL, C_NULL, C_NULL)
+
+nu_of(::TwoLinkDynamics{NU}) where {NU} = NU
+
+# Per-step derivative tiles of arbitrary closures on the host, exactly the reference's
+# calls: linearize_dynamics (backward_pass.jl:32-33), immediate_cost_quadratization
+# (:95-99; 𝐏 = jacobian of ∂L∂u w.r.t. x, nu × nx) and final_cost_quadratization
+# (:142-143). Returned in the ABI's row-major per-step layout (ilqr_tiles).
+function derivative_tiles(x::AbstractMatrix, u::AbstractMatrix, f, ℓ, ℓf)
+    N, nx = size(x); M, nu = size(u)
+    A = zeros(nx, nx, M); B = zeros(nu, nx, M); lx = zeros(nx, M); lu = zeros(nu, M)
+    lxx = zeros(nx, nx, M); lux = zeros(nx, nu, M); luu = zeros(nu, nu, M)
+    for i in 1:M
+        xi = x[i, :]; ui = u[i, :]
+        A[:, :, i] = permutedims(jacobian(z -> f(z, ui), xi))          # :32
+        B[:, :, i] = permutedims(jacobian(v -> f(xi, v), ui))          # :33
+        ∂L∂u(z, v) = gradient(w -> ℓ(z, w), v)
+        lx[:, i] = gradient(z -> ℓ(z, ui), xi)                          # :95
+        lu[:, i] = ∂L∂u(xi, ui)                                         # :96
+        lxx[:, :, i] = permutedims(hessian(z -> ℓ(z, ui), xi))          # :97
+        lux[:, :, i] = permutedims(jacobian(z -> ∂L∂u(z, ui), xi))      # :98 (𝐏, nu × nx)
+        luu[:, :, i] = permutedims(hessian(v -> ℓ(xi, v), ui))          # :99
+    end
+    xN = x[N, :]
+    lfx = gradient(ℓf, xN)                                              # :142
+    lfxx = permutedims(hessian(ℓf, xN))                                 # :143
+    return (A=A, B=B, lx=lx, lu=lu, lxx=lxx, lux=lux, luu=luu, lfx=lfx, lfxx=lfxx)
 end
 
-problem(h::Handle, f, l, lf) =
-    throw(ArgumentError("the HIP path runs the LQ family: pass LinearDynamics / QuadraticCost / QuadraticFinalCost"))
+function backward_tiles_device(x::AbstractMatrix, u::AbstractMatrix, f, ℓ, ℓf)
+    N, nx = size(x); M, nu = size(u)
+    h = Handle(nx, nu, M, 1)
+    t = derivative_tiles(x, u, f, ℓ, ℓf)
+    tl = Ref(Tiles(upload(h, t.A), upload(h, t.B), upload(h, t.lx), upload(h, t.lu), upload(h, t.lxx),
+                   upload(h, t.lux), upload(h, t.luu), upload(h, t.lfx), upload(h, t.lfxx)))
+    dd = alloc(h, Float64, M * nu); Kd = alloc(h, Float64, M * nu * nx); st = alloc(h, Int32, 1)
+    check(ccall((:ilqr_backward_tiles, libilqr), Cint,
+                (Ptr{Cvoid}, Ref{Tiles}, Ref{Options}, Ptr{Float64}, Ptr{Float64}, Ptr{Int32}),
+                h.ptr, tl, default_options(), dd, Kd, st), "ilqr_backward_tiles")
+    return from_abi(download!(h, zeros(nu, M), dd)), gains_from_abi(download!(h, zeros(nx, nu, M), Kd))
+end
 
 """backward_pass(x, u, dynamicsf, immediate_cost, final_cost) -> (δu::T×nu, K::T×nu×nx)"""
 function backward_pass(x::AbstractMatrix, u::AbstractMatrix, dynamicsf, immediate_cost, final_cost)
     N, nx = size(x); M, nu = size(u)
-    @assert(N == M + 1)
+    @assert(N == M + 1)                                                 # backward_pass.jl:329
+    family(dynamicsf, immediate_cost, final_cost) == :tiles &&
+        return backward_tiles_device(x, u, dynamicsf, immediate_cost, final_cost)
     h = Handle(nx, nu, M, 1)
     p = Ref(problem(h, dynamicsf, immediate_cost, final_cost))
     xd = upload(h, to_abi(x)); ud = upload(h, to_abi(u))
@@ -135,17 +260,73 @@ function backward_pass(x::AbstractMatrix, u::AbstractMatrix, dynamicsf, immediat
     check(ccall((:ilqr_backward, libilqr), Cint,
                 (Ptr{Cvoid}, Ref{Problem}, Ref{Options}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Int32}),
                 h.ptr, p, default_options(), xd, ud, dd, Kd, st), "ilqr_backward")
-    du = from_abi(download!(h, zeros(nu, M), dd))                     # (T × nu)
-    Kabi = download!(h, zeros(nx, nu, M), Kd)                          # C (T, nu, nx) row-major
-    K = permutedims(Kabi, (3, 2, 1))                                   # (T × nu × nx) like 𝐊s
+    du = from_abi(download!(h, zeros(nu, M), dd))                       # (T × nu)
+    K = gains_from_abi(download!(h, zeros(nx, nu, M), Kd))              # (T × nu × nx) like 𝐊s
     return du, K
+end
+
+# total_cost_generator (forward_pass.jl:182-196), for the host rollout of the tiles path
+function total_cost(x̄, ū, x_traj, ℓ, ℓf)
+    s = 0.
+    for i in 1:size(ū, 1)
+        s += ℓ(x̄[i, :] - x_traj[i, :], ū[i, :])
+    end
+    return s + ℓf(x̄[end, :])
+end
+
+# forward_pass.jl:55-93 for a closure the device cannot run: the reference's loop on the
+# host (it must call the user's Julia dynamicsf), the unbounded search capped at max_trials
+function forward_host(x, u, x_traj, δu, K, prev_cost, f, ℓ, ℓf; max_trials=default_options().max_trials)
+    N, nx = size(x); M, nu = size(u)
+    x̄ = zeros(eltype(x), N, nx); ū = zeros(eltype(u), M, nu)
+    x̄[1, :] .= x[1, :]
+    α = 1.0; new_cost = 0.0
+    for trial in 1:max_trials
+        for k in 1:M
+            δx = x̄[k, :] - x[k, :]
+            ū[k, :] .= u[k, :] + α * δu[k, :] + K[k, :, :] * δx
+            x̄[k+1, :] .= f(x̄[k, :], ū[k, :])
+        end
+        new_cost = total_cost(x̄, ū, x_traj, ℓ, ℓf)
+        prev_cost - new_cost > 0 && break
+        trial == max_trials && throw(LineSearchExhausted())
+        α /= 2
+    end
+    @assert !any(isnan, ū)                                              # forward_pass.jl:89
+    @assert !any(isnan, x̄)                                              # forward_pass.jl:90
+    return (x̄, ū, new_cost)
+end
+
+"""forward_pass(x, u, x_traj, δu, K, prev_cost, dynamicsf, immediate_cost, final_cost) -> (x̄, ū, new_cost)"""
+function forward_pass(x::AbstractMatrix, u::AbstractMatrix, x_traj::AbstractMatrix, δu::AbstractMatrix,
+                      K::AbstractArray{<:Real,3}, prev_cost::Real, dynamicsf, immediate_cost, final_cost)
+    N, nx = size(x); M, nu = size(u)
+    @assert(N == M + 1)                                                 # forward_pass.jl:62
+    family(dynamicsf, immediate_cost, final_cost) == :tiles &&
+        return forward_host(x, u, x_traj, δu, K, prev_cost, dynamicsf, immediate_cost, final_cost)
+    h = Handle(nx, nu, M, 1)
+    p = Ref(problem(h, dynamicsf, immediate_cost, final_cost))
+    xd = upload(h, to_abi(x)); ud = upload(h, to_abi(u)); xt = upload(h, to_abi(x_traj))
+    dd = upload(h, to_abi(δu)); Kd = upload(h, gains_to_abi(K))
+    pc = upload(h, Float64[prev_cost])
+    xo = alloc(h, Float64, N * nx); uo = alloc(h, Float64, M * nu); co = alloc(h, Float64, 1)
+    st = alloc(h, Int32, 1)
+    check(ccall((:ilqr_forward, libilqr), Cint,
+                (Ptr{Cvoid}, Ref{Problem}, Ref{Options}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64},
+                 Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64},
+                 Ptr{Int32}, Ptr{Int32}),
+                h.ptr, p, default_options(), xd, ud, xt, dd, Kd, pc, xo, uo, co, C_NULL, st), "ilqr_forward")
+    x̄ = from_abi(download!(h, zeros(nx, N), xo)); ū = from_abi(download!(h, zeros(nu, M), uo))
+    return (x̄, ū, download!(h, zeros(1), co)[1])
 end
 
 """fit(x_init, u_init, dynamicsf, immediate_cost, final_cost; x_traj, max_iter, tol) -> (x̄, ū)"""
 function fit(x_init::AbstractMatrix, u_init::AbstractMatrix, dynamicsf, immediate_cost, final_cost;
              x_traj=zero(x_init), max_iter::Int64=100, tol::Float64=1e-6)
     N, nx = size(x_init); M, nu = size(u_init)
-    @assert(N == M + 1, "size(x_init)[2] == size(u_init)[1]")
+    @assert(N == M + 1, "size(x_init)[2] == size(u_init)[1]")          # forward_pass.jl:156
+    family(dynamicsf, immediate_cost, final_cost) == :tiles &&
+        return fit_tiles(x_init, u_init, dynamicsf, immediate_cost, final_cost, x_traj, max_iter, tol)
     h = Handle(nx, nu, M, 1)
     p = Ref(problem(h, dynamicsf, immediate_cost, final_cost))
     o = default_options(); o.max_iter = max_iter; o.tol = tol
@@ -155,9 +336,28 @@ function fit(x_init::AbstractMatrix, u_init::AbstractMatrix, dynamicsf, immediat
                (Ptr{Cvoid}, Ref{Problem}, Ref{Options}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64},
                 Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Int32}, Ptr{Int32}),
                h.ptr, p, o, xi, ui, xt, xo, uo, C_NULL, C_NULL, C_NULL)
-    st == ILQR_ERR_NAN && throw(AssertionError("!any(isnan, ...)"))
-    st == ILQR_ERR_LS_EXHAUSTED || check(st, "ilqr_fit")
+    st == ILQR_ERR_LS_EXHAUSTED || check(st, "ilqr_fit")   # exhausted: the last iterate is returned
     return from_abi(download!(h, zeros(nx, N), xo)), from_abi(download!(h, zeros(nu, M), uo))
+end
+
+# fit (forward_pass.jl:148-179) for arbitrary closures: tiles backward on the GPU, host
+# rollout; same return semantics (the iterate before the update that met tol, :171)
+function fit_tiles(x_init, u_init, f, ℓ, ℓf, x_traj, max_iter, tol)
+    x̄ⁱ = x_init; ūⁱ = u_init
+    prev_cost = Inf
+    for iter in 1:max_iter
+        δu, K = backward_tiles_device(x̄ⁱ, ūⁱ, f, ℓ, ℓf)                 # :162
+        x̄ⁱ⁺¹, ūⁱ⁺¹, new_cost = try                                      # :163-166
+            forward_host(x̄ⁱ, ūⁱ, x_traj, δu, K, prev_cost, f, ℓ, ℓf)
+        catch e
+            e isa LineSearchExhausted && break     # the reference would loop forever here
+            rethrow()
+        end
+        @assert(prev_cost > new_cost); prev_cost = new_cost             # :168
+        convert(Float64, sum((ūⁱ⁺¹ - ūⁱ) .^ 2)) <= tol && break          # :171
+        x̄ⁱ = x̄ⁱ⁺¹; ūⁱ = ūⁱ⁺¹                                           # :174-175
+    end
+    return (x̄ⁱ, ūⁱ)
 end
 
 """Batched problem (new API): per-instance A (nx,nx,B) … and trajectories (nx, N, B)."""
@@ -170,12 +370,10 @@ end
 function solve!(prob::iLQRProblem; max_iter::Int64=100, tol::Float64=1e-6)
     nx, N, nb = size(prob.x); nu = size(prob.u, 1); M = N - 1
     h = Handle(nx, nu, M, nb)
-    # Julia (nx, nx, B) column-major is C (B, nx, nx) with each matrix transposed
-    tr(a) = Array{Float64}(permutedims(a, (2, 1, 3)))
-    p = Ref(Problem(ILQR_PROBLEM_LQ, 0, upload(h, tr(prob.A)), upload(h, tr(prob.B)), upload(h, tr(prob.Q)),
-                    upload(h, tr(prob.R)), upload(h, tr(prob.Qf))))
+    p = Ref(Problem(ILQR_PROBLEM_LQ, 0, upload(h, rowmajor3(prob.A)), upload(h, rowmajor3(prob.B)),
+                    upload(h, rowmajor3(prob.Q)), upload(h, rowmajor3(prob.R)), upload(h, rowmajor3(prob.Qf))))
     o = default_options(); o.max_iter = max_iter; o.tol = tol
-    xi = upload(h, prob.x); ui = upload(h, prob.u)
+    xi = upload(h, prob.x); ui = upload(h, prob.u)                      # (nx, N, B) is the ABI layout as is
     xo = alloc(h, Float64, length(prob.x)); uo = alloc(h, Float64, length(prob.u))
     st = ccall((:ilqr_fit, libilqr), Cint,
                (Ptr{Cvoid}, Ref{Problem}, Ref{Options}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64},
@@ -194,8 +392,7 @@ function solve!(prob::iLQRProblem, devices::Vector{Int}; max_iter::Int64=100, to
     check(ccall((:ilqr_multi_create, libilqr), Cint,
                 (Ref{Ptr{Cvoid}}, Ptr{Cint}, Cint, Cint, Cint, Cint, Cint),
                 r, Cint.(devices), length(devices), nx, nu, M, nb), "ilqr_multi_create")
-    tr(a) = Array{Float64}(permutedims(a, (2, 1, 3)))
-    A, B, Q, R, Qf = tr(prob.A), tr(prob.B), tr(prob.Q), tr(prob.R), tr(prob.Qf)
+    A, B, Q, R, Qf = rowmajor3(prob.A), rowmajor3(prob.B), rowmajor3(prob.Q), rowmajor3(prob.R), rowmajor3(prob.Qf)
     try
         GC.@preserve A B Q R Qf begin
             p = Ref(Problem(ILQR_PROBLEM_LQ, 0, pointer(A), pointer(B), pointer(Q), pointer(R), pointer(Qf)))
@@ -243,16 +440,12 @@ function chain_fit(c::Chain, x_init::Array{E,3}, u_init::Array{E,3}; max_iter::I
                 (Ref{Ptr{Cvoid}}, Cint, Ref{Chain}, Cint, Cint, Int32, Int32),
                 r, 0, c, M, nb, dt, linearization), "ilqr_chain_create")
     h = Handle(nx, nu, M, 1)                 # device-memory helper only
-    dev(a) = (p = alloc(h, E, length(a));
-              check(ccall((:ilqr_memcpy_h2d, libilqr), Cint, (Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Csize_t),
-                          h.ptr, p, a, sizeof(a)), "ilqr_memcpy_h2d"); p)
-    xi = dev(x_init); ui = dev(u_init)
+    xi = upload(h, x_init); ui = upload(h, u_init)
     xo = alloc(h, E, length(x_init)); uo = alloc(h, E, length(u_init)); sd = alloc(h, Int32, nb)
     o = default_options(); o.max_iter = max_iter; o.tol = tol
     st = ccall((:ilqr_chain_fit, libilqr), Cint,
                (Ptr{Cvoid}, Ref{Options}, Ptr{E}, Ptr{E}, Ptr{E}, Ptr{E}, Ptr{E}, Ptr{E}, Ptr{Int32}, Ptr{Int32}),
                r[], o, xi, ui, C_NULL, xo, uo, C_NULL, C_NULL, sd)
-    st == ILQR_ERR_NAN && throw(AssertionError("!any(isnan, ...)"))
     st == ILQR_ERR_LS_EXHAUSTED || check(st, "ilqr_chain_fit")
     x = download!(h, similar(x_init), xo); u = download!(h, similar(u_init), uo)
     status = download!(h, zeros(Int32, nb), sd)

@@ -1,0 +1,231 @@
+"""The Julia shim's boundary, exercised without Julia: every entry point of
+ilqr.jl_amd/julia/iLQRHIP.jl replayed through the same C symbols with the same
+buffers — the column-major memory of the Julia arrays the shim builds (its
+permutedims conventions restated in tests/julia_layout.py), uploaded with the ABI's
+own ilqr_malloc / ilqr_memcpy_h2d and read back with ilqr_memcpy_d2h, exactly as the
+shim does — and compared with the oracle in the reference's layout (x::(N×nx),
+δu::(T×nu), 𝐊s::(T×nu×nx)).
+
+Covers: backward_pass / forward_pass / fit on the LQ family (per-trajectory
+`to_abi`, `gains_to_abi`/`gains_from_abi`), the 2-link structs (nu = 2 and the nu = 1
+variant) dispatched to ILQR_PROBLEM_TWO_LINK, the TILES fallback for arbitrary closures
+(host derivative tiles → ilqr_backward_tiles), and batched solve! ((2,1,3) per-instance
+matrices, (nx, N, B) trajectories).
+"""
+import ctypes as C
+import os
+
+import numpy as np
+import pytest
+
+import julia_layout as J
+from ilqr_amd import _lib
+from oracle import ilqr_oracle as O
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def load(name):
+    z = np.load(os.path.join(GOLD, name + ".npz"), allow_pickle=False)
+    return {k: z[k] for k in z.files}
+
+
+def rel(a, b):
+    a, b = np.asarray(a, float), np.asarray(b, float)
+    return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-300))
+
+
+class Handle:
+    """iLQRHIP.Handle: ilqr_create + buffers from ilqr_malloc, freed with it."""
+
+    def __init__(self, nx, nu, T, batch):
+        self.lib = _lib.load()
+        h = C.c_void_p()
+        _lib.check(self.lib.ilqr_create(C.byref(h), 0, nx, nu, T, batch), "ilqr_create")
+        self.h, self.bufs = h, []
+
+    def alloc(self, dtype, n):
+        p = C.c_void_p()
+        _lib.check(self.lib.ilqr_malloc(self.h, max(n, 1) * np.dtype(dtype).itemsize, C.byref(p)), "ilqr_malloc")
+        self.bufs.append(p)
+        return p
+
+    def upload(self, a, dtype=np.float64):
+        buf = np.ascontiguousarray(J.memory(a).astype(dtype))
+        p = self.alloc(dtype, buf.size)
+        _lib.check(self.lib.ilqr_memcpy_h2d(self.h, p, buf.ctypes.data_as(C.c_void_p), buf.nbytes), "h2d")
+        return p
+
+    def download(self, shape, p, dtype=np.float64):
+        buf = np.empty(int(np.prod(shape)), dtype=dtype)
+        _lib.check(self.lib.ilqr_memcpy_d2h(self.h, buf.ctypes.data_as(C.c_void_p), p, buf.nbytes), "d2h")
+        return J.from_memory(buf, shape)
+
+    def close(self):
+        for p in self.bufs:
+            self.lib.ilqr_free(self.h, p)
+        self.lib.ilqr_destroy(self.h)
+
+
+def lq_problem(h, A, B, Q, R, Qf):
+    """iLQRHIP.problem(h, ::LinearDynamics, ::QuadraticCost, ::QuadraticFinalCost)."""
+    return _lib.Problem(_lib.PROBLEM_LQ, 0, *(h.upload(J.rowmajor(M)).value for M in (A, B, Q, R, Qf)))
+
+
+def tl_problem():
+    return _lib.Problem(_lib.PROBLEM_TWO_LINK, 0, None, None, None, None, None)
+
+
+def shim_backward(prob_fn, x, u):
+    """iLQRHIP.backward_pass for a device family."""
+    N, nx = x.shape
+    M, nu = u.shape
+    h = Handle(nx, nu, M, 1)
+    p = prob_fn(h)
+    xd, ud = h.upload(J.to_abi(x)), h.upload(J.to_abi(u))
+    dd, Kd, st = h.alloc(np.float64, M * nu), h.alloc(np.float64, M * nu * nx), h.alloc(np.int32, 1)
+    _lib.check(h.lib.ilqr_backward(h.h, C.byref(p), C.byref(_lib.default_options()), xd, ud, dd, Kd, st),
+               "ilqr_backward")
+    du = J.from_abi(h.download((nu, M), dd))
+    K = J.gains_from_abi(h.download((nx, nu, M), Kd))
+    h.close()
+    return du, K
+
+
+def shim_forward(prob_fn, x, u, x_traj, du, K, prev_cost):
+    N, nx = x.shape
+    M, nu = u.shape
+    h = Handle(nx, nu, M, 1)
+    p = prob_fn(h)
+    xd, ud, xt = h.upload(J.to_abi(x)), h.upload(J.to_abi(u)), h.upload(J.to_abi(x_traj))
+    dd, Kd = h.upload(J.to_abi(du)), h.upload(J.gains_to_abi(K))
+    pc = h.upload(J.jl([prev_cost]))
+    xo, uo, co = h.alloc(np.float64, N * nx), h.alloc(np.float64, M * nu), h.alloc(np.float64, 1)
+    st = h.alloc(np.int32, 1)
+    _lib.check(h.lib.ilqr_forward(h.h, C.byref(p), C.byref(_lib.default_options()), xd, ud, xt, dd, Kd, pc,
+                                  xo, uo, co, None, st), "ilqr_forward")
+    out = (J.from_abi(h.download((nx, N), xo)), J.from_abi(h.download((nu, M), uo)),
+           float(h.download((1,), co)[0]))
+    h.close()
+    return out
+
+
+def shim_fit(prob_fn, x_init, u_init, x_traj, max_iter, tol):
+    N, nx = x_init.shape
+    M, nu = u_init.shape
+    h = Handle(nx, nu, M, 1)
+    p = prob_fn(h)
+    o = _lib.default_options(max_iter=max_iter, tol=tol)
+    xi, ui, xt = h.upload(J.to_abi(x_init)), h.upload(J.to_abi(u_init)), h.upload(J.to_abi(x_traj))
+    xo, uo = h.alloc(np.float64, N * nx), h.alloc(np.float64, M * nu)
+    rc = h.lib.ilqr_fit(h.h, C.byref(p), C.byref(o), xi, ui, xt, xo, uo, None, None, None)
+    assert rc in (_lib.OK, _lib.ERR_LS_EXHAUSTED)
+    out = J.from_abi(h.download((nx, N), xo)), J.from_abi(h.download((nu, M), uo))
+    h.close()
+    return out
+
+
+@pytest.fixture(scope="module")
+def quad():
+    return load("dense_xtraj")
+
+
+@pytest.mark.gpu
+def test_shim_lq_backward_pass(gpu, quad):
+    g = quad
+    b = 1
+    du, K = shim_backward(lambda h: lq_problem(h, g["A"][b], g["B"][b], g["Q"][b], g["R"][b], g["Qf"][b]),
+                          g["x"][b], g["u"][b])
+    assert du.shape == g["d"][b].shape and K.shape == g["K"][b].shape    # (T × nu), (T × nu × nx)
+    assert rel(du, g["d"][b]) < 1e-8 and rel(K, g["K"][b]) < 1e-8
+
+
+@pytest.mark.gpu
+def test_shim_lq_forward_pass_with_x_traj(gpu, quad):
+    g = quad
+    b = 0
+    x̄, ū, c = shim_forward(lambda h: lq_problem(h, g["A"][b], g["B"][b], g["Q"][b], g["R"][b], g["Qf"][b]),
+                            g["x"][b], g["u"][b], g["xtraj"][b], g["d"][b], g["K"][b], np.inf)
+    assert rel(x̄, g["fw_x"][b]) < 1e-10 and rel(ū, g["fw_u"][b]) < 1e-10
+    assert abs(c - g["fw_cost"][b]) / g["fw_cost"][b] < 1e-11
+
+
+@pytest.mark.gpu
+def test_shim_lq_fit(gpu, quad):
+    g = quad
+    b = 1
+    x, u = shim_fit(lambda h: lq_problem(h, g["A"][b], g["B"][b], g["Q"][b], g["R"][b], g["Qf"][b]),
+                    g["x"][b], g["u"][b], g["xtraj"][b], 30, 1e-6)
+    assert rel(x, g["fit_x"][b]) < 1e-8 and rel(u, g["fit_u"][b]) < 1e-8
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nu,name", [(2, "twolink_t50"), (1, "twolink_nu1_t50")])
+def test_shim_two_link_structs(gpu, nu, name):
+    """TwoLinkDynamics{NU}/TwoLinkCost/TwoLinkFinalCost → ILQR_PROBLEM_TWO_LINK."""
+    g = load(name)
+    b = 2
+    du, K = shim_backward(lambda h: tl_problem(), g["x"][b], g["u"][b])
+    assert rel(du, g["d"][b]) < 1e-10 and rel(K, g["K"][b]) < 1e-10
+    x̄, ū, c = shim_forward(lambda h: tl_problem(), g["x"][b], g["u"][b], np.zeros_like(g["x"][b]),
+                            g["d"][b], g["K"][b], np.inf)
+    assert rel(x̄, g["fw_x"][b]) < 1e-11 and abs(c - g["fw_cost"][b]) / g["fw_cost"][b] < 1e-12
+    x, u = shim_fit(lambda h: tl_problem(), g["x"][b], g["u"][b], np.zeros_like(g["x"][b]), 40, 1e-6)
+    assert rel(u, g["fit_u"][b]) < 1e-9
+
+
+@pytest.mark.gpu
+def test_shim_tiles_fallback_arbitrary_closures(gpu):
+    """Arbitrary closures (here the oracle's plain 2-link functions, not the recognised
+    structs): derivative tiles on the host (iLQRHIP.derivative_tiles; oracle.dual
+    standing in for ForwardDiff) → ilqr_backward_tiles on the device; the gains equal
+    the reference restatement's backward_pass."""
+    g = load("twolink_t50")
+    b = 1
+    x, u = g["x"][b], g["u"][b]
+    TL = O.TwoLink
+    t = J.derivative_tiles(x, u, TL.dynamicsf, TL.immediate_cost, TL.final_cost)
+    N, nx = x.shape
+    M, nu = u.shape
+    h = Handle(nx, nu, M, 1)
+    tl = _lib.Tiles(*(h.upload(t[k]).value for k in ("A", "B", "lx", "lu", "lxx", "lux", "luu", "lfx", "lfxx")))
+    dd, Kd, st = h.alloc(np.float64, M * nu), h.alloc(np.float64, M * nu * nx), h.alloc(np.int32, 1)
+    _lib.check(h.lib.ilqr_backward_tiles(h.h, C.byref(tl), C.byref(_lib.default_options()), dd, Kd, st),
+               "ilqr_backward_tiles")
+    du, K = J.from_abi(h.download((nu, M), dd)), J.gains_from_abi(h.download((nx, nu, M), Kd))
+    h.close()
+    assert rel(du, g["d"][b]) < 1e-10 and rel(K, g["K"][b]) < 1e-10
+
+
+def test_shim_tiles_layout_is_row_major_per_step():
+    """The tiles' Julia arrays hold each step's matrices transposed, i.e. their memory is
+    the ABI's row-major (T, r, c) blocks (a layout-only property: no GPU)."""
+    rng = np.random.default_rng(1)
+    A = rng.standard_normal((3, 4, 4))                 # three steps' A_t
+    Aj = J.jl(np.zeros((4, 4, 3)))
+    for i in range(3):
+        Aj[:, :, i] = A[i].T
+    assert np.array_equal(J.memory(Aj), A.reshape(-1))
+
+
+@pytest.mark.gpu
+def test_shim_solve_batched(gpu):
+    """solve!(::iLQRProblem): Julia (nx, nx, B) per-instance matrices permuted (2,1,3),
+    trajectories (nx, N, B) passed as they are."""
+    g = load("dense_t16")
+    nb = g["A"].shape[0]
+    T = g["u"].shape[1]
+    nx, nu = g["A"].shape[1], g["B"].shape[2]
+    jA, jB, jQ, jR, jQf = (J.jl(np.moveaxis(g[k], 0, -1)) for k in ("A", "B", "Q", "R", "Qf"))  # A[:, :, b]
+    jx = J.jl(np.transpose(g["x"], (2, 1, 0)))        # x[:, t, b]
+    ju = J.jl(np.transpose(g["u"], (2, 1, 0)))
+    h = Handle(nx, nu, T, nb)
+    p = _lib.Problem(_lib.PROBLEM_LQ, 0, *(h.upload(J.rowmajor3(a)).value for a in (jA, jB, jQ, jR, jQf)))
+    o = _lib.default_options(max_iter=30, tol=1e-6)
+    xi, ui = h.upload(jx), h.upload(ju)
+    xo, uo = h.alloc(np.float64, jx.size), h.alloc(np.float64, ju.size)
+    assert h.lib.ilqr_fit(h.h, C.byref(p), C.byref(o), xi, ui, None, xo, uo, None, None, None) == _lib.OK
+    x, u = h.download(jx.shape, xo), h.download(ju.shape, uo)
+    h.close()
+    for b in range(nb):
+        assert rel(x[:, :, b].T, g["fit_x"][b]) < 1e-8 and rel(u[:, :, b].T, g["fit_u"][b]) < 1e-8
