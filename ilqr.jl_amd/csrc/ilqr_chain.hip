@@ -13,11 +13,14 @@
 //  * linearize_dynamics (src/backward_pass.jl:25-40, ForwardDiff): forward-mode dual
 //    numbers (ILQR_LINEARIZE_DUAL, exact like the reference) or central finite
 //    differences (ILQR_LINEARIZE_CENTRAL_FD, what BASELINE config 5 names), one lane
-//    per (trajectory, step).
+//    per (trajectory, step, direction).
 //  * immediate_cost / final_cost (:85-116) on the joint rows: Σ qwᵢ(θ*ᵢ−θᵢ)² + Σ rwₖuₖ²
 //    and Σ qfwᵢ(θ*ᵢ−θᵢ)²; their derivatives are the exact constants.
-//  * backward_pass / forward_pass / fit: lane-per-trajectory Riccati recursion and
-//    RK4 rollout + α-halving line search, in the handle's dtype (fp32 or fp64).
+//  * backward_pass / forward_pass / fit: the Riccati recursion (four trajectories per
+//    wave on the 4-block f64 MFMA for 2-joint chains, lane per trajectory otherwise)
+//    and the RK4 rollout + α-halving line search (a 16-lane group per trajectory,
+//    component-parallel Newton-Euler for chains of ≤ 3 joints), in the handle's dtype
+//    (fp32 or fp64).
 // Layout as the other families (include/ilqr.h): x (B, T+1, nx), u/d (B, T, nu),
 // K (B, T, nu, nx), trajectory slowest, nx = 2·n_joints.
 #include <hip/hip_runtime.h>
@@ -219,8 +222,10 @@ __device__ __forceinline__ void to_parent(const S (&R)[9], const S (&w)[3], S (&
 }
 
 // The same coordinate changes as in-place Rodrigues rotations (no R_i): fewer
-// constants live at once, which the central-difference linearisation needs (its
-// kernel reads the chain from SGPRs, and R0x/R0aa there spill ~90 of them).
+// constants live at once. Only built with ILQR_CHAIN_FD_ROT=0 (the central-difference
+// linearisation used it while one lane ran all directions and R0x/R0aa spilled ~90
+// SGPRs; with one direction per lane the 3×3 form is faster);
+// tests/test_build.py compiles that alternate so it cannot rot.
 template <class S, class V, int NJ>
 __device__ __forceinline__ void rod_to_child(const ChainK<V, NJ>& P, int i, const S& c, const S& s,
                                              const S (&w)[3], S (&o)[3]) {
@@ -416,63 +421,6 @@ __device__ __forceinline__ void chain_xdot(const ChainK<V, NJ>& P, const S (&x)[
   }
 }
 
-// chain_xdot with the NJ + 1 recursive Newton-Euler passes of one evaluation spread
-// over the 4 lanes of a lane group (lane role 0: the bias with q̇ and gravity; role
-// k+1: M's column k, q̇ = 0, q̈ = e_k, no gravity), run as ONE uniform pass with
-// per-lane inputs (the zero terms are exact, so every lane gets the bits of the
-// separate passes), then gathered with lane shuffles; every lane of the group then
-// holds the same [q̇; v̇]. The forward rollout is a dependent chain per trajectory:
-// this cuts its latency per step to about a third at 4× the lanes.
-template <int NJ, int NU, bool ROT = true, class S, class V>
-__device__ __forceinline__ void chain_xdot_split(const ChainK<V, NJ>& P, const S (&x)[2 * NJ],
-                                                 const S (&u)[NU], S (&xd)[2 * NJ]) {
-  static_assert(NJ + 1 <= 4, "one lane per pass in a group of 4");
-  const int role = threadIdx.x & 3;
-  const int base = (threadIdx.x & 63) & ~3;
-  S c[NJ], s[NJ], qd[NJ], qdd[NJ], tau[NJ];
-#pragma unroll
-  for (int i = 0; i < NJ; ++i) {
-    scs(x[i], s[i], c[i]);
-    qd[i] = role == 0 ? x[NJ + i] : S(V(0));
-    qdd[i] = S(V(role == i + 1 ? 1 : 0));
-  }
-  rnea<true, true, ROT>(P, c, s, qd, qdd, tau, V(role == 0 ? 1 : 0));
-  S b[NJ], M[NJ][NJ];
-#pragma unroll
-  for (int i = 0; i < NJ; ++i) {
-    b[i] = __shfl(tau[i], base);
-#pragma unroll
-    for (int k = 0; k < NJ; ++k) M[i][k] = __shfl(tau[i], base + 1 + k);
-  }
-  S r[NJ];
-#pragma unroll
-  for (int i = 0; i < NJ; ++i) r[i] = (i < NU ? u[i < NU ? i : 0] : S(V(0))) - b[i];
-#pragma unroll
-  for (int k = 0; k < NJ; ++k) {
-    const S inv = crecip(M[k][k]);
-#pragma unroll
-    for (int i = k + 1; i < NJ; ++i) {
-      const S l = M[i][k] * inv;
-#pragma unroll
-      for (int j = k + 1; j < NJ; ++j) M[i][j] = M[i][j] - l * M[k][j];
-      r[i] = r[i] - l * r[k];
-    }
-  }
-  S q2[NJ];
-#pragma unroll
-  for (int i = NJ - 1; i >= 0; --i) {
-    S acc = r[i];
-#pragma unroll
-    for (int j = i + 1; j < NJ; ++j) acc = acc - M[i][j] * q2[j];
-    q2[i] = acc * crecip(M[i][i]);
-  }
-#pragma unroll
-  for (int i = 0; i < NJ; ++i) {
-    xd[i] = x[NJ + i];
-    xd[NJ + i] = q2[i];
-  }
-}
-
 // ---------------------------------------------------------------------------
 // Component-parallel Newton-Euler (v7 forward): a 16-lane group per trajectory,
 // lane 4·role + c. The role picks the pass (0: bias with q̇ and gravity, k+1: M's
@@ -584,6 +532,9 @@ template <int NJ, int NU, class V>
 __device__ __forceinline__ void chain_xdot_cv(const ChainK<V, NJ>& P, const V (&x)[2 * NJ],
                                               const V (&u)[NU], V (&xd)[2 * NJ]) {
   static_assert(NJ + 1 <= 4, "one role per pass in a group of 16");
+  // lane c of a quad evaluates joint min(c, NJ − 1) and the quad reads joint i from its
+  // lane i (bc0/bc1/bc2 below): only joints 0..2 have a broadcast
+  static_assert(NJ <= 3, "one sin/cos per lane: a quad holds at most three joints");
   const int l16 = threadIdx.x & 15;
   const int role = l16 >> 2, cmp = l16 & 3;
   V c[NJ], s[NJ], qd[NJ], qdd[NJ], tau[NJ];
@@ -754,8 +705,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LIN == ILQR
 #pragma unroll
   for (int k = 0; k < NU; ++k) z[NX + k] = ub[k];
   if constexpr (LIN == ILQR_LINEARIZE_DUAL) {
-    // the reference's two ForwardDiff.jacobian calls, two directions per pass (a pass
-    // carrying all ND directions would spill: ≈4.6 KB of scratch per lane)
+    // the reference's two ForwardDiff.jacobian calls, one direction per lane (this
+    // lane's column k of [A | B]; a pass carrying all ND directions would spill:
+    // ≈4.6 KB of scratch per lane)
     constexpr int DC = 1;
     using D = DualT<DC, V>;
     {
@@ -1288,8 +1240,9 @@ __global__ __launch_bounds__(CH_WG) void chain_backward_kernel(ChainK<V, NJ> P, 
   if (status) status[b] = nan ? ILQR_TRAJ_NAN : ILQR_TRAJ_OK;
 }
 
-// lanes per trajectory of the forward kernels: 4 with the lane-split dynamics
-constexpr int CH_FW_LANES = 16;  // lanes per trajectory in the forward (chain_xdot_cv)
+// lanes per trajectory of the forward kernels: a 16-lane group (one DPP row) running
+// the component-parallel Newton-Euler (chain_xdot_cv)
+constexpr int CH_FW_LANES = 16;
 
 // four trajectories per wave, four waves per workgroup (2-joint chains)
 template <class V, int NU>

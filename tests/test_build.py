@@ -1,0 +1,24 @@
+"""Compile-only checks of the HIP sources' non-default build variants (no GPU needed:
+hipcc cross-compiles gfx950 here). The product library is built with the defaults
+(ilqr.jl_amd/csrc/Makefile); the alternates below are measured ablations kept for the
+record, so they are compiled here to keep them from rotting unseen."""
+import os
+import shutil
+import subprocess
+
+import pytest
+
+CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "ilqr.jl_amd", "csrc")
+HIPCC = "/opt/rocm/bin/hipcc"
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC) and shutil.which("hipcc") is None, reason="no hipcc")
+def test_chain_macro_alternates_compile(tmp_path):
+    """ilqr_chain.hip with the Rodrigues-form central differences
+    (ILQR_CHAIN_FD_ROT=0) and the unpacked ±h evaluation (ILQR_CHAIN_FD_PAIR=0)."""
+    hipcc = HIPCC if os.path.exists(HIPCC) else shutil.which("hipcc")
+    cmd = [hipcc, "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-mllvm", "-amdgpu-mfma-vgpr-form=1",
+           "-fno-slp-vectorize", "-DILQR_CHAIN_FD_ROT=0", "-DILQR_CHAIN_FD_PAIR=0", "-c",
+           os.path.join(CSRC, "ilqr_chain.hip"), "-o", str(tmp_path / "chain_alt.o")]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]

@@ -23,6 +23,9 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "ilqr.jl_amd")]
 
 from ilqr_amd import _lib  # noqa: E402
 from ilqr_amd.chain import ChainSolver, rbd_2dof_problem, rbd_initial_states  # noqa: E402
+from tools import flops as FL  # noqa: E402
+
+PEAK_TFLOPS = {"f32": 157.3, "f64": 78.6}   # MI355X vector FP32 / FP64 (spec; MI355X_MICROARCH.md)
 
 
 def timed(fn, n, stream):
@@ -40,7 +43,9 @@ def cpu_baseline(pr, x, u, budget_s):
     fp64, central differences, OpenMP over trajectories) on a bounded sample: one
     cold-start iteration per trajectory."""
     from oracle import cref
-    threads = min(16, os.cpu_count() or 1)
+    visible = len(os.sched_getaffinity(0))
+    share = os.environ.get("OMP_NUM_THREADS")
+    threads = min(visible, int(share)) if share and share.isdigit() and int(share) > 0 else visible
     n = 16
     while True:
         idx = np.arange(n) % x.shape[0]
@@ -96,6 +101,40 @@ def main():
         ms_ev = timed(step, args.steps, stream)
         ms = max(ms_ev, (time.perf_counter() - t0) * 1000.0 / args.steps)
         ok = bool((st == 0).all().item())
+        # per-kernel times and the roofline object (algorithmic FLOPs, tools/flops.py)
+        d = torch.empty((B, T, pr.nu), dtype=dt, device=dev)
+        K = torch.empty((B, T, pr.nu, pr.nx), dtype=dt, device=dev)
+        A = torch.empty((B, T, pr.nx, pr.nx), dtype=dt, device=dev)
+        Bm = torch.empty((B, T, pr.nx, pr.nu), dtype=dt, device=dev)
+        o = _lib.default_options()
+        import ctypes as C
+        P = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
+        lin_fn = lambda: s.lib.ilqr_chain_linearize(s.h, P(x), P(u), P(A), P(Bm))  # noqa: E731
+        bw = lambda: s.lib.ilqr_chain_backward(s.h, C.byref(o), P(x), P(u), P(d), P(K), None)  # noqa: E731
+        pinf = torch.full((B,), float("inf"), dtype=dt, device=dev)
+        nc = torch.empty_like(pinf)
+        fw = lambda: s.lib.ilqr_chain_forward(s.h, C.byref(o), P(x), P(u), None, P(d), P(K), P(pinf),  # noqa: E731
+                                              P(xn), P(un), P(nc), None, None)
+        for fn in (lin_fn, bw, fw):
+            fn()
+        lin_ms = timed(lin_fn, args.steps, stream)
+        bw_ms = timed(bw, args.steps, stream)   # ilqr_chain_backward = linearise + Riccati
+        fw_ms = timed(fw, args.steps, stream)
+        nd = pr.nx + pr.nu
+        f_rk4 = FL.chain_dynamics_flops(pr)
+        lin_fl = (f_rk4 * FL.dual_factor(nd) if lin == "dual" else 2 * nd * f_rk4 + nd * pr.nx) * T * B
+        ric_fl = FL.riccati_flops_per_step(pr.nx, pr.nu) * T * B
+        fw_fl = FL.forward_flops_per_step(pr.nx, pr.nu, f_rk4) * T * B
+        peak = PEAK_TFLOPS[args.dtype]
+        kern = {"linearize": (lin_ms, lin_fl), "riccati": (max(bw_ms - lin_ms, 1e-6), ric_fl),
+                "forward": (fw_ms, fw_fl)}
+        roof = {"bound": "forward latency/issue (16 lanes per trajectory), linearisation VALU issue",
+                "unit": "TFLOP/s", "peak": peak, "peak_dtype": args.dtype,
+                "flops_note": f"RK4 of the restated RBD formulas = {f_rk4} flop (tools/flops.py)"}
+        for k, (ms_k, fl) in kern.items():
+            roof[k] = {"avg_launch_ms": ms_k, "algorithmic_flops": fl,
+                       "achieved": fl / (ms_k * 1e-3) / 1e12, "frac": fl / (ms_k * 1e-3) / 1e12 / peak}
+        roof["achieved"], roof["frac"] = roof["forward"]["achieved"], roof["forward"]["frac"]
         res = {"metric": f"batched iLQR iterations/sec (fwd+bwd pass), RBD 2-DoF arm fixed base, "
                          f"nx=4 nu={pr.nu} T={T}",
                "value": 1000.0 / ms, "unit": f"batched iterations/s (batch={B})", "n_gpus": 1,
@@ -105,6 +144,7 @@ def main():
                           "batch": B, "T": T, "linearization": lin},
                "traj_iters_per_s": B * 1000.0 / ms,
                "mean_line_search_trials": float(trials.double().mean().item()), "all_ok": ok,
+               "roofline": roof,
                "cpu_baseline": None}
         if not args.no_cpu:
             if base is None:

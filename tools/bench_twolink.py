@@ -1,8 +1,10 @@
-"""Secondary benchmark: BASELINE config 2 — the 2-link arm (nx=4, nu=2, T=50),
-batch 1024 random x₀, fp64, 1 GPU. Same step definition as bench.py (one
-cold-start fit iteration over the batch: linearise + backward + forward with
-line search), timed with HIP events on the handle's stream. Prints one JSON line.
-Not the driver's headline (bench.py); see DESIGN.md §2-link.
+"""Secondary benchmark: BASELINE config 2 — the 2-link arm (nx=4, nu=2, or the nu=1
+variant f(x, [u₁, 0]) with --nu 1; T=50), batch 1024 random x₀, fp64, 1 GPU. Step:
+one cold-start fit iteration over the batch (linearise + backward + forward with
+line search), timed with HIP events on the handle's stream. Prints one JSON line with
+a roofline object per kernel (algorithmic FLOPs of the reference's formulas,
+tools/flops.py, against the FP64 peak). Not the driver's headline (bench.py); see
+DESIGN.md §2-link.
 """
 from __future__ import annotations
 
@@ -22,6 +24,9 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "ilqr.jl_amd")]
 from ilqr_amd import _lib  # noqa: E402
 from ilqr_amd.problems import two_link_initial_states  # noqa: E402
 from ilqr_amd.solver import Solver, _ptr  # noqa: E402
+from tools import flops as FL  # noqa: E402
+
+FP64_PEAK_TFLOPS = 78.6
 
 
 def timed(fn, n, stream):
@@ -40,14 +45,15 @@ def main():
     ap.add_argument("--warmup", type=int, default=500)
     ap.add_argument("--batch", type=int, default=1024)
     ap.add_argument("--T", type=int, default=50)
+    ap.add_argument("--nu", type=int, default=2, choices=[1, 2])
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
-    B, T = args.batch, args.T
+    B, T, NU = args.batch, args.T, args.nu
     dev = torch.device("cuda", 0)
-    s = Solver(4, 2, T, B, kind=_lib.PROBLEM_TWO_LINK)
+    s = Solver(4, NU, T, B, kind=_lib.PROBLEM_TWO_LINK)
     x0 = two_link_initial_states(B)
-    u = torch.zeros((B, T, 2), dtype=torch.float64, device=dev)
+    u = torch.zeros((B, T, NU), dtype=torch.float64, device=dev)
     x = s.rollout(torch.from_numpy(x0).to(dev), u)
     xn, un = torch.empty_like(x), torch.empty_like(u)
     pc = torch.empty((B,), dtype=torch.float64, device=dev)
@@ -68,8 +74,8 @@ def main():
     ms_wall = (time.perf_counter() - t0) * 1000.0 / args.steps
     ms = max(ms_ev, ms_wall)
 
-    d = torch.empty((B, T, 2), dtype=torch.float64, device=dev)
-    K = torch.empty((B, T, 2, 4), dtype=torch.float64, device=dev)
+    d = torch.empty((B, T, NU), dtype=torch.float64, device=dev)
+    K = torch.empty((B, T, NU, 4), dtype=torch.float64, device=dev)
     o = _lib.default_options()
     bw = lambda: s.lib.ilqr_backward(s.h, s._p(), C.byref(o), _ptr(x), _ptr(u), _ptr(d), _ptr(K), None)
     bw()
@@ -81,13 +87,34 @@ def main():
     fw()
     fw_ms = timed(fw, args.steps, stream)
 
+    # algorithmic FLOPs (tools/flops.py): linearise = dual RK4 over 4+NU directions,
+    # backward = the Riccati step count, forward = one trial (1 on a cold start)
+    f_rk4 = FL.twolink_dynamics_flops(NU)
+    lin_fl = f_rk4 * FL.dual_factor(4 + NU) * T * B
+    ric_fl = FL.riccati_flops_per_step(4, NU) * T * B
+    fw_fl = FL.forward_flops_per_step(4, NU, f_rk4) * T * B
+    roof = {"bound": "latency (one lane per trajectory in the forward; B = 1024 fills 16 waves)",
+            "unit": "TFLOP/s", "peak": FP64_PEAK_TFLOPS,
+            "backward": {"kernels": "tl_linearize + tl_backward (4 trajectories per wave, 4x4x4 f64 MFMA)",
+                         "avg_launch_ms": bw_ms, "algorithmic_flops": lin_fl + ric_fl,
+                         "achieved": (lin_fl + ric_fl) / (bw_ms * 1e-3) / 1e12},
+            "forward": {"kernel": "tl_forward (one lane per trajectory)", "avg_launch_ms": fw_ms,
+                        "algorithmic_flops": fw_fl, "achieved": fw_fl / (fw_ms * 1e-3) / 1e12},
+            "flops_note": f"RK4 of the reference's formulas = {f_rk4} flop (tools/flops.py); dual factor "
+                          f"1+2·ND; Riccati per SURVEY §8d"}
+    for k in ("backward", "forward"):
+        roof[k]["frac"] = roof[k]["achieved"] / FP64_PEAK_TFLOPS
+    roof["achieved"] = roof["forward"]["achieved"]
+    roof["frac"] = roof["forward"]["frac"]
     out = {
-        "metric": "batched iLQR iterations/sec (fwd+bwd pass), 2-link arm nx=4 nu=2 T=50, batch=1024",
+        "metric": f"batched iLQR iterations/sec (fwd+bwd pass), 2-link arm nx=4 nu={NU} T={T}, batch={B}",
         "value": 1000.0 / ms, "unit": "batched iterations/s (batch=1024)", "n_gpus": 1,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True,
         "dtype": "f64", "data": "synthetic: x0 = default_rng(b).random(4), u0 = 0, rollout",
-        "config": {"workload": "2-link arm fit iteration (cold start)", "T": T, "batch": B},
+        "config": {"workload": "2-link arm fit iteration (cold start)", "T": T, "batch": B, "nu": NU,
+                   "variant": "reference shape" if NU == 2 else "f(x, [u1, 0]), build-defined, not reference-pinned"},
         "backward_ms": bw_ms, "forward_ms": fw_ms, "event_ms": ms_ev, "wall_ms": ms_wall,
+        "roofline": roof,
         "traj_iters_per_s": B * 1000.0 / ms,
         "mean_trials": float(trials.double().mean()), "all_ok": bool((st == 0).all()),
         "cpu_baseline": None,
@@ -95,6 +122,8 @@ def main():
     if not args.no_cpu:
         try:
             from oracle import cref
+            if NU != 2:
+                raise NotImplementedError("the C restatement covers the reference's nu = 2 only")
             out["cpu_baseline"] = cref.twolink_cpu_baseline(x.cpu().numpy(), u.cpu().numpy(), B,
                                                             args.cpu_budget)
         except Exception as e:
