@@ -411,7 +411,14 @@ def main():
                                 "trajectory_status_counts": dflt_status,
                                 "note": "the reference's default call: tol = 1e-6, max_iter = 100 (converged trajectories leave the batch)"},
         "single_iteration_cold": {"ms": single_ms, "batched_it_per_s": 1000.0 / single_ms,
-                                  "note": "round-1 step: one iteration from cold per step (ilqr_iterate)"},
+                                  "note": "one iteration from cold per step (ilqr_iterate = one launch of "
+                                          "lq_iter_fused4: every wave's backward then its forward)"},
+        "iteration_kernel": {"kernel": "lq_iter_fused4 (backward_pass + forward_pass, 4 trajectories per wave)",
+                             "avg_launch_ms": single_ms,
+                             "achieved_tflops": it_flops / (single_ms * 1e-3) / 1e12,
+                             "frac_fp64_peak": it_flops / (single_ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS,
+                             "achieved_gbps": it_bytes / (single_ms * 1e-3) / 1e9,
+                             "frac_hbm_peak": it_bytes / (single_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS},
         "allgather_costs_ms": gather_ms,
         "allgather_check": gathered,
         "cpu_baseline": None,

@@ -1,0 +1,352 @@
+// Forward pass + line search of the LQ family, four trajectories per wave with the
+// per-step inputs streamed HBM → LDS (the "ring" forward), and the DPP
+// mat-vec helpers it uses. Private header: included by ilqr_lq.hip (the forward and
+// pipelined kernels) and ilqr_bw4.hip (the fused backward + forward iteration kernel).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <type_traits>
+
+#include "../../include/ilqr.h"
+#include "ilqr_internal.h"
+#include "ilqr_device.h"
+
+namespace ilqr {
+namespace {
+
+// Σ_k<16 bcast_k(src)·c[k]: src is broadcast from lane k of each 16-lane row
+// (DPP64 row_newbcast, gfx90a+), 4 independent accumulators. `s_nop 4` covers the
+// VALU→DPP and EXEC→DPP hazards for whatever the compiler scheduled in front.
+__device__ __forceinline__ double dpp_dot16(double src, const double (&c)[16]) {
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+  asm("s_nop 4\n\t"
+      "v_fmac_f64_dpp %[a0], %[s], %[c0] row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[a1], %[s], %[c1] row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[a2], %[s], %[c2] row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[a3], %[s], %[c3] row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[a0], %[s], %[c4] row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[a1], %[s], %[c5] row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[a2], %[s], %[c6] row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[a3], %[s], %[c7] row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[a0], %[s], %[c8] row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[a1], %[s], %[c9] row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[a2], %[s], %[c10] row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[a3], %[s], %[c11] row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[a0], %[s], %[c12] row_newbcast:12 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[a1], %[s], %[c13] row_newbcast:13 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[a2], %[s], %[c14] row_newbcast:14 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[a3], %[s], %[c15] row_newbcast:15 row_mask:0xf bank_mask:0xf\n\t"
+      : [a0] "+v"(a0), [a1] "+v"(a1), [a2] "+v"(a2), [a3] "+v"(a3)
+      : [s] "v"(src), [c0] "v"(c[0]), [c1] "v"(c[1]), [c2] "v"(c[2]), [c3] "v"(c[3]), [c4] "v"(c[4]), [c5] "v"(c[5]), [c6] "v"(c[6]), [c7] "v"(c[7]), [c8] "v"(c[8]), [c9] "v"(c[9]), [c10] "v"(c[10]), [c11] "v"(c[11]), [c12] "v"(c[12]), [c13] "v"(c[13]), [c14] "v"(c[14]), [c15] "v"(c[15]));
+  return (a0 + a1) + (a2 + a3);
+}
+
+// Σ_k<12 bcast_k(src)·c[k]: src is broadcast from lane k of each 16-lane row
+// (DPP64 row_newbcast, gfx90a+), 4 independent accumulators. `s_nop 4` covers the
+// VALU→DPP and EXEC→DPP hazards for whatever the compiler scheduled in front.
+__device__ __forceinline__ double dpp_dot12(double src, const double (&c)[12]) {
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+  asm("s_nop 4\n\t"
+      "v_fmac_f64_dpp %[a0], %[s], %[c0] row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[a1], %[s], %[c1] row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[a2], %[s], %[c2] row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[a3], %[s], %[c3] row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[a0], %[s], %[c4] row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[a1], %[s], %[c5] row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[a2], %[s], %[c6] row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[a3], %[s], %[c7] row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[a0], %[s], %[c8] row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[a1], %[s], %[c9] row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[a2], %[s], %[c10] row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[a3], %[s], %[c11] row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+      : [a0] "+v"(a0), [a1] "+v"(a1), [a2] "+v"(a2), [a3] "+v"(a3)
+      : [s] "v"(src), [c0] "v"(c[0]), [c1] "v"(c[1]), [c2] "v"(c[2]), [c3] "v"(c[3]), [c4] "v"(c[4]), [c5] "v"(c[5]), [c6] "v"(c[6]), [c7] "v"(c[7]), [c8] "v"(c[8]), [c9] "v"(c[9]), [c10] "v"(c[10]), [c11] "v"(c[11]));
+  return (a0 + a1) + (a2 + a3);
+}
+
+// dpp_dot16 for a block-diagonal row held in 12 registers: lanes 0..11 of each row
+// (banks 0-2) take Σ_k<12 bcast_k(src)·c[k], lanes 12..15 (bank 3) Σ_m<4
+// bcast_{12+m}(src)·c[m] — the same accumulators and order as dpp_dot16 on the
+// zero-padded row [c[0..11] | 0] resp. [0 | c[0..3]].
+__device__ __forceinline__ double dpp_dot16_bd(double src, const double (&c)[12]) {
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+  asm("s_nop 4\n\t"
+      "v_fmac_f64_dpp %[a0], %[s], %[c0] row_newbcast:0 row_mask:0xf bank_mask:0x7\n\t"
+      "v_fmac_f64_dpp %[a1], %[s], %[c1] row_newbcast:1 row_mask:0xf bank_mask:0x7\n\t"
+      "v_fmac_f64_dpp %[a2], %[s], %[c2] row_newbcast:2 row_mask:0xf bank_mask:0x7\n\t"
+      "v_fmac_f64_dpp %[a3], %[s], %[c3] row_newbcast:3 row_mask:0xf bank_mask:0x7\n\t"
+      "v_fmac_f64_dpp %[a0], %[s], %[c4] row_newbcast:4 row_mask:0xf bank_mask:0x7\n\t"
+      "v_fmac_f64_dpp %[a1], %[s], %[c5] row_newbcast:5 row_mask:0xf bank_mask:0x7\n\t"
+      "v_fmac_f64_dpp %[a2], %[s], %[c6] row_newbcast:6 row_mask:0xf bank_mask:0x7\n\t"
+      "v_fmac_f64_dpp %[a3], %[s], %[c7] row_newbcast:7 row_mask:0xf bank_mask:0x7\n\t"
+      "v_fmac_f64_dpp %[a0], %[s], %[c8] row_newbcast:8 row_mask:0xf bank_mask:0x7\n\t"
+      "v_fmac_f64_dpp %[a1], %[s], %[c9] row_newbcast:9 row_mask:0xf bank_mask:0x7\n\t"
+      "v_fmac_f64_dpp %[a2], %[s], %[c10] row_newbcast:10 row_mask:0xf bank_mask:0x7\n\t"
+      "v_fmac_f64_dpp %[a3], %[s], %[c11] row_newbcast:11 row_mask:0xf bank_mask:0x7\n\t"
+      "v_fmac_f64_dpp %[a0], %[s], %[c0] row_newbcast:12 row_mask:0xf bank_mask:0x8\n\t"
+      "v_fmac_f64_dpp %[a1], %[s], %[c1] row_newbcast:13 row_mask:0xf bank_mask:0x8\n\t"
+      "v_fmac_f64_dpp %[a2], %[s], %[c2] row_newbcast:14 row_mask:0xf bank_mask:0x8\n\t"
+      "v_fmac_f64_dpp %[a3], %[s], %[c3] row_newbcast:15 row_mask:0xf bank_mask:0x8\n\t"
+      : [a0] "+v"(a0), [a1] "+v"(a1), [a2] "+v"(a2), [a3] "+v"(a3)
+      : [s] "v"(src), [c0] "v"(c[0]), [c1] "v"(c[1]), [c2] "v"(c[2]), [c3] "v"(c[3]), [c4] "v"(c[4]), [c5] "v"(c[5]), [c6] "v"(c[6]), [c7] "v"(c[7]), [c8] "v"(c[8]), [c9] "v"(c[9]), [c10] "v"(c[10]), [c11] "v"(c[11]));
+  return (a0 + a1) + (a2 + a3);
+}
+
+struct FwdOut {
+  double cost;
+  int trials;
+  int accepted;  // 1 accepted, 0 exhausted / NaN
+};
+
+
+// Forward pass of a wave's four trajectories b0 .. b0+3 (contiguous) with the per-step
+// inputs streamed HBM → LDS by the wave itself (global_load_lds_dwordx4, no VGPRs
+// held in flight) PF steps ahead into a ring of R slots. Same lane roles and the
+// same arithmetic in the same order as lq_forward_group — bit-identical results —
+// but ≈100 VGPRs instead of ≈250 and a deeper prefetch: it runs inside kernels that
+// also run the backward pass (128 VGPRs at 4 waves/SIMD). Called by the WHOLE wave
+// (every lane produces a slice of every group's inputs); `active` masks the groups
+// that compute, and the line-search loop is uniform (a group that accepted stops
+// storing). One slot (3 KB): K rows [0,192), x [192,240), u [240,256), x_traj
+// [256,304), δu [304,320) doubles; group g at K + 48g, x/x_traj + 12g, u/δu + 4g.
+constexpr int RING_SLOT = 384;  // doubles per ring slot
+constexpr int RING_LAREA = 4 * 160 + 16;  // Q, R of the wave's 4 trajectories (+ read overhang)
+
+template <int NX, int NU, int R, int PF>
+__device__ FwdOut lq_forward_wave_ring(const LQParams& P, int b0, int B, int T, bool active,
+                                       const double* __restrict__ x, const double* __restrict__ u,
+                                       const double* __restrict__ xtraj, const double* __restrict__ dg,
+                                       const double* __restrict__ Kg, double prev_cost,
+                                       double* __restrict__ xnew, double* __restrict__ unew,
+                                       double* du2_out, const LSParams& ls, double* ring) {
+  static_assert(NX == 12 && NU == 4, "slot layout and lane map are written for nx = 12, nu = 4");
+  static_assert(R > PF && PF >= 1, "the slot being refilled must not be the one being read");
+  constexpr uint32_t OOR = 0x80000000u;
+  const int l = threadIdx.x & 63;
+  const int g = l >> 4;
+  const int j = l & 15;
+  const bool is_x = j < NX;
+  const bool is_u = !is_x;
+  const int iu = is_u ? j - NX : 0;
+  const int jx = is_x ? j : 0;
+  const int nt = B - b0 < 4 ? B - b0 : 4;  // trajectories present in this wave
+  const int b = b0 + (g < nt ? g : 0);     // absent groups alias trajectory b0 (never stored)
+
+  const double* Ab = P.A + (size_t)b * NX * NX;
+  const double* Bb = P.B + (size_t)b * NX * NU;
+  const double* Qfb = P.Qf + (size_t)b * NX * NX;
+  double Fr[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const double a = ldz(is_x && k < NX, Ab + jx * NX + (k < NX ? k : 0), Ab);
+    const double bb = ldz(is_x && k >= NX, Bb + jx * NU + (k >= NX ? k - NX : 0), Bb);
+    Fr[k] = a + bb;
+  }
+  // the cost Hessian rows live in LDS after the ring (re-read every step: registers
+  // are the scarce resource): trajectory g's Q at 160g, R at 160g + 144
+  double* const Ls = ring + R * RING_SLOT;
+  for (int i = l; i < 4 * 160; i += 64) {
+    const int gg = i / 160, e = i % 160;
+    const size_t bt = (size_t)b0 + (gg < nt ? gg : 0);
+    Ls[i] = e < NX * NX ? P.Q[bt * NX * NX + e] : P.R[bt * NU * NU + (e < NX * NX ? 0 : e - NX * NX)];
+  }
+  const int la = is_x ? g * 160 + jx * NX : g * 160 + NX * NX + iu * NU;  // this lane's L row
+  wave_lds_fence();
+
+  // producer: lane l moves 16 B per instruction; three instructions fill one slot
+  //   #1: K chunk l (of 96)   #2: K chunk 64+l | x chunk l−32 | u chunk l−56
+  //   #3: x_traj chunk l | δu chunk l−24 | (lanes 32..63 repeat lanes 0..31)
+  auto tr = [&](int gg) { return (size_t)(b0 + (gg < nt ? gg : 0)); };
+  const double* xt0 = xtraj ? xtraj : x;  // x_traj = NULL: read x with weight 0
+  const double xtw = xtraj ? 1.0 : 0.0;
+  const char *p1, *p2, *p3;
+  uint32_t s1, s2, s3;  // bytes per step
+  {
+    const int c = l;
+    p1 = reinterpret_cast<const char*>(Kg + tr(c / 24) * T * NU * NX + 2 * (c % 24));
+    s1 = NU * NX * 8;
+    if (l < 32) {
+      const int c2 = 64 + l;
+      p2 = reinterpret_cast<const char*>(Kg + tr(c2 / 24) * T * NU * NX + 2 * (c2 % 24));
+      s2 = NU * NX * 8;
+    } else if (l < 56) {
+      const int m = l - 32;
+      p2 = reinterpret_cast<const char*>(x + tr(m / 6) * (T + 1) * NX + 2 * (m % 6));
+      s2 = NX * 8;
+    } else {
+      const int m = l - 56;
+      p2 = reinterpret_cast<const char*>(u + tr(m / 2) * T * NU + 2 * (m % 2));
+      s2 = NU * 8;
+    }
+    const int l3 = l & 31;
+    if (l3 < 24) {
+      p3 = reinterpret_cast<const char*>(xt0 + tr(l3 / 6) * (T + 1) * NX + 2 * (l3 % 6));
+      s3 = NX * 8;
+    } else {
+      const int m = l3 - 24;
+      p3 = reinterpret_cast<const char*>(dg + tr(m / 2) * T * NU + 2 * (m % 2));
+      s3 = NU * 8;
+    }
+  }
+  const uint32_t ring_lds = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) double*)ring;
+  auto produce = [&](int t) {
+    uint32_t tt = (uint32_t)(t < T ? t : T - 1);  // clamped: loaded, never read
+    asm volatile("" : "+s"(tt));  // no hoisting of the prologue's addresses out of the trial loop
+    const uint32_t m0 = ring_lds + (uint32_t)((t % R) * RING_SLOT * 8);
+    asm volatile("global_load_lds_dwordx4 %0, off" ::"v"(p1 + (size_t)tt * s1), "{m0}"(m0) : "memory");
+    asm volatile("global_load_lds_dwordx4 %0, off" ::"v"(p2 + (size_t)tt * s2), "{m0}"(m0 + 1024) : "memory");
+    asm volatile("global_load_lds_dwordx4 %0, off" ::"v"(p3 + (size_t)tt * s3), "{m0}"(m0 + 2048) : "memory");
+  };
+  // vmcnt immediates (gfx9: vmcnt[3:0] | expcnt 7 << 4 | lgkmcnt 15 << 8 | vmcnt[5:4] << 14):
+  // per step the wave issues 3 slot loads then 2 result stores, so slot t is
+  // complete once ≤ 5·PF − 3 ops are outstanding (≤ 3·PF − 3 while the prologue
+  // loads are the newest)
+  constexpr int N_SS = 5 * PF - 3, N_PRO = 3 * PF - 3;
+  auto wait_slot = [](auto n) {
+    constexpr int v = decltype(n)::value;
+    static_assert(v >= 0 && v < 64, "vmcnt is 6 bits");
+    __builtin_amdgcn_s_waitcnt((v & 15) | (7 << 4) | (15 << 8) | ((v >> 4) << 14));
+    asm volatile("" ::: "memory");
+  };
+
+  const int ka = g * 48 + iu * NX;                                 // K row of (g, iu)
+  const int va = is_x ? 192 + g * 12 + jx : 240 + g * 4 + iu;      // x (x lanes) / u (u lanes)
+  const int vb = is_x ? 256 + g * 12 + jx : 304 + g * 4 + iu;      // x_traj / δu
+  const auto rXN = buffer_rsrc(xnew + (size_t)b0 * (T + 1) * NX, (uint32_t)nt * (T + 1) * NX * 8);
+  const auto rUN = buffer_rsrc(unew + (size_t)b0 * T * NU, (uint32_t)nt * T * NU * 8);
+  const uint32_t oxs = is_x ? (uint32_t)(g * (T + 1) * NX + jx) * 8 : OOR;
+  const uint32_t ous = is_u ? (uint32_t)(g * T * NU + iu) * 8 : OOR;
+
+  double alpha = ls.alpha0;
+  FwdOut out{INFINITY, 0, 0};
+  bool open = active;  // still line-searching
+  double du2_acc = 0.0;
+  for (int trial = 1; trial <= ls.max_trials && __any(open); ++trial) {
+#pragma unroll
+    for (int t = 0; t < PF; ++t) produce(t);
+    double xb = 0.0;  // x̄₁ = x₁ (:65), taken from slot 0 once it has landed
+    double cost = 0.0, du2 = 0.0;
+    const uint32_t ox = open ? oxs : OOR, ou = open ? ous : OOR;  // closed groups store nothing
+    auto step = [&](int t) {
+      const double* sl = ring + (t % R) * RING_SLOT;
+      const double a = sl[va], bq = sl[vb];
+      if (t == 0) xb = is_x ? a : 0.0;
+      double Kr[NX];
+      const double2* kr = reinterpret_cast<const double2*>(sl + ka);
+#pragma unroll
+      for (int k = 0; k < NX / 2; ++k) {
+        const double2 v = kr[k];
+        Kr[2 * k] = v.x;
+        Kr[2 * k + 1] = v.y;
+      }
+      // δx = x̄ₖ − xₖ (:72); ūₖ = uₖ + α δuₖ + Kₖ δx (:73)
+      const double dx = is_x ? xb - a : 0.0;
+      const double kdx = dpp_dot12(dx, Kr);
+      const double ub = fma(alpha, bq, a) + kdx;
+      const double z = is_x ? xb : ub;
+      const double v = is_x ? fma(-xtw, bq, xb) : ub;
+      const double e = is_x ? 0.0 : ub - a;
+      produce(t + PF);  // slot (t+PF)%R was last read at step t+PF−R < t
+      double Lr[NX];  // Q row (x lanes); R row in slots 0..NU-1 (u lanes), rest unused
+      const double2* lr = reinterpret_cast<const double2*>(Ls + la);
+#pragma unroll
+      for (int k = 0; k < NX / 2; ++k) {
+        const double2 q = lr[k];
+        Lr[2 * k] = q.x;
+        Lr[2 * k + 1] = q.y;
+      }
+      const double lv = dpp_dot16_bd(v, Lr);
+      const double xn = dpp_dot16(z, Fr);
+      cost = fma(v, lv, cost);
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, z), rXN, ox, (uint32_t)t * NX * 8, 0);
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, z), rUN, ou, (uint32_t)t * NU * 8, 0);
+      du2 = fma(e, e, du2);
+      xb = xn;
+    };
+    const int tp = T < PF ? T : PF;
+    for (int t = 0; t < tp; ++t) {
+      wait_slot(std::integral_constant<int, N_PRO>{});
+      step(t);
+    }
+    for (int t = tp; t < T; ++t) {
+      wait_slot(std::integral_constant<int, N_SS>{});
+      step(t);
+    }
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, xb), rXN, ox, (uint32_t)T * NX * 8, 0);
+    // Qf row (x lanes; u lanes read row 0 and zero it): one base address, 6 × 16 B
+    const double2* qrow = reinterpret_cast<const double2*>(Qfb + jx * NX);
+    asm volatile("" : "+v"(qrow));  // keep the row address from being hoisted as 12 pointers
+    double Qfr[NX];
+#pragma unroll
+    for (int k = 0; k < NX / 2; ++k) {
+      const double2 q = qrow[k];
+      Qfr[2 * k] = is_x ? q.x : 0.0;
+      Qfr[2 * k + 1] = is_x ? q.y : 0.0;
+    }
+    const double lf = dpp_dot12(is_x ? xb : 0.0, Qfr);
+    cost = fma(is_x ? xb : 0.0, lf, cost);
+    cost = rowsum16(cost);
+    du2 = rowsum16(du2);
+    if (open) {
+      out.trials = trial;
+      out.cost = cost;
+      du2_acc = du2;
+      if (prev_cost - cost > 0.0) {  // (:77-80); NaN compares false → keep searching
+        out.accepted = 1;
+        open = false;
+      }
+    }
+    alpha *= ls.shrink;  // (:82); unused by closed groups
+    // the loads of the clamped steps past the horizon are still in flight: drain them
+    // before the next trial's prologue reuses the slots
+    __builtin_amdgcn_s_waitcnt((0) | (7 << 4) | (15 << 8));
+    asm volatile("" ::: "memory");
+  }
+  if (du2_out) *du2_out = du2_acc;
+  return out;
+}
+
+// forward ring inside the pipe kernel: the workgroup's backward scratch holds R slots
+constexpr int PIPE_R = 8, PIPE_PF = 7;
+
+// forward pass + convergence test (:163-175) of the wave's trajectories b0 .. b0+3;
+// called by the whole wave, groups whose status is not OK (or past B) sit out
+// (`active`: this lane's group runs; the caller read it from status)
+template <int NX, int NU>
+__device__ __forceinline__ void iter_forward_wave_active(const LQParams& P, int b0, int B, int T,
+                                                         const IterArgs& a, const LSParams& ls,
+                                                         double* ring, bool active) {
+  const int j = threadIdx.x & 15;
+  const int b = b0 + ((threadIdx.x & 63) >> 4);
+  double du2 = 0.0;
+  const double pc = (a.prev_cost && active) ? a.prev_cost[b] : INFINITY;
+  const FwdOut r = lq_forward_wave_ring<NX, NU, PIPE_R, PIPE_PF>(P, b0, B, T, active, a.x, a.u,
+                                                                 a.xtraj, a.d, a.K, pc, a.xnew,
+                                                                 a.unew, &du2, ls, ring);
+  if (j == 0 && active) {
+    if (a.trials) a.trials[b] = r.trials;
+    if (a.du2) a.du2[b] = du2;
+    if (a.iters) a.iters[b] = a.iter;
+    if (!r.accepted) {
+      a.status[b] = (r.cost != r.cost) ? ILQR_TRAJ_NAN : ILQR_TRAJ_LS_EXHAUSTED;
+      if (a.res_parity) a.res_parity[b] = a.parity;
+    } else {
+      a.new_cost[b] = r.cost;
+      if (du2 <= ls.tol) {
+        a.status[b] = ILQR_TRAJ_CONVERGED;
+        if (a.res_parity) a.res_parity[b] = a.parity;
+      }
+    }
+  }
+}
+
+template <int NX, int NU>
+__device__ __forceinline__ void iter_forward_wave(const LQParams& P, int b0, int B, int T,
+                                                  const IterArgs& a, const LSParams& ls,
+                                                  double* ring) {
+  const int b = b0 + ((threadIdx.x & 63) >> 4);
+  const bool active = b < B && a.status[b < B ? b : b0] == ILQR_TRAJ_OK;
+  iter_forward_wave_active<NX, NU>(P, b0, B, T, a, ls, ring, active);
+}
+
+}  // namespace
+}  // namespace ilqr

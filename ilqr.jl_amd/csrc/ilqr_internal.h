@@ -54,6 +54,10 @@ hipError_t launch_lq_backward4(const LQParams& p, int B, int T, const double* x,
                                double* d, double* K, int32_t* status, double mu, hipStream_t s);
 hipError_t launch_lq_iter_backward4(const LQParams& p, int B, int T, const IterArgs& a, double mu,
                                     hipStream_t s);
+// backward (four trajectories per wave) + LDS-ring forward of one fit iteration in one
+// launch, (12, 4) only; the same bits as the two launches
+hipError_t launch_lq_iter_fused4(const LQParams& p, int B, int T, const IterArgs& a, const LSParams& ls,
+                                 hipStream_t s);
 hipError_t launch_lq_backward_v6(int nx, int nu, const LQParams& p, int B, int T, const double* x,
                                  const double* u, double* d, double* K, int32_t* status, double mu,
                                  hipStream_t s);

@@ -43,11 +43,12 @@ class MultiSolver:
         except Exception:
             pass
 
-    def set_schedule(self, pipelined: bool = False, ring_forward: bool = True, backward: str = "auto"):
+    def set_schedule(self, pipelined: bool = False, ring_forward: bool = True, backward: str = "auto",
+                     fused: bool = True):
         """As Solver.set_schedule, on every device's handle."""
         bk = {"auto": 0, "wave": _lib.SCHED_BACKWARD_WAVE, "block": _lib.SCHED_BACKWARD_BLOCK}[backward]
         flags = ((_lib.SCHED_PIPELINED if pipelined else 0) | (_lib.SCHED_RING_FORWARD if ring_forward else 0)
-                 | bk)
+                 | bk | (_lib.SCHED_FUSED if fused and not pipelined and backward != "wave" else 0))
         _lib.check(self.lib.ilqr_multi_set_schedule(self.h, flags), "ilqr_multi_set_schedule")
 
     def fit(self, lq: LQBatch, x_init, u_init, x_traj=None, max_iter=100, tol=1e-6, mu=None,

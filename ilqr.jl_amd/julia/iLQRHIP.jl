@@ -157,6 +157,7 @@ const ILQR_SCHED_PIPELINED = Int32(1)
 const ILQR_SCHED_RING_FORWARD = Int32(2)
 const ILQR_SCHED_BACKWARD_WAVE = Int32(4)
 const ILQR_SCHED_BACKWARD_BLOCK = Int32(8)
+const ILQR_SCHED_FUSED = Int32(16)
 set_schedule!(h::Handle, flags::Integer) =
     check(ccall((:ilqr_set_schedule, libilqr), Cint, (Ptr{Cvoid}, Cint), h.ptr, flags), "ilqr_set_schedule")
 

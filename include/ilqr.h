@@ -151,7 +151,12 @@ ilqr_status ilqr_sync(ilqr_handle* h);
  *   ILQR_SCHED_PIPELINED     fit runs one kernel per iteration in which half of the
  *                            workgroups do forward(i-1) then backward(i) while the
  *                            other half do backward(i) then forward(i) (default off;
- *                            implies ILQR_SCHED_BACKWARD_WAVE).
+ *                            implies ILQR_SCHED_BACKWARD_WAVE);
+ *   ILQR_SCHED_FUSED         ilqr_iterate / ilqr_fit run each iteration as ONE kernel:
+ *                            every wave does the backward pass of its four trajectories
+ *                            then their ring forward pass (with the BLOCK backward and
+ *                            the ring forward; ignored otherwise; not with WAVE or
+ *                            PIPELINED). A new handle starts with RING_FORWARD | FUSED.
  * Schedules with the same backward kernel return the same bits; the two backward
  * kernels agree to rounding. Unknown bits, or BLOCK with WAVE or
  * PIPELINED → ILQR_ERR_BAD_ARG. */
@@ -159,6 +164,7 @@ ilqr_status ilqr_sync(ilqr_handle* h);
 #define ILQR_SCHED_RING_FORWARD 2
 #define ILQR_SCHED_BACKWARD_WAVE 4
 #define ILQR_SCHED_BACKWARD_BLOCK 8
+#define ILQR_SCHED_FUSED 16
 ilqr_status ilqr_set_schedule(ilqr_handle* h, int flags);
 
 /* iLQR.backward_pass (backward_pass.jl:324-357): gains d (batch,T,nu) and

@@ -537,3 +537,32 @@ def test_fit_output_aliasing_input(gpu, max_iter, tol):
     assert rc == ref.call_status
     assert torch.equal(xi, ref.x) and torch.equal(ui, ref.u) and torch.equal(it, ref.iters)
     assert torch.equal(st, ref.status) and torch.equal(cost, ref.cost)
+
+
+@pytest.mark.parametrize("nb,T", [(4096, 100), (37, 17), (5, 3), (2051, 9)])
+def test_fused_iteration_equals_two_launches(gpu, nb, T):
+    """ILQR_SCHED_FUSED (one kernel: the block backward then the ring forward per wave)
+    returns the bits of the two-launch iteration, through iterate and fit, with a NaN
+    trajectory sharing a wave with clean ones."""
+    lq, x, u = (quadrotor_batch(nb, T=T, seed0=0) if nb == 4096
+                else random_lq_batch(nb, 12, 4, T, seed=nb * 5 + T))
+    if nb != 4096:
+        x[nb // 2, 1, 3] = np.nan
+    s = Solver(12, 4, T, nb)
+    s.set_problem(lq)
+    outs = []
+    for fused in (False, True):
+        s.set_schedule(backward="block", fused=fused)
+        xi, ui = dev(x), dev(u)
+        xn, un = torch.zeros_like(xi), torch.zeros_like(ui)  # a skipped (NaN) trajectory is never written
+        pc = torch.full((nb,), float("inf"), dtype=torch.float64, device="cuda")
+        st = torch.zeros((nb,), dtype=torch.int32, device="cuda")
+        tr = torch.zeros((nb,), dtype=torch.int32, device="cuda")
+        for _ in range(3):
+            s.iterate(xi, ui, xn, un, pc, st, trials=tr, options=_lib.default_options(tol=-1.0))
+            xi, xn, ui, un = xn, xi, un, ui
+        r = s.fit(dev(x), dev(u), max_iter=6, tol=1e-8)
+        torch.cuda.synchronize()
+        outs.append((xi, ui, pc, st, tr, r.x, r.u, r.cost, r.iters, r.status))
+    for a, b in zip(*outs):
+        torch.testing.assert_close(a, b, rtol=0, atol=0, equal_nan=True)
