@@ -381,260 +381,6 @@ __device__ unsigned lq_backward4_wave(const LQParams& P, int b0, int B, unsigned
   return r;
 }
 
-// v8 schedule of the same recursion (identical arithmetic, so identical bits): the
-// step is one basic block from the S hand-off to the gain solve. The L z branch runs
-// first; Y's B column and H go first so that H's LDS round trip overlaps the 27 MFMAs
-// of Y's A columns; after the read, the (H + μI) factor's dependent VALU chain shares
-// its block with the 41 independent MFMAs of G, Qxx and the gradient, which the
-// scheduler interleaves into the factor's latency gaps (v7 issued them before the
-// read, leaving the factor to run alone on the critical path).
-// SG bits (probe only): 1 = ask the scheduler for explicit VALU/MFMA alternation;
-// 2 = record the loop's shader-clock and 100 MHz real-time deltas into clk[0..1].
-template <int SG = 0>
-__device__ unsigned lq_backward4_wave_v8(const LQParams& P, int b0, int B, unsigned active, int T,
-                                         const double* __restrict__ x, const double* __restrict__ u,
-                                         double* __restrict__ d_out, double* __restrict__ K_out,
-                                         double mu, double* lds, unsigned long long* clk = nullptr) {
-  constexpr int NX = 12, NU = 4;
-  b0 = __builtin_amdgcn_readfirstlane(b0);
-  const int l = threadIdx.x & 63;
-  const int rho = l >> 4;
-  const int beta = (l >> 2) & 3;
-  const int kap = l & 3;
-  const int b = b0 + beta;
-  const bool live = b < B && ((active >> beta) & 1u);
-  const int bc = b < B ? b : B - 1;
-  const int nslot = B - b0 < 4 ? B - b0 : 4;
-
-  const double* Ab = P.A + (size_t)bc * NX * NX;
-  const double* Bb = P.B + (size_t)bc * NX * NU;
-  const double* Qb = P.Q + (size_t)bc * NX * NX;
-  const double* Rb = P.R + (size_t)bc * NU * NU;
-  const double* Qfb = P.Qf + (size_t)bc * NX * NX;
-
-  double F[3][4], L[3][3];
-#pragma unroll
-  for (int K = 0; K < 3; ++K) {
-    const int r = 4 * K + rho;
-#pragma unroll
-    for (int J = 0; J < 3; ++J) F[K][J] = Ab[r * NX + 4 * J + kap];
-    F[K][3] = Bb[r * NU + kap];
-#pragma unroll
-    for (int I = 0; I < 3; ++I) L[K][I] = Qb[r * NX + 4 * I + kap] + Qb[(4 * I + kap) * NX + r];
-  }
-  const double LR = Rb[rho * NU + kap] + Rb[kap * NU + rho];
-  const int tr_src = (16 * kap + 4 * beta + rho) * 4;
-
-  double S[3][3], s[3];
-  {
-    const double* xN = x + ((size_t)bc * (T + 1) + T) * NX;
-    double xr[3];
-#pragma unroll
-    for (int K = 0; K < 3; ++K) {
-      const int r = 4 * K + rho;
-      xr[K] = xN[r];
-#pragma unroll
-      for (int I = 0; I < 3; ++I) S[K][I] = Qfb[r * NX + 4 * I + kap] + Qfb[(4 * I + kap) * NX + r];
-    }
-#pragma unroll
-    for (int I = 0; I < 3; ++I) {
-      double v = 0.0;
-#pragma unroll
-      for (int K = 0; K < 3; ++K) v = mf4(S[K][I], xr[K], v);
-      s[I] = v;
-    }
-  }
-
-  const auto rX = buffer_rsrc(const_cast<double*>(x) + (size_t)b0 * (T + 1) * NX, (uint32_t)(nslot * (T + 1) * NX * 8));
-  const auto rU = buffer_rsrc(const_cast<double*>(u) + (size_t)b0 * T * NU, (uint32_t)(nslot * T * NU * 8));
-  const auto rK = buffer_rsrc(K_out + (size_t)b0 * T * NU * NX, (uint32_t)(nslot * T * NU * NX * 8));
-  const auto rD = buffer_rsrc(d_out + (size_t)b0 * T * NU, (uint32_t)(nslot * T * NU * 8));
-  const uint32_t DEAD = 0x80000000u;
-  const uint32_t kv = live ? (uint32_t)((beta * T * NU * NX + rho * NX + kap) * 8) : DEAD;
-  const uint32_t dv = (live && kap == 0) ? (uint32_t)((beta * T * NU + rho) * 8) : DEAD;
-
-  double Lzq[4] = {0.0, 0.0, 0.0, 0.0}, zq[4];
-  auto load_zq = [&](int t0) {
-    const int tz = t0 - kap > 0 ? t0 - kap : 0;
-    const uint32_t xo = (uint32_t)(((beta * (T + 1) + tz) * NX + rho) * 8);
-    const uint32_t uo = (uint32_t)(((beta * T + tz) * NU + rho) * 8);
-#pragma unroll
-    for (int K = 0; K < 3; ++K) zq[K] = buf_ld(rX, xo + 32 * K, 0);
-    zq[3] = buf_ld(rU, uo, 0);
-  };
-  load_zq(T - 1);
-
-  double* Hl = lds + beta * 16;
-  double Klast[4];
-  __builtin_amdgcn_s_waitcnt(0);
-  unsigned long long c0 = 0, r0 = 0;
-  if constexpr ((SG & 2) != 0) {
-    c0 = __builtin_readcyclecounter();
-    r0 = __builtin_amdgcn_s_memrealtime();
-  }
-
-  for (int t = T - 1; t >= 0; --t) {
-    // L z for steps t .. t-3 (column κ = step t-κ) every fourth step, then the next
-    // four steps' z — the step's only branch, ahead of the S-dependent block
-    const int j = (T - 1 - t) & 3;
-    if (j == 0) {
-#pragma unroll
-      for (int I = 0; I < 3; ++I) {
-        double v = 0.0;
-#pragma unroll
-        for (int K = 0; K < 3; ++K) v = mf4(L[K][I], zq[K], v);
-        Lzq[I] = v;
-      }
-      Lzq[3] = mf4(LR, zq[3], 0.0);
-      load_zq(t - 4);
-    }
-    // Y's B column, then H = R + Rᵀ + BᵀSB → LDS
-    double Y[3][4];
-#pragma unroll
-    for (int I = 0; I < 3; ++I) {
-      double v = 0.0;
-#pragma unroll
-      for (int K = 0; K < 3; ++K) v = mf4(S[K][I], F[K][3], v);
-      Y[I][3] = v;
-    }
-    double H = LR;
-#pragma unroll
-    for (int K = 0; K < 3; ++K) H = mf4(F[K][3], Y[K][3], H);
-    Hl[rho * 4 + kap] = H;
-    // Y's A columns cover the LDS round trip
-#pragma unroll
-    for (int J = 0; J < 3; ++J)
-#pragma unroll
-      for (int I = 0; I < 3; ++I) {
-        double v = 0.0;
-#pragma unroll
-        for (int K = 0; K < 3; ++K) v = mf4(S[K][I], F[K][J], v);
-        Y[I][J] = v;
-      }
-    wave_lds_fence();
-    double h[4][4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int k = 0; k <= i; ++k) h[i][k] = Hl[i * 4 + k];
-    // (H + μI) = L D Lᵀ in every lane of the slot, M = L⁻¹, this lane's M[ρ][κ], D⁻¹[ρ]
-    LDLT<4, 1> f;
-    f.factor(h, mu);
-    double Mf[4][4];
-    Mf[1][0] = -f.l[1][0];
-    Mf[2][1] = -f.l[2][1];
-    Mf[2][0] = fma(f.l[2][1], f.l[1][0], -f.l[2][0]);
-    Mf[3][2] = -f.l[3][2];
-    Mf[3][1] = fma(f.l[3][2], f.l[2][1], -f.l[3][1]);
-    Mf[3][0] = fma(-f.l[3][2], Mf[2][0], fma(-f.l[3][1], Mf[1][0], -f.l[3][0]));
-    double Mn = rho == kap ? 1.0 : 0.0;
-#pragma unroll
-    for (int i = 1; i < 4; ++i)
-#pragma unroll
-      for (int jj = 0; jj < i; ++jj) Mn = (rho == i && kap == jj) ? Mf[i][jj] : Mn;
-    double dsel = f.dinv[0];
-#pragma unroll
-    for (int i = 1; i < 4; ++i) dsel = rho == i ? f.dinv[i] : dsel;
-    const double Mt = lane_perm(Mn, tr_src), Mnd = Mn * dsel;
-    // independent of the factor: the gradient [lx + Aᵀs | lu + Bᵀs], G = BᵀSA, Qxx
-    double gv[4];
-    {
-      const int src = ((l & ~3) | j) * 4;
-#pragma unroll
-      for (int I = 0; I < 4; ++I) {
-        double v = lane_perm(Lzq[I], src);
-#pragma unroll
-        for (int K = 0; K < 3; ++K) v = mf4(F[K][I], s[K], v);
-        gv[I] = v;
-      }
-    }
-    double G[3], Z[3][3];
-#pragma unroll
-    for (int J = 0; J < 3; ++J) {
-      double v = 0.0;
-#pragma unroll
-      for (int K = 0; K < 3; ++K) v = mf4(F[K][3], Y[K][J], v);
-      G[J] = v;
-    }
-#pragma unroll
-    for (int I = 0; I < 3; ++I)
-#pragma unroll
-      for (int J = I; J < 3; ++J) {
-        double v = L[I][J];
-#pragma unroll
-        for (int K = 0; K < 3; ++K) v = mf4(F[K][I], Y[K][J], v);
-        Z[I][J] = v;
-      }
-    if constexpr ((SG & 1) != 0) {
-      // alternate one VALU op with one MFMA through the factor's chain
-#pragma unroll
-      for (int q = 0; q < 40; ++q) {
-        __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      }
-    }
-    // K_aug = −(D⁻¹M)ᵀ (M [G | g]) (two triangular sweeps as MFMA stages)
-    double Kg[4];
-#pragma unroll
-    for (int J = 0; J < 4; ++J) Kg[J] = mf4n(Mnd, mf4(Mt, J < 3 ? G[J] : gv[3], 0.0), 0.0);
-#pragma unroll
-    for (int J = 0; J < 3; ++J) buf_st(Kg[J], rK, kv + 32 * J, (uint32_t)(t * NU * NX * 8));
-    buf_st(Kg[3], rD, dv, (uint32_t)(t * NU * 8));
-    // step_back: [S | s] = [Qxx | lx + Aᵀs] − K_augᵀ W, W = μ K_aug − [G | g]
-    double W[4];
-#pragma unroll
-    for (int J = 0; J < 3; ++J) W[J] = fma(mu, Kg[J], -G[J]);
-    W[3] = fma(mu, Kg[3], -gv[3]);
-#pragma unroll
-    for (int I = 0; I < 3; ++I) {
-#pragma unroll
-      for (int J = I; J < 3; ++J) S[I][J] = mf4n(Kg[I], W[J], Z[I][J]);
-      s[I] = mf4n(Kg[I], W[3], gv[I]);
-    }
-    if ((t % SYM_EVERY) == 0) {
-#pragma unroll
-      for (int I = 0; I < 3; ++I) S[I][I] = 0.5 * (S[I][I] + lane_perm(S[I][I], tr_src));
-    }
-#pragma unroll
-    for (int I = 0; I < 3; ++I)
-#pragma unroll
-      for (int J = I + 1; J < 3; ++J) S[J][I] = lane_perm(S[I][J], tr_src);
-#pragma unroll
-    for (int J = 0; J < 4; ++J) Klast[J] = Kg[J];
-  }
-  if constexpr ((SG & 2) != 0) {
-    __builtin_amdgcn_s_waitcnt(0);
-    const unsigned long long c1 = __builtin_readcyclecounter(), r1 = __builtin_amdgcn_s_memrealtime();
-    if (clk && l == 0) { clk[0] = c1 - c0; clk[1] = r1 - r0; }
-  }
-  bool nan = false;
-#pragma unroll
-  for (int J = 0; J < 4; ++J) nan |= __builtin_isnan(Klast[J]);
-  const unsigned long long nb = __ballot(nan);
-  unsigned r = 0;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) r |= (nb & slot_lanes(q)) ? (1u << q) : 0u;
-  return r;
-}
-
-template <int SG = 0>
-__global__ __launch_bounds__(256) void lq_backward4_v8_kernel(LQParams P, int B, int T,
-                                                              const double* __restrict__ x,
-                                                              const double* __restrict__ u,
-                                                              double* __restrict__ d,
-                                                              double* __restrict__ K,
-                                                              int32_t* __restrict__ status, double mu,
-                                                              unsigned long long* clk = nullptr) {
-  __shared__ __attribute__((aligned(16))) double lds[BW4_WAVES * BW4_LDS];
-  const int w = threadIdx.x >> 6;
-  const int b0 = (blockIdx.x * BW4_WAVES + w) * BW4_SLOTS;
-  if (b0 >= B) return;
-  const unsigned nan = lq_backward4_wave_v8<SG>(P, b0, B, 0xFu, T, x, u, d, K, mu, lds + w * BW4_LDS,
-                                                clk ? clk + 2 * (b0 / BW4_SLOTS) : nullptr);
-  const int l = threadIdx.x & 63;
-  if (status && l < BW4_SLOTS && b0 + l < B) status[b0 + l] = ((nan >> l) & 1u) ? ILQR_TRAJ_NAN : ILQR_TRAJ_OK;
-}
-
 template <int ABL = 0>
 __global__ __launch_bounds__(256) void lq_backward4_kernel(LQParams P, int B, int T,
                                                            const double* __restrict__ x,
