@@ -16,11 +16,9 @@ namespace {
 __device__ __attribute__((noinline)) void big_sincos(double x, double* s, double* c) {
   sincos(x, s, c);
 }
-__device__ __forceinline__ void fast_sincos(double x, double& s, double& c) {
-  if (__builtin_expect(fabs(x) > 1e5, 0)) {
-    big_sincos(x, &s, &c);
-    return;
-  }
+// the reduction and polynomials alone: valid for |x| ≤ 1e5 (a caller that cannot
+// branch per evaluation checks the range itself and redoes the rare large argument)
+__device__ __forceinline__ void sincos_reduced(double x, double& s, double& c) {
   const double k = rint(x * 6.36619772367581382433e-01);  // x · 2/π
   double r = fma(-k, 1.5707963267948966e+00, x);
   r = fma(-k, 6.123233995736766e-17, r);
@@ -45,6 +43,13 @@ __device__ __forceinline__ void fast_sincos(double x, double& s, double& c) {
   const double b = (q & 1) ? sr : cr;
   s = (q & 2) ? -a : a;
   c = ((q + 1) & 2) ? -b : b;
+}
+__device__ __forceinline__ void fast_sincos(double x, double& s, double& c) {
+  if (__builtin_expect(fabs(x) > 1e5, 0)) {
+    big_sincos(x, &s, &c);
+    return;
+  }
+  sincos_reduced(x, s, c);
 }
 
 // fp32 counterpart: Cody-Waite reduction by π/2 (three-part float constant, Cephes

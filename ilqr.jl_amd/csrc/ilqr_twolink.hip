@@ -27,8 +27,10 @@
 //    family's ilqr_bw4.hip layout), the same exact step_back rewrite as the LQ
 //    kernels ([S s] = [Qxx | lx+Aᵀs] − Kᵀ((H+2μI)[K|d]); S's upper triangle
 //    mirrored, so it is symmetric by construction).
-//  * tl_forward: one lane per trajectory, RK4 rollout + α-halving line search
-//    (src/forward_pass.jl:55-93), inputs of step t+1 prefetched during step t.
+//  * tl_forward: RK4 rollout + α-halving line search (src/forward_pass.jl:55-93), a
+//    group of L = 4 lanes per trajectory evaluating four line-search candidates side by
+//    side (one lane per trajectory past B = 65536), on an RK4 rearranged for a short
+//    dependent chain (rk4_roll); inputs of step t+1 prefetched during step t.
 // The sequential passes are latency-bound (one RK4 or one Riccati step per step per
 // lane); with B = 1024 the chip is far from full — see DESIGN.md for the measured
 // numbers and what would change that.
@@ -49,7 +51,10 @@ constexpr int TL_NX = 4;
 template <int NU> constexpr int tl_nj() { return TL_NX * (TL_NX + NU); }
 template <int NU> constexpr int tl_njr() { return tl_nj<NU>() + 4; }  // 28 (NU = 2), 24 (NU = 1)
 constexpr int TL_NJR_MAX = 28;
-constexpr int TL_FW_PF = 2;                      // forward prefetch depth (steps)
+#ifndef ILQR_TL_FW_PF
+#define ILQR_TL_FW_PF 2
+#endif
+constexpr int TL_FW_PF = ILQR_TL_FW_PF;          // forward prefetch depth (steps)
 constexpr int TL_BW4_PF = 4;                     // backward prefetch depth (steps)
 
 // ---------------------------------------------------------------------------
@@ -408,12 +413,121 @@ __device__ unsigned tl_backward4_wave(const TwoLinkParams& P, int b0, int B, uns
 }
 
 // ---------------------------------------------------------------------------
-// Forward rollout + line search (src/forward_pass.jl:55-93), one lane per trajectory.
+// The rollout's RK4 in double (forward pass and rollout; the linearisation keeps
+// rk4<Dual> above). The same dynamics as continuous_dynamics + rk4, rearranged for
+// fewer instructions and a shorter dependent chain per step — one lane runs a step in
+// ≈230 f64 ops against ≈390 for rk4<double>:
+//  * θ̈ = M⁻¹(u − Cθ̇) with C = −g[1 ½; ½ 0], g = β sin θ₂ θ̇₂ (the k = 2-only Coriolis
+//    matrix of the reference, :36-47), and det M = δ(α − δ) − β² cos²θ₂ (M's entries
+//    are affine in cos θ₂): one 2×2 solve applied to a vector instead of M\C and M⁻¹u;
+//  * θ₁ never enters f, so the stages' θ₁ is never formed;
+//  * stages 2-4 take sin/cos(θ₂ + h) (h = ½k₁[2], ½k₂[2], k₃[2]) from stage 1's sin/cos θ₂
+//    by the angle-addition formulas and Taylor series in h (|h| ≤ 1/8: truncation below
+//    0.2 ulp); a rollout that meets a larger h is redone on rk4<double>.
+// Mathematically the reference's dynamicsf (2_link_helper_functions.jl:49-79); the
+// rounding differs from rk4<double>'s by a few ulp per step (tests/test_gpu_twolink.py).
+// ILQR_TL_RK4_SHIFT=0 builds the forward on rk4<double> instead (tools/tl_fw_probe.hip).
 // ---------------------------------------------------------------------------
+#ifndef ILQR_TL_RK4_SHIFT
+#define ILQR_TL_RK4_SHIFT 1
+#endif
+
+struct TLRoll {
+  double alpha, beta, delta, beta2, det0, bsq, dt;
+};
+__device__ __forceinline__ TLRoll tl_roll_consts(const TwoLinkParams& P) {
+  return {P.alpha, P.beta, P.delta, 2.0 * P.beta, P.delta * (P.alpha - P.delta), P.beta * P.beta, P.dt};
+}
+
+// θ̈ at (θ₂ with sin s2 / cos c2, θ̇ = (w1, w2), u)
+template <int NU>
+__device__ __forceinline__ void tl_accel(const TLRoll& R, double s2, double c2, double w1, double w2,
+                                         const double (&u)[NU], double& a1, double& a2) {
+  const double g = (R.beta * s2) * w2;
+  const double r0 = fma(g, fma(0.5, w2, w1), u[0]);  // u₁ − (Cθ̇)₁
+  const double hg = 0.5 * g;
+  const double r1 = NU > 1 ? fma(hg, w1, u[NU - 1]) : hg * w1;  // u₂ − (Cθ̇)₂
+  const double m00 = fma(R.beta2, c2, R.alpha);
+  const double m01 = fma(R.beta, c2, R.delta);
+  const double idet = tl_recip(fma(-(R.bsq * c2), c2, R.det0));
+  a1 = fma(R.delta, r0, -(m01 * r1)) * idet;
+  a2 = fma(m00, r1, -(m01 * r0)) * idet;
+}
+
+// sin/cos(θ + h) from s0 = sin θ, c0 = cos θ, for |h| ≤ 1/8 (the caller flags larger h)
+__device__ __forceinline__ void sincos_shift(double s0, double c0, double h, double& s, double& c) {
+  const double z = h * h;
+  double ps = fma(z, 1.0 / 362880.0, -1.0 / 5040.0);
+  ps = fma(z, ps, 1.0 / 120.0);
+  ps = fma(z, ps, -1.0 / 6.0);
+  const double sh = fma(h * z, ps, h);  // sin h, through h⁹
+  double pc = fma(z, -1.0 / 3628800.0, 1.0 / 40320.0);
+  pc = fma(z, pc, -1.0 / 720.0);
+  pc = fma(z, pc, 1.0 / 24.0);
+  pc = fma(z, pc, -0.5);
+  const double ch = fma(z, pc, 1.0);  // cos h, through h¹⁰
+  s = fma(s0, ch, c0 * sh);
+  c = fma(c0, ch, -(s0 * sh));
+}
+
+// One RK4 step without a branch (one basic block, so the scheduler can overlap the
+// stages' independent chains and the next step's reduction). `bad` is set when an
+// argument left the ranges the branch-free forms cover (|θ₂| > 1e5, |h| > 1/8); the
+// caller then redoes the rollout on rk4<double>.
+template <int NU>
+__device__ __forceinline__ void rk4_roll(const TLRoll& R, const double (&x)[4], const double (&u)[NU],
+                                         double (&out)[4], bool& bad) {
+  double s1, c1, s, c, a, b;
+  sincos_reduced(x[1], s1, c1);
+  tl_accel<NU>(R, s1, c1, x[2], x[3], u, a, b);
+  const double k10 = R.dt * x[2], k11 = R.dt * x[3], k12 = R.dt * a, k13 = R.dt * b;
+  double y2 = x[2] + 0.5 * k12, y3 = x[3] + 0.5 * k13;
+  sincos_shift(s1, c1, 0.5 * k11, s, c);
+  tl_accel<NU>(R, s, c, y2, y3, u, a, b);
+  const double k20 = R.dt * y2, k21 = R.dt * y3, k22 = R.dt * a, k23 = R.dt * b;
+  y2 = x[2] + 0.5 * k22;
+  y3 = x[3] + 0.5 * k23;
+  sincos_shift(s1, c1, 0.5 * k21, s, c);
+  tl_accel<NU>(R, s, c, y2, y3, u, a, b);
+  const double k30 = R.dt * y2, k31 = R.dt * y3, k32 = R.dt * a, k33 = R.dt * b;
+  y2 = x[2] + k32;
+  y3 = x[3] + k33;
+  sincos_shift(s1, c1, k31, s, c);
+  tl_accel<NU>(R, s, c, y2, y3, u, a, b);
+  const double k40 = R.dt * y2, k41 = R.dt * y3, k42 = R.dt * a, k43 = R.dt * b;
+  constexpr double sixth = 1.0 / 6.0;
+  out[0] = x[0] + sixth * (((k10 + 2.0 * k20) + 2.0 * k30) + k40);
+  out[1] = x[1] + sixth * (((k11 + 2.0 * k21) + 2.0 * k31) + k41);
+  out[2] = x[2] + sixth * (((k12 + 2.0 * k22) + 2.0 * k32) + k42);
+  out[3] = x[3] + sixth * (((k13 + 2.0 * k23) + 2.0 * k33) + k43);
+  // |h| ≤ 1/8 for h = ½k₁₁, ½k₂₁, k₃₁ ⇐ max(|k₁₁|, |k₂₁|, 2|k₃₁|) ≤ 1/4 (NaN: not flagged,
+  // the rollout is NaN on either path)
+  const double hm = fmax(fmax(fabs(k11), fabs(k21)), 2.0 * fabs(k31));
+  bad |= (hm > 0.25) | (fabs(x[1]) > 1e5);
+}
+
+// ---------------------------------------------------------------------------
+// Forward rollout + line search (src/forward_pass.jl:55-93) with L line-search
+// candidates per trajectory evaluated side by side: lane `sub` of a trajectory's
+// group of L adjacent lanes rolls out trial r·L + sub + 1 in round r, at
+// α = α₀·shrinkʳᴸ⁺ˢᵘᵇ formed by the same repeated multiplication as the reference's
+// `α *= shrink` (:82), and the group accepts the FIRST candidate in trial order whose
+// cost decreased (:77-80) — the sequential search's answer, bit for bit. Lane sub = 0
+// stores its rollout as it goes; an accepted candidate of another lane rolls out once
+// more, storing (same α, same rollout). Trials 1..L cost one pass (L = 1 is the
+// sequential search). With B·L ≤ 65536 the extra lanes sit on otherwise idle SIMDs.
+// ---------------------------------------------------------------------------
+template <bool ROBUST>
+struct TLPath {
+  static constexpr bool value = ROBUST;
+};
+
 struct TLFwdOut {
   double cost;
+  double du2;
   int trials;
   int accepted;
+  bool owner;  // this lane holds the trajectory's result
 };
 
 template <int NU>
@@ -421,22 +535,21 @@ struct TLStepIn {
   double x[4], xt[4], u[NU], d[NU], K[4 * NU];
 };
 
-template <int NU>
-__device__ TLFwdOut tl_forward_lane(const TwoLinkParams& P, int b, int T,
-                                    const double* __restrict__ x, const double* __restrict__ u,
-                                    const double* __restrict__ xtraj,
-                                    const double* __restrict__ dg, const double* __restrict__ Kg,
-                                    double prev_cost, double* __restrict__ xnew,
-                                    double* __restrict__ unew, double* du2_out,
-                                    const LSParams& ls) {
+template <int NU, int L>
+__device__ TLFwdOut tl_forward_group(const TwoLinkParams& P, int b, int B, int T,
+                                     const double* __restrict__ x, const double* __restrict__ u,
+                                     const double* __restrict__ xtraj,
+                                     const double* __restrict__ dg, const double* __restrict__ Kg,
+                                     double prev_cost, double* __restrict__ xnew,
+                                     double* __restrict__ unew, const LSParams& ls) {
   const double* xb0 = x + (size_t)b * (T + 1) * TL_NX;
   const double* ub0 = u + (size_t)b * T * NU;
   const double* xt0 = (xtraj ? xtraj : x) + (size_t)b * (T + 1) * TL_NX;
   const double xtw = xtraj ? 1.0 : 0.0;  // x_traj = NULL means zeros (forward_pass.jl:151)
   const double* d0 = dg + (size_t)b * T * NU;
   const double* K0 = Kg + (size_t)b * T * NU * TL_NX;
-  double* xo = xnew + (size_t)b * (T + 1) * TL_NX;
-  double* uo = unew + (size_t)b * T * NU;
+  const TLRoll R = tl_roll_consts(P);
+  const int lane = threadIdx.x & 63, sub = lane & (L - 1), gbase = lane & ~(L - 1);
 
   auto load = [&](int t, TLStepIn<NU>& in) {
     const int tt = t < T ? t : T - 1;
@@ -453,17 +566,42 @@ __device__ TLFwdOut tl_forward_lane(const TwoLinkParams& P, int b, int T,
     }
   };
 
-  double alpha = ls.alpha0;
-  TLFwdOut out{0.0, 0, 0};
-  double du2 = 0.0;
-  for (int trial = 1; trial <= ls.max_trials; ++trial) {
+  // the wave's outputs through buffer resources on its first trajectory: a lane that
+  // does not store gets an out-of-range offset (dropped by the bounds check), so the
+  // stores need no branch and a pass's steps stay one basic block for the scheduler
+  const int bw = __builtin_amdgcn_readfirstlane(b);
+  const int nslot = B - bw < 64 / L ? B - bw : 64 / L;
+  const auto rX = buffer_rsrc(xnew + (size_t)bw * (T + 1) * TL_NX, (uint32_t)((size_t)nslot * (T + 1) * TL_NX * 8));
+  const auto rU = buffer_rsrc(unew + (size_t)bw * T * NU, (uint32_t)((size_t)nslot * T * NU * 8));
+  const uint32_t offX = (uint32_t)((size_t)(b - bw) * (T + 1) * TL_NX * 8);
+  const uint32_t offU = (uint32_t)((size_t)(b - bw) * T * NU * 8);
+
+  TLFwdOut out{0.0, 0.0, 0, 0, false};
+  double alpha_r = ls.alpha0;  // α of this round's first candidate
+  double alpha = alpha_r;
+  for (int j = 0; j < sub; ++j) alpha *= ls.shrink;
+  int r = 0;
+  bool store = sub == 0, rerun = false;
+  struct Pass {
+    double cost, du2;
+    bool bad;
+  };
+  // one rollout at α (:64-76): ROBUST = rk4<double> (every argument range), else rk4_roll
+  auto pass = [&](auto robust) -> Pass {
+    constexpr bool ROBUST = decltype(robust)::value;
+    const uint32_t sx = store ? offX : 0x80000000u, su = store ? offU : 0x80000000u;
     double xb[4];
     {
       const double4 xv = *reinterpret_cast<const double4*>(xb0);  // x̄₁ = x₁ (:65)
       xb[0] = xv.x; xb[1] = xv.y; xb[2] = xv.z; xb[3] = xv.w;
     }
-    double cost = 0.0;
-    du2 = 0.0;
+    auto put_x = [&](int t) {
+      typedef unsigned u4v_ __attribute__((ext_vector_type(4)));
+      const uint32_t o = sx + (uint32_t)(t * TL_NX * 8);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v_, make_double2(xb[0], xb[1])), rX, o, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v_, make_double2(xb[2], xb[3])), rX, o + 16, 0, 0);
+    };
+    Pass p{0.0, 0.0, false};
     auto step = [&](int t, const TLStepIn<NU>& in) {
       // δx = x̄ₖ − xₖ (:72); ūₖ = uₖ + α δuₖ + Kₖ δx (:73)
       double dx[4];
@@ -483,20 +621,21 @@ __device__ TLFwdOut tl_forward_lane(const TwoLinkParams& P, int b, int T,
       double uu;
       if constexpr (NU == 2) uu = ubar[0] * ubar[0] + ubar[NU - 1] * ubar[NU - 1];
       else uu = ubar[0] * ubar[0];
-      cost += (e0 * e0 + e1 * e1) + uu;
-      *reinterpret_cast<double4*>(xo + (size_t)t * TL_NX) = make_double4(xb[0], xb[1], xb[2], xb[3]);
+      p.cost += (e0 * e0 + e1 * e1) + uu;
+      put_x(t);
 #pragma unroll
-      for (int a = 0; a < NU; ++a) uo[(size_t)t * NU + a] = ubar[a];
+      for (int a = 0; a < NU; ++a) store_or_drop(ubar[a], rU, true, su + (uint32_t)((t * NU + a) * 8));
       const double du0 = ubar[0] - in.u[0];
       if constexpr (NU == 2) {
         const double du1 = ubar[NU - 1] - in.u[NU - 1];
-        du2 = fma(du0, du0, fma(du1, du1, du2));
+        p.du2 = fma(du0, du0, fma(du1, du1, p.du2));
       } else {
-        du2 = fma(du0, du0, du2);
+        p.du2 = fma(du0, du0, p.du2);
       }
       // x̄ₖ₊₁ = f(x̄ₖ, ūₖ) (:74)
       double xn[4];
-      rk4<double, NU>(P, xb, ubar, xn);
+      if constexpr (ROBUST) rk4<double, NU>(P, xb, ubar, xn);
+      else rk4_roll<NU>(R, xb, ubar, xn, p.bad);
 #pragma unroll
       for (int i = 0; i < 4; ++i) xb[i] = xn[i];
     };
@@ -515,26 +654,57 @@ __device__ TLFwdOut tl_forward_lane(const TwoLinkParams& P, int b, int T,
 #pragma unroll
     for (int k = 0; k < TL_FW_PF - 1; ++k)
       if (t + k < T) step(t + k, ring[k]);
-    *reinterpret_cast<double4*>(xo + (size_t)T * TL_NX) = make_double4(xb[0], xb[1], xb[2], xb[3]);
+    put_x(T);
     // final_cost(x̄_N) on the raw state (:192; 2_link_helper_functions.jl:100-108)
     const double f0 = P.tgt0 - xb[0], f1 = P.tgt1 - xb[1];
-    cost += f0 * f0 + f1 * f1;
-    out.trials = trial;
-    out.cost = cost;
-    if (prev_cost - cost > 0.0) {  // (:77-80); NaN compares false → keep searching
+    p.cost += f0 * f0 + f1 * f1;
+    return p;
+  };
+  while (true) {
+#if ILQR_TL_RK4_SHIFT
+    Pass p = pass(TLPath<false>{});
+    if (p.bad) p = pass(TLPath<true>{});  // an argument out of rk4_roll's ranges: redo
+#else
+    const Pass p = pass(TLPath<true>{});
+#endif
+    const double cost = p.cost, du2 = p.du2;
+    if (rerun) break;  // the accepted candidate's rollout, now stored
+    const int k = r * L + sub;  // 0-based trial index of this lane's candidate
+    const bool acc = k < ls.max_trials && prev_cost - cost > 0.0;  // NaN compares false
+    const unsigned am = (unsigned)(__ballot(acc) >> gbase) & ((1u << L) - 1u);
+    if (am) {
+      const int first = __builtin_ctz(am);
+      if (sub != first) break;
+      out.trials = k + 1;
       out.accepted = 1;
+      out.cost = cost;
+      out.du2 = du2;
+      out.owner = true;
+      if (store) break;
+      store = rerun = true;  // roll out once more, storing
+      continue;
+    }
+    if ((r + 1) * L >= ls.max_trials) {  // exhausted (the reference would loop forever)
+      if (k == ls.max_trials - 1) {
+        out.trials = k + 1;
+        out.cost = cost;
+        out.du2 = du2;
+        out.owner = true;
+      }
       break;
     }
-    alpha *= ls.shrink;  // (:82)
+    ++r;
+#pragma unroll
+    for (int j = 0; j < L; ++j) alpha_r *= ls.shrink;
+    alpha = alpha_r;
+    for (int j = 0; j < sub; ++j) alpha *= ls.shrink;
   }
-  if (du2_out) *du2_out = du2;
   return out;
 }
 
 // ---------------------------------------------------------------------------
 // Kernels
 // ---------------------------------------------------------------------------
-constexpr int TL_WG = 64;  // one wave per workgroup: B = 1024 spreads over 16 CUs
 
 // four trajectories per wave, four waves per workgroup
 constexpr int TL_BW4_WAVES = 4;
@@ -555,17 +725,27 @@ __global__ __launch_bounds__(64 * TL_BW4_WAVES) void tl_backward_kernel(TwoLinkP
   if (status && l < 4 && b0 + l < B) status[b0 + l] = ((nan >> l) & 1u) ? ILQR_TRAJ_NAN : ILQR_TRAJ_OK;
 }
 
-template <int NU>
-__global__ __launch_bounds__(TL_WG) void tl_forward_kernel(
+// L = 4 line-search candidates per trajectory up to B = 65536, one lane per trajectory
+// past it. At B = 1024 the candidate lanes sit on otherwise idle SIMDs (trial 1: 28.0
+// vs 27.6 µs; trials 1-4: 61.9 vs 143.5 µs, nu = 1, T = 50); at B = 65536, where one
+// lane per trajectory already fills every SIMD, the candidates' extra waves still hide
+// latency (236 vs 275 µs; profiles/r02/tl_fw_probe.log). W waves per workgroup: 1 for
+// the candidate grids (four 1-lane waves on one CU at B = 1024 ran 27.6 → 54.7 µs), 4
+// past B = 65536 (1-wave workgroups past 256 waves were packed two to a SIMD).
+inline int tl_fw_lanes(int B) { return B <= 65536 ? 4 : 1; }
+
+template <int NU, int L, int W>
+__global__ __launch_bounds__(64 * W) void tl_forward_kernel(
     TwoLinkParams P, int B, int T, const double* __restrict__ x, const double* __restrict__ u,
     const double* __restrict__ xtraj, const double* __restrict__ d, const double* __restrict__ K,
     const double* __restrict__ prev_cost, double* __restrict__ xnew, double* __restrict__ unew,
     double* __restrict__ new_cost, int32_t* __restrict__ trials, int32_t* __restrict__ status,
     LSParams ls) {
-  const int b = blockIdx.x * TL_WG + threadIdx.x;
+  const int b = (blockIdx.x * 64 * W + threadIdx.x) / L;  // a group of L lanes per trajectory
   if (b >= B) return;
   const double pc = prev_cost ? prev_cost[b] : INFINITY;
-  const TLFwdOut r = tl_forward_lane<NU>(P, b, T, x, u, xtraj, d, K, pc, xnew, unew, nullptr, ls);
+  const TLFwdOut r = tl_forward_group<NU, L>(P, b, B, T, x, u, xtraj, d, K, pc, xnew, unew, ls);
+  if (!r.owner) return;
   if (!r.accepted) {  // exhausted (the reference would loop forever): return the inputs
     for (int i = 0; i < (T + 1) * TL_NX; ++i) xnew[(size_t)b * (T + 1) * TL_NX + i] = x[(size_t)b * (T + 1) * TL_NX + i];
     for (int i = 0; i < T * NU; ++i) unew[(size_t)b * T * NU + i] = u[(size_t)b * T * NU + i];
@@ -599,24 +779,23 @@ __global__ __launch_bounds__(64 * TL_BW4_WAVES) void tl_iter_backward_kernel(Two
 }
 
 // Forward part + the convergence test (:163-175).
-template <int NU>
-__global__ __launch_bounds__(TL_WG) void tl_iter_forward_kernel(TwoLinkParams P, int B, int T,
-                                                                IterArgs a, LSParams ls) {
-  const int b = blockIdx.x * TL_WG + threadIdx.x;
+template <int NU, int L, int W>
+__global__ __launch_bounds__(64 * W) void tl_iter_forward_kernel(TwoLinkParams P, int B, int T,
+                                                                 IterArgs a, LSParams ls) {
+  const int b = (blockIdx.x * 64 * W + threadIdx.x) / L;
   if (b >= B || a.status[b] != ILQR_TRAJ_OK) return;
-  double du2 = 0.0;
   const double pc = a.prev_cost ? a.prev_cost[b] : INFINITY;
-  const TLFwdOut r = tl_forward_lane<NU>(P, b, T, a.x, a.u, a.xtraj, a.d, a.K, pc, a.xnew, a.unew,
-                                         &du2, ls);
+  const TLFwdOut r = tl_forward_group<NU, L>(P, b, B, T, a.x, a.u, a.xtraj, a.d, a.K, pc, a.xnew, a.unew, ls);
+  if (!r.owner) return;
   if (a.trials) a.trials[b] = r.trials;
-  if (a.du2) a.du2[b] = du2;
+  if (a.du2) a.du2[b] = r.du2;
   if (a.iters) a.iters[b] = a.iter;
   if (!r.accepted) {
     a.status[b] = (r.cost != r.cost) ? ILQR_TRAJ_NAN : ILQR_TRAJ_LS_EXHAUSTED;
     if (a.res_parity) a.res_parity[b] = a.parity;
   } else {
     a.new_cost[b] = r.cost;  // prev_cost = new_cost (:168)
-    if (du2 <= ls.tol) {      // (:171) break BEFORE the update → result is the input iterate
+    if (r.du2 <= ls.tol) {   // (:171) break BEFORE the update → result is the input iterate
       a.status[b] = ILQR_TRAJ_CONVERGED;
       if (a.res_parity) a.res_parity[b] = a.parity;
     }
@@ -664,27 +843,39 @@ hipError_t tl_backward_nu(const TwoLinkParams& P, int B, int T, const double* x,
   return hipGetLastError();
 }
 
+// the forward's buffer resources span one wave's trajectories: 64 · (T+1) · 32 bytes
+// below 2³¹ (the out-of-range offset that drops a store)
+inline bool tl_fw_fits(int T) { return (size_t)64 * (T + 1) * TL_NX * 8 < 0x80000000ull; }
+
 template <int NU>
 hipError_t tl_forward_nu(const TwoLinkParams& P, int B, int T, const double* x, const double* u,
                          const double* xtraj, const double* d, const double* K,
                          const double* prev_cost, double* xnew, double* unew, double* new_cost,
                          int32_t* trials, int32_t* status, const LSParams& ls, hipStream_t s) {
-  tl_forward_kernel<NU><<<(B + TL_WG - 1) / TL_WG, TL_WG, 0, s>>>(P, B, T, x, u, xtraj, d, K,
-                                                                  prev_cost, xnew, unew, new_cost,
-                                                                  trials, status, ls);
+  if (!tl_fw_fits(T)) return hipErrorInvalidValue;
+  if (tl_fw_lanes(B) == 4)
+    tl_forward_kernel<NU, 4, 1><<<(4 * B + 63) / 64, 64, 0, s>>>(
+        P, B, T, x, u, xtraj, d, K, prev_cost, xnew, unew, new_cost, trials, status, ls);
+  else
+    tl_forward_kernel<NU, 1, 4><<<(B + 255) / 256, 256, 0, s>>>(
+        P, B, T, x, u, xtraj, d, K, prev_cost, xnew, unew, new_cost, trials, status, ls);
   return hipGetLastError();
 }
 
 template <int NU>
 hipError_t tl_iteration_nu(const TwoLinkParams& P, int B, int T, const IterArgs& a, double* J,
                            const LSParams& ls, hipStream_t s) {
+  if (!tl_fw_fits(T)) return hipErrorInvalidValue;
   tl_linearize_kernel<NU><<<dim3((B + 255) / 256, T), 256, 0, s>>>(P, B, T, a.x, a.u, a.status, J);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const int per_wg = 4 * TL_BW4_WAVES;
   tl_iter_backward_kernel<NU><<<(B + per_wg - 1) / per_wg, 64 * TL_BW4_WAVES, 0, s>>>(P, B, T, a, J, ls.mu);
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  tl_iter_forward_kernel<NU><<<(B + TL_WG - 1) / TL_WG, TL_WG, 0, s>>>(P, B, T, a, ls);
+  if (tl_fw_lanes(B) == 4)
+    tl_iter_forward_kernel<NU, 4, 1><<<(4 * B + 63) / 64, 64, 0, s>>>(P, B, T, a, ls);
+  else
+    tl_iter_forward_kernel<NU, 1, 4><<<(B + 255) / 256, 256, 0, s>>>(P, B, T, a, ls);
   return hipGetLastError();
 }
 }  // namespace

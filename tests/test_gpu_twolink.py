@@ -278,3 +278,90 @@ def test_tl_nu1_config2_batch(gpu):
                        tol=1e-6, max_trials=64, history=h)
         assert int(r.iters[b]) == len(h), b
         assert rel(r.u[b], fu) < TOL_FIT, b
+
+
+# -- the forward's line-search candidate groups and rollout fallback (ilqr_twolink.hip:
+# tl_forward_group, rk4_roll) ---------------------------------------------------------------
+def _search_case(g, scales):
+    """Trajectories of the fixture with δu scaled so the α-halving search needs 1..n
+    trials against prev_cost = the cost of the input trajectory."""
+    TL = O.TwoLink
+    nb = g["u"].shape[0]
+    idx = np.arange(len(scales)) % nb
+    x, u, K = g["x"][idx], g["u"][idx], g["K"][idx]
+    d = g["d"][idx] * np.asarray(scales, dtype=float)[:, None, None]
+    pc = np.array([O.total_cost_generator(np.zeros_like(x[i]), TL.immediate_cost, TL.final_cost)(x[i], u[i])
+                   for i in range(len(scales))])
+    return x, u, d, K, pc
+
+
+def test_tl_forward_candidates_match_sequential(gpu, g):
+    """Four candidates per trajectory side by side (B ≤ 65536) accept the trial the
+    sequential search of forward_pass.jl:70-87 accepts: trial counts 1..>4 (rounds past
+    the first), rollouts and costs against the oracle."""
+    nb, T = g["u"].shape[:2]
+    scales = [1, 3, 6, 12, 24, 48, 96, 3, 400]  # trials 1-7 and 9 (tests/golden: 3 trajectories)
+    x, u, d, K, pc = _search_case(g, scales)
+    s = tl_solver(T, len(scales))
+    xn, un, cost, trials, st = s.forward(dev(x), dev(u), dev(d), dev(K), dev(pc))
+    assert (st.cpu().numpy() == _lib.TRAJ_OK).all()
+    TL = O.TwoLink
+    seen = set()
+    for i in range(len(scales)):
+        so = {}
+        xo, uo, co = O.forward_pass(x[i], u[i], np.zeros_like(x[i]), d[i], K[i], pc[i], TL.dynamicsf,
+                                    TL.immediate_cost, TL.final_cost, max_trials=64, stats=so)
+        assert int(trials[i]) == so["trials"], i
+        seen.add(so["trials"])
+        assert rel(xn[i], xo) < 1e-11 and rel(un[i], uo) < 1e-11, i
+        assert abs(float(cost[i]) - co) / co < TOL_COST, i
+    assert max(seen) > 4 and len(seen) >= 4, seen  # first, later and past-the-first-round trials
+
+
+def test_tl_forward_exhaustion_across_rounds(gpu, g):
+    """max_trials = 6 (not a multiple of the 4 candidates): an unreachable prev_cost
+    exhausts after trial 6 with the inputs returned; a reachable one accepts."""
+    nb, T = g["u"].shape[:2]
+    x, u, d, K, pc = _search_case(g, [1, 24])  # the second needs 5 trials
+    pc[0] = -1.0  # no rollout has a negative cost
+    s = tl_solver(T, 2)
+    xn, un, cost, trials, st = s.forward(dev(x), dev(u), dev(d), dev(K), dev(pc), max_trials=6)
+    st = st.cpu().numpy()
+    assert st[0] == _lib.TRAJ_LS_EXHAUSTED and int(trials[0]) == 6
+    assert rel(xn[0], x[0]) == 0.0 and rel(un[0], u[0]) == 0.0
+    assert st[1] == _lib.TRAJ_OK and 1 < int(trials[1]) <= 6
+
+
+def test_tl_forward_wide_batch_equals_grouped(gpu, g):
+    """Past B = 65536 the forward runs one lane per trajectory (sequential trials); the
+    same trajectories in a small batch (candidate groups) give bit-identical results."""
+    nb, T = g["u"].shape[:2]
+    scales = [1, 6, 24, 96, 48, 3, 12, 48]
+    x, u, d, K, pc = _search_case(g, scales)
+    Bw = 65544
+    rep = np.arange(Bw) % len(scales)
+    sw = tl_solver(T, Bw)
+    rw = sw.forward(dev(x[rep]), dev(u[rep]), dev(d[rep]), dev(K[rep]), dev(pc[rep]))
+    ss = tl_solver(T, len(scales))
+    rs = ss.forward(dev(x), dev(u), dev(d), dev(K), dev(pc))
+    for a, b in zip(rw, rs):
+        a, b = a.cpu().numpy(), b.cpu().numpy()
+        for off in (0, 8 * 1000, Bw - len(scales) - (Bw % len(scales))):
+            np.testing.assert_array_equal(a[off:off + len(scales)], b)
+
+
+def test_tl_rollout_fast_velocity_fallback(gpu):
+    """|θ̇₂|·Δt beyond rk4_roll's series range (h > 1/8) redoes the rollout on the
+    generic RK4; fast and slow trajectories share waves. Rollouts against the oracle."""
+    T = 30
+    rng = np.random.default_rng(5)
+    x0 = rng.random((64, 4))
+    x0[::3, 3] = 40.0 * (rng.random(22) - 0.5) + 30.0  # |θ̇₂| up to 50 rad/s
+    x0[1::7, 1] = 1e3 + rng.random(9)                   # large angles (reduction by π/2)
+    u = 0.5 * rng.standard_normal((64, T, 2))
+    s = tl_solver(T, 64)
+    x = s.rollout(dev(x0), dev(u))
+    f, _, _ = two_link_closures()
+    for b in range(64):
+        ref = O.rollout(x0[b], u[b], f)
+        assert rel(x[b], ref) < TOL_ROLL * 10, b

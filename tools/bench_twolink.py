@@ -93,12 +93,12 @@ def main():
     lin_fl = f_rk4 * FL.dual_factor(4 + NU) * T * B
     ric_fl = FL.riccati_flops_per_step(4, NU) * T * B
     fw_fl = FL.forward_flops_per_step(4, NU, f_rk4) * T * B
-    roof = {"bound": "latency (one lane per trajectory in the forward; B = 1024 fills 16 waves)",
+    roof = {"bound": "latency (the forward is one dependent RK4 chain per trajectory; B = 1024 fills 64 of 1024 SIMDs)",
             "unit": "TFLOP/s", "peak": FP64_PEAK_TFLOPS,
             "backward": {"kernels": "tl_linearize + tl_backward (4 trajectories per wave, 4x4x4 f64 MFMA)",
                          "avg_launch_ms": bw_ms, "algorithmic_flops": lin_fl + ric_fl,
                          "achieved": (lin_fl + ric_fl) / (bw_ms * 1e-3) / 1e12},
-            "forward": {"kernel": "tl_forward (one lane per trajectory)", "avg_launch_ms": fw_ms,
+            "forward": {"kernel": "tl_forward (4 line-search candidate lanes per trajectory, branch-free rk4_roll)", "avg_launch_ms": fw_ms,
                         "algorithmic_flops": fw_fl, "achieved": fw_fl / (fw_ms * 1e-3) / 1e12},
             "flops_note": f"RK4 of the reference's formulas = {f_rk4} flop (tools/flops.py); dual factor "
                           f"1+2·ND; Riccati per SURVEY §8d"}
