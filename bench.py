@@ -418,7 +418,9 @@ def main():
                              "achieved_tflops": it_flops / (single_ms * 1e-3) / 1e12,
                              "frac_fp64_peak": it_flops / (single_ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS,
                              "achieved_gbps": it_bytes / (single_ms * 1e-3) / 1e9,
-                             "frac_hbm_peak": it_bytes / (single_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS},
+                             "frac_hbm_peak": it_bytes / (single_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
+                             "algorithmic_bytes_per_launch": it_bytes,
+                             "traffic": (pmc or {}).get("hbm_bytes_per_fused_launch")},
         "allgather_costs_ms": gather_ms,
         "allgather_check": gathered,
         "cpu_baseline": None,

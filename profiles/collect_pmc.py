@@ -29,6 +29,7 @@ def read(d, counter):
             name = r["Kernel_Name"]
             key = ("backward" if "lq_iter_backward" in name else
                    "forward" if "lq_iter_forward" in name else
+                   "fused" if "lq_iter_fused" in name else
                    "backward_api" if "lq_backward" in name else None)
             if key:
                 vals[key].append(float(r["Counter_Value"]))
@@ -48,6 +49,8 @@ def main(fetch_dir, write_dir, out):
     be = res.get("backward") or res.get("backward_api")
     if be:
         res["hbm_bytes_per_backward_launch"] = be["hbm_bytes_corrected"]
+    if res.get("fused"):
+        res["hbm_bytes_per_fused_launch"] = res["fused"]["hbm_bytes_corrected"]
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res, indent=1))
 
