@@ -94,15 +94,23 @@ def lq_fit(lq, x_init, u_init, x_traj=None, max_iter=100, tol=1e-6, mu=0.01, max
     return xo, uo, cost, iters, st
 
 
+def host_threads():
+    """Threads for a CPU-baseline leg: every CPU this process may run on, capped at the
+    operator's per-GPU share when OMP_NUM_THREADS is set (16 on the GPU pool)."""
+    n = len(os.sched_getaffinity(0))
+    share = os.environ.get("OMP_NUM_THREADS", "")
+    return min(n, int(share)) if share.isdigit() and int(share) > 0 else n
+
+
 # -- 2-link arm (test/2_link_example) ---------------------------------------------
 def tl_backward(x, u, mu=0.01, symmetrize=False, nthreads=0):
     lib = load()
     x, u = _f64(x), _f64(u)
-    nb, T = u.shape[:2]
-    d = np.empty((nb, T, 2))
-    K = np.empty((nb, T, 2, 4))
+    nb, T, nu = u.shape
+    d = np.empty((nb, T, nu))
+    K = np.empty((nb, T, nu, 4))
     st = np.empty(nb, dtype=np.int32)
-    lib.oracle_tl_backward(nb, T, _p(x), _p(u), C.c_double(mu), int(symmetrize), _p(d), _p(K),
+    lib.oracle_tl_backward(nb, T, nu, _p(x), _p(u), C.c_double(mu), int(symmetrize), _p(d), _p(K),
                            _p(st), nthreads)
     return d, K, st
 
@@ -110,14 +118,14 @@ def tl_backward(x, u, mu=0.01, symmetrize=False, nthreads=0):
 def tl_forward(x, u, x_traj, d, K, prev_cost, max_trials=64, alpha0=1.0, shrink=0.5, nthreads=0):
     lib = load()
     x, u, d, K = _f64(x), _f64(u), _f64(d), _f64(K)
-    nb, T = u.shape[:2]
+    nb, T, nu = u.shape
     xt = None if x_traj is None else _f64(x_traj)
     pc = _f64(np.broadcast_to(np.asarray(prev_cost, dtype=np.float64), (nb,)))
     xn = np.empty((nb, T + 1, 4))
-    un = np.empty((nb, T, 2))
+    un = np.empty((nb, T, nu))
     cost = np.empty(nb)
     tr = np.empty(nb, dtype=np.int32)
-    lib.oracle_tl_forward(nb, T, _p(x), _p(u), _p(xt), _p(d), _p(K), _p(pc), _p(xn), _p(un),
+    lib.oracle_tl_forward(nb, T, nu, _p(x), _p(u), _p(xt), _p(d), _p(K), _p(pc), _p(xn), _p(un),
                           _p(cost), _p(tr), max_trials, C.c_double(alpha0), C.c_double(shrink),
                           nthreads)
     return xn, un, cost, tr
@@ -127,14 +135,14 @@ def tl_fit(x_init, u_init, x_traj=None, max_iter=100, tol=1e-6, mu=0.01, max_tri
            symmetrize=False, nthreads=0):
     lib = load()
     xi, ui = _f64(x_init), _f64(u_init)
-    nb, T = ui.shape[:2]
+    nb, T, nu = ui.shape
     xt = None if x_traj is None else _f64(x_traj)
     xo = np.empty((nb, T + 1, 4))
-    uo = np.empty((nb, T, 2))
+    uo = np.empty((nb, T, nu))
     cost = np.empty(nb)
     iters = np.empty(nb, dtype=np.int32)
     st = np.empty(nb, dtype=np.int32)
-    lib.oracle_tl_fit(nb, T, _p(xi), _p(ui), _p(xt), max_iter, C.c_double(tol), C.c_double(mu),
+    lib.oracle_tl_fit(nb, T, nu, _p(xi), _p(ui), _p(xt), max_iter, C.c_double(tol), C.c_double(mu),
                       int(symmetrize), max_trials, _p(xo), _p(uo), _p(cost), _p(iters), _p(st),
                       nthreads)
     return xo, uo, cost, iters, st
@@ -142,9 +150,9 @@ def tl_fit(x_init, u_init, x_traj=None, max_iter=100, tol=1e-6, mu=0.01, max_tri
 
 def twolink_cpu_baseline(x, u, batch, budget_s):
     """bench_twolink's cpu_baseline leg: one cold-start iteration (backward +
-    forward) per trajectory of the 2-link workload, OpenMP over trajectories."""
+    forward) per trajectory of the 2-link workload (nu from u), OpenMP over trajectories."""
     import time
-    threads = min(16, os.cpu_count() or 1)
+    threads = host_threads()
     n = 64
     while True:
         idx = np.arange(n) % x.shape[0]

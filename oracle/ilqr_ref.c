@@ -314,10 +314,49 @@ static double tl_fcost(const prob_t* P, const double* x) {
   const double e0 = TL.tgt0 - x[0], e1 = TL.tgt1 - x[1];
   return (e0 * e0 + e1 * e1) * 1.0;
 }
-static prob_t tl_problem(int T) {
+/* the nu = 1 variant f(x, [u₁, 0]) (BASELINE.json configs 1-2; build-defined, see
+ * oracle/ilqr_oracle.py TwoLink.dynamicsf_nu1): the second torque a constant 0, its
+ * dual direction absent */
+static void tl_lin1(const prob_t* P, int t, const double* x, const double* u, double* A, double* B) {
+  (void)P; (void)t;
+  dual6 xs[4], us[2], out[4];
+  for (int i = 0; i < 4; ++i) { xs[i] = dc(x[i]); xs[i].d[i] = 1.0; }
+  us[0] = dc(u[0]);
+  us[0].d[4] = 1.0;
+  us[1] = dc(0.0);
+  tl_rk4_dual(xs, us, out);
+  for (int i = 0; i < 4; ++i) {
+    for (int k = 0; k < 4; ++k) A[i * 4 + k] = out[i].d[k];
+    B[i] = out[i].d[4];
+  }
+}
+static void tl_quad1(const prob_t* P, int t, const double* x, const double* u, double* qv,
+                     double* r, double* Q, double* Pm, double* R) {
+  (void)P; (void)t;
+  memset(Q, 0, sizeof(double) * 16);
+  memset(Pm, 0, sizeof(double) * 4);
+  qv[0] = 2 * (TL.tgt0 - x[0]) * -1.0;
+  qv[1] = 2 * (TL.tgt1 - x[1]) * -1.0;
+  qv[2] = qv[3] = 0.0;
+  Q[0] = Q[5] = 2.0;
+  r[0] = 2 * u[0];
+  R[0] = 2.0;
+}
+static void tl_dyn1(const prob_t* P, const double* x, const double* u, double* xn) {
+  (void)P;
+  const double u2[2] = {u[0], 0.0};
+  tl_rk4(x, u2, xn);
+}
+static double tl_cost1(const prob_t* P, const double* x, const double* u) {
+  (void)P;
+  const double e0 = TL.tgt0 - x[0], e1 = TL.tgt1 - x[1];
+  return (e0 * e0 + e1 * e1) * 1.0 + (u[0] * u[0]) * 1.0;
+}
+static prob_t tl_problem(int T, int nu) {
   tl_init();
   prob_t P = {4, 2, T, NULL, NULL, NULL, NULL, NULL, NULL, tl_lin, tl_quad, tl_fquad, tl_dyn, tl_cost, tl_fcost};
-  return P;
+  prob_t P1 = {4, 1, T, NULL, NULL, NULL, NULL, NULL, NULL, tl_lin1, tl_quad1, tl_fquad, tl_dyn1, tl_cost1, tl_fcost};
+  return nu == 1 ? P1 : P;
 }
 
 /* -- TILES family: the derivative calls' results supplied per step by the caller --
@@ -828,46 +867,46 @@ int oracle_lq_fit(int Bn, int T, int n, int m, const double* A, const double* Bm
 }
 
 /* -- 2-link arm entry points (same conventions as the LQ ones) -- */
-int oracle_tl_backward(int Bn, int T, const double* x, const double* u, double mu, int sym,
+int oracle_tl_backward(int Bn, int T, int nu, const double* x, const double* u, double mu, int sym,
                        double* d, double* K, int* status, int nthreads) {
   set_threads(nthreads);
-  const prob_t P = tl_problem(T);
+  const prob_t P = tl_problem(T, nu);
   int nans = 0;
 #pragma omp parallel for schedule(static) reduction(+ : nans)
   for (int b = 0; b < Bn; ++b) {
-    const int bad = backward_one(&P, x + (size_t)b * (T + 1) * 4, u + (size_t)b * T * 2, mu, sym,
-                                 d + (size_t)b * T * 2, K + (size_t)b * T * 8);
+    const int bad = backward_one(&P, x + (size_t)b * (T + 1) * 4, u + (size_t)b * T * nu, mu, sym,
+                                 d + (size_t)b * T * nu, K + (size_t)b * T * nu * 4);
     if (status) status[b] = bad ? 4 : 0;
     nans += bad;
   }
   return nans;
 }
 
-int oracle_tl_forward(int Bn, int T, const double* x, const double* u, const double* xtraj,
+int oracle_tl_forward(int Bn, int T, int nu, const double* x, const double* u, const double* xtraj,
                       const double* d, const double* K, const double* prev_cost, double* xnew,
                       double* unew, double* cost, int* trials, int max_trials, double alpha0,
                       double shrink, int nthreads) {
   set_threads(nthreads);
-  const prob_t P = tl_problem(T);
+  const prob_t P = tl_problem(T, nu);
   int fails = 0;
 #pragma omp parallel for schedule(static) reduction(+ : fails)
   for (int b = 0; b < Bn; ++b) {
-    const int tr = forward_one(&P, x + (size_t)b * (T + 1) * 4, u + (size_t)b * T * 2,
-                               xtraj ? xtraj + (size_t)b * (T + 1) * 4 : NULL, d + (size_t)b * T * 2,
-                               K + (size_t)b * T * 8, prev_cost[b], xnew + (size_t)b * (T + 1) * 4,
-                               unew + (size_t)b * T * 2, &cost[b], max_trials, alpha0, shrink);
+    const int tr = forward_one(&P, x + (size_t)b * (T + 1) * 4, u + (size_t)b * T * nu,
+                               xtraj ? xtraj + (size_t)b * (T + 1) * 4 : NULL, d + (size_t)b * T * nu,
+                               K + (size_t)b * T * nu * 4, prev_cost[b], xnew + (size_t)b * (T + 1) * 4,
+                               unew + (size_t)b * T * nu, &cost[b], max_trials, alpha0, shrink);
     if (trials) trials[b] = tr;
     fails += tr < 0;
   }
   return fails;
 }
 
-int oracle_tl_fit(int Bn, int T, const double* x_init, const double* u_init, const double* xtraj,
+int oracle_tl_fit(int Bn, int T, int nu, const double* x_init, const double* u_init, const double* xtraj,
                   int max_iter, double tol, double mu, int sym, int max_trials, double* x_out,
                   double* u_out, double* cost, int* iters, int* status, int nthreads) {
   set_threads(nthreads);
-  const prob_t P = tl_problem(T);
-  const size_t xs = (size_t)(T + 1) * 4, us = (size_t)T * 2;
+  const prob_t P = tl_problem(T, nu);
+  const size_t xs = (size_t)(T + 1) * 4, us = (size_t)T * nu;
 #pragma omp parallel for schedule(dynamic, 4)
   for (int b = 0; b < Bn; ++b)
     fit_one(&P, x_init + b * xs, u_init + b * us, xtraj ? xtraj + b * xs : NULL, max_iter, tol, mu,

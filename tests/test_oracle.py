@@ -222,3 +222,18 @@ def test_c_oracle_twolink_agrees_with_golden():
     xo, uo, co, it, st = cref.tl_fit(g["x"], g["u"], max_iter=40)
     assert np.array_equal(it, g["fit_iters"]) and (st == 1).all()
     assert rel(xo, g["fit_x"]) < 1e-12 and rel(uo, g["fit_u"]) < 1e-12
+
+
+def test_c_oracle_twolink_nu1_agrees_with_golden():
+    """The C restatement's nu = 1 variant (f(x, [u₁, 0])) against the Python oracle's
+    twolink_nu1_t50 fixture (TwoLink.dynamicsf_nu1): backward, forward and fit."""
+    g = _load("twolink_nu1_t50")
+    d, K, st = cref.tl_backward(g["x"], g["u"])
+    assert d.shape[-1] == 1 and K.shape[-2:] == (1, 4)
+    assert (st == 0).all() and rel(d, g["d"]) < 1e-12 and rel(K, g["K"]) < 1e-12
+    xn, un, c, tr = cref.tl_forward(g["x"], g["u"], None, g["d"], g["K"], np.inf)
+    assert (tr == 1).all() and rel(xn, g["fw_x"]) < 1e-13 and rel(un, g["fw_u"]) < 1e-13
+    assert rel(c, g["fw_cost"]) < 1e-14
+    xo, uo, co, it, st = cref.tl_fit(g["x"], g["u"], max_iter=40)
+    assert np.array_equal(it, g["fit_iters"]) and (st == 1).all()
+    assert rel(xo, g["fit_x"]) < 1e-12 and rel(uo, g["fit_u"]) < 1e-12

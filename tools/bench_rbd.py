@@ -1,5 +1,6 @@
 """Secondary benchmark: BASELINE config 5 — the RBD example (RigidBodyDynamics-style
-dynamics of test/urdf/2Dof_arm.urdf, fixed base: nx = 4, nu = 2 or 1), T = 100,
+dynamics of test/urdf/2Dof_arm.urdf, fixed base: nx = 4, nu = 1 as the config states, or
+--nu 2), T = 100,
 batch 2048 random x₀, fp32, linearised on the device by central finite differences
 (BASELINE's wording) or dual numbers (the reference's ForwardDiff). Same step as
 bench.py: one cold-start fit iteration over the batch (linearise + backward +
@@ -67,7 +68,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--batch", type=int, default=2048)
     ap.add_argument("--T", type=int, default=100)
-    ap.add_argument("--nu", type=int, default=2)
+    ap.add_argument("--nu", type=int, default=1, choices=[1, 2],
+                    help="1 = BASELINE config 5 as stated; 2 = both joints actuated")
     ap.add_argument("--dtype", default="f32", choices=["f32", "f64"])
     ap.add_argument("--lin", default="fd,dual")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
