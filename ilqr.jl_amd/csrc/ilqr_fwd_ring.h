@@ -63,6 +63,41 @@ __device__ __forceinline__ double dpp_dot12(double src, const double (&c)[12]) {
   return (a0 + a1) + (a2 + a3);
 }
 
+// dpp_dot16 in two parts with the same four accumulators and the same order per
+// accumulator (a0: k = 0, 4, 8, 12; a1: 1, 5, 9, 13; …), so (a0 + a1) + (a2 + a3) after
+// both parts is dpp_dot16's bits: the first 12 terms from `src` (lanes 0..11 of the
+// row), the last 4 from `src2` (lanes 12..15), issued once src2 exists.
+struct Acc4 {
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+  __device__ __forceinline__ double sum() const { return (a0 + a1) + (a2 + a3); }
+};
+__device__ __forceinline__ void dpp_acc16_head(Acc4& r, double src, const double (&c)[16]) {
+  asm("s_nop 4\n\t"
+      "v_fmac_f64_dpp %[a0], %[s], %[c0] row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[a1], %[s], %[c1] row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[a2], %[s], %[c2] row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[a3], %[s], %[c3] row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[a0], %[s], %[c4] row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[a1], %[s], %[c5] row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[a2], %[s], %[c6] row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[a3], %[s], %[c7] row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[a0], %[s], %[c8] row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[a1], %[s], %[c9] row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[a2], %[s], %[c10] row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[a3], %[s], %[c11] row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+      : [a0] "+v"(r.a0), [a1] "+v"(r.a1), [a2] "+v"(r.a2), [a3] "+v"(r.a3)
+      : [s] "v"(src), [c0] "v"(c[0]), [c1] "v"(c[1]), [c2] "v"(c[2]), [c3] "v"(c[3]), [c4] "v"(c[4]), [c5] "v"(c[5]), [c6] "v"(c[6]), [c7] "v"(c[7]), [c8] "v"(c[8]), [c9] "v"(c[9]), [c10] "v"(c[10]), [c11] "v"(c[11]));
+}
+__device__ __forceinline__ void dpp_acc16_tail(Acc4& r, double src2, const double (&c)[16]) {
+  asm("s_nop 4\n\t"
+      "v_fmac_f64_dpp %[a0], %[s], %[c12] row_newbcast:12 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[a1], %[s], %[c13] row_newbcast:13 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[a2], %[s], %[c14] row_newbcast:14 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[a3], %[s], %[c15] row_newbcast:15 row_mask:0xf bank_mask:0xf\n\t"
+      : [a0] "+v"(r.a0), [a1] "+v"(r.a1), [a2] "+v"(r.a2), [a3] "+v"(r.a3)
+      : [s] "v"(src2), [c12] "v"(c[12]), [c13] "v"(c[13]), [c14] "v"(c[14]), [c15] "v"(c[15]));
+}
+
 // dpp_dot16 for a block-diagonal row held in 12 registers: lanes 0..11 of each row
 // (banks 0-2) take Σ_k<12 bcast_k(src)·c[k], lanes 12..15 (bank 3) Σ_m<4
 // bcast_{12+m}(src)·c[m] — the same accumulators and order as dpp_dot16 on the
@@ -91,6 +126,98 @@ __device__ __forceinline__ double dpp_dot16_bd(double src, const double (&c)[12]
   return (a0 + a1) + (a2 + a3);
 }
 
+#ifndef ILQR_FW_ABLATE
+#define ILQR_FW_ABLATE 0
+#endif
+
+// Row broadcasts through LDS instead of DPP: every lane writes its value to the wave's
+// scratch, each lane reads its row's 16 values back (ds_read_b128, a broadcast per
+// row) and accumulates with plain FMAs — the same four accumulators, operands and
+// order as the DPP helpers above, so the same bits. A v_fmac_f64_dpp row_newbcast
+// issues in ≈18 cycles at one wave per SIMD against ≈8 for a plain f64 FMA
+// (tools/fw_alt.sh ablations, profiles/r02/fw_ablate.log).
+#ifndef ILQR_FW_LDS_BCAST
+#define ILQR_FW_LDS_BCAST 0
+#endif
+struct RowBcast {
+  double* buf;  // this wave's 64-double scratch vector
+  int l, row;   // lane, first lane of its 16-lane row
+  __device__ __forceinline__ void put(double v) const {
+    buf[l] = v;
+    wave_lds_fence();
+  }
+  template <int K0, int N>
+  __device__ __forceinline__ void get(double (&w)[N]) const {
+    static_assert(K0 % 2 == 0 && N % 2 == 0, "16-byte reads");
+    const double2* p = reinterpret_cast<const double2*>(buf + row + K0);
+#pragma unroll
+    for (int k = 0; k < N / 2; ++k) {
+      const double2 v = p[k];
+      w[2 * k] = v.x;
+      w[2 * k + 1] = v.y;
+    }
+  }
+};
+// Σ_k<12 bcast_k(src)·c[k] (dpp_dot12's bits)
+__device__ __forceinline__ double lds_dot12(const RowBcast& rb, double src, const double (&c)[12]) {
+  rb.put(src);
+  double w[12];
+  rb.get<0>(w);
+  Acc4 r;
+#pragma unroll
+  for (int k = 0; k < 12; k += 4) {
+    r.a0 = fma(w[k], c[k], r.a0);
+    r.a1 = fma(w[k + 1], c[k + 1], r.a1);
+    r.a2 = fma(w[k + 2], c[k + 2], r.a2);
+    r.a3 = fma(w[k + 3], c[k + 3], r.a3);
+  }
+  return r.sum();
+}
+// dpp_acc16_head / dpp_acc16_tail
+__device__ __forceinline__ void lds_acc16_head(const RowBcast& rb, Acc4& r, double src, const double (&c)[16]) {
+  rb.put(src);
+  double w[12];
+  rb.get<0>(w);
+#pragma unroll
+  for (int k = 0; k < 12; k += 4) {
+    r.a0 = fma(w[k], c[k], r.a0);
+    r.a1 = fma(w[k + 1], c[k + 1], r.a1);
+    r.a2 = fma(w[k + 2], c[k + 2], r.a2);
+    r.a3 = fma(w[k + 3], c[k + 3], r.a3);
+  }
+}
+__device__ __forceinline__ void lds_acc16_tail(const RowBcast& rb, Acc4& r, double src2, const double (&c)[16]) {
+  rb.put(src2);
+  double w[4];
+  rb.get<12>(w);
+  r.a0 = fma(w[0], c[12], r.a0);
+  r.a1 = fma(w[1], c[13], r.a1);
+  r.a2 = fma(w[2], c[14], r.a2);
+  r.a3 = fma(w[3], c[15], r.a3);
+}
+// dpp_dot16_bd: lanes 0..11 of a row Σ_k<12 bcast_k·c[k], lanes 12..15 Σ_m<4 bcast_{12+m}·c[m]
+__device__ __forceinline__ double lds_dot16_bd(const RowBcast& rb, double src, const double (&c)[12], bool x_lane) {
+  rb.put(src);
+  double w[16];
+  rb.get<0>(w);
+  Acc4 r;
+  if (x_lane) {
+#pragma unroll
+    for (int k = 0; k < 12; k += 4) {
+      r.a0 = fma(w[k], c[k], r.a0);
+      r.a1 = fma(w[k + 1], c[k + 1], r.a1);
+      r.a2 = fma(w[k + 2], c[k + 2], r.a2);
+      r.a3 = fma(w[k + 3], c[k + 3], r.a3);
+    }
+  } else {
+    r.a0 = fma(w[12], c[0], r.a0);
+    r.a1 = fma(w[13], c[1], r.a1);
+    r.a2 = fma(w[14], c[2], r.a2);
+    r.a3 = fma(w[15], c[3], r.a3);
+  }
+  return r.sum();
+}
+
 struct FwdOut {
   double cost;
   int trials;
@@ -109,9 +236,15 @@ struct FwdOut {
 // storing). One slot (3 KB): K rows [0,192), x [192,240), u [240,256), x_traj
 // [256,304), δu [304,320) doubles; group g at K + 48g, x/x_traj + 12g, u/δu + 4g.
 constexpr int RING_SLOT = 384;  // doubles per ring slot
-constexpr int RING_LAREA = 4 * 160 + 16;  // Q, R of the wave's 4 trajectories (+ read overhang)
+// Q, R of the wave's 4 trajectories (+ read overhang), then the row-broadcast scratch
+// (four 64-double vectors, ILQR_FW_LDS_BCAST)
+constexpr int RING_LAREA = 4 * 160 + 16 + 4 * 64;
 
-template <int NX, int NU, int R, int PF>
+// LR_REGS: the wave's Q/R cost rows live in registers for the whole pass (kernels with
+// one wave per SIMD and VGPRs to spare); otherwise they are re-read from LDS every step
+// (the pipelined kernel's 128-VGPR budget). An LDS read in the step is a wait the
+// in-order wave cannot issue past.
+template <int NX, int NU, int R, int PF, bool LR_REGS = true>
 __device__ FwdOut lq_forward_wave_ring(const LQParams& P, int b0, int B, int T, bool active,
                                        const double* __restrict__ x, const double* __restrict__ u,
                                        const double* __restrict__ xtraj, const double* __restrict__ dg,
@@ -150,6 +283,19 @@ __device__ FwdOut lq_forward_wave_ring(const LQParams& P, int b0, int B, int T, 
     Ls[i] = e < NX * NX ? P.Q[bt * NX * NX + e] : P.R[bt * NU * NU + (e < NX * NX ? 0 : e - NX * NX)];
   }
   const int la = is_x ? g * 160 + jx * NX : g * 160 + NX * NX + iu * NU;  // this lane's L row
+  double Lk[NX];  // the cost row in registers (LR_REGS)
+  if constexpr (LR_REGS) {
+    const double2* lr = reinterpret_cast<const double2*>(Ls + la);
+#pragma unroll
+    for (int k = 0; k < NX / 2; ++k) {
+      const double2 q = lr[k];
+      Lk[2 * k] = q.x;
+      Lk[2 * k + 1] = q.y;
+    }
+  }
+  double* const bc = Ls + 4 * 160 + 16;  // row-broadcast scratch: x̄, δx, ū, v
+  [[maybe_unused]] const RowBcast rbx{bc, l, g * 16}, rbd{bc + 64, l, g * 16}, rbu{bc + 128, l, g * 16},
+      rbv{bc + 192, l, g * 16};
   wave_lds_fence();
 
   // producer: lane l moves 16 B per instruction; three instructions fill one slot
@@ -223,54 +369,89 @@ __device__ FwdOut lq_forward_wave_ring(const LQParams& P, int b0, int B, int T, 
   for (int trial = 1; trial <= ls.max_trials && __any(open); ++trial) {
 #pragma unroll
     for (int t = 0; t < PF; ++t) produce(t);
-    double xb = 0.0;  // x̄₁ = x₁ (:65), taken from slot 0 once it has landed
     double cost = 0.0, du2 = 0.0;
     const uint32_t ox = open ? oxs : OOR, ou = open ? ous : OOR;  // closed groups store nothing
-    auto step = [&](int t) {
+    // slot t's operands are read into registers at the end of step t − 1 (software
+    // pipelining of the LDS reads: their latency is off the step's dependent chain)
+    struct Slot {
+      double a, bq, Kr[NX];
+    };
+    auto read_slot = [&](int t, Slot& o) {
       const double* sl = ring + (t % R) * RING_SLOT;
-      const double a = sl[va], bq = sl[vb];
-      if (t == 0) xb = is_x ? a : 0.0;
-      double Kr[NX];
+      o.a = sl[va];
+      o.bq = sl[vb];
       const double2* kr = reinterpret_cast<const double2*>(sl + ka);
 #pragma unroll
       for (int k = 0; k < NX / 2; ++k) {
         const double2 v = kr[k];
-        Kr[2 * k] = v.x;
-        Kr[2 * k + 1] = v.y;
+        o.Kr[2 * k] = v.x;
+        o.Kr[2 * k + 1] = v.y;
       }
+    };
+    Slot cur;
+    wait_slot(std::integral_constant<int, N_PRO>{});
+    read_slot(0, cur);
+    double xb = is_x ? cur.a : 0.0;  // x̄₁ = x₁ (:65)
+    auto step = [&](int t, auto next_wait) {
+      // x̄ₖ₊₁ = A x̄ₖ + B ūₖ: the A part (broadcasts from the x lanes) does not need ūₖ
+      Acc4 xa;
+#if ILQR_FW_LDS_BCAST
+      lds_acc16_head(rbx, xa, xb, Fr);
+#else
+      dpp_acc16_head(xa, xb, Fr);
+#endif
       // δx = x̄ₖ − xₖ (:72); ūₖ = uₖ + α δuₖ + Kₖ δx (:73)
-      const double dx = is_x ? xb - a : 0.0;
-      const double kdx = dpp_dot12(dx, Kr);
-      const double ub = fma(alpha, bq, a) + kdx;
+      const double dx = is_x ? xb - cur.a : 0.0;
+#if ILQR_FW_LDS_BCAST
+      const double kdx = lds_dot12(rbd, dx, cur.Kr);
+#else
+      const double kdx = dpp_dot12(dx, cur.Kr);
+#endif
+      const double ub = fma(alpha, cur.bq, cur.a) + kdx;
       const double z = is_x ? xb : ub;
-      const double v = is_x ? fma(-xtw, bq, xb) : ub;
-      const double e = is_x ? 0.0 : ub - a;
+      const double v = is_x ? fma(-xtw, cur.bq, xb) : ub;
+      const double e = is_x ? 0.0 : ub - cur.a;
+#if ILQR_FW_LDS_BCAST
+      lds_acc16_tail(rbu, xa, ub, Fr);  // the B part: broadcasts from the u lanes
+#else
+      dpp_acc16_tail(xa, ub, Fr);  // the B part: broadcasts from the u lanes
+#endif
       produce(t + PF);  // slot (t+PF)%R was last read at step t+PF−R < t
       double Lr[NX];  // Q row (x lanes); R row in slots 0..NU-1 (u lanes), rest unused
-      const double2* lr = reinterpret_cast<const double2*>(Ls + la);
+      if constexpr (LR_REGS) {
 #pragma unroll
-      for (int k = 0; k < NX / 2; ++k) {
-        const double2 q = lr[k];
-        Lr[2 * k] = q.x;
-        Lr[2 * k + 1] = q.y;
+        for (int k = 0; k < NX; ++k) Lr[k] = Lk[k];
+      } else {
+        const double2* lr = reinterpret_cast<const double2*>(Ls + la);
+#pragma unroll
+        for (int k = 0; k < NX / 2; ++k) {
+          const double2 q = lr[k];
+          Lr[2 * k] = q.x;
+          Lr[2 * k + 1] = q.y;
+        }
       }
+#if ILQR_FW_ABLATE & 1  // probe only (tools/fw_alt.sh): no cost row
+      const double lv = Lr[0];
+#elif ILQR_FW_LDS_BCAST
+      const double lv = lds_dot16_bd(rbv, v, Lr, is_x);
+#else
       const double lv = dpp_dot16_bd(v, Lr);
-      const double xn = dpp_dot16(z, Fr);
+#endif
       cost = fma(v, lv, cost);
+#if ILQR_FW_ABLATE & 2  // probe only: no result stores
+      if (t < 0)
+#endif
       __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, z), rXN, ox, (uint32_t)t * NX * 8, 0);
       __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, z), rUN, ou, (uint32_t)t * NU * 8, 0);
       du2 = fma(e, e, du2);
-      xb = xn;
+      xb = xa.sum();
+      // slot t + 1 (past the horizon: a clamped step's slot, read and never used)
+      wait_slot(next_wait);
+      read_slot(t + 1, cur);
     };
     const int tp = T < PF ? T : PF;
-    for (int t = 0; t < tp; ++t) {
-      wait_slot(std::integral_constant<int, N_PRO>{});
-      step(t);
-    }
-    for (int t = tp; t < T; ++t) {
-      wait_slot(std::integral_constant<int, N_SS>{});
-      step(t);
-    }
+    for (int t = 0; t < tp - 1; ++t) step(t, std::integral_constant<int, N_PRO>{});
+    for (int t = tp - 1; t < T; ++t) step(t, std::integral_constant<int, N_SS>{});
     __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, xb), rXN, ox, (uint32_t)T * NX * 8, 0);
     // Qf row (x lanes; u lanes read row 0 and zero it): one base address, 6 × 16 B
     const double2* qrow = reinterpret_cast<const double2*>(Qfb + jx * NX);
@@ -296,9 +477,9 @@ __device__ FwdOut lq_forward_wave_ring(const LQParams& P, int b0, int B, int T, 
       }
     }
     alpha *= ls.shrink;  // (:82); unused by closed groups
-    // the loads of the clamped steps past the horizon are still in flight: drain them
-    // before the next trial's prologue reuses the slots
-    __builtin_amdgcn_s_waitcnt((0) | (7 << 4) | (15 << 8));
+    // the loads of the clamped steps past the horizon (and the read of slot T) are
+    // still in flight: drain them before the next trial's prologue reuses the slots
+    __builtin_amdgcn_s_waitcnt((0) | (7 << 4) | (0 << 8));
     asm volatile("" ::: "memory");
   }
   if (du2_out) *du2_out = du2_acc;
@@ -311,7 +492,7 @@ constexpr int PIPE_R = 8, PIPE_PF = 7;
 // forward pass + convergence test (:163-175) of the wave's trajectories b0 .. b0+3;
 // called by the whole wave, groups whose status is not OK (or past B) sit out
 // (`active`: this lane's group runs; the caller read it from status)
-template <int NX, int NU>
+template <int NX, int NU, bool LR_REGS = true>
 __device__ __forceinline__ void iter_forward_wave_active(const LQParams& P, int b0, int B, int T,
                                                          const IterArgs& a, const LSParams& ls,
                                                          double* ring, bool active) {
@@ -319,7 +500,7 @@ __device__ __forceinline__ void iter_forward_wave_active(const LQParams& P, int 
   const int b = b0 + ((threadIdx.x & 63) >> 4);
   double du2 = 0.0;
   const double pc = (a.prev_cost && active) ? a.prev_cost[b] : INFINITY;
-  const FwdOut r = lq_forward_wave_ring<NX, NU, PIPE_R, PIPE_PF>(P, b0, B, T, active, a.x, a.u,
+  const FwdOut r = lq_forward_wave_ring<NX, NU, PIPE_R, PIPE_PF, LR_REGS>(P, b0, B, T, active, a.x, a.u,
                                                                  a.xtraj, a.d, a.K, pc, a.xnew,
                                                                  a.unew, &du2, ls, ring);
   if (j == 0 && active) {
@@ -339,13 +520,13 @@ __device__ __forceinline__ void iter_forward_wave_active(const LQParams& P, int 
   }
 }
 
-template <int NX, int NU>
+template <int NX, int NU, bool LR_REGS = true>
 __device__ __forceinline__ void iter_forward_wave(const LQParams& P, int b0, int B, int T,
                                                   const IterArgs& a, const LSParams& ls,
                                                   double* ring) {
   const int b = b0 + ((threadIdx.x & 63) >> 4);
   const bool active = b < B && a.status[b < B ? b : b0] == ILQR_TRAJ_OK;
-  iter_forward_wave_active<NX, NU>(P, b0, B, T, a, ls, ring, active);
+  iter_forward_wave_active<NX, NU, LR_REGS>(P, b0, B, T, a, ls, ring, active);
 }
 
 }  // namespace

@@ -796,7 +796,10 @@ __host__ __device__ __forceinline__ bool pipe_role_a(int g) { return (((g >> 8) 
 // Four waves per workgroup, each with its own ring (116 KB of LDS: one workgroup per
 // CU, one wave per SIMD); one-wave workgroups let the dispatcher pack two waves onto a
 // SIMD (the fused kernel).
-constexpr int FW_WAVES = 4;
+#ifndef ILQR_FW_WAVES
+#define ILQR_FW_WAVES 4
+#endif
+constexpr int FW_WAVES = ILQR_FW_WAVES;
 template <int NX, int NU>
 __global__ __launch_bounds__(64 * FW_WAVES) void lq_forward_ring_kernel(
     LQParams P, int B, int T, const double* __restrict__ x, const double* __restrict__ u,
@@ -848,7 +851,7 @@ __global__ __launch_bounds__(256, 4) void lq_iter_pipe_kernel(LQParams P, int B,
   const int b0 = blockIdx.x * WAVES_PER_WG;
   const bool role_a = pipe_role_a(blockIdx.x);
   auto forward4 = [&](const IterArgs& a) {  // wave 0: the workgroup's 4 trajectories
-    if (w == 0) iter_forward_wave<NX, NU>(P, b0, B, T, a, ls, lds);  // ring: the whole WG's scratch
+    if (w == 0) iter_forward_wave<NX, NU, false>(P, b0, B, T, a, ls, lds);  // ring: the whole WG's scratch
   };
   auto backward = [&](const IterArgs& a) {
     const int b = b0 + w;

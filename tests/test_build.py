@@ -22,3 +22,16 @@ def test_chain_macro_alternates_compile(tmp_path):
            os.path.join(CSRC, "ilqr_chain.hip"), "-o", str(tmp_path / "chain_alt.o")]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-2000:]
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC) and shutil.which("hipcc") is None, reason="no hipcc")
+def test_forward_ring_alternates_compile(tmp_path):
+    """ilqr_lq.hip's ring forward with the LDS row broadcasts (ILQR_FW_LDS_BCAST=1,
+    bit-identical, measured slower), one-wave workgroups (ILQR_FW_WAVES=1) and the
+    ablation bits (ILQR_FW_ABLATE=3) that tools/fw_alt.sh builds."""
+    hipcc = HIPCC if os.path.exists(HIPCC) else shutil.which("hipcc")
+    cmd = [hipcc, "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-DILQR_FW_LDS_BCAST=1",
+           "-DILQR_FW_WAVES=1", "-DILQR_FW_ABLATE=3", "-c", os.path.join(CSRC, "ilqr_lq.hip"),
+           "-o", str(tmp_path / "lq_alt.o")]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]

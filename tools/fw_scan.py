@@ -7,6 +7,10 @@ from ilqr_amd import _lib
 from ilqr_amd.problems import quadrotor_batch
 from ilqr_amd.solver import Solver, _ptr
 
+if len(sys.argv) > 1:  # an alternate build of libilqr_hip.so (tools/fw_alt.sh)
+    _lib._lib = _lib.load(sys.argv[1])
+    print("library:", sys.argv[1])
+
 for B in (256, 1024, 2048, 4096, 8192):
     lq, x0, u0 = quadrotor_batch(B, T=100, seed0=0)
     s = Solver(12, 4, 100, B); s.set_problem(lq); s._bind_stream()
