@@ -26,6 +26,7 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <string>
@@ -593,13 +594,77 @@ __device__ __forceinline__ void chain_xdot_cv(const ChainK<V, NJ>& P, const V (&
   }
 }
 
-// RK4 (RBD_helper_functions.jl:70-78)
-template <int NJ, int NU, bool SPLIT = false, bool ROT = true, class S, class V>
-__device__ __forceinline__ void chain_rk4(const ChainK<V, NJ>& P, const S (&x)[2 * NJ],
+// ---------------------------------------------------------------------------
+// Closed-form dynamics of a 2-joint fixed-base chain (round 2, the default for the
+// iteration kernels of 2-joint chains). M(q) depends on q₂ only (turning the whole
+// chain about joint 1's fixed axis preserves its kinetic energy) and is a trigonometric
+// polynomial of degree 2 in q₂ (body 2's rotation enters its kinetic energy
+// quadratically, every factor affine in cos q₂, sin q₂); the gravity torque ∂V/∂q is
+// bilinear in (1, cos q₁, sin q₁) ⊗ (1, cos q₂, sin q₂) (each COM's height is). The
+// coefficients are sampled from the recursive Newton-Euler above, in fp64, when the
+// handle is created — M at 5 angles, g on a 3×3 grid: the discrete Fourier transform is
+// exact for these degrees — and the result is checked against the recursion at random
+// states before it is used (chain_trig_check_kernel). The velocity term is the
+// Christoffel form of M′ = dM/dq₂: c = q̇₂·M′q̇ − ½ e₂ q̇ᵀM′q̇. The same f(x, u) as the
+// recursion (RBD_helper_functions.jl:61-66), ≈60 operations and two sin/cos instead
+// of the three Newton-Euler passes; the rounding differs.
+// ---------------------------------------------------------------------------
+template <class V>
+struct ChainTrig {
+  V Mc[3][5];     // M₀₀, M₀₁, M₁₁: a₀ + a₁ cos q₂ + b₁ sin q₂ + a₂ cos 2q₂ + b₂ sin 2q₂
+  V dMc[3][4];    // dM/dq₂ on (cos q₂, sin q₂, cos 2q₂, sin 2q₂): (b₁, −a₁, 2b₂, −2a₂)
+  V Gc[2][3][3];  // g_i = Σ_ab Gc[i][a][b] φ_a(q₁) φ_b(q₂), φ = (1, cos, sin)
+  V dt;
+  V tgt[2], qw[2], rw[2], qfw[2];  // joint-space cost (as ChainK)
+};
+
+template <int NU, class S, class V>
+__device__ __forceinline__ void chain_xdot_trig(const ChainTrig<V>& P, const S (&x)[4], const S (&u)[NU],
+                                                S (&xd)[4]) {
+  S s1, c1, s2, c2;
+  scs(x[0], s1, c1);
+  scs(x[1], s2, c2);
+  const S C2 = c2 * c2 - s2 * s2, S2 = V(2) * (s2 * c2);
+  S m[3], dm[3];
+#pragma unroll
+  for (int e = 0; e < 3; ++e) {
+    m[e] = P.Mc[e][0] + (((P.Mc[e][1] * c2 + P.Mc[e][2] * s2) + P.Mc[e][3] * C2) + P.Mc[e][4] * S2);
+    dm[e] = ((P.dMc[e][0] * c2 + P.dMc[e][1] * s2) + P.dMc[e][2] * C2) + P.dMc[e][3] * S2;
+  }
+  S g[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    S h[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) h[a] = P.Gc[i][a][0] + (P.Gc[i][a][1] * c2 + P.Gc[i][a][2] * s2);
+    g[i] = h[0] + (h[1] * c1 + h[2] * s1);
+  }
+  const S w0 = x[2], w1 = x[3];
+  const S p0 = dm[0] * w0 + dm[1] * w1, p1 = dm[1] * w0 + dm[2] * w1;  // M′q̇
+  const S qq = w0 * p0 + w1 * p1;                                      // q̇ᵀM′q̇
+  S r0 = u[0] - (w1 * p0 + g[0]);
+  S r1 = (w1 * p1 - V(0.5) * qq) + g[1];
+  if constexpr (NU > 1) r1 = u[NU - 1] - r1;
+  else r1 = -r1;
+  const S det = m[0] * m[2] - m[1] * m[1];
+  const S id = crecip(det);
+  xd[0] = w0;
+  xd[1] = w1;
+  xd[2] = (m[2] * r0 - m[1] * r1) * id;
+  xd[3] = (m[0] * r1 - m[1] * r0) * id;
+}
+
+// RK4 (RBD_helper_functions.jl:70-78) on either parameter set: ChainK (the recursion;
+// SPLIT = the 16-lane component-parallel form) or ChainTrig (closed form, 2 joints)
+template <int NJ, int NU, bool SPLIT = false, bool ROT = true, class S, class PK>
+__device__ __forceinline__ void chain_rk4(const PK& P, const S (&x)[2 * NJ],
                                           const S (&u)[NU], S (&out)[2 * NJ]) {
   constexpr int NX = 2 * NJ;
-  auto xdot = [](const ChainK<V, NJ>& Pc, const S (&xx)[2 * NJ], const S (&uu)[NU], S (&o)[2 * NJ]) {
-    if constexpr (SPLIT)
+  using V = decltype(P.dt);
+  auto xdot = [](const PK& Pc, const S (&xx)[2 * NJ], const S (&uu)[NU], S (&o)[2 * NJ]) {
+    if constexpr (std::is_same_v<PK, ChainTrig<V>>)
+      chain_xdot_trig<NU>(Pc, xx, uu, o);
+    else if constexpr (SPLIT)
       chain_xdot_cv<NJ, NU>(Pc, xx, uu, o);
     else
       chain_xdot<NJ, NU, ROT>(Pc, xx, uu, o);
@@ -635,8 +700,8 @@ __device__ __forceinline__ void chain_rk4(const ChainK<V, NJ>& P, const S (&x)[2
 // ---------------------------------------------------------------------------
 // f(x, u) for n points (a rollout primitive and the dynamics parity test)
 // ---------------------------------------------------------------------------
-template <class V, int NJ, int NU>
-__global__ __launch_bounds__(256) void chain_dynamics_kernel(ChainK<V, NJ> P, int n,
+template <class V, int NJ, int NU, class PK = ChainK<V, NJ>>
+__global__ __launch_bounds__(256) void chain_dynamics_kernel(PK P, int n,
                                                              const V* __restrict__ x,
                                                              const V* __restrict__ u,
                                                              V* __restrict__ xo) {
@@ -683,8 +748,8 @@ struct Rec {
 #ifndef ILQR_CHAIN_FD_WAVES
 #define ILQR_CHAIN_FD_WAVES 3
 #endif
-template <class V, int NJ, int NU, int LIN>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LIN == ILQR_LINEARIZE_CENTRAL_FD ? ILQR_CHAIN_FD_WAVES : ILQR_CHAIN_DUAL_WAVES))) void chain_linearize_kernel(ChainK<V, NJ> P, int B, int T,
+template <class V, int NJ, int NU, int LIN, class PK = ChainK<V, NJ>>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LIN == ILQR_LINEARIZE_CENTRAL_FD ? ILQR_CHAIN_FD_WAVES : ILQR_CHAIN_DUAL_WAVES))) void chain_linearize_kernel(PK P, int B, int T,
                                                               const V* __restrict__ x,
                                                               const V* __restrict__ u,
                                                               const int32_t* __restrict__ status,
@@ -976,8 +1041,8 @@ struct ChainFwdOut {
   int accepted;
 };
 
-template <class V, int NJ, int NU, bool SPLIT = false>
-__device__ ChainFwdOut<V> chain_forward_lane(const ChainK<V, NJ>& P, int b, int T,
+template <class V, int NJ, int NU, bool SPLIT = false, class PK = ChainK<V, NJ>>
+__device__ ChainFwdOut<V> chain_forward_lane(const PK& P, int b, int T,
                                              const V* __restrict__ x, const V* __restrict__ u,
                                              const V* __restrict__ xtraj, const V* __restrict__ dg,
                                              const V* __restrict__ Kg, V prev_cost,
@@ -1353,6 +1418,106 @@ __global__ __launch_bounds__(CH_WG) void chain_iter_forward_kernel(ChainK<V, NJ>
   }
 }
 
+// ---------------------------------------------------------------------------
+// Closed-form dynamics (ChainTrig): coefficient samples, the check against the
+// recursion, and the forward kernels (one lane per trajectory: the closed form has
+// nothing for a 16-lane group to split)
+// ---------------------------------------------------------------------------
+constexpr int CH_TRIG_SAMPLES = 15 + 18;  // M at 5 angles (3 entries), g on 3×3 (2 entries)
+__global__ void chain_trig_sample_kernel(ChainK<double, 2> P, double* __restrict__ out) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const double two_pi = 6.283185307179586476925286766559;
+  const double zero[2] = {0.0, 0.0}, e0[2] = {1.0, 0.0}, e1[2] = {0.0, 1.0};
+  for (int k = 0; k < 5; ++k) {  // M(q₂ = 2πk/5); M does not depend on q₁
+    double c[2] = {1.0, 0.0}, sn[2] = {0.0, 0.0};
+    sincos(two_pi * k / 5.0, &sn[1], &c[1]);
+    double m0[2], m1[2];
+    rnea<false, false, true>(P, c, sn, zero, e0, m0);
+    rnea<false, false, true>(P, c, sn, zero, e1, m1);
+    out[3 * k] = m0[0];
+    out[3 * k + 1] = 0.5 * (m1[0] + m0[1]);  // symmetric up to rounding
+    out[3 * k + 2] = m1[1];
+  }
+  for (int a = 0; a < 3; ++a)
+    for (int b = 0; b < 3; ++b) {  // g(q₁ = 2πa/3, q₂ = 2πb/3)
+      double c[2], sn[2], g[2];
+      sincos(two_pi * a / 3.0, &sn[0], &c[0]);
+      sincos(two_pi * b / 3.0, &sn[1], &c[1]);
+      rnea<false, true, true>(P, c, sn, zero, zero, g);
+      out[15 + 2 * (3 * a + b)] = g[0];
+      out[15 + 2 * (3 * a + b) + 1] = g[1];
+    }
+}
+
+// |f_trig − f_rnea| / max(1, |f_rnea|) at n pseudo-random states and torques (fp64)
+__global__ void chain_trig_check_kernel(ChainK<double, 2> P, ChainTrig<double> Q, int n,
+                                        double* __restrict__ err) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t h = 0x9E3779B9u * (uint32_t)(i + 1);
+  auto rnd = [&](double lo, double hi) {
+    h ^= h << 13; h ^= h >> 17; h ^= h << 5;
+    return lo + (hi - lo) * ((h & 0xFFFFFF) / 16777216.0);
+  };
+  double x[4] = {rnd(-4, 4), rnd(-4, 4), rnd(-6, 6), rnd(-6, 6)}, u[2] = {rnd(-3, 3), rnd(-3, 3)};
+  double a[4], b[4];
+  chain_xdot<2, 2, true>(P, x, u, a);
+  chain_xdot_trig<2>(Q, x, u, b);
+  double e = 0.0, m = 1.0;
+  for (int k = 0; k < 4; ++k) {
+    e = fmax(e, fabs(a[k] - b[k]));
+    m = fmax(m, fabs(a[k]));
+  }
+  err[i] = e / m;
+}
+
+template <class V, int NU>
+__global__ __launch_bounds__(CH_WG) void chain_forward_trig_kernel(
+    ChainTrig<V> P, int B, int T, const V* __restrict__ x, const V* __restrict__ u,
+    const V* __restrict__ xtraj, const V* __restrict__ d, const V* __restrict__ K,
+    const V* __restrict__ prev_cost, V* __restrict__ xnew, V* __restrict__ unew,
+    V* __restrict__ new_cost, int32_t* __restrict__ trials, int32_t* __restrict__ status,
+    LSParams ls) {
+  constexpr int NX = 4;
+  const int b = blockIdx.x * CH_WG + threadIdx.x;
+  if (b >= B) return;
+  const V pc = prev_cost ? prev_cost[b] : V(INFINITY);
+  const ChainFwdOut<V> r = chain_forward_lane<V, 2, NU, false, ChainTrig<V>>(P, b, T, x, u, xtraj, d, K, pc,
+                                                                              xnew, unew, nullptr, ls);
+  if (!r.accepted) {  // exhausted (the reference would loop forever): return the inputs
+    for (int i = 0; i < (T + 1) * NX; ++i) xnew[(size_t)b * (T + 1) * NX + i] = x[(size_t)b * (T + 1) * NX + i];
+    for (int i = 0; i < T * NU; ++i) unew[(size_t)b * T * NU + i] = u[(size_t)b * T * NU + i];
+  }
+  new_cost[b] = r.cost;
+  if (trials) trials[b] = r.trials;
+  if (status) status[b] = r.accepted ? ILQR_TRAJ_OK
+                                     : (r.cost != r.cost ? ILQR_TRAJ_NAN : ILQR_TRAJ_LS_EXHAUSTED);
+}
+
+template <class V, int NU>
+__global__ __launch_bounds__(CH_WG) void chain_iter_forward_trig_kernel(ChainTrig<V> P, int B, int T,
+                                                                        ChainIter<V> a, LSParams ls) {
+  const int b = blockIdx.x * CH_WG + threadIdx.x;
+  if (b >= B || a.status[b] != ILQR_TRAJ_OK) return;
+  V du2 = V(0);
+  const V pc = a.prev_cost ? a.prev_cost[b] : V(INFINITY);
+  const ChainFwdOut<V> r = chain_forward_lane<V, 2, NU, false, ChainTrig<V>>(P, b, T, a.x, a.u, a.xtraj, a.d,
+                                                                              a.K, pc, a.xnew, a.unew, &du2, ls);
+  if (a.trials) a.trials[b] = r.trials;
+  if (a.du2) a.du2[b] = du2;
+  if (a.iters) a.iters[b] = a.iter;
+  if (!r.accepted) {
+    a.status[b] = (r.cost != r.cost) ? ILQR_TRAJ_NAN : ILQR_TRAJ_LS_EXHAUSTED;
+    if (a.res_parity) a.res_parity[b] = a.parity;
+  } else {
+    a.new_cost[b] = r.cost;           // prev_cost = new_cost (:168)
+    if ((double)du2 <= ls.tol) {      // (:171) break BEFORE the update
+      a.status[b] = ILQR_TRAJ_CONVERGED;
+      if (a.res_parity) a.res_parity[b] = a.parity;
+    }
+  }
+}
+
 // x_out[b] = (res_parity[b] ? x1 : x0)[b]; still-running trajectories → MAX_ITER
 template <class V>
 __global__ __launch_bounds__(256) void chain_gather_kernel(int B, int nxe, int nue, const V* x0,
@@ -1405,6 +1570,13 @@ struct ilqr_chain_handle {
   int32_t* status = nullptr;
   int32_t* res_parity = nullptr;
   int32_t* iters = nullptr;
+  // closed-form dynamics of 2-joint chains (ilqr_chain_set_dynamics): available once
+  // sampled and checked against the recursion at creation, used unless RNEA is asked for
+  bool trig_ok = false;
+  int32_t dyn_mode = ILQR_CHAIN_DYN_AUTO;
+  double trig_err = 0.0;  // the check's max relative error
+  ilqr::ChainTrig<double> trig{};
+  bool use_trig() const { return trig_ok && dyn_mode != ILQR_CHAIN_DYN_RNEA; }
 };
 
 namespace {
@@ -1465,6 +1637,96 @@ ilqr::ChainK<V, NJ> chain_consts(const ilqr_chain& c) {
   return P;
 }
 
+// ChainTrig<V> from the fp64 coefficients and the chain's cost
+template <class V>
+ilqr::ChainTrig<V> trig_consts(const ilqr_chain_handle* h) {
+  ilqr::ChainTrig<V> Q{};
+  const ilqr::ChainTrig<double>& D = h->trig;
+  for (int e = 0; e < 3; ++e) {
+    for (int k = 0; k < 5; ++k) Q.Mc[e][k] = (V)D.Mc[e][k];
+    for (int k = 0; k < 4; ++k) Q.dMc[e][k] = (V)D.dMc[e][k];
+  }
+  for (int i = 0; i < 2; ++i)
+    for (int a = 0; a < 3; ++a)
+      for (int b = 0; b < 3; ++b) Q.Gc[i][a][b] = (V)D.Gc[i][a][b];
+  const ilqr_chain& c = h->chain;
+  for (int i = 0; i < 2; ++i) {
+    Q.tgt[i] = (V)c.target[i];
+    Q.qw[i] = (V)c.q_weight[i];
+    Q.rw[i] = (V)c.r_weight[i];
+    Q.qfw[i] = (V)c.qf_weight[i];
+  }
+  Q.dt = (V)c.dt;
+  return Q;
+}
+
+// Samples M and g with the recursion (fp64, on the device), takes their discrete
+// Fourier coefficients (exact for M's degree 2 in q₂ and g's degree 1 in each angle:
+// 5 and 3 points), and checks f against the recursion at 256 random states. Leaves
+// trig_ok false when the check fails (the recursion is then used).
+hipError_t chain_trig_build(ilqr_chain_handle* h) {
+  h->trig_ok = false;
+  if (h->nj != 2) return hipSuccess;
+  const auto P = chain_consts<double, 2>(h->chain);
+  constexpr int NCHK = 256;
+  double* dev = nullptr;
+  hipError_t e = hipMalloc(&dev, sizeof(double) * (ilqr::CH_TRIG_SAMPLES + NCHK));
+  if (e != hipSuccess) return e;
+  double smp[ilqr::CH_TRIG_SAMPLES], err[NCHK];
+  ilqr::chain_trig_sample_kernel<<<1, 64>>>(P, dev);
+  e = hipGetLastError();
+  if (e == hipSuccess) e = hipMemcpy(smp, dev, sizeof(smp), hipMemcpyDeviceToHost);
+  if (e == hipSuccess) {
+    ilqr::ChainTrig<double>& D = h->trig;
+    const double two_pi = 6.283185307179586476925286766559;
+    for (int en = 0; en < 3; ++en) {  // a₀ + a₁ cos + b₁ sin + a₂ cos 2 + b₂ sin 2 from 5 samples
+      double a0 = 0, a1 = 0, b1 = 0, a2 = 0, b2 = 0;
+      for (int k = 0; k < 5; ++k) {
+        const double f = smp[3 * k + en], t = two_pi * k / 5.0;
+        a0 += f;
+        a1 += f * std::cos(t);
+        b1 += f * std::sin(t);
+        a2 += f * std::cos(2 * t);
+        b2 += f * std::sin(2 * t);
+      }
+      D.Mc[en][0] = a0 / 5;
+      D.Mc[en][1] = 2 * a1 / 5;
+      D.Mc[en][2] = 2 * b1 / 5;
+      D.Mc[en][3] = 2 * a2 / 5;
+      D.Mc[en][4] = 2 * b2 / 5;
+      D.dMc[en][0] = D.Mc[en][2];       // d/dq (b₁ sin) = b₁ cos
+      D.dMc[en][1] = -D.Mc[en][1];      // d/dq (a₁ cos) = −a₁ sin
+      D.dMc[en][2] = 2 * D.Mc[en][4];   // d/dq (b₂ sin 2q) = 2b₂ cos 2q
+      D.dMc[en][3] = -2 * D.Mc[en][3];  // d/dq (a₂ cos 2q) = −2a₂ sin 2q
+    }
+    for (int i = 0; i < 2; ++i) {  // 2-D transform on the 3×3 grid: φ = (1, cos, sin)
+      for (int a = 0; a < 3; ++a)
+        for (int b = 0; b < 3; ++b) {
+          double acc = 0.0;
+          for (int ka = 0; ka < 3; ++ka)
+            for (int kb = 0; kb < 3; ++kb) {
+              const double ta = two_pi * ka / 3.0, tb = two_pi * kb / 3.0;
+              const double fa = a == 0 ? 1.0 / 3 : (a == 1 ? 2.0 / 3 * std::cos(ta) : 2.0 / 3 * std::sin(ta));
+              const double fb = b == 0 ? 1.0 / 3 : (b == 1 ? 2.0 / 3 * std::cos(tb) : 2.0 / 3 * std::sin(tb));
+              acc += smp[15 + 2 * (3 * ka + kb) + i] * fa * fb;
+            }
+          D.Gc[i][a][b] = acc;
+        }
+    }
+    D.dt = h->chain.dt;
+    ilqr::chain_trig_check_kernel<<<NCHK / 64, 64>>>(P, D, NCHK, dev + ilqr::CH_TRIG_SAMPLES);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipMemcpy(err, dev + ilqr::CH_TRIG_SAMPLES, sizeof(err), hipMemcpyDeviceToHost);
+  (void)hipFree(dev);
+  if (e != hipSuccess) return e;
+  double m = 0.0;
+  for (double v : err) m = std::isnan(v) ? INFINITY : std::max(m, v);
+  h->trig_err = m;
+  h->trig_ok = m < 1e-9;
+  return hipSuccess;
+}
+
 ilqr::LSParams chain_ls(const ilqr_options* o) {
   ilqr_options def;
   ilqr_default_options(&def);
@@ -1493,6 +1755,19 @@ struct ChainOps {
     const auto P = chain_consts<V, NJ>(h->chain);
     const size_t lanes = (size_t)h->batch * h->T * (NX + NU);
     const dim3 grid((unsigned)((lanes + 255) / 256));
+    if constexpr (NJ == 2) {
+      if (h->use_trig()) {
+        const auto Q = trig_consts<V>(h);
+        using TK = ilqr::ChainTrig<V>;
+        if (h->lin == ILQR_LINEARIZE_DUAL)
+          ilqr::chain_linearize_kernel<V, NJ, NU, ILQR_LINEARIZE_DUAL, TK>
+              <<<grid, 256, 0, h->stream>>>(Q, h->batch, h->T, x, u, st, (V*)h->J);
+        else
+          ilqr::chain_linearize_kernel<V, NJ, NU, ILQR_LINEARIZE_CENTRAL_FD, TK>
+              <<<grid, 256, 0, h->stream>>>(Q, h->batch, h->T, x, u, st, (V*)h->J);
+        return hipGetLastError();
+      }
+    }
     if (h->lin == ILQR_LINEARIZE_DUAL)
       ilqr::chain_linearize_kernel<V, NJ, NU, ILQR_LINEARIZE_DUAL>
           <<<grid, 256, 0, h->stream>>>(P, h->batch, h->T, x, u, st, (V*)h->J);
@@ -1525,6 +1800,14 @@ struct ChainOps {
   static hipError_t forward(ilqr_chain_handle* h, const V* x, const V* u, const V* xt, const V* d,
                             const V* K, const V* pc, V* xn, V* un, V* nc, int32_t* tr,
                             int32_t* st, const ilqr::LSParams& ls) {
+    if constexpr (NJ == 2) {
+      if (h->use_trig()) {
+        ilqr::chain_forward_trig_kernel<V, NU><<<(h->batch + ilqr::CH_WG - 1) / ilqr::CH_WG, ilqr::CH_WG, 0,
+                                                 h->stream>>>(trig_consts<V>(h), h->batch, h->T, x, u, xt, d,
+                                                              K, pc, xn, un, nc, tr, st, ls);
+        return hipGetLastError();
+      }
+    }
     const auto P = chain_consts<V, NJ>(h->chain);
     ilqr::chain_forward_kernel<V, NJ, NU><<<(h->batch * ilqr::CH_FW_LANES + ilqr::CH_WG - 1) / ilqr::CH_WG, ilqr::CH_WG,
                                             0, h->stream>>>(P, h->batch, h->T, x, u, xt, d, K, pc,
@@ -1544,12 +1827,26 @@ struct ChainOps {
           <<<g, ilqr::CH_WG, 0, h->stream>>>(P, h->batch, h->T, a, (const V*)h->J, (V)ls.mu);
     }
     if ((e = hipGetLastError()) != hipSuccess) return e;
+    if constexpr (NJ == 2) {
+      if (h->use_trig()) {
+        ilqr::chain_iter_forward_trig_kernel<V, NU><<<(h->batch + ilqr::CH_WG - 1) / ilqr::CH_WG, ilqr::CH_WG,
+                                                      0, h->stream>>>(trig_consts<V>(h), h->batch, h->T, a, ls);
+        return hipGetLastError();
+      }
+    }
     const int gf = (h->batch * ilqr::CH_FW_LANES + ilqr::CH_WG - 1) / ilqr::CH_WG;
     ilqr::chain_iter_forward_kernel<V, NJ, NU><<<gf, ilqr::CH_WG, 0, h->stream>>>(P, h->batch, h->T,
                                                                                  a, ls);
     return hipGetLastError();
   }
   static hipError_t dynamics(ilqr_chain_handle* h, const V* x, const V* u, V* xo, int n) {
+    if constexpr (NJ == 2) {
+      if (h->use_trig()) {
+        ilqr::chain_dynamics_kernel<V, NJ, NU, ilqr::ChainTrig<V>>
+            <<<(n + 255) / 256, 256, 0, h->stream>>>(trig_consts<V>(h), n, x, u, xo);
+        return hipGetLastError();
+      }
+    }
     const auto P = chain_consts<V, NJ>(h->chain);
     ilqr::chain_dynamics_kernel<V, NJ, NU><<<(n + 255) / 256, 256, 0, h->stream>>>(P, n, x, u, xo);
     return hipGetLastError();
@@ -1696,9 +1993,29 @@ ilqr_status ilqr_chain_create(ilqr_chain_handle** out, int device, const ilqr_ch
     ilqr_chain_destroy(h);
     return chain_hip_fail(e, "ilqr_chain_create: hipMalloc");
   }
+  if (iter_supported(h->nj, h->nu) && (e = chain_trig_build(h)) != hipSuccess) {
+    ilqr_chain_destroy(h);
+    return chain_hip_fail(e, "ilqr_chain_create: closed-form dynamics");
+  }
   *out = h;
   return ILQR_OK;
 }
+
+ilqr_status ilqr_chain_set_dynamics(ilqr_chain_handle* h, int32_t mode) {
+  if (!h) return ILQR_ERR_BAD_ARG;
+  if (mode != ILQR_CHAIN_DYN_AUTO && mode != ILQR_CHAIN_DYN_RNEA && mode != ILQR_CHAIN_DYN_CLOSED_FORM)
+    return ILQR_ERR_BAD_ARG;
+  if (mode == ILQR_CHAIN_DYN_CLOSED_FORM && !h->trig_ok) return ILQR_ERR_UNSUPPORTED;
+  h->dyn_mode = mode;
+  return ILQR_OK;
+}
+
+int32_t ilqr_chain_get_dynamics(const ilqr_chain_handle* h) {
+  if (!h) return -1;
+  return h->use_trig() ? ILQR_CHAIN_DYN_CLOSED_FORM : ILQR_CHAIN_DYN_RNEA;
+}
+
+double ilqr_chain_closed_form_error(const ilqr_chain_handle* h) { return h ? h->trig_err : -1.0; }
 
 ilqr_status ilqr_chain_destroy(ilqr_chain_handle* h) {
   if (!h) return ILQR_OK;

@@ -45,6 +45,9 @@ F64 = 0
 F32 = 1
 LINEARIZE_DUAL = 0
 LINEARIZE_CENTRAL_FD = 1
+CHAIN_DYN_AUTO = 0          # ilqr_chain_dynamics_mode
+CHAIN_DYN_RNEA = 1
+CHAIN_DYN_CLOSED_FORM = 2
 CHAIN_MAX_JOINTS = 8
 
 
@@ -111,6 +114,9 @@ SIGNATURES = {
                                     C.c_int, C.c_int32, C.c_int32]),
     "ilqr_chain_destroy": (C.c_int, [P]),
     "ilqr_chain_set_stream": (C.c_int, [P, P]),
+    "ilqr_chain_set_dynamics": (C.c_int, [P, C.c_int32]),
+    "ilqr_chain_get_dynamics": (C.c_int32, [P]),
+    "ilqr_chain_closed_form_error": (C.c_double, [P]),
     "ilqr_chain_sync": (C.c_int, [P]),
     "ilqr_chain_dynamics": (C.c_int, [P, P, P, P, C.c_int]),
     "ilqr_chain_linearize": (C.c_int, [P, P, P, P, P]),

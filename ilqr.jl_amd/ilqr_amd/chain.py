@@ -159,6 +159,24 @@ class ChainSolver:
         self.h = h
         self.iterates = bool(self.lib.ilqr_chain_supported(self.nj, self.nu))
 
+    def set_dynamics(self, mode: str):
+        """The iteration kernels' dynamics evaluator (2-joint chains): "auto" (the closed
+        form when its creation check passed), "rnea" (the recursive Newton-Euler, the
+        restatement of RigidBodyDynamics.jl's calls) or "closed_form"."""
+        m = {"auto": _lib.CHAIN_DYN_AUTO, "rnea": _lib.CHAIN_DYN_RNEA,
+             "closed_form": _lib.CHAIN_DYN_CLOSED_FORM}[mode]
+        _lib.check(self.lib.ilqr_chain_set_dynamics(self.h, m), "ilqr_chain_set_dynamics")
+
+    @property
+    def dynamics_mode(self) -> str:
+        return {_lib.CHAIN_DYN_RNEA: "rnea", _lib.CHAIN_DYN_CLOSED_FORM: "closed_form"}[
+            int(self.lib.ilqr_chain_get_dynamics(self.h))]
+
+    @property
+    def closed_form_error(self) -> float:
+        """Max relative deviation of the closed form from the recursion at creation."""
+        return float(self.lib.ilqr_chain_closed_form_error(self.h))
+
     def close(self):
         if getattr(self, "h", None):
             self.lib.ilqr_chain_destroy(self.h)

@@ -263,6 +263,24 @@ ilqr_status ilqr_chain_create(ilqr_chain_handle** out, int device, const ilqr_ch
                               int batch, int32_t dtype, int32_t linearization);
 ilqr_status ilqr_chain_destroy(ilqr_chain_handle* h);
 ilqr_status ilqr_chain_set_stream(ilqr_chain_handle* h, void* hip_stream);
+/* Dynamics evaluator of the iteration kernels (2-joint chains). The recursive
+ * Newton-Euler restates RigidBodyDynamics.jl's dynamics_bias / mass_matrix
+ * (RBD_helper_functions.jl:61-66); the closed form is the same f(x, u) as a
+ * trigonometric polynomial whose coefficients the handle samples from the recursion
+ * in fp64 at creation and checks against it at random states (rounding differs).
+ * AUTO (a new handle) = the closed form when its check passed, else the recursion;
+ * CLOSED_FORM when unavailable → ILQR_ERR_UNSUPPORTED. */
+typedef enum {
+  ILQR_CHAIN_DYN_AUTO = 0,
+  ILQR_CHAIN_DYN_RNEA = 1,
+  ILQR_CHAIN_DYN_CLOSED_FORM = 2
+} ilqr_chain_dynamics_mode;
+ilqr_status ilqr_chain_set_dynamics(ilqr_chain_handle* h, int32_t mode);
+/* the evaluator in effect (RNEA or CLOSED_FORM), −1 for a NULL handle */
+int32_t ilqr_chain_get_dynamics(const ilqr_chain_handle* h);
+/* the closed form's max relative deviation from the recursion at the creation check
+ * (fp64; ≥ 1e-9 means the closed form is not used) */
+double ilqr_chain_closed_form_error(const ilqr_chain_handle* h);
 ilqr_status ilqr_chain_sync(ilqr_chain_handle* h);
 /* dynamicsf for n independent (x, u) pairs: x (n, nx), u (n, nu) → x_next (n, nx) */
 ilqr_status ilqr_chain_dynamics(ilqr_chain_handle* h, const void* x, const void* u, void* x_next,

@@ -25,11 +25,31 @@ import pytest
 import torch
 
 from ilqr_amd import _lib
-from ilqr_amd.chain import (ChainSolver, chain_closures, load_robot, rbd_2dof_problem,
+from ilqr_amd.chain import (ChainSolver as _ChainSolver, chain_closures, load_robot, rbd_2dof_problem,
                             ChainProblem)
 
 pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+# Every test of this module runs with both dynamics evaluators of 2-joint chains: the
+# closed form (the default, ilqr_chain_set_dynamics AUTO) and the recursive
+# Newton-Euler that restates RigidBodyDynamics.jl's calls, against the same oracle and
+# tolerances.
+_MODE = ["closed_form"]
+
+
+@pytest.fixture(params=["closed_form", "rnea"], autouse=True)
+def dyn_mode(request):
+    _MODE[0] = request.param
+    yield request.param
+
+
+def ChainSolver(pr, *a, **k):  # noqa: N802 — shadows the import for this module's handles
+    s = _ChainSolver(pr, *a, **k)
+    if pr.n_joints == 2:
+        s.set_dynamics(_MODE[0])
+        assert s.dynamics_mode == _MODE[0]
+    return s
 
 
 def rel(a, b):
@@ -359,3 +379,27 @@ def test_config5_batch2048_iteration_vs_c_oracle(gpu):
     assert (tro == 1).all()
     assert rel(un.cpu().numpy()[idx], uo) < t["fw"] and rel(xn.cpu().numpy()[idx], xo) < t["fw"]
     assert rel(pc.cpu().numpy()[idx], co) < t["fw"]
+
+
+@pytest.mark.parametrize("name", ["rbd", "coupled"])
+@pytest.mark.parametrize("nu", [1, 2])
+def test_closed_form_equals_recursion(gpu, name, nu):
+    """The closed form (trigonometric M(q₂), bilinear g, Christoffel velocity term, its
+    coefficients sampled from the recursion at creation) against the recursion at
+    random states, fp64, one RK4 step and the creation check's own figure."""
+    from ilqr_amd.chain import coupled_2dof_problem
+    pr = rbd_2dof_problem(nu) if name == "rbd" else coupled_2dof_problem(nu)
+    n = 512
+    s = _ChainSolver(pr, 1, n, dtype=torch.float64)
+    assert s.closed_form_error < 1e-12, s.closed_form_error
+    rng = np.random.default_rng(11)
+    x = torch.from_numpy(np.concatenate([rng.uniform(-4, 4, (n, 2)), rng.uniform(-6, 6, (n, 2))], 1)).cuda()
+    u = torch.from_numpy(rng.uniform(-3, 3, (n, nu))).cuda()
+    s.set_dynamics("closed_form")
+    a = s.dynamics(x, u)
+    s.set_dynamics("rnea")
+    b = s.dynamics(x, u)
+    assert rel(a, b) < 1e-13
+    assert s.dynamics_mode == "rnea"
+    s.set_dynamics("auto")
+    assert s.dynamics_mode == "closed_form"

@@ -74,6 +74,8 @@ def main():
     ap.add_argument("--lin", default="fd,dual")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--dynamics", default="auto", choices=["auto", "rnea", "closed_form"],
+                    help="the chain handle's dynamics evaluator (ilqr_chain_set_dynamics)")
     args = ap.parse_args()
     B, T = args.batch, args.T
     dt = torch.float32 if args.dtype == "f32" else torch.float64
@@ -83,6 +85,7 @@ def main():
     base = None
     for lin in args.lin.split(","):
         s = ChainSolver(pr, T, B, dtype=dt, linearization=lin)
+        s.set_dynamics(args.dynamics)
         u = torch.zeros((B, T, pr.nu), dtype=dt, device=dev)
         x = s.rollout(torch.from_numpy(x0).to(dev, dt), u)
         xn, un = torch.empty_like(x), torch.empty_like(u)
@@ -130,7 +133,9 @@ def main():
         peak = PEAK_TFLOPS[args.dtype]
         kern = {"linearize": (lin_ms, lin_fl), "riccati": (max(bw_ms - lin_ms, 1e-6), ric_fl),
                 "forward": (fw_ms, fw_fl)}
-        roof = {"bound": "forward latency/issue (16 lanes per trajectory), linearisation VALU issue",
+        roof = {"bound": ("forward latency/issue (one lane per trajectory, closed-form dynamics)"
+                          if s.dynamics_mode == "closed_form" else
+                          "forward latency/issue (16 lanes per trajectory)") + ", linearisation VALU issue",
                 "unit": "TFLOP/s", "peak": peak, "peak_dtype": args.dtype,
                 "flops_note": f"RK4 of the restated RBD formulas = {f_rk4} flop (tools/flops.py)"}
         for k, (ms_k, fl) in kern.items():
@@ -143,7 +148,8 @@ def main():
                "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms,
                "higher_is_better": True, "dtype": args.dtype, "data": "synthetic x0 ~ U(-1,1)",
                "config": {"workload": "BASELINE config 5 (RBD_2_link_example, fixed base)",
-                          "batch": B, "T": T, "linearization": lin},
+                          "batch": B, "T": T, "linearization": lin, "dynamics": s.dynamics_mode,
+                          "closed_form_check": s.closed_form_error},
                "traj_iters_per_s": B * 1000.0 / ms,
                "mean_line_search_trials": float(trials.double().mean().item()), "all_ok": ok,
                "roofline": roof,
