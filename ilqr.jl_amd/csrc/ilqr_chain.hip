@@ -37,6 +37,7 @@
 #include "ilqr_internal.h"
 #include "ilqr_device.h"
 #include "ilqr_math.h"
+#include "ilqr_fwd_group.h"
 
 namespace ilqr {
 namespace {
@@ -618,12 +619,11 @@ struct ChainTrig {
   V tgt[2], qw[2], rw[2], qfw[2];  // joint-space cost (as ChainK)
 };
 
+// q̈ from sin/cos of both joint angles, q̇ = (w0, w1) and u
 template <int NU, class S, class V>
-__device__ __forceinline__ void chain_xdot_trig(const ChainTrig<V>& P, const S (&x)[4], const S (&u)[NU],
-                                                S (&xd)[4]) {
-  S s1, c1, s2, c2;
-  scs(x[0], s1, c1);
-  scs(x[1], s2, c2);
+__device__ __forceinline__ void chain_qdd_trig(const ChainTrig<V>& P, const S& s1, const S& c1, const S& s2,
+                                               const S& c2, const S& w0, const S& w1, const S (&u)[NU],
+                                               S& a0, S& a1) {
   const S C2 = c2 * c2 - s2 * s2, S2 = V(2) * (s2 * c2);
   S m[3], dm[3];
 #pragma unroll
@@ -639,7 +639,6 @@ __device__ __forceinline__ void chain_xdot_trig(const ChainTrig<V>& P, const S (
     for (int a = 0; a < 3; ++a) h[a] = P.Gc[i][a][0] + (P.Gc[i][a][1] * c2 + P.Gc[i][a][2] * s2);
     g[i] = h[0] + (h[1] * c1 + h[2] * s1);
   }
-  const S w0 = x[2], w1 = x[3];
   const S p0 = dm[0] * w0 + dm[1] * w1, p1 = dm[1] * w0 + dm[2] * w1;  // M′q̇
   const S qq = w0 * p0 + w1 * p1;                                      // q̇ᵀM′q̇
   S r0 = u[0] - (w1 * p0 + g[0]);
@@ -648,11 +647,95 @@ __device__ __forceinline__ void chain_xdot_trig(const ChainTrig<V>& P, const S (
   else r1 = -r1;
   const S det = m[0] * m[2] - m[1] * m[1];
   const S id = crecip(det);
-  xd[0] = w0;
-  xd[1] = w1;
-  xd[2] = (m[2] * r0 - m[1] * r1) * id;
-  xd[3] = (m[0] * r1 - m[1] * r0) * id;
+  a0 = (m[2] * r0 - m[1] * r1) * id;
+  a1 = (m[0] * r1 - m[1] * r0) * id;
 }
+
+template <int NU, class S, class V>
+__device__ __forceinline__ void chain_xdot_trig(const ChainTrig<V>& P, const S (&x)[4], const S (&u)[NU],
+                                                S (&xd)[4]) {
+  S s1, c1, s2, c2;
+  scs(x[0], s1, c1);
+  scs(x[1], s2, c2);
+  xd[0] = x[2];
+  xd[1] = x[3];
+  chain_qdd_trig<NU>(P, s1, c1, s2, c2, x[2], x[3], u, xd[2], xd[3]);
+}
+
+// One RK4 step of the closed form without a branch (the forward's fast path, as the
+// 2-link's rk4_roll): stage 1 reduces both angles, stages 2-4 shift their sin/cos by
+// h = ½k₁, ½k₂, k₃ (|h| ≤ 1/8); `bad` flags |h| > 1/8 or an angle past the reduction's
+// range, and the caller redoes the rollout on chain_rk4 (NaN: not flagged, NaN either way)
+template <int NU, class V>
+__device__ __forceinline__ void chain_trig_rk4_fast(const ChainTrig<V>& P, const V (&x)[4], const V (&u)[NU],
+                                                    V (&out)[4], bool& bad) {
+  const V h = V(0.5);
+  V s10, c10, s20, c20, s1, c1, s2, c2, a0, a1;
+  sincos_red_t(x[0], s10, c10);
+  sincos_red_t(x[1], s20, c20);
+  chain_qdd_trig<NU>(P, s10, c10, s20, c20, x[2], x[3], u, a0, a1);
+  const V k10 = P.dt * x[2], k11 = P.dt * x[3], k12 = P.dt * a0, k13 = P.dt * a1;
+  V y2 = x[2] + h * k12, y3 = x[3] + h * k13;
+  sincos_shift_t(s10, c10, h * k10, s1, c1);
+  sincos_shift_t(s20, c20, h * k11, s2, c2);
+  chain_qdd_trig<NU>(P, s1, c1, s2, c2, y2, y3, u, a0, a1);
+  const V k20 = P.dt * y2, k21 = P.dt * y3, k22 = P.dt * a0, k23 = P.dt * a1;
+  y2 = x[2] + h * k22;
+  y3 = x[3] + h * k23;
+  sincos_shift_t(s10, c10, h * k20, s1, c1);
+  sincos_shift_t(s20, c20, h * k21, s2, c2);
+  chain_qdd_trig<NU>(P, s1, c1, s2, c2, y2, y3, u, a0, a1);
+  const V k30 = P.dt * y2, k31 = P.dt * y3, k32 = P.dt * a0, k33 = P.dt * a1;
+  y2 = x[2] + k32;
+  y3 = x[3] + k33;
+  sincos_shift_t(s10, c10, k30, s1, c1);
+  sincos_shift_t(s20, c20, k31, s2, c2);
+  chain_qdd_trig<NU>(P, s1, c1, s2, c2, y2, y3, u, a0, a1);
+  const V k40 = P.dt * y2, k41 = P.dt * y3, k42 = P.dt * a0, k43 = P.dt * a1;
+  const V sixth = V(1) / V(6);
+  out[0] = x[0] + sixth * (((k10 + V(2) * k20) + V(2) * k30) + k40);
+  out[1] = x[1] + sixth * (((k11 + V(2) * k21) + V(2) * k31) + k41);
+  out[2] = x[2] + sixth * (((k12 + V(2) * k22) + V(2) * k32) + k42);
+  out[3] = x[3] + sixth * (((k13 + V(2) * k23) + V(2) * k33) + k43);
+  const V hm = fmax(fmax(fmax(fabs(k10), fabs(k11)), fmax(fabs(k20), fabs(k21))),
+                    V(2) * fmax(fabs(k30), fabs(k31)));
+  bad |= ((int)(hm > V(0.25)) | (int)(fabs(x[0]) > ReducedRange<V>::v) | (int)(fabs(x[1]) > ReducedRange<V>::v)) != 0;
+}
+
+// the chain's closed form as a model of the shared forward group (ilqr_fwd_group.h)
+template <class V_, int NU_>
+struct ChainTrigModel {
+  using V = V_;
+  static constexpr int NU = NU_;
+  static constexpr bool HAS_FAST = true;
+  ChainTrig<V> P;
+  __device__ __forceinline__ void rk4_fast(const V (&x)[4], const V (&u)[NU], V (&o)[4], bool& bad) const {
+    chain_trig_rk4_fast<NU>(P, x, u, o, bad);
+  }
+  __device__ __forceinline__ void rk4_robust(const V (&x)[4], const V (&u)[NU], V (&o)[4]) const;
+  // ℓ(x̄ₖ − x_trajₖ, ūₖ) on the joints (forward_pass.jl:187-190; RBD_helper_functions.jl:85-99)
+  __device__ __forceinline__ V stage_cost(const V (&xb)[4], const V (&xt)[4], V xtw, const V (&ub)[NU]) const {
+    V lk = V(0);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const V e = P.tgt[i] - fma(-xtw, xt[i], xb[i]);
+      lk = fma(P.qw[i] * e, e, lk);
+    }
+#pragma unroll
+    for (int a = 0; a < NU; ++a) lk = fma(P.rw[a] * ub[a], ub[a], lk);
+    return lk;
+  }
+  // final_cost(x̄_N) on the raw state (:192; RBD_helper_functions.jl:105-116)
+  __device__ __forceinline__ V final_cost(const V (&xb)[4]) const {
+    V lf = V(0);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const V e = P.tgt[i] - xb[i];
+      lf = fma(P.qfw[i] * e, e, lf);
+    }
+    return lf;
+  }
+};
 
 // RK4 (RBD_helper_functions.jl:70-78) on either parameter set: ChainK (the recursion;
 // SPLIT = the 16-lane component-parallel form) or ChainTrig (closed form, 2 joints)
@@ -695,6 +778,12 @@ __device__ __forceinline__ void chain_rk4(const PK& P, const S (&x)[2 * NJ],
     k4[i] = P.dt * k4[i];
     out[i] = x[i] + (V(1) / V(6)) * (((k1[i] + V(2) * k2[i]) + V(2) * k3[i]) + k4[i]);
   }
+}
+
+template <class V_, int NU_>
+__device__ __forceinline__ void ChainTrigModel<V_, NU_>::rk4_robust(const V (&x)[4], const V (&u)[NU],
+                                                                   V (&o)[4]) const {
+  chain_rk4<2, NU>(P, x, u, o);
 }
 
 // ---------------------------------------------------------------------------
@@ -1471,19 +1560,21 @@ __global__ void chain_trig_check_kernel(ChainK<double, 2> P, ChainTrig<double> Q
   err[i] = e / m;
 }
 
-template <class V, int NU>
-__global__ __launch_bounds__(CH_WG) void chain_forward_trig_kernel(
+// L line-search candidates per trajectory (ilqr_fwd_group.h), W waves per workgroup
+template <class V, int NU, int L, int W>
+__global__ __launch_bounds__(64 * W) void chain_forward_trig_kernel(
     ChainTrig<V> P, int B, int T, const V* __restrict__ x, const V* __restrict__ u,
     const V* __restrict__ xtraj, const V* __restrict__ d, const V* __restrict__ K,
     const V* __restrict__ prev_cost, V* __restrict__ xnew, V* __restrict__ unew,
     V* __restrict__ new_cost, int32_t* __restrict__ trials, int32_t* __restrict__ status,
     LSParams ls) {
   constexpr int NX = 4;
-  const int b = blockIdx.x * CH_WG + threadIdx.x;
+  const int b = (blockIdx.x * 64 * W + threadIdx.x) / L;
   if (b >= B) return;
   const V pc = prev_cost ? prev_cost[b] : V(INFINITY);
-  const ChainFwdOut<V> r = chain_forward_lane<V, 2, NU, false, ChainTrig<V>>(P, b, T, x, u, xtraj, d, K, pc,
-                                                                              xnew, unew, nullptr, ls);
+  const ChainTrigModel<V, NU> m{P};
+  const FgOut<V> r = fwd_group<ChainTrigModel<V, NU>, L>(m, b, B, T, x, u, xtraj, d, K, pc, xnew, unew, ls);
+  if (!r.owner) return;
   if (!r.accepted) {  // exhausted (the reference would loop forever): return the inputs
     for (int i = 0; i < (T + 1) * NX; ++i) xnew[(size_t)b * (T + 1) * NX + i] = x[(size_t)b * (T + 1) * NX + i];
     for (int i = 0; i < T * NU; ++i) unew[(size_t)b * T * NU + i] = u[(size_t)b * T * NU + i];
@@ -1494,24 +1585,25 @@ __global__ __launch_bounds__(CH_WG) void chain_forward_trig_kernel(
                                      : (r.cost != r.cost ? ILQR_TRAJ_NAN : ILQR_TRAJ_LS_EXHAUSTED);
 }
 
-template <class V, int NU>
-__global__ __launch_bounds__(CH_WG) void chain_iter_forward_trig_kernel(ChainTrig<V> P, int B, int T,
-                                                                        ChainIter<V> a, LSParams ls) {
-  const int b = blockIdx.x * CH_WG + threadIdx.x;
+template <class V, int NU, int L, int W>
+__global__ __launch_bounds__(64 * W) void chain_iter_forward_trig_kernel(ChainTrig<V> P, int B, int T,
+                                                                         ChainIter<V> a, LSParams ls) {
+  const int b = (blockIdx.x * 64 * W + threadIdx.x) / L;
   if (b >= B || a.status[b] != ILQR_TRAJ_OK) return;
-  V du2 = V(0);
   const V pc = a.prev_cost ? a.prev_cost[b] : V(INFINITY);
-  const ChainFwdOut<V> r = chain_forward_lane<V, 2, NU, false, ChainTrig<V>>(P, b, T, a.x, a.u, a.xtraj, a.d,
-                                                                              a.K, pc, a.xnew, a.unew, &du2, ls);
+  const ChainTrigModel<V, NU> m{P};
+  const FgOut<V> r = fwd_group<ChainTrigModel<V, NU>, L>(m, b, B, T, a.x, a.u, a.xtraj, a.d, a.K, pc, a.xnew,
+                                                          a.unew, ls);
+  if (!r.owner) return;
   if (a.trials) a.trials[b] = r.trials;
-  if (a.du2) a.du2[b] = du2;
+  if (a.du2) a.du2[b] = r.du2;
   if (a.iters) a.iters[b] = a.iter;
   if (!r.accepted) {
     a.status[b] = (r.cost != r.cost) ? ILQR_TRAJ_NAN : ILQR_TRAJ_LS_EXHAUSTED;
     if (a.res_parity) a.res_parity[b] = a.parity;
   } else {
-    a.new_cost[b] = r.cost;           // prev_cost = new_cost (:168)
-    if ((double)du2 <= ls.tol) {      // (:171) break BEFORE the update
+    a.new_cost[b] = r.cost;             // prev_cost = new_cost (:168)
+    if ((double)r.du2 <= ls.tol) {      // (:171) break BEFORE the update
       a.status[b] = ILQR_TRAJ_CONVERGED;
       if (a.res_parity) a.res_parity[b] = a.parity;
     }
@@ -1802,9 +1894,15 @@ struct ChainOps {
                             int32_t* st, const ilqr::LSParams& ls) {
     if constexpr (NJ == 2) {
       if (h->use_trig()) {
-        ilqr::chain_forward_trig_kernel<V, NU><<<(h->batch + ilqr::CH_WG - 1) / ilqr::CH_WG, ilqr::CH_WG, 0,
-                                                 h->stream>>>(trig_consts<V>(h), h->batch, h->T, x, u, xt, d,
-                                                              K, pc, xn, un, nc, tr, st, ls);
+        if (!ilqr::fg_fits<V>(h->T)) return hipErrorInvalidValue;
+        const auto Q = trig_consts<V>(h);
+        const int B = h->batch;
+        if (ilqr::fg_lanes(B) == 4)
+          ilqr::chain_forward_trig_kernel<V, NU, 4, 1><<<(4 * B + 63) / 64, 64, 0, h->stream>>>(
+              Q, B, h->T, x, u, xt, d, K, pc, xn, un, nc, tr, st, ls);
+        else
+          ilqr::chain_forward_trig_kernel<V, NU, 1, 4><<<(B + 255) / 256, 256, 0, h->stream>>>(
+              Q, B, h->T, x, u, xt, d, K, pc, xn, un, nc, tr, st, ls);
         return hipGetLastError();
       }
     }
@@ -1829,8 +1927,13 @@ struct ChainOps {
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if constexpr (NJ == 2) {
       if (h->use_trig()) {
-        ilqr::chain_iter_forward_trig_kernel<V, NU><<<(h->batch + ilqr::CH_WG - 1) / ilqr::CH_WG, ilqr::CH_WG,
-                                                      0, h->stream>>>(trig_consts<V>(h), h->batch, h->T, a, ls);
+        if (!ilqr::fg_fits<V>(h->T)) return hipErrorInvalidValue;
+        const auto Q = trig_consts<V>(h);
+        const int B = h->batch;
+        if (ilqr::fg_lanes(B) == 4)
+          ilqr::chain_iter_forward_trig_kernel<V, NU, 4, 1><<<(4 * B + 63) / 64, 64, 0, h->stream>>>(Q, B, h->T, a, ls);
+        else
+          ilqr::chain_iter_forward_trig_kernel<V, NU, 1, 4><<<(B + 255) / 256, 256, 0, h->stream>>>(Q, B, h->T, a, ls);
         return hipGetLastError();
       }
     }

@@ -59,11 +59,16 @@ __device__ __forceinline__ void fast_sincos(double x, double& s, double& c) {
 __device__ __attribute__((noinline)) void big_sincosf(float x, float* s, float* c) {
   sincosf(x, s, c);
 }
+__device__ __forceinline__ void sincosf_reduced(float x, float& s, float& c);
 __device__ __forceinline__ void fast_sincosf(float x, float& s, float& c) {
   if (__builtin_expect(fabsf(x) > 8192.0f, 0)) {
     big_sincosf(x, &s, &c);
     return;
   }
+  sincosf_reduced(x, s, c);
+}
+// the reduction and polynomials alone: valid for |x| ≤ 8192
+__device__ __forceinline__ void sincosf_reduced(float x, float& s, float& c) {
   const float k = rintf(x * 0.63661977236758134f);  // x · 2/π
   float r = fmaf(-k, 1.5703125f, x);
   r = fmaf(-k, 4.837512969970703125e-4f, r);
@@ -81,6 +86,36 @@ __device__ __forceinline__ void fast_sincosf(float x, float& s, float& c) {
   s = (q & 2) ? -a : a;
   c = ((q + 1) & 2) ? -b : b;
 }
+
+// sin/cos(θ + h) from s0 = sin θ, c0 = cos θ by the angle-addition formulas and Taylor
+// series in h, for |h| ≤ 1/8 (the caller flags larger h): fp64 through h⁹ / h¹⁰,
+// fp32 through h⁵ / h⁴ (truncation below 0.2 ulp of the type in both)
+__device__ __forceinline__ void sincos_shift_t(double s0, double c0, double h, double& s, double& c) {
+  const double z = h * h;
+  double ps = fma(z, 1.0 / 362880.0, -1.0 / 5040.0);
+  ps = fma(z, ps, 1.0 / 120.0);
+  ps = fma(z, ps, -1.0 / 6.0);
+  const double sh = fma(h * z, ps, h);
+  double pc = fma(z, -1.0 / 3628800.0, 1.0 / 40320.0);
+  pc = fma(z, pc, -1.0 / 720.0);
+  pc = fma(z, pc, 1.0 / 24.0);
+  pc = fma(z, pc, -0.5);
+  const double ch = fma(z, pc, 1.0);
+  s = fma(s0, ch, c0 * sh);
+  c = fma(c0, ch, -(s0 * sh));
+}
+__device__ __forceinline__ void sincos_shift_t(float s0, float c0, float h, float& s, float& c) {
+  const float z = h * h;
+  const float sh = fmaf(h * z, fmaf(z, 1.0f / 120.0f, -1.0f / 6.0f), h);
+  const float ch = fmaf(z, fmaf(z, 1.0f / 24.0f, -0.5f), 1.0f);
+  s = fmaf(s0, ch, c0 * sh);
+  c = fmaf(c0, ch, -(s0 * sh));
+}
+__device__ __forceinline__ void sincos_red_t(double x, double& s, double& c) { sincos_reduced(x, s, c); }
+__device__ __forceinline__ void sincos_red_t(float x, float& s, float& c) { sincosf_reduced(x, s, c); }
+template <class V> struct ReducedRange;                       // |x| the reductions cover
+template <> struct ReducedRange<double> { static constexpr double v = 1e5; };
+template <> struct ReducedRange<float> { static constexpr float v = 8192.0f; };
 
 }  // namespace
 }  // namespace ilqr

@@ -40,6 +40,7 @@
 #include "ilqr_internal.h"
 #include "ilqr_device.h"
 #include "ilqr_math.h"
+#include "ilqr_fwd_group.h"
 #include "../../include/ilqr.h"
 
 namespace ilqr {
@@ -51,10 +52,6 @@ constexpr int TL_NX = 4;
 template <int NU> constexpr int tl_nj() { return TL_NX * (TL_NX + NU); }
 template <int NU> constexpr int tl_njr() { return tl_nj<NU>() + 4; }  // 28 (NU = 2), 24 (NU = 1)
 constexpr int TL_NJR_MAX = 28;
-#ifndef ILQR_TL_FW_PF
-#define ILQR_TL_FW_PF 2
-#endif
-constexpr int TL_FW_PF = ILQR_TL_FW_PF;          // forward prefetch depth (steps)
 constexpr int TL_BW4_PF = 4;                     // backward prefetch depth (steps)
 
 // ---------------------------------------------------------------------------
@@ -507,200 +504,39 @@ __device__ __forceinline__ void rk4_roll(const TLRoll& R, const double (&x)[4], 
 }
 
 // ---------------------------------------------------------------------------
-// Forward rollout + line search (src/forward_pass.jl:55-93) with L line-search
-// candidates per trajectory evaluated side by side: lane `sub` of a trajectory's
-// group of L adjacent lanes rolls out trial r·L + sub + 1 in round r, at
-// α = α₀·shrinkʳᴸ⁺ˢᵘᵇ formed by the same repeated multiplication as the reference's
-// `α *= shrink` (:82), and the group accepts the FIRST candidate in trial order whose
-// cost decreased (:77-80) — the sequential search's answer, bit for bit. Lane sub = 0
-// stores its rollout as it goes; an accepted candidate of another lane rolls out once
-// more, storing (same α, same rollout). Trials 1..L cost one pass (L = 1 is the
-// sequential search). With B·L ≤ 65536 the extra lanes sit on otherwise idle SIMDs.
+// The arm as a model of the shared forward group (ilqr_fwd_group.h: four line-search
+// candidates per trajectory, branch-free stores, the fast/robust RK4 pair)
 // ---------------------------------------------------------------------------
-template <bool ROBUST>
-struct TLPath {
-  static constexpr bool value = ROBUST;
-};
-
-struct TLFwdOut {
-  double cost;
-  double du2;
-  int trials;
-  int accepted;
-  bool owner;  // this lane holds the trajectory's result
-};
-
-template <int NU>
-struct TLStepIn {
-  double x[4], xt[4], u[NU], d[NU], K[4 * NU];
-};
-
-template <int NU, int L>
-__device__ TLFwdOut tl_forward_group(const TwoLinkParams& P, int b, int B, int T,
-                                     const double* __restrict__ x, const double* __restrict__ u,
-                                     const double* __restrict__ xtraj,
-                                     const double* __restrict__ dg, const double* __restrict__ Kg,
-                                     double prev_cost, double* __restrict__ xnew,
-                                     double* __restrict__ unew, const LSParams& ls) {
-  const double* xb0 = x + (size_t)b * (T + 1) * TL_NX;
-  const double* ub0 = u + (size_t)b * T * NU;
-  const double* xt0 = (xtraj ? xtraj : x) + (size_t)b * (T + 1) * TL_NX;
-  const double xtw = xtraj ? 1.0 : 0.0;  // x_traj = NULL means zeros (forward_pass.jl:151)
-  const double* d0 = dg + (size_t)b * T * NU;
-  const double* K0 = Kg + (size_t)b * T * NU * TL_NX;
-  const TLRoll R = tl_roll_consts(P);
-  const int lane = threadIdx.x & 63, sub = lane & (L - 1), gbase = lane & ~(L - 1);
-
-  auto load = [&](int t, TLStepIn<NU>& in) {
-    const int tt = t < T ? t : T - 1;
-    const double4 xv = *reinterpret_cast<const double4*>(xb0 + (size_t)tt * TL_NX);
-    const double4 tv = *reinterpret_cast<const double4*>(xt0 + (size_t)tt * TL_NX);
-    in.x[0] = xv.x; in.x[1] = xv.y; in.x[2] = xv.z; in.x[3] = xv.w;
-    in.xt[0] = tv.x; in.xt[1] = tv.y; in.xt[2] = tv.z; in.xt[3] = tv.w;
-#pragma unroll
-    for (int a = 0; a < NU; ++a) {
-      in.u[a] = ub0[(size_t)tt * NU + a];
-      in.d[a] = d0[(size_t)tt * NU + a];
-      const double4 kr = reinterpret_cast<const double4*>(K0 + (size_t)tt * NU * TL_NX)[a];
-      in.K[4 * a] = kr.x; in.K[4 * a + 1] = kr.y; in.K[4 * a + 2] = kr.z; in.K[4 * a + 3] = kr.w;
-    }
-  };
-
-  // the wave's outputs through buffer resources on its first trajectory: a lane that
-  // does not store gets an out-of-range offset (dropped by the bounds check), so the
-  // stores need no branch and a pass's steps stay one basic block for the scheduler
-  const int bw = __builtin_amdgcn_readfirstlane(b);
-  const int nslot = B - bw < 64 / L ? B - bw : 64 / L;
-  const auto rX = buffer_rsrc(xnew + (size_t)bw * (T + 1) * TL_NX, (uint32_t)((size_t)nslot * (T + 1) * TL_NX * 8));
-  const auto rU = buffer_rsrc(unew + (size_t)bw * T * NU, (uint32_t)((size_t)nslot * T * NU * 8));
-  const uint32_t offX = (uint32_t)((size_t)(b - bw) * (T + 1) * TL_NX * 8);
-  const uint32_t offU = (uint32_t)((size_t)(b - bw) * T * NU * 8);
-
-  TLFwdOut out{0.0, 0.0, 0, 0, false};
-  double alpha_r = ls.alpha0;  // α of this round's first candidate
-  double alpha = alpha_r;
-  for (int j = 0; j < sub; ++j) alpha *= ls.shrink;
-  int r = 0;
-  bool store = sub == 0, rerun = false;
-  struct Pass {
-    double cost, du2;
-    bool bad;
-  };
-  // one rollout at α (:64-76): ROBUST = rk4<double> (every argument range), else rk4_roll
-  auto pass = [&](auto robust) -> Pass {
-    constexpr bool ROBUST = decltype(robust)::value;
-    const uint32_t sx = store ? offX : 0x80000000u, su = store ? offU : 0x80000000u;
-    double xb[4];
-    {
-      const double4 xv = *reinterpret_cast<const double4*>(xb0);  // x̄₁ = x₁ (:65)
-      xb[0] = xv.x; xb[1] = xv.y; xb[2] = xv.z; xb[3] = xv.w;
-    }
-    auto put_x = [&](int t) {
-      typedef unsigned u4v_ __attribute__((ext_vector_type(4)));
-      const uint32_t o = sx + (uint32_t)(t * TL_NX * 8);
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v_, make_double2(xb[0], xb[1])), rX, o, 0, 0);
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v_, make_double2(xb[2], xb[3])), rX, o + 16, 0, 0);
-    };
-    Pass p{0.0, 0.0, false};
-    auto step = [&](int t, const TLStepIn<NU>& in) {
-      // δx = x̄ₖ − xₖ (:72); ūₖ = uₖ + α δuₖ + Kₖ δx (:73)
-      double dx[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) dx[i] = xb[i] - in.x[i];
-      double ubar[NU];
-#pragma unroll
-      for (int a = 0; a < NU; ++a) {
-        double kdx = 0.0;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) kdx = fma(in.K[a * 4 + i], dx[i], kdx);
-        ubar[a] = fma(alpha, in.d[a], in.u[a]) + kdx;
-      }
-      // ℓ(x̄ₖ − x_trajₖ, ūₖ) (:187-190; 2_link_helper_functions.jl:82-97)
-      const double e0 = P.tgt0 - fma(-xtw, in.xt[0], xb[0]);
-      const double e1 = P.tgt1 - fma(-xtw, in.xt[1], xb[1]);
-      double uu;
-      if constexpr (NU == 2) uu = ubar[0] * ubar[0] + ubar[NU - 1] * ubar[NU - 1];
-      else uu = ubar[0] * ubar[0];
-      p.cost += (e0 * e0 + e1 * e1) + uu;
-      put_x(t);
-#pragma unroll
-      for (int a = 0; a < NU; ++a) store_or_drop(ubar[a], rU, true, su + (uint32_t)((t * NU + a) * 8));
-      const double du0 = ubar[0] - in.u[0];
-      if constexpr (NU == 2) {
-        const double du1 = ubar[NU - 1] - in.u[NU - 1];
-        p.du2 = fma(du0, du0, fma(du1, du1, p.du2));
-      } else {
-        p.du2 = fma(du0, du0, p.du2);
-      }
-      // x̄ₖ₊₁ = f(x̄ₖ, ūₖ) (:74)
-      double xn[4];
-      if constexpr (ROBUST) rk4<double, NU>(P, xb, ubar, xn);
-      else rk4_roll<NU>(R, xb, ubar, xn, p.bad);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) xb[i] = xn[i];
-    };
-    // inputs of the next TL_FW_PF steps in flight (HBM latency ≈ one RK4 step)
-    TLStepIn<NU> ring[TL_FW_PF];
-#pragma unroll
-    for (int k = 0; k < TL_FW_PF; ++k) load(k, ring[k]);
-    int t = 0;
-    for (; t + TL_FW_PF <= T; t += TL_FW_PF) {
-#pragma unroll
-      for (int k = 0; k < TL_FW_PF; ++k) {
-        step(t + k, ring[k]);
-        load(t + k + TL_FW_PF, ring[k]);
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < TL_FW_PF - 1; ++k)
-      if (t + k < T) step(t + k, ring[k]);
-    put_x(T);
-    // final_cost(x̄_N) on the raw state (:192; 2_link_helper_functions.jl:100-108)
-    const double f0 = P.tgt0 - xb[0], f1 = P.tgt1 - xb[1];
-    p.cost += f0 * f0 + f1 * f1;
-    return p;
-  };
-  while (true) {
-#if ILQR_TL_RK4_SHIFT
-    Pass p = pass(TLPath<false>{});
-    if (p.bad) p = pass(TLPath<true>{});  // an argument out of rk4_roll's ranges: redo
-#else
-    const Pass p = pass(TLPath<true>{});
-#endif
-    const double cost = p.cost, du2 = p.du2;
-    if (rerun) break;  // the accepted candidate's rollout, now stored
-    const int k = r * L + sub;  // 0-based trial index of this lane's candidate
-    const bool acc = k < ls.max_trials && prev_cost - cost > 0.0;  // NaN compares false
-    const unsigned am = (unsigned)(__ballot(acc) >> gbase) & ((1u << L) - 1u);
-    if (am) {
-      const int first = __builtin_ctz(am);
-      if (sub != first) break;
-      out.trials = k + 1;
-      out.accepted = 1;
-      out.cost = cost;
-      out.du2 = du2;
-      out.owner = true;
-      if (store) break;
-      store = rerun = true;  // roll out once more, storing
-      continue;
-    }
-    if ((r + 1) * L >= ls.max_trials) {  // exhausted (the reference would loop forever)
-      if (k == ls.max_trials - 1) {
-        out.trials = k + 1;
-        out.cost = cost;
-        out.du2 = du2;
-        out.owner = true;
-      }
-      break;
-    }
-    ++r;
-#pragma unroll
-    for (int j = 0; j < L; ++j) alpha_r *= ls.shrink;
-    alpha = alpha_r;
-    for (int j = 0; j < sub; ++j) alpha *= ls.shrink;
+template <int NU_>
+struct TwoLinkModel {
+  using V = double;
+  static constexpr int NU = NU_;
+  static constexpr bool HAS_FAST = ILQR_TL_RK4_SHIFT != 0;
+  TwoLinkParams P;
+  TLRoll R;
+  __device__ __forceinline__ void rk4_fast(const double (&x)[4], const double (&u)[NU], double (&o)[4],
+                                           bool& bad) const {
+    rk4_roll<NU>(R, x, u, o, bad);
   }
-  return out;
-}
+  __device__ __forceinline__ void rk4_robust(const double (&x)[4], const double (&u)[NU], double (&o)[4]) const {
+    rk4<double, NU>(P, x, u, o);
+  }
+  // ℓ(x̄ₖ − x_trajₖ, ūₖ) (forward_pass.jl:187-190; 2_link_helper_functions.jl:82-97)
+  __device__ __forceinline__ double stage_cost(const double (&xb)[4], const double (&xt)[4], double xtw,
+                                               const double (&ub)[NU]) const {
+    const double e0 = P.tgt0 - fma(-xtw, xt[0], xb[0]);
+    const double e1 = P.tgt1 - fma(-xtw, xt[1], xb[1]);
+    double uu;
+    if constexpr (NU == 2) uu = ub[0] * ub[0] + ub[NU - 1] * ub[NU - 1];
+    else uu = ub[0] * ub[0];
+    return (e0 * e0 + e1 * e1) + uu;
+  }
+  // final_cost(x̄_N) on the raw state (:192; 2_link_helper_functions.jl:100-108)
+  __device__ __forceinline__ double final_cost(const double (&xb)[4]) const {
+    const double f0 = P.tgt0 - xb[0], f1 = P.tgt1 - xb[1];
+    return f0 * f0 + f1 * f1;
+  }
+};
 
 // ---------------------------------------------------------------------------
 // Kernels
@@ -732,7 +568,7 @@ __global__ __launch_bounds__(64 * TL_BW4_WAVES) void tl_backward_kernel(TwoLinkP
 // latency (236 vs 275 µs; profiles/r02/tl_fw_probe.log). W waves per workgroup: 1 for
 // the candidate grids (four 1-lane waves on one CU at B = 1024 ran 27.6 → 54.7 µs), 4
 // past B = 65536 (1-wave workgroups past 256 waves were packed two to a SIMD).
-inline int tl_fw_lanes(int B) { return B <= 65536 ? 4 : 1; }
+inline int tl_fw_lanes(int B) { return fg_lanes(B); }
 
 template <int NU, int L, int W>
 __global__ __launch_bounds__(64 * W) void tl_forward_kernel(
@@ -744,7 +580,8 @@ __global__ __launch_bounds__(64 * W) void tl_forward_kernel(
   const int b = (blockIdx.x * 64 * W + threadIdx.x) / L;  // a group of L lanes per trajectory
   if (b >= B) return;
   const double pc = prev_cost ? prev_cost[b] : INFINITY;
-  const TLFwdOut r = tl_forward_group<NU, L>(P, b, B, T, x, u, xtraj, d, K, pc, xnew, unew, ls);
+  const TwoLinkModel<NU> m{P, tl_roll_consts(P)};
+  const FgOut<double> r = fwd_group<TwoLinkModel<NU>, L>(m, b, B, T, x, u, xtraj, d, K, pc, xnew, unew, ls);
   if (!r.owner) return;
   if (!r.accepted) {  // exhausted (the reference would loop forever): return the inputs
     for (int i = 0; i < (T + 1) * TL_NX; ++i) xnew[(size_t)b * (T + 1) * TL_NX + i] = x[(size_t)b * (T + 1) * TL_NX + i];
@@ -785,7 +622,9 @@ __global__ __launch_bounds__(64 * W) void tl_iter_forward_kernel(TwoLinkParams P
   const int b = (blockIdx.x * 64 * W + threadIdx.x) / L;
   if (b >= B || a.status[b] != ILQR_TRAJ_OK) return;
   const double pc = a.prev_cost ? a.prev_cost[b] : INFINITY;
-  const TLFwdOut r = tl_forward_group<NU, L>(P, b, B, T, a.x, a.u, a.xtraj, a.d, a.K, pc, a.xnew, a.unew, ls);
+  const TwoLinkModel<NU> m{P, tl_roll_consts(P)};
+  const FgOut<double> r = fwd_group<TwoLinkModel<NU>, L>(m, b, B, T, a.x, a.u, a.xtraj, a.d, a.K, pc, a.xnew,
+                                                          a.unew, ls);
   if (!r.owner) return;
   if (a.trials) a.trials[b] = r.trials;
   if (a.du2) a.du2[b] = r.du2;
@@ -845,7 +684,7 @@ hipError_t tl_backward_nu(const TwoLinkParams& P, int B, int T, const double* x,
 
 // the forward's buffer resources span one wave's trajectories: 64 · (T+1) · 32 bytes
 // below 2³¹ (the out-of-range offset that drops a store)
-inline bool tl_fw_fits(int T) { return (size_t)64 * (T + 1) * TL_NX * 8 < 0x80000000ull; }
+inline bool tl_fw_fits(int T) { return fg_fits<double>(T); }
 
 template <int NU>
 hipError_t tl_forward_nu(const TwoLinkParams& P, int B, int T, const double* x, const double* u,

@@ -1,6 +1,6 @@
 // Probe: the 2-link forward kernel (ilqr_twolink.hip) at BASELINE config 2's size,
 // B = 1024, T = 50 (argv: B T), for the build variants of the rollout
-// (-DILQR_TL_RK4_SHIFT=0/1, -DILQR_TL_FW_PF), the line-search lanes per trajectory L and
+// (-DILQR_TL_RK4_SHIFT=0/1, -DILQR_FW_GROUP_PF), the line-search lanes per trajectory L and
 // the waves per workgroup W, with one accepted trial (prev_cost = +Inf) and with a
 // four-trial search (prev_cost = −Inf, max_trials = 4: exhausted after trial 4). Prints
 // one JSON line per NU. Build: tools/tl_fw_probe.sh.
@@ -63,7 +63,7 @@ void run(int B, int T) {
   LSParams ls{0.0, 1.0, 0.5, 1e-6, 4};
   const int reps = 200;
   printf("{\"nu\": %d, \"B\": %d, \"T\": %d, \"rk4_shift\": %d, \"pf\": %d", NU, B, T,
-         ILQR_TL_RK4_SHIFT, ILQR_TL_FW_PF);
+         ILQR_TL_RK4_SHIFT, ILQR_FW_GROUP_PF);
   auto both = [&](const char* tag, auto f) {
     printf(", \"us_%s_trial1\": %.2f, \"us_%s_trials4\": %.2f", tag, f(pinf), tag, f(pneg));
   };
