@@ -426,13 +426,20 @@ struct Chain                 # ilqr_chain (include/ilqr.h), ILQR_CHAIN_MAX_JOINT
     qf_weight::NTuple{8,Float64}
 end
 
-"""chain_fit(chain, x_init, u_init; max_iter, tol, linearization) → (x̄, ū, status)
+const ILQR_CHAIN_DYN_AUTO = Int32(0)         # ilqr_chain_set_dynamics (include/ilqr.h)
+const ILQR_CHAIN_DYN_RNEA = Int32(1)
+const ILQR_CHAIN_DYN_CLOSED_FORM = Int32(2)
+
+"""chain_fit(chain, x_init, u_init; max_iter, tol, linearization, dynamics) → (x̄, ū, status)
 
 Batched fit of the chain family; x_init (nx, T+1, batch), u_init (nu, T, batch) as
 Array{Float32,3} (fp32, BASELINE config 5) or Array{Float64,3}: the element type picks
-the device precision, as the reference's generic Julia code would."""
+the device precision, as the reference's generic Julia code would. `dynamics` picks the
+2-joint evaluator (AUTO: the closed form sampled from the Newton-Euler recursion at
+creation; RNEA: the recursion itself)."""
 function chain_fit(c::Chain, x_init::Array{E,3}, u_init::Array{E,3}; max_iter::Int64=100,
-                   tol::Float64=1e-6, linearization=ILQR_LINEARIZE_DUAL) where {E<:Union{Float32,Float64}}
+                   tol::Float64=1e-6, linearization=ILQR_LINEARIZE_DUAL,
+                   dynamics=ILQR_CHAIN_DYN_AUTO) where {E<:Union{Float32,Float64}}
     nx, N, nb = size(x_init); nu = size(u_init, 1); M = N - 1
     @assert(size(u_init, 2) == M)
     r = Ref{Ptr{Cvoid}}(C_NULL)
@@ -440,6 +447,8 @@ function chain_fit(c::Chain, x_init::Array{E,3}, u_init::Array{E,3}; max_iter::I
     check(ccall((:ilqr_chain_create, libilqr), Cint,
                 (Ref{Ptr{Cvoid}}, Cint, Ref{Chain}, Cint, Cint, Int32, Int32),
                 r, 0, c, M, nb, dt, linearization), "ilqr_chain_create")
+    check(ccall((:ilqr_chain_set_dynamics, libilqr), Cint, (Ptr{Cvoid}, Int32), r[], dynamics),
+          "ilqr_chain_set_dynamics")
     h = Handle(nx, nu, M, 1)                 # device-memory helper only
     xi = upload(h, x_init); ui = upload(h, u_init)
     xo = alloc(h, E, length(x_init)); uo = alloc(h, E, length(u_init)); sd = alloc(h, Int32, nb)
