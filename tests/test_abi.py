@@ -92,3 +92,17 @@ def test_no_oracle_in_the_product_path():
                 txt = open(os.path.join(dirpath, f), encoding="utf-8").read()
                 for bad in ("import oracle", "from oracle", "libilqr_oracle", "ilqr_ref"):
                     assert bad not in txt, (f, bad)
+
+
+def test_julia_shim_ccalls_declared_symbols():
+    """Every `ccall((:ilqr_…, libilqr), …)` of the Julia shim names a function that
+    include/ilqr.h declares and the library exports (the shim cannot run here)."""
+    src = open(os.path.join(ROOT, "ilqr.jl_amd", "julia", "iLQRHIP.jl")).read()
+    called = set(re.findall(r"ccall\(\(:(ilqr_[a-z0-9_]+),\s*libilqr\)", src))
+    assert {"ilqr_fit", "ilqr_backward", "ilqr_forward", "ilqr_backward_tiles",
+            "ilqr_chain_fit", "ilqr_chain_set_dynamics"} <= called, called
+    declared = set(declared_functions())
+    assert called <= declared, called - declared
+    lib = _lib.load()
+    for name in called:
+        assert hasattr(lib, name), name
