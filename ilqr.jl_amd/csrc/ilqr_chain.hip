@@ -1325,8 +1325,22 @@ __device__ unsigned chain_backward4_wave(const ChainK<V, 2>& P, int b0, int B, u
   double* Hl = lds + beta * 16;
 
   constexpr int PF = CH_BW4_PF;
-  double rA[PF], rB[PF], rT[PF], rU[PF];
-  auto ld = [&](uint32_t off, int t) { return ch_ld<V>(rJ, off, (uint32_t)(t * NR * W)); };
+  // the ring holds the records' raw words: an fp32 record converted at the load would
+  // make the step that issued it wait for it (the conversion consumes the load), which
+  // defeats the prefetch — the conversion happens at the use, PF steps later
+  using Raw = std::conditional_t<sizeof(V) == 4, uint32_t, double>;
+  Raw rA[PF], rB[PF], rT[PF], rU[PF];
+  auto ld = [&](uint32_t off, int t) -> Raw {
+    if constexpr (sizeof(V) == 4)
+      return __builtin_amdgcn_raw_buffer_load_b32(rJ, off, (uint32_t)(t * NR * W), 0);
+    else
+      return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rJ, off, (uint32_t)(t * NR * W), 0));
+  };
+  auto cv = [](Raw r) -> double {
+    asm volatile("" : "+v"(r));  // the conversion stays at the use
+    if constexpr (sizeof(V) == 4) return (double)__builtin_bit_cast(float, r);
+    else return r;
+  };
 #pragma unroll
   for (int k = 0; k < PF; ++k) {
     const int tk = T - 1 - k > 0 ? T - 1 - k : 0;
@@ -1335,26 +1349,41 @@ __device__ unsigned chain_backward4_wave(const ChainK<V, 2>& P, int b0, int B, u
   __builtin_amdgcn_s_waitcnt(0);
   double Kl = 0.0, dl = 0.0;
   auto step = [&](int t, int k) {
-    const double A = rA[k], Bm = rB[k], th = rT[k], uu = rU[k];
+    const double A = cv(rA[k]), Bm = cv(rB[k]), th = cv(rT[k]), uu = cv(rU[k]);
     const int tn = t - PF > 0 ? t - PF : 0;
     rA[k] = ld(oA, tn); rB[k] = ld(oB, tn); rT[k] = ld(oT, tn); rU[k] = ld(oU, tn);
     const double lx = rj ? -qw2 * (tg - th) : 0.0;
     const double lu = rw2 * uu;
-    const double Y0 = ch_mf(S, A, 0.0), Y1 = ch_mf(S, Bm, 0.0);
-    const double H = ch_mf(Bm, Y1, luu);                          // luu + BᵀSB
-    Hl[rho * 4 + kap] = H;
+    const double Y0 = ch_mf(S, A, 0.0);
     const double Z = ch_mf(A, Y0, lxx);                           // lxx + AᵀSA
     const double G = ch_mf(Bm, Y0, 0.0);                          // BᵀSA
     const double gx = ch_mf(A, s, lx), gu = ch_mf(Bm, s, lu);     // lx + Aᵀs, lu + Bᵀs
-    wave_lds_fence();
-    const double h00 = Hl[0], h10 = Hl[4], h11 = Hl[5];
-    wave_lds_fence();
-    // (H + μI)⁻¹ on the (≤ 2) × (≤ 2) u block by its adjugate (H = luu + O(Δt²)BᵀSB)
-    const double a00 = h00 + mu, a11 = h11 + mu;
-    const double idet = rcp<2>(fma(a00, a11, -h10 * h10));
-    const bool in2 = rho < 2 && kap < 2;
-    const double Hi = !in2 ? 0.0 : (rho != kap ? -h10 : (rho == 0 ? a11 : a00)) * idet;
-    const double K = ch_mfn(Hi, G, 0.0), d = ch_mfn(Hi, gu, 0.0);
+    double K, d;
+    if constexpr (NU == 2) {
+      const double Y1 = ch_mf(S, Bm, 0.0);
+      const double H = ch_mf(Bm, Y1, luu);                        // luu + BᵀSB
+      Hl[rho * 4 + kap] = H;
+      wave_lds_fence();
+      const double h00 = Hl[0], h10 = Hl[4], h11 = Hl[5];
+      wave_lds_fence();
+      // (H + μI)⁻¹ of the 2×2 u block by its adjugate (H = luu + O(Δt²)BᵀSB)
+      const double a00 = h00 + mu, a11 = h11 + mu;
+      const double idet = rcp<2>(fma(a00, a11, -h10 * h10));
+      const bool in2 = rho < 2 && kap < 2;
+      const double Hi = !in2 ? 0.0 : (rho != kap ? -h10 : (rho == 0 ? a11 : a00)) * idet;
+      K = ch_mfn(Hi, G, 0.0);
+      d = ch_mfn(Hi, gu, 0.0);
+    } else {
+      // 1×1 H in every lane of the slot from B's column replicated over κ (a quad
+      // broadcast): no LDS hand-off, and the gains are VALU products (ilqr_twolink.hip)
+      const double Br = dpp_quad_bcast0(Bm);
+      const double Y1 = ch_mf(S, Br, 0.0);                        // S·b, replicated
+      const double H = ch_mf(Br, Y1, 2.0 * (double)P.rw[0]);      // luu + bᵀSb everywhere
+      const double hi = rcp<2>(H + mu);
+      K = -(hi * G);
+      d = -(hi * gu);
+      (void)Hl; (void)luu;
+    }
     ch_st<V>(K, rK, kv, kv == DEAD ? 0u : (uint32_t)(t * NU * NX * W));
     ch_st<V>(d, rD, dv, dv == DEAD ? 0u : (uint32_t)(t * NU * W));
     const double Wk = fma(mu, K, -G), Wd = fma(mu, d, -gu);

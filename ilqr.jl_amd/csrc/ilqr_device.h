@@ -45,6 +45,17 @@ __device__ __forceinline__ double rowsum16(double v) {
   return v;
 }
 
+// lane 0 of each quad to the whole quad (DPP quad_perm [0,0,0,0]), a double: in the
+// 4-block MFMA layout (lane 16ρ + 4β + κ) the quad is κ = 0..3, so this turns column 0
+// of a block into a replicated vector
+__device__ __forceinline__ double dpp_quad_bcast0(double x) {
+  typedef unsigned u2v_ __attribute__((ext_vector_type(2)));
+  const u2v_ p = __builtin_bit_cast(u2v_, x);
+  const u2v_ q = {(unsigned)__builtin_amdgcn_mov_dpp((int)p.x, 0x00, 0xF, 0xF, true),
+                  (unsigned)__builtin_amdgcn_mov_dpp((int)p.y, 0x00, 0xF, 0xF, true)};
+  return __builtin_bit_cast(double, q);
+}
+
 // Cross-lane LDS hand-off inside one wave: DS ops of a wave execute in order, so
 // only the compiler must be kept from moving LDS accesses across this point.
 __device__ __forceinline__ void wave_lds_fence() {

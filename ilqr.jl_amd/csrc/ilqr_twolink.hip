@@ -359,30 +359,39 @@ __device__ unsigned tl_backward4_wave(const TwoLinkParams& P, int b0, int B, uns
     // immediate_cost_quadratization (:81-109): lx = [2(θ−θ*), 0, 0], lu = 2u
     const double lx = rho < 2 ? -2.0 * (tg - th) : 0.0;
     const double lu = ru ? 2.0 * uu : 0.0;
-    const double Y0 = mfa(S, A, 0.0), Y1 = mfa(S, Bm, 0.0);      // S·A, S·B
-    const double H = mfa(Bm, Y1, lxx);                            // luu + BᵀSB
-    Hl[rho * 4 + kap] = H;
+    const double Y0 = mfa(S, A, 0.0);                             // S·A
     const double Z = mfa(A, Y0, lxx);                             // lxx + AᵀSA
     const double G = mfa(Bm, Y0, 0.0);                            // BᵀSA (lux = 0)
     const double gx = mfa(A, s, lx), gu = mfa(Bm, s, lu);         // lx + Aᵀs, lu + Bᵀs
     // feedback_parameters (:207-218): (H + μI)⁻¹ of the NU×NU block by its adjugate, in
     // every lane (H = 2I + BᵀSB with B = O(Δt): condition ≈ 1, so the explicit inverse
     // costs nothing in accuracy and one MFMA stage less than two triangular sweeps)
-    wave_lds_fence();
-    const double h00 = Hl[0], h10 = Hl[4], h11 = Hl[5];
-    wave_lds_fence();
-    double Hi;
+    double K, d;
     if constexpr (NU == 2) {
+      const double Y1 = mfa(S, Bm, 0.0);                          // S·B
+      const double H = mfa(Bm, Y1, lxx);                          // luu + BᵀSB
+      Hl[rho * 4 + kap] = H;
+      wave_lds_fence();
+      const double h00 = Hl[0], h10 = Hl[4], h11 = Hl[5];
+      wave_lds_fence();
       const double a00 = h00 + mu, a11 = h11 + mu;
       const double idet = rcp<2>(fma(a00, a11, -h10 * h10));
       const bool in2 = rho < 2 && kap < 2;
-      Hi = !in2 ? 0.0 : (rho != kap ? -h10 : (rho == 0 ? a11 : a00)) * idet;
+      const double Hi = !in2 ? 0.0 : (rho != kap ? -h10 : (rho == 0 ? a11 : a00)) * idet;
+      K = mfa_n(Hi, G, 0.0);                                      // −(H+μI)⁻¹ G
+      d = mfa_n(Hi, gu, 0.0);                                     // −(H+μI)⁻¹ g
     } else {
-      (void)h10; (void)h11;
-      Hi = (rho == 0 && kap == 0) ? rcp<2>(h00 + mu) : 0.0;
+      // H is 1×1: with B's column replicated over κ (a quad broadcast) the two MFMAs
+      // that form it leave bᵀSb in every lane of the slot — no LDS hand-off — and the
+      // gains are VALU products: the bits of the block form (its other terms are 0)
+      const double Br = dpp_quad_bcast0(Bm);
+      const double Y1 = mfa(S, Br, 0.0);                          // S·b, replicated
+      const double H = mfa(Br, Y1, 2.0);                          // luu + bᵀSb everywhere
+      const double hi = rcp<2>(H + mu);
+      K = -(hi * G);                                              // −(H+μ)⁻¹ G (row 0)
+      d = -(hi * gu);                                             // −(H+μ)⁻¹ g
+      (void)Hl;
     }
-    const double K = mfa_n(Hi, G, 0.0);                           // −(H+μI)⁻¹ G
-    const double d = mfa_n(Hi, gu, 0.0);                          // −(H+μI)⁻¹ g
     store_or_drop(K, rK, kv != 0x80000000u, kv + (uint32_t)(t * NU * TL_NX * 8));
     store_or_drop(d, rD, dv != 0x80000000u, dv + (uint32_t)(t * NU * 8));
     // step_back (:262-273), exact rewrite: W = (H+2μI)[K|d] = μ[K|d] − [G|g]
