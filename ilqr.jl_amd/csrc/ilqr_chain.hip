@@ -613,7 +613,6 @@ __device__ __forceinline__ void chain_xdot_cv(const ChainK<V, NJ>& P, const V (&
 template <class V>
 struct ChainTrig {
   V Mc[3][5];     // M₀₀, M₀₁, M₁₁: a₀ + a₁ cos q₂ + b₁ sin q₂ + a₂ cos 2q₂ + b₂ sin 2q₂
-  V dMc[3][4];    // dM/dq₂ on (cos q₂, sin q₂, cos 2q₂, sin 2q₂): (b₁, −a₁, 2b₂, −2a₂)
   V Gc[2][3][3];  // g_i = Σ_ab Gc[i][a][b] φ_a(q₁) φ_b(q₂), φ = (1, cos, sin)
   V dt;
   V tgt[2], qw[2], rw[2], qfw[2];  // joint-space cost (as ChainK)
@@ -629,7 +628,9 @@ __device__ __forceinline__ void chain_qdd_trig(const ChainTrig<V>& P, const S& s
 #pragma unroll
   for (int e = 0; e < 3; ++e) {
     m[e] = P.Mc[e][0] + (((P.Mc[e][1] * c2 + P.Mc[e][2] * s2) + P.Mc[e][3] * C2) + P.Mc[e][4] * S2);
-    dm[e] = ((P.dMc[e][0] * c2 + P.dMc[e][1] * s2) + P.dMc[e][2] * C2) + P.dMc[e][3] * S2;
+    // dM/dq₂ = b₁ cos − a₁ sin + 2(b₂ cos 2q − a₂ sin 2q) (the kernel argument holds M's
+    // coefficients only: fewer scalar registers than a second table)
+    dm[e] = (P.Mc[e][2] * c2 - P.Mc[e][1] * s2) + V(2) * (P.Mc[e][4] * C2 - P.Mc[e][3] * S2);
   }
   S g[2];
 #pragma unroll
@@ -1765,7 +1766,6 @@ ilqr::ChainTrig<V> trig_consts(const ilqr_chain_handle* h) {
   const ilqr::ChainTrig<double>& D = h->trig;
   for (int e = 0; e < 3; ++e) {
     for (int k = 0; k < 5; ++k) Q.Mc[e][k] = (V)D.Mc[e][k];
-    for (int k = 0; k < 4; ++k) Q.dMc[e][k] = (V)D.dMc[e][k];
   }
   for (int i = 0; i < 2; ++i)
     for (int a = 0; a < 3; ++a)
@@ -1815,10 +1815,6 @@ hipError_t chain_trig_build(ilqr_chain_handle* h) {
       D.Mc[en][2] = 2 * b1 / 5;
       D.Mc[en][3] = 2 * a2 / 5;
       D.Mc[en][4] = 2 * b2 / 5;
-      D.dMc[en][0] = D.Mc[en][2];       // d/dq (b₁ sin) = b₁ cos
-      D.dMc[en][1] = -D.Mc[en][1];      // d/dq (a₁ cos) = −a₁ sin
-      D.dMc[en][2] = 2 * D.Mc[en][4];   // d/dq (b₂ sin 2q) = 2b₂ cos 2q
-      D.dMc[en][3] = -2 * D.Mc[en][3];  // d/dq (a₂ cos 2q) = −2a₂ sin 2q
     }
     for (int i = 0; i < 2; ++i) {  // 2-D transform on the 3×3 grid: φ = (1, cos, sin)
       for (int a = 0; a < 3; ++a)
