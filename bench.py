@@ -146,6 +146,8 @@ def main():
     ap.add_argument("--T", type=int, default=100)
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds for the CPU baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--forward", default="dpp", choices=["dpp", "mfma"],
+                    help="the ring forward's mat-vecs: DPP row broadcasts or the 4-block f64 MFMA")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -172,6 +174,7 @@ def main():
     lq, x0, u0 = quadrotor_batch(B, T=T, seed0=rank * B)
     s = Solver(NX, NU, T, B, device=local)
     s.set_problem(lq)
+    s.set_schedule(forward_mfma=args.forward == "mfma")
     lib, h = s.lib, s.h
     x = torch.from_numpy(x0).to(dev)
     u = torch.from_numpy(u0).to(dev)
@@ -375,7 +378,8 @@ def main():
         "data": "synthetic: per-instance randomised hover-linearised quadrotor LQ (SURVEY.md §8d)",
         "config": {"workload": f"quadrotor-style LQ iLQR.fit, {FIT_ITERS} iterations from cold, tol disabled",
                    "nx": NX, "nu": NU, "T": T, "batch_per_gpu": B, "global_batch": B * world,
-                   "parallelism": f"independent trajectories, {world} rank(s), no data-path collective"},
+                   "parallelism": f"independent trajectories, {world} rank(s), no data-path collective",
+                   "forward": args.forward},
         "clock_settle_s": settle_s, "clock_settle_fits": n_settle,
         "fit_timing": fit_stats,
         "roofline": {"bound": "mfma", "kernel": "lq_iter_backward4 (backward_pass, 4 trajectories per wave, v_mfma_f64_4x4x4_4b)",

@@ -53,6 +53,7 @@ struct ilqr_handle {
   // forward of sequential iterations through the LDS-ring kernel
   bool pipelined = false;
   bool fw_ring = true;
+  bool fw_mfma = false;  // ILQR_SCHED_FORWARD_MFMA: the ring forward on the 4-block f64 MFMA
   // backward + forward of an iteration in one launch (ILQR_SCHED_FUSED, default on),
   // with the four-trajectories-per-wave backward and the ring forward only: 166 → 159 µs
   // per headline iteration (no kernel boundary)
@@ -139,11 +140,12 @@ ilqr_status enqueue_iteration(ilqr_handle* h, const ilqr_problem* p, const ilqr:
   const ilqr::LQParams P = lq_params(p);
   if (h->nchunks == 1) {  // one stream, no cross-stream events (each hand-off costs ~10 µs)
     if (h->fused && !h->bw_wave && h->fw_ring && h->nx == 12 && h->nu == 4) {
-      HIP_TRY(ilqr::launch_lq_iter_fused4(P, h->batch, h->T, a, ls, h->stream));
+      HIP_TRY(ilqr::launch_lq_iter_fused4(P, h->batch, h->T, a, ls, h->stream, h->fw_mfma));
       return ILQR_OK;
     }
     HIP_TRY(ilqr::launch_lq_iter_backward(h->nx, h->nu, P, 0, h->batch, h->T, a, ls.mu, h->stream, h->bw_wave));
-    HIP_TRY(ilqr::launch_lq_iter_forward(h->nx, h->nu, P, 0, h->batch, h->T, a, ls, h->stream, h->fw_ring));
+    HIP_TRY(ilqr::launch_lq_iter_forward(h->nx, h->nu, P, 0, h->batch, h->T, a, ls, h->stream, h->fw_ring,
+                                         h->fw_mfma));
     return ILQR_OK;
   }
   for (int c = 0; c < h->nchunks; ++c) {
@@ -215,6 +217,7 @@ ilqr_status ensure_pad(ilqr_handle* h) {
   h->pad->pipelined = h->pipelined;
   h->pad->fused = h->fused;
   h->pad->fw_ring = h->fw_ring;
+  h->pad->fw_mfma = h->fw_mfma;
   h->pad->bw_wave = h->bw_wave;
   return ILQR_OK;
 }
@@ -406,13 +409,14 @@ ilqr_status ilqr_set_stream(ilqr_handle* h, void* s) {
 
 ilqr_status ilqr_set_schedule(ilqr_handle* h, int flags) {
   if (!h || (flags & ~(ILQR_SCHED_PIPELINED | ILQR_SCHED_RING_FORWARD | ILQR_SCHED_BACKWARD_WAVE |
-                      ILQR_SCHED_BACKWARD_BLOCK | ILQR_SCHED_FUSED)) != 0)
+                      ILQR_SCHED_BACKWARD_BLOCK | ILQR_SCHED_FUSED | ILQR_SCHED_FORWARD_MFMA)) != 0)
     return ILQR_ERR_BAD_ARG;
   if ((flags & ILQR_SCHED_FUSED) && (flags & (ILQR_SCHED_BACKWARD_WAVE | ILQR_SCHED_PIPELINED)))
     return ILQR_ERR_BAD_ARG;
   h->pipelined = (flags & ILQR_SCHED_PIPELINED) != 0;
   h->fused = (flags & ILQR_SCHED_FUSED) != 0;
   h->fw_ring = (flags & ILQR_SCHED_RING_FORWARD) != 0;
+  h->fw_mfma = (flags & ILQR_SCHED_FORWARD_MFMA) != 0;
   if ((flags & ILQR_SCHED_BACKWARD_BLOCK) && (flags & (ILQR_SCHED_BACKWARD_WAVE | ILQR_SCHED_PIPELINED)))
     return ILQR_ERR_BAD_ARG;
   h->bw_wave = (flags & (ILQR_SCHED_BACKWARD_WAVE | ILQR_SCHED_PIPELINED)) != 0 ||
@@ -421,6 +425,7 @@ ilqr_status ilqr_set_schedule(ilqr_handle* h, int flags) {
     h->pad->pipelined = h->pipelined;
     h->pad->fused = h->fused;
     h->pad->fw_ring = h->fw_ring;
+  h->pad->fw_mfma = h->fw_mfma;
     h->pad->bw_wave = h->bw_wave;
   }
   return ILQR_OK;
@@ -514,7 +519,7 @@ ilqr_status ilqr_forward(ilqr_handle* h, const ilqr_problem* p, const ilqr_optio
   else
     HIP_TRY(ilqr::launch_lq_forward(h->nx, h->nu, lq_params(p), h->batch, h->T, x, u, x_traj, d,
                                     K, prev_cost, x_new, u_new, new_cost, trials, status,
-                                    ls_params(o), h->stream, h->fw_ring));
+                                    ls_params(o), h->stream, h->fw_ring, h->fw_mfma));
   return status ? fold_status(h, status) : ILQR_OK;
 }
 

@@ -430,6 +430,7 @@ __global__ __launch_bounds__(256) void lq_iter_backward4_kernel(LQParams P, int 
 // dispatcher packed two of them onto one SIMD.
 constexpr int FUSED_WAVES = 4;
 constexpr int FUSED_LDS = PIPE_R * RING_SLOT + RING_LAREA;  // doubles per wave
+template <bool MF>
 __global__ __launch_bounds__(64 * FUSED_WAVES) void lq_iter_fused4_kernel(LQParams P, int B, int T,
                                                                          IterArgs a, LSParams ls) {
   __shared__ __attribute__((aligned(16))) double lds_all[FUSED_WAVES * FUSED_LDS];
@@ -454,16 +455,22 @@ __global__ __launch_bounds__(64 * FUSED_WAVES) void lq_iter_fused4_kernel(LQPara
   __builtin_amdgcn_s_waitcnt(0);
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
   const unsigned run = active & ~nan;
-  iter_forward_wave_active<12, 4>(P, b0, B, T, a, ls, lds, ((run >> (l >> 4)) & 1u) != 0);
+  if constexpr (MF)
+    iter_forward_wave_mfma(P, b0, B, T, a, ls, lds, run);
+  else
+    iter_forward_wave_active<12, 4>(P, b0, B, T, a, ls, lds, ((run >> (l >> 4)) & 1u) != 0);
 }
 
 }  // namespace
 
 hipError_t launch_lq_iter_fused4(const LQParams& p, int B, int T, const IterArgs& a, const LSParams& ls,
-                                 hipStream_t s) {
+                                 hipStream_t s, bool mfma) {
   if (B <= 0) return hipSuccess;
   const int per_wg = FUSED_WAVES * BW4_SLOTS;
-  lq_iter_fused4_kernel<<<(B + per_wg - 1) / per_wg, 64 * FUSED_WAVES, 0, s>>>(p, B, T, a, ls);
+  if (mfma)
+    lq_iter_fused4_kernel<true><<<(B + per_wg - 1) / per_wg, 64 * FUSED_WAVES, 0, s>>>(p, B, T, a, ls);
+  else
+    lq_iter_fused4_kernel<false><<<(B + per_wg - 1) / per_wg, 64 * FUSED_WAVES, 0, s>>>(p, B, T, a, ls);
   return hipGetLastError();
 }
 

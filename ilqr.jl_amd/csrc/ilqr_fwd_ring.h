@@ -486,6 +486,222 @@ __device__ FwdOut lq_forward_wave_ring(const LQParams& P, int b0, int B, int T, 
   return out;
 }
 
+// ---------------------------------------------------------------------------
+// The same forward pass on the 4-block f64 MFMA (round 2, ILQR_SCHED_FORWARD_MFMA):
+// the backward's layout — lane 16ρ + 4β + κ holds element [ρ][κ] of trajectory slot β's
+// 4×4 block, fm4(a, b, c) = c + aᵀb, vectors "replicated" (v[4I+ρ] in every κ). Per
+// step: ū = u + αδu + Kδx (3 MFMAs, one per δx block, in parallel), x̄' = A x̄ + B ū
+// (12: the A part does not wait for ū), ℓ = vᵀQv + ūᵀRū (9 for Qv, 3 + 1 + 1 for the
+// dot products, which the MFMA leaves replicated over the slot's 16 lanes): 29 MFMAs
+// for four trajectories against 44 DPP FMAs of the row form per four. The slot ring,
+// its producer and its waits are the row form's; the operands are read from the slot
+// in the block layout (Kᵀ blocks: K[κ][4J+ρ]). The constant blocks Aᵀ, Bᵀ, Qᵀ, Rᵀ
+// (Qfᵀ at the end of a trial) are loaded once. Arithmetic order differs from the row
+// form (MFMA sums of four): results agree to rounding (tests/test_gpu_parity.py).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double fm4(double a, double b, double c) {
+  return __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c, 0, 0, 0);
+}
+
+template <int R, int PF>
+__device__ FwdOut lq_forward_wave_mfma(const LQParams& P, int b0, int B, int T, unsigned run,
+                                       const double* __restrict__ x, const double* __restrict__ u,
+                                       const double* __restrict__ xtraj, const double* __restrict__ dg,
+                                       const double* __restrict__ Kg, double prev_cost,
+                                       double* __restrict__ xnew, double* __restrict__ unew,
+                                       double* du2_out, const LSParams& ls, double* ring) {
+  constexpr int NX = 12, NU = 4;
+  static_assert(R > PF && PF >= 1, "the slot being refilled must not be the one being read");
+  constexpr uint32_t OOR = 0x80000000u;
+  const int l = threadIdx.x & 63;
+  const int rho = l >> 4, beta = (l >> 2) & 3, kap = l & 3;
+  const int nt = B - b0 < 4 ? B - b0 : 4;
+  const int bb = b0 + (beta < nt ? beta : 0);  // absent slots alias trajectory b0 (never stored)
+  const bool active = beta < nt && ((run >> beta) & 1u);
+
+  // constant blocks (the A operand of fm4 is the block transposed)
+  const double* Ab = P.A + (size_t)bb * NX * NX;
+  const double* Bb = P.B + (size_t)bb * NX * NU;
+  const double* Qb = P.Q + (size_t)bb * NX * NX;
+  double AT[3][3], BT[3], QT[3][3];
+#pragma unroll
+  for (int I = 0; I < 3; ++I) {
+#pragma unroll
+    for (int J = 0; J < 3; ++J) {
+      AT[I][J] = Ab[(4 * I + kap) * NX + 4 * J + rho];
+      QT[I][J] = Qb[(4 * I + kap) * NX + 4 * J + rho];
+    }
+    BT[I] = Bb[(4 * I + kap) * NU + rho];
+  }
+  const double RT = P.R[(size_t)bb * NU * NU + kap * NU + rho];
+
+  // producer (the row form's: three global_load_lds_dwordx4 per step fill one slot)
+  auto tr = [&](int gg) { return (size_t)(b0 + (gg < nt ? gg : 0)); };
+  const double* xt0 = xtraj ? xtraj : x;
+  const double xtw = xtraj ? 1.0 : 0.0;
+  const char *p1, *p2, *p3;
+  uint32_t s1, s2, s3;
+  {
+    const int c = l;
+    p1 = reinterpret_cast<const char*>(Kg + tr(c / 24) * T * NU * NX + 2 * (c % 24));
+    s1 = NU * NX * 8;
+    if (l < 32) {
+      const int c2 = 64 + l;
+      p2 = reinterpret_cast<const char*>(Kg + tr(c2 / 24) * T * NU * NX + 2 * (c2 % 24));
+      s2 = NU * NX * 8;
+    } else if (l < 56) {
+      const int m = l - 32;
+      p2 = reinterpret_cast<const char*>(x + tr(m / 6) * (T + 1) * NX + 2 * (m % 6));
+      s2 = NX * 8;
+    } else {
+      const int m = l - 56;
+      p2 = reinterpret_cast<const char*>(u + tr(m / 2) * T * NU + 2 * (m % 2));
+      s2 = NU * 8;
+    }
+    const int l3 = l & 31;
+    if (l3 < 24) {
+      p3 = reinterpret_cast<const char*>(xt0 + tr(l3 / 6) * (T + 1) * NX + 2 * (l3 % 6));
+      s3 = NX * 8;
+    } else {
+      const int m = l3 - 24;
+      p3 = reinterpret_cast<const char*>(dg + tr(m / 2) * T * NU + 2 * (m % 2));
+      s3 = NU * 8;
+    }
+  }
+  const uint32_t ring_lds = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) double*)ring;
+  auto produce = [&](int t) {
+    uint32_t tt = (uint32_t)(t < T ? t : T - 1);
+    asm volatile("" : "+s"(tt));
+    const uint32_t m0 = ring_lds + (uint32_t)((t % R) * RING_SLOT * 8);
+    asm volatile("global_load_lds_dwordx4 %0, off" ::"v"(p1 + (size_t)tt * s1), "{m0}"(m0) : "memory");
+    asm volatile("global_load_lds_dwordx4 %0, off" ::"v"(p2 + (size_t)tt * s2), "{m0}"(m0 + 1024) : "memory");
+    asm volatile("global_load_lds_dwordx4 %0, off" ::"v"(p3 + (size_t)tt * s3), "{m0}"(m0 + 2048) : "memory");
+  };
+  constexpr int N_SS = 5 * PF - 3, N_PRO = 3 * PF - 3;
+  auto wait_slot = [](auto n) {
+    constexpr int v = decltype(n)::value;
+    static_assert(v >= 0 && v < 64, "vmcnt is 6 bits");
+    __builtin_amdgcn_s_waitcnt((v & 15) | (7 << 4) | (15 << 8) | ((v >> 4) << 14));
+    asm volatile("" ::: "memory");
+  };
+  // per step the wave issues 3 slot loads, then 4 result stores (3 x̄ blocks, ū): the
+  // row form's wait counts assume 2 stores per step, so this form waits with its own
+  constexpr int M_SS = 7 * PF - 3;
+  (void)N_SS;
+
+  // this lane's operands in a slot (block layout)
+  const int oK = 48 * beta + 12 * kap + rho;        // + 4J: K[κ][4J+ρ] of slot β
+  const int oX = 192 + 12 * beta + rho;             // + 4J: x[4J+ρ]
+  const int oXT = 256 + 12 * beta + rho;            // + 4J: x_traj[4J+ρ]
+  const int oU = 240 + 4 * beta + rho, oD = 304 + 4 * beta + rho;
+  const auto rXN = buffer_rsrc(xnew + (size_t)b0 * (T + 1) * NX, (uint32_t)nt * (T + 1) * NX * 8);
+  const auto rUN = buffer_rsrc(unew + (size_t)b0 * T * NU, (uint32_t)nt * T * NU * 8);
+  const bool st_lane = kap == 0;
+  const uint32_t oxs = (uint32_t)(beta * (T + 1) * NX + rho) * 8;  // + 32I + 96t
+  const uint32_t ous = (uint32_t)(beta * T * NU + rho) * 8;        // + 32t
+
+  double alpha = ls.alpha0;
+  FwdOut out{INFINITY, 0, 0};
+  bool open = active;
+  double du2_acc = 0.0;
+  for (int trial = 1; trial <= ls.max_trials && __any(open); ++trial) {
+#pragma unroll
+    for (int t = 0; t < PF; ++t) produce(t);
+    double cost = 0.0, du2 = 0.0;
+    double cq[3] = {0.0, 0.0, 0.0}, cr = 0.0;  // per-block cost accumulators (no chain between them)
+    const bool so = open && st_lane;
+    const uint32_t ox = so ? oxs : OOR, ou = so ? ous : OOR;
+    wait_slot(std::integral_constant<int, N_PRO>{});
+    double xb[3];
+    {
+      const double* sl = ring;
+#pragma unroll
+      for (int J = 0; J < 3; ++J) xb[J] = sl[oX + 4 * J];  // x̄₁ = x₁ (:65)
+    }
+    auto step = [&](int t, auto wait_n) {
+      wait_n();
+      const double* sl = ring + (t % R) * RING_SLOT;
+      double xk[3], xt[3], KT[3];
+#pragma unroll
+      for (int J = 0; J < 3; ++J) {
+        xk[J] = sl[oX + 4 * J];
+        xt[J] = sl[oXT + 4 * J];
+        KT[J] = sl[oK + 4 * J];
+      }
+      const double uk = sl[oU], dk = sl[oD];
+      // x̄ₖ₊₁'s A part first: it does not need ūₖ
+      double y[3];
+#pragma unroll
+      for (int I = 0; I < 3; ++I) y[I] = fm4(AT[I][2], xb[2], fm4(AT[I][1], xb[1], fm4(AT[I][0], xb[0], 0.0)));
+      // δx = x̄ₖ − xₖ (:72); ūₖ = uₖ + α δuₖ + Kₖ δx (:73)
+      const double k0 = fm4(KT[0], xb[0] - xk[0], 0.0);
+      const double k1 = fm4(KT[1], xb[1] - xk[1], 0.0);
+      const double k2 = fm4(KT[2], xb[2] - xk[2], fma(alpha, dk, uk));
+      const double ub = k2 + (k0 + k1);
+      produce(t + PF);
+      // ℓ(x̄ₖ − x_trajₖ, ūₖ) = vᵀQv + ūᵀRū (:187-190), accumulated in every lane of the slot
+      double v[3];
+#pragma unroll
+      for (int J = 0; J < 3; ++J) v[J] = fma(-xtw, xt[J], xb[J]);
+      double qv[3];
+#pragma unroll
+      for (int I = 0; I < 3; ++I) qv[I] = fm4(QT[I][2], v[2], fm4(QT[I][1], v[1], fm4(QT[I][0], v[0], 0.0)));
+      const double ru = fm4(RT, ub, 0.0);
+#pragma unroll
+      for (int I = 0; I < 3; ++I) cq[I] = fm4(v[I], qv[I], cq[I]);
+      cr = fm4(ub, ru, cr);
+#pragma unroll
+      for (int I = 0; I < 3; ++I)
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, xb[I]), rXN, ox,
+                                              (uint32_t)(t * NX * 8 + 32 * I), 0);
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, ub), rUN, ou, (uint32_t)t * NU * 8, 0);
+      const double e = ub - uk;
+      du2 = fma(e, e, du2);
+      // x̄ₖ₊₁ = A x̄ₖ + B ūₖ (:74)
+#pragma unroll
+      for (int I = 0; I < 3; ++I) xb[I] = fm4(BT[I], ub, y[I]);
+    };
+    const int tp = T < PF ? T : PF;
+    auto w_pro = [&] { wait_slot(std::integral_constant<int, N_PRO>{}); };
+    auto w_ss = [&] { wait_slot(std::integral_constant<int, M_SS>{}); };
+    for (int t = 0; t < tp; ++t) step(t, w_pro);
+    for (int t = tp; t < T; ++t) step(t, w_ss);
+    cost = ((cq[0] + cq[1]) + cq[2]) + cr;
+#pragma unroll
+    for (int I = 0; I < 3; ++I)
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, xb[I]), rXN, ox,
+                                            (uint32_t)(T * NX * 8 + 32 * I), 0);
+    // final_cost(x̄_N) = x̄ᵀQf x̄ on the raw state (:192)
+    {
+      const double* Qfb = P.Qf + (size_t)bb * NX * NX;
+#pragma unroll
+      for (int I = 0; I < 3; ++I) {
+        double qv = 0.0;
+#pragma unroll
+        for (int J = 0; J < 3; ++J) qv = fm4(Qfb[(4 * I + kap) * NX + 4 * J + rho], xb[J], qv);
+        cost = fm4(xb[I], qv, cost);
+      }
+    }
+    // Σ(ū − u)² over the slot's four u rows (lanes 16ρ + 4β + κ, ρ = 0..3)
+    du2 += __shfl_xor(du2, 16);
+    du2 += __shfl_xor(du2, 32);
+    if (open) {
+      out.trials = trial;
+      out.cost = cost;
+      du2_acc = du2;
+      if (prev_cost - cost > 0.0) {  // (:77-80); NaN compares false → keep searching
+        out.accepted = 1;
+        open = false;
+      }
+    }
+    alpha *= ls.shrink;  // (:82)
+    __builtin_amdgcn_s_waitcnt((0) | (7 << 4) | (0 << 8));
+    asm volatile("" ::: "memory");
+  }
+  if (du2_out) *du2_out = du2_acc;
+  return out;
+}
+
 // forward ring inside the pipe kernel: the workgroup's backward scratch holds R slots
 constexpr int PIPE_R = 8, PIPE_PF = 7;
 
@@ -504,6 +720,36 @@ __device__ __forceinline__ void iter_forward_wave_active(const LQParams& P, int 
                                                                  a.xtraj, a.d, a.K, pc, a.xnew,
                                                                  a.unew, &du2, ls, ring);
   if (j == 0 && active) {
+    if (a.trials) a.trials[b] = r.trials;
+    if (a.du2) a.du2[b] = du2;
+    if (a.iters) a.iters[b] = a.iter;
+    if (!r.accepted) {
+      a.status[b] = (r.cost != r.cost) ? ILQR_TRAJ_NAN : ILQR_TRAJ_LS_EXHAUSTED;
+      if (a.res_parity) a.res_parity[b] = a.parity;
+    } else {
+      a.new_cost[b] = r.cost;
+      if (du2 <= ls.tol) {
+        a.status[b] = ILQR_TRAJ_CONVERGED;
+        if (a.res_parity) a.res_parity[b] = a.parity;
+      }
+    }
+  }
+}
+
+// forward pass + convergence test of the wave's trajectories b0 .. b0+3 on the MFMA form;
+// `run` masks the slots that run (bit β)
+__device__ __forceinline__ void iter_forward_wave_mfma(const LQParams& P, int b0, int B, int T,
+                                                       const IterArgs& a, const LSParams& ls,
+                                                       double* ring, unsigned run) {
+  const int l = threadIdx.x & 63;
+  const int beta = (l >> 2) & 3;
+  const int b = b0 + beta;
+  const bool active = b < B && ((run >> beta) & 1u);
+  double du2 = 0.0;
+  const double pc = (a.prev_cost && active) ? a.prev_cost[b] : INFINITY;
+  const FwdOut r = lq_forward_wave_mfma<PIPE_R, PIPE_PF>(P, b0, B, T, run, a.x, a.u, a.xtraj, a.d, a.K, pc,
+                                                         a.xnew, a.unew, &du2, ls, ring);
+  if (l < 16 && (l & 3) == 0 && active) {  // lane 4β: ρ = κ = 0 of slot β
     if (a.trials) a.trials[b] = r.trials;
     if (a.du2) a.du2[b] = du2;
     if (a.iters) a.iters[b] = a.iter;

@@ -57,7 +57,7 @@ hipError_t launch_lq_iter_backward4(const LQParams& p, int B, int T, const IterA
 // backward (four trajectories per wave) + LDS-ring forward of one fit iteration in one
 // launch, (12, 4) only; the same bits as the two launches
 hipError_t launch_lq_iter_fused4(const LQParams& p, int B, int T, const IterArgs& a, const LSParams& ls,
-                                 hipStream_t s);
+                                 hipStream_t s, bool mfma = false);
 hipError_t launch_lq_backward_v6(int nx, int nu, const LQParams& p, int B, int T, const double* x,
                                  const double* u, double* d, double* K, int32_t* status, double mu,
                                  hipStream_t s);
@@ -65,14 +65,14 @@ hipError_t launch_lq_forward(int nx, int nu, const LQParams& p, int B, int T, co
                              const double* u, const double* xtraj, const double* d,
                              const double* K, const double* prev_cost, double* xnew,
                              double* unew, double* new_cost, int32_t* trials, int32_t* status,
-                             const LSParams& ls, hipStream_t s, bool ring = false);
+                             const LSParams& ls, hipStream_t s, bool ring = false, bool mfma = false);
 // The two halves of one fit iteration over trajectories [b0, b1) (pointers in
 // `a` and `p` address the whole batch).
 hipError_t launch_lq_iter_backward(int nx, int nu, const LQParams& p, int b0, int b1, int T,
                                    const IterArgs& a, double mu, hipStream_t s, bool wave = false);
 hipError_t launch_lq_iter_forward(int nx, int nu, const LQParams& p, int b0, int b1, int T,
                                   const IterArgs& a, const LSParams& ls, hipStream_t s,
-                                  bool ring = false);
+                                  bool ring = false, bool mfma = false);
 // Pipelined fit iteration (DESIGN.md §fit driver): role-B workgroups run iteration
 // `cur` (backward then forward), role-A workgroups the forward of iteration `prev`
 // then the backward of `cur`; flags select the phases (PIPE_* below).

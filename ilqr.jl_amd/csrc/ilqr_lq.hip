@@ -800,7 +800,7 @@ __host__ __device__ __forceinline__ bool pipe_role_a(int g) { return (((g >> 8) 
 #define ILQR_FW_WAVES 4
 #endif
 constexpr int FW_WAVES = ILQR_FW_WAVES;
-template <int NX, int NU>
+template <int NX, int NU, bool MF = false>
 __global__ __launch_bounds__(64 * FW_WAVES) void lq_forward_ring_kernel(
     LQParams P, int B, int T, const double* __restrict__ x, const double* __restrict__ u,
     const double* __restrict__ xtraj, const double* __restrict__ d, const double* __restrict__ K,
@@ -812,12 +812,20 @@ __global__ __launch_bounds__(64 * FW_WAVES) void lq_forward_ring_kernel(
   double* ring = ring_all + w * (PIPE_R * RING_SLOT + RING_LAREA);
   const int b0 = (blockIdx.x * FW_WAVES + w) * 4;
   if (b0 >= B) return;
-  const int j = threadIdx.x & 15;
-  const int b = b0 + ((threadIdx.x & 63) >> 4);
+  // the row form: trajectory of lane l = l >> 4, index j = l & 15 within it; the MFMA
+  // form: trajectory (l >> 2) & 3, index 4ρ + κ
+  const int l = threadIdx.x & 63;
+  const int j = MF ? ((l >> 4) << 2) | (l & 3) : l & 15;
+  const int b = b0 + (MF ? (l >> 2) & 3 : l >> 4);
   const bool active = b < B;
   const double pc = (prev_cost && active) ? prev_cost[b] : INFINITY;
-  const FwdOut r = lq_forward_wave_ring<NX, NU, PIPE_R, PIPE_PF>(P, b0, B, T, active, x, u, xtraj, d,
-                                                                 K, pc, xnew, unew, nullptr, ls, ring);
+  FwdOut r;
+  if constexpr (MF)
+    r = lq_forward_wave_mfma<PIPE_R, PIPE_PF>(P, b0, B, T, 0xFu, x, u, xtraj, d, K, pc, xnew, unew, nullptr, ls,
+                                              ring);
+  else
+    r = lq_forward_wave_ring<NX, NU, PIPE_R, PIPE_PF>(P, b0, B, T, active, x, u, xtraj, d, K, pc, xnew, unew,
+                                                      nullptr, ls, ring);
   if (!active) return;
   if (!r.accepted) {
     for (int i = j; i < (T + 1) * NX; i += 16) xnew[(size_t)b * (T + 1) * NX + i] = x[(size_t)b * (T + 1) * NX + i];
@@ -832,14 +840,22 @@ __global__ __launch_bounds__(64 * FW_WAVES) void lq_forward_ring_kernel(
 }
 
 // Part 2 with the LDS-ring forward (one wave, four trajectories per workgroup).
-template <int NX, int NU>
+template <int NX, int NU, bool MF = false>
 __global__ __launch_bounds__(64 * FW_WAVES) void lq_iter_forward_ring_kernel(LQParams P, int B, int T,
                                                                             IterArgs a, LSParams ls) {
   __shared__ __attribute__((aligned(16))) double ring_all[FW_WAVES * (PIPE_R * RING_SLOT + RING_LAREA)];
   const int w = threadIdx.x >> 6;
   const int b0 = (blockIdx.x * FW_WAVES + w) * 4;
   if (b0 >= B) return;
-  iter_forward_wave<NX, NU>(P, b0, B, T, a, ls, ring_all + w * (PIPE_R * RING_SLOT + RING_LAREA));
+  double* ring = ring_all + w * (PIPE_R * RING_SLOT + RING_LAREA);
+  if constexpr (MF) {
+    unsigned run = 0;
+    for (int q = 0; q < 4; ++q)
+      if (b0 + q < B && a.status[b0 + q] == ILQR_TRAJ_OK) run |= 1u << q;
+    iter_forward_wave_mfma(P, b0, B, T, a, ls, ring, run);
+  } else {
+    iter_forward_wave<NX, NU>(P, b0, B, T, a, ls, ring);
+  }
 }
 
 template <int NX, int NU>
@@ -1008,10 +1024,12 @@ hipError_t launch_lq_forward(int nx, int nu, const LQParams& p, int B, int T, co
                              const double* u, const double* xtraj, const double* d,
                              const double* K, const double* prev_cost, double* xnew,
                              double* unew, double* new_cost, int32_t* trials, int32_t* status,
-                             const LSParams& ls, hipStream_t s, bool ring) {
+                             const LSParams& ls, hipStream_t s, bool ring, bool mfma) {
   const int grid = (B + 3) / 4;
   if (ring) {
     const int gridr = (B + 4 * FW_WAVES - 1) / (4 * FW_WAVES);
+    if (mfma)
+      ILQR_DISPATCH(12, 4, (lq_forward_ring_kernel<NX_, NU_, true><<<gridr, 64 * FW_WAVES, 0, s>>>(p, B, T, x, u, xtraj, d, K, prev_cost, xnew, unew, new_cost, trials, status, ls)));
     ILQR_DISPATCH(12, 4, (lq_forward_ring_kernel<NX_, NU_><<<gridr, 64 * FW_WAVES, 0, s>>>(p, B, T, x, u, xtraj, d, K, prev_cost, xnew, unew, new_cost, trials, status, ls)));
   }
   ILQR_DISPATCH(12, 4, (lq_forward_kernel<NX_, NU_><<<grid, 64, 0, s>>>(p, B, T, x, u, xtraj, d, K, prev_cost, xnew, unew, new_cost, trials, status, ls)));
@@ -1062,12 +1080,15 @@ hipError_t launch_lq_iter_backward(int nx, int nu, const LQParams& p, int b0, in
 }
 
 hipError_t launch_lq_iter_forward(int nx, int nu, const LQParams& p, int b0, int b1, int T,
-                                  const IterArgs& a, const LSParams& ls, hipStream_t s, bool ring) {
+                                  const IterArgs& a, const LSParams& ls, hipStream_t s, bool ring,
+                                  bool mfma) {
   const int B = b1 - b0;
   if (B <= 0) return hipSuccess;
   const LQParams ps = shift(p, nx, nu, b0);
   const IterArgs as = shift(a, nx, nu, T, b0);
   if (ring) {
+    if (mfma)
+      ILQR_DISPATCH(12, 4, (lq_iter_forward_ring_kernel<NX_, NU_, true><<<(B + 4 * FW_WAVES - 1) / (4 * FW_WAVES), 64 * FW_WAVES, 0, s>>>(ps, B, T, as, ls)));
     ILQR_DISPATCH(12, 4, (lq_iter_forward_ring_kernel<NX_, NU_><<<(B + 4 * FW_WAVES - 1) / (4 * FW_WAVES), 64 * FW_WAVES, 0, s>>>(ps, B, T, as, ls)));
   }
   ILQR_DISPATCH(12, 4, (lq_iter_forward_kernel<NX_, NU_><<<(B + 3) / 4, 64, 0, s>>>(ps, B, T, as, ls)));

@@ -34,6 +34,7 @@ SCHED_RING_FORWARD = 2
 SCHED_BACKWARD_WAVE = 4
 SCHED_BACKWARD_BLOCK = 8
 SCHED_FUSED = 16
+SCHED_FORWARD_MFMA = 32
 
 PROBLEM_LQ = 1
 PROBLEM_TWO_LINK = 2

@@ -81,18 +81,20 @@ class Solver:
         _lib.check(self.lib.ilqr_set_stream(self.h, C.c_void_p(s)), "ilqr_set_stream")
 
     def set_schedule(self, pipelined: bool = False, ring_forward: bool = True,
-                     backward: str = "auto", fused: bool = True):
+                     backward: str = "auto", fused: bool = True, forward_mfma: bool = False):
         """LQ launch schedule (ilqr_set_schedule). pipelined: fit overlaps half of the
         workgroups' forward passes with the other half's backward passes (implies
         backward="wave"); ring_forward: the forward pass streams its inputs HBM → LDS
         ahead of use; backward: "wave" one trajectory per wave (16x16x4 MFMA),
         "block" four per wave (4x4x4 4-block MFMA), "auto" block from 2048
         trajectories up; fused: iterate/fit run backward + forward as one kernel (with the
-        "block" backward and the ring forward). Schedules with the same backward kernel
-        return the same bits."""
+        "block" backward and the ring forward); forward_mfma: the ring forward's mat-vecs
+        on the 4-block f64 MFMA (other rounding). Schedules with the same backward kernel
+        and forward form return the same bits."""
         bk = {"auto": 0, "wave": _lib.SCHED_BACKWARD_WAVE, "block": _lib.SCHED_BACKWARD_BLOCK}[backward]
         flags = ((_lib.SCHED_PIPELINED if pipelined else 0) | (_lib.SCHED_RING_FORWARD if ring_forward else 0)
-                 | bk | (_lib.SCHED_FUSED if fused and not pipelined and backward != "wave" else 0))
+                 | bk | (_lib.SCHED_FUSED if fused and not pipelined and backward != "wave" else 0)
+                 | (_lib.SCHED_FORWARD_MFMA if forward_mfma else 0))
         _lib.check(self.lib.ilqr_set_schedule(self.h, flags), "ilqr_set_schedule")
 
     def set_problem(self, lq):

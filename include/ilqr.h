@@ -157,6 +157,10 @@ ilqr_status ilqr_sync(ilqr_handle* h);
  *                            then their ring forward pass (with the BLOCK backward and
  *                            the ring forward; ignored otherwise; not with WAVE or
  *                            PIPELINED). A new handle starts with RING_FORWARD | FUSED.
+ *   ILQR_SCHED_FORWARD_MFMA  the ring forward pass (and the fused kernel's) runs its
+ *                            mat-vecs on the 4-block f64 MFMA in the backward's layout
+ *                            instead of DPP row broadcasts: the same function, other
+ *                            rounding (agrees to 1e-12).
  * Schedules with the same backward kernel return the same bits; the two backward
  * kernels agree to rounding. Unknown bits, or BLOCK with WAVE or
  * PIPELINED → ILQR_ERR_BAD_ARG. */
@@ -165,6 +169,7 @@ ilqr_status ilqr_sync(ilqr_handle* h);
 #define ILQR_SCHED_BACKWARD_WAVE 4
 #define ILQR_SCHED_BACKWARD_BLOCK 8
 #define ILQR_SCHED_FUSED 16
+#define ILQR_SCHED_FORWARD_MFMA 32
 ilqr_status ilqr_set_schedule(ilqr_handle* h, int flags);
 
 /* iLQR.backward_pass (backward_pass.jl:324-357): gains d (batch,T,nu) and

@@ -57,10 +57,12 @@ def headline():
     s.close()
 
 
-def test_bench_step_iterations_vs_oracle(gpu, headline):
+@pytest.mark.parametrize("forward_mfma", [False, True])
+def test_bench_step_iterations_vs_oracle(gpu, headline, forward_mfma):
     """The chained iterations of the bench's fit, each against the oracle's; then two
-    more at the fp64 floor."""
+    more at the fp64 floor. Both forms of the forward (DPP rows, 4-block MFMA)."""
     s, lq, x, u, idx = headline
+    s.set_schedule(forward_mfma=forward_mfma)
     xi, ui = torch.from_numpy(x).cuda(), torch.from_numpy(u).cuda()
     xn, un = torch.empty_like(xi), torch.empty_like(ui)
     pc = torch.empty((4096,), dtype=torch.float64, device="cuda")
@@ -98,10 +100,12 @@ def test_bench_step_iterations_vs_oracle(gpu, headline):
         xi, xn, ui, un = xn, xi, un, ui
 
 
-def test_bench_fit_vs_oracle_fit(gpu, headline):
+@pytest.mark.parametrize("forward_mfma", [False, True])
+def test_bench_fit_vs_oracle_fit(gpu, headline, forward_mfma):
     """ilqr_fit(max_iter = 3, tol < 0) — the bench's timed call — against the
     restatement's fit on the sample: result, cost, iteration count, status."""
     s, lq, x, u, idx = headline
+    s.set_schedule(forward_mfma=forward_mfma)
     r = s.fit(torch.from_numpy(x).cuda(), torch.from_numpy(u).cuda(), max_iter=FIT_ITERS, tol=-1.0)
     assert r.call_status == _lib.OK
     xo, uo, co, it, st = cref.lq_fit(sub(lq, idx), x[idx], u[idx], max_iter=FIT_ITERS, tol=-1.0,

@@ -566,3 +566,70 @@ def test_fused_iteration_equals_two_launches(gpu, nb, T):
         outs.append((xi, ui, pc, st, tr, r.x, r.u, r.cost, r.iters, r.status))
     for a, b in zip(*outs):
         torch.testing.assert_close(a, b, rtol=0, atol=0, equal_nan=True)
+
+
+# -- the forward pass on the 4-block MFMA (ILQR_SCHED_FORWARD_MFMA) ---------------------------
+@pytest.mark.parametrize("name", LQ_FIXTURES)
+def test_forward_mfma_matches_golden(gpu, name):
+    """The MFMA form of the ring forward (ilqr_fwd_ring.h: lq_forward_wave_mfma) against
+    the oracle's forward_pass fixtures: the same tolerances as the DPP form."""
+    g = load(name)
+    s, _ = solver_for(g)
+    s.set_schedule(forward_mfma=True)
+    nb = g["A"].shape[0]
+    xt = dev(g["xtraj"]) if "xtraj" in g else None
+    pc = torch.full((nb,), float("inf"), dtype=torch.float64, device="cuda")
+    xn, un, c, tr, st = s.forward(dev(g["x"]), dev(g["u"]), dev(g["d"]), dev(g["K"]), pc, x_traj=xt)
+    assert (st.cpu().numpy() == 0).all()
+    assert rel(xn, g["fw_x"]) < TOL_ROLL and rel(un, g["fw_u"]) < TOL_ROLL
+    assert rel(c, g["fw_cost"]) < TOL_COST
+    assert np.array_equal(tr.cpu().numpy(), g["fw_trials"])
+
+
+@pytest.mark.parametrize("name", LQ_FIXTURES)
+def test_fit_mfma_matches_golden(gpu, name):
+    g = load(name)
+    meta = json.loads(str(g["meta"]))
+    s, _ = solver_for(g)
+    s.set_schedule(forward_mfma=True)
+    xt = dev(g["xtraj"]) if "xtraj" in g else None
+    r = s.fit(dev(g["x"]), dev(g["u"]), x_traj=xt, max_iter=meta["fit_max_iter"], tol=meta["tol"])
+    assert r.call_status == 0
+    assert np.array_equal(r.iters.cpu().numpy(), g["fit_iters"])
+    assert rel(r.u, g["fit_u"]) < 1e-8 and rel(r.x, g["fit_x"]) < 1e-8
+
+
+@pytest.mark.parametrize("nb,T", [(4096, 100), (37, 23)])
+def test_fused_mfma_equals_split_mfma(gpu, nb, T):
+    """With the MFMA forward, the fused iteration returns the split schedule's bits
+    (iterate and fit, a NaN trajectory sharing a wave with clean ones), and it agrees
+    with the DPP forward to rounding."""
+    lq, x, u = (quadrotor_batch(nb, T=T, seed0=0) if nb == 4096
+                else random_lq_batch(nb, 12, 4, T, seed=nb * 7 + T))
+    if nb != 4096:
+        x[nb // 2, 1, 3] = np.nan
+    s = Solver(12, 4, T, nb)
+    s.set_problem(lq)
+    outs = []
+    for fused, mfma in ((False, True), (True, True), (True, False)):
+        s.set_schedule(backward="block", fused=fused, forward_mfma=mfma)
+        xi, ui = dev(x), dev(u)
+        xn, un = torch.zeros_like(xi), torch.zeros_like(ui)
+        pc = torch.full((nb,), float("inf"), dtype=torch.float64, device="cuda")
+        st = torch.zeros((nb,), dtype=torch.int32, device="cuda")
+        tr = torch.zeros((nb,), dtype=torch.int32, device="cuda")
+        for _ in range(3):
+            s.iterate(xi, ui, xn, un, pc, st, trials=tr, options=_lib.default_options(tol=-1.0))
+            xi, xn, ui, un = xn, xi, un, ui
+        r = s.fit(dev(x), dev(u), max_iter=6, tol=1e-8)
+        torch.cuda.synchronize()
+        outs.append((xi, ui, pc, st, tr, r.x, r.u, r.cost, r.iters, r.status))
+    for a, b in zip(outs[0], outs[1]):
+        torch.testing.assert_close(a, b, rtol=0, atol=0, equal_nan=True)
+    ok = outs[1][3].cpu().numpy() == outs[2][3].cpu().numpy()
+    assert ok.all()
+    for a, b in zip(outs[1][:3], outs[2][:3]):  # x̄, ū, cost after three iterations
+        a, b = a.cpu().numpy(), b.cpu().numpy()
+        fin = np.isfinite(b)
+        assert np.array_equal(np.isfinite(a), fin)
+        assert np.abs(a[fin] - b[fin]).max() <= 1e-10 * max(np.abs(b[fin]).max(), 1e-300)

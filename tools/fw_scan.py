@@ -7,13 +7,15 @@ from ilqr_amd import _lib
 from ilqr_amd.problems import quadrotor_batch
 from ilqr_amd.solver import Solver, _ptr
 
-if len(sys.argv) > 1:  # an alternate build of libilqr_hip.so (tools/fw_alt.sh)
-    _lib._lib = _lib.load(sys.argv[1])
-    print("library:", sys.argv[1])
+MFMA = "mfma" in sys.argv[1:]  # the forward's MFMA form (ILQR_SCHED_FORWARD_MFMA)
+LIBS = [a for a in sys.argv[1:] if a.endswith(".so")]
+if LIBS:  # an alternate build of libilqr_hip.so (tools/fw_alt.sh)
+    _lib._lib = _lib.load(LIBS[0])
+    print("library:", LIBS[0])
 
 for B in (256, 1024, 2048, 4096, 8192):
     lq, x0, u0 = quadrotor_batch(B, T=100, seed0=0)
-    s = Solver(12, 4, 100, B); s.set_problem(lq); s._bind_stream()
+    s = Solver(12, 4, 100, B); s.set_problem(lq); s._bind_stream(); s.set_schedule(forward_mfma=MFMA)
     x, u = torch.from_numpy(x0).cuda(), torch.from_numpy(u0).cuda()
     d = torch.empty((B, 100, 4), dtype=torch.float64, device="cuda"); K = torch.empty((B, 100, 4, 12), dtype=torch.float64, device="cuda")
     o = _lib.default_options()
