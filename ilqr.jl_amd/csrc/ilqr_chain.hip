@@ -163,6 +163,10 @@ __device__ __forceinline__ F2 crecip(F2 x) {
 #ifndef ILQR_CHAIN_FD_PAIR
 #define ILQR_CHAIN_FD_PAIR 1
 #endif
+// the fp32 forward's fast step on packed joint pairs (chain_trig_rk4_fast2)
+#ifndef ILQR_CHAIN_F2_FAST
+#define ILQR_CHAIN_F2_FAST 1
+#endif
 
 template <class S> struct ValueOf { using type = S; };
 template <int N, class V> struct ValueOf<DualT<N, V>> { using type = V; };
@@ -703,6 +707,106 @@ __device__ __forceinline__ void chain_trig_rk4_fast(const ChainTrig<V>& P, const
   bad |= ((int)(hm > V(0.25)) | (int)(fabs(x[0]) > ReducedRange<V>::v) | (int)(fabs(x[1]) > ReducedRange<V>::v)) != 0;
 }
 
+// ---------------------------------------------------------------------------
+// The fp32 fast step with the two joints packed (v_pk_* arithmetic on (joint 1,
+// joint 2) pairs: the angle reductions and shifts, M's diagonal, g, M′q̇, the solve and
+// the RK4 glue), the configuration BASELINE config 5 runs. The same operations as
+// chain_trig_rk4_fast per component, so the same bits.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ F2 f2fma(F2 a, F2 b, F2 c) { return __builtin_elementwise_fma(a, b, c); }
+
+// sincosf_reduced on both components
+__device__ __forceinline__ void sincos2_reduced(F2 x, F2& s, F2& c) {
+  const F2 kx = x * 0.63661977236758134f;
+  const F2 k = F2{rintf(kx.x), rintf(kx.y)};
+  F2 r = f2fma(-k, F2(1.5703125f), x);
+  r = f2fma(-k, F2(4.837512969970703125e-4f), r);
+  r = f2fma(-k, F2(7.54978995489188216e-8f), r);
+  const F2 z = r * r;
+  F2 ps = f2fma(z, F2(-1.9515295891e-4f), F2(8.3321608736e-3f));
+  ps = f2fma(z, ps, F2(-1.6666654611e-1f));
+  const F2 sr = f2fma(r * z, ps, r);
+  F2 pc = f2fma(z, F2(2.443315711809948e-5f), F2(-1.388731625493765e-3f));
+  pc = f2fma(z, pc, F2(4.166664568298827e-2f));
+  const F2 cr = f2fma(z * z, pc, f2fma(F2(-0.5f), z, F2(1.0f)));
+  const int q0 = (int)k.x & 3, q1 = (int)k.y & 3;
+  const float a0 = (q0 & 1) ? cr.x : sr.x, b0 = (q0 & 1) ? sr.x : cr.x;
+  const float a1 = (q1 & 1) ? cr.y : sr.y, b1 = (q1 & 1) ? sr.y : cr.y;
+  s = F2{(q0 & 2) ? -a0 : a0, (q1 & 2) ? -a1 : a1};
+  c = F2{((q0 + 1) & 2) ? -b0 : b0, ((q1 + 1) & 2) ? -b1 : b1};
+}
+// sincos_shift_t (fp32) on both components
+__device__ __forceinline__ void sincos2_shift(F2 s0, F2 c0, F2 h, F2& s, F2& c) {
+  const F2 z = h * h;
+  const F2 sh = f2fma(h * z, f2fma(z, F2(1.0f / 120.0f), F2(-1.0f / 6.0f)), h);
+  const F2 ch = f2fma(z, f2fma(z, F2(1.0f / 24.0f), F2(-0.5f)), F2(1.0f));
+  s = f2fma(s0, ch, c0 * sh);
+  c = f2fma(c0, ch, -(s0 * sh));
+}
+
+// q̈ (both joints) from packed sin/cos (joint 1, joint 2), q̇ and u
+template <int NU>
+__device__ __forceinline__ F2 chain_qdd_trig2(const ChainTrig<float>& P, F2 sn, F2 cs, F2 w, const float (&u)[NU]) {
+  const float s2 = sn.y, c2 = cs.y;
+  const float C2 = c2 * c2 - s2 * s2, S2 = 2.0f * (s2 * c2);
+  // (M₀₀, M₁₁) packed, M₀₁ alone; dM/dq₂ likewise
+  const F2 md = F2{P.Mc[0][0], P.Mc[2][0]} +
+                (((F2{P.Mc[0][1], P.Mc[2][1]} * c2 + F2{P.Mc[0][2], P.Mc[2][2]} * s2) +
+                  F2{P.Mc[0][3], P.Mc[2][3]} * C2) + F2{P.Mc[0][4], P.Mc[2][4]} * S2);
+  const float m01 = P.Mc[1][0] + (((P.Mc[1][1] * c2 + P.Mc[1][2] * s2) + P.Mc[1][3] * C2) + P.Mc[1][4] * S2);
+  const F2 dmd = (F2{P.Mc[0][2], P.Mc[2][2]} * c2 - F2{P.Mc[0][1], P.Mc[2][1]} * s2) +
+                 2.0f * (F2{P.Mc[0][4], P.Mc[2][4]} * C2 - F2{P.Mc[0][3], P.Mc[2][3]} * S2);
+  const float dm01 = (P.Mc[1][2] * c2 - P.Mc[1][1] * s2) + 2.0f * (P.Mc[1][4] * C2 - P.Mc[1][3] * S2);
+  // g (both components): h_a = G[·][a][0] + G[·][a][1] cos q₂ + G[·][a][2] sin q₂
+  F2 h[3];
+#pragma unroll
+  for (int a = 0; a < 3; ++a)
+    h[a] = F2{P.Gc[0][a][0], P.Gc[1][a][0]} +
+           (F2{P.Gc[0][a][1], P.Gc[1][a][1]} * c2 + F2{P.Gc[0][a][2], P.Gc[1][a][2]} * s2);
+  const F2 g = h[0] + (h[1] * cs.x + h[2] * sn.x);
+  // M′q̇ = (dM₀₀ w₀ + dM₀₁ w₁, dM₀₁ w₀ + dM₁₁ w₁)
+  const F2 p = F2{dmd.x * w.x + dm01 * w.y, dm01 * w.x + dmd.y * w.y};
+  const float qq = w.x * p.x + w.y * p.y;
+  const float r0 = u[0] - (w.y * p.x + g.x);
+  float r1 = (w.y * p.y - 0.5f * qq) + g.y;
+  if constexpr (NU > 1) r1 = u[NU - 1] - r1;
+  else r1 = -r1;
+  const float det = md.x * md.y - m01 * m01;
+  const float id = crecip(det);
+  return F2{(md.y * r0 - m01 * r1) * id, (md.x * r1 - m01 * r0) * id};
+}
+
+template <int NU>
+__device__ __forceinline__ void chain_trig_rk4_fast2(const ChainTrig<float>& P, const float (&x)[4],
+                                                     const float (&u)[NU], float (&out)[4], bool& bad) {
+  const F2 q{x[0], x[1]}, w{x[2], x[3]};
+  const float dt = P.dt;
+  F2 s0, c0, sn, cs;
+  sincos2_reduced(q, s0, c0);
+  F2 a = chain_qdd_trig2<NU>(P, s0, c0, w, u);
+  const F2 k1p = dt * w, k1v = dt * a;
+  F2 y = w + 0.5f * k1v;
+  sincos2_shift(s0, c0, 0.5f * k1p, sn, cs);
+  a = chain_qdd_trig2<NU>(P, sn, cs, y, u);
+  const F2 k2p = dt * y, k2v = dt * a;
+  y = w + 0.5f * k2v;
+  sincos2_shift(s0, c0, 0.5f * k2p, sn, cs);
+  a = chain_qdd_trig2<NU>(P, sn, cs, y, u);
+  const F2 k3p = dt * y, k3v = dt * a;
+  y = w + k3v;
+  sincos2_shift(s0, c0, k3p, sn, cs);
+  a = chain_qdd_trig2<NU>(P, sn, cs, y, u);
+  const F2 k4p = dt * y, k4v = dt * a;
+  const float sixth = 1.0f / 6.0f;
+  const F2 op = q + sixth * (((k1p + 2.0f * k2p) + 2.0f * k3p) + k4p);
+  const F2 ov = w + sixth * (((k1v + 2.0f * k2v) + 2.0f * k3v) + k4v);
+  out[0] = op.x; out[1] = op.y; out[2] = ov.x; out[3] = ov.y;
+  const F2 m1 = __builtin_elementwise_max(__builtin_elementwise_abs(k1p), __builtin_elementwise_abs(k2p));
+  const F2 m2 = __builtin_elementwise_max(m1, 2.0f * __builtin_elementwise_abs(k3p));
+  const float hm = fmaxf(m2.x, m2.y);
+  bad |= ((int)(hm > 0.25f) | (int)(fabsf(x[0]) > 8192.0f) | (int)(fabsf(x[1]) > 8192.0f)) != 0;
+}
+
 // the chain's closed form as a model of the shared forward group (ilqr_fwd_group.h)
 template <class V_, int NU_>
 struct ChainTrigModel {
@@ -711,7 +815,11 @@ struct ChainTrigModel {
   static constexpr bool HAS_FAST = true;
   ChainTrig<V> P;
   __device__ __forceinline__ void rk4_fast(const V (&x)[4], const V (&u)[NU], V (&o)[4], bool& bad) const {
-    chain_trig_rk4_fast<NU>(P, x, u, o, bad);
+#if ILQR_CHAIN_F2_FAST
+    if constexpr (std::is_same_v<V, float>) chain_trig_rk4_fast2<NU>(P, x, u, o, bad);
+    else
+#endif
+      chain_trig_rk4_fast<NU>(P, x, u, o, bad);
   }
   __device__ __forceinline__ void rk4_robust(const V (&x)[4], const V (&u)[NU], V (&o)[4]) const;
   // ℓ(x̄ₖ − x_trajₖ, ūₖ) on the joints (forward_pass.jl:187-190; RBD_helper_functions.jl:85-99)
