@@ -710,8 +710,8 @@ __device__ __forceinline__ void chain_trig_rk4_fast(const ChainTrig<V>& P, const
 // ---------------------------------------------------------------------------
 // The fp32 fast step with the two joints packed (v_pk_* arithmetic on (joint 1,
 // joint 2) pairs: the angle reductions and shifts, M's diagonal, g, M′q̇, the solve and
-// the RK4 glue), the configuration BASELINE config 5 runs. The same operations as
-// chain_trig_rk4_fast per component, so the same bits.
+// the RK4 glue), the configuration BASELINE config 5 runs. The formulas of
+// chain_trig_rk4_fast per component (FMA contraction may place roundings differently).
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ F2 f2fma(F2 a, F2 b, F2 c) { return __builtin_elementwise_fma(a, b, c); }
 
