@@ -614,12 +614,87 @@ __device__ __forceinline__ void chain_xdot_cv(const ChainK<V, NJ>& P, const V (&
 // recursion (RBD_helper_functions.jl:61-66), ≈60 operations and two sin/cos instead
 // of the three Newton-Euler passes; the rounding differs.
 // ---------------------------------------------------------------------------
+// ---------------------------------------------------------------------------
+// cost_functions.jl's task-space final cost (src/cost_functions.jl:5-27, the device side
+// of ilqr_chain_set_simple_costs): ℓ_f(x) = w Σ_k (p_k(q) − t_k)² where p is the root-
+// frame position of a point fixed on one body. Through two revolute joints each
+// coordinate is bilinear in (1, cos q₁, sin q₁) ⊗ (1, cos q₂, sin q₂) (Rodrigues is
+// affine in cos, sin of each angle), so the handle stores the coefficients, sampled from
+// the kinematics on the 3×3 grid like g's. The reference's reading takes the point's z
+// for every k (work_space_traj[end] .- transpose(final_target), :21): the handle then
+// stores z's coefficients in all three rows. Lives in device memory (one pointer in the
+// kernel arguments; read only when the cost mode is set).
+// ---------------------------------------------------------------------------
+struct ChainTask {
+  double Pc[3][3][3];  // p_k = Σ_ab Pc[k][a][b] φ_a(q₁) φ_b(q₂), φ = (1, cos, sin)
+  double t[3];         // final_target
+  double w;            // weight
+};
+
+// ℓ_f(q) in V (the forward's final cost, forward_pass.jl:192); the sum runs in the
+// reference's order: weight · ((e₁² + e₂²) + e₃²) (cost_functions.jl:21-23)
+template <class V>
+__device__ __forceinline__ V chain_task_cost(const ChainTask* __restrict__ C, V q0, V q1) {
+  V s0, c0, s1, c1;
+  vsincos(q0, s0, c0);
+  vsincos(q1, s1, c1);
+  V acc = V(0);
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    V h[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+      h[a] = (V)C->Pc[k][a][0] + ((V)C->Pc[k][a][1] * c1 + (V)C->Pc[k][a][2] * s1);
+    const V e = (h[0] + (h[1] * c0 + h[2] * s0)) - (V)C->t[k];
+    acc = acc + e * e;
+  }
+  return (V)C->w * acc;
+}
+
+// ∇ℓ_f and ∇²ℓ_f on (q₁, q₂) in f64 (final_cost_quadratization, backward_pass.jl:134-153):
+// 2w Σ_k e_k ∇p_k and 2w Σ_k (∇p_k ∇p_kᵀ + e_k ∇²p_k), e_k = p_k − t_k. H = (H₁₁, H₁₂, H₂₂).
+__device__ __forceinline__ void chain_task_quad(const ChainTask* __restrict__ C, double q0, double q1,
+                                                double (&g)[2], double (&H)[3]) {
+  double s0, c0, s1, c1;
+  vsincos(q0, s0, c0);
+  vsincos(q1, s1, c1);
+  g[0] = g[1] = H[0] = H[1] = H[2] = 0.0;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    double h[3], hd[3], hdd[3];  // φ(q₂), φ′(q₂), φ″(q₂) contracted with the q₂ index
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      const double* r = C->Pc[k][a];
+      h[a] = r[0] + (r[1] * c1 + r[2] * s1);
+      hd[a] = r[2] * c1 - r[1] * s1;
+      hdd[a] = -(r[1] * c1 + r[2] * s1);
+    }
+    const double p = h[0] + (h[1] * c0 + h[2] * s0);
+    const double p0 = h[2] * c0 - h[1] * s0, p1 = hd[0] + (hd[1] * c0 + hd[2] * s0);
+    const double p00 = -(h[1] * c0 + h[2] * s0), p01 = hd[2] * c0 - hd[1] * s0;
+    const double p11 = hdd[0] + (hdd[1] * c0 + hdd[2] * s0);
+    const double e = p - C->t[k];
+    g[0] += e * p0;
+    g[1] += e * p1;
+    H[0] += p0 * p0 + e * p00;
+    H[1] += p0 * p1 + e * p01;
+    H[2] += p1 * p1 + e * p11;
+  }
+  const double w2 = 2.0 * C->w;
+  g[0] *= w2;
+  g[1] *= w2;
+  H[0] *= w2;
+  H[1] *= w2;
+  H[2] *= w2;
+}
+
 template <class V>
 struct ChainTrig {
   V Mc[3][5];     // M₀₀, M₀₁, M₁₁: a₀ + a₁ cos q₂ + b₁ sin q₂ + a₂ cos 2q₂ + b₂ sin 2q₂
   V Gc[2][3][3];  // g_i = Σ_ab Gc[i][a][b] φ_a(q₁) φ_b(q₂), φ = (1, cos, sin)
   V dt;
   V tgt[2], qw[2], rw[2], qfw[2];  // joint-space cost (as ChainK)
+  const ChainTask* task;           // the task-space final cost in place of qfw's, or null
 };
 
 // q̈ from sin/cos of both joint angles, q̇ = (w0, w1) and u
@@ -836,6 +911,7 @@ struct ChainTrigModel {
   }
   // final_cost(x̄_N) on the raw state (:192; RBD_helper_functions.jl:105-116)
   __device__ __forceinline__ V final_cost(const V (&xb)[4]) const {
+    if (P.task) return chain_task_cost<V>(P.task, xb[0], xb[1]);  // cost_functions.jl:16-24
     V lf = V(0);
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -1400,7 +1476,7 @@ template <class V, int NU>
 __device__ unsigned chain_backward4_wave(const ChainK<V, 2>& P, int b0, int B, unsigned active, int T,
                                          const V* __restrict__ x, const V* __restrict__ J,
                                          V* __restrict__ dg, V* __restrict__ Kg, double mu,
-                                         double* lds) {
+                                         double* lds, const ChainTask* task) {
   constexpr int NJ = 2, NX = 4, ND = NX + NU, NR = Rec<NJ, NU>::N, NJAC = Rec<NJ, NU>::NJAC;
   constexpr uint32_t DEAD = 0x80000000u, W = sizeof(V);
   b0 = __builtin_amdgcn_readfirstlane(b0);
@@ -1419,6 +1495,14 @@ __device__ unsigned chain_backward4_wave(const ChainK<V, 2>& P, int b0, int B, u
   double S = (rho == kap && rj) ? qfw2 : 0.0;
   const double xT = (double)x[((size_t)bc * (T + 1) + T) * NX + jr];
   double s = rj ? -qfw2 * (tg - xT) : 0.0;
+  if (task) {  // the task-space final cost (cost_functions.jl:16-24): ∇ℓ_f, ∇²ℓ_f on the q rows
+    const size_t o = ((size_t)bc * (T + 1) + T) * NX;
+    double g[2], H[3];
+    chain_task_quad(task, (double)x[o], (double)x[o + 1], g, H);
+    const double h0 = jr == 0 ? H[0] : H[1], h1 = jr == 0 ? H[1] : H[2];
+    S = (rj && kap < NJ) ? (kap == 0 ? h0 : h1) : 0.0;
+    s = rj ? (jr == 0 ? g[0] : g[1]) : 0.0;
+  }
 
   const auto rJ = buffer_rsrc(const_cast<V*>(J) + (size_t)b0 * T * NR, (uint32_t)(nslot * T * NR * W));
   const uint32_t base = (uint32_t)(beta * T * NR * W);
@@ -1542,12 +1626,13 @@ __global__ __launch_bounds__(256) void chain_backward4_kernel(ChainK<V, 2> P, in
                                                               const V* __restrict__ x,
                                                               const V* __restrict__ J,
                                                               V* __restrict__ d, V* __restrict__ K,
-                                                              int32_t* __restrict__ status, V mu) {
+                                                              int32_t* __restrict__ status, V mu,
+                                                              const ChainTask* task) {
   __shared__ double lds[4 * 64];
   const int w = threadIdx.x >> 6;
   const int b0 = (blockIdx.x * 4 + w) * 4;
   if (b0 >= B) return;
-  const unsigned nan = chain_backward4_wave<V, NU>(P, b0, B, 0xFu, T, x, J, d, K, (double)mu, lds + w * 64);
+  const unsigned nan = chain_backward4_wave<V, NU>(P, b0, B, 0xFu, T, x, J, d, K, (double)mu, lds + w * 64, task);
   const int l = threadIdx.x & 63;
   if (status && l < 4 && b0 + l < B) status[b0 + l] = ((nan >> l) & 1u) ? ILQR_TRAJ_NAN : ILQR_TRAJ_OK;
 }
@@ -1595,7 +1680,8 @@ __global__ __launch_bounds__(CH_WG) void chain_iter_backward_kernel(ChainK<V, NJ
 // computed on and never stored
 template <class V, int NU>
 __global__ __launch_bounds__(256) void chain_iter_backward4_kernel(ChainK<V, 2> P, int B, int T,
-                                                                   ChainIter<V> a, const V* J, V mu) {
+                                                                   ChainIter<V> a, const V* J, V mu,
+                                                                   const ChainTask* task) {
   __shared__ double lds[4 * 64];
   const int w = threadIdx.x >> 6;
   const int b0 = (blockIdx.x * 4 + w) * 4;
@@ -1605,7 +1691,8 @@ __global__ __launch_bounds__(256) void chain_iter_backward4_kernel(ChainK<V, 2> 
     if (b0 + q < B && a.status[b0 + q] == ILQR_TRAJ_OK) active |= 1u << q;
   if (active == 0) return;
   const unsigned nan =
-      chain_backward4_wave<V, NU>(P, b0, B, active, T, a.x, J, a.d, a.K, (double)mu, lds + w * 64) & active;
+      chain_backward4_wave<V, NU>(P, b0, B, active, T, a.x, J, a.d, a.K, (double)mu, lds + w * 64, task) &
+      active;
   const int l = threadIdx.x & 63;
   if (l < 4 && ((nan >> l) & 1u)) {
     a.status[b0 + l] = ILQR_TRAJ_NAN;  // reference: AssertionError at backward_pass.jl:353
@@ -1807,6 +1894,13 @@ struct ilqr_chain_handle {
   double trig_err = 0.0;  // the check's max relative error
   ilqr::ChainTrig<double> trig{};
   bool use_trig() const { return trig_ok && dyn_mode != ILQR_CHAIN_DYN_RNEA; }
+  // cost_functions.jl's factories (ilqr_chain_set_simple_costs): the mode, the chain's
+  // joint-space weights as created (restored by ILQR_CHAIN_COST_JOINT) and the
+  // task-space final cost's coefficients in device memory
+  int32_t cost_mode = ILQR_CHAIN_COST_JOINT;
+  ilqr_chain created{};
+  ilqr::ChainTask* task_dev = nullptr;
+  const ilqr::ChainTask* task() const { return cost_mode == ILQR_CHAIN_COST_JOINT ? nullptr : task_dev; }
 };
 
 namespace {
@@ -1886,6 +1980,7 @@ ilqr::ChainTrig<V> trig_consts(const ilqr_chain_handle* h) {
     Q.qfw[i] = (V)c.qf_weight[i];
   }
   Q.dt = (V)c.dt;
+  Q.task = h->task();
   return Q;
 }
 
@@ -1952,6 +2047,80 @@ hipError_t chain_trig_build(ilqr_chain_handle* h) {
   return hipSuccess;
 }
 
+// transform_to_root(state, body) * point (RigidBodyDynamics.jl; cost_functions.jl:20): the
+// root-frame position of a point given in body `body`'s frame (−1 = the fixed base) at
+// joint angles q, composing x_parent = p_i + R0_i·Rot(a_i, q_i)·x_child down the chain (fp64)
+void chain_point_position(const ilqr_chain& c, int body, const double pt[3], const double* q,
+                          double out[3]) {
+  double w[3] = {pt[0], pt[1], pt[2]};
+  for (int i = body; i >= 0; --i) {
+    const double* a = c.axis[i];
+    const double cq = std::cos(q[i]), sq = std::sin(q[i]);
+    const double adw = a[0] * w[0] + a[1] * w[1] + a[2] * w[2];
+    const double axw[3] = {a[1] * w[2] - a[2] * w[1], a[2] * w[0] - a[0] * w[2], a[0] * w[1] - a[1] * w[0]};
+    double r[3];
+    for (int k = 0; k < 3; ++k) r[k] = cq * w[k] + sq * axw[k] + (1.0 - cq) * adw * a[k];
+    for (int k = 0; k < 3; ++k)
+      w[k] = c.joint_pos[i][k] +
+             (c.joint_rot[i][3 * k] * r[0] + c.joint_rot[i][3 * k + 1] * r[1] + c.joint_rot[i][3 * k + 2] * r[2]);
+  }
+  for (int k = 0; k < 3; ++k) out[k] = w[k];
+}
+
+// The task cost's coefficients: p sampled on the 3×3 grid of (q₁, q₂) and transformed
+// like g's (exact for the bilinear form), then checked against the kinematics at 64
+// pseudo-random angles. Returns the check's max deviation relative to the point's reach.
+double chain_task_build(const ilqr_chain& c, int body, const double pt[3], const double tgt[3],
+                        double weight, bool literal, ilqr::ChainTask& C) {
+  const double two_pi = 6.283185307179586476925286766559;
+  double smp[3][3][3];  // [ka][kb][coordinate]
+  for (int ka = 0; ka < 3; ++ka)
+    for (int kb = 0; kb < 3; ++kb) {
+      const double q[2] = {two_pi * ka / 3.0, two_pi * kb / 3.0};
+      chain_point_position(c, body, pt, q, smp[ka][kb]);
+    }
+  double P[3][3][3];
+  for (int k = 0; k < 3; ++k)
+    for (int a = 0; a < 3; ++a)
+      for (int b = 0; b < 3; ++b) {
+        double acc = 0.0;
+        for (int ka = 0; ka < 3; ++ka)
+          for (int kb = 0; kb < 3; ++kb) {
+            const double ta = two_pi * ka / 3.0, tb = two_pi * kb / 3.0;
+            const double fa = a == 0 ? 1.0 / 3 : (a == 1 ? 2.0 / 3 * std::cos(ta) : 2.0 / 3 * std::sin(ta));
+            const double fb = b == 0 ? 1.0 / 3 : (b == 1 ? 2.0 / 3 * std::cos(tb) : 2.0 / 3 * std::sin(tb));
+            acc += smp[ka][kb][k] * fa * fb;
+          }
+        P[k][a][b] = acc;
+      }
+  for (int k = 0; k < 3; ++k)
+    for (int a = 0; a < 3; ++a)
+      for (int b = 0; b < 3; ++b) C.Pc[k][a][b] = P[literal ? 2 : k][a][b];
+  for (int k = 0; k < 3; ++k) C.t[k] = tgt[k];
+  C.w = weight;
+  double err = 0.0, reach = 1.0;
+  uint64_t st = 0x9E3779B97F4A7C15ull;
+  for (int n = 0; n < 64; ++n) {
+    double q[2];
+    for (double& v : q) {
+      st = st * 6364136223846793005ull + 1442695040888963407ull;
+      v = ((double)(st >> 11) * (1.0 / 9007199254740992.0) - 0.5) * 4.0 * two_pi;
+    }
+    double ref[3];
+    chain_point_position(c, body, pt, q, ref);
+    const double c0 = std::cos(q[0]), s0 = std::sin(q[0]), c1 = std::cos(q[1]), s1 = std::sin(q[1]);
+    const double f0[3] = {1.0, c0, s0}, f1[3] = {1.0, c1, s1};
+    for (int k = 0; k < 3; ++k) {
+      double v = 0.0;
+      for (int a = 0; a < 3; ++a)
+        for (int b = 0; b < 3; ++b) v += P[k][a][b] * f0[a] * f1[b];
+      err = std::max(err, std::fabs(v - ref[k]));
+      reach = std::max(reach, std::fabs(ref[k]));
+    }
+  }
+  return err / reach;
+}
+
 ilqr::LSParams chain_ls(const ilqr_options* o) {
   ilqr_options def;
   ilqr_default_options(&def);
@@ -2014,7 +2183,7 @@ struct ChainOps {
     const auto P = chain_consts<V, NJ>(h->chain);
     if constexpr (NJ == 2) {  // four trajectories per wave on the f64 MFMA
       ilqr::chain_backward4_kernel<V, NU><<<(h->batch + 15) / 16, 256, 0, h->stream>>>(
-          P, h->batch, h->T, x, (const V*)h->J, d, K, st, (V)mu);
+          P, h->batch, h->T, x, (const V*)h->J, d, K, st, (V)mu, h->task());
       return hipGetLastError();
     }
     ilqr::chain_backward_kernel<V, NJ, NU><<<(h->batch + ilqr::CH_WG - 1) / ilqr::CH_WG, ilqr::CH_WG,
@@ -2051,7 +2220,8 @@ struct ChainOps {
     const auto P = chain_consts<V, NJ>(h->chain);
     if constexpr (NJ == 2) {
       ilqr::chain_iter_backward4_kernel<V, NU>
-          <<<(h->batch + 15) / 16, 256, 0, h->stream>>>(P, h->batch, h->T, a, (const V*)h->J, (V)ls.mu);
+          <<<(h->batch + 15) / 16, 256, 0, h->stream>>>(P, h->batch, h->T, a, (const V*)h->J, (V)ls.mu,
+                                                         h->task());
     } else {
       const int g = (h->batch + ilqr::CH_WG - 1) / ilqr::CH_WG;
       ilqr::chain_iter_backward_kernel<V, NJ, NU>
@@ -2208,6 +2378,7 @@ ilqr_status ilqr_chain_create(ilqr_chain_handle** out, int device, const ilqr_ch
   h->dtype = dtype;
   h->lin = linearization;
   h->chain = *chain;
+  h->created = *chain;
   const size_t w = vsize(h), B = (size_t)batch, nx = 2 * (size_t)h->nj, nu = (size_t)h->nu;
   hipError_t e = hipSuccess;
   if (iter_supported(h->nj, h->nu)) {  // dynamics-only shapes need no workspace
@@ -2242,9 +2413,59 @@ ilqr_status ilqr_chain_set_dynamics(ilqr_chain_handle* h, int32_t mode) {
   if (mode != ILQR_CHAIN_DYN_AUTO && mode != ILQR_CHAIN_DYN_RNEA && mode != ILQR_CHAIN_DYN_CLOSED_FORM)
     return ILQR_ERR_BAD_ARG;
   if (mode == ILQR_CHAIN_DYN_CLOSED_FORM && !h->trig_ok) return ILQR_ERR_UNSUPPORTED;
+  // the task-space final cost is evaluated by the closed-form forward only
+  if (mode == ILQR_CHAIN_DYN_RNEA && h->cost_mode != ILQR_CHAIN_COST_JOINT) return ILQR_ERR_UNSUPPORTED;
   h->dyn_mode = mode;
   return ILQR_OK;
 }
+
+ilqr_status ilqr_chain_set_simple_costs(ilqr_chain_handle* h, int32_t mode, int32_t body,
+                                        const double* point, const double* final_target,
+                                        double weight) {
+  if (!h) return ILQR_ERR_BAD_ARG;
+  if (mode != ILQR_CHAIN_COST_JOINT && mode != ILQR_CHAIN_COST_SIMPLE &&
+      mode != ILQR_CHAIN_COST_SIMPLE_EUCLIDEAN)
+    return ILQR_ERR_BAD_ARG;
+  if (mode == ILQR_CHAIN_COST_JOINT) {  // the joint-space costs the handle was created with
+    if (h->cost_mode != ILQR_CHAIN_COST_JOINT) {
+      CH_TRY(hipStreamSynchronize(h->stream));  // launches in flight still read the old cost
+      h->chain = h->created;
+      h->cost_mode = ILQR_CHAIN_COST_JOINT;
+    }
+    return ILQR_OK;
+  }
+  if (!point || !final_target || !std::isfinite(weight)) return ILQR_ERR_BAD_ARG;
+  if (body < -1 || body >= h->nj) return ILQR_ERR_BAD_ARG;
+  for (int k = 0; k < 3; ++k)
+    if (!std::isfinite(point[k]) || !std::isfinite(final_target[k])) return ILQR_ERR_BAD_ARG;
+  if (!iter_supported(h->nj, h->nu) || !h->use_trig()) {
+    g_chain_error = "ilqr_chain_set_simple_costs: needs a 2-joint chain on the closed-form dynamics";
+    return ILQR_ERR_UNSUPPORTED;
+  }
+  ilqr::ChainTask C{};
+  const double err =
+      chain_task_build(h->created, body, point, final_target, weight, mode == ILQR_CHAIN_COST_SIMPLE, C);
+  if (!(err < 1e-12)) {
+    g_chain_error = "ilqr_chain_set_simple_costs: the point's coordinates are not bilinear in "
+                    "(cos, sin) of the joint angles (kinematics check failed)";
+    return ILQR_ERR_UNSUPPORTED;
+  }
+  CH_TRY(hipSetDevice(h->device));
+  CH_TRY(hipStreamSynchronize(h->stream));
+  if (!h->task_dev) CH_TRY(hipMalloc(&h->task_dev, sizeof(ilqr::ChainTask)));
+  CH_TRY(hipMemcpy(h->task_dev, &C, sizeof(C), hipMemcpyHostToDevice));
+  // simple_immediate_cost = Σ uᵢ² (cost_functions.jl:45-51): q_weight 0, r_weight 1
+  h->chain = h->created;
+  for (int i = 0; i < ILQR_CHAIN_MAX_JOINTS; ++i) {
+    h->chain.q_weight[i] = 0.0;
+    h->chain.r_weight[i] = 1.0;
+    h->chain.qf_weight[i] = 0.0;
+  }
+  h->cost_mode = mode;
+  return ILQR_OK;
+}
+
+int32_t ilqr_chain_get_cost_mode(const ilqr_chain_handle* h) { return h ? h->cost_mode : -1; }
 
 int32_t ilqr_chain_get_dynamics(const ilqr_chain_handle* h) {
   if (!h) return -1;
@@ -2262,6 +2483,7 @@ ilqr_status ilqr_chain_destroy(ilqr_chain_handle* h) {
   }
   for (void* p : {h->K, h->d, h->J, h->prev_cost, h->du2}) (void)hipFree(p);
   for (int32_t* p : {h->trials, h->status, h->res_parity, h->iters}) (void)hipFree(p);
+  (void)hipFree(h->task_dev);
   delete h;
   return ILQR_OK;
 }

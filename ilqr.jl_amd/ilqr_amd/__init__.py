@@ -10,7 +10,7 @@ __all__ = ["LinearDynamics", "QuadraticCost", "QuadraticFinalCost", "LQBatch",
            "TwoLinkFinalCost", "two_link_closures", "two_link_initial_states", "quadrotor_batch", "quadrotor_instance", "random_lq_batch",
            "fit", "backward_pass", "forward_pass", "Solver", "selftest", "LineSearchExhausted",
            "ChainSolver", "ChainProblem", "rbd_2dof_problem", "chain_closures", "load_robot",
-           "rbd_initial_states"]
+           "rbd_initial_states", "simple_final_cost", "simple_immediate_cost"]
 
 
 def __getattr__(name):
@@ -23,6 +23,9 @@ def __getattr__(name):
                 "rbd_initial_states"):
         from . import chain
         return getattr(chain, name)
+    if name in ("simple_final_cost", "simple_immediate_cost"):
+        from . import cost_functions
+        return getattr(cost_functions, name)
     if name in ("Solver", "selftest", "FitResult"):
         from . import solver
         return getattr(solver, name)

@@ -49,6 +49,9 @@ LINEARIZE_CENTRAL_FD = 1
 CHAIN_DYN_AUTO = 0          # ilqr_chain_dynamics_mode
 CHAIN_DYN_RNEA = 1
 CHAIN_DYN_CLOSED_FORM = 2
+CHAIN_COST_JOINT = 0            # ilqr_chain_cost_mode (cost_functions.jl's factories)
+CHAIN_COST_SIMPLE = 1
+CHAIN_COST_SIMPLE_EUCLIDEAN = 2
 CHAIN_MAX_JOINTS = 8
 
 
@@ -118,6 +121,9 @@ SIGNATURES = {
     "ilqr_chain_set_dynamics": (C.c_int, [P, C.c_int32]),
     "ilqr_chain_get_dynamics": (C.c_int32, [P]),
     "ilqr_chain_closed_form_error": (C.c_double, [P]),
+    "ilqr_chain_set_simple_costs": (C.c_int, [P, C.c_int32, C.c_int32, C.POINTER(C.c_double),
+                                              C.POINTER(C.c_double), C.c_double]),
+    "ilqr_chain_get_cost_mode": (C.c_int32, [P]),
     "ilqr_chain_sync": (C.c_int, [P]),
     "ilqr_chain_dynamics": (C.c_int, [P, P, P, P, C.c_int]),
     "ilqr_chain_linearize": (C.c_int, [P, P, P, P, P]),

@@ -36,6 +36,7 @@ import torch
 from . import _lib
 from . import tiles as _tiles
 from .chain import ChainSolver, chain_problem_of
+from .cost_functions import simple_costs_of
 from .problems import (LinearDynamics, QuadraticCost, QuadraticFinalCost, is_two_link,
                        lq_from_closures)
 from .solver import Solver
@@ -97,7 +98,15 @@ def _chain_solver(xb, ub, dynamicsf, immediate_cost, final_cost, dtype):
     p = chain_problem_of(dynamicsf, immediate_cost, final_cost)
     if (p.nx, p.nu) != (nx, nu):
         raise AssertionError(f"problem is ({p.nx}, {p.nu}) but x/u are ({nx}, {nu})")
-    return ChainSolver(p, M, nb, dtype=dtype, device=_device())
+    s = ChainSolver(p, M, nb, dtype=dtype, device=_device())
+    fc = simple_costs_of(p, immediate_cost, final_cost)   # cost_functions.jl's factories
+    if fc is not None:
+        try:
+            s.set_simple_costs(fc.body, fc.point, fc.final_target, fc.weight, fc.euclidean)
+        except Exception:
+            s.close()
+            raise
+    return s
 
 
 def _tiles_solver(xb, ub):

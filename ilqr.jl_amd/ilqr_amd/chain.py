@@ -177,6 +177,30 @@ class ChainSolver:
         """Max relative deviation of the closed form from the recursion at creation."""
         return float(self.lib.ilqr_chain_closed_form_error(self.h))
 
+    def set_simple_costs(self, body, point, final_target, weight, euclidean: bool = False):
+        """cost_functions.jl's simple_immediate_cost / simple_final_cost in place of the
+        problem's joint-space costs (ilqr_chain_set_simple_costs): ℓ = Σ uᵢ² and
+        ℓ_f = weight·Σₖ (p_z − final_targetₖ)² for the point `point` of body `body`
+        (0-based link index or the name of the joint that moves it; −1 = the base), or
+        the squared distance Σₖ (pₖ − final_targetₖ)² with euclidean=True."""
+        b = body_index(self.p.chain, body)
+        pt = (C.c_double * 3)(*[float(v) for v in np.asarray(point, float).reshape(3)])
+        tg = (C.c_double * 3)(*[float(v) for v in np.asarray(final_target, float).reshape(3)])
+        mode = _lib.CHAIN_COST_SIMPLE_EUCLIDEAN if euclidean else _lib.CHAIN_COST_SIMPLE
+        _lib.check(self.lib.ilqr_chain_set_simple_costs(self.h, mode, b, pt, tg, float(weight)),
+                   "ilqr_chain_set_simple_costs")
+
+    def set_joint_costs(self):
+        """Back to the ChainProblem's joint-space costs."""
+        _lib.check(self.lib.ilqr_chain_set_simple_costs(self.h, _lib.CHAIN_COST_JOINT, 0, None, None, 0.0),
+                   "ilqr_chain_set_simple_costs")
+
+    @property
+    def cost_mode(self) -> str:
+        return {_lib.CHAIN_COST_JOINT: "joint", _lib.CHAIN_COST_SIMPLE: "simple",
+                _lib.CHAIN_COST_SIMPLE_EUCLIDEAN: "simple_euclidean"}[
+            int(self.lib.ilqr_chain_get_cost_mode(self.h))]
+
     def close(self):
         if getattr(self, "h", None):
             self.lib.ilqr_chain_destroy(self.h)
@@ -337,10 +361,30 @@ def chain_closures(problem: ChainProblem):
     return ChainDynamics(problem), ChainCost(problem), ChainFinalCost(problem)
 
 
+def body_index(chain: Chain, body) -> int:
+    """A body of the chain as ilqr_chain_set_simple_costs numbers it: the link joint i
+    moves is body i (RigidBodyDynamics' successor of joint i), −1 the fixed base. Takes
+    the index or the joint's name."""
+    if isinstance(body, str):
+        if body not in chain.names:
+            raise ValueError(f"no joint named {body!r} (joints: {chain.names})")
+        return chain.names.index(body)
+    b = int(body)
+    if not -1 <= b < chain.n:
+        raise ValueError(f"body {b} outside -1..{chain.n - 1}")
+    return b
+
+
 def chain_problem_of(dynamicsf, immediate_cost, final_cost):
-    """The ChainProblem behind a recognised closure triple, else None."""
-    if (isinstance(dynamicsf, ChainDynamics) and isinstance(immediate_cost, ChainCost)
-            and isinstance(final_cost, ChainFinalCost)
-            and dynamicsf.problem is immediate_cost.problem is final_cost.problem):
-        return dynamicsf.problem
+    """The ChainProblem behind a recognised closure triple, else None: the problem's own
+    joint-space costs, or cost_functions.jl's simple costs on the problem's chain."""
+    if not isinstance(dynamicsf, ChainDynamics):
+        return None
+    p = dynamicsf.problem
+    if (isinstance(immediate_cost, ChainCost) and isinstance(final_cost, ChainFinalCost)
+            and p is immediate_cost.problem is final_cost.problem):
+        return p
+    from .cost_functions import simple_costs_of
+    if simple_costs_of(p, immediate_cost, final_cost) is not None:
+        return p
     return None

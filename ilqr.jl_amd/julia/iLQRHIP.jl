@@ -429,6 +429,20 @@ end
 const ILQR_CHAIN_DYN_AUTO = Int32(0)         # ilqr_chain_set_dynamics (include/ilqr.h)
 const ILQR_CHAIN_DYN_RNEA = Int32(1)
 const ILQR_CHAIN_DYN_CLOSED_FORM = Int32(2)
+const ILQR_CHAIN_COST_JOINT = Int32(0)       # ilqr_chain_set_simple_costs (include/ilqr.h)
+const ILQR_CHAIN_COST_SIMPLE = Int32(1)
+const ILQR_CHAIN_COST_SIMPLE_EUCLIDEAN = Int32(2)
+
+"""The pair simple_immediate_cost / simple_final_cost(mechanism, body, point,
+final_target, weight) of src/cost_functions.jl on the chain's handle: Σuᵢ² and
+weight·Σₖ(p_z − final_targetₖ)² for `point` in the frame of `body` (the link joint
+`body` moves, 0-based; −1 the base); euclidean = true takes Σₖ(pₖ − final_targetₖ)²."""
+struct SimpleCosts
+    body::Int32; point::NTuple{3,Float64}; final_target::NTuple{3,Float64}; weight::Float64
+    euclidean::Bool
+end
+simple_costs(body, point, final_target, weight; euclidean::Bool=false) =
+    SimpleCosts(Int32(body), Tuple(Float64.(point)), Tuple(Float64.(final_target)), Float64(weight), euclidean)
 
 """chain_fit(chain, x_init, u_init; max_iter, tol, linearization, dynamics) → (x̄, ū, status)
 
@@ -436,10 +450,12 @@ Batched fit of the chain family; x_init (nx, T+1, batch), u_init (nu, T, batch) 
 Array{Float32,3} (fp32, BASELINE config 5) or Array{Float64,3}: the element type picks
 the device precision, as the reference's generic Julia code would. `dynamics` picks the
 2-joint evaluator (AUTO: the closed form sampled from the Newton-Euler recursion at
-creation; RNEA: the recursion itself)."""
+creation; RNEA: the recursion itself). `costs = simple_costs(…)` replaces the chain's
+joint-space costs with cost_functions.jl's pair (2-joint chains, closed form)."""
 function chain_fit(c::Chain, x_init::Array{E,3}, u_init::Array{E,3}; max_iter::Int64=100,
                    tol::Float64=1e-6, linearization=ILQR_LINEARIZE_DUAL,
-                   dynamics=ILQR_CHAIN_DYN_AUTO) where {E<:Union{Float32,Float64}}
+                   dynamics=ILQR_CHAIN_DYN_AUTO,
+                   costs::Union{Nothing,SimpleCosts}=nothing) where {E<:Union{Float32,Float64}}
     nx, N, nb = size(x_init); nu = size(u_init, 1); M = N - 1
     @assert(size(u_init, 2) == M)
     r = Ref{Ptr{Cvoid}}(C_NULL)
@@ -449,6 +465,13 @@ function chain_fit(c::Chain, x_init::Array{E,3}, u_init::Array{E,3}; max_iter::I
                 r, 0, c, M, nb, dt, linearization), "ilqr_chain_create")
     check(ccall((:ilqr_chain_set_dynamics, libilqr), Cint, (Ptr{Cvoid}, Int32), r[], dynamics),
           "ilqr_chain_set_dynamics")
+    if costs !== nothing
+        mode = costs.euclidean ? ILQR_CHAIN_COST_SIMPLE_EUCLIDEAN : ILQR_CHAIN_COST_SIMPLE
+        pt = collect(costs.point); tg = collect(costs.final_target)
+        check(ccall((:ilqr_chain_set_simple_costs, libilqr), Cint,
+                    (Ptr{Cvoid}, Int32, Int32, Ptr{Float64}, Ptr{Float64}, Float64),
+                    r[], mode, costs.body, pt, tg, costs.weight), "ilqr_chain_set_simple_costs")
+    end
     h = Handle(nx, nu, M, 1)                 # device-memory helper only
     xi = upload(h, x_init); ui = upload(h, u_init)
     xo = alloc(h, E, length(x_init)); uo = alloc(h, E, length(u_init)); sd = alloc(h, Int32, nb)

@@ -286,6 +286,31 @@ int32_t ilqr_chain_get_dynamics(const ilqr_chain_handle* h);
 /* the closed form's max relative deviation from the recursion at the creation check
  * (fp64; ≥ 1e-9 means the closed form is not used) */
 double ilqr_chain_closed_form_error(const ilqr_chain_handle* h);
+/* cost_functions.jl's factories (src/cost_functions.jl:5-54), replacing the handle's
+ * joint-space costs for 2-joint chains:
+ *   simple_final_cost(mechanism, body, point, final_target, weight)(x)
+ *       = weight · Σₖ (p_z(q) − final_targetₖ)²                               (:5-27)
+ *   simple_immediate_cost(...)(x, u) = Σ uᵢ²  (its arguments are unused)     (:34-54)
+ * where p(q) = transform_to_root(state, body) * point is the root-frame position of
+ * `point` (given in the frame of body `body`: the link joint `body` moves, 0-based; −1 =
+ * the fixed base) at the joint angles q = x[0:n_joints]. The reference differences the
+ * point's LAST coordinate (work_space_traj[end]) against every target component
+ * (ILQR_CHAIN_COST_SIMPLE keeps that reading); ILQR_CHAIN_COST_SIMPLE_EUCLIDEAN takes
+ * Σₖ (pₖ − final_targetₖ)², the squared distance. The reference passes the whole state
+ * to set_configuration! (a BoundsError for a fixed base); the joint angles are what it
+ * can mean. ILQR_CHAIN_COST_JOINT restores the costs of ilqr_chain_create (point,
+ * final_target, weight ignored). Needs the closed-form dynamics (ILQR_ERR_UNSUPPORTED
+ * otherwise; ilqr_chain_set_dynamics(RNEA) is refused while a simple cost is set). */
+typedef enum {
+  ILQR_CHAIN_COST_JOINT = 0,
+  ILQR_CHAIN_COST_SIMPLE = 1,
+  ILQR_CHAIN_COST_SIMPLE_EUCLIDEAN = 2
+} ilqr_chain_cost_mode;
+ilqr_status ilqr_chain_set_simple_costs(ilqr_chain_handle* h, int32_t mode, int32_t body,
+                                        const double* point, const double* final_target,
+                                        double weight);
+/* the cost mode in effect, −1 for a NULL handle */
+int32_t ilqr_chain_get_cost_mode(const ilqr_chain_handle* h);
 ilqr_status ilqr_chain_sync(ilqr_chain_handle* h);
 /* dynamicsf for n independent (x, u) pairs: x (n, nx), u (n, nu) → x_next (n, nx) */
 ilqr_status ilqr_chain_dynamics(ilqr_chain_handle* h, const void* x, const void* u, void* x_next,

@@ -288,14 +288,13 @@ class ChainModel:
 
 
 # -- independent formulation for the known-answer tests ---------------------------------
-def mass_matrix_jacobian(chain, q):
-    """M(q) = Σ_i m_i J_vᵢᵀ J_vᵢ + J_ωᵢᵀ (R_i I_ci R_iᵀ) J_ωᵢ from world-frame forward
-    kinematics (a formulation independent of the RNEA above)."""
-    n = chain.n
+def world_frames(chain, q):
+    """World-frame forward kinematics, root to tip: (origin, world axis, orientation) of
+    every body frame (matrix exponential of the joint axis; independent of the RNEA)."""
     R = np.eye(3)
     o = np.zeros(3)
     frames = []
-    for i in range(n):
+    for i in range(chain.n):
         o = o + R @ chain.p[i]
         Rj = R @ chain.R0[i]
         a_w = Rj @ chain.axis[i]
@@ -304,6 +303,14 @@ def mass_matrix_jacobian(chain, q):
         Rq = np.eye(3) + np.sin(q[i]) * K + (1 - np.cos(q[i])) * K @ K
         R = Rj @ Rq
         frames.append((o.copy(), a_w, R.copy()))
+    return frames
+
+
+def mass_matrix_jacobian(chain, q):
+    """M(q) = Σ_i m_i J_vᵢᵀ J_vᵢ + J_ωᵢᵀ (R_i I_ci R_iᵀ) J_ωᵢ from world-frame forward
+    kinematics (a formulation independent of the RNEA above)."""
+    n = chain.n
+    frames = world_frames(chain, q)
     M = np.zeros((n, n))
     for i in range(n):
         oi, _, Ri = frames[i]

@@ -23,6 +23,7 @@ from ilqr_amd.chain import (coupled_2dof_problem, load_robot, rbd_2dof_problem, 
                             rbd_initial_states)
 from ilqr_amd.problems import quadrotor_batch, random_lq_batch  # noqa: E402
 from oracle import ilqr_oracle as O  # noqa: E402
+from oracle import cost_functions as OC  # noqa: E402
 from oracle import rbd as RBD  # noqa: E402
 
 MAX_TRIALS = 60
@@ -98,14 +99,20 @@ def twolink_case(name, x0s, T, fit_iters=40, tol=1e-6, nu=2):
     print(name, "fit iters", fiters.tolist())
 
 
-def chain_case(name, nu, x0s, T, fit_iters=20, tol=1e-6, pr=None, robot="2dof_arm"):
+def chain_case(name, nu, x0s, T, fit_iters=20, tol=1e-6, pr=None, robot="2dof_arm", simple=None):
     """RBD family (ILQR_PROBLEM_CHAIN) on the fixed-base 2Dof_arm (or `pr`): oracle.rbd
     dynamics (RNEA + RK4, exact Jacobians by forward-mode AD) through the generic
-    oracle passes."""
+    oracle passes. `simple` = dict(body, point, final_target, weight, euclidean): the
+    costs of cost_functions.jl's factories (oracle.cost_functions, differentiated by
+    the ForwardDiff restatement) instead of the joint-space ones."""
     pr = rbd_2dof_problem(nu) if pr is None else pr
     model = RBD.ChainModel(pr.chain, pr.dt)
     cost = RBD.ChainCost(pr.target, pr.q_weight, pr.r_weight, pr.qf_weight)
     f, l, lf = RBD.chain_closures(model, cost)
+    if simple is not None:
+        a = (pr.chain, simple["body"], simple["point"], simple["final_target"], simple["weight"])
+        l = OC.simple_immediate_cost(*a)
+        lf = OC.simple_final_cost(*a, euclidean=simple["euclidean"])
     nb, nx = len(x0s), pr.nx
     u = np.zeros((nb, T, nu))
     x = np.empty((nb, T + 1, nx))
@@ -144,7 +151,7 @@ def chain_case(name, nu, x0s, T, fit_iters=20, tol=1e-6, pr=None, robot="2dof_ar
                         fw_x=xn, fw_u=un, fw_cost=fwc, fit_x=fx, fit_u=fu, fit_cost=fcost,
                         fit_iters=fiters, fit_status=fstatus,
                         meta=np.array(json.dumps({"T": T, "nu": nu, "fit_max_iter": fit_iters,
-                                                  "tol": tol, "robot": robot})))
+                                                  "tol": tol, "robot": robot, "simple": simple})))
     print(name, "fit iters", fiters.tolist(), "status", fstatus.tolist())
 
 
@@ -180,6 +187,21 @@ def main(only=()):
                    pr=coupled_2dof_problem(2), robot="coupled_2dof")
         chain_case("chain2c_nu1_t40", 1, rbd_initial_states(3, 2, seed0=40), T=40,
                    pr=coupled_2dof_problem(1), robot="coupled_2dof")
+    if want("chaintask"):
+        # cost_functions.jl's simple_final_cost / simple_immediate_cost: the tip point's
+        # z against every target component (the reference's reading), and the squared
+        # distance (euclidean) on the coupled chain
+        chain_case("chaintask_t60", 2, rbd_initial_states(3, 2, seed0=50), T=60, robot="2dof_arm",
+                   simple=dict(body=1, point=[0.0, 0.0, 0.5], final_target=[0.3, 0.5, 0.4],
+                               weight=2e4, euclidean=False))
+        chain_case("chaintask_c_nu1_t40", 1, rbd_initial_states(2, 2, seed0=60), T=40,
+                   pr=coupled_2dof_problem(1), robot="coupled_2dof",
+                   simple=dict(body=1, point=[0.2, 0.1, 0.3], final_target=[0.6, 0.2, 0.7],
+                               weight=2e5, euclidean=False))
+        chain_case("chaintask_c_euc_t40", 2, rbd_initial_states(2, 2, seed0=70), T=40,
+                   pr=coupled_2dof_problem(2), robot="coupled_2dof",
+                   simple=dict(body=1, point=[0.2, 0.1, 0.3], final_target=[1.2, 1.0, 0.5],
+                               weight=2e5, euclidean=True))
     if want("twolink_nu1"):
         # the nu = 1 variant of configs 1-2: f(x, [u₁, 0]), T = 50
         rng = np.random.default_rng(2025)
