@@ -15,10 +15,11 @@ HIPCC = "/opt/rocm/bin/hipcc"
 @pytest.mark.skipif(not os.path.exists(HIPCC) and shutil.which("hipcc") is None, reason="no hipcc")
 def test_chain_macro_alternates_compile(tmp_path):
     """ilqr_chain.hip with the Rodrigues-form central differences
-    (ILQR_CHAIN_FD_ROT=0) and the unpacked ±h evaluation (ILQR_CHAIN_FD_PAIR=0)."""
+    (ILQR_CHAIN_FD_ROT=0), the unpacked ±h evaluation (ILQR_CHAIN_FD_PAIR=0) and the
+    unpacked fp32 closed-form step (ILQR_CHAIN_F2_FAST=0)."""
     hipcc = HIPCC if os.path.exists(HIPCC) else shutil.which("hipcc")
     cmd = [hipcc, "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-mllvm", "-amdgpu-mfma-vgpr-form=1",
-           "-fno-slp-vectorize", "-DILQR_CHAIN_FD_ROT=0", "-DILQR_CHAIN_FD_PAIR=0", "-c",
+           "-fno-slp-vectorize", "-DILQR_CHAIN_FD_ROT=0", "-DILQR_CHAIN_FD_PAIR=0", "-DILQR_CHAIN_F2_FAST=0", "-c",
            os.path.join(CSRC, "ilqr_chain.hip"), "-o", str(tmp_path / "chain_alt.o")]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-2000:]
@@ -33,5 +34,17 @@ def test_forward_ring_alternates_compile(tmp_path):
     cmd = [hipcc, "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-DILQR_FW_LDS_BCAST=1",
            "-DILQR_FW_WAVES=1", "-DILQR_FW_ABLATE=3", "-c", os.path.join(CSRC, "ilqr_lq.hip"),
            "-o", str(tmp_path / "lq_alt.o")]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC) and shutil.which("hipcc") is None, reason="no hipcc")
+def test_twolink_alternates_compile(tmp_path):
+    """ilqr_twolink.hip without the branch-free shifted-sincos RK4 (ILQR_TL_RK4_SHIFT=0:
+    the forward group's robust pass only) and with a 4-deep forward prefetch."""
+    hipcc = HIPCC if os.path.exists(HIPCC) else shutil.which("hipcc")
+    cmd = [hipcc, "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-mllvm", "-amdgpu-mfma-vgpr-form=1",
+           "-DILQR_TL_RK4_SHIFT=0", "-DILQR_FW_GROUP_PF=4", "-c", os.path.join(CSRC, "ilqr_twolink.hip"),
+           "-o", str(tmp_path / "tl_alt.o")]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-2000:]
