@@ -32,6 +32,7 @@ struct ilqr_handle {
   int32_t* host_status = nullptr;  // pinned host copy of a status array (fold_status)
   // fit's convergence poll: running-trajectory counts of the last two iterations,
   // written by the device into host-mapped memory, each behind an event
+  // [2] = fit's call-status flags (gather_kernel: bit 0 NaN, bit 1 exhausted line search)
   int32_t* host_running = nullptr;
   int32_t* dev_running = nullptr;  // device alias of host_running
   hipEvent_t ev_poll[2] = {nullptr, nullptr};
@@ -126,6 +127,12 @@ ilqr::LSParams ls_params(const ilqr_options* o) {
 
 ilqr_status join(ilqr_handle* h, const ilqr_problem* p);
 
+// the LQ iteration runs as one lq_iter_fused4 launch (enqueue_iteration)
+bool fused_path(const ilqr_handle* h, const ilqr_problem* p) {
+  return !two_link(p) && h->nchunks == 1 && h->fused && !h->bw_wave && h->fw_ring && h->nx == 12 &&
+         h->nu == 4;
+}
+
 // Enqueue one fit iteration for the whole batch: backward(c) on the handle's
 // stream, forward(c) on the side stream after it. With `chain`, backward(c) first
 // waits for the previous iteration's forward(c) (same trajectories); otherwise the
@@ -139,7 +146,7 @@ ilqr_status enqueue_iteration(ilqr_handle* h, const ilqr_problem* p, const ilqr:
   }
   const ilqr::LQParams P = lq_params(p);
   if (h->nchunks == 1) {  // one stream, no cross-stream events (each hand-off costs ~10 µs)
-    if (h->fused && !h->bw_wave && h->fw_ring && h->nx == 12 && h->nu == 4) {
+    if (fused_path(h, p)) {
       HIP_TRY(ilqr::launch_lq_iter_fused4(P, h->batch, h->T, a, ls, h->stream, h->fw_mfma));
       return ILQR_OK;
     }
@@ -336,7 +343,7 @@ ilqr_status ilqr_create(ilqr_handle** out, int device, int nx, int nu, int T, in
   if (e == hipSuccess) e = hipMalloc(&h->iters, sizeof(int32_t) * B);
   if (e == hipSuccess) e = hipHostMalloc(&h->host_status, sizeof(int32_t) * B, hipHostMallocDefault);
   if (e == hipSuccess)
-    e = hipHostMalloc(&h->host_running, sizeof(int32_t) * 2, hipHostMallocMapped | hipHostMallocCoherent);
+    e = hipHostMalloc(&h->host_running, sizeof(int32_t) * 4, hipHostMallocMapped | hipHostMallocCoherent);
   if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&h->dev_running, h->host_running, 0);
   for (int c = 0; c < 2 && e == hipSuccess; ++c) e = hipEventCreateWithFlags(&h->ev_poll[c], hipEventDisableTiming);
   if (e == hipSuccess && ilqr::tl_supported(nx, nu))
@@ -593,8 +600,13 @@ ilqr_status ilqr_fit(ilqr_handle* h, const ilqr_problem* p, const ilqr_options* 
     return fst;
   }
   hipStream_t s = h->stream;
-  // prev_cost = Inf (forward_pass.jl:159), status OK, result "the input", iters 0
-  HIP_TRY(ilqr::launch_fit_init(h->batch, h->prev_cost, h->status, h->res_parity, h->iters, s));
+  // prev_cost = Inf (forward_pass.jl:159), status OK, result "the input", iters 0: by
+  // the first iteration's kernel itself on the fused LQ path, else by a kernel here
+  const bool init_in_iter = fused_path(h, p) && !h->pipelined && o->max_iter > 0;
+  if (!init_in_iter)
+    HIP_TRY(ilqr::launch_fit_init(h->batch, h->prev_cost, h->status, h->res_parity, h->iters, s));
+  volatile int32_t* flags = h->host_running + 2;
+  *flags = 0;
   const ilqr::LSParams ls = ls_params(o);
   // Iteration `it` reads x̄ⁱ (the caller's x_init/u_init for it = 1, no copy; else
   // the handle's buffer (it−1)&1) and writes buffer it&1 (x̄ⁱ, ūⁱ = x̄ⁱ⁺¹, ūⁱ⁺¹,
@@ -632,6 +644,7 @@ ilqr_status ilqr_fit(ilqr_handle* h, const ilqr_problem* p, const ilqr_options* 
     a.iters = h->iters;
     a.parity = it == 1 ? ilqr::PARITY_INPUT : par;
     a.iter = it;
+    a.init = init_in_iter && it == 1;
     return a;
   };
   if (!two_link(p) && h->pipelined) {
@@ -678,8 +691,10 @@ ilqr_status ilqr_fit(ilqr_handle* h, const ilqr_problem* p, const ilqr_options* 
   HIP_TRY(ilqr::launch_gather_result(h->batch, h->T, h->nx, h->nu, x_init, u_init, h->xbuf[0],
                                      h->ubuf[0], h->xbuf[1], h->ubuf[1], h->res_parity, h->status,
                                      last, h->prev_cost, h->iters, x_out, u_out, cost, iters,
-                                     status, s));
-  return fold_status(h, h->status);
+                                     status, h->dev_running + 2, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  const int32_t f = __atomic_load_n(h->host_running + 2, __ATOMIC_ACQUIRE);
+  return (f & 1) ? ILQR_ERR_NAN : ((f & 2) ? ILQR_ERR_LS_EXHAUSTED : ILQR_OK);
 }
 
 ilqr_status ilqr_malloc(ilqr_handle* h, size_t bytes, void** ptr) {

@@ -439,16 +439,36 @@ __global__ __launch_bounds__(64 * FUSED_WAVES) void lq_iter_fused4_kernel(LQPara
   double* lds = lds_all + w * FUSED_LDS;
   const int b0 = (blockIdx.x * FUSED_WAVES + w) * BW4_SLOTS;
   if (b0 >= B) return;
-  unsigned active = 0;
-#pragma unroll
-  for (int q = 0; q < BW4_SLOTS; ++q)
-    if (b0 + q < B && a.status[b0 + q] == ILQR_TRAJ_OK) active |= 1u << q;
-  if (active == 0) return;
-  const unsigned nan = lq_backward4_wave(P, b0, B, active, T, a.x, a.u, a.d, a.K, ls.mu, lds) & active;
   const int l = threadIdx.x & 63;
-  if (l < BW4_SLOTS && ((nan >> l) & 1u)) {
-    a.status[b0 + l] = ILQR_TRAJ_NAN;  // reference: AssertionError at backward_pass.jl:353
-    if (a.res_parity) a.res_parity[b0 + l] = a.parity;
+  // the lane that writes slot q's per-trajectory words (the forward's writer: lane 16q
+  // in the row form, lane 4q in the MFMA form), so the writes of one slot keep program order
+  const bool owner = MF ? (l < 16 && (l & 3) == 0) : (l & 15) == 0;
+  const int q = MF ? (l >> 2) & 3 : l >> 4;
+  unsigned active = 0;
+  IterArgs ai = a;
+  if (a.init) {
+    // fit's first iteration (fit_init_kernel's job, :159): every present trajectory
+    // runs from prev_cost = Inf
+    const int nt = B - b0 < BW4_SLOTS ? B - b0 : BW4_SLOTS;
+    active = (1u << nt) - 1u;
+    if (owner && q < nt) {
+      const int b = b0 + q;
+      a.new_cost[b] = INFINITY;  // = prev_cost (in place)
+      a.status[b] = ILQR_TRAJ_OK;
+      a.res_parity[b] = PARITY_INPUT;
+      a.iters[b] = 0;
+    }
+    ai.prev_cost = nullptr;  // +Inf without reading
+  } else {
+#pragma unroll
+    for (int q = 0; q < BW4_SLOTS; ++q)
+      if (b0 + q < B && a.status[b0 + q] == ILQR_TRAJ_OK) active |= 1u << q;
+    if (active == 0) return;
+  }
+  const unsigned nan = lq_backward4_wave(P, b0, B, active, T, a.x, a.u, a.d, a.K, ls.mu, lds) & active;
+  if (owner && ((nan >> q) & 1u)) {
+    a.status[b0 + q] = ILQR_TRAJ_NAN;  // reference: AssertionError at backward_pass.jl:353
+    if (a.res_parity) a.res_parity[b0 + q] = a.parity;
   }
   // the gains this wave stored are what its forward streams in: every store complete,
   // and the LDS scratch free for the ring
@@ -456,9 +476,9 @@ __global__ __launch_bounds__(64 * FUSED_WAVES) void lq_iter_fused4_kernel(LQPara
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
   const unsigned run = active & ~nan;
   if constexpr (MF)
-    iter_forward_wave_mfma(P, b0, B, T, a, ls, lds, run);
+    iter_forward_wave_mfma(P, b0, B, T, ai, ls, lds, run);
   else
-    iter_forward_wave_active<12, 4>(P, b0, B, T, a, ls, lds, ((run >> (l >> 4)) & 1u) != 0);
+    iter_forward_wave_active<12, 4>(P, b0, B, T, ai, ls, lds, ((run >> (l >> 4)) & 1u) != 0);
 }
 
 }  // namespace

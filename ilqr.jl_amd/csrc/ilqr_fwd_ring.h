@@ -402,7 +402,9 @@ __device__ FwdOut lq_forward_wave_ring(const LQParams& P, int b0, int B, int T, 
 #endif
       // δx = x̄ₖ − xₖ (:72); ūₖ = uₖ + α δuₖ + Kₖ δx (:73)
       const double dx = is_x ? xb - cur.a : 0.0;
-#if ILQR_FW_LDS_BCAST
+#if ILQR_FW_ABLATE & 4  // probe only: no K δx product (the c-form's saving)
+      const double kdx = dx;
+#elif ILQR_FW_LDS_BCAST
       const double kdx = lds_dot12(rbd, dx, cur.Kr);
 #else
       const double kdx = dpp_dot12(dx, cur.Kr);

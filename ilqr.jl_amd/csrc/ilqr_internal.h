@@ -41,6 +41,8 @@ struct IterArgs {
   int32_t* iters;       // (B) out, may be null: last iteration index that processed the trajectory
   int parity;           // parity of (x, u) in the fit ping-pong
   int iter;             // 1-based iteration index (fit)
+  int init;             // fit's first iteration on the fused LQ kernel: the kernel itself sets
+                        // prev_cost = Inf, status OK, res_parity = input, iters = 0 (fit_init)
 };
 
 // Returns hipSuccess or the launch error. All launches are asynchronous on `s`.
@@ -97,7 +99,8 @@ hipError_t launch_gather_result(int B, int T, int nx, int nu, const double* xin,
                                 const double* u1, const int32_t* res_parity, int32_t* status,
                                 int final_parity, const double* fit_cost, const int32_t* fit_iters,
                                 double* x_out, double* u_out, double* cost_out,
-                                int32_t* iters_out, int32_t* status_out, hipStream_t s);
+                                int32_t* iters_out, int32_t* status_out, int32_t* flags,
+                                hipStream_t s);
 // (N, R, C) row-major → (N, R2, C2) zero-padded (R2 ≥ R, C2 ≥ C), and back.
 hipError_t launch_pad3(const double* src, double* dst, size_t N, int R, int C, int R2, int C2,
                        hipStream_t s);

@@ -890,29 +890,36 @@ __global__ __launch_bounds__(256, 4) void lq_iter_pipe_kernel(LQParams P, int B,
   }
 }
 
-__global__ void gather_kernel(int B, int T, int nx, int nu, const double* xin, const double* uin,
-                              const double* x0, const double* u0, const double* x1,
-                              const double* u1, const int32_t* res_parity, int32_t* status,
-                              int final_parity, const double* fit_cost, const int32_t* fit_iters,
-                              double* x_out, double* u_out, double* cost_out, int32_t* iters_out,
-                              int32_t* status_out) {
-  const int b = blockIdx.x;
+// One wave per trajectory (four per block). `flags` (host-mapped, may be null)
+// collects the call status: bit 0 a NaN trajectory, bit 1 an exhausted line search.
+__global__ __launch_bounds__(256) void gather_kernel(int B, int T, int nx, int nu, const double* xin,
+                                                     const double* uin, const double* x0, const double* u0,
+                                                     const double* x1, const double* u1,
+                                                     const int32_t* res_parity, int32_t* status,
+                                                     int final_parity, const double* fit_cost,
+                                                     const int32_t* fit_iters, double* x_out, double* u_out,
+                                                     double* cost_out, int32_t* iters_out,
+                                                     int32_t* status_out, int32_t* flags) {
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int l = threadIdx.x & 63;
   if (b >= B) return;
-  const bool running = status[b] == ILQR_TRAJ_OK;
+  const int32_t st0 = status[b];
+  const bool running = st0 == ILQR_TRAJ_OK;
   const int par = running ? final_parity : res_parity[b];
   if (par != PARITY_OUT) {  // PARITY_OUT: the last iteration wrote x_out / u_out itself
     const double* xs = (par == PARITY_INPUT ? xin : (par ? x1 : x0)) + (size_t)b * (T + 1) * nx;
     const double* us = (par == PARITY_INPUT ? uin : (par ? u1 : u0)) + (size_t)b * T * nu;
-    for (int i = threadIdx.x; i < (T + 1) * nx; i += blockDim.x) x_out[(size_t)b * (T + 1) * nx + i] = xs[i];
-    for (int i = threadIdx.x; i < T * nu; i += blockDim.x) u_out[(size_t)b * T * nu + i] = us[i];
+    for (int i = l; i < (T + 1) * nx; i += 64) x_out[(size_t)b * (T + 1) * nx + i] = xs[i];
+    for (int i = l; i < T * nu; i += 64) u_out[(size_t)b * T * nu + i] = us[i];
   }
-  __syncthreads();  // every wave of the block has read status[b] before it changes
-  if (threadIdx.x == 0) {
-    const int32_t st = running ? ILQR_TRAJ_MAX_ITER : status[b];
+  if (l == 0) {  // the lane that read status[b] is the one that rewrites it
+    const int32_t st = running ? ILQR_TRAJ_MAX_ITER : st0;
     status[b] = st;
     if (status_out) status_out[b] = st;
     if (cost_out) cost_out[b] = fit_cost[b];
     if (iters_out) iters_out[b] = fit_iters[b];
+    const int f = (st == ILQR_TRAJ_NAN ? 1 : 0) | (st == ILQR_TRAJ_LS_EXHAUSTED ? 2 : 0);
+    if (flags && f) __hip_atomic_fetch_or(flags, f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
@@ -1108,11 +1115,12 @@ hipError_t launch_gather_result(int B, int T, int nx, int nu, const double* xin,
                                 const double* u1, const int32_t* res_parity, int32_t* status,
                                 int final_parity, const double* fit_cost, const int32_t* fit_iters,
                                 double* x_out, double* u_out, double* cost_out,
-                                int32_t* iters_out, int32_t* status_out, hipStream_t s) {
+                                int32_t* iters_out, int32_t* status_out, int32_t* flags,
+                                hipStream_t s) {
   if (B <= 0) return hipSuccess;
-  gather_kernel<<<B, 256, 0, s>>>(B, T, nx, nu, xin, uin, x0, u0, x1, u1, res_parity, status,
-                                  final_parity, fit_cost, fit_iters, x_out, u_out, cost_out,
-                                  iters_out, status_out);
+  gather_kernel<<<(B + 3) / 4, 256, 0, s>>>(B, T, nx, nu, xin, uin, x0, u0, x1, u1, res_parity, status,
+                                            final_parity, fit_cost, fit_iters, x_out, u_out, cost_out,
+                                            iters_out, status_out, flags);
   return hipGetLastError();
 }
 

@@ -6,6 +6,10 @@ sys.path[:0] = [R, os.path.join(R, "ilqr.jl_amd")]
 from ilqr_amd import _lib
 from ilqr_amd.problems import quadrotor_batch
 from ilqr_amd.solver import Solver, _ptr
+LIBS = [a for a in sys.argv[1:] if a.endswith(".so")]
+if LIBS:  # an alternate build of libilqr_hip.so (tools/fw_alt.sh, tools/fw_ab4.sh)
+    _lib._lib = _lib.load(LIBS[0])
+    print("library:", LIBS[0])
 
 B, T = 4096, 100
 lq, x0, u0 = quadrotor_batch(B, T=T, seed0=0)
