@@ -633,3 +633,50 @@ def test_fused_mfma_equals_split_mfma(gpu, nb, T):
         fin = np.isfinite(b)
         assert np.array_equal(np.isfinite(a), fin)
         assert np.abs(a[fin] - b[fin]).max() <= 1e-10 * max(np.abs(b[fin]).max(), 1e-300)
+
+
+@pytest.mark.parametrize("nb,T,max_iter,tol,max_trials,nan,inplace", [
+    (37, 17, 1, -1.0, None, False, False),
+    (37, 17, 3, -1.0, None, True, False),
+    (2051, 9, 2, -1.0, None, True, True),
+    (37, 17, 6, 1e-8, None, False, False),
+    (41, 20, 40, 1e-9, None, True, False),
+    (37, 17, 5, -1.0, 1, False, False),
+    (37, 17, 5, -1.0, 1, True, True),
+    (5, 3, 4, 1e-3, None, False, True),
+])
+def test_fit_in_kernel_init(gpu, nb, T, max_iter, tol, max_trials, nan, inplace):
+    """The fused path's fit initialises its per-trajectory state in the first
+    iteration's kernel (no fit_init launch); the split schedule launches fit_init.
+    Same bits and call status (the gather's host-mapped flags), over early stops
+    (converged, exhausted line searches, NaN), fits whose poll ends before max_iter,
+    in-place calls (x_out = x_init: the gather's copy path) and ragged batches."""
+    import ctypes as C
+    lq, x, u = random_lq_batch(nb, 12, 4, T, seed=nb + 7 * T + max_iter)
+    if nan:
+        x[nb // 3, 1, 2] = np.nan
+    s = Solver(12, 4, T, nb)
+    s.set_problem(lq)
+    outs = []
+    for fused in (False, True):
+        s.set_schedule(backward="block", fused=fused)
+        xi, ui = dev(x), dev(u)
+        if inplace:
+            cost = torch.empty((nb,), dtype=torch.float64, device="cuda")
+            it = torch.empty((nb,), dtype=torch.int32, device="cuda")
+            st = torch.empty((nb,), dtype=torch.int32, device="cuda")
+            s._bind_stream()
+            o = _lib.default_options(max_iter=max_iter, tol=tol, max_trials=max_trials)
+            p = C.c_void_p
+            rc = s.lib.ilqr_fit(s.h, s._p(), C.byref(o), p(xi.data_ptr()), p(ui.data_ptr()), None,
+                                p(xi.data_ptr()), p(ui.data_ptr()), p(cost.data_ptr()),
+                                p(it.data_ptr()), p(st.data_ptr()))
+            outs.append((rc, xi, ui, cost, it, st))
+        else:
+            r = s.fit(xi, ui, max_iter=max_iter, tol=tol, max_trials=max_trials)
+            outs.append((r.call_status, r.x, r.u, r.cost, r.iters, r.status))
+    assert outs[0][0] == outs[1][0]
+    for a, b in zip(outs[0][1:], outs[1][1:]):
+        torch.testing.assert_close(a, b, rtol=0, atol=0, equal_nan=True)
+    if nan:
+        assert outs[1][5][nb // 3].item() == _lib.TRAJ_NAN
