@@ -174,6 +174,20 @@ __device__ unsigned lq_backward4_wave(const LQParams& P, int b0, int B, unsigned
     for (int K = 0; K < 3; ++K) z[K] = buf_ld(rX, zxo + 32 * K, (uint32_t)(t * NX * 8));
     z[3] = buf_ld(rU, zuo, (uint32_t)(t * NU * 8));
   };
+  // L z for the four steps from t0 (column κ = step t0 − κ), from zq; then the next
+  // four steps' z. Computed one step ahead of its first use, so each step's column
+  // permutes can issue at the top of the step, behind the S·F MFMAs.
+  auto lz_block = [&](int t0) {
+#pragma unroll
+    for (int I = 0; I < 3; ++I) {
+      double v = 0.0;
+#pragma unroll
+      for (int K = 0; K < 3; ++K) v = mf4(L[K][I], zq[K], v);
+      Lzq[I] = v;
+    }
+    Lzq[3] = mf4(LR, zq[3], 0.0);
+    load_zq(t0 - 4);
+  };
   if constexpr (LZ4) load_zq(T - 1);
   else load_z(T - 1, zc);
 
@@ -182,6 +196,7 @@ __device__ unsigned lq_backward4_wave(const LQParams& P, int b0, int B, unsigned
   // every load of the prologue lands here, so the loop's waits only count the loop's
   // own loads
   __builtin_amdgcn_s_waitcnt(0);
+  if constexpr (LZ4 && (ABL & 256) == 0) lz_block(T - 1);
 
   for (int t = T - 1; t >= 0; --t) {
     if constexpr ((ABL & 64) != 0) {
@@ -191,7 +206,18 @@ __device__ unsigned lq_backward4_wave(const LQParams& P, int b0, int B, unsigned
       load_z(t > 0 ? t - 1 : 0, zn);
     }
 
-    // Y = S·F, column block 3 (B) first: H needs it
+    // this step's L z columns (LZ4): the permutes issue here, their LDS latency hidden
+    // behind the S·F products
+    [[maybe_unused]] double lzp[4];
+    if constexpr (LZ4 && (ABL & 256) == 0) {
+      const int src = ((l & ~3) | ((T - 1 - t) & 3)) * 4;
+#pragma unroll
+      for (int I = 0; I < 4; ++I) lzp[I] = lane_perm(Lzq[I], src);
+    }
+    // Y = S·F, column block 3 (B) first: H needs it. Each sum runs over K = 0, 1, 2;
+    // its K ≤ I terms read stored upper blocks S[K][I], its K > I terms the lower blocks
+    // that the previous step's lane permutations produce: all 24 upper-block products
+    // issue first (same summation order), so the permutes' latency hides behind them.
     double Y[3][4];
 #pragma unroll
     for (int J = 3; J >= 0; --J)
@@ -199,9 +225,16 @@ __device__ unsigned lq_backward4_wave(const LQParams& P, int b0, int B, unsigned
       for (int I = 0; I < 3; ++I) {
         double v = 0.0;
 #pragma unroll
-        for (int K = 0; K < 3; ++K) v = mf4(S[K][I], F[K][J], v);
+        for (int K = 0; K <= I; ++K) v = mf4(S[K][I], F[K][J], v);
         Y[I][J] = v;
       }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int J = 3; J >= 0; --J)
+#pragma unroll
+      for (int I = 0; I < 2; ++I)
+#pragma unroll
+        for (int K = I + 1; K < 3; ++K) Y[I][J] = mf4(S[K][I], F[K][J], Y[I][J]);
     // H = R + Rᵀ + BᵀSB → LDS, read back whole by the slot's lanes
     double H = LR;
 #pragma unroll
@@ -212,19 +245,19 @@ __device__ unsigned lq_backward4_wave(const LQParams& P, int b0, int B, unsigned
     double gv[4];
     if constexpr (LZ4) {
       const int j = (T - 1 - t) & 3;
-      if (j == 0) {  // L z for steps t .. t-3, then the next four steps' z
-#pragma unroll
-        for (int I = 0; I < 3; ++I) {
-          double v = 0.0;
-#pragma unroll
-          for (int K = 0; K < 3; ++K) v = mf4(L[K][I], zq[K], v);
-          Lzq[I] = v;
-        }
-        Lzq[3] = mf4(LR, zq[3], 0.0);
-        load_zq(t - 4);
-      }
       double lz[4];
       if constexpr ((ABL & 256) != 0) {  // through LDS: column j of each block, replicated
+        if (j == 0) {  // L z for steps t .. t-3, then the next four steps' z
+#pragma unroll
+          for (int I = 0; I < 3; ++I) {
+            double v = 0.0;
+#pragma unroll
+            for (int K = 0; K < 3; ++K) v = mf4(L[K][I], zq[K], v);
+            Lzq[I] = v;
+          }
+          Lzq[3] = mf4(LR, zq[3], 0.0);
+          load_zq(t - 4);
+        }
         double* Lzl = lds + 64 + beta * 64;
         if (j == 0) {
           double2* w = reinterpret_cast<double2*>(Lzl + (kap * 4 + rho) * 4);
@@ -236,9 +269,8 @@ __device__ unsigned lq_backward4_wave(const LQParams& P, int b0, int B, unsigned
         const double2 a = rd[0], c = rd[1];
         lz[0] = a.x; lz[1] = a.y; lz[2] = c.x; lz[3] = c.y;
       } else {
-        const int src = ((l & ~3) | j) * 4;
 #pragma unroll
-        for (int I = 0; I < 4; ++I) lz[I] = lane_perm(Lzq[I], src);
+        for (int I = 0; I < 4; ++I) lz[I] = lzp[I];
       }
 #pragma unroll
       for (int I = 0; I < 4; ++I) {
@@ -370,6 +402,10 @@ __device__ unsigned lq_backward4_wave(const LQParams& P, int b0, int B, unsigned
     }
 #pragma unroll
     for (int J = 0; J < 4; ++J) Klast[J] = Kg[J];
+    // the next step starts a block of four: its L z now (LZ4)
+    if constexpr (LZ4 && (ABL & 256) == 0) {
+      if (((T - t) & 3) == 0 && t > 0) lz_block(t - 1);
+    }
   }
   bool nan = false;
 #pragma unroll

@@ -25,6 +25,8 @@ case $WHAT in
   pmc) step pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- python bench.py --steps 5 --warmup 1 --no-cpu
        step pmc_write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run -- python bench.py --steps 5 --warmup 1 --no-cpu
        python profiles/collect_pmc.py gpurun_out/pmc_fetch gpurun_out/pmc_write gpurun_out/pmc.json > gpurun_out/pmc_summary.log 2>&1 ;;
+  mfma) step pmc_mfma 300 rocprofv3 --pmc MfmaUtil MfmaFlopsF64 SQ_INSTS_VALU_MFMA_F64 SQ_INSTS_VALU GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d gpurun_out/pmc_mfma -o run -- python bench.py --steps 5 --warmup 1 --no-cpu
+        python profiles/collect_mfma.py gpurun_out/pmc_mfma gpurun_out/mfma.json > gpurun_out/mfma_summary.log 2>&1 ;;
   tl) step pytest_twolink 600 python -m pytest tests/test_gpu_twolink.py -x -q ;;
   tiles) step pytest_tiles 600 python -m pytest tests/test_gpu_tiles.py -x -q ;;
   tlbench) step bench_twolink 300 python tools/bench_twolink.py ;;
