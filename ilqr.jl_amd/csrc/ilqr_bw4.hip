@@ -41,6 +41,10 @@
 namespace ilqr {
 namespace {
 
+#ifndef ILQR_BW4_MFMA_T
+#define ILQR_BW4_MFMA_T 1
+#endif
+
 constexpr int BW4_SLOTS = 4;          // trajectories per wave
 constexpr int BW4_WAVES = 4;          // waves per workgroup
 constexpr int BW4_LDS = 64 + 256;     // doubles of LDS per wave: the four H tiles, L z columns
@@ -123,6 +127,11 @@ __device__ unsigned lq_backward4_wave(const LQParams& P, int b0, int B, unsigned
 
   // the lane permutation ρ ↔ κ (block transpose within each slot)
   const int tr_src = (16 * kap + 4 * beta + rho) * 4;
+  // ... and the same transpose on the MFMA: mf4(a, I, 0) = aᵀ, exact (products with 1
+  // and 0); mf4(a, I/2, a/2) = (a + aᵀ)/2 with one rounding, = 0.5·(a + aᵀ) bit for bit
+  // (ILQR_BW4_MFMA_T: a ≈50-cycle MFMA result instead of a ds_bpermute round trip on
+  // the solve's and the symmetrisation's dependent chains)
+  [[maybe_unused]] const double Id = rho == kap ? 1.0 : 0.0, Ih = rho == kap ? 0.5 : 0.0;
 
   // terminal value function (final_cost_quadratization :134-153): S = Qf + Qfᵀ, s = S x_N
   double S[3][3], s[3];
@@ -365,7 +374,11 @@ __device__ unsigned lq_backward4_wave(const LQParams& P, int b0, int B, unsigned
 #pragma unroll
       for (int J = 0; J < 4; ++J) Kg[J] = mf4n(Hi, J < 3 ? G[J] : gv[3], 0.0);
     } else {
+#if ILQR_BW4_MFMA_T
+      const double Mt = mf4(Mn, Id, 0.0), Mnd = Mn * dsel;
+#else
       const double Mt = lane_perm(Mn, tr_src), Mnd = Mn * dsel;
+#endif
 #pragma unroll
       for (int J = 0; J < 4; ++J) Kg[J] = mf4n(Mnd, mf4(Mt, J < 3 ? G[J] : gv[3], 0.0), 0.0);
     }
@@ -390,7 +403,12 @@ __device__ unsigned lq_backward4_wave(const LQParams& P, int b0, int B, unsigned
     }
     if ((ABL & 128) == 0 && (t % SYM_EVERY) == 0) {
 #pragma unroll
-      for (int I = 0; I < 3; ++I) S[I][I] = 0.5 * (S[I][I] + lane_perm(S[I][I], tr_src));
+      for (int I = 0; I < 3; ++I)
+#if ILQR_BW4_MFMA_T
+        S[I][I] = mf4(S[I][I], Ih, 0.5 * S[I][I]);
+#else
+        S[I][I] = 0.5 * (S[I][I] + lane_perm(S[I][I], tr_src));
+#endif
     }
 #pragma unroll
     for (int I = 0; I < 3; ++I)

@@ -1,0 +1,17 @@
+#!/bin/bash
+# Alternate builds of the backward file (ilqr_bw4.hip) for A/B timing with
+# tools/fused_probe.py <lib>: tools/fwalt/libilqr_hip_<name>.so
+#   bwt0: block transposes by ds_bpermute (ILQR_BW4_MFMA_T=0) instead of the MFMA
+set -e
+cd "$(dirname "$0")/.."
+make -C ilqr.jl_amd/csrc > /dev/null
+mkdir -p tools/fwalt
+O=ilqr.jl_amd/lib/obj
+build() {  # build <name> <flags...>
+  local n=$1; shift
+  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -mllvm -amdgpu-mfma-vgpr-form=1 "$@" \
+    -c ilqr.jl_amd/csrc/ilqr_bw4.hip -o tools/fwalt/bw4_$n.o
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o tools/fwalt/libilqr_hip_$n.so $O/ilqr_lq.hip.o tools/fwalt/bw4_$n.o \
+    $O/ilqr_twolink.hip.o $O/ilqr_tiles.hip.o $O/ilqr_chain.hip.o $O/ilqr_abi.cpp.o $O/ilqr_multi.cpp.o -lpthread
+}
+build bwt0 -DILQR_BW4_MFMA_T=0

@@ -21,6 +21,8 @@ st = torch.zeros((B,), dtype=torch.int32, device="cuda")
 xo, uo = torch.empty_like(x), torch.empty_like(u)
 o1 = _lib.default_options(tol=-1.0)
 o3 = _lib.default_options(max_iter=3, tol=-1.0)
+d = torch.empty((B, T, 4), dtype=torch.float64, device="cuda"); K = torch.empty((B, T, 4, 12), dtype=torch.float64, device="cuda")
+def bw(): s.lib.ilqr_backward(s.h, s._p(), C.byref(o1), _ptr(x), _ptr(u), _ptr(d), _ptr(K), None)
 def it(): s.iterate(x, u, xn, un, None, st, options=o1, new_cost=pc)
 def fit(): s.lib.ilqr_fit(s.h, s._p(), C.byref(o3), _ptr(x), _ptr(u), None, _ptr(xo), _ptr(uo), None, None, None)
 for rep in range(3):
@@ -34,4 +36,6 @@ for rep in range(3):
         ms_it = e0.elapsed_time(e1) / 200
         t0 = time.perf_counter(); [fit() for _ in range(60)]; torch.cuda.synchronize()
         ms_fit = (time.perf_counter() - t0) * 1000 / 60 / 3
-        print(f"fused={fused!s:5}  iterate {ms_it*1000:7.1f} us   fit(3) {ms_fit*1000:7.1f} us/iteration", flush=True)
+        e0.record(); [bw() for _ in range(200)]; e1.record(); torch.cuda.synchronize()
+        ms_bw = e0.elapsed_time(e1) / 200
+        print(f"fused={fused!s:5}  iterate {ms_it*1000:7.1f} us   fit(3) {ms_fit*1000:7.1f} us/iteration   backward {ms_bw*1000:6.1f} us", flush=True)
