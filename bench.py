@@ -91,6 +91,31 @@ def load_pmc_traffic(profiles_dir):
     return best
 
 
+def load_mfma_pmc(profiles_dir):
+    """MFMA utilisation per kernel from the committed rocprofv3 pass
+    (profiles/mfma_*.json, written by profiles/collect_mfma.py), or None."""
+    best = None
+    if os.path.isdir(profiles_dir):
+        for f in sorted(os.listdir(profiles_dir)):
+            if f.startswith("mfma_") and f.endswith(".json"):
+                try:
+                    best = json.load(open(os.path.join(profiles_dir, f)))
+                except Exception:
+                    pass
+    return best
+
+
+def mfma_summary(m, key):
+    e = (m or {}).get(key)
+    if not e:
+        return None
+    return {"mfma_busy_pct": e.get("MfmaUtil"), "mfma_tflops": e.get("mfma_tflops"),
+            "mfma_frac_of_fp64_peak": e.get("mfma_frac_of_peak"),
+            "f64_mfma_insts_per_launch": e.get("SQ_INSTS_VALU_MFMA_F64"),
+            "valu_insts_per_launch": e.get("SQ_INSTS_VALU"),
+            "source": "rocprofv3 --pmc MfmaUtil MfmaFlopsF64 (profiles/mfma_*.json)"}
+
+
 def cpu_threads():
     """Host threads for the CPU baseline: every CPU this process may run on, capped
     at the box's CPU share when the operator sets one (OMP_NUM_THREADS = 16 per GPU
@@ -356,6 +381,7 @@ def main():
     traffic = None
     if pmc and pmc.get("batch") == B and pmc.get("T") == T:
         traffic = pmc.get("hbm_bytes_per_backward_launch")
+    mf = load_mfma_pmc(os.path.join(ROOT, "profiles"))
     achieved_tf = bw_flops / (bw_ms * 1e-3) / 1e12
     # serial ceiling of the backward-then-forward schedule: backward at the FP64 spec
     # peak + forward at the guide's measured streaming-copy rate
@@ -387,7 +413,8 @@ def main():
                      "frac": achieved_tf / FP64_PEAK_TFLOPS, "traffic": traffic,
                      "avg_launch_ms": bw_ms, "algorithmic_flops_per_launch": bw_flops,
                      "algorithmic_bytes_per_launch": bw_bytes,
-                     "hbm_achieved_gbps": bw_bytes / (bw_ms * 1e-3) / 1e9},
+                     "hbm_achieved_gbps": bw_bytes / (bw_ms * 1e-3) / 1e9,
+                     "mfma_pmc": mfma_summary(mf, "backward_api")},
         "forward_kernel": {"bound": "hbm", "kernel": "lq_forward (forward_pass + line search, LDS-ring input stream)",
                            "avg_launch_ms": fw_ms, "algorithmic_bytes_per_launch": fw_bytes,
                            "achieved_gbps": fw_bytes / (fw_ms * 1e-3) / 1e9,
@@ -424,7 +451,8 @@ def main():
                              "achieved_gbps": it_bytes / (single_ms * 1e-3) / 1e9,
                              "frac_hbm_peak": it_bytes / (single_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
                              "algorithmic_bytes_per_launch": it_bytes,
-                             "traffic": (pmc or {}).get("hbm_bytes_per_fused_launch")},
+                             "traffic": (pmc or {}).get("hbm_bytes_per_fused_launch"),
+                             "mfma_pmc": mfma_summary(mf, "fused")},
         "allgather_costs_ms": gather_ms,
         "allgather_check": gathered,
         "cpu_baseline": None,
