@@ -323,10 +323,20 @@ __device__ FwdOut lq_forward_wave_ring(const LQParams& P, int b0, int B, int T, 
       p2 = reinterpret_cast<const char*>(u + tr(m / 2) * T * NU + 2 * (m % 2));
       s2 = NU * 8;
     }
+#if ILQR_FW_ABLATE & 8  // probe only: x / u / x_traj reads served from the K rows (cache)
+    if (l >= 32) {
+      p2 = reinterpret_cast<const char*>(Kg + tr(0) * T * NU * NX + 2 * (l % 24));
+      s2 = NU * NX * 8;
+    }
+#endif
     const int l3 = l & 31;
     if (l3 < 24) {
       p3 = reinterpret_cast<const char*>(xt0 + tr(l3 / 6) * (T + 1) * NX + 2 * (l3 % 6));
       s3 = NX * 8;
+#if ILQR_FW_ABLATE & 8
+      p3 = reinterpret_cast<const char*>(Kg + tr(0) * T * NU * NX + 2 * (l3 % 24));
+      s3 = NU * NX * 8;
+#endif
     } else {
       const int m = l3 - 24;
       p3 = reinterpret_cast<const char*>(dg + tr(m / 2) * T * NU + 2 * (m % 2));
