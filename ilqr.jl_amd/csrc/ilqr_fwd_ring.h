@@ -254,6 +254,9 @@ __device__ FwdOut lq_forward_wave_ring(const LQParams& P, int b0, int B, int T, 
   static_assert(NX == 12 && NU == 4, "slot layout and lane map are written for nx = 12, nu = 4");
   static_assert(R > PF && PF >= 1, "the slot being refilled must not be the one being read");
   constexpr uint32_t OOR = 0x80000000u;
+  // wave-uniform in an SGPR: the result stores' buffer resources derive from it (a VGPR
+  // resource makes every store a readfirstlane waterfall loop)
+  b0 = __builtin_amdgcn_readfirstlane(b0);
   const int l = threadIdx.x & 63;
   const int g = l >> 4;
   const int j = l & 15;
@@ -527,6 +530,7 @@ __device__ FwdOut lq_forward_wave_mfma(const LQParams& P, int b0, int B, int T, 
   constexpr uint32_t OOR = 0x80000000u;
   const int l = threadIdx.x & 63;
   const int rho = l >> 4, beta = (l >> 2) & 3, kap = l & 3;
+  b0 = __builtin_amdgcn_readfirstlane(b0);  // wave-uniform: SGPR buffer resources, no waterfall
   const int nt = B - b0 < 4 ? B - b0 : 4;
   const int bb = b0 + (beta < nt ? beta : 0);  // absent slots alias trajectory b0 (never stored)
   const bool active = beta < nt && ((run >> beta) & 1u);
