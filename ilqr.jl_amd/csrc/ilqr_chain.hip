@@ -1577,8 +1577,10 @@ __device__ unsigned chain_backward4_wave(const ChainK<V, 2>& P, int b0, int B, u
       d = -(hi * gu);
       (void)Hl; (void)luu;
     }
-    ch_st<V>(K, rK, kv, kv == DEAD ? 0u : (uint32_t)(t * NU * NX * W));
-    ch_st<V>(d, rD, dv, dv == DEAD ? 0u : (uint32_t)(t * NU * W));
+    // wave-uniform soffset (a per-lane one makes each store a readfirstlane waterfall
+    // loop); a DEAD voffset stays out of range whatever the step
+    ch_st<V>(K, rK, kv, (uint32_t)(t * NU * NX * W));
+    ch_st<V>(d, rD, dv, (uint32_t)(t * NU * W));
     const double Wk = fma(mu, K, -G), Wd = fma(mu, d, -gu);
     const double Sf = ch_mfn(K, Wk, Z);
     const double Sm = __builtin_bit_cast(double, u2v{(unsigned)__builtin_amdgcn_ds_bpermute(tr_src, (int)__builtin_bit_cast(u2v, Sf).x),
