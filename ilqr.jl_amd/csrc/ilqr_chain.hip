@@ -1514,7 +1514,7 @@ __device__ unsigned chain_backward4_wave(const ChainK<V, 2>& P, int b0, int B, u
   const auto rD = buffer_rsrc(dg + (size_t)b0 * T * NU, (uint32_t)(nslot * T * NU * W));
   const uint32_t kv = (live && ru) ? (uint32_t)((beta * T * NU * NX + rho * NX + kap) * W) : DEAD;
   const uint32_t dv = (live && ru && kap == 0) ? (uint32_t)((beta * T * NU + rho) * W) : DEAD;
-  const int tr_src = (16 * kap + 4 * beta + rho) * 4;
+  const double Id = rho == kap ? 1.0 : 0.0;  // the identity block
   double* Hl = lds + beta * 16;
 
   constexpr int PF = CH_BW4_PF;
@@ -1583,8 +1583,9 @@ __device__ unsigned chain_backward4_wave(const ChainK<V, 2>& P, int b0, int B, u
     ch_st<V>(d, rD, dv, (uint32_t)(t * NU * W));
     const double Wk = fma(mu, K, -G), Wd = fma(mu, d, -gu);
     const double Sf = ch_mfn(K, Wk, Z);
-    const double Sm = __builtin_bit_cast(double, u2v{(unsigned)__builtin_amdgcn_ds_bpermute(tr_src, (int)__builtin_bit_cast(u2v, Sf).x),
-                                                     (unsigned)__builtin_amdgcn_ds_bpermute(tr_src, (int)__builtin_bit_cast(u2v, Sf).y)});
+    // Sfᵀ on the MFMA (ch_mf(Sf, I, 0), exact): its ≈50-cycle result instead of a
+    // ds_bpermute round trip on the recursion's chain
+    const double Sm = ch_mf(Sf, Id, 0.0);
     S = rho <= kap ? Sf : Sm;                                      // upper triangle, mirrored
     s = ch_mfn(K, Wd, gx);
     Kl = K; dl = d;

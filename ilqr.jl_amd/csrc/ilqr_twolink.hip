@@ -289,12 +289,6 @@ __device__ __forceinline__ double mfa(double a, double b, double c) {
 __device__ __forceinline__ double mfa_n(double a, double b, double c) {  // −aᵀb + c
   return __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c, 0, 0, 1);
 }
-__device__ __forceinline__ double lane_perm2(double v, int src_byte) {
-  u2v p = __builtin_bit_cast(u2v, v);
-  p.x = (unsigned)__builtin_amdgcn_ds_bpermute(src_byte, (int)p.x);
-  p.y = (unsigned)__builtin_amdgcn_ds_bpermute(src_byte, (int)p.y);
-  return __builtin_bit_cast(double, p);
-}
 
 // Slots whose bit in `active` is clear, or past B, compute on clamped data and store
 // nothing. Returns the NaN slots (bit β). As in ilqr_bw4.hip, a NaN in any K_t or d_t
@@ -338,7 +332,7 @@ __device__ unsigned tl_backward4_wave(const TwoLinkParams& P, int b0, int B, uns
   const auto rD = buffer_rsrc(dg + (size_t)b0 * T * NU, (uint32_t)(nslot * T * NU * 8));
   const uint32_t kv = (live && ru) ? (uint32_t)((beta * T * NU * TL_NX + rho * TL_NX + kap) * 8) : 0x80000000u;
   const uint32_t dv = (live && ru && kap == 0) ? (uint32_t)((beta * T * NU + rho) * 8) : 0x80000000u;
-  const int tr_src = (16 * kap + 4 * beta + rho) * 4;  // lane of element [κ][ρ]
+  const double Id = rho == kap ? 1.0 : 0.0;            // the identity block
   double* Hl = lds + beta * 16;
 
   // inputs TL_BW4_PF steps ahead in a register ring (a step is ≈0.5 µs, HBM latency
@@ -398,7 +392,9 @@ __device__ unsigned tl_backward4_wave(const TwoLinkParams& P, int b0, int B, uns
     const double W = fma(mu, K, -G), Wd = fma(mu, d, -gu);
     const double Sf = mfa_n(K, W, Z);                             // Qxx − KᵀW_K
     // S as the reference's symmetric matrix: the upper triangle, mirrored
-    const double Sm = lane_perm2(Sf, tr_src);
+    // (the transpose on the MFMA, mfa(Sf, I, 0) = Sfᵀ exactly: a ≈50-cycle result where
+    // a ds_bpermute round trip sat on the recursion's chain)
+    const double Sm = mfa(Sf, Id, 0.0);
     S = rho <= kap ? Sf : Sm;
     s = mfa_n(K, Wd, gx);                                         // lx + Aᵀs − KᵀW_d
     Kl = K; dl = d;
