@@ -1,0 +1,72 @@
+"""ISA regression guards for the headline kernels (CPU only: hipcc cross-compiles
+gfx950 here). Compiles ilqr_bw4.hip (the fused iteration, the backward) with the
+product flags and -save-temps, then checks the generated gfx950 assembly for two
+code-generation traps found by reading the ISA (late round 2):
+  * waterfall loops — a buffer access whose resource or scalar offset the compiler
+    cannot prove wave-uniform becomes a `v_readfirstlane` / `s_and_saveexec` /
+    `s_cbranch_execnz` loop around every load or store (the ring forward's x̄/ū stores
+    and the chain backward's gain stores were such loops);
+  * scratch (private-memory spills) in the step loops."""
+import os
+import re
+import shutil
+import subprocess
+
+import pytest
+
+CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "ilqr.jl_amd", "csrc")
+HIPCC = "/opt/rocm/bin/hipcc"
+
+
+def _functions(asm):
+    """{mangled kernel name: list of instruction lines}"""
+    out, cur = {}, None
+    for line in asm.split("\n"):
+        m = re.match(r"^(_Z\S+):", line)
+        if m:
+            cur = m.group(1)
+            out[cur] = []
+            continue
+        if line.startswith(".Lfunc_end"):
+            cur = None
+        elif cur is not None:
+            out[cur].append(re.sub(r"\s+", " ", line.strip()))
+    return out
+
+
+def _waterfalls(body):
+    """loops that branch back on execnz around a readfirstlane and a memory access"""
+    labels = {}
+    for k, l in enumerate(body):
+        m = re.match(r"^(\.LBB\w+):", l)
+        if m:
+            labels[m.group(1)] = k
+    found = []
+    for k, l in enumerate(body):
+        m = re.search(r"s_cbranch_execnz (\.LBB\w+)", l)
+        if m and labels.get(m.group(1), 1 << 30) < k:
+            seg = body[labels[m.group(1)]:k + 1]
+            if any("v_readfirstlane" in x for x in seg) and any(x.startswith(("buffer_", "global_")) for x in seg):
+                found.append(k)
+    return found
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC) and shutil.which("hipcc") is None, reason="no hipcc")
+def test_headline_kernels_have_no_waterfall_loops_or_scratch(tmp_path):
+    hipcc = HIPCC if os.path.exists(HIPCC) else shutil.which("hipcc")
+    cmd = [hipcc, "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-mllvm", "-amdgpu-mfma-vgpr-form=1",
+           "-save-temps", "-c", os.path.join(CSRC, "ilqr_bw4.hip"), "-o", str(tmp_path / "bw4.o")]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=900, cwd=tmp_path)
+    assert r.returncode == 0, r.stderr[-2000:]
+    asm_file = [f for f in os.listdir(tmp_path) if f.endswith("gfx950.s")]
+    assert asm_file, os.listdir(tmp_path)
+    funcs = _functions(open(tmp_path / asm_file[0]).read())
+    # the default (row-form forward) fused iteration, the fit's backward leg and the
+    # ilqr_backward kernel
+    checked = [n for n in funcs if re.search(r"lq_iter_fused4_kernelILb0E|lq_iter_backward4_kernel|"
+                                             r"lq_backward4_kernelILi0E", n)]
+    assert len(checked) == 3, sorted(funcs)
+    for n in checked:
+        body = funcs[n]
+        assert not _waterfalls(body), f"{n}: waterfall loop(s) at {_waterfalls(body)}"
+        assert not [x for x in body if x.startswith("scratch_")], f"{n}: scratch accesses"
