@@ -44,6 +44,11 @@ namespace {
 #ifndef ILQR_BW4_MFMA_T
 #define ILQR_BW4_MFMA_T 1
 #endif
+// μ folded into H's MFMA accumulator (R + Rᵀ + μI): no per-step pivot adds (backward
+// 103.8 -> 102.7 us, tools/bw_alt.sh; 0 = the add in the factorisation)
+#ifndef ILQR_BW4_MU_IN_H
+#define ILQR_BW4_MU_IN_H 1
+#endif
 
 constexpr int BW4_SLOTS = 4;          // trajectories per wave
 constexpr int BW4_WAVES = 4;          // waves per workgroup
@@ -124,6 +129,7 @@ __device__ unsigned lq_backward4_wave(const LQParams& P, int b0, int B, unsigned
     for (int I = 0; I < 3; ++I) L[K][I] = Qb[r * NX + 4 * I + kap] + Qb[(4 * I + kap) * NX + r];
   }
   const double LR = Rb[rho * NU + kap] + Rb[kap * NU + rho];
+  [[maybe_unused]] const double LRmu = rho == kap ? LR + mu : LR;  // R + Rᵀ + μI
 
   // the lane permutation ρ ↔ κ (block transpose within each slot)
   const int tr_src = (16 * kap + 4 * beta + rho) * 4;
@@ -245,7 +251,7 @@ __device__ unsigned lq_backward4_wave(const LQParams& P, int b0, int B, unsigned
 #pragma unroll
         for (int K = I + 1; K < 3; ++K) Y[I][J] = mf4(S[K][I], F[K][J], Y[I][J]);
     // H = R + Rᵀ + BᵀSB → LDS, read back whole by the slot's lanes
-    double H = LR;
+    double H = ILQR_BW4_MU_IN_H ? LRmu : LR;
 #pragma unroll
     for (int K = 0; K < 3; ++K) H = mf4(F[K][3], Y[K][3], H);
     Hl[rho * 4 + kap] = H;
@@ -326,6 +332,8 @@ __device__ unsigned lq_backward4_wave(const LQParams& P, int b0, int B, unsigned
       }
 
     // (H + μI) = L D Lᵀ in every lane of the slot (feedback_parameters :207-218)
+    // (read right after the write instead — its latency behind the gradient, G and
+    // Qxx MFMAs — measured slower: 103.8 -> 105.6 us)
     wave_lds_fence();
     double h[4][4];
 #pragma unroll
@@ -342,7 +350,7 @@ __device__ unsigned lq_backward4_wave(const LQParams& P, int b0, int B, unsigned
         for (int k = 0; k < i; ++k) f.l[i][k] = h[i][k] * 1e-3;
       }
     } else {
-      f.factor(h, mu);
+      f.factor<!ILQR_BW4_MU_IN_H>(h, mu);
     }
     // M = L⁻¹ (unit lower)
     double Mf[4][4];

@@ -103,11 +103,13 @@ template <int NU, int NEWTON = 2>
 struct LDLT {
   double l[NU][NU];
   double dinv[NU];
+  // ADD_MU = false: h already holds H + μI (the caller folded μ into H's accumulator)
+  template <bool ADD_MU = true>
   __device__ __forceinline__ void factor(const double (&h)[NU][NU], double mu) {
     double t[NU][NU];  // t[i][k] = L[i][k] · D[k]
 #pragma unroll
     for (int k = 0; k < NU; ++k) {
-      double dk = h[k][k] + mu;
+      double dk = ADD_MU ? h[k][k] + mu : h[k][k];
 #pragma unroll
       for (int p = 0; p < k; ++p) dk = fma(-l[k][p], t[k][p], dk);
       dinv[k] = rcp<NEWTON>(dk);

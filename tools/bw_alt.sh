@@ -1,7 +1,10 @@
 #!/bin/bash
 # Alternate builds of the backward file (ilqr_bw4.hip) for A/B timing with
 # tools/fused_probe.py <lib>: tools/fwalt/libilqr_hip_<name>.so
-#   bwt0: block transposes by ds_bpermute (ILQR_BW4_MFMA_T=0) instead of the MFMA
+#   base: the product flags
+#   mu:   μ folded into H's accumulator (ILQR_BW4_MU_IN_H=1)
+#   hre:  H read back from LDS right after its write (ILQR_BW4_HREAD_EARLY=1)
+#   both: the two together
 set -e
 cd "$(dirname "$0")/.."
 make -C ilqr.jl_amd/csrc > /dev/null
@@ -14,4 +17,8 @@ build() {  # build <name> <flags...>
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o tools/fwalt/libilqr_hip_$n.so $O/ilqr_lq.hip.o tools/fwalt/bw4_$n.o \
     $O/ilqr_twolink.hip.o $O/ilqr_tiles.hip.o $O/ilqr_chain.hip.o $O/ilqr_abi.cpp.o $O/ilqr_multi.cpp.o -lpthread
 }
-build bwt0 -DILQR_BW4_MFMA_T=0
+if [ $# -gt 0 ]; then build "$@"; exit 0; fi
+build base
+build mu -DILQR_BW4_MU_IN_H=1
+build hre -DILQR_BW4_HREAD_EARLY=1
+build both -DILQR_BW4_MU_IN_H=1 -DILQR_BW4_HREAD_EARLY=1

@@ -100,6 +100,48 @@ def twolink_dynamics_flops(nu=2):
     return Counter.n
 
 
+def chain_closed_form_flops(nu=1):
+    """Primal FLOPs of one RK4 step of the 2-joint chain's closed form, the evaluator the
+    iteration kernels run by default (ilqr_chain.hip chain_qdd_trig / chain_xdot_trig:
+    M(q₂) and dM/dq₂ as trigonometric polynomials, bilinear gravity, the Christoffel
+    velocity term, a 2×2 solve). The recursion's count (chain_dynamics_flops) is what the
+    reference's RigidBodyDynamics.jl calls perform; the closed form does ~16× fewer, so
+    a roofline priced on the recursion's count would exceed the peak."""
+    Mc = [[Flop(0.1 * (e + 1) + 0.01 * k) for k in range(5)] for e in range(3)]
+    Gc = [[[Flop(0.2 + 0.01 * (i + a + b)) for b in range(3)] for a in range(3)] for i in range(2)]
+    dt = 0.01
+
+    def xdot(x, u):
+        s1, c1, s2, c2 = x[0].sin(), x[0].cos(), x[1].sin(), x[1].cos()
+        w0, w1 = x[2], x[3]
+        C2, S2 = c2 * c2 - s2 * s2, 2.0 * (s2 * c2)
+        m, dm = [], []
+        for e in range(3):
+            m.append(Mc[e][0] + (((Mc[e][1] * c2 + Mc[e][2] * s2) + Mc[e][3] * C2) + Mc[e][4] * S2))
+            dm.append((Mc[e][2] * c2 - Mc[e][1] * s2) + 2.0 * (Mc[e][4] * C2 - Mc[e][3] * S2))
+        g = []
+        for i in range(2):
+            h = [Gc[i][a][0] + (Gc[i][a][1] * c2 + Gc[i][a][2] * s2) for a in range(3)]
+            g.append(h[0] + (h[1] * c1 + h[2] * s1))
+        p0, p1 = dm[0] * w0 + dm[1] * w1, dm[1] * w0 + dm[2] * w1
+        qq = w0 * p0 + w1 * p1
+        r0 = u[0] - (w1 * p0 + g[0])
+        r1 = (w1 * p1 - 0.5 * qq) + g[1]
+        r1 = u[-1] - r1 if nu > 1 else -r1
+        idet = 1.0 / (m[0] * m[2] - m[1] * m[1])
+        return [w0, w1, (m[2] * r0 - m[1] * r1) * idet, (m[0] * r1 - m[1] * r0) * idet]
+
+    x = [Flop(0.3), Flop(-0.4), Flop(0.5), Flop(0.6)]
+    u = [Flop(0.1), Flop(0.2)][:nu]
+    Counter.n = 0
+    k1 = [dt * v for v in xdot(x, u)]
+    k2 = [dt * v for v in xdot([x[i] + 0.5 * k1[i] for i in range(4)], u)]
+    k3 = [dt * v for v in xdot([x[i] + 0.5 * k2[i] for i in range(4)], u)]
+    k4 = [dt * v for v in xdot([x[i] + k3[i] for i in range(4)], u)]
+    [x[i] + (1.0 / 6.0) * (((k1[i] + 2.0 * k2[i]) + 2.0 * k3[i]) + k4[i]) for i in range(4)]
+    return Counter.n
+
+
 def dual_factor(nd):
     """FLOPs of a forward-mode dual evaluation per primal FLOP (mix-weighted average of
     add 1+ND, mul 1+3ND, div 2+4ND, constant scaling 1+ND): ~1 + 2ND."""
@@ -121,4 +163,5 @@ if __name__ == "__main__":
     from ilqr_amd.chain import rbd_2dof_problem
     for nu in (2, 1):
         print("2-link nu", nu, "RK4 flops", twolink_dynamics_flops(nu))
-        print("chain 2dof nu", nu, "RK4 flops", chain_dynamics_flops(rbd_2dof_problem(nu)))
+        print("chain 2dof nu", nu, "RK4 flops", chain_dynamics_flops(rbd_2dof_problem(nu)),
+              "closed form", chain_closed_form_flops(nu))
