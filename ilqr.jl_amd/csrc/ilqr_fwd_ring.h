@@ -129,6 +129,20 @@ __device__ __forceinline__ double dpp_dot16_bd(double src, const double (&c)[12]
 #ifndef ILQR_FW_ABLATE
 #define ILQR_FW_ABLATE 0
 #endif
+// cache policy of the ring forward's memory traffic (probe: tools/fw_alt.sh): the aux
+// bits of the x̄/ū result stores (gfx950: 1 sc0, 2 nt, 16 sc1) and a " nt" hint on the
+// slot loads (every input the forward streams is dead after its step)
+#ifndef ILQR_FW_ST_AUX
+#define ILQR_FW_ST_AUX 0
+#endif
+#ifndef ILQR_FW_LD_NT
+#define ILQR_FW_LD_NT 0
+#endif
+#if ILQR_FW_LD_NT
+#define ILQR_FW_LDS_OP "global_load_lds_dwordx4 %0, off nt"
+#else
+#define ILQR_FW_LDS_OP "global_load_lds_dwordx4 %0, off"
+#endif
 
 // Row broadcasts through LDS instead of DPP: every lane writes its value to the wave's
 // scratch, each lane reads its row's 16 values back (ds_read_b128, a broadcast per
@@ -326,6 +340,10 @@ __device__ FwdOut lq_forward_wave_ring(const LQParams& P, int b0, int B, int T, 
       p2 = reinterpret_cast<const char*>(u + tr(m / 2) * T * NU + 2 * (m % 2));
       s2 = NU * 8;
     }
+#if ILQR_FW_ABLATE & 16  // probe only: every step reads step 0's K rows (cache)
+    s1 = 0;
+    if (l < 32) s2 = 0;
+#endif
 #if ILQR_FW_ABLATE & 8  // probe only: x / u / x_traj reads served from the K rows (cache)
     if (l >= 32) {
       p2 = reinterpret_cast<const char*>(Kg + tr(0) * T * NU * NX + 2 * (l % 24));
@@ -351,9 +369,9 @@ __device__ FwdOut lq_forward_wave_ring(const LQParams& P, int b0, int B, int T, 
     uint32_t tt = (uint32_t)(t < T ? t : T - 1);  // clamped: loaded, never read
     asm volatile("" : "+s"(tt));  // no hoisting of the prologue's addresses out of the trial loop
     const uint32_t m0 = ring_lds + (uint32_t)((t % R) * RING_SLOT * 8);
-    asm volatile("global_load_lds_dwordx4 %0, off" ::"v"(p1 + (size_t)tt * s1), "{m0}"(m0) : "memory");
-    asm volatile("global_load_lds_dwordx4 %0, off" ::"v"(p2 + (size_t)tt * s2), "{m0}"(m0 + 1024) : "memory");
-    asm volatile("global_load_lds_dwordx4 %0, off" ::"v"(p3 + (size_t)tt * s3), "{m0}"(m0 + 2048) : "memory");
+    asm volatile(ILQR_FW_LDS_OP ::"v"(p1 + (size_t)tt * s1), "{m0}"(m0) : "memory");
+    asm volatile(ILQR_FW_LDS_OP ::"v"(p2 + (size_t)tt * s2), "{m0}"(m0 + 1024) : "memory");
+    asm volatile(ILQR_FW_LDS_OP ::"v"(p3 + (size_t)tt * s3), "{m0}"(m0 + 2048) : "memory");
   };
   // vmcnt immediates (gfx9: vmcnt[3:0] | expcnt 7 << 4 | lgkmcnt 15 << 8 | vmcnt[5:4] << 14):
   // per step the wave issues 3 slot loads then 2 result stores, so slot t is
@@ -456,8 +474,8 @@ __device__ FwdOut lq_forward_wave_ring(const LQParams& P, int b0, int B, int T, 
 #if ILQR_FW_ABLATE & 2  // probe only: no result stores
       if (t < 0)
 #endif
-      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, z), rXN, ox, (uint32_t)t * NX * 8, 0);
-      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, z), rUN, ou, (uint32_t)t * NU * 8, 0);
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, z), rXN, ox, (uint32_t)t * NX * 8, ILQR_FW_ST_AUX);
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, z), rUN, ou, (uint32_t)t * NU * 8, ILQR_FW_ST_AUX);
       du2 = fma(e, e, du2);
       xb = xa.sum();
       // slot t + 1 (past the horizon: a clamped step's slot, read and never used)
@@ -467,7 +485,7 @@ __device__ FwdOut lq_forward_wave_ring(const LQParams& P, int b0, int B, int T, 
     const int tp = T < PF ? T : PF;
     for (int t = 0; t < tp - 1; ++t) step(t, std::integral_constant<int, N_PRO>{});
     for (int t = tp - 1; t < T; ++t) step(t, std::integral_constant<int, N_SS>{});
-    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, xb), rXN, ox, (uint32_t)T * NX * 8, 0);
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, xb), rXN, ox, (uint32_t)T * NX * 8, ILQR_FW_ST_AUX);
     // Qf row (x lanes; u lanes read row 0 and zero it): one base address, 6 × 16 B
     const double2* qrow = reinterpret_cast<const double2*>(Qfb + jx * NX);
     asm volatile("" : "+v"(qrow));  // keep the row address from being hoisted as 12 pointers
@@ -589,9 +607,9 @@ __device__ FwdOut lq_forward_wave_mfma(const LQParams& P, int b0, int B, int T, 
     uint32_t tt = (uint32_t)(t < T ? t : T - 1);
     asm volatile("" : "+s"(tt));
     const uint32_t m0 = ring_lds + (uint32_t)((t % R) * RING_SLOT * 8);
-    asm volatile("global_load_lds_dwordx4 %0, off" ::"v"(p1 + (size_t)tt * s1), "{m0}"(m0) : "memory");
-    asm volatile("global_load_lds_dwordx4 %0, off" ::"v"(p2 + (size_t)tt * s2), "{m0}"(m0 + 1024) : "memory");
-    asm volatile("global_load_lds_dwordx4 %0, off" ::"v"(p3 + (size_t)tt * s3), "{m0}"(m0 + 2048) : "memory");
+    asm volatile(ILQR_FW_LDS_OP ::"v"(p1 + (size_t)tt * s1), "{m0}"(m0) : "memory");
+    asm volatile(ILQR_FW_LDS_OP ::"v"(p2 + (size_t)tt * s2), "{m0}"(m0 + 1024) : "memory");
+    asm volatile(ILQR_FW_LDS_OP ::"v"(p3 + (size_t)tt * s3), "{m0}"(m0 + 2048) : "memory");
   };
   constexpr int N_SS = 5 * PF - 3, N_PRO = 3 * PF - 3;
   auto wait_slot = [](auto n) {
@@ -669,8 +687,8 @@ __device__ FwdOut lq_forward_wave_mfma(const LQParams& P, int b0, int B, int T, 
 #pragma unroll
       for (int I = 0; I < 3; ++I)
         __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, xb[I]), rXN, ox,
-                                              (uint32_t)(t * NX * 8 + 32 * I), 0);
-      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, ub), rUN, ou, (uint32_t)t * NU * 8, 0);
+                                              (uint32_t)(t * NX * 8 + 32 * I), ILQR_FW_ST_AUX);
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, ub), rUN, ou, (uint32_t)t * NU * 8, ILQR_FW_ST_AUX);
       const double e = ub - uk;
       du2 = fma(e, e, du2);
       // x̄ₖ₊₁ = A x̄ₖ + B ūₖ (:74)
@@ -686,7 +704,7 @@ __device__ FwdOut lq_forward_wave_mfma(const LQParams& P, int b0, int B, int T, 
 #pragma unroll
     for (int I = 0; I < 3; ++I)
       __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, xb[I]), rXN, ox,
-                                            (uint32_t)(T * NX * 8 + 32 * I), 0);
+                                            (uint32_t)(T * NX * 8 + 32 * I), ILQR_FW_ST_AUX);
     // final_cost(x̄_N) = x̄ᵀQf x̄ on the raw state (:192)
     {
       const double* Qfb = P.Qf + (size_t)bb * NX * NX;

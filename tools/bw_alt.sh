@@ -2,7 +2,7 @@
 # Alternate builds of the backward file (ilqr_bw4.hip) for A/B timing with
 # tools/fused_probe.py <lib>: tools/fwalt/libilqr_hip_<name>.so
 #   base: the product flags
-#   mu:   μ folded into H's accumulator (ILQR_BW4_MU_IN_H=1)
+#   mu0:  μ added in the factorisation (ILQR_BW4_MU_IN_H=0; the product folds it into H)
 #   hre:  H read back from LDS right after its write (ILQR_BW4_HREAD_EARLY=1)
 #   both: the two together
 set -e
@@ -19,6 +19,4 @@ build() {  # build <name> <flags...>
 }
 if [ $# -gt 0 ]; then build "$@"; exit 0; fi
 build base
-build mu -DILQR_BW4_MU_IN_H=1
-build hre -DILQR_BW4_HREAD_EARLY=1
-build both -DILQR_BW4_MU_IN_H=1 -DILQR_BW4_HREAD_EARLY=1
+build mu0 -DILQR_BW4_MU_IN_H=0

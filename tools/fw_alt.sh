@@ -1,22 +1,19 @@
 #!/bin/bash
-# Alternate builds of libilqr_hip.so for tools/fw_scan.py <lib>: the standalone ring
-# forward on one-wave workgroups (ILQR_FW_WAVES=1) and forward ablations
-# (ILQR_FW_ABLATE bits: 1 no cost row, 2 no x̄ stores), the DPP row broadcasts
-# (ILQR_FW_LDS_BCAST=0); the product objects otherwise.
+# Alternate builds of libilqr_hip.so with flags on BOTH files that hold the ring
+# forward (ilqr_lq.hip: the split schedule's forward; ilqr_bw4.hip: the fused
+# iteration), for A/B timing with tools/fused_probe.py <lib> / tools/gpu_bwab.sh:
+#   tools/fw_alt.sh <name> <flags...>   ->  tools/fwalt/libilqr_hip_<name>.so
+# e.g. -DILQR_FW_ST_AUX=2 (nt result stores), -DILQR_FW_LD_NT=1 (nt slot loads),
+# -DILQR_FW_ABLATE=<bits> (timing-only ablations), -DILQR_FW_LDS_BCAST=1.
 set -e
 cd "$(dirname "$0")/.."
 make -C ilqr.jl_amd/csrc > /dev/null
 mkdir -p tools/fwalt
 O=ilqr.jl_amd/lib/obj
-build() {  # build <name> <flags...>
-  local n=$1; shift
-  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 "$@" -c ilqr.jl_amd/csrc/ilqr_lq.hip -o tools/fwalt/ilqr_lq_$n.o
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o tools/fwalt/libilqr_hip_$n.so tools/fwalt/ilqr_lq_$n.o \
-    $O/ilqr_bw4.hip.o $O/ilqr_twolink.hip.o $O/ilqr_tiles.hip.o $O/ilqr_chain.hip.o $O/ilqr_abi.cpp.o $O/ilqr_multi.cpp.o -lpthread
-}
-build w1 -DILQR_FW_WAVES=1 &
-build lds -DILQR_FW_LDS_BCAST=1 &
-build ab1 -DILQR_FW_ABLATE=1 &
-build ab2 -DILQR_FW_ABLATE=2 &
-build ab3 -DILQR_FW_ABLATE=3 &
+n=$1; shift
+F="-O3 -std=c++17 -fPIC --offload-arch=gfx950"
+/opt/rocm/bin/hipcc $F "$@" -c ilqr.jl_amd/csrc/ilqr_lq.hip -o tools/fwalt/lq_$n.o &
+/opt/rocm/bin/hipcc $F -mllvm -amdgpu-mfma-vgpr-form=1 "$@" -c ilqr.jl_amd/csrc/ilqr_bw4.hip -o tools/fwalt/bw4_$n.o &
 wait
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o tools/fwalt/libilqr_hip_$n.so tools/fwalt/lq_$n.o tools/fwalt/bw4_$n.o \
+  $O/ilqr_twolink.hip.o $O/ilqr_tiles.hip.o $O/ilqr_chain.hip.o $O/ilqr_abi.cpp.o $O/ilqr_multi.cpp.o -lpthread
