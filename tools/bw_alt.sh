@@ -3,8 +3,6 @@
 # tools/fused_probe.py <lib>: tools/fwalt/libilqr_hip_<name>.so
 #   base: the product flags
 #   mu0:  μ added in the factorisation (ILQR_BW4_MU_IN_H=0; the product folds it into H)
-#   hre:  H read back from LDS right after its write (ILQR_BW4_HREAD_EARLY=1)
-#   both: the two together
 set -e
 cd "$(dirname "$0")/.."
 make -C ilqr.jl_amd/csrc > /dev/null
