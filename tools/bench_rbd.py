@@ -136,7 +136,8 @@ def main():
         peak = PEAK_TFLOPS[args.dtype]
         kern = {"linearize": (lin_ms, lin_fl), "riccati": (max(bw_ms - lin_ms, 1e-6), ric_fl),
                 "forward": (fw_ms, fw_fl)}
-        roof = {"bound": ("forward latency/issue (one lane per trajectory, closed-form dynamics)"
+        roof = {"bound": ("forward latency/issue (a dependent RK4 chain per trajectory, 4 candidate lanes each, "
+                          "closed-form dynamics)"
                           if s.dynamics_mode == "closed_form" else
                           "forward latency/issue (16 lanes per trajectory)") + ", linearisation VALU issue",
                 "unit": "TFLOP/s", "peak": peak, "peak_dtype": args.dtype,
@@ -148,6 +149,11 @@ def main():
             roof[k] = {"avg_launch_ms": ms_k, "algorithmic_flops": fl,
                        "achieved": fl / (ms_k * 1e-3) / 1e12, "frac": fl / (ms_k * 1e-3) / 1e12 / peak}
         roof["achieved"], roof["frac"] = roof["forward"]["achieved"], roof["forward"]["frac"]
+        # the forward's real bound: T dependent RK4 steps per trajectory (4 line-search
+        # candidate lanes each: 4B of the chip's 65,536 lanes), so its time is T × the
+        # latency of one step — the FLOP fraction is small by construction
+        roof["forward"]["step_latency_ns"] = fw_ms * 1e6 / T
+        roof["forward"]["lanes_busy_frac"] = min(1.0, 4 * B / (1024 * 64))
         res = {"metric": f"batched iLQR iterations/sec (fwd+bwd pass), RBD 2-DoF arm fixed base, "
                          f"nx=4 nu={pr.nu} T={T}",
                "value": 1000.0 / ms, "unit": f"batched iterations/s (batch={B})", "n_gpus": 1,

@@ -108,6 +108,10 @@ def main():
         roof[k]["frac"] = roof[k]["achieved"] / FP64_PEAK_TFLOPS
     roof["achieved"] = roof["forward"]["achieved"]
     roof["frac"] = roof["forward"]["frac"]
+    # the forward's real bound: T dependent RK4 steps per trajectory, so its time is
+    # T × the latency of one step (one wave's instruction stream), whatever the batch
+    roof["forward"]["step_latency_ns"] = fw_ms * 1e6 / T
+    roof["forward"]["lanes_busy_frac"] = min(1.0, 4 * B / (1024 * 64))
     out = {
         "metric": f"batched iLQR iterations/sec (fwd+bwd pass), 2-link arm nx=4 nu={NU} T={T}, batch={B}",
         "value": 1000.0 / ms, "unit": "batched iterations/s (batch=1024)", "n_gpus": 1,
