@@ -49,6 +49,17 @@ namespace {
 #ifndef ILQR_BW4_MU_IN_H
 #define ILQR_BW4_MU_IN_H 1
 #endif
+// the solve's per-lane operands (M[ρ][κ], D⁻¹[ρ]) by 0/1-mask FMAs instead of select
+// chains: every VALU instruction beside the MFMAs costs the wave ≈6 cycles of issue,
+// b32 selects as much as f64 FMAs (tools/ubench_mix.hip)
+// the lower S blocks as MFMA transposes of the upper ones (mf4(a, I, 0) = aᵀ, exact)
+// instead of ds_bpermute lane permutations
+#ifndef ILQR_BW4_SLOW_MFMA
+#define ILQR_BW4_SLOW_MFMA 1
+#endif
+#ifndef ILQR_BW4_SEL_FMA
+#define ILQR_BW4_SEL_FMA 1
+#endif
 
 constexpr int BW4_SLOTS = 4;          // trajectories per wave
 constexpr int BW4_WAVES = 4;          // waves per workgroup
@@ -138,6 +149,16 @@ __device__ unsigned lq_backward4_wave(const LQParams& P, int b0, int B, unsigned
   // (ILQR_BW4_MFMA_T: a ≈50-cycle MFMA result instead of a ds_bpermute round trip on
   // the solve's and the symmetrisation's dependent chains)
   [[maybe_unused]] const double Id = rho == kap ? 1.0 : 0.0, Ih = rho == kap ? 0.5 : 0.0;
+  // lane masks of the solve's per-lane entries (ILQR_BW4_SEL_FMA): M[i][j] (i > j) at
+  // lane (ρ, κ) = (i, j), the unit diagonal, D⁻¹[i] at row ρ = i
+  [[maybe_unused]] double sel_m[4][4], sel_r[4];
+  [[maybe_unused]] const double sel_d = Id;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    sel_r[i] = rho == i ? 1.0 : 0.0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) sel_m[i][j] = (rho == i && kap == j) ? 1.0 : 0.0;
+  }
 
   // terminal value function (final_cost_quadratization :134-153): S = Qf + Qfᵀ, s = S x_N
   double S[3][3], s[3];
@@ -213,7 +234,14 @@ __device__ unsigned lq_backward4_wave(const LQParams& P, int b0, int B, unsigned
   __builtin_amdgcn_s_waitcnt(0);
   if constexpr (LZ4 && (ABL & 256) == 0) lz_block(T - 1);
 
-  for (int t = T - 1; t >= 0; --t) {
+  // lane-permutation sources of the L z columns, one per step of a block of four
+  int lz_src[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) lz_src[j] = ((l & ~3) | j) * 4;
+  // one step of the recursion; JJ = (T − 1 − t) mod 4 (the step's column of its L z block)
+  // is static: the loop below runs the steps four at a time
+  auto step = [&](const int t, auto jc) {
+    constexpr int JJ = decltype(jc)::value;
     if constexpr ((ABL & 64) != 0) {
 #pragma unroll
       for (int k = 0; k < 4; ++k) zn[k] = zc[k] * 0.5;
@@ -225,9 +253,8 @@ __device__ unsigned lq_backward4_wave(const LQParams& P, int b0, int B, unsigned
     // behind the S·F products
     [[maybe_unused]] double lzp[4];
     if constexpr (LZ4 && (ABL & 256) == 0) {
-      const int src = ((l & ~3) | ((T - 1 - t) & 3)) * 4;
 #pragma unroll
-      for (int I = 0; I < 4; ++I) lzp[I] = lane_perm(Lzq[I], src);
+      for (int I = 0; I < 4; ++I) lzp[I] = lane_perm(Lzq[I], lz_src[JJ]);
     }
     // Y = S·F, column block 3 (B) first: H needs it. Each sum runs over K = 0, 1, 2;
     // its K ≤ I terms read stored upper blocks S[K][I], its K > I terms the lower blocks
@@ -259,7 +286,7 @@ __device__ unsigned lq_backward4_wave(const LQParams& P, int b0, int B, unsigned
     // gradient [lx + Aᵀs | lu + Bᵀs] (:181, :269)
     double gv[4];
     if constexpr (LZ4) {
-      const int j = (T - 1 - t) & 3;
+      constexpr int j = JJ;
       double lz[4];
       if constexpr ((ABL & 256) != 0) {  // through LDS: column j of each block, replicated
         if (j == 0) {  // L z for steps t .. t-3, then the next four steps' z
@@ -361,14 +388,28 @@ __device__ unsigned lq_backward4_wave(const LQParams& P, int b0, int B, unsigned
     Mf[3][1] = fma(f.l[3][2], f.l[2][1], -f.l[3][1]);
     Mf[3][0] = fma(-f.l[3][2], Mf[2][0], fma(-f.l[3][1], Mf[1][0], -f.l[3][0]));
     // this lane's entries: Mn = M[ρ][κ], D⁻¹[ρ]
-    double Mn = rho == kap ? 1.0 : 0.0;
+    double Mn, dsel;
+    if constexpr (ILQR_BW4_SEL_FMA) {
+      // Σ (0/1 lane mask) × entry: exact (x·1 = x, x·0 = ±0 and x ± 0 = x), so the same
+      // bits as the selects, in 10 f64 ops where the selects took 18 b32 ones
+      Mn = sel_d;
 #pragma unroll
-    for (int i = 1; i < 4; ++i)
+      for (int i = 1; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < i; ++j) Mn = (rho == i && kap == j) ? Mf[i][j] : Mn;
-    double dsel = f.dinv[0];
+        for (int j = 0; j < i; ++j) Mn = fma(sel_m[i][j], Mf[i][j], Mn);
+      dsel = sel_r[0] * f.dinv[0];
 #pragma unroll
-    for (int i = 1; i < 4; ++i) dsel = rho == i ? f.dinv[i] : dsel;
+      for (int i = 1; i < 4; ++i) dsel = fma(sel_r[i], f.dinv[i], dsel);
+    } else {
+      Mn = rho == kap ? 1.0 : 0.0;
+#pragma unroll
+      for (int i = 1; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < i; ++j) Mn = (rho == i && kap == j) ? Mf[i][j] : Mn;
+      dsel = f.dinv[0];
+#pragma unroll
+      for (int i = 1; i < 4; ++i) dsel = rho == i ? f.dinv[i] : dsel;
+    }
 
     // K_aug = −(H + μI)⁻¹ [G | g] = −(D⁻¹M)ᵀ (M [G | g]): the LDLᵀ solve's two
     // triangular sweeps as two MFMA stages. A operands: M·  wants M[κ][ρ] (the
@@ -421,7 +462,8 @@ __device__ unsigned lq_backward4_wave(const LQParams& P, int b0, int B, unsigned
 #pragma unroll
     for (int I = 0; I < 3; ++I)
 #pragma unroll
-      for (int J = I + 1; J < 3; ++J) S[J][I] = (ABL & 2) ? S[I][J] : lane_perm(S[I][J], tr_src);
+      for (int J = I + 1; J < 3; ++J)
+        S[J][I] = (ABL & 2) ? S[I][J] : ILQR_BW4_SLOW_MFMA ? mf4(S[I][J], Id, 0.0) : lane_perm(S[I][J], tr_src);
     if constexpr (!LZ4) {
 #pragma unroll
       for (int k = 0; k < 4; ++k) zc[k] = zn[k];
@@ -429,10 +471,24 @@ __device__ unsigned lq_backward4_wave(const LQParams& P, int b0, int B, unsigned
 #pragma unroll
     for (int J = 0; J < 4; ++J) Klast[J] = Kg[J];
     // the next step starts a block of four: its L z now (LZ4)
-    if constexpr (LZ4 && (ABL & 256) == 0) {
-      if (((T - t) & 3) == 0 && t > 0) lz_block(t - 1);
+    if constexpr (LZ4 && (ABL & 256) == 0 && JJ == 3) {
+      if (t > 0) lz_block(t - 1);
     }
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  using I3 = std::integral_constant<int, 3>;
+  int t = T - 1;
+  for (; t >= 3; t -= 4) {
+    step(t, I0{});
+    step(t - 1, I1{});
+    step(t - 2, I2{});
+    step(t - 3, I3{});
   }
+  if (t >= 0) step(t, I0{});
+  if (t >= 1) step(t - 1, I1{});
+  if (t >= 2) step(t - 2, I2{});
   bool nan = false;
 #pragma unroll
   for (int J = 0; J < 4; ++J) nan |= __builtin_isnan(Klast[J]);
