@@ -19,6 +19,7 @@ __global__ __launch_bounds__(256) void k(double* out, long long* cyc) {
   double a0 = threadIdx.x, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, x = 1.0 + threadIdx.x * 1e-3, y = 0.5;
   double f0 = 1, f1 = 2, f2 = 3, f3 = 4;
   unsigned u0 = threadIdx.x, u1 = u0 + 1, u2 = u0 + 2, u3 = u0 + 3;
+  const int ad = ((threadIdx.x & ~3) | 1) * 4;
   long long t0 = __builtin_readcyclecounter();
   for (int it = 0; it < 16; ++it) {
     if constexpr (KIND == 0) {  // MFMAs alone
@@ -47,6 +48,18 @@ __global__ __launch_bounds__(256) void k(double* out, long long* cyc) {
                            "v_fma_f32 %[u2], %[u2], %[u3], %[u0]\n\t"
                            "v_fma_f32 %[u3], %[u3], %[u0], %[u1]\n\t")
                    : AOUT, [u0] "+v"(u0), [u1] "+v"(u1), [u2] "+v"(u2), [u3] "+v"(u3) : XIN);
+    } else if constexpr (KIND == 7) {  // + ds_bpermute_b32 (results consumed after the group)
+      asm volatile(REP8(MF "ds_bpermute_b32 %[u0], %[ad], %[u1]\n\t"
+                           "ds_bpermute_b32 %[u1], %[ad], %[u2]\n\t"
+                           "ds_bpermute_b32 %[u2], %[ad], %[u3]\n\t"
+                           "ds_bpermute_b32 %[u3], %[ad], %[u0]\n\t") "s_waitcnt lgkmcnt(0)\n\t"
+                   : AOUT, [u0] "+v"(u0), [u1] "+v"(u1), [u2] "+v"(u2), [u3] "+v"(u3) : XIN, [ad] "v"(ad));
+    } else if constexpr (KIND == 8) {  // + v_mov_b32 DPP quad broadcast
+      asm volatile(REP8(MF "v_mov_b32_dpp %[u0], %[u1] quad_perm:[1,1,1,1] row_mask:0xf bank_mask:0xf\n\t"
+                           "v_mov_b32_dpp %[u1], %[u2] quad_perm:[2,2,2,2] row_mask:0xf bank_mask:0xf\n\t"
+                           "v_mov_b32_dpp %[u2], %[u3] quad_perm:[3,3,3,3] row_mask:0xf bank_mask:0xf\n\t"
+                           "v_mov_b32_dpp %[u3], %[u0] quad_perm:[0,0,0,0] row_mask:0xf bank_mask:0xf\n\t")
+                   : AOUT, [u0] "+v"(u0), [u1] "+v"(u1), [u2] "+v"(u2), [u3] "+v"(u3) : XIN);
     } else if constexpr (KIND == 5) {  // the 64 b32 selects alone
       asm volatile(REP8("v_cndmask_b32_e32 %0, %0, %1, vcc\n\t"
                         "v_cndmask_b32_e32 %1, %1, %2, vcc\n\t"
@@ -73,10 +86,11 @@ int main() {
   hipMalloc(&out, G * 256 * 8);
   hipMalloc(&cyc, G * 8);
   const char* names[] = {"64 MFMA", "64 MFMA + 64 v_cndmask_b32", "64 MFMA + 64 v_add_u32", "64 MFMA + 64 v_fma_f64",
-                         "64 MFMA + 64 v_fma_f32", "64 v_cndmask_b32 alone", "64 v_fma_f64 alone"};
-  void (*kern[])(double*, long long*) = {k<0>, k<1>, k<2>, k<3>, k<4>, k<5>, k<6>};
+                         "64 MFMA + 64 v_fma_f32", "64 v_cndmask_b32 alone", "64 v_fma_f64 alone",
+                         "64 MFMA + 64 ds_bpermute_b32", "64 MFMA + 64 v_mov_b32_dpp"};
+  void (*kern[])(double*, long long*) = {k<0>, k<1>, k<2>, k<3>, k<4>, k<5>, k<6>, k<7>, k<8>};
   for (int rep = 0; rep < 2; ++rep)
-    for (int v = 0; v < 7; ++v) {
+    for (int v = 0; v < 9; ++v) {
       kern[v]<<<G, 256>>>(out, cyc);
       long long h[G];
       hipMemcpy(h, cyc, sizeof h, hipMemcpyDeviceToHost);
