@@ -258,6 +258,26 @@ def test_backward4_ragged_batch_and_nan_slot(gpu, nb):
         assert rel(K.cpu().numpy()[ok], Kc) < TOL_GAIN_SYM and rel(d.cpu().numpy()[ok], dc) < TOL_GAIN_SYM
 
 
+@pytest.mark.parametrize("T", [1, 2, 3, 6, 14, 19])
+def test_backward4_horizon_remainders(gpu, T):
+    """The four-trajectories-per-wave backward runs its step loop four steps at a time
+    (static L z column per step) plus a remainder of T mod 4 steps: every remainder,
+    and horizons shorter than one block, against the oracle (backward and fit)."""
+    nb = 7
+    lq, x, u = random_lq_batch(nb, 12, 4, T, seed=300 + T)
+    s = Solver(12, 4, T, nb)
+    s.set_problem(lq)
+    s.set_schedule(backward="block")
+    d, K, st = s.backward(dev(x), dev(u))
+    assert (st.cpu().numpy() == 0).all()
+    dc, Kc, _ = cref.lq_backward(lq, x, u, symmetrize=True)
+    assert rel(K, Kc) < TOL_GAIN_SYM and rel(d, dc) < TOL_GAIN_SYM
+    r = s.fit(dev(x), dev(u), max_iter=6, tol=1e-9)
+    xo, uo, co, it, sto = cref.lq_fit(lq, x, u, max_iter=6, tol=1e-9, symmetrize=True)
+    assert np.array_equal(r.iters.cpu().numpy(), it)
+    assert rel(r.u.cpu().numpy(), uo) < 1e-8
+
+
 def test_headline_fit_reaches_kkt_and_cost_is_monotone(gpu, headline):
     s, lq, x, u = headline
     # three iterations with tol disabled: every trajectory improves (α = 1 from cold,
