@@ -129,19 +129,30 @@ __device__ __forceinline__ double dpp_dot16_bd(double src, const double (&c)[12]
 #ifndef ILQR_FW_ABLATE
 #define ILQR_FW_ABLATE 0
 #endif
-// cache policy of the ring forward's memory traffic (probe: tools/fw_alt.sh): the aux
-// bits of the x̄/ū result stores (gfx950: 1 sc0, 2 nt, 16 sc1) and a " nt" hint on the
-// slot loads (every input the forward streams is dead after its step)
+// cache policy of the ring forward's memory traffic (tools/fw_alt.sh): the aux bits of
+// the x̄/ū result stores (gfx950: 1 sc0, 2 nt, 16 sc1: both slower) and a " nt" hint on
+// the slot loads — on all three (1: +10 µs, the x_traj = NULL re-reads of x then miss)
+// or on the first alone (2, the default: 64 of the step's 96 K-row chunks, read once;
+// forward 52.6 → 48.9 µs at B = 4096, bench 6,530 → 6,650 batched it/s,
+// profiles/r02/bench_ab_k_nt.log). A slot layout with both K loads pure and hinted
+// measured slower (52.6 µs, bench_ab_k_pure.log).
 #ifndef ILQR_FW_ST_AUX
 #define ILQR_FW_ST_AUX 0
 #endif
 #ifndef ILQR_FW_LD_NT
-#define ILQR_FW_LD_NT 0
+#define ILQR_FW_LD_NT 2
 #endif
-#if ILQR_FW_LD_NT
+#if ILQR_FW_LD_NT == 1
 #define ILQR_FW_LDS_OP "global_load_lds_dwordx4 %0, off nt"
 #else
 #define ILQR_FW_LDS_OP "global_load_lds_dwordx4 %0, off"
+#endif
+// ILQR_FW_LD_NT = 2: the hint on the first slot load only (K rows alone: dead after
+// the step, never re-read from cache)
+#if ILQR_FW_LD_NT == 2
+#define ILQR_FW_LDS_OP1 "global_load_lds_dwordx4 %0, off nt"
+#else
+#define ILQR_FW_LDS_OP1 ILQR_FW_LDS_OP
 #endif
 
 // Row broadcasts through LDS instead of DPP: every lane writes its value to the wave's
@@ -369,7 +380,7 @@ __device__ FwdOut lq_forward_wave_ring(const LQParams& P, int b0, int B, int T, 
     uint32_t tt = (uint32_t)(t < T ? t : T - 1);  // clamped: loaded, never read
     asm volatile("" : "+s"(tt));  // no hoisting of the prologue's addresses out of the trial loop
     const uint32_t m0 = ring_lds + (uint32_t)((t % R) * RING_SLOT * 8);
-    asm volatile(ILQR_FW_LDS_OP ::"v"(p1 + (size_t)tt * s1), "{m0}"(m0) : "memory");
+    asm volatile(ILQR_FW_LDS_OP1 ::"v"(p1 + (size_t)tt * s1), "{m0}"(m0) : "memory");
     asm volatile(ILQR_FW_LDS_OP ::"v"(p2 + (size_t)tt * s2), "{m0}"(m0 + 1024) : "memory");
     asm volatile(ILQR_FW_LDS_OP ::"v"(p3 + (size_t)tt * s3), "{m0}"(m0 + 2048) : "memory");
   };
