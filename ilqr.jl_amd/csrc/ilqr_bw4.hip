@@ -26,10 +26,14 @@
 //   W        = (H + 2μI) K_aug = −([G | g] + μP)
 //   S[I][J]  = mf4(P[I], W[J], Z[I][J])  (I ≤ J < 3),  s[I] = mf4(P[I], W[3], gv[I])
 //            = [Qxx | lx + Aᵀs] − K_augᵀ(H + 2μI)K_aug   (step_back :268-270)
-//   S[J][I]  = S[I][J]ᵀ by a lane permutation (ds_bpermute), diagonal blocks
-//              symmetrised every SYM_EVERY steps as in the 16×16 kernel.
+//   S[J][I]  = S[I][J]ᵀ by an MFMA transpose (mf4(a, I, 0) = aᵀ, exact), diagonal
+//              blocks symmetrised every SYM_EVERY steps as in the 16×16 kernel.
 // The solve is LDLᵀ as in the one-trajectory kernel, applied as the triangular
-// factors' explicit inverses on the MFMA (M = L⁻¹ has six entries).
+// factors' explicit inverses on the MFMA (M = L⁻¹ has six entries). The step loop runs
+// four steps at a time (each step's column of its L z block is then static). At one
+// wave per SIMD the step is issue-bound: every instruction costs the wave's issue
+// (≈16 cycles an MFMA, ≈6 any VALU op, tools/ubench_mix.hip), so the step is written
+// for instruction count.
 #include <hip/hip_runtime.h>
 #include <math.h>
 
@@ -49,14 +53,14 @@ namespace {
 #ifndef ILQR_BW4_MU_IN_H
 #define ILQR_BW4_MU_IN_H 1
 #endif
-// the solve's per-lane operands (M[ρ][κ], D⁻¹[ρ]) by 0/1-mask FMAs instead of select
-// chains: every VALU instruction beside the MFMAs costs the wave ≈6 cycles of issue,
-// b32 selects as much as f64 FMAs (tools/ubench_mix.hip)
 // the lower S blocks as MFMA transposes of the upper ones (mf4(a, I, 0) = aᵀ, exact)
-// instead of ds_bpermute lane permutations
+// instead of ds_bpermute lane permutations (0: the permutes)
 #ifndef ILQR_BW4_SLOW_MFMA
 #define ILQR_BW4_SLOW_MFMA 1
 #endif
+// the solve's per-lane operands (M[ρ][κ], D⁻¹[ρ]) by 0/1-mask FMAs instead of select
+// chains: every VALU instruction beside the MFMAs costs the wave ≈6 cycles of issue,
+// b32 selects as much as f64 FMAs (tools/ubench_mix.hip; 0: the selects)
 #ifndef ILQR_BW4_SEL_FMA
 #define ILQR_BW4_SEL_FMA 1
 #endif
