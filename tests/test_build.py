@@ -48,3 +48,18 @@ def test_twolink_alternates_compile(tmp_path):
            "-o", str(tmp_path / "tl_alt.o")]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-2000:]
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC) and shutil.which("hipcc") is None, reason="no hipcc")
+def test_backward4_alternates_compile(tmp_path):
+    """ilqr_bw4.hip with the round-2 instruction cuts undone — μ added in the
+    factorisation (ILQR_BW4_MU_IN_H=0), select chains for the solve's per-lane operands
+    (ILQR_BW4_SEL_FMA=0), lower S blocks by lane permutation (ILQR_BW4_SLOW_MFMA=0),
+    transposes by permutation (ILQR_BW4_MFMA_T=0) — and the forward's slot loads without
+    the non-temporal hint (ILQR_FW_LD_NT=0): the A/B baselines of tools/bw_alt.sh."""
+    hipcc = HIPCC if os.path.exists(HIPCC) else shutil.which("hipcc")
+    cmd = [hipcc, "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-mllvm", "-amdgpu-mfma-vgpr-form=1",
+           "-DILQR_BW4_MU_IN_H=0", "-DILQR_BW4_SEL_FMA=0", "-DILQR_BW4_SLOW_MFMA=0", "-DILQR_BW4_MFMA_T=0",
+           "-DILQR_FW_LD_NT=0", "-c", os.path.join(CSRC, "ilqr_bw4.hip"), "-o", str(tmp_path / "bw4_alt.o")]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
