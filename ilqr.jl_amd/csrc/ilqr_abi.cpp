@@ -35,6 +35,7 @@ struct ilqr_handle {
   // [2] = fit's call-status flags (gather_kernel: bit 0 NaN, bit 1 exhausted line search)
   int32_t* host_running = nullptr;
   int32_t* dev_running = nullptr;  // device alias of host_running
+  int32_t* dev_flags = nullptr;    // gather_kernel's device call-status word + block ticket
   hipEvent_t ev_poll[2] = {nullptr, nullptr};
   // LQ problems of another shape (nx ≤ 12, nu ≤ 4) run zero-padded on an inner
   // (12, 4) handle (created on the first such call): zero rows/columns of A, B, Q, R,
@@ -65,6 +66,17 @@ struct ilqr_handle {
   // SIMDs and the shorter per-wave chain of the one-trajectory kernel wins:
   // profiles/r01/bw4_scan.txt)
   bool bw_wave = false;
+  // the fused LQ iteration's cooperative line search (ILQR_SCHED_SEQUENTIAL_SEARCH
+  // turns it off): per-trajectory records, candidate costs, the publication list and
+  // its counters (zeroed here, re-armed by every launch's last wave)
+  bool coop = true;
+  ilqr::LSCoopRec* coop_rec = nullptr;
+  double* coop_cost = nullptr;
+  double* coop_du2 = nullptr;
+  uint64_t* coop_list = nullptr;
+  int32_t* coop_ctl = nullptr;
+  uint32_t coop_gen = 0;  // fused launches so far (the list's generation tag)
+  ilqr::LSCoop* coop_dev = nullptr;  // the struct of the above, in device memory
   int bound[3] = {0, 0, 0};
   hipEvent_t ev_bw[2] = {nullptr, nullptr};
   hipEvent_t ev_fw[2] = {nullptr, nullptr};
@@ -147,7 +159,10 @@ ilqr_status enqueue_iteration(ilqr_handle* h, const ilqr_problem* p, const ilqr:
   const ilqr::LQParams P = lq_params(p);
   if (h->nchunks == 1) {  // one stream, no cross-stream events (each hand-off costs ~10 µs)
     if (fused_path(h, p)) {
-      HIP_TRY(ilqr::launch_lq_iter_fused4(P, h->batch, h->T, a, ls, h->stream, h->fw_mfma));
+      ilqr::IterArgs ac = a;
+      ac.coop = h->coop ? h->coop_dev : nullptr;
+      ac.coop_gen = ++h->coop_gen;
+      HIP_TRY(ilqr::launch_lq_iter_fused4(P, h->batch, h->T, ac, ls, h->stream, h->fw_mfma));
       return ILQR_OK;
     }
     HIP_TRY(ilqr::launch_lq_iter_backward(h->nx, h->nu, P, 0, h->batch, h->T, a, ls.mu, h->stream, h->bw_wave));
@@ -226,6 +241,7 @@ ilqr_status ensure_pad(ilqr_handle* h) {
   h->pad->fw_ring = h->fw_ring;
   h->pad->fw_mfma = h->fw_mfma;
   h->pad->bw_wave = h->bw_wave;
+  h->pad->coop = h->coop;
   return ILQR_OK;
 }
 
@@ -345,7 +361,24 @@ ilqr_status ilqr_create(ilqr_handle** out, int device, int nx, int nu, int T, in
   if (e == hipSuccess)
     e = hipHostMalloc(&h->host_running, sizeof(int32_t) * 4, hipHostMallocMapped | hipHostMallocCoherent);
   if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&h->dev_running, h->host_running, 0);
+  if (e == hipSuccess) e = hipMalloc(&h->dev_flags, sizeof(int32_t) * 2);
+  if (e == hipSuccess) e = hipMemset(h->dev_flags, 0, sizeof(int32_t) * 2);
   for (int c = 0; c < 2 && e == hipSuccess; ++c) e = hipEventCreateWithFlags(&h->ev_poll[c], hipEventDisableTiming);
+  if (e == hipSuccess && nx == 12 && nu == 4) {
+    e = hipMalloc(&h->coop_rec, sizeof(ilqr::LSCoopRec) * B);
+    if (e == hipSuccess) e = hipMalloc(&h->coop_cost, sizeof(double) * B * ilqr::COOP_MAX_TRIALS);
+    if (e == hipSuccess) e = hipMalloc(&h->coop_du2, sizeof(double) * B * ilqr::COOP_MAX_TRIALS);
+    if (e == hipSuccess) e = hipMalloc(&h->coop_list, sizeof(uint64_t) * B);
+    if (e == hipSuccess) e = hipMalloc(&h->coop_ctl, sizeof(int32_t) * 2);
+    if (e == hipSuccess) e = hipMemset(h->coop_list, 0, sizeof(uint64_t) * B);  // generation 0: stale
+    if (e == hipSuccess) e = hipMemset(h->coop_ctl, 0, sizeof(int32_t) * 2);
+    if (e == hipSuccess) e = hipMalloc(&h->coop_dev, sizeof(ilqr::LSCoop));
+    if (e == hipSuccess) {
+      const ilqr::LSCoop c{h->coop_rec, h->coop_cost, h->coop_du2, h->coop_list, h->coop_ctl};
+      e = hipMemcpy(h->coop_dev, &c, sizeof(c), hipMemcpyHostToDevice);
+    }
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+  }
   if (e == hipSuccess && ilqr::tl_supported(nx, nu))
     e = hipMalloc(&h->J, sizeof(double) * ilqr::tl_workspace_doubles(batch, T));
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking);
@@ -391,6 +424,13 @@ ilqr_status ilqr_destroy(ilqr_handle* h) {
   (void)hipFree(h->iters);
   if (h->host_status) (void)hipHostFree(h->host_status);
   if (h->host_running) (void)hipHostFree(h->host_running);
+  (void)hipFree(h->dev_flags);
+  (void)hipFree(h->coop_rec);
+  (void)hipFree(h->coop_cost);
+  (void)hipFree(h->coop_du2);
+  (void)hipFree(h->coop_list);
+  (void)hipFree(h->coop_ctl);
+  (void)hipFree(h->coop_dev);
   for (int c = 0; c < 2; ++c)
     if (h->ev_poll[c]) (void)hipEventDestroy(h->ev_poll[c]);
   if (h->pad) {
@@ -416,24 +456,23 @@ ilqr_status ilqr_set_stream(ilqr_handle* h, void* s) {
 
 ilqr_status ilqr_set_schedule(ilqr_handle* h, int flags) {
   if (!h || (flags & ~(ILQR_SCHED_PIPELINED | ILQR_SCHED_RING_FORWARD | ILQR_SCHED_BACKWARD_WAVE |
-                      ILQR_SCHED_BACKWARD_BLOCK | ILQR_SCHED_FUSED | ILQR_SCHED_FORWARD_MFMA)) != 0)
+                      ILQR_SCHED_BACKWARD_BLOCK | ILQR_SCHED_FUSED | ILQR_SCHED_FORWARD_MFMA |
+                      ILQR_SCHED_SEQUENTIAL_SEARCH)) != 0)
     return ILQR_ERR_BAD_ARG;
+  // every combination check before any handle state changes
   if ((flags & ILQR_SCHED_FUSED) && (flags & (ILQR_SCHED_BACKWARD_WAVE | ILQR_SCHED_PIPELINED)))
     return ILQR_ERR_BAD_ARG;
-  h->pipelined = (flags & ILQR_SCHED_PIPELINED) != 0;
-  h->fused = (flags & ILQR_SCHED_FUSED) != 0;
-  h->fw_ring = (flags & ILQR_SCHED_RING_FORWARD) != 0;
-  h->fw_mfma = (flags & ILQR_SCHED_FORWARD_MFMA) != 0;
   if ((flags & ILQR_SCHED_BACKWARD_BLOCK) && (flags & (ILQR_SCHED_BACKWARD_WAVE | ILQR_SCHED_PIPELINED)))
     return ILQR_ERR_BAD_ARG;
-  h->bw_wave = (flags & (ILQR_SCHED_BACKWARD_WAVE | ILQR_SCHED_PIPELINED)) != 0 ||
-               (!(flags & ILQR_SCHED_BACKWARD_BLOCK) && h->batch < BW4_MIN_BATCH);
-  if (h->pad) {
-    h->pad->pipelined = h->pipelined;
-    h->pad->fused = h->fused;
-    h->pad->fw_ring = h->fw_ring;
-  h->pad->fw_mfma = h->fw_mfma;
-    h->pad->bw_wave = h->bw_wave;
+  for (ilqr_handle* t : {h, h->pad}) {
+    if (!t) continue;
+    t->pipelined = (flags & ILQR_SCHED_PIPELINED) != 0;
+    t->fused = (flags & ILQR_SCHED_FUSED) != 0;
+    t->fw_ring = (flags & ILQR_SCHED_RING_FORWARD) != 0;
+    t->fw_mfma = (flags & ILQR_SCHED_FORWARD_MFMA) != 0;
+    t->coop = (flags & ILQR_SCHED_SEQUENTIAL_SEARCH) == 0;
+    t->bw_wave = (flags & (ILQR_SCHED_BACKWARD_WAVE | ILQR_SCHED_PIPELINED)) != 0 ||
+                 (!(flags & ILQR_SCHED_BACKWARD_BLOCK) && h->batch < BW4_MIN_BATCH);
   }
   return ILQR_OK;
 }
@@ -576,6 +615,14 @@ ilqr_status ilqr_fit(ilqr_handle* h, const ilqr_problem* p, const ilqr_options* 
                      const double* x_init, const double* u_init, const double* x_traj,
                      double* x_out, double* u_out, double* cost, int32_t* iters,
                      int32_t* status) {
+  return ilqr_fit_ex(h, p, o, x_init, u_init, x_traj, x_out, u_out, cost, iters, status, nullptr);
+}
+
+ilqr_status ilqr_fit_ex(ilqr_handle* h, const ilqr_problem* p, const ilqr_options* o,
+                        const double* x_init, const double* u_init, const double* x_traj,
+                        double* x_out, double* u_out, double* cost, int32_t* iters,
+                        int32_t* status, const ilqr_history* hist) {
+  if (hist && !hist->cost && !hist->trials && !hist->alpha && !hist->du2) hist = nullptr;
   ilqr_status st = check_problem(h, p);
   if (st != ILQR_OK) return st;
   if ((st = check_options(o)) != ILQR_OK) return st;
@@ -591,8 +638,8 @@ ilqr_status ilqr_fit(ilqr_handle* h, const ilqr_problem* p, const ilqr_options* 
     ILQR_TRY(pad_x(h, x_init, h->px));
     ILQR_TRY(pad_u(h, u_init, h->pu));
     if (x_traj) ILQR_TRY(pad_x(h, x_traj, h->pxt));
-    const ilqr_status fst = ilqr_fit(h->pad, &pp, o, h->px, h->pu, x_traj ? h->pxt : nullptr,
-                                     h->pxn, h->pun, cost, iters, status);
+    const ilqr_status fst = ilqr_fit_ex(h->pad, &pp, o, h->px, h->pu, x_traj ? h->pxt : nullptr,
+                                        h->pxn, h->pun, cost, iters, status, hist);
     if (fst != ILQR_OK && fst != ILQR_ERR_NAN && fst != ILQR_ERR_LS_EXHAUSTED) return fst;
     ILQR_TRY(unpad_x(h, h->pxn, x_out));
     ILQR_TRY(unpad_u(h, h->pun, u_out));
@@ -602,7 +649,10 @@ ilqr_status ilqr_fit(ilqr_handle* h, const ilqr_problem* p, const ilqr_options* 
   hipStream_t s = h->stream;
   // prev_cost = Inf (forward_pass.jl:159), status OK, result "the input", iters 0: by
   // the first iteration's kernel itself on the fused LQ path, else by a kernel here
-  const bool init_in_iter = fused_path(h, p) && !h->pipelined && o->max_iter > 0;
+  // the pipelined schedule interleaves two iterations per launch: a fit that records
+  // its history runs the sequential schedule instead (the same bits)
+  const bool pipe = !two_link(p) && h->pipelined && !hist;
+  const bool init_in_iter = fused_path(h, p) && !pipe && o->max_iter > 0;
   if (!init_in_iter)
     HIP_TRY(ilqr::launch_fit_init(h->batch, h->prev_cost, h->status, h->res_parity, h->iters, s));
   volatile int32_t* flags = h->host_running + 2;
@@ -647,7 +697,7 @@ ilqr_status ilqr_fit(ilqr_handle* h, const ilqr_problem* p, const ilqr_options* 
     a.init = init_in_iter && it == 1;
     return a;
   };
-  if (!two_link(p) && h->pipelined) {
+  if (pipe) {
     // Launch `it` runs iteration it for role-B workgroups and forward(it−1) +
     // backward(it) for role A; launch max_iter+1 drains A's last forward.
     for (int it = 1; it <= o->max_iter + 1; ++it) {
@@ -665,17 +715,24 @@ ilqr_status ilqr_fit(ilqr_handle* h, const ilqr_problem* p, const ilqr_options* 
   // reads iteration it−1's count while the GPU runs iteration it (no idle gap; at most
   // one iteration of already-stopped waves is enqueued past the last useful one).
   const bool poll = o->tol >= 0.0 && o->max_iter > 2;
-  for (int it = 1; (two_link(p) || !h->pipelined) && it <= o->max_iter; ++it) {  // forward_pass.jl:161
+  for (int it = 1; !pipe && it <= o->max_iter; ++it) {  // forward_pass.jl:161
     // iterations chain per chunk: chunk 0's next backward overlaps chunk 1's forward
     const ilqr_status st = enqueue_iteration(h, p, iter_args(it), ls, /*chain=*/true);
     if (st != ILQR_OK) return st;
+    // the history record and the count run behind every chunk's forward without
+    // joining the main stream (a join would keep chunk 0's next backward from
+    // overlapping chunk 1's forward): the forwards of all chunks are in order on the
+    // side stream
+    const hipStream_t ps = (two_link(p) || h->nchunks == 1) ? s : h->side;
+    if (hist)
+      HIP_TRY(ilqr::launch_record_history(h->batch, it, h->status, h->iters, h->trials, h->prev_cost, h->du2,
+                                          false, ls.alpha0, ls.shrink, hist->cost, hist->trials, hist->alpha,
+                                          hist->du2, ps));
+    if (hist && ps == h->side)  // the next backwards (they may set NAN) after the record
+      for (int c = 0; c < h->nchunks; ++c) HIP_TRY(hipEventRecord(h->ev_fw[c], h->side));
     if (!poll || it == o->max_iter) continue;
-    {
-      const ilqr_status js = join(h, p);
-      if (js != ILQR_OK) return js;
-    }
-    HIP_TRY(ilqr::launch_count_running(h->batch, h->status, h->dev_running + (it & 1), s));
-    HIP_TRY(hipEventRecord(h->ev_poll[it & 1], s));
+    HIP_TRY(ilqr::launch_count_running(h->batch, h->status, h->dev_running + (it & 1), ps));
+    HIP_TRY(hipEventRecord(h->ev_poll[it & 1], ps));
     if (it >= 2) {
       HIP_TRY(hipEventSynchronize(h->ev_poll[(it - 1) & 1]));
       if (__atomic_load_n(h->host_running + ((it - 1) & 1), __ATOMIC_ACQUIRE) == 0) break;
@@ -691,7 +748,7 @@ ilqr_status ilqr_fit(ilqr_handle* h, const ilqr_problem* p, const ilqr_options* 
   HIP_TRY(ilqr::launch_gather_result(h->batch, h->T, h->nx, h->nu, x_init, u_init, h->xbuf[0],
                                      h->ubuf[0], h->xbuf[1], h->ubuf[1], h->res_parity, h->status,
                                      last, h->prev_cost, h->iters, x_out, u_out, cost, iters,
-                                     status, h->dev_running + 2, s));
+                                     status, h->dev_flags, h->dev_running + 2, s));
   HIP_TRY(hipStreamSynchronize(s));
   const int32_t f = __atomic_load_n(h->host_running + 2, __ATOMIC_ACQUIRE);
   return (f & 1) ? ILQR_ERR_NAN : ((f & 2) ? ILQR_ERR_LS_EXHAUSTED : ILQR_OK);

@@ -559,8 +559,11 @@ __global__ __launch_bounds__(64 * FUSED_WAVES) void lq_iter_fused4_kernel(LQPara
   static_assert(FUSED_LDS >= BW4_LDS, "backward scratch fits the ring");
   const int w = threadIdx.x >> 6;
   double* lds = lds_all + w * FUSED_LDS;
-  const int b0 = (blockIdx.x * FUSED_WAVES + w) * BW4_SLOTS;
-  if (b0 >= B) return;
+  const int wid = blockIdx.x * FUSED_WAVES + w;
+  const int b0 = wid * BW4_SLOTS;
+  // the cooperative line search (row-form forward, 2 ≤ max_trials ≤ 64): every wave of
+  // the launch takes part, present or not
+  const bool coop = !MF && a.coop && ls.max_trials >= 2 && ls.max_trials <= COOP_MAX_TRIALS;
   const int l = threadIdx.x & 63;
   // the lane that writes slot q's per-trajectory words (the forward's writer: lane 16q
   // in the row form, lane 4q in the MFMA form), so the writes of one slot keep program order
@@ -568,39 +571,50 @@ __global__ __launch_bounds__(64 * FUSED_WAVES) void lq_iter_fused4_kernel(LQPara
   const int q = MF ? (l >> 2) & 3 : l >> 4;
   unsigned active = 0;
   IterArgs ai = a;
-  if (a.init) {
-    // fit's first iteration (fit_init_kernel's job, :159): every present trajectory
-    // runs from prev_cost = Inf
-    const int nt = B - b0 < BW4_SLOTS ? B - b0 : BW4_SLOTS;
-    active = (1u << nt) - 1u;
-    if (owner && q < nt) {
-      const int b = b0 + q;
-      a.new_cost[b] = INFINITY;  // = prev_cost (in place)
-      a.status[b] = ILQR_TRAJ_OK;
-      a.res_parity[b] = PARITY_INPUT;
-      a.iters[b] = 0;
-    }
-    ai.prev_cost = nullptr;  // +Inf without reading
-  } else {
+  if (a.coop && wid == 0 && l == 0) {
+    // the next launch's list length (this launch counts in ctl[gen & 1])
+    int32_t* ctl = a.coop->ctl;
+    __hip_atomic_store(ctl + ((a.coop_gen + 1) & 1), 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (b0 < B) {
+    if (a.init) {
+      // fit's first iteration (fit_init_kernel's job, :159): every present trajectory
+      // runs from prev_cost = Inf
+      const int nt = B - b0 < BW4_SLOTS ? B - b0 : BW4_SLOTS;
+      active = (1u << nt) - 1u;
+      if (owner && q < nt) {
+        const int b = b0 + q;
+        a.new_cost[b] = INFINITY;  // = prev_cost (in place)
+        a.status[b] = ILQR_TRAJ_OK;
+        a.res_parity[b] = PARITY_INPUT;
+        a.iters[b] = 0;
+      }
+      ai.prev_cost = nullptr;  // +Inf without reading
+    } else {
 #pragma unroll
-    for (int q = 0; q < BW4_SLOTS; ++q)
-      if (b0 + q < B && a.status[b0 + q] == ILQR_TRAJ_OK) active |= 1u << q;
-    if (active == 0) return;
+      for (int q = 0; q < BW4_SLOTS; ++q)
+        if (b0 + q < B && a.status[b0 + q] == ILQR_TRAJ_OK) active |= 1u << q;
+    }
   }
-  const unsigned nan = lq_backward4_wave(P, b0, B, active, T, a.x, a.u, a.d, a.K, ls.mu, lds) & active;
-  if (owner && ((nan >> q) & 1u)) {
-    a.status[b0 + q] = ILQR_TRAJ_NAN;  // reference: AssertionError at backward_pass.jl:353
-    if (a.res_parity) a.res_parity[b0 + q] = a.parity;
+  if (active != 0) {
+    const unsigned nan = lq_backward4_wave(P, b0, B, active, T, a.x, a.u, a.d, a.K, ls.mu, lds) & active;
+    if (owner && ((nan >> q) & 1u)) {
+      a.status[b0 + q] = ILQR_TRAJ_NAN;  // reference: AssertionError at backward_pass.jl:353
+      if (a.res_parity) a.res_parity[b0 + q] = a.parity;
+    }
+    // the gains this wave stored are what its forward streams in: every store complete,
+    // and the LDS scratch free for the ring
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    const unsigned run = active & ~nan;
+    if constexpr (MF)
+      iter_forward_wave_mfma(P, b0, B, T, ai, ls, lds, run);
+    else if (coop)
+      iter_forward_wave_coop<12, 4>(P, b0, B, T, ai, ls, lds, ((run >> (l >> 4)) & 1u) != 0);
+    else
+      iter_forward_wave_active<12, 4>(P, b0, B, T, ai, ls, lds, ((run >> (l >> 4)) & 1u) != 0);
   }
-  // the gains this wave stored are what its forward streams in: every store complete,
-  // and the LDS scratch free for the ring
-  __builtin_amdgcn_s_waitcnt(0);
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-  const unsigned run = active & ~nan;
-  if constexpr (MF)
-    iter_forward_wave_mfma(P, b0, B, T, ai, ls, lds, run);
-  else
-    iter_forward_wave_active<12, 4>(P, b0, B, T, ai, ls, lds, ((run >> (l >> 4)) & 1u) != 0);
+  if (coop) lq_coop_search<12, 4>(P, B, T, ai, ls, lds, wid);
 }
 
 }  // namespace

@@ -1821,7 +1821,7 @@ __global__ __launch_bounds__(64 * W) void chain_iter_forward_trig_kernel(ChainTr
   const V pc = a.prev_cost ? a.prev_cost[b] : V(INFINITY);
   const ChainTrigModel<V, NU> m{P};
   const FgOut<V> r = fwd_group<ChainTrigModel<V, NU>, L>(m, b, B, T, a.x, a.u, a.xtraj, a.d, a.K, pc, a.xnew,
-                                                          a.unew, ls);
+                                                          a.unew, ls, a.res_parity == nullptr);
   if (!r.owner) return;
   if (a.trials) a.trials[b] = r.trials;
   if (a.du2) a.du2[b] = r.du2;
@@ -2315,7 +2315,7 @@ ilqr_status chain_fold_status(ilqr_chain_handle* h, const int32_t* dev_status) {
 template <class V>
 ilqr_status chain_fit_t(ilqr_chain_handle* h, const ilqr_options* o, const void* x_init,
                         const void* u_init, const void* x_traj, void* x_out, void* u_out,
-                        void* cost, int32_t* iters, int32_t* status) {
+                        void* cost, int32_t* iters, int32_t* status, const ilqr_history* hist) {
   const size_t B = (size_t)h->batch, nx = 2 * (size_t)h->nj;
   const size_t nxe = (h->T + 1) * nx, nue = (size_t)h->T * h->nu;
   hipStream_t s = h->stream;
@@ -2338,6 +2338,10 @@ ilqr_status chain_fit_t(ilqr_chain_handle* h, const ilqr_options* o, const void*
     a.parity = par;
     a.iter = it;
     CH_TRY(dispatch<V>(h, [&](auto ops) { return decltype(ops)::iteration(h, a, ls); }));
+    if (hist)  // the per-iteration record (ilqr_history)
+      CH_TRY(ilqr::launch_record_history(h->batch, it, h->status, h->iters, h->trials, h->prev_cost, h->du2,
+                                         sizeof(V) == 4, ls.alpha0, ls.shrink, hist->cost, hist->trials,
+                                         hist->alpha, hist->du2, s));
     par ^= 1;  // x̄ⁱ, ūⁱ = x̄ⁱ⁺¹, ūⁱ⁺¹ (:174-175)
   }
   ilqr::chain_gather_kernel<V><<<dim3(1, h->batch), 256, 0, s>>>(
@@ -2590,14 +2594,21 @@ ilqr_status ilqr_chain_iterate(ilqr_chain_handle* h, const ilqr_options* o, cons
 ilqr_status ilqr_chain_fit(ilqr_chain_handle* h, const ilqr_options* o, const void* x_init,
                            const void* u_init, const void* x_traj, void* x_out, void* u_out,
                            void* cost, int32_t* iters, int32_t* status) {
+  return ilqr_chain_fit_ex(h, o, x_init, u_init, x_traj, x_out, u_out, cost, iters, status, nullptr);
+}
+
+ilqr_status ilqr_chain_fit_ex(ilqr_chain_handle* h, const ilqr_options* o, const void* x_init,
+                              const void* u_init, const void* x_traj, void* x_out, void* u_out,
+                              void* cost, int32_t* iters, int32_t* status, const ilqr_history* hist) {
   if (!h || !x_init || !u_init || !x_out || !u_out) return ILQR_ERR_BAD_ARG;
+  if (hist && !hist->cost && !hist->trials && !hist->alpha && !hist->du2) hist = nullptr;
   if (!iter_supported(h->nj, h->nu)) return ILQR_ERR_UNSUPPORTED;
   ilqr_status st = chain_check_options(o);
   if (st != ILQR_OK) return st;
   CH_TRY(hipSetDevice(h->device));
   if (h->dtype == ILQR_F32)
-    return chain_fit_t<float>(h, o, x_init, u_init, x_traj, x_out, u_out, cost, iters, status);
-  return chain_fit_t<double>(h, o, x_init, u_init, x_traj, x_out, u_out, cost, iters, status);
+    return chain_fit_t<float>(h, o, x_init, u_init, x_traj, x_out, u_out, cost, iters, status, hist);
+  return chain_fit_t<double>(h, o, x_init, u_init, x_traj, x_out, u_out, cost, iters, status, hist);
 }
 
 ilqr_status ilqr_chain_sync(ilqr_chain_handle* h) {

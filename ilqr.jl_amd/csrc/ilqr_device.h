@@ -69,6 +69,15 @@ __device__ __forceinline__ void wave_lds_fence() {
 // tolerances; the factorisation is the kernel's critical path, tools/ablate_bw).
 // 64-bit global store without an exec branch: a raw buffer store whose offset is
 // pushed out of range (dropped by the hardware bounds check) on inactive lanes.
+// a pointer the compiler must treat as wave-uniform (its value is, but divergence
+// analysis lost it): both halves through v_readfirstlane
+template <class P>
+__device__ __forceinline__ P* uniform_ptr(P* p) {
+  const uint64_t v = (uint64_t)(uintptr_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return (P*)(uintptr_t)(((uint64_t)hi << 32) | lo);
+}
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t buffer_rsrc(void* base, uint32_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(base, 0, (int)bytes, 0x00020000);  // gfx9 dword3
 }

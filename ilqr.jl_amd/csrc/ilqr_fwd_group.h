@@ -9,7 +9,10 @@
 // cost decreased (:77-80) — the sequential search's answer, bit for bit. Lane sub = 0
 // stores its rollout as it goes; an accepted candidate of another lane rolls out once
 // more, storing (same α, same rollout). Trials 1..L cost one pass (L = 1 is the
-// sequential search).
+// sequential search). An exhausted search leaves x_new / u_new holding the LAST trial's
+// rollout, as the sequential search does (its lane rolls out once more, storing, when
+// it is not lane 0) — unless `store_exhausted` is false (fit, which keeps the previous
+// iterate of an exhausted trajectory and never reads them).
 //
 // A Model supplies the arithmetic of one family (value type V, NU inputs):
 //   rk4_fast(x, u, out, bad)  one RK4 step without a branch; sets `bad` when an argument
@@ -81,7 +84,8 @@ __device__ FgOut<typename Model::V> fwd_group(const Model& m, int b, int B, int 
                                                const typename Model::V* __restrict__ Kg,
                                                typename Model::V prev_cost,
                                                typename Model::V* __restrict__ xnew,
-                                               typename Model::V* __restrict__ unew, const LSParams& ls) {
+                                               typename Model::V* __restrict__ unew, const LSParams& ls,
+                                               bool store_exhausted = true) {
   using V = typename Model::V;
   using V4 = typename Fg4<V>::T;
   constexpr int NU = Model::NU, NX = 4;
@@ -216,6 +220,10 @@ __device__ FgOut<typename Model::V> fwd_group(const Model& m, int b, int B, int 
         out.cost = cost;
         out.du2 = du2;
         out.owner = true;
+        if (store_exhausted && !store) {  // the last trial's rollout, stored
+          store = rerun = true;
+          continue;
+        }
       }
       break;
     }

@@ -247,6 +247,22 @@ struct FwdOut {
   double cost;
   int trials;
   int accepted;  // 1 accepted, 0 exhausted / NaN
+  bool eo;       // candidate pass: α·δu vanished at every step (see CandPass)
+};
+
+// One CANDIDATE pass of the cooperative line search (lq_coop_search below): the wave's
+// four groups roll out the SAME trajectory, each at its own α (trial j's α, formed by
+// the reference's repeated `α *= shrink`, :82), once, with the sequential search's
+// arithmetic and order — so a candidate's cost is bit for bit that trial's cost. Only
+// the group `store_group` stores its rollout (−1: none). Each group also reports `eo`:
+// fma(α, δuₖ, uₖ) == uₖ at every step. Then every later trial j' > j rolls out
+// identically (exact: α' ≤ α and rounding is monotone, so fma(α', δu, u) rounds to u as
+// well, every ūₖ = uₖ + Kₖδxₖ is the same and so is the whole rollout), i.e. once such
+// a trial is rejected the search of forward_pass.jl:70-87 capped at max_trials ends
+// exhausted with that rollout and cost.
+struct CandPass {
+  double alpha;     // this lane's group's α
+  int store_group;  // group that stores its rollout into x_new/u_new of the trajectory
 };
 
 
@@ -269,13 +285,17 @@ constexpr int RING_LAREA = 4 * 160 + 16 + 4 * 64;
 // one wave per SIMD and VGPRs to spare); otherwise they are re-read from LDS every step
 // (the pipelined kernel's 128-VGPR budget). An LDS read in the step is a wait the
 // in-order wave cannot issue past.
-template <int NX, int NU, int R, int PF, bool LR_REGS = true>
+//
+// CAND: one candidate pass (CandPass above) of trajectory b0 in all four groups — no
+// search loop; the result is this group's cost, du2 and eo.
+template <int NX, int NU, int R, int PF, bool LR_REGS = true, bool CAND = false>
 __device__ FwdOut lq_forward_wave_ring(const LQParams& P, int b0, int B, int T, bool active,
                                        const double* __restrict__ x, const double* __restrict__ u,
                                        const double* __restrict__ xtraj, const double* __restrict__ dg,
                                        const double* __restrict__ Kg, double prev_cost,
                                        double* __restrict__ xnew, double* __restrict__ unew,
-                                       double* du2_out, const LSParams& ls, double* ring) {
+                                       double* du2_out, const LSParams& ls, double* ring,
+                                       const CandPass& cand = CandPass{0.0, -1}) {
   static_assert(NX == 12 && NU == 4, "slot layout and lane map are written for nx = 12, nu = 4");
   static_assert(R > PF && PF >= 1, "the slot being refilled must not be the one being read");
   constexpr uint32_t OOR = 0x80000000u;
@@ -289,7 +309,8 @@ __device__ FwdOut lq_forward_wave_ring(const LQParams& P, int b0, int B, int T, 
   const bool is_u = !is_x;
   const int iu = is_u ? j - NX : 0;
   const int jx = is_x ? j : 0;
-  const int nt = B - b0 < 4 ? B - b0 : 4;  // trajectories present in this wave
+  // trajectories present in this wave (a candidate pass: one, in every group)
+  const int nt = CAND ? 1 : (B - b0 < 4 ? B - b0 : 4);
   const int b = b0 + (g < nt ? g : 0);     // absent groups alias trajectory b0 (never stored)
 
   const double* Ab = P.A + (size_t)b * NX * NX;
@@ -399,20 +420,29 @@ __device__ FwdOut lq_forward_wave_ring(const LQParams& P, int b0, int B, int T, 
   const int ka = g * 48 + iu * NX;                                 // K row of (g, iu)
   const int va = is_x ? 192 + g * 12 + jx : 240 + g * 4 + iu;      // x (x lanes) / u (u lanes)
   const int vb = is_x ? 256 + g * 12 + jx : 304 + g * 4 + iu;      // x_traj / δu
-  const auto rXN = buffer_rsrc(xnew + (size_t)b0 * (T + 1) * NX, (uint32_t)nt * (T + 1) * NX * 8);
-  const auto rUN = buffer_rsrc(unew + (size_t)b0 * T * NU, (uint32_t)nt * T * NU * 8);
-  const uint32_t oxs = is_x ? (uint32_t)(g * (T + 1) * NX + jx) * 8 : OOR;
-  const uint32_t ous = is_u ? (uint32_t)(g * T * NU + iu) * 8 : OOR;
+  // the resources' words made provably wave-uniform (the candidate passes run inside
+  // the cooperative search's loops, where the compiler loses track of it: a divergent
+  // resource is a readfirstlane waterfall loop around every store)
+  const auto rXN = buffer_rsrc(uniform_ptr(xnew + (size_t)b0 * (T + 1) * NX),
+                               (uint32_t)__builtin_amdgcn_readfirstlane(nt * (T + 1) * NX * 8));
+  const auto rUN = buffer_rsrc(uniform_ptr(unew + (size_t)b0 * T * NU),
+                               (uint32_t)__builtin_amdgcn_readfirstlane(nt * T * NU * 8));
+  const int gs = CAND ? 0 : g;  // this group's trajectory within the stored span
+  const uint32_t oxs = is_x ? (uint32_t)(gs * (T + 1) * NX + jx) * 8 : OOR;
+  const uint32_t ous = is_u ? (uint32_t)(gs * T * NU + iu) * 8 : OOR;
 
-  double alpha = ls.alpha0;
-  FwdOut out{INFINITY, 0, 0};
+  double alpha = CAND ? cand.alpha : ls.alpha0;
+  FwdOut out{INFINITY, 0, 0, false};
   bool open = active;  // still line-searching
   double du2_acc = 0.0;
-  for (int trial = 1; trial <= ls.max_trials && __any(open); ++trial) {
+  const int trials_max = CAND ? 1 : ls.max_trials;
+  for (int trial = 1; trial <= trials_max && __any(open); ++trial) {
 #pragma unroll
     for (int t = 0; t < PF; ++t) produce(t);
     double cost = 0.0, du2 = 0.0;
-    const uint32_t ox = open ? oxs : OOR, ou = open ? ous : OOR;  // closed groups store nothing
+    bool eo = true;  // CAND: fma(α, δuₖ, uₖ) == uₖ so far (u lanes)
+    const bool st = open && (!CAND || g == cand.store_group);
+    const uint32_t ox = st ? oxs : OOR, ou = st ? ous : OOR;  // closed groups store nothing
     // slot t's operands are read into registers at the end of step t − 1 (software
     // pipelining of the LDS reads: their latency is off the step's dependent chain)
     struct Slot {
@@ -451,7 +481,9 @@ __device__ FwdOut lq_forward_wave_ring(const LQParams& P, int b0, int B, int T, 
 #else
       const double kdx = dpp_dot12(dx, cur.Kr);
 #endif
-      const double ub = fma(alpha, cur.bq, cur.a) + kdx;
+      const double ua = fma(alpha, cur.bq, cur.a);
+      const double ub = ua + kdx;
+      if constexpr (CAND) eo = eo && (is_x || ua == cur.a);
       const double z = is_x ? xb : ub;
       const double v = is_x ? fma(-xtw, cur.bq, xb) : ub;
       const double e = is_x ? 0.0 : ub - cur.a;
@@ -511,6 +543,16 @@ __device__ FwdOut lq_forward_wave_ring(const LQParams& P, int b0, int B, int T, 
     cost = fma(is_x ? xb : 0.0, lf, cost);
     cost = rowsum16(cost);
     du2 = rowsum16(du2);
+    if constexpr (CAND) {
+      const uint64_t bad = __ballot(!eo);
+      out.eo = ((bad >> (16 * g)) & 0xFFFFull) == 0;
+      out.trials = 1;
+      out.cost = cost;
+      du2_acc = du2;
+      __builtin_amdgcn_s_waitcnt((0) | (7 << 4) | (0 << 8));
+      asm volatile("" ::: "memory");
+      break;
+    }
     if (open) {
       out.trials = trial;
       out.cost = cost;
@@ -802,6 +844,297 @@ __device__ __forceinline__ void iter_forward_wave_mfma(const LQParams& P, int b0
       a.status[b] = (r.cost != r.cost) ? ILQR_TRAJ_NAN : ILQR_TRAJ_LS_EXHAUSTED;
       if (a.res_parity) a.res_parity[b] = a.parity;
     } else {
+      a.new_cost[b] = r.cost;
+      if (du2 <= ls.tol) {
+        a.status[b] = ILQR_TRAJ_CONVERGED;
+        if (a.res_parity) a.res_parity[b] = a.parity;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Cooperative line search (the fused LQ iteration, DESIGN.md §4 "line-search tail").
+// The wave-lockstep search above runs trial after trial for as long as ANY of a wave's
+// four trajectories is open: at the fp64 cost floor a few trajectories in a thousand
+// reject every α and the whole launch waits ≈64 full passes for them (round 2:
+// 1,482 batched it/s for a 5-iteration fit against 6,541 for 3). Here the search of
+// forward_pass.jl:70-87 keeps its exact answer but not its sequence:
+//  * every trajectory runs trial 1 in its own wave (the common case: accepted);
+//  * one still open is PUBLISHED (record + list entry) and all waves of the launch that
+//    are done with their own trajectories hand out its remaining trials four at a time
+//    (lq_forward_wave_ring<CAND>: the four groups of a wave roll out one trajectory at
+//    four α's, bit for bit the sequential trials' rollouts and costs);
+//  * each evaluated trial lowers `best` (accepted) or `stop` (rejected with α·δu
+//    vanished at every step: all later trials are that trial again, CandPass) and sets
+//    its mask bit; the wave whose bits complete trials 1..min(best, stop, max_trials)
+//    finalises: trial `best` if any (trial 2 was stored as it ran, another one is rolled
+//    out once more, storing), else the exhausted search's last trial (its rollout stored
+//    for ilqr_iterate; fit keeps the previous iterate and skips it) — the sequential
+//    search's x̄, ū, cost, Σ(ū − u)², trial count and status;
+//  * the last wave to leave re-arms the list for the next launch.
+// Liveness: nobody waits for a result — each grabbed trial is evaluated by the wave that
+// grabbed it, and the wave completing the needed set finalises. Idle waves wait for more
+// work only while the launch is co-resident (coop.wait) and not past a time limit.
+// ---------------------------------------------------------------------------
+// Memory ordering. The search's shared words (records, list, counters, candidate costs)
+// are only touched by agent-scope atomics, which the XCDs see coherently; the waves
+// POLL them with relaxed loads and never with acquire semantics — an acquire at agent
+// scope invalidates the XCD's L2 (buffer_inv sc1), and a thousand waiting waves doing
+// that every microsecond ran the headline iteration at 349 µs instead of 154 µs.
+// Values a decision depends on are read by read-modify-writes (the atomic's own
+// coherent value); rollout stores that another XCD may overwrite later in the launch
+// (trial 1's by the publisher, trial 2's stored as it ran) are written back by a
+// release fence before the word that hands the trajectory on — a handful per launch.
+__device__ __forceinline__ int32_t ag_ld(const int32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int32_t ag_rmw_ld(int32_t* p) {  // the coherent current value
+  return __hip_atomic_fetch_or(p, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ag_rmw_ldd(double* p) {
+  const uint64_t v = __hip_atomic_fetch_or(reinterpret_cast<uint64_t*>(p), (uint64_t)0, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+  return __builtin_bit_cast(double, v);
+}
+__device__ __forceinline__ void ag_st(int32_t* p, int32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void ag_std(double* p, double v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void release_agent() { __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent"); }
+__device__ __forceinline__ void complete_vmem() {  // every issued load / store / atomic done
+  __builtin_amdgcn_s_waitcnt((0) | (7 << 4) | (15 << 8));
+  asm volatile("" ::: "memory");
+}
+// smallest of best, stop, max_trials: hint (relaxed loads) or exact (read-modify-writes)
+__device__ __forceinline__ int coop_lim_hint(const LSCoopRec* R, int max_trials) {
+  const int be = ag_ld(&R->best), st = ag_ld(&R->stop);
+  const int m = be < st ? be : st;
+  return m < max_trials ? m : max_trials;
+}
+__device__ __forceinline__ int coop_lim(LSCoopRec* R, int max_trials) {
+  const int be = ag_rmw_ld(&R->best), st = ag_rmw_ld(&R->stop);
+  const int m = be < st ? be : st;
+  return m < max_trials ? m : max_trials;
+}
+// α of trial j: the reference's repeated α *= shrink (:82), j − 1 times
+__device__ __forceinline__ double trial_alpha(const LSParams& ls, int j) {
+  double a = ls.alpha0;
+  for (int k = 1; k < j; ++k) a *= ls.shrink;
+  return a;
+}
+
+// Publish trajectory b (trial 1 rejected) in launch `gen`: called by one lane.
+__device__ __forceinline__ void coop_publish(const LSCoop& c, uint32_t gen, int b, int max_trials) {
+  LSCoopRec* R = c.rec + b;
+  ag_st(&R->next, 2);
+  ag_st(&R->best, max_trials + 1);
+  ag_st(&R->stop, max_trials + 1);
+  ag_st(&R->fin, 0);
+  __hip_atomic_store(&R->mask, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // trial 1 done
+  release_agent();  // the record, and trial 1's rollout stores, before the entry
+  const int slot = __hip_atomic_fetch_add(c.ctl + (gen & 1), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(c.list + slot, ((uint64_t)gen << 32) | (uint32_t)b, __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// A published trajectory with trials left to hand out, breadth first (smallest `next`,
+// ties to the first entry at or after this wave's rotated start); -1 if none. Relaxed
+// reads: a hint, the grab itself is exact. `unwritten`: a reserved list slot is not
+// written yet (its publisher is mid-way: the slot still holds another launch's entry).
+__device__ __attribute__((unused)) int coop_find(const LSCoop& c, uint32_t gen, int n, int max_trials,
+                                                 int start, bool& unwritten) {
+  const int l = threadIdx.x & 63;
+  int best_b = -1, best_next = 0x7fffffff;
+  for (int base = 0; base < n; base += 64) {
+    int i = start + base + l;
+    i = i >= n ? i - n : i;
+    i = i >= n ? i - n : i;
+    int key = 0x7fffffff, bb = -1;
+    bool unw = false;
+    if (base + l < n) {
+      const uint64_t e = __hip_atomic_load(c.list + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if ((uint32_t)(e >> 32) != gen) {
+        unw = true;
+      } else {
+        bb = (int)(uint32_t)e;
+        const LSCoopRec* R = c.rec + bb;
+        const int nx = ag_ld(&R->next);
+        if (nx <= coop_lim_hint(R, max_trials)) key = nx;
+      }
+    }
+    if (__any(unw)) unwritten = true;
+    int m = key;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      const int q = __shfl_xor(m, o);
+      m = q < m ? q : m;
+    }
+    m = __builtin_amdgcn_readfirstlane(m);
+    if (m < best_next) {
+      const uint64_t lanes = __ballot(key == m);
+      const int k = __builtin_ctzll(lanes);
+      best_next = m;
+      best_b = __builtin_amdgcn_readlane(bb, k);
+      if (m <= 2) break;  // nothing is fresher than an untouched trajectory
+    }
+  }
+  return best_b;
+}
+
+// Trajectory b's outcome, once trials 1..lim are evaluated (whole wave).
+template <int NX, int NU>
+__device__ void coop_finalize(const LQParams& P, int b, int B, int T, const IterArgs& a, const LSCoop& c,
+                              const LSParams& ls, double* ring, int lim) {
+  LSCoopRec* R = c.rec + b;
+  int best = 0;
+  double cost = 0.0, du2 = 0.0;
+  if ((threadIdx.x & 63) == 0) {
+    best = ag_rmw_ld(&R->best);
+    cost = ag_rmw_ldd(c.cost + (size_t)b * COOP_MAX_TRIALS + lim - 1);
+    du2 = ag_rmw_ldd(c.du2 + (size_t)b * COOP_MAX_TRIALS + lim - 1);
+  }
+  const bool accepted = __builtin_amdgcn_readfirstlane(best) <= ls.max_trials;  // then best == lim
+  // trial 2's group stored as it ran; any other final rollout is rolled out again,
+  // storing (an exhausted one only for ilqr_iterate: fit keeps the previous iterate)
+  if (lim != 2 && (accepted || !a.res_parity)) {
+    const int g = (threadIdx.x & 63) >> 4;
+    double scratch = 0.0;
+    (void)lq_forward_wave_ring<NX, NU, PIPE_R, PIPE_PF, true, true>(
+        P, b, B, T, g == 0, a.x, a.u, a.xtraj, a.d, a.K, 0.0, a.xnew, a.unew, &scratch, ls, ring,
+        CandPass{trial_alpha(ls, lim), 0});
+  }
+  if ((threadIdx.x & 63) == 0) {
+    if (a.trials) a.trials[b] = accepted ? lim : ls.max_trials;
+    if (a.du2) a.du2[b] = du2;
+    if (a.iters) a.iters[b] = a.iter;
+    if (!accepted) {
+      a.status[b] = (cost != cost) ? ILQR_TRAJ_NAN : ILQR_TRAJ_LS_EXHAUSTED;
+      if (a.res_parity) a.res_parity[b] = a.parity;
+    } else {
+      a.new_cost[b] = cost;  // prev_cost = new_cost (:168)
+      if (du2 <= ls.tol) {   // (:171)
+        a.status[b] = ILQR_TRAJ_CONVERGED;
+        if (a.res_parity) a.res_parity[b] = a.parity;
+      }
+    }
+  }
+}
+
+// Grab trials j0 .. j0+3 of trajectory b, evaluate them, and finalise b if these were
+// the last needed (whole wave).
+template <int NX, int NU>
+__device__ void coop_evaluate(const LQParams& P, int b, int B, int T, const IterArgs& a, const LSCoop& c,
+                              const LSParams& ls, double* ring) {
+  LSCoopRec* R = c.rec + b;
+  const int l = threadIdx.x & 63, g = l >> 4;
+  int j0 = 0, lim0 = 0;
+  if (l == 0) {
+    j0 = __hip_atomic_fetch_add(&R->next, 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    lim0 = coop_lim(R, ls.max_trials);
+  }
+  j0 = __builtin_amdgcn_readfirstlane(j0);
+  lim0 = __builtin_amdgcn_readfirstlane(lim0);
+  if (j0 > lim0) return;  // raced past the needed set: nothing to do
+  const int j = j0 + g;   // this group's trial
+  const bool mine = j <= lim0;
+  // the cost to beat: written before this launch (in place by fit's finaliser of b only,
+  // once no trial of b is needed any more)
+  const double pc = a.prev_cost ? a.prev_cost[b] : INFINITY;
+  double du2 = 0.0;
+  const FwdOut r = lq_forward_wave_ring<NX, NU, PIPE_R, PIPE_PF, true, true>(
+      P, b, B, T, mine, a.x, a.u, a.xtraj, a.d, a.K, pc, a.xnew, a.unew, &du2, ls, ring,
+      CandPass{trial_alpha(ls, j), j0 == 2 ? 0 : -1});
+  if ((l & 15) == 0 && mine) {
+    ag_std(c.cost + (size_t)b * COOP_MAX_TRIALS + j - 1, r.cost);
+    ag_std(c.du2 + (size_t)b * COOP_MAX_TRIALS + j - 1, du2);
+    if (pc - r.cost > 0.0)  // (:77-80); NaN compares false
+      __hip_atomic_fetch_min(&R->best, j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else if (r.eo)
+      __hip_atomic_fetch_min(&R->stop, j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  // costs and best/stop complete before the mask bits; trial 2's rollout (stored as it
+  // ran) also written back from this XCD's L2
+  if (j0 == 2)
+    release_agent();
+  else
+    complete_vmem();
+  int fin = 0, lim = 0;
+  if (l == 0) {
+    uint64_t bits = 0;
+    for (int k = 0; k < 4; ++k)
+      if (j0 + k <= lim0) bits |= 1ull << (j0 + k - 1);
+    const uint64_t m =
+        __hip_atomic_fetch_or(&R->mask, bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) | bits;
+    lim = coop_lim(R, ls.max_trials);
+    const uint64_t need = lim >= 64 ? ~0ull : ((1ull << lim) - 1ull);
+    if ((m & need) == need) {
+      int z = 0;
+      fin = __hip_atomic_compare_exchange_strong(&R->fin, &z, 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT) ? 1 : 0;
+    }
+  }
+  fin = __builtin_amdgcn_readfirstlane(fin);
+  lim = __builtin_amdgcn_readfirstlane(lim);
+  if (fin) coop_finalize<NX, NU>(P, b, B, T, a, c, ls, ring, lim);
+}
+
+// The work loop every wave of the launch enters once it is done with its own
+// trajectories: while a published trajectory has trials to hand out, grab and evaluate;
+// then leave. Nobody waits for work that is not there yet: a wave always finds its own
+// published trajectories (it wrote their entries), so a helper that left early costs
+// only speed — and waves waiting for later publications measured expensive (a thousand
+// waves polling the list length slowed the waves still working: cold iteration 144 →
+// 219 µs; with a per-wave done counter and exit ticket, same-address atomics from every
+// wave, 190 µs). Each launch counts its list in ctl[gen & 1] and zeroes the other half
+// for the next launch; stale entries carry another generation.
+template <int NX, int NU>
+__device__ void lq_coop_search(const LQParams& P, int B, int T, const IterArgs& a, const LSParams& ls,
+                               double* ring, int wid) {
+  const LSCoop c = *a.coop;  // scalar loads, here at the end of the wave's own work
+  const uint32_t gen = a.coop_gen;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  constexpr uint64_t WAIT_TICKS = 20000;  // 200 µs at the 100 MHz real-time counter
+  while (true) {
+    const int n = __builtin_amdgcn_readfirstlane(ag_ld(c.ctl + (gen & 1)));
+    if (n == 0) break;
+    bool unwritten = false;
+    const int b = coop_find(c, gen, n, ls.max_trials, (int)(((uint64_t)wid * 2654435761u) % (uint32_t)n),
+                            unwritten);
+    if (b >= 0) {
+      coop_evaluate<NX, NU>(P, b, B, T, a, c, ls, ring);
+      continue;
+    }
+    // a reserved entry is written moments after its slot: worth a short wait
+    if (!unwritten || __builtin_amdgcn_s_memrealtime() - t0 > WAIT_TICKS) break;
+    __builtin_amdgcn_s_sleep(8);
+  }
+}
+
+// The fused iteration's forward with the cooperative search: trial 1 in the wave's own
+// groups (the ring forward's sequential code at max_trials = 1); an accepted trajectory
+// is done as in iter_forward_wave_active, an open one is published.
+template <int NX, int NU>
+__device__ __forceinline__ void iter_forward_wave_coop(const LQParams& P, int b0, int B, int T,
+                                                       const IterArgs& a, const LSParams& ls,
+                                                       double* ring, bool active) {
+  const int j = threadIdx.x & 15;
+  const int b = b0 + ((threadIdx.x & 63) >> 4);
+  LSParams ls1 = ls;
+  ls1.max_trials = 1;
+  double du2 = 0.0;
+  const double pc = (a.prev_cost && active) ? a.prev_cost[b] : INFINITY;
+  const FwdOut r = lq_forward_wave_ring<NX, NU, PIPE_R, PIPE_PF>(P, b0, B, T, active, a.x, a.u, a.xtraj, a.d,
+                                                                 a.K, pc, a.xnew, a.unew, &du2, ls1, ring);
+  if (j == 0 && active) {
+    if (!r.accepted) {
+      coop_publish(*a.coop, a.coop_gen, b, ls.max_trials);  // status stays OK until finalised
+    } else {
+      if (a.trials) a.trials[b] = 1;
+      if (a.du2) a.du2[b] = du2;
+      if (a.iters) a.iters[b] = a.iter;
       a.new_cost[b] = r.cost;
       if (du2 <= ls.tol) {
         a.status[b] = ILQR_TRAJ_CONVERGED;

@@ -23,6 +23,29 @@ struct LSParams {
   int max_trials;  // line-search cap
 };
 
+// Cooperative line search of the fused LQ iteration (lq_coop_search, ilqr_fwd_ring.h;
+// DESIGN.md §4): a trajectory still open after its first trial is published to a list,
+// and every wave of the launch that is done with its own trajectories evaluates the
+// remaining trials of published ones, four candidates per grab. Needs max_trials ≤ 64
+// (one mask bit per trial).
+struct LSCoopRec {  // per trajectory, agent-scope atomics only
+  int32_t next;     // next trial to hand out
+  int32_t best;     // smallest accepted trial (max_trials + 1: none yet)
+  int32_t stop;     // smallest rejected trial whose α·δu vanished (max_trials + 1: none)
+  int32_t fin;      // 0 → 1 by the wave that finalises the trajectory
+  uint64_t mask;    // bit j − 1: trial j evaluated
+  uint64_t pad;
+};
+struct LSCoop {
+  LSCoopRec* rec;     // (B); nullptr: the sequential search of the ring forward
+  double* cost;       // (B, 64) each evaluated trial's cost
+  double* du2;        // (B, 64) each evaluated trial's Σ(ū − u)²
+  uint64_t* list;     // (B) published trajectories: launch generation << 32 | trajectory
+                      // (an entry of another generation is stale: not written yet)
+  int32_t* ctl;       // [gen & 1]: list length of launch `gen` (the launch zeroes the other)
+};
+constexpr int COOP_MAX_TRIALS = 64;
+
 // Buffers of one fused iteration (fit loop body).
 struct IterArgs {
   const double* x;      // (B, T+1, nx) current iterate
@@ -43,6 +66,10 @@ struct IterArgs {
   int iter;             // 1-based iteration index (fit)
   int init;             // fit's first iteration on the fused LQ kernel: the kernel itself sets
                         // prev_cost = Inf, status OK, res_parity = input, iters = 0 (fit_init)
+  const LSCoop* coop;   // the fused LQ kernel's cooperative line search (device memory, one
+                        // per handle; read only when the search starts, so its pointers
+                        // hold no SGPRs through the backward pass); nullptr: off
+  uint32_t coop_gen;    // the launch's generation (per handle, counts fused launches)
 };
 
 // Returns hipSuccess or the launch error. All launches are asynchronous on `s`.
@@ -93,14 +120,15 @@ hipError_t launch_fit_init(int B, double* prev_cost, int32_t* status, int32_t* r
                            int32_t* iters, hipStream_t s);
 // x_out[b] = the buffer res_parity[b] names (final_parity for still-running ones,
 // whose status becomes MAX_ITER), and u; cost/iters/status copied out (each may be
-// null).
+// null). The call-status bits go through dflags (two zeroed device words, re-armed by
+// the kernel) into `flags` (host-mapped, may be null).
 hipError_t launch_gather_result(int B, int T, int nx, int nu, const double* xin, const double* uin,
                                 const double* x0, const double* u0, const double* x1,
                                 const double* u1, const int32_t* res_parity, int32_t* status,
                                 int final_parity, const double* fit_cost, const int32_t* fit_iters,
                                 double* x_out, double* u_out, double* cost_out,
-                                int32_t* iters_out, int32_t* status_out, int32_t* flags,
-                                hipStream_t s);
+                                int32_t* iters_out, int32_t* status_out, int32_t* dflags,
+                                int32_t* flags, hipStream_t s);
 // (N, R, C) row-major → (N, R2, C2) zero-padded (R2 ≥ R, C2 ≥ C), and back.
 hipError_t launch_pad3(const double* src, double* dst, size_t N, int R, int C, int R2, int C2,
                        hipStream_t s);
@@ -108,6 +136,14 @@ hipError_t launch_unpad3(const double* src, double* dst, size_t N, int R, int C,
                          hipStream_t s);
 hipError_t launch_fill_i32(int32_t* p, int n, int32_t v, hipStream_t s);
 hipError_t launch_fill_f64(double* p, int n, double v, hipStream_t s);
+// fit's per-iteration record (ilqr_history, include/ilqr.h) of iteration `it`, from the
+// per-trajectory words the iteration kernels left (iters[b] == it: the trajectory ran
+// it; cost = the in-place prev_cost; status after the iteration). Cost/du2 arrays of
+// the family's dtype (f32: float), α formed in that dtype as the forward formed it.
+hipError_t launch_record_history(int B, int it, const int32_t* status, const int32_t* iters,
+                                 const int32_t* trials, const void* cost, const void* du2, bool f32,
+                                 double alpha0, double shrink, double* h_cost, int32_t* h_trials,
+                                 double* h_alpha, double* h_du2, hipStream_t s);
 // *out = #trajectories with status OK (out may be host-mapped memory)
 hipError_t launch_count_running(int B, const int32_t* status, int32_t* out, hipStream_t s);
 bool lq_supported(int nx, int nu);

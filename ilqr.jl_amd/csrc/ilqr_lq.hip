@@ -890,8 +890,11 @@ __global__ __launch_bounds__(256, 4) void lq_iter_pipe_kernel(LQParams P, int B,
   }
 }
 
-// One wave per trajectory (four per block). `flags` (host-mapped, may be null)
-// collects the call status: bit 0 a NaN trajectory, bit 1 an exhausted line search.
+// One wave per trajectory (four per block). The call status (bit 0 a NaN trajectory,
+// bit 1 an exhausted line search) is OR-ed into a DEVICE word, dflags[0], with
+// device-scope atomics; the last block to finish (ticket dflags[1]) copies it to
+// `flags` (host-mapped, may be null) with one plain store and re-arms both words for
+// the next call — no device atomics on host memory (those need PCIe AtomicOps).
 __global__ __launch_bounds__(256) void gather_kernel(int B, int T, int nx, int nu, const double* xin,
                                                      const double* uin, const double* x0, const double* u0,
                                                      const double* x1, const double* u1,
@@ -899,28 +902,62 @@ __global__ __launch_bounds__(256) void gather_kernel(int B, int T, int nx, int n
                                                      int final_parity, const double* fit_cost,
                                                      const int32_t* fit_iters, double* x_out, double* u_out,
                                                      double* cost_out, int32_t* iters_out,
-                                                     int32_t* status_out, int32_t* flags) {
+                                                     int32_t* status_out, int32_t* dflags, int32_t* flags) {
   const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int l = threadIdx.x & 63;
+  if (b < B) {
+    const int32_t st0 = status[b];
+    const bool running = st0 == ILQR_TRAJ_OK;
+    const int par = running ? final_parity : res_parity[b];
+    if (par != PARITY_OUT) {  // PARITY_OUT: the last iteration wrote x_out / u_out itself
+      const double* xs = (par == PARITY_INPUT ? xin : (par ? x1 : x0)) + (size_t)b * (T + 1) * nx;
+      const double* us = (par == PARITY_INPUT ? uin : (par ? u1 : u0)) + (size_t)b * T * nu;
+      for (int i = l; i < (T + 1) * nx; i += 64) x_out[(size_t)b * (T + 1) * nx + i] = xs[i];
+      for (int i = l; i < T * nu; i += 64) u_out[(size_t)b * T * nu + i] = us[i];
+    }
+    if (l == 0) {  // the lane that read status[b] is the one that rewrites it
+      const int32_t st = running ? ILQR_TRAJ_MAX_ITER : st0;
+      status[b] = st;
+      if (status_out) status_out[b] = st;
+      if (cost_out) cost_out[b] = fit_cost[b];
+      if (iters_out) iters_out[b] = fit_iters[b];
+      const int f = (st == ILQR_TRAJ_NAN ? 1 : 0) | (st == ILQR_TRAJ_LS_EXHAUSTED ? 2 : 0);
+      if (f) __hip_atomic_fetch_or(dflags, f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    const int ticket = __hip_atomic_fetch_add(dflags + 1, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (ticket == (int)gridDim.x - 1) {  // every block's OR is visible
+      const int32_t v = __hip_atomic_load(dflags, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+      if (flags) *(volatile int32_t*)flags = v;
+      dflags[0] = 0;
+      dflags[1] = 0;
+    }
+  }
+}
+
+template <class V>
+__global__ void record_history_kernel(int B, int it, const int32_t* __restrict__ status,
+                                      const int32_t* __restrict__ iters, const int32_t* __restrict__ trials,
+                                      const V* __restrict__ cost, const V* __restrict__ du2, V alpha0, V shrink,
+                                      double* h_cost, int32_t* h_trials, double* h_alpha, double* h_du2) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
-  const int32_t st0 = status[b];
-  const bool running = st0 == ILQR_TRAJ_OK;
-  const int par = running ? final_parity : res_parity[b];
-  if (par != PARITY_OUT) {  // PARITY_OUT: the last iteration wrote x_out / u_out itself
-    const double* xs = (par == PARITY_INPUT ? xin : (par ? x1 : x0)) + (size_t)b * (T + 1) * nx;
-    const double* us = (par == PARITY_INPUT ? uin : (par ? u1 : u0)) + (size_t)b * T * nu;
-    for (int i = l; i < (T + 1) * nx; i += 64) x_out[(size_t)b * (T + 1) * nx + i] = xs[i];
-    for (int i = l; i < T * nu; i += 64) u_out[(size_t)b * T * nu + i] = us[i];
+  const size_t o = (size_t)(it - 1) * B + b;
+  const bool ran = iters[b] == it;
+  const int32_t st = status[b];
+  const bool acc = ran && (st == ILQR_TRAJ_OK || st == ILQR_TRAJ_CONVERGED);
+  const int n = ran ? trials[b] : 0;
+  if (h_trials) h_trials[o] = n;
+  if (h_cost) h_cost[o] = acc ? (double)cost[b] : (double)NAN;
+  if (h_alpha) {
+    V a = alpha0;  // the forward's repeated α *= shrink (forward_pass.jl:82)
+    for (int k = 1; k < n; ++k) a *= shrink;
+    h_alpha[o] = acc ? (double)a : (double)NAN;
   }
-  if (l == 0) {  // the lane that read status[b] is the one that rewrites it
-    const int32_t st = running ? ILQR_TRAJ_MAX_ITER : st0;
-    status[b] = st;
-    if (status_out) status_out[b] = st;
-    if (cost_out) cost_out[b] = fit_cost[b];
-    if (iters_out) iters_out[b] = fit_iters[b];
-    const int f = (st == ILQR_TRAJ_NAN ? 1 : 0) | (st == ILQR_TRAJ_LS_EXHAUSTED ? 2 : 0);
-    if (flags && f) __hip_atomic_fetch_or(flags, f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
+  if (h_du2) h_du2[o] = ran ? (double)du2[b] : (double)NAN;
 }
 
 __global__ void fit_init_kernel(int B, double* prev_cost, int32_t* status, int32_t* res_parity,
@@ -1115,12 +1152,29 @@ hipError_t launch_gather_result(int B, int T, int nx, int nu, const double* xin,
                                 const double* u1, const int32_t* res_parity, int32_t* status,
                                 int final_parity, const double* fit_cost, const int32_t* fit_iters,
                                 double* x_out, double* u_out, double* cost_out,
-                                int32_t* iters_out, int32_t* status_out, int32_t* flags,
-                                hipStream_t s) {
+                                int32_t* iters_out, int32_t* status_out, int32_t* dflags,
+                                int32_t* flags, hipStream_t s) {
   if (B <= 0) return hipSuccess;
   gather_kernel<<<(B + 3) / 4, 256, 0, s>>>(B, T, nx, nu, xin, uin, x0, u0, x1, u1, res_parity, status,
                                             final_parity, fit_cost, fit_iters, x_out, u_out, cost_out,
-                                            iters_out, status_out, flags);
+                                            iters_out, status_out, dflags, flags);
+  return hipGetLastError();
+}
+
+hipError_t launch_record_history(int B, int it, const int32_t* status, const int32_t* iters,
+                                 const int32_t* trials, const void* cost, const void* du2, bool f32,
+                                 double alpha0, double shrink, double* h_cost, int32_t* h_trials,
+                                 double* h_alpha, double* h_du2, hipStream_t s) {
+  if (B <= 0) return hipSuccess;
+  const unsigned g = (unsigned)((B + 255) / 256);
+  if (f32)
+    record_history_kernel<float><<<g, 256, 0, s>>>(B, it, status, iters, trials, (const float*)cost,
+                                                   (const float*)du2, (float)alpha0, (float)shrink, h_cost,
+                                                   h_trials, h_alpha, h_du2);
+  else
+    record_history_kernel<double><<<g, 256, 0, s>>>(B, it, status, iters, trials, (const double*)cost,
+                                                    (const double*)du2, alpha0, shrink, h_cost, h_trials,
+                                                    h_alpha, h_du2);
   return hipGetLastError();
 }
 

@@ -629,7 +629,7 @@ __global__ __launch_bounds__(64 * W) void tl_iter_forward_kernel(TwoLinkParams P
   const double pc = a.prev_cost ? a.prev_cost[b] : INFINITY;
   const TwoLinkModel<NU> m{P, tl_roll_consts(P)};
   const FgOut<double> r = fwd_group<TwoLinkModel<NU>, L>(m, b, B, T, a.x, a.u, a.xtraj, a.d, a.K, pc, a.xnew,
-                                                          a.unew, ls);
+                                                          a.unew, ls, a.res_parity == nullptr);
   if (!r.owner) return;
   if (a.trials) a.trials[b] = r.trials;
   if (a.du2) a.du2[b] = r.du2;

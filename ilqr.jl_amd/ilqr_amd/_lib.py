@@ -35,6 +35,7 @@ SCHED_BACKWARD_WAVE = 4
 SCHED_BACKWARD_BLOCK = 8
 SCHED_FUSED = 16
 SCHED_FORWARD_MFMA = 32
+SCHED_SEQUENTIAL_SEARCH = 64
 
 PROBLEM_LQ = 1
 PROBLEM_TWO_LINK = 2
@@ -68,6 +69,11 @@ class Tiles(C.Structure):
 class Options(C.Structure):
     _fields_ = [("max_iter", C.c_int32), ("max_trials", C.c_int32), ("tol", C.c_double),
                 ("mu", C.c_double), ("alpha0", C.c_double), ("shrink", C.c_double)]
+
+
+class History(C.Structure):
+    """ilqr_history (include/ilqr.h): device arrays (max_iter, batch), each may be NULL."""
+    _fields_ = [("cost", C.c_void_p), ("trials", C.c_void_p), ("alpha", C.c_void_p), ("du2", C.c_void_p)]
 
 
 class ChainStruct(C.Structure):
@@ -107,6 +113,8 @@ SIGNATURES = {
     "ilqr_iterate": (C.c_int, [P, C.POINTER(Problem), C.POINTER(Options), P, P, P, P, P, P,
                                P, P, P, P]),
     "ilqr_fit": (C.c_int, [P, C.POINTER(Problem), C.POINTER(Options), P, P, P, P, P, P, P, P]),
+    "ilqr_fit_ex": (C.c_int, [P, C.POINTER(Problem), C.POINTER(Options), P, P, P, P, P, P, P, P,
+                              C.POINTER(History)]),
     "ilqr_malloc": (C.c_int, [P, C.c_size_t, C.POINTER(P)]),
     "ilqr_free": (C.c_int, [P, P]),
     "ilqr_memcpy_h2d": (C.c_int, [P, P, P, C.c_size_t]),
@@ -131,6 +139,7 @@ SIGNATURES = {
     "ilqr_chain_forward": (C.c_int, [P, C.POINTER(Options), P, P, P, P, P, P, P, P, P, P, P]),
     "ilqr_chain_iterate": (C.c_int, [P, C.POINTER(Options), P, P, P, P, P, P, P, P, P, P]),
     "ilqr_chain_fit": (C.c_int, [P, C.POINTER(Options), P, P, P, P, P, P, P, P]),
+    "ilqr_chain_fit_ex": (C.c_int, [P, C.POINTER(Options), P, P, P, P, P, P, P, P, C.POINTER(History)]),
 }
 
 _lib = None

@@ -197,9 +197,13 @@ def forward_pass(x, u, x_traj, du, K, prev_cost, dynamicsf, immediate_cost, fina
 
 
 def fit(x_init, u_init, dynamicsf, immediate_cost, final_cost, *, x_traj=None,
-        max_iter: int = 100, tol: float = 1e-6, return_info: bool = False):
+        max_iter: int = 100, tol: float = 1e-6, return_info: bool = False, verbose: bool = False):
     """→ (x̄, ū) exactly like iLQR.fit (forward_pass.jl:148-179), including its
-    quirk of returning the iterate BEFORE the update that met `tol` (:171)."""
+    quirk of returning the iterate BEFORE the update that met `tol` (:171).
+    verbose: print the reference's per-iteration line `Iteration: i  Total Cost: c`
+    (:167) — for each trajectory of a batch — from the fit's history (ilqr_fit_ex);
+    return_info adds it as info["history"] (arrays (max_iter, batch): cost, trials,
+    alpha, du2)."""
     if not isinstance(max_iter, (int, np.integer)) or isinstance(max_iter, bool):
         raise TypeError("max_iter::Int64")   # forward_pass.jl:152
     xb, batched, is_t = _as_batch(x_init, "x_init", 2)
@@ -212,17 +216,22 @@ def fit(x_init, u_init, dynamicsf, immediate_cost, final_cost, *, x_traj=None,
     fam = _family(dynamicsf, immediate_cost, final_cost)
     if fam == "closures":
         r = _fit_closures(xb, ub, xt, dynamicsf, immediate_cost, final_cost, int(max_iter),
-                          float(tol))
+                          float(tol), history=verbose or return_info)
     elif fam == "chain":
         dt = _eltype(x_init)
         s = _chain_solver(xb, ub, dynamicsf, immediate_cost, final_cost, dt)
         r = s.fit(xb.to(dt), ub.to(dt), x_traj=None if xt is None else xt.to(dt),
-                  max_iter=int(max_iter), tol=float(tol))
+                  max_iter=int(max_iter), tol=float(tol), history=verbose or return_info)
         s.close()
     else:
         s = _solver(xb, ub, dynamicsf, immediate_cost, final_cost)
-        r = s.fit(xb, ub, x_traj=xt, max_iter=int(max_iter), tol=float(tol))
+        r = s.fit(xb, ub, x_traj=xt, max_iter=int(max_iter), tol=float(tol),
+                  history=verbose or return_info)
         s.close()
+    if verbose and r.history is not None:
+        from .solver import print_history
+        for b in range(xb.shape[0]):
+            print_history(r.history, b)
     st = r.status.cpu().numpy()
     if (st == _lib.TRAJ_NAN).any():
         raise AssertionError("NaN in a trajectory (reference: AssertionError)")
@@ -232,11 +241,13 @@ def fit(x_init, u_init, dynamicsf, immediate_cost, final_cost, *, x_traj=None,
     out = (_out(r.x, batched, is_t), _out(r.u, batched, is_t))
     if return_info:
         info = {"cost": r.cost.cpu().numpy(), "iters": r.iters.cpu().numpy(), "status": st}
+        if r.history is not None:
+            info["history"] = {k: v.cpu().numpy() for k, v in r.history.items()}
         return out + (info,)
     return out
 
 
-def _fit_closures(xb, ub, xt, dynamicsf, immediate_cost, final_cost, max_iter, tol):
+def _fit_closures(xb, ub, xt, dynamicsf, immediate_cost, final_cost, max_iter, tol, history=False):
     """fit (forward_pass.jl:148-179) for arbitrary torch closures: per iteration,
     derivative tiles (torch.func on the device) → ilqr_backward_tiles (HIP) →
     forward_pass rollout of the user dynamics (torch on the device). Trajectories
@@ -249,7 +260,12 @@ def _fit_closures(xb, ub, xt, dynamicsf, immediate_cost, final_cost, max_iter, t
     prev = torch.full((nb,), float("inf"), dtype=torch.float64, device=dev)   # :159
     status = torch.zeros(nb, dtype=torch.int32, device=dev)
     iters = torch.zeros(nb, dtype=torch.int32, device=dev)
-    max_trials = _lib.default_options().max_trials
+    opts = _lib.default_options()
+    max_trials = opts.max_trials
+    hist = None
+    if history:
+        from .solver import alloc_history
+        hist, _ = alloc_history(max_iter, nb, dev)
     for it in range(1, max_iter + 1):                                            # :161
         run = status == _lib.TRAJ_OK
         if not bool(run.any()):
@@ -258,8 +274,8 @@ def _fit_closures(xb, ub, xt, dynamicsf, immediate_cost, final_cost, max_iter, t
         d, K, bst = s.backward_tiles(tl)                                          # :162
         status = torch.where(run & (bst == _lib.TRAJ_NAN), _lib.TRAJ_NAN, status).to(torch.int32)
         run = status == _lib.TRAJ_OK
-        xn, un, c, _, ok = _tiles.rollout_forward(xi, ui, xt, d, K, prev, dynamicsf,
-                                                  immediate_cost, final_cost, max_trials)  # :163-166
+        xn, un, c, ntr, ok = _tiles.rollout_forward(xi, ui, xt, d, K, prev, dynamicsf,
+                                                    immediate_cost, final_cost, max_trials)  # :163-166
         iters = torch.where(run, it, iters).to(torch.int32)
         bad = run & ~ok
         status = torch.where(bad, torch.where(torch.isnan(c), _lib.TRAJ_NAN, _lib.TRAJ_LS_EXHAUSTED),
@@ -268,13 +284,20 @@ def _fit_closures(xb, ub, xt, dynamicsf, immediate_cost, final_cost, max_iter, t
         prev = torch.where(acc, c, prev)                                          # :168
         du2 = ((un - ui) ** 2).sum(dim=(1, 2))
         conv = acc & (du2 <= tol)                                                 # :171
+        if hist is not None:  # ilqr_history's fields for this iteration
+            ntr = torch.as_tensor(ntr, device=dev).to(torch.int32)
+            hist["trials"][it - 1] = torch.where(run, ntr, 0)
+            hist["cost"][it - 1] = torch.where(acc, c, float("nan"))
+            alpha = opts.alpha0 * torch.pow(torch.full_like(c, opts.shrink), (ntr - 1).clamp(min=0).double())
+            hist["alpha"][it - 1] = torch.where(acc, alpha, float("nan"))
+            hist["du2"][it - 1] = torch.where(run, du2, float("nan"))
         status = torch.where(conv, _lib.TRAJ_CONVERGED, status).to(torch.int32)
         step = acc & ~conv
         xi = torch.where(step[:, None, None], xn, xi)                            # :174-175
         ui = torch.where(step[:, None, None], un, ui)
     s.close()
     status = torch.where(status == _lib.TRAJ_OK, _lib.TRAJ_MAX_ITER, status).to(torch.int32)
-    return FitResult(xi, ui, prev, iters, status, _lib.OK)
+    return FitResult(xi, ui, prev, iters, status, _lib.OK, hist)
 
 
 __all__ = ["fit", "backward_pass", "forward_pass", "LineSearchExhausted"]

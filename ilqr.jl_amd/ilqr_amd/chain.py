@@ -25,7 +25,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from .solver import FitResult, _ptr, _req
+from .solver import FitResult, _ptr, _req, alloc_history
 from .urdf import Chain, parse_urdf
 
 ROBOTS = os.path.join(os.path.dirname(os.path.abspath(__file__)), "robots")
@@ -298,8 +298,10 @@ class ChainSolver:
                                                _ptr(new_cost), _ptr(du2), _ptr(trials),
                                                _ptr(status)), "ilqr_chain_iterate")
 
-    def fit(self, x_init, u_init, max_iter=100, tol=1e-6, x_traj=None, options=None) -> FitResult:
-        """iLQR.fit (forward_pass.jl:148-179) for the whole batch; synchronises."""
+    def fit(self, x_init, u_init, max_iter=100, tol=1e-6, x_traj=None, options=None,
+            history: bool = False) -> FitResult:
+        """iLQR.fit (forward_pass.jl:148-179) for the whole batch; synchronises. history:
+        also return the per-iteration record (ilqr_chain_fit_ex; FitResult.history)."""
         self._xu(x_init, u_init)
         B = self.batch
         xo, uo = torch.empty_like(x_init), torch.empty_like(u_init)
@@ -308,11 +310,13 @@ class ChainSolver:
         st = self._new(B, dtype=torch.int32)
         o = options or _lib.default_options(max_iter=max_iter, tol=tol)
         self._bind()
-        cs = _lib.check(self.lib.ilqr_chain_fit(self.h, C.byref(o), _ptr(x_init), _ptr(u_init),
-                                                _ptr(x_traj), _ptr(xo), _ptr(uo), _ptr(cost),
-                                                _ptr(iters), _ptr(st)),
+        hist, hst = alloc_history(o.max_iter, B, x_init.device) if history else (None, None)
+        cs = _lib.check(self.lib.ilqr_chain_fit_ex(self.h, C.byref(o), _ptr(x_init), _ptr(u_init),
+                                                   _ptr(x_traj), _ptr(xo), _ptr(uo), _ptr(cost),
+                                                   _ptr(iters), _ptr(st),
+                                                   C.byref(hst) if hst is not None else None),
                         "ilqr_chain_fit", allow=(_lib.ERR_NAN, _lib.ERR_LS_EXHAUSTED))
-        return FitResult(xo, uo, cost, iters, st, cs)
+        return FitResult(xo, uo, cost, iters, st, cs, hist)
 
 
 # -- reference-API callables (recognised by ilqr_amd.fit & co.) ---------------------------

@@ -44,12 +44,14 @@ class MultiSolver:
             pass
 
     def set_schedule(self, pipelined: bool = False, ring_forward: bool = True, backward: str = "auto",
-                     fused: bool = True, forward_mfma: bool = False):
+                     fused: bool = True, forward_mfma: bool = False,
+                     sequential_search: bool = False):
         """As Solver.set_schedule, on every device's handle."""
         bk = {"auto": 0, "wave": _lib.SCHED_BACKWARD_WAVE, "block": _lib.SCHED_BACKWARD_BLOCK}[backward]
         flags = ((_lib.SCHED_PIPELINED if pipelined else 0) | (_lib.SCHED_RING_FORWARD if ring_forward else 0)
                  | bk | (_lib.SCHED_FUSED if fused and not pipelined and backward != "wave" else 0)
-                 | (_lib.SCHED_FORWARD_MFMA if forward_mfma else 0))
+                 | (_lib.SCHED_FORWARD_MFMA if forward_mfma else 0)
+                 | (_lib.SCHED_SEQUENTIAL_SEARCH if sequential_search else 0))
         _lib.check(self.lib.ilqr_multi_set_schedule(self.h, flags), "ilqr_multi_set_schedule")
 
     def fit(self, lq: LQBatch, x_init, u_init, x_traj=None, max_iter=100, tol=1e-6, mu=None,

@@ -41,6 +41,30 @@ class FitResult:
     iters: torch.Tensor    # (B,) iterations run
     status: torch.Tensor   # (B,) ILQR_TRAJ_* codes
     call_status: int       # ilqr_status of the whole call
+    history: dict = None   # fit(history=True): ilqr_history arrays (max_iter, B) — "cost",
+                           # "trials", "alpha", "du2" (include/ilqr.h)
+
+
+def alloc_history(max_iter: int, batch: int, device):
+    """Device arrays for ilqr_history, NaN / 0 filled (entries past the last iteration
+    stay so), and the struct pointing at them."""
+    n = max(max_iter, 1)
+    h = {"cost": torch.full((n, batch), float("nan"), dtype=torch.float64, device=device),
+         "trials": torch.zeros((n, batch), dtype=torch.int32, device=device),
+         "alpha": torch.full((n, batch), float("nan"), dtype=torch.float64, device=device),
+         "du2": torch.full((n, batch), float("nan"), dtype=torch.float64, device=device)}
+    st = _lib.History(*(h[k].data_ptr() for k in ("cost", "trials", "alpha", "du2")))
+    return h, st
+
+
+def print_history(hist, b: int = 0):
+    """The reference's per-iteration line (forward_pass.jl:167) for trajectory b."""
+    tr = hist["trials"][:, b].cpu().numpy()
+    c = hist["cost"][:, b].cpu().numpy()
+    for i in range(len(tr)):
+        if tr[i] == 0:
+            break
+        print(f"Iteration: {i + 1}\t\tTotal Cost: {float(c[i])!r}")  # Julia prints the shortest repr too
 
 
 class Solver:
@@ -81,7 +105,8 @@ class Solver:
         _lib.check(self.lib.ilqr_set_stream(self.h, C.c_void_p(s)), "ilqr_set_stream")
 
     def set_schedule(self, pipelined: bool = False, ring_forward: bool = True,
-                     backward: str = "auto", fused: bool = True, forward_mfma: bool = False):
+                     backward: str = "auto", fused: bool = True, forward_mfma: bool = False,
+                     sequential_search: bool = False):
         """LQ launch schedule (ilqr_set_schedule). pipelined: fit overlaps half of the
         workgroups' forward passes with the other half's backward passes (implies
         backward="wave"); ring_forward: the forward pass streams its inputs HBM → LDS
@@ -89,12 +114,15 @@ class Solver:
         "block" four per wave (4x4x4 4-block MFMA), "auto" block from 2048
         trajectories up; fused: iterate/fit run backward + forward as one kernel (with the
         "block" backward and the ring forward); forward_mfma: the ring forward's mat-vecs
-        on the 4-block f64 MFMA (other rounding). Schedules with the same backward kernel
-        and forward form return the same bits."""
+        on the 4-block f64 MFMA (other rounding); sequential_search: the fused iteration's
+        line search trial after trial per wave instead of the cooperative search (same
+        bits, include/ilqr.h). Schedules with the same backward kernel and forward form
+        return the same bits."""
         bk = {"auto": 0, "wave": _lib.SCHED_BACKWARD_WAVE, "block": _lib.SCHED_BACKWARD_BLOCK}[backward]
         flags = ((_lib.SCHED_PIPELINED if pipelined else 0) | (_lib.SCHED_RING_FORWARD if ring_forward else 0)
                  | bk | (_lib.SCHED_FUSED if fused and not pipelined and backward != "wave" else 0)
-                 | (_lib.SCHED_FORWARD_MFMA if forward_mfma else 0))
+                 | (_lib.SCHED_FORWARD_MFMA if forward_mfma else 0)
+                 | (_lib.SCHED_SEQUENTIAL_SEARCH if sequential_search else 0))
         _lib.check(self.lib.ilqr_set_schedule(self.h, flags), "ilqr_set_schedule")
 
     def set_problem(self, lq):
@@ -216,8 +244,9 @@ class Solver:
         _lib.check(rc, "ilqr_iterate")
 
     def fit(self, x_init, u_init, x_traj=None, max_iter=100, tol=1e-6, mu=None,
-            max_trials=None) -> FitResult:
-        """iLQR.fit for the batch (synchronises)."""
+            max_trials=None, history: bool = False) -> FitResult:
+        """iLQR.fit for the batch (synchronises). history: also return the per-iteration
+        record (ilqr_fit_ex; FitResult.history)."""
         if not isinstance(max_iter, int):
             raise TypeError("max_iter::Int64")  # forward_pass.jl:152
         B, T, nx, nu = self.batch, self.T, self.nx, self.nu
@@ -231,10 +260,12 @@ class Solver:
         st = torch.empty((B,), dtype=torch.int32, device=self.dev)
         self._bind_stream()
         o = _lib.default_options(max_iter=max_iter, tol=float(tol), mu=mu, max_trials=max_trials)
-        rc = self.lib.ilqr_fit(self.h, self._p(), C.byref(o), _ptr(x_init), _ptr(u_init),
-                               _ptr(x_traj), _ptr(xo), _ptr(uo), _ptr(cost), _ptr(iters), _ptr(st))
+        hist, hst = alloc_history(max_iter, B, self.dev) if history else (None, None)
+        rc = self.lib.ilqr_fit_ex(self.h, self._p(), C.byref(o), _ptr(x_init), _ptr(u_init),
+                                  _ptr(x_traj), _ptr(xo), _ptr(uo), _ptr(cost), _ptr(iters), _ptr(st),
+                                  C.byref(hst) if hst is not None else None)
         _lib.check(rc, "ilqr_fit", allow=(_lib.ERR_NAN, _lib.ERR_LS_EXHAUSTED))
-        return FitResult(xo, uo, cost, iters, st, rc)
+        return FitResult(xo, uo, cost, iters, st, rc, hist)
 
 
 def selftest(device: int = 0) -> int:

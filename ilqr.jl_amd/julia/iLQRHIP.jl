@@ -54,6 +54,10 @@ struct Tiles                 # ilqr_tiles: per-step derivatives of an arbitrary 
     lux::Ptr{Float64}; luu::Ptr{Float64}; lfx::Ptr{Float64}; lfxx::Ptr{Float64}
 end
 
+struct History               # ilqr_history: device arrays (max_iter × batch), iteration-major
+    cost::Ptr{Float64}; trials::Ptr{Int32}; alpha::Ptr{Float64}; du2::Ptr{Float64}
+end
+
 mutable struct Options       # ilqr_options
     max_iter::Int32
     max_trials::Int32
@@ -158,6 +162,8 @@ const ILQR_SCHED_RING_FORWARD = Int32(2)
 const ILQR_SCHED_BACKWARD_WAVE = Int32(4)
 const ILQR_SCHED_BACKWARD_BLOCK = Int32(8)
 const ILQR_SCHED_FUSED = Int32(16)
+const ILQR_SCHED_FORWARD_MFMA = Int32(32)
+const ILQR_SCHED_SEQUENTIAL_SEARCH = Int32(64)
 set_schedule!(h::Handle, flags::Integer) =
     check(ccall((:ilqr_set_schedule, libilqr), Cint, (Ptr{Cvoid}, Cint), h.ptr, flags), "ilqr_set_schedule")
 
@@ -321,29 +327,43 @@ function forward_pass(x::AbstractMatrix, u::AbstractMatrix, x_traj::AbstractMatr
     return (x̄, ū, download!(h, zeros(1), co)[1])
 end
 
-"""fit(x_init, u_init, dynamicsf, immediate_cost, final_cost; x_traj, max_iter, tol) -> (x̄, ū)"""
+# the reference's per-iteration line (forward_pass.jl:167), from a fit's history
+function print_history(cost::AbstractVector, trials::AbstractVector)
+    for i in eachindex(trials)
+        trials[i] == 0 && break
+        println("Iteration: ", i, "\t\tTotal Cost: ", cost[i])
+    end
+end
+
+"""fit(x_init, u_init, dynamicsf, immediate_cost, final_cost; x_traj, max_iter, tol, verbose) -> (x̄, ū)
+
+verbose = true prints the reference's `Iteration: i  Total Cost: c` line for every
+iteration (forward_pass.jl:167), from the device fit's history (ilqr_fit_ex)."""
 function fit(x_init::AbstractMatrix, u_init::AbstractMatrix, dynamicsf, immediate_cost, final_cost;
-             x_traj=zero(x_init), max_iter::Int64=100, tol::Float64=1e-6)
+             x_traj=zero(x_init), max_iter::Int64=100, tol::Float64=1e-6, verbose::Bool=false)
     N, nx = size(x_init); M, nu = size(u_init)
     @assert(N == M + 1, "size(x_init)[2] == size(u_init)[1]")          # forward_pass.jl:156
     family(dynamicsf, immediate_cost, final_cost) == :tiles &&
-        return fit_tiles(x_init, u_init, dynamicsf, immediate_cost, final_cost, x_traj, max_iter, tol)
+        return fit_tiles(x_init, u_init, dynamicsf, immediate_cost, final_cost, x_traj, max_iter, tol, verbose)
     h = Handle(nx, nu, M, 1)
     p = Ref(problem(h, dynamicsf, immediate_cost, final_cost))
     o = default_options(); o.max_iter = max_iter; o.tol = tol
     xi = upload(h, to_abi(x_init)); ui = upload(h, to_abi(u_init)); xt = upload(h, to_abi(x_traj))
     xo = alloc(h, Float64, N * nx); uo = alloc(h, Float64, M * nu)
-    st = ccall((:ilqr_fit, libilqr), Cint,
+    hc = alloc(h, Float64, max_iter); ht = upload(h, zeros(Int32, max(max_iter, 1)))
+    hist = Ref(History(hc, ht, C_NULL, C_NULL))
+    st = ccall((:ilqr_fit_ex, libilqr), Cint,
                (Ptr{Cvoid}, Ref{Problem}, Ref{Options}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64},
-                Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Int32}, Ptr{Int32}),
-               h.ptr, p, o, xi, ui, xt, xo, uo, C_NULL, C_NULL, C_NULL)
+                Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Int32}, Ptr{Int32}, Ref{History}),
+               h.ptr, p, o, xi, ui, xt, xo, uo, C_NULL, C_NULL, C_NULL, hist)
     st == ILQR_ERR_LS_EXHAUSTED || check(st, "ilqr_fit")   # exhausted: the last iterate is returned
+    verbose && print_history(download!(h, zeros(max_iter), hc), download!(h, zeros(Int32, max(max_iter, 1)), ht))
     return from_abi(download!(h, zeros(nx, N), xo)), from_abi(download!(h, zeros(nu, M), uo))
 end
 
 # fit (forward_pass.jl:148-179) for arbitrary closures: tiles backward on the GPU, host
 # rollout; same return semantics (the iterate before the update that met tol, :171)
-function fit_tiles(x_init, u_init, f, ℓ, ℓf, x_traj, max_iter, tol)
+function fit_tiles(x_init, u_init, f, ℓ, ℓf, x_traj, max_iter, tol, verbose=false)
     x̄ⁱ = x_init; ūⁱ = u_init
     prev_cost = Inf
     for iter in 1:max_iter
@@ -354,6 +374,7 @@ function fit_tiles(x_init, u_init, f, ℓ, ℓf, x_traj, max_iter, tol)
             e isa LineSearchExhausted && break     # the reference would loop forever here
             rethrow()
         end
+        verbose && println("Iteration: ", iter, "\t\tTotal Cost: ", new_cost)   # :167
         @assert(prev_cost > new_cost); prev_cost = new_cost             # :168
         convert(Float64, sum((ūⁱ⁺¹ - ūⁱ) .^ 2)) <= tol && break          # :171
         x̄ⁱ = x̄ⁱ⁺¹; ūⁱ = ūⁱ⁺¹                                           # :174-175
@@ -367,8 +388,10 @@ struct iLQRProblem
     x::Array{Float64,3}; u::Array{Float64,3}
 end
 
-"""solve!(prob; max_iter, tol): fits every instance; overwrites prob.x / prob.u."""
-function solve!(prob::iLQRProblem; max_iter::Int64=100, tol::Float64=1e-6)
+"""solve!(prob; max_iter, tol, history): fits every instance; overwrites prob.x / prob.u.
+history = true returns (prob, h) with h the per-iteration record (ilqr_fit_ex): Julia
+arrays (batch, max_iter) `cost`, `trials`, `alpha`, `du2` (include/ilqr.h ilqr_history)."""
+function solve!(prob::iLQRProblem; max_iter::Int64=100, tol::Float64=1e-6, history::Bool=false)
     nx, N, nb = size(prob.x); nu = size(prob.u, 1); M = N - 1
     h = Handle(nx, nu, M, nb)
     p = Ref(Problem(ILQR_PROBLEM_LQ, 0, upload(h, rowmajor3(prob.A)), upload(h, rowmajor3(prob.B)),
@@ -376,13 +399,20 @@ function solve!(prob::iLQRProblem; max_iter::Int64=100, tol::Float64=1e-6)
     o = default_options(); o.max_iter = max_iter; o.tol = tol
     xi = upload(h, prob.x); ui = upload(h, prob.u)                      # (nx, N, B) is the ABI layout as is
     xo = alloc(h, Float64, length(prob.x)); uo = alloc(h, Float64, length(prob.u))
-    st = ccall((:ilqr_fit, libilqr), Cint,
+    n = max(max_iter, 1)
+    # (max_iter, batch) row-major = Julia (batch, max_iter): no permute on the way back
+    hd = history ? (alloc(h, Float64, n * nb), upload(h, zeros(Int32, n * nb)), alloc(h, Float64, n * nb),
+                    alloc(h, Float64, n * nb)) : (C_NULL, C_NULL, C_NULL, C_NULL)
+    hist = Ref(History(hd...))
+    st = ccall((:ilqr_fit_ex, libilqr), Cint,
                (Ptr{Cvoid}, Ref{Problem}, Ref{Options}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64},
-                Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Int32}, Ptr{Int32}),
-               h.ptr, p, o, xi, ui, C_NULL, xo, uo, C_NULL, C_NULL, C_NULL)
+                Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Int32}, Ptr{Int32}, Ref{History}),
+               h.ptr, p, o, xi, ui, C_NULL, xo, uo, C_NULL, C_NULL, C_NULL, hist)
     st in (ILQR_OK, ILQR_ERR_LS_EXHAUSTED) || check(st, "ilqr_fit")
     download!(h, prob.x, xo); download!(h, prob.u, uo)
-    return prob
+    history || return prob
+    return prob, (cost=download!(h, zeros(nb, n), hd[1]), trials=download!(h, zeros(Int32, nb, n), hd[2]),
+                  alpha=download!(h, zeros(nb, n), hd[3]), du2=download!(h, zeros(nb, n), hd[4]))
 end
 
 """solve!(prob, devices; …): the same over several GPUs of this node in one process

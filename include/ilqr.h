@@ -161,6 +161,16 @@ ilqr_status ilqr_sync(ilqr_handle* h);
  *                            mat-vecs on the 4-block f64 MFMA in the backward's layout
  *                            instead of DPP row broadcasts: the same function, other
  *                            rounding (agrees to 1e-12).
+ *   ILQR_SCHED_SEQUENTIAL_SEARCH the fused iteration runs the line search wave by
+ *                            wave, trial after trial (forward_pass.jl:70-87 as written).
+ *                            Without it (the default) a trajectory still open after
+ *                            trial 1 has its remaining trials evaluated four at a time
+ *                            by every wave of the launch with nothing else to do,
+ *                            ending at the first accepted trial or as soon as α·δu
+ *                            vanishes at every step (each later trial is then the same
+ *                            rollout): the same x̄, ū, cost, Σ(ū − u)², trial count and
+ *                            status, bit for bit (max_trials ≤ 64, else
+ *                            sequential).
  * Schedules with the same backward kernel return the same bits; the two backward
  * kernels agree to rounding. Unknown bits, or BLOCK with WAVE or
  * PIPELINED → ILQR_ERR_BAD_ARG. */
@@ -170,6 +180,7 @@ ilqr_status ilqr_sync(ilqr_handle* h);
 #define ILQR_SCHED_BACKWARD_BLOCK 8
 #define ILQR_SCHED_FUSED 16
 #define ILQR_SCHED_FORWARD_MFMA 32
+#define ILQR_SCHED_SEQUENTIAL_SEARCH 64
 ilqr_status ilqr_set_schedule(ilqr_handle* h, int flags);
 
 /* iLQR.backward_pass (backward_pass.jl:324-357): gains d (batch,T,nu) and
@@ -204,7 +215,10 @@ ilqr_status ilqr_forward(ilqr_handle* h, const ilqr_problem* p, const ilqr_optio
  * the cost to beat (NULL = +Inf, fit's first iteration, forward_pass.jl:159);
  * new_cost (batch, may alias prev_cost) receives the accepted cost; du2 (batch,
  * may be NULL) receives Σ(ū_new − u)²; status is read (non-zero = skip) and
- * set to CONVERGED / LS_EXHAUSTED / NAN. Asynchronous. The bench "step". */
+ * set to CONVERGED / LS_EXHAUSTED / NAN. A trajectory whose line search exhausts
+ * max_trials leaves the LAST trial's rollout in (x_new, u_new), as the sequential
+ * search of forward_pass.jl:70-87 capped at max_trials would (fit never reads it: an
+ * exhausted trajectory keeps its iterate). Asynchronous. The bench "step". */
 ilqr_status ilqr_iterate(ilqr_handle* h, const ilqr_problem* p, const ilqr_options* o,
                          const double* x, const double* u, const double* x_traj,
                          double* x_new, double* u_new, const double* prev_cost,
@@ -221,6 +235,32 @@ ilqr_status ilqr_fit(ilqr_handle* h, const ilqr_problem* p, const ilqr_options* 
                      const double* x_init, const double* u_init, const double* x_traj,
                      double* x_out, double* u_out, double* cost, int32_t* iters,
                      int32_t* status);
+
+/* Per-iteration record of a fit: what the reference prints on every iteration
+ * (`Iteration: i  Total Cost: new_cost`, forward_pass.jl:167) and inside its line
+ * search (α, :83-85), kept per trajectory instead of printed. Device
+ * arrays of max_iter × batch elements, iteration-major (element [(i−1)·batch + b] is
+ * iteration i of trajectory b), each may be NULL:
+ *   cost    the accepted rollout's cost (the printed Total Cost); NaN when the
+ *           trajectory did not run iteration i (it had stopped) or its search failed
+ *   trials  line-search trials of iteration i (0: did not run)
+ *   alpha   the accepted step α = alpha0·shrink^(trials−1) (NaN as for cost)
+ *   du2     Σ(ū − u)² of the iteration's last trial, the convergence test's quantity
+ *           (:171; NaN: did not run)
+ * Entries past a fit's last iteration (every trajectory stopped, or the poll broke
+ * the loop) are left as they were. */
+typedef struct {
+  double* cost;
+  int32_t* trials;
+  double* alpha;
+  double* du2;
+} ilqr_history;
+
+/* ilqr_fit plus the per-iteration record (history may be NULL: ilqr_fit). */
+ilqr_status ilqr_fit_ex(ilqr_handle* h, const ilqr_problem* p, const ilqr_options* o,
+                        const double* x_init, const double* u_init, const double* x_traj,
+                        double* x_out, double* u_out, double* cost, int32_t* iters,
+                        int32_t* status, const ilqr_history* history);
 
 /* ---------------------------------------------------------------------------
  * RBD problem family (ILQR_PROBLEM_CHAIN): a fixed-base serial chain of revolute
@@ -335,6 +375,12 @@ ilqr_status ilqr_chain_iterate(ilqr_chain_handle* h, const ilqr_options* o, cons
 ilqr_status ilqr_chain_fit(ilqr_chain_handle* h, const ilqr_options* o, const void* x_init,
                            const void* u_init, const void* x_traj, void* x_out, void* u_out,
                            void* cost, int32_t* iters, int32_t* status);
+/* ilqr_chain_fit plus the per-iteration record (ilqr_history, double arrays whatever
+ * the handle's dtype; NULL: ilqr_chain_fit). */
+ilqr_status ilqr_chain_fit_ex(ilqr_chain_handle* h, const ilqr_options* o, const void* x_init,
+                              const void* u_init, const void* x_traj, void* x_out, void* u_out,
+                              void* cost, int32_t* iters, int32_t* status,
+                              const ilqr_history* history);
 
 /* Multi-GPU fit in one process (what a single-process Julia host
  * uses): the batch is split into contiguous blocks over `devices` (block i holds

@@ -99,7 +99,7 @@ def test_julia_shim_ccalls_declared_symbols():
     include/ilqr.h declares and the library exports (the shim cannot run here)."""
     src = open(os.path.join(ROOT, "ilqr.jl_amd", "julia", "iLQRHIP.jl")).read()
     called = set(re.findall(r"ccall\(\(:(ilqr_[a-z0-9_]+),\s*libilqr\)", src))
-    assert {"ilqr_fit", "ilqr_backward", "ilqr_forward", "ilqr_backward_tiles",
+    assert {"ilqr_fit_ex", "ilqr_backward", "ilqr_forward", "ilqr_backward_tiles",
             "ilqr_chain_fit", "ilqr_chain_set_dynamics"} <= called, called
     declared = set(declared_functions())
     assert called <= declared, called - declared

@@ -110,7 +110,8 @@ def shim_forward(prob_fn, x, u, x_traj, du, K, prev_cost):
     return out
 
 
-def shim_fit(prob_fn, x_init, u_init, x_traj, max_iter, tol):
+def shim_fit(prob_fn, x_init, u_init, x_traj, max_iter, tol, with_history=False):
+    """iLQRHIP.fit: ilqr_fit_ex with the (cost, trials) history the verbose print reads."""
     N, nx = x_init.shape
     M, nu = u_init.shape
     h = Handle(nx, nu, M, 1)
@@ -118,9 +119,14 @@ def shim_fit(prob_fn, x_init, u_init, x_traj, max_iter, tol):
     o = _lib.default_options(max_iter=max_iter, tol=tol)
     xi, ui, xt = h.upload(J.to_abi(x_init)), h.upload(J.to_abi(u_init)), h.upload(J.to_abi(x_traj))
     xo, uo = h.alloc(np.float64, N * nx), h.alloc(np.float64, M * nu)
-    rc = h.lib.ilqr_fit(h.h, C.byref(p), C.byref(o), xi, ui, xt, xo, uo, None, None, None)
+    hc = h.alloc(np.float64, max_iter)
+    ht = h.upload(J.jl(np.zeros(max(max_iter, 1))), dtype=np.int32)
+    hist = _lib.History(hc.value, ht.value, None, None)
+    rc = h.lib.ilqr_fit_ex(h.h, C.byref(p), C.byref(o), xi, ui, xt, xo, uo, None, None, None, C.byref(hist))
     assert rc in (_lib.OK, _lib.ERR_LS_EXHAUSTED)
     out = J.from_abi(h.download((nx, N), xo)), J.from_abi(h.download((nu, M), uo))
+    if with_history:  # print_history's inputs: download!(h, zeros(max_iter), hc), … Int32 …
+        out = out + (h.download((max_iter,), hc), h.download((max(max_iter, 1),), ht, dtype=np.int32))
     h.close()
     return out
 
@@ -154,9 +160,13 @@ def test_shim_lq_forward_pass_with_x_traj(gpu, quad):
 def test_shim_lq_fit(gpu, quad):
     g = quad
     b = 1
-    x, u = shim_fit(lambda h: lq_problem(h, g["A"][b], g["B"][b], g["Q"][b], g["R"][b], g["Qf"][b]),
-                    g["x"][b], g["u"][b], g["xtraj"][b], 30, 1e-6)
+    x, u, hc, ht = shim_fit(lambda h: lq_problem(h, g["A"][b], g["B"][b], g["Q"][b], g["R"][b], g["Qf"][b]),
+                            g["x"][b], g["u"][b], g["xtraj"][b], 30, 1e-6, with_history=True)
     assert rel(x, g["fit_x"][b]) < 1e-8 and rel(u, g["fit_u"][b]) < 1e-8
+    # fit(...; verbose=true) prints one line per iteration with trials > 0: the oracle's costs
+    n = int(g["fit_iters"][b])
+    assert (ht[:n] > 0).all() and (ht[n:] == 0).all()
+    assert rel(hc[:n], g["fit_cost"][b, :n]) < 1e-9
 
 
 @pytest.mark.gpu
@@ -224,8 +234,18 @@ def test_shim_solve_batched(gpu):
     o = _lib.default_options(max_iter=30, tol=1e-6)
     xi, ui = h.upload(jx), h.upload(ju)
     xo, uo = h.alloc(np.float64, jx.size), h.alloc(np.float64, ju.size)
-    assert h.lib.ilqr_fit(h.h, C.byref(p), C.byref(o), xi, ui, None, xo, uo, None, None, None) == _lib.OK
+    n = 30  # solve!(prob; history=true): (max_iter, batch) row-major = Julia (batch, max_iter)
+    hd = (h.alloc(np.float64, n * nb), h.upload(J.jl(np.zeros(n * nb)), dtype=np.int32),
+          h.alloc(np.float64, n * nb), h.alloc(np.float64, n * nb))
+    hist = _lib.History(*(q.value for q in hd))
+    assert h.lib.ilqr_fit_ex(h.h, C.byref(p), C.byref(o), xi, ui, None, xo, uo, None, None, None,
+                             C.byref(hist)) == _lib.OK
     x, u = h.download(jx.shape, xo), h.download(ju.shape, uo)
+    cost = h.download((nb, n), hd[0])
+    trials = h.download((nb, n), hd[1], dtype=np.int32)
     h.close()
     for b in range(nb):
         assert rel(x[:, :, b].T, g["fit_x"][b]) < 1e-8 and rel(u[:, :, b].T, g["fit_u"][b]) < 1e-8
+        k = int(g["fit_iters"][b])
+        assert (trials[b, :k] > 0).all() and (trials[b, k:] == 0).all()
+        assert rel(cost[b, :k], g["fit_cost"][b, :k]) < 1e-9

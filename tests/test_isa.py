@@ -46,7 +46,12 @@ def _waterfalls(body):
         m = re.search(r"s_cbranch_execnz (\.LBB\w+)", l)
         if m and labels.get(m.group(1), 1 << 30) < k:
             seg = body[labels[m.group(1)]:k + 1]
-            if any("v_readfirstlane" in x for x in seg) and any(x.startswith(("buffer_", "global_")) for x in seg):
+            # the waterfall's signature: exec narrowed to the lanes matching the
+            # readfirstlane'd value, the access, then `s_xor_b64 exec, exec, …` and the
+            # branch back (a backward execnz branch of an ordinary if/else block layout
+            # has no exec-destination xor)
+            if (any("v_readfirstlane" in x for x in seg) and any(x.startswith(("buffer_", "global_")) for x in seg)
+                    and any(x.startswith("s_xor_b64 exec, exec") for x in seg)):
                 found.append(k)
     return found
 

@@ -19,6 +19,11 @@ case $WHAT in
   test) step pytest_gpu 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
         step smoke 180 python -c "import __graft_entry__ as g; g.smoke()" ;;
   bench) step bench 300 python bench.py ;;
+  hist) step pytest_hist 400 python -u -m pytest tests/test_gpu_history.py -m gpu -x -v --timeout 200 --timeout-method thread ;;
+  ab) step ab 200 python tools/ab_coop.py ;;
+  ls) step pytest_ls 400 python -u -m pytest tests/test_gpu_line_search.py -m gpu -x -v --timeout 200 --timeout-method thread ;;
+  cfg) step pytest_cfg 400 python -u -m pytest tests/test_gpu_configs.py -m gpu -x -v -s --timeout 200 --timeout-method thread ;;
+  smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
   prof) step rocprof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 50 --warmup 300 --no-cpu ;;
   ablate) step ablate 120 ./tools/ablate_bw ;;
   dist2) ILQR_DIST_BACKEND=gloo step dist2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 2 --steps 5 --warmup 1 --no-cpu ;;
