@@ -9,6 +9,7 @@
 
 #include <string>
 #include <thread>
+#include <utility>
 #include <vector>
 
 #include "../../include/ilqr.h"
@@ -22,6 +23,10 @@ struct Shard {
   double *A = nullptr, *B = nullptr, *Q = nullptr, *R = nullptr, *Qf = nullptr;
   double *x = nullptr, *u = nullptr, *xt = nullptr, *xo = nullptr, *uo = nullptr, *cost = nullptr;
   int32_t *iters = nullptr, *status = nullptr;
+  // fit history scratch (max_iter, nb) per shard, grown on demand (ilqr_multi_fit_resident)
+  double *hcost = nullptr, *halpha = nullptr, *hdu2 = nullptr;
+  int32_t* htrials = nullptr;
+  int hcap = 0;  // iterations the scratch holds
   hipStream_t stream = nullptr;
 };
 
@@ -30,6 +35,9 @@ struct Shard {
 struct ilqr_multi {
   int nx = 0, nu = 0, T = 0, batch = 0;
   std::vector<Shard> shards;
+  int32_t kind = 0;        // problem set by ilqr_multi_set_problem (0: none yet)
+  bool loaded = false;     // trajectories loaded (ilqr_multi_load) or left by a fit
+  bool have_result = false;
 };
 
 namespace {
@@ -48,56 +56,118 @@ int severity(ilqr_status s) {  // which status the call reports when shards diff
 void free_shard(Shard& s) {
   if (s.h) ilqr_destroy(s.h);
   (void)hipSetDevice(s.device);
-  for (double* p : {s.A, s.B, s.Q, s.R, s.Qf, s.x, s.u, s.xt, s.xo, s.uo, s.cost}) (void)hipFree(p);
+  for (double* p : {s.A, s.B, s.Q, s.R, s.Qf, s.x, s.u, s.xt, s.xo, s.uo, s.cost, s.hcost, s.halpha, s.hdu2})
+    (void)hipFree(p);
   (void)hipFree(s.iters);
   (void)hipFree(s.status);
+  (void)hipFree(s.htrials);
   if (s.stream) (void)hipStreamDestroy(s.stream);
   s = Shard{};
 }
 
-// one device's part of ilqr_multi_fit
-ilqr_status run_shard(const ilqr_multi* m, Shard& s, const ilqr_problem* p, const ilqr_options* o,
-                      const double* x_init, const double* u_init, const double* x_traj,
-                      double* x_out, double* u_out, double* cost, int32_t* iters, int32_t* status) {
+ilqr_status hip_status(hipError_t e) { return e == hipSuccess ? ILQR_OK : ILQR_ERR_HIP; }
+
+// the problem descriptor of a shard: its resident per-instance LQ data; the 2-link arm
+// has none
+ilqr_problem shard_problem(int32_t kind, const Shard& s) {
+  if (kind == ILQR_PROBLEM_LQ) return ilqr_problem{kind, 0, s.A, s.B, s.Q, s.R, s.Qf};
+  return ilqr_problem{kind, 0, nullptr, nullptr, nullptr, nullptr, nullptr};
+}
+
+// Per-device steps of the multi-device calls (each runs on the shard's thread, on the
+// shard's stream). Host arrays hold the whole batch; shard i's block starts at b0.
+ilqr_status shard_set_problem(const ilqr_multi* m, Shard& s, const ilqr_problem* p) {
   if (s.nb == 0) return ILQR_OK;
   if (hipSetDevice(s.device) != hipSuccess) return ILQR_ERR_HIP;
-  const int nx = m->nx, nu = m->nu, T = m->T;
+  const int nx = m->nx, nu = m->nu;
   const size_t b0 = (size_t)s.b0, nb = (size_t)s.nb;
-  const size_t xs = (size_t)(T + 1) * nx, us = (size_t)T * nu;
   auto h2d = [&](double* dst, const double* src, size_t per) {
     return hipMemcpyAsync(dst, src + b0 * per, sizeof(double) * nb * per, hipMemcpyHostToDevice, s.stream);
   };
   hipError_t e = hipSuccess;
-  ilqr_problem dp = *p;
   if (p->kind == ILQR_PROBLEM_LQ) {
     if (e == hipSuccess) e = h2d(s.A, p->A, (size_t)nx * nx);
     if (e == hipSuccess) e = h2d(s.B, p->B, (size_t)nx * nu);
     if (e == hipSuccess) e = h2d(s.Q, p->Q, (size_t)nx * nx);
     if (e == hipSuccess) e = h2d(s.R, p->R, (size_t)nu * nu);
     if (e == hipSuccess) e = h2d(s.Qf, p->Qf, (size_t)nx * nx);
-    dp.A = s.A;
-    dp.B = s.B;
-    dp.Q = s.Q;
-    dp.R = s.R;
-    dp.Qf = s.Qf;
   }
-  if (e == hipSuccess) e = h2d(s.x, x_init, xs);
-  if (e == hipSuccess) e = h2d(s.u, u_init, us);
+  if (e == hipSuccess) e = hipStreamSynchronize(s.stream);
+  return hip_status(e);
+}
+
+ilqr_status shard_load(const ilqr_multi* m, Shard& s, const double* x, const double* u, const double* x_traj) {
+  if (s.nb == 0) return ILQR_OK;
+  if (hipSetDevice(s.device) != hipSuccess) return ILQR_ERR_HIP;
+  const size_t b0 = (size_t)s.b0, nb = (size_t)s.nb;
+  const size_t xs = (size_t)(m->T + 1) * m->nx, us = (size_t)m->T * m->nu;
+  auto h2d = [&](double* dst, const double* src, size_t per) {
+    return hipMemcpyAsync(dst, src + b0 * per, sizeof(double) * nb * per, hipMemcpyHostToDevice, s.stream);
+  };
+  hipError_t e = hipSuccess;
+  if (x) e = h2d(s.x, x, xs);
+  if (e == hipSuccess && u) e = h2d(s.u, u, us);
   if (e == hipSuccess && x_traj) e = h2d(s.xt, x_traj, xs);
-  if (e != hipSuccess) return ILQR_ERR_HIP;
-  const ilqr_status st = ilqr_fit(s.h, &dp, o, s.x, s.u, x_traj ? s.xt : nullptr, s.xo, s.uo, s.cost,
-                                  s.iters, s.status);
-  if (st != ILQR_OK && st != ILQR_ERR_NAN && st != ILQR_ERR_LS_EXHAUSTED) return st;
+  if (e == hipSuccess) e = hipStreamSynchronize(s.stream);
+  return hip_status(e);
+}
+
+// fit from the shard's resident (x, u) into its resident results (xo, uo, cost, …)
+ilqr_status shard_fit(const ilqr_multi* m, Shard& s, const ilqr_options* o, bool use_x_traj,
+                      const ilqr_history* hist) {
+  if (s.nb == 0) return ILQR_OK;
+  if (hipSetDevice(s.device) != hipSuccess) return ILQR_ERR_HIP;
+  const ilqr_problem dp = shard_problem(m->kind, s);
+  // the history's shard block: its columns b0 .. b0+nb of each (max_iter, batch) array,
+  // written through a per-shard (max_iter, nb) device scratch and copied out below
+  ilqr_history sh{};
+  if (hist) sh = ilqr_history{hist->cost ? s.hcost : nullptr, hist->trials ? s.htrials : nullptr,
+                              hist->alpha ? s.halpha : nullptr, hist->du2 ? s.hdu2 : nullptr};
+  const ilqr_status st = ilqr_fit_ex(s.h, &dp, o, s.x, s.u, use_x_traj ? s.xt : nullptr, s.xo, s.uo, s.cost,
+                                     s.iters, s.status, hist ? &sh : nullptr);
+  (void)m;
+  return st;
+}
+
+ilqr_status shard_gather(const ilqr_multi* m, Shard& s, double* x_out, double* u_out, double* cost,
+                         int32_t* iters, int32_t* status) {
+  if (s.nb == 0) return ILQR_OK;
+  if (hipSetDevice(s.device) != hipSuccess) return ILQR_ERR_HIP;
+  const size_t b0 = (size_t)s.b0, nb = (size_t)s.nb;
+  const size_t xs = (size_t)(m->T + 1) * m->nx, us = (size_t)m->T * m->nu;
   auto d2h = [&](void* dst, const void* src, size_t bytes) {
     return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s.stream);
   };
-  if (e == hipSuccess) e = d2h(x_out + b0 * xs, s.xo, sizeof(double) * nb * xs);
-  if (e == hipSuccess) e = d2h(u_out + b0 * us, s.uo, sizeof(double) * nb * us);
+  hipError_t e = hipSuccess;
+  if (x_out) e = d2h(x_out + b0 * xs, s.xo, sizeof(double) * nb * xs);
+  if (e == hipSuccess && u_out) e = d2h(u_out + b0 * us, s.uo, sizeof(double) * nb * us);
   if (e == hipSuccess && cost) e = d2h(cost + b0, s.cost, sizeof(double) * nb);
   if (e == hipSuccess && iters) e = d2h(iters + b0, s.iters, sizeof(int32_t) * nb);
   if (e == hipSuccess && status) e = d2h(status + b0, s.status, sizeof(int32_t) * nb);
   if (e == hipSuccess) e = hipStreamSynchronize(s.stream);
-  return e == hipSuccess ? st : ILQR_ERR_HIP;
+  return hip_status(e);
+}
+
+// run fn(shard) on one host thread per shard; the most severe status
+template <class F>
+ilqr_status each_shard(ilqr_multi* m, F fn) {
+  const int n = (int)m->shards.size();
+  std::vector<ilqr_status> res(n, ILQR_OK);
+  std::vector<std::thread> th;
+  th.reserve(n);
+  for (int i = 0; i < n; ++i) th.emplace_back([&, i] { res[i] = fn(m->shards[i]); });
+  for (auto& t : th) t.join();
+  ilqr_status worst = ILQR_OK;
+  for (ilqr_status s : res)
+    if (severity(s) > severity(worst)) worst = s;
+  return worst;
+}
+
+ilqr_status check_problem(const ilqr_multi* m, const ilqr_problem* p) {
+  if (!p) return ILQR_ERR_BAD_ARG;
+  if (p->kind == ILQR_PROBLEM_LQ && (!p->A || !p->B || !p->Q || !p->R || !p->Qf)) return ILQR_ERR_BAD_ARG;
+  if (!ilqr_supported(p->kind, m->nx, m->nu)) return ILQR_ERR_UNSUPPORTED;
+  return ILQR_OK;
 }
 
 }  // namespace
@@ -171,28 +241,115 @@ ilqr_status ilqr_multi_set_schedule(ilqr_multi* m, int flags) {
   return ILQR_OK;
 }
 
+ilqr_status ilqr_multi_set_problem(ilqr_multi* m, const ilqr_problem* host_problem) {
+  if (!m) return ILQR_ERR_BAD_ARG;
+  ilqr_status st = check_problem(m, host_problem);
+  if (st != ILQR_OK) return st;
+  st = each_shard(m, [&](Shard& s) { return shard_set_problem(m, s, host_problem); });
+  m->kind = st == ILQR_OK ? host_problem->kind : 0;
+  return st;
+}
+
+ilqr_status ilqr_multi_load(ilqr_multi* m, const double* x, const double* u, const double* x_traj) {
+  if (!m || (!x && !u && !x_traj) || (!m->loaded && (!x || !u))) return ILQR_ERR_BAD_ARG;
+  const ilqr_status st = each_shard(m, [&](Shard& s) { return shard_load(m, s, x, u, x_traj); });
+  if (st == ILQR_OK) m->loaded = true;
+  return st;
+}
+
+ilqr_status ilqr_multi_fit_resident(ilqr_multi* m, const ilqr_options* o, int flags,
+                                    const ilqr_history* history) {
+  if (!m || !m->kind || (flags & ~(ILQR_MULTI_WARM_START | ILQR_MULTI_USE_X_TRAJ)) != 0) return ILQR_ERR_BAD_ARG;
+  if ((flags & ILQR_MULTI_WARM_START) ? !m->have_result : !m->loaded) return ILQR_ERR_BAD_ARG;
+  const ilqr_history* hist = history;
+  if (hist && !hist->cost && !hist->trials && !hist->alpha && !hist->du2) hist = nullptr;
+  ilqr_options def;
+  ilqr_default_options(&def);
+  const int max_iter = (o ? o : &def)->max_iter;
+  if (hist && max_iter > 0) {  // per-shard history scratch, allocated on first use
+    for (Shard& s : m->shards) {
+      if (s.nb == 0 || s.hcap >= max_iter) continue;
+      if (hipSetDevice(s.device) != hipSuccess) return ILQR_ERR_HIP;
+      for (double* q : {s.hcost, s.halpha, s.hdu2}) (void)hipFree(q);
+      (void)hipFree(s.htrials);
+      s.hcost = s.halpha = s.hdu2 = nullptr;
+      s.htrials = nullptr;
+      s.hcap = 0;
+      const size_t n = (size_t)max_iter * s.nb;
+      hipError_t e = hipMalloc(&s.hcost, sizeof(double) * n);
+      if (e == hipSuccess) e = hipMalloc(&s.halpha, sizeof(double) * n);
+      if (e == hipSuccess) e = hipMalloc(&s.hdu2, sizeof(double) * n);
+      if (e == hipSuccess) e = hipMalloc(&s.htrials, sizeof(int32_t) * n);
+      if (e != hipSuccess) return ILQR_ERR_HIP;
+      s.hcap = max_iter;
+    }
+  }
+  const ilqr_status st = each_shard(m, [&](Shard& s) -> ilqr_status {
+    if ((flags & ILQR_MULTI_WARM_START) && s.nb) {  // the previous result is the new start
+      std::swap(s.x, s.xo);
+      std::swap(s.u, s.uo);
+    }
+    ilqr_status r = shard_fit(m, s, o, (flags & ILQR_MULTI_USE_X_TRAJ) != 0, hist);
+    if ((r == ILQR_OK || r == ILQR_ERR_NAN || r == ILQR_ERR_LS_EXHAUSTED) && hist && s.nb && max_iter > 0) {
+      // the shard's (max_iter, nb) record into columns b0 .. b0+nb of the caller's
+      // (max_iter, batch) arrays (device memory of any device: peer copies)
+      auto cp = [&](void* dst, const void* src, size_t w) {
+        return hipMemcpy2DAsync((char*)dst + w * s.b0, w * m->batch, src, w * s.nb, w * s.nb, max_iter,
+                                hipMemcpyDefault, s.stream);
+      };
+      hipError_t e = hipSuccess;
+      if (hist->cost) e = cp(hist->cost, s.hcost, sizeof(double));
+      if (e == hipSuccess && hist->trials) e = cp(hist->trials, s.htrials, sizeof(int32_t));
+      if (e == hipSuccess && hist->alpha) e = cp(hist->alpha, s.halpha, sizeof(double));
+      if (e == hipSuccess && hist->du2) e = cp(hist->du2, s.hdu2, sizeof(double));
+      if (e == hipSuccess) e = hipStreamSynchronize(s.stream);
+      if (e != hipSuccess) r = ILQR_ERR_HIP;
+    }
+    return r;
+  });
+  m->have_result = severity(st) <= severity(ILQR_ERR_NAN);
+  return st;
+}
+
+ilqr_status ilqr_multi_gather(ilqr_multi* m, double* x_out, double* u_out, double* cost, int32_t* iters,
+                              int32_t* status) {
+  if (!m || !m->have_result) return ILQR_ERR_BAD_ARG;
+  return each_shard(m, [&](Shard& s) { return shard_gather(m, s, x_out, u_out, cost, iters, status); });
+}
+
 ilqr_status ilqr_multi_fit(ilqr_multi* m, const ilqr_problem* p, const ilqr_options* o,
                            const double* x_init, const double* u_init, const double* x_traj,
                            double* x_out, double* u_out, double* cost, int32_t* iters,
                            int32_t* status) {
   if (!m || !p || !x_init || !u_init || !x_out || !u_out) return ILQR_ERR_BAD_ARG;
-  if (p->kind == ILQR_PROBLEM_LQ && (!p->A || !p->B || !p->Q || !p->R || !p->Qf)) return ILQR_ERR_BAD_ARG;
-  if (!ilqr_supported(p->kind, m->nx, m->nu)) return ILQR_ERR_UNSUPPORTED;
-  const int n = (int)m->shards.size();
-  std::vector<ilqr_status> res(n, ILQR_OK);
-  std::vector<std::thread> th;
-  th.reserve(n);
-  for (int i = 0; i < n; ++i)
-    th.emplace_back([&, i] {
-      res[i] = run_shard(m, m->shards[i], p, o, x_init, u_init, x_traj, x_out, u_out, cost, iters, status);
-    });
-  for (auto& t : th) t.join();
-  ilqr_status worst = ILQR_OK;
-  for (ilqr_status s : res)
-    if (severity(s) > severity(worst)) worst = s;
-  return worst;
+  ilqr_status st = check_problem(m, p);
+  if (st != ILQR_OK) return st;
+  // host in, host out: every call moves the problem and the trajectories both ways
+  // (the device-resident calls above keep them on the devices)
+  st = each_shard(m, [&](Shard& s) -> ilqr_status {
+    ilqr_status r = shard_set_problem(m, s, p);
+    if (r == ILQR_OK) r = shard_load(m, s, x_init, u_init, x_traj);
+    if (r != ILQR_OK) return r;
+    const ilqr_problem dp = shard_problem(p->kind, s);
+    if (s.nb == 0) return ILQR_OK;
+    r = ilqr_fit(s.h, &dp, o, s.x, s.u, x_traj ? s.xt : nullptr, s.xo, s.uo, s.cost, s.iters, s.status);
+    if (r != ILQR_OK && r != ILQR_ERR_NAN && r != ILQR_ERR_LS_EXHAUSTED) return r;
+    const ilqr_status g = shard_gather(m, s, x_out, u_out, cost, iters, status);
+    return g != ILQR_OK ? g : r;
+  });
+  m->kind = severity(st) <= severity(ILQR_ERR_NAN) ? p->kind : 0;
+  m->loaded = m->have_result = m->kind != 0;
+  return st;
 }
 
 int ilqr_multi_devices(const ilqr_multi* m) { return m ? (int)m->shards.size() : 0; }
+
+ilqr_status ilqr_host_alloc(size_t bytes, void** ptr) {
+  if (!ptr) return ILQR_ERR_BAD_ARG;
+  *ptr = nullptr;
+  return hip_status(hipHostMalloc(ptr, bytes > 0 ? bytes : 1, hipHostMallocDefault));
+}
+
+ilqr_status ilqr_host_free(void* ptr) { return ptr ? hip_status(hipHostFree(ptr)) : ILQR_OK; }
 
 }  // extern "C"

@@ -36,6 +36,8 @@ SCHED_BACKWARD_BLOCK = 8
 SCHED_FUSED = 16
 SCHED_FORWARD_MFMA = 32
 SCHED_SEQUENTIAL_SEARCH = 64
+MULTI_WARM_START = 1
+MULTI_USE_X_TRAJ = 2
 
 PROBLEM_LQ = 1
 PROBLEM_TWO_LINK = 2
@@ -106,6 +108,12 @@ SIGNATURES = {
     "ilqr_multi_set_schedule": (C.c_int, [P, C.c_int]),
     "ilqr_multi_devices": (C.c_int, [P]),
     "ilqr_multi_fit": (C.c_int, [P, C.POINTER(Problem), C.POINTER(Options), P, P, P, P, P, P, P, P]),
+    "ilqr_multi_set_problem": (C.c_int, [P, C.POINTER(Problem)]),
+    "ilqr_multi_load": (C.c_int, [P, P, P, P]),
+    "ilqr_multi_fit_resident": (C.c_int, [P, C.POINTER(Options), C.c_int, C.POINTER(History)]),
+    "ilqr_multi_gather": (C.c_int, [P, P, P, P, P, P]),
+    "ilqr_host_alloc": (C.c_int, [C.c_size_t, C.POINTER(P)]),
+    "ilqr_host_free": (C.c_int, [P]),
     "ilqr_backward": (C.c_int, [P, C.POINTER(Problem), C.POINTER(Options), P, P, P, P, P]),
     "ilqr_backward_tiles": (C.c_int, [P, C.POINTER(Tiles), C.POINTER(Options), P, P, P]),
     "ilqr_forward": (C.c_int, [P, C.POINTER(Problem), C.POINTER(Options), P, P, P, P, P, P,

@@ -1,9 +1,11 @@
 """Single-process multi-GPU fit (ilqr_multi_* in include/ilqr.h):
 the batch is sharded in contiguous blocks over the given devices, each shard runs
 ilqr_fit concurrently on its own device (one host thread per device inside the
-library). Host numpy in, host numpy out — what a single-process host (the Julia
-shim's fit_multi) hands over. The one-process-per-GPU path with torch.distributed
-is ilqr_amd.dist."""
+library). `fit`: host numpy in, host numpy out — what a single-process host (the Julia
+shim's solve!) hands over, every array crossing PCIe on every call. The resident calls
+(`set_problem`, `load`, `fit_resident`, `gather`) keep problem and trajectories on the
+devices between calls (an MPC loop). The one-process-per-GPU path with
+torch.distributed is ilqr_amd.dist."""
 from __future__ import annotations
 
 import ctypes as C
@@ -75,3 +77,70 @@ class MultiSolver:
                                      _ptr(xt), _ptr(xo), _ptr(uo), _ptr(cost), _ptr(iters), _ptr(st))
         _lib.check(rc, "ilqr_multi_fit", allow=(_lib.ERR_NAN, _lib.ERR_LS_EXHAUSTED))
         return xo, uo, cost, iters, st, rc
+
+    # -- device-resident calls -------------------------------------------------------
+    def set_problem(self, lq: LQBatch = None, kind: int = _lib.PROBLEM_LQ):
+        """Upload the per-instance problem once (ilqr_multi_set_problem)."""
+        if kind == _lib.PROBLEM_LQ:
+            self._arrs = {k: _host(getattr(lq, k)) for k in ("A", "B", "Q", "R", "Qf")}
+            prob = _lib.Problem(kind, 0, *(self._arrs[k].ctypes.data for k in ("A", "B", "Q", "R", "Qf")))
+        else:
+            prob = _lib.Problem(kind, 0, None, None, None, None, None)
+        _lib.check(self.lib.ilqr_multi_set_problem(self.h, C.byref(prob)), "ilqr_multi_set_problem")
+
+    def load(self, x=None, u=None, x_traj=None):
+        """Upload trajectories (host numpy; None keeps what the devices hold)."""
+        B, T, nx, nu = self.batch, self.T, self.nx, self.nu
+        a = [None if v is None else _host(v) for v in (x, u, x_traj)]
+        for v, shp in zip(a, ((B, T + 1, nx), (B, T, nu), (B, T + 1, nx))):
+            if v is not None and v.shape != shp:
+                raise AssertionError(f"expected {shp}, got {v.shape}")
+        _lib.check(self.lib.ilqr_multi_load(self.h, *(_ptr(v) for v in a)), "ilqr_multi_load")
+
+    def fit_resident(self, max_iter=100, tol=1e-6, warm_start=False, use_x_traj=False, history=None):
+        """Fit from the resident trajectories (or the previous result) into resident
+        results; nothing crosses PCIe. history: a solver.alloc_history struct (device
+        arrays (max_iter, batch)) or None. → call status."""
+        if not isinstance(max_iter, int):
+            raise TypeError("max_iter::Int64")
+        o = _lib.default_options(max_iter=max_iter, tol=float(tol))
+        flags = (_lib.MULTI_WARM_START if warm_start else 0) | (_lib.MULTI_USE_X_TRAJ if use_x_traj else 0)
+        rc = self.lib.ilqr_multi_fit_resident(self.h, C.byref(o), flags,
+                                              C.byref(history) if history is not None else None)
+        return _lib.check(rc, "ilqr_multi_fit_resident", allow=(_lib.ERR_NAN, _lib.ERR_LS_EXHAUSTED))
+
+    def gather(self, x=True, u=True, cost=True, iters=True, status=True, out=None):
+        """Copy the last fit's results to host (only the fields asked for). `out`: a dict
+        of preallocated (pinned, see HostBuffers) arrays to fill instead of new ones."""
+        B, T, nx, nu = self.batch, self.T, self.nx, self.nu
+        shapes = {"x": ((B, T + 1, nx), np.float64), "u": ((B, T, nu), np.float64), "cost": ((B,), np.float64),
+                  "iters": ((B,), np.int32), "status": ((B,), np.int32)}
+        want = {"x": x, "u": u, "cost": cost, "iters": iters, "status": status}
+        res = {}
+        for k, (shp, dt) in shapes.items():
+            if want[k]:
+                res[k] = out[k] if out is not None and k in out else np.empty(shp, dtype=dt)
+        _lib.check(self.lib.ilqr_multi_gather(self.h, *(_ptr(res.get(k)) for k in shapes)), "ilqr_multi_gather")
+        return res
+
+
+class HostBuffers:
+    """Pinned host arrays (ilqr_host_alloc) for MultiSolver.gather / load: PCIe at
+    full rate instead of the driver's pageable staging."""
+
+    def __init__(self, **shapes):
+        self.lib = _lib.load()
+        self._ptrs, self.arrays = [], {}
+        for k, (shape, dtype) in shapes.items():
+            n = int(np.prod(shape)) * np.dtype(dtype).itemsize
+            p = C.c_void_p()
+            _lib.check(self.lib.ilqr_host_alloc(n, C.byref(p)), "ilqr_host_alloc")
+            self._ptrs.append(p)
+            buf = (C.c_char * n).from_address(p.value)
+            self.arrays[k] = np.frombuffer(buf, dtype=dtype).reshape(shape)
+
+    def close(self):
+        self.arrays = {}
+        for p in self._ptrs:
+            self.lib.ilqr_host_free(p)
+        self._ptrs = []

@@ -401,6 +401,35 @@ ilqr_status ilqr_multi_fit(ilqr_multi* m, const ilqr_problem* host_problem, cons
                            double* x_out, double* u_out, double* cost, int32_t* iters,
                            int32_t* status);
 
+/* Device-resident multi-device solving (an MPC loop over many instances): the problem
+ * and the trajectories stay on their devices between calls; only what the caller asks
+ * for crosses PCIe.
+ *   ilqr_multi_set_problem  upload the per-instance problem (host arrays, whole batch)
+ *                           once; ILQR_PROBLEM_LQ / ILQR_PROBLEM_TWO_LINK;
+ *   ilqr_multi_load         upload x (batch, T+1, nx), u (batch, T, nu) and/or x_traj
+ *                           (host; NULL keeps what the devices hold; x and u are both
+ *                           required the first time);
+ *   ilqr_multi_fit_resident fit every shard from the resident (x, u) — or, with
+ *                           ILQR_MULTI_WARM_START, from the previous fit's result —
+ *                           into resident results; ILQR_MULTI_USE_X_TRAJ uses the loaded
+ *                           x_traj. history (may be NULL): ilqr_history of the whole
+ *                           batch, device arrays (max_iter, batch) on any device. Same
+ *                           status rules as ilqr_multi_fit;
+ *   ilqr_multi_gather       copy the last fit's results to host arrays (each may be
+ *                           NULL: only what is asked for moves; pinned host memory,
+ *                           e.g. from ilqr_host_alloc, moves at full PCIe rate). */
+#define ILQR_MULTI_WARM_START 1
+#define ILQR_MULTI_USE_X_TRAJ 2
+ilqr_status ilqr_multi_set_problem(ilqr_multi* m, const ilqr_problem* host_problem);
+ilqr_status ilqr_multi_load(ilqr_multi* m, const double* x, const double* u, const double* x_traj);
+ilqr_status ilqr_multi_fit_resident(ilqr_multi* m, const ilqr_options* o, int flags,
+                                    const ilqr_history* history);
+ilqr_status ilqr_multi_gather(ilqr_multi* m, double* x_out, double* u_out, double* cost, int32_t* iters,
+                              int32_t* status);
+/* Pinned (page-locked) host memory for the multi-device transfers. */
+ilqr_status ilqr_host_alloc(size_t bytes, void** ptr);
+ilqr_status ilqr_host_free(void* ptr);
+
 /* Device memory helpers so a host-language shim (Julia ccall) needs no GPU package. */
 ilqr_status ilqr_malloc(ilqr_handle* h, size_t bytes, void** ptr);
 ilqr_status ilqr_free(ilqr_handle* h, void* ptr);

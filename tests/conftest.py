@@ -16,7 +16,7 @@ def pytest_configure(config):
 # GPU modules in the order they run: the BASELINE configs and the headline first, so
 # that `-m gpu -x` stopping on a family's unit test cannot hide them; then the LQ
 # parity suite, the 2-link family, tiles, layouts, and the chain family last.
-_ORDER = ("test_gpu_configs", "test_gpu_headline", "test_gpu_line_search", "test_gpu_history", "test_gpu_parity", "test_gpu_twolink",
+_ORDER = ("test_gpu_configs", "test_gpu_headline", "test_gpu_line_search", "test_gpu_history", "test_gpu_multi", "test_gpu_parity", "test_gpu_twolink",
           "test_gpu_tiles", "test_gpu_julia_layout", "test_gpu_cost_functions", "test_gpu_chain")
 
 

@@ -21,6 +21,8 @@ case $WHAT in
   bench) step bench 300 python bench.py ;;
   hist) step pytest_hist 400 python -u -m pytest tests/test_gpu_history.py -m gpu -x -v --timeout 200 --timeout-method thread ;;
   ab) step ab 200 python tools/ab_coop.py ;;
+  multi) step pytest_multi 400 python -u -m pytest tests/test_gpu_multi.py -m gpu -x -v --timeout 200 --timeout-method thread
+         step bench_multi 300 python tools/bench_multi.py ;;
   ls) step pytest_ls 400 python -u -m pytest tests/test_gpu_line_search.py -m gpu -x -v --timeout 200 --timeout-method thread ;;
   cfg) step pytest_cfg 400 python -u -m pytest tests/test_gpu_configs.py -m gpu -x -v -s --timeout 200 --timeout-method thread ;;
   smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
