@@ -1,0 +1,17 @@
+#!/bin/bash
+# Host sanitizer runs on a GPU box (prebuilt here by tools/san/run_cpu.sh; device code is
+# not instrumented): the ABI driver's GPU paths — fit_ex with history, iterate, the
+# multi-device host path and resident calls with their per-shard host threads — under
+# ASan+UBSan and under TSan. Each step under its own time limit; stops on a crash-class
+# exit. Logs into gpurun_out/.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+mkdir -p gpurun_out
+run() {  # run <name> <cmd...>
+  timeout -k 10 240 "$@" > "gpurun_out/$1.log" 2>&1
+  local rc=$?
+  echo "== $1 rc=$rc"; tail -3 "gpurun_out/$1.log"
+  return $rc
+}
+# the HIP runtime is not instrumented: its allocations are not leaks of ours
+ASAN_OPTIONS=detect_leaks=0 run san_address ./ilqr.jl_amd/lib/san_address/abi_driver &&
+TSAN_OPTIONS="suppressions=tools/san/tsan.supp" run san_thread ./ilqr.jl_amd/lib/san_thread/abi_driver
