@@ -946,42 +946,52 @@ __device__ __forceinline__ void coop_publish(const LSCoop& c, uint32_t gen, int 
 // written yet (its publisher is mid-way: the slot still holds another launch's entry).
 __device__ __attribute__((unused)) int coop_find(const LSCoop& c, uint32_t gen, int n, int max_trials,
                                                  int start, bool& unwritten) {
+  // The shared words are read at the coherence point (≈1 µs a round trip): each lane
+  // takes CH entries of a batch of 64·CH, their list words in one round trip and their
+  // records in a second, instead of two round trips per 64 entries.
+  constexpr int CH = 8;
   const int l = threadIdx.x & 63;
-  int best_b = -1, best_next = 0x7fffffff;
-  for (int base = 0; base < n; base += 64) {
-    int i = start + base + l;
-    i = i >= n ? i - n : i;
-    i = i >= n ? i - n : i;
-    int key = 0x7fffffff, bb = -1;
-    bool unw = false;
-    if (base + l < n) {
-      const uint64_t e = __hip_atomic_load(c.list + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if ((uint32_t)(e >> 32) != gen) {
-        unw = true;
-      } else {
-        bb = (int)(uint32_t)e;
-        const LSCoopRec* R = c.rec + bb;
-        const int nx = ag_ld(&R->next);
-        if (nx <= coop_lim_hint(R, max_trials)) key = nx;
-      }
+  uint64_t best = ~0ull;  // (next << 32) | position from `start`: smallest next, then earliest
+  for (int base = 0; base < n; base += 64 * CH) {
+    uint64_t e[CH];
+#pragma unroll
+    for (int k = 0; k < CH; ++k) {
+      const int pos = base + 64 * k + l;
+      int i = start + pos;
+      i = i >= n ? i - n : i;
+      e[k] = pos < n ? __hip_atomic_load(c.list + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                     : ((uint64_t)gen << 32) | 0xFFFFFFFFull;  // past the list: no entry
     }
-    if (__any(unw)) unwritten = true;
-    int m = key;
+    int nx[CH], lim[CH];
+#pragma unroll
+    for (int k = 0; k < CH; ++k) {
+      const uint32_t bb = (uint32_t)e[k];
+      const bool ok = (uint32_t)(e[k] >> 32) == gen && bb != 0xFFFFFFFFu;
+      const LSCoopRec* R = c.rec + (ok ? bb : 0);
+      nx[k] = ok ? ag_ld(&R->next) : 0x7fffffff;
+      lim[k] = ok ? coop_lim_hint(R, max_trials) : 0;
+      if ((uint32_t)(e[k] >> 32) != gen) unwritten = true;  // reserved, not yet written
+    }
+#pragma unroll
+    for (int k = 0; k < CH; ++k) {
+      const uint64_t key = ((uint64_t)(uint32_t)nx[k] << 32) | (uint32_t)(base + 64 * k + l);
+      if (nx[k] <= lim[k] && key < best) best = key;
+    }
+    // wave minimum
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) {
-      const int q = __shfl_xor(m, o);
-      m = q < m ? q : m;
+      const uint64_t q = __shfl_xor(best, o);
+      best = q < best ? q : best;
     }
-    m = __builtin_amdgcn_readfirstlane(m);
-    if (m < best_next) {
-      const uint64_t lanes = __ballot(key == m);
-      const int k = __builtin_ctzll(lanes);
-      best_next = m;
-      best_b = __builtin_amdgcn_readlane(bb, k);
-      if (m <= 2) break;  // nothing is fresher than an untouched trajectory
-    }
+    if ((best >> 32) <= 2) break;  // nothing is fresher than an untouched trajectory
   }
-  return best_b;
+  unwritten = __any(unwritten);
+  if (best == ~0ull) return -1;
+  const uint32_t pos = __builtin_amdgcn_readfirstlane((uint32_t)best);
+  int i = start + (int)pos;
+  i = i >= n ? i - n : i;
+  const uint64_t e = __hip_atomic_load(c.list + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return __builtin_amdgcn_readfirstlane((int)(uint32_t)e);
 }
 
 // Trajectory b's outcome, once trials 1..lim are evaluated (whole wave).
