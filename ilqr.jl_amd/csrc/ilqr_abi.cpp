@@ -35,7 +35,7 @@ struct ilqr_handle {
   // [2] = fit's call-status flags (gather_kernel: bit 0 NaN, bit 1 exhausted line search)
   int32_t* host_running = nullptr;
   int32_t* dev_running = nullptr;  // device alias of host_running
-  int32_t* dev_flags = nullptr;    // gather_kernel's device call-status word + block ticket
+  int32_t* dev_flags = nullptr;    // gather_kernel's device call-status word
   hipEvent_t ev_poll[2] = {nullptr, nullptr};
   // LQ problems of another shape (nx ≤ 12, nu ≤ 4) run zero-padded on an inner
   // (12, 4) handle (created on the first such call): zero rows/columns of A, B, Q, R,

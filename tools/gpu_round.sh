@@ -42,6 +42,8 @@ case $WHAT in
   rbdbench) step bench_rbd 300 python tools/bench_rbd.py ;;
   rbdprof) step rocprof_rbd 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_rbd -o run --output-format csv -- python tools/bench_rbd.py --steps 20 --warmup 5 --no-cpu ;;
   rcp) step rcp 60 ./tools/rcp_test ;;
+  fit5) step tail_probe 200 python tools/tail_probe.py
+        step rocprof_fit5 200 rocprofv3 --kernel-trace -d gpurun_out/prof_fit5 -o run --output-format csv -- python tools/fit5_trace.py ;;
   ubench) step ubench 120 ./tools/ubench_f64 ;;
 esac
 done
