@@ -45,25 +45,17 @@
 namespace ilqr {
 namespace {
 
-#ifndef ILQR_BW4_MFMA_T
-#define ILQR_BW4_MFMA_T 1
-#endif
-// μ folded into H's MFMA accumulator (R + Rᵀ + μI): no per-step pivot adds (backward
-// 103.8 -> 102.7 us, tools/bw_alt.sh; 0 = the add in the factorisation)
-#ifndef ILQR_BW4_MU_IN_H
-#define ILQR_BW4_MU_IN_H 1
-#endif
-// the lower S blocks as MFMA transposes of the upper ones (mf4(a, I, 0) = aᵀ, exact)
-// instead of ds_bpermute lane permutations (0: the permutes)
-#ifndef ILQR_BW4_SLOW_MFMA
-#define ILQR_BW4_SLOW_MFMA 1
-#endif
-// the solve's per-lane operands (M[ρ][κ], D⁻¹[ρ]) by 0/1-mask FMAs instead of select
-// chains: every VALU instruction beside the MFMAs costs the wave ≈6 cycles of issue,
-// b32 selects as much as f64 FMAs (tools/ubench_mix.hip; 0: the selects)
-#ifndef ILQR_BW4_SEL_FMA
-#define ILQR_BW4_SEL_FMA 1
-#endif
+// Measured choices of the step (the alternates they replaced, and the probe bits of
+// tools/bw4_probe.hip, live in tools/ablation/restore_alternates.patch):
+//  * μ folded into H's MFMA accumulator (R + Rᵀ + μI): no per-step pivot adds
+//    (backward 103.8 -> 102.7 us; the alternate added it in the factorisation);
+//  * the lower S blocks, the solve's Mᵀ and the diagonal symmetrisation as MFMA
+//    transposes (mf4(a, I, 0) = aᵀ, exact) instead of ds_bpermute lane permutations;
+//  * the solve's per-lane operands (M[ρ][κ], D⁻¹[ρ]) by 0/1-mask FMAs instead of select
+//    chains: every VALU instruction beside the MFMAs costs the wave ≈6 cycles of issue,
+//    b32 selects as much as f64 FMAs (tools/ubench_mix.hip);
+//  * L z for four steps per MFMA set, its columns moved by lane permutations (one per
+//    step, behind the S·F products) rather than one MFMA set per step or an LDS pass.
 
 constexpr int BW4_SLOTS = 4;          // trajectories per wave
 constexpr int BW4_WAVES = 4;          // waves per workgroup
@@ -94,23 +86,15 @@ __device__ __forceinline__ double mf4n(double a, double b, double c) {
 __device__ __forceinline__ double buf_ld(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
   return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0));
 }
-template <int AUX = 0>
 __device__ __forceinline__ void buf_st(double v, __amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
-  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, v), r, voff, soff, AUX);
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, v), r, voff, soff, 0);
 }
 
-// ABL: bits for tools/bw4_probe.hip only (0 in the product). Ablations (wrong
-// gains): 1 no factorisation, 2 no transposes, 4 no gradient, 8 no gain stores,
-// 64 no z loads, 128 no diagonal-block symmetrisation. Variants (correct gains): 16 the explicit (H + μI)⁻¹ instead of
-// the two triangular sweeps, 32 L z per step instead of four steps per MFMA, 256
-// the L z columns through LDS instead of lane permutations.
-//
 // Backward pass of trajectories b0 .. b0+3 (slots with active bit clear, or past B,
 // compute on clamped data and store nothing). Returns the slots whose gains hold a
 // NaN (bit β): the reference's @assert !any(isnan, ...) (:353-354). A NaN in any K_t
 // or d_t reaches K_0 or d_0 (S and s carry it down the recursion; no step compares,
 // selects or clamps), so the test reads the last step's gains only.
-template <int ABL = 0>
 __device__ unsigned lq_backward4_wave(const LQParams& P, int b0, int B, unsigned active, int T,
                                       const double* __restrict__ x, const double* __restrict__ u,
                                       double* __restrict__ d_out, double* __restrict__ K_out,
@@ -144,19 +128,17 @@ __device__ unsigned lq_backward4_wave(const LQParams& P, int b0, int B, unsigned
     for (int I = 0; I < 3; ++I) L[K][I] = Qb[r * NX + 4 * I + kap] + Qb[(4 * I + kap) * NX + r];
   }
   const double LR = Rb[rho * NU + kap] + Rb[kap * NU + rho];
-  [[maybe_unused]] const double LRmu = rho == kap ? LR + mu : LR;  // R + Rᵀ + μI
+  const double LRmu = rho == kap ? LR + mu : LR;  // R + Rᵀ + μI
 
-  // the lane permutation ρ ↔ κ (block transpose within each slot)
-  const int tr_src = (16 * kap + 4 * beta + rho) * 4;
-  // ... and the same transpose on the MFMA: mf4(a, I, 0) = aᵀ, exact (products with 1
-  // and 0); mf4(a, I/2, a/2) = (a + aᵀ)/2 with one rounding, = 0.5·(a + aᵀ) bit for bit
-  // (ILQR_BW4_MFMA_T: a ≈50-cycle MFMA result instead of a ds_bpermute round trip on
-  // the solve's and the symmetrisation's dependent chains)
-  [[maybe_unused]] const double Id = rho == kap ? 1.0 : 0.0, Ih = rho == kap ? 0.5 : 0.0;
-  // lane masks of the solve's per-lane entries (ILQR_BW4_SEL_FMA): M[i][j] (i > j) at
-  // lane (ρ, κ) = (i, j), the unit diagonal, D⁻¹[i] at row ρ = i
-  [[maybe_unused]] double sel_m[4][4], sel_r[4];
-  [[maybe_unused]] const double sel_d = Id;
+  // the block transpose within each slot on the MFMA: mf4(a, I, 0) = aᵀ, exact (products
+  // with 1 and 0); mf4(a, I/2, a/2) = (a + aᵀ)/2 with one rounding, = 0.5·(a + aᵀ) bit
+  // for bit (a ≈50-cycle MFMA result instead of a ds_bpermute round trip on the solve's
+  // and the symmetrisation's dependent chains)
+  const double Id = rho == kap ? 1.0 : 0.0, Ih = rho == kap ? 0.5 : 0.0;
+  // lane masks of the solve's per-lane entries: M[i][j] (i > j) at lane (ρ, κ) = (i, j),
+  // the unit diagonal, D⁻¹[i] at row ρ = i
+  double sel_m[4][4], sel_r[4];
+  const double sel_d = Id;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     sel_r[i] = rho == i ? 1.0 : 0.0;
@@ -196,10 +178,9 @@ __device__ unsigned lq_backward4_wave(const LQParams& P, int b0, int B, unsigned
   const uint32_t kv = live ? (uint32_t)((beta * T * NU * NX + rho * NX + kap) * 8) : DEAD;
   const uint32_t dv = (live && kap == 0) ? (uint32_t)((beta * T * NU + rho) * 8) : DEAD;
 
-  // z_t = [x_t; u_t] (cost gradient L z, :101-106). LZ4: one MFMA set gives L z for
-  // steps t0 .. t0-3 (column κ = step t0-κ); each step permutes its column out.
-  constexpr bool LZ4 = (ABL & 32) == 0;
-  double Lzq[4] = {0.0, 0.0, 0.0, 0.0}, zq[4], zc[4], zn[4];
+  // z_t = [x_t; u_t] (cost gradient L z, :101-106): one MFMA set gives L z for steps
+  // t0 .. t0-3 (column κ = step t0-κ); each step permutes its column out.
+  double Lzq[4] = {0.0, 0.0, 0.0, 0.0}, zq[4];
   auto load_zq = [&](int t0) {  // clamped at step 0
     const int tz = t0 - kap > 0 ? t0 - kap : 0;
     const uint32_t xo = (uint32_t)(((beta * (T + 1) + tz) * NX + rho) * 8);
@@ -207,12 +188,6 @@ __device__ unsigned lq_backward4_wave(const LQParams& P, int b0, int B, unsigned
 #pragma unroll
     for (int K = 0; K < 3; ++K) zq[K] = buf_ld(rX, xo + 32 * K, 0);
     zq[3] = buf_ld(rU, uo, 0);
-  };
-  const uint32_t zxo = (uint32_t)((beta * (T + 1) * NX + rho) * 8), zuo = (uint32_t)((beta * T * NU + rho) * 8);
-  auto load_z = [&](int t, double (&z)[4]) {
-#pragma unroll
-    for (int K = 0; K < 3; ++K) z[K] = buf_ld(rX, zxo + 32 * K, (uint32_t)(t * NX * 8));
-    z[3] = buf_ld(rU, zuo, (uint32_t)(t * NU * 8));
   };
   // L z for the four steps from t0 (column κ = step t0 − κ), from zq; then the next
   // four steps' z. Computed one step ahead of its first use, so each step's column
@@ -228,15 +203,14 @@ __device__ unsigned lq_backward4_wave(const LQParams& P, int b0, int B, unsigned
     Lzq[3] = mf4(LR, zq[3], 0.0);
     load_zq(t0 - 4);
   };
-  if constexpr (LZ4) load_zq(T - 1);
-  else load_z(T - 1, zc);
+  load_zq(T - 1);
 
   double* Hl = lds + beta * 16;
   double Klast[4];
   // every load of the prologue lands here, so the loop's waits only count the loop's
   // own loads
   __builtin_amdgcn_s_waitcnt(0);
-  if constexpr (LZ4 && (ABL & 256) == 0) lz_block(T - 1);
+  lz_block(T - 1);
 
   // lane-permutation sources of the L z columns, one per step of a block of four
   int lz_src[4];
@@ -246,20 +220,11 @@ __device__ unsigned lq_backward4_wave(const LQParams& P, int b0, int B, unsigned
   // is static: the loop below runs the steps four at a time
   auto step = [&](const int t, auto jc) {
     constexpr int JJ = decltype(jc)::value;
-    if constexpr ((ABL & 64) != 0) {
+    // this step's L z columns: the permutes issue here, their LDS latency hidden behind
+    // the S·F products
+    double lzp[4];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) zn[k] = zc[k] * 0.5;
-    } else if constexpr (!LZ4) {
-      load_z(t > 0 ? t - 1 : 0, zn);
-    }
-
-    // this step's L z columns (LZ4): the permutes issue here, their LDS latency hidden
-    // behind the S·F products
-    [[maybe_unused]] double lzp[4];
-    if constexpr (LZ4 && (ABL & 256) == 0) {
-#pragma unroll
-      for (int I = 0; I < 4; ++I) lzp[I] = lane_perm(Lzq[I], lz_src[JJ]);
-    }
+    for (int I = 0; I < 4; ++I) lzp[I] = lane_perm(Lzq[I], lz_src[JJ]);
     // Y = S·F, column block 3 (B) first: H needs it. Each sum runs over K = 0, 1, 2;
     // its K ≤ I terms read stored upper blocks S[K][I], its K > I terms the lower blocks
     // that the previous step's lane permutations produce: all 24 upper-block products
@@ -282,66 +247,19 @@ __device__ unsigned lq_backward4_wave(const LQParams& P, int b0, int B, unsigned
 #pragma unroll
         for (int K = I + 1; K < 3; ++K) Y[I][J] = mf4(S[K][I], F[K][J], Y[I][J]);
     // H = R + Rᵀ + BᵀSB → LDS, read back whole by the slot's lanes
-    double H = ILQR_BW4_MU_IN_H ? LRmu : LR;
+    double H = LRmu;
 #pragma unroll
     for (int K = 0; K < 3; ++K) H = mf4(F[K][3], Y[K][3], H);
     Hl[rho * 4 + kap] = H;
 
     // gradient [lx + Aᵀs | lu + Bᵀs] (:181, :269)
     double gv[4];
-    if constexpr (LZ4) {
-      constexpr int j = JJ;
-      double lz[4];
-      if constexpr ((ABL & 256) != 0) {  // through LDS: column j of each block, replicated
-        if (j == 0) {  // L z for steps t .. t-3, then the next four steps' z
 #pragma unroll
-          for (int I = 0; I < 3; ++I) {
-            double v = 0.0;
+    for (int I = 0; I < 4; ++I) {
+      double v = lzp[I];
 #pragma unroll
-            for (int K = 0; K < 3; ++K) v = mf4(L[K][I], zq[K], v);
-            Lzq[I] = v;
-          }
-          Lzq[3] = mf4(LR, zq[3], 0.0);
-          load_zq(t - 4);
-        }
-        double* Lzl = lds + 64 + beta * 64;
-        if (j == 0) {
-          double2* w = reinterpret_cast<double2*>(Lzl + (kap * 4 + rho) * 4);
-          w[0] = double2{Lzq[0], Lzq[1]};
-          w[1] = double2{Lzq[2], Lzq[3]};
-          wave_lds_fence();
-        }
-        const double2* rd = reinterpret_cast<const double2*>(Lzl + (j * 4 + rho) * 4);
-        const double2 a = rd[0], c = rd[1];
-        lz[0] = a.x; lz[1] = a.y; lz[2] = c.x; lz[3] = c.y;
-      } else {
-#pragma unroll
-        for (int I = 0; I < 4; ++I) lz[I] = lzp[I];
-      }
-#pragma unroll
-      for (int I = 0; I < 4; ++I) {
-        double v = lz[I];
-#pragma unroll
-        for (int K = 0; K < 3; ++K) v = mf4(F[K][I], s[K], v);
-        gv[I] = v;
-      }
-    } else if constexpr ((ABL & 4) != 0) {
-#pragma unroll
-      for (int I = 0; I < 4; ++I) gv[I] = I < 3 ? s[I] + zc[I] : zc[3];
-    } else {
-#pragma unroll
-      for (int I = 0; I < 4; ++I) {
-        double v = 0.0;
-        if (I < 3) {
-#pragma unroll
-          for (int K = 0; K < 3; ++K) v = mf4(L[K][I], zc[K], v);
-        } else {
-          v = mf4(LR, zc[3], v);
-        }
-#pragma unroll
-        for (int K = 0; K < 3; ++K) v = mf4(F[K][I], s[K], v);
-        gv[I] = v;
-      }
+      for (int K = 0; K < 3; ++K) v = mf4(F[K][I], s[K], v);
+      gv[I] = v;
     }
     // G = BᵀSA (lux = 0) and Qxx = lxx + AᵀSA (upper blocks)
     double G[3], Z[3][3];
@@ -373,16 +291,7 @@ __device__ unsigned lq_backward4_wave(const LQParams& P, int b0, int B, unsigned
       for (int k = 0; k <= i; ++k) h[i][k] = Hl[i * 4 + k];
     wave_lds_fence();
     LDLT<4, 1> f;
-    if constexpr ((ABL & 1) != 0) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        f.dinv[i] = h[i][i];
-#pragma unroll
-        for (int k = 0; k < i; ++k) f.l[i][k] = h[i][k] * 1e-3;
-      }
-    } else {
-      f.factor<!ILQR_BW4_MU_IN_H>(h, mu);
-    }
+    f.factor<false>(h, mu);  // μ is in H already
     // M = L⁻¹ (unit lower)
     double Mf[4][4];
     Mf[1][0] = -f.l[1][0];
@@ -392,55 +301,31 @@ __device__ unsigned lq_backward4_wave(const LQParams& P, int b0, int B, unsigned
     Mf[3][1] = fma(f.l[3][2], f.l[2][1], -f.l[3][1]);
     Mf[3][0] = fma(-f.l[3][2], Mf[2][0], fma(-f.l[3][1], Mf[1][0], -f.l[3][0]));
     // this lane's entries: Mn = M[ρ][κ], D⁻¹[ρ]
-    double Mn, dsel;
-    if constexpr (ILQR_BW4_SEL_FMA) {
-      // Σ (0/1 lane mask) × entry: exact (x·1 = x, x·0 = ±0 and x ± 0 = x), so the same
-      // bits as the selects, in 10 f64 ops where the selects took 18 b32 ones
-      Mn = sel_d;
+    // Σ (0/1 lane mask) × entry: exact (x·1 = x, x·0 = ±0 and x ± 0 = x), so the same
+    // bits as selects, in 10 f64 ops where the selects took 18 b32 ones
+    double Mn = sel_d;
 #pragma unroll
-      for (int i = 1; i < 4; ++i)
+    for (int i = 1; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < i; ++j) Mn = fma(sel_m[i][j], Mf[i][j], Mn);
-      dsel = sel_r[0] * f.dinv[0];
+      for (int j = 0; j < i; ++j) Mn = fma(sel_m[i][j], Mf[i][j], Mn);
+    double dsel = sel_r[0] * f.dinv[0];
 #pragma unroll
-      for (int i = 1; i < 4; ++i) dsel = fma(sel_r[i], f.dinv[i], dsel);
-    } else {
-      Mn = rho == kap ? 1.0 : 0.0;
-#pragma unroll
-      for (int i = 1; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < i; ++j) Mn = (rho == i && kap == j) ? Mf[i][j] : Mn;
-      dsel = f.dinv[0];
-#pragma unroll
-      for (int i = 1; i < 4; ++i) dsel = rho == i ? f.dinv[i] : dsel;
-    }
+    for (int i = 1; i < 4; ++i) dsel = fma(sel_r[i], f.dinv[i], dsel);
 
     // K_aug = −(H + μI)⁻¹ [G | g] = −(D⁻¹M)ᵀ (M [G | g]): the LDLᵀ solve's two
     // triangular sweeps as two MFMA stages. A operands: M·  wants M[κ][ρ] (the
     // transpose of Mn, by the lane permutation), (D⁻¹M)ᵀ· wants D⁻¹[ρ] M[ρ][κ].
-    // (Forming (H + μI)⁻¹ = Mᵀ D⁻¹ M explicitly instead — ablation bit 16 — costs
-    // two digits on the headline's near-rank-1 H: 2e-11 against the oracle where
-    // the sweeps give 1.7e-13, profiles/r01/bw4_quad.txt.)
+    // (Forming (H + μI)⁻¹ = Mᵀ D⁻¹ M explicitly instead costs two digits on the
+    // headline's near-rank-1 H: 2e-11 against the oracle where the sweeps give 1.7e-13,
+    // profiles/r01/bw4_quad.txt; a residual-checked Newton-Schulz inverse measured
+    // slower, tools/ablation/bw4_newton_schulz.patch.)
     double Kg[4];
-    if constexpr ((ABL & 16) != 0) {
-      const double Hi = mf4(Mn, Mn * dsel, 0.0);
+    const double Mt = mf4(Mn, Id, 0.0), Mnd = Mn * dsel;
 #pragma unroll
-      for (int J = 0; J < 4; ++J) Kg[J] = mf4n(Hi, J < 3 ? G[J] : gv[3], 0.0);
-    } else {
-#if ILQR_BW4_MFMA_T
-      const double Mt = mf4(Mn, Id, 0.0), Mnd = Mn * dsel;
-#else
-      const double Mt = lane_perm(Mn, tr_src), Mnd = Mn * dsel;
-#endif
+    for (int J = 0; J < 4; ++J) Kg[J] = mf4n(Mnd, mf4(Mt, J < 3 ? G[J] : gv[3], 0.0), 0.0);
 #pragma unroll
-      for (int J = 0; J < 4; ++J) Kg[J] = mf4n(Mnd, mf4(Mt, J < 3 ? G[J] : gv[3], 0.0), 0.0);
-    }
-    if constexpr ((ABL & 8) == 0) {
-      constexpr int AUX = (ABL >> 9) & 7;  // probe only: cache-policy bits of the gain stores
-#pragma unroll
-      for (int J = 0; J < 3; ++J) buf_st<AUX>(Kg[J], rK, kv + 32 * J, (uint32_t)(t * NU * NX * 8));
-      buf_st<AUX>(Kg[3], rD, dv, (uint32_t)(t * NU * 8));
-    }
+    for (int J = 0; J < 3; ++J) buf_st(Kg[J], rK, kv + 32 * J, (uint32_t)(t * NU * NX * 8));
+    buf_st(Kg[3], rD, dv, (uint32_t)(t * NU * 8));
 
     // step_back (:268-270): W = (H + 2μI) K_aug = μ K_aug − [G | g],
     // [S | s] = [Qxx | lx + Aᵀs] − K_augᵀ W
@@ -454,28 +339,18 @@ __device__ unsigned lq_backward4_wave(const LQParams& P, int b0, int B, unsigned
       for (int J = I; J < 3; ++J) S[I][J] = mf4n(Kg[I], W[J], Z[I][J]);
       s[I] = mf4n(Kg[I], W[3], gv[I]);
     }
-    if ((ABL & 128) == 0 && (t % SYM_EVERY) == 0) {
+    if ((t % SYM_EVERY) == 0) {
 #pragma unroll
-      for (int I = 0; I < 3; ++I)
-#if ILQR_BW4_MFMA_T
-        S[I][I] = mf4(S[I][I], Ih, 0.5 * S[I][I]);
-#else
-        S[I][I] = 0.5 * (S[I][I] + lane_perm(S[I][I], tr_src));
-#endif
+      for (int I = 0; I < 3; ++I) S[I][I] = mf4(S[I][I], Ih, 0.5 * S[I][I]);
     }
 #pragma unroll
     for (int I = 0; I < 3; ++I)
 #pragma unroll
-      for (int J = I + 1; J < 3; ++J)
-        S[J][I] = (ABL & 2) ? S[I][J] : ILQR_BW4_SLOW_MFMA ? mf4(S[I][J], Id, 0.0) : lane_perm(S[I][J], tr_src);
-    if constexpr (!LZ4) {
-#pragma unroll
-      for (int k = 0; k < 4; ++k) zc[k] = zn[k];
-    }
+      for (int J = I + 1; J < 3; ++J) S[J][I] = mf4(S[I][J], Id, 0.0);
 #pragma unroll
     for (int J = 0; J < 4; ++J) Klast[J] = Kg[J];
-    // the next step starts a block of four: its L z now (LZ4)
-    if constexpr (LZ4 && (ABL & 256) == 0 && JJ == 3) {
+    // the next step starts a block of four: its L z now
+    if constexpr (JJ == 3) {
       if (t > 0) lz_block(t - 1);
     }
   };
@@ -503,7 +378,6 @@ __device__ unsigned lq_backward4_wave(const LQParams& P, int b0, int B, unsigned
   return r;
 }
 
-template <int ABL = 0>
 __global__ __launch_bounds__(256) void lq_backward4_kernel(LQParams P, int B, int T,
                                                            const double* __restrict__ x,
                                                            const double* __restrict__ u,
@@ -514,7 +388,7 @@ __global__ __launch_bounds__(256) void lq_backward4_kernel(LQParams P, int B, in
   const int w = threadIdx.x >> 6;
   const int b0 = (blockIdx.x * BW4_WAVES + w) * BW4_SLOTS;
   if (b0 >= B) return;
-  const unsigned nan = lq_backward4_wave<ABL>(P, b0, B, 0xFu, T, x, u, d, K, mu, lds + w * BW4_LDS);
+  const unsigned nan = lq_backward4_wave(P, b0, B, 0xFu, T, x, u, d, K, mu, lds + w * BW4_LDS);
   const int l = threadIdx.x & 63;
   if (status && l < BW4_SLOTS && b0 + l < B) status[b0 + l] = ((nan >> l) & 1u) ? ILQR_TRAJ_NAN : ILQR_TRAJ_OK;
 }
@@ -638,7 +512,7 @@ int bw4_grid(int B) {
 hipError_t launch_lq_backward4(const LQParams& p, int B, int T, const double* x, const double* u,
                                double* d, double* K, int32_t* status, double mu, hipStream_t s) {
   if (B <= 0) return hipSuccess;
-  lq_backward4_kernel<0><<<bw4_grid(B), 256, 0, s>>>(p, B, T, x, u, d, K, status, mu);
+  lq_backward4_kernel<<<bw4_grid(B), 256, 0, s>>>(p, B, T, x, u, d, K, status, mu);
   return hipGetLastError();
 }
 

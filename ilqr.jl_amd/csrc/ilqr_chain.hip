@@ -160,13 +160,6 @@ __device__ __forceinline__ F2 crecip(F2 x) {
   const F2 r = F2{__builtin_amdgcn_rcpf(x.x), __builtin_amdgcn_rcpf(x.y)};
   return (F2(1.0f) - x * r) * r + r;
 }
-#ifndef ILQR_CHAIN_FD_PAIR
-#define ILQR_CHAIN_FD_PAIR 1
-#endif
-// the fp32 forward's fast step on packed joint pairs (chain_trig_rk4_fast2)
-#ifndef ILQR_CHAIN_F2_FAST
-#define ILQR_CHAIN_F2_FAST 1
-#endif
 
 template <class S> struct ValueOf { using type = S; };
 template <int N, class V> struct ValueOf<DualT<N, V>> { using type = V; };
@@ -227,43 +220,11 @@ __device__ __forceinline__ void to_parent(const S (&R)[9], const S (&w)[3], S (&
   for (int r = 0; r < 3; ++r) o[r] = R[3 * r] * w[0] + R[3 * r + 1] * w[1] + R[3 * r + 2] * w[2];
 }
 
-// The same coordinate changes as in-place Rodrigues rotations (no R_i): fewer
-// constants live at once. Only built with ILQR_CHAIN_FD_ROT=0 (the central-difference
-// linearisation used it while one lane ran all directions and R0x/R0aa spilled ~90
-// SGPRs; with one direction per lane the 3×3 form is faster);
-// tests/test_build.py compiles that alternate so it cannot rot.
-template <class S, class V, int NJ>
-__device__ __forceinline__ void rod_to_child(const ChainK<V, NJ>& P, int i, const S& c, const S& s,
-                                             const S (&w)[3], S (&o)[3]) {
-  S y[3];
-#pragma unroll
-  for (int r = 0; r < 3; ++r) y[r] = P.R0[i][r] * w[0] + P.R0[i][3 + r] * w[1] + P.R0[i][6 + r] * w[2];
-  S axy[3];
-  crossc(P.ax[i], y, axy);
-  const S ady = P.ax[i][0] * y[0] + P.ax[i][1] * y[1] + P.ax[i][2] * y[2];
-  const S k = (V(1) - c) * ady;
-#pragma unroll
-  for (int r = 0; r < 3; ++r) o[r] = c * y[r] - s * axy[r] + P.ax[i][r] * k;
-}
-template <class S, class V, int NJ>
-__device__ __forceinline__ void rod_to_parent(const ChainK<V, NJ>& P, int i, const S& c, const S& s,
-                                              const S (&w)[3], S (&o)[3]) {
-  S axw[3];
-  crossc(P.ax[i], w, axw);
-  const S adw = P.ax[i][0] * w[0] + P.ax[i][1] * w[1] + P.ax[i][2] * w[2];
-  const S k = (V(1) - c) * adw;
-  S y[3];
-#pragma unroll
-  for (int r = 0; r < 3; ++r) y[r] = c * w[r] + s * axw[r] + P.ax[i][r] * k;
-#pragma unroll
-  for (int r = 0; r < 3; ++r) o[r] = P.R0[i][3 * r] * y[0] + P.R0[i][3 * r + 1] * y[1] + P.R0[i][3 * r + 2] * y[2];
-}
-
 // Recursive Newton-Euler: τ = M(q) q̈ + [VEL] C(q, q̇)q̇ + [GRAV] g(q).
 // qd is read only when VEL; qdd[i] is the joint acceleration.
 // gs scales gravity (the lane-split forward runs the bias and the mass-matrix
 // columns as one uniform pass with per-lane q̇, q̈ and gravity; 1 elsewhere, folded)
-template <bool VEL, bool GRAV, bool ROT, int NJ, class S, class V>
+template <bool VEL, bool GRAV, int NJ, class S, class V>
 __device__ __forceinline__ void rnea(const ChainK<V, NJ>& P, const S (&c)[NJ], const S (&s)[NJ],
                                      const S (&qd)[NJ], const S (&qdd)[NJ], S (&tau)[NJ],
                                      V gs = V(1)) {
@@ -275,17 +236,14 @@ __device__ __forceinline__ void rnea(const ChainK<V, NJ>& P, const S (&c)[NJ], c
     al[r] = S(V(0));
     ac[r] = S(GRAV ? -P.g[r] * gs : V(0));  // fictitious base acceleration −g
   }
-  S fn[NJ][3], ff[NJ][3], R[ROT ? NJ : 1][9];
-  if constexpr (ROT) {
+  // joint transforms as 3×3 products of the per-evaluation R_i (in-place Rodrigues
+  // rotations measured slower once the linearisation ran one direction per lane,
+  // DESIGN.md §4; tools/ablation/restore_alternates.patch)
+  S fn[NJ][3], ff[NJ][3], R[NJ][9];
 #pragma unroll
-    for (int i = 0; i < NJ; ++i) joint_rot(P, i, c[i], s[i], R[i]);
-  }
-  auto tc = [&](int i, const S (&w)[3], S (&o)[3]) {
-    if constexpr (ROT) to_child(R[i], w, o); else rod_to_child(P, i, c[i], s[i], w, o);
-  };
-  auto tp = [&](int i, const S (&w)[3], S (&o)[3]) {
-    if constexpr (ROT) to_parent(R[i], w, o); else rod_to_parent(P, i, c[i], s[i], w, o);
-  };
+  for (int i = 0; i < NJ; ++i) joint_rot(P, i, c[i], s[i], R[i]);
+  auto tc = [&](int i, const S (&w)[3], S (&o)[3]) { to_child(R[i], w, o); };
+  auto tp = [&](int i, const S (&w)[3], S (&o)[3]) { to_parent(R[i], w, o); };
 #pragma unroll
   for (int i = 0; i < NJ; ++i) {
     S t[3], u3[3];
@@ -374,7 +332,7 @@ __device__ __forceinline__ void rnea(const ChainK<V, NJ>& P, const S (&c)[NJ], c
 
 // [q̇; v̇] with v̇ = M \ (τ − bias)  (RBD_helper_functions.jl:61-66).
 // nu = NJ drives every joint; nu = 1 drives joint 1 only.
-template <int NJ, int NU, bool ROT = true, class S, class V>
+template <int NJ, int NU, class S, class V>
 __device__ __forceinline__ void chain_xdot(const ChainK<V, NJ>& P, const S (&x)[2 * NJ],
                                            const S (&u)[NU], S (&xd)[2 * NJ]) {
   S c[NJ], s[NJ];
@@ -386,14 +344,14 @@ __device__ __forceinline__ void chain_xdot(const ChainK<V, NJ>& P, const S (&x)[
     zero[i] = S(V(0));
     qd[i] = x[NJ + i];
   }
-  rnea<true, true, ROT>(P, c, s, qd, zero, b);  // dynamics_bias
+  rnea<true, true>(P, c, s, qd, zero, b);  // dynamics_bias
   S M[NJ][NJ];
 #pragma unroll
   for (int k = 0; k < NJ; ++k) {  // mass_matrix, column k = RNEA(q, 0, e_k)
     S e[NJ], col[NJ];
 #pragma unroll
     for (int j = 0; j < NJ; ++j) e[j] = S(V(j == k ? 1 : 0));
-    rnea<false, false, ROT>(P, c, s, zero, e, col);
+    rnea<false, false>(P, c, s, zero, e, col);
 #pragma unroll
     for (int i = 0; i < NJ; ++i) M[i][k] = col[i];
   }
@@ -890,11 +848,9 @@ struct ChainTrigModel {
   static constexpr bool HAS_FAST = true;
   ChainTrig<V> P;
   __device__ __forceinline__ void rk4_fast(const V (&x)[4], const V (&u)[NU], V (&o)[4], bool& bad) const {
-#if ILQR_CHAIN_F2_FAST
+    // fp32: the joints packed (v_pk_* pairs)
     if constexpr (std::is_same_v<V, float>) chain_trig_rk4_fast2<NU>(P, x, u, o, bad);
-    else
-#endif
-      chain_trig_rk4_fast<NU>(P, x, u, o, bad);
+    else chain_trig_rk4_fast<NU>(P, x, u, o, bad);
   }
   __device__ __forceinline__ void rk4_robust(const V (&x)[4], const V (&u)[NU], V (&o)[4]) const;
   // ℓ(x̄ₖ − x_trajₖ, ūₖ) on the joints (forward_pass.jl:187-190; RBD_helper_functions.jl:85-99)
@@ -924,7 +880,7 @@ struct ChainTrigModel {
 
 // RK4 (RBD_helper_functions.jl:70-78) on either parameter set: ChainK (the recursion;
 // SPLIT = the 16-lane component-parallel form) or ChainTrig (closed form, 2 joints)
-template <int NJ, int NU, bool SPLIT = false, bool ROT = true, class S, class PK>
+template <int NJ, int NU, bool SPLIT = false, class S, class PK>
 __device__ __forceinline__ void chain_rk4(const PK& P, const S (&x)[2 * NJ],
                                           const S (&u)[NU], S (&out)[2 * NJ]) {
   constexpr int NX = 2 * NJ;
@@ -935,7 +891,7 @@ __device__ __forceinline__ void chain_rk4(const PK& P, const S (&x)[2 * NJ],
     else if constexpr (SPLIT)
       chain_xdot_cv<NJ, NU>(Pc, xx, uu, o);
     else
-      chain_xdot<NJ, NU, ROT>(Pc, xx, uu, o);
+      chain_xdot<NJ, NU>(Pc, xx, uu, o);
   };
   S k1[NX], k2[NX], k3[NX], k4[NX], y[NX];
   const V h = V(0.5);
@@ -1007,23 +963,13 @@ struct Rec {
 // (v7 ran one lane per (b, t) over all ND directions: 3,200 waves at B=2048, T=100 on a
 // 3-wave/SIMD occupancy — a second, nearly empty round on 32 CUs.)
 // occupancy asked of the linearisation: central differences, the ±h pair packed
-// (ILQR_CHAIN_FD_PAIR), at 3 waves/SIMD (168 VGPRs; config 5 2,208 it/s against 2,175
+// (one packed evaluation), at 3 waves/SIMD (168 VGPRs; config 5 2,208 it/s against 2,175
 // at 2 waves, 1,962 at 4 where it spills, and 2,163 unpacked at 4 waves); the dual
 // kernel at 2 (256 VGPRs, ~150 spilled, still faster than 1 wave with 300 registers:
 // config 5 dual 1,710 → 1,908 it/s)
-// joint transforms of the central-difference linearisation: 0 = Rodrigues rotations in
-// place, 1 = 3×3 products of the per-evaluation R_i (the forward's form)
-#ifndef ILQR_CHAIN_FD_ROT
-#define ILQR_CHAIN_FD_ROT 1
-#endif
-#ifndef ILQR_CHAIN_DUAL_WAVES
-#define ILQR_CHAIN_DUAL_WAVES 2
-#endif
-#ifndef ILQR_CHAIN_FD_WAVES
-#define ILQR_CHAIN_FD_WAVES 3
-#endif
+constexpr int CHAIN_FD_WAVES = 3, CHAIN_DUAL_WAVES = 2;
 template <class V, int NJ, int NU, int LIN, class PK = ChainK<V, NJ>>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LIN == ILQR_LINEARIZE_CENTRAL_FD ? ILQR_CHAIN_FD_WAVES : ILQR_CHAIN_DUAL_WAVES))) void chain_linearize_kernel(PK P, int B, int T,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LIN == ILQR_LINEARIZE_CENTRAL_FD ? CHAIN_FD_WAVES : CHAIN_DUAL_WAVES))) void chain_linearize_kernel(PK P, int B, int T,
                                                               const V* __restrict__ x,
                                                               const V* __restrict__ u,
                                                               const int32_t* __restrict__ status,
@@ -1088,7 +1034,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LIN == ILQR
 #pragma unroll
       for (int j = 0; j < NU; ++j)
         if (NX + j == k) { up[j] = zp; um[j] = zm; }
-#if ILQR_CHAIN_FD_PAIR
       if constexpr (sizeof(V) == 4) {
         // f(z + h e_k) and f(z − h e_k) run the same instruction stream: one packed
         // evaluation (v_pk_* on the pair)
@@ -1097,14 +1042,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LIN == ILQR
         for (int j = 0; j < NX; ++j) x2[j] = F2{(float)xp[j], (float)xm[j]};
 #pragma unroll
         for (int j = 0; j < NU; ++j) u2[j] = F2{(float)up[j], (float)um[j]};
-        chain_rk4<NJ, NU, false, ILQR_CHAIN_FD_ROT>(P, x2, u2, f2);
+        chain_rk4<NJ, NU>(P, x2, u2, f2);
 #pragma unroll
         for (int j = 0; j < NX; ++j) { fp[j] = f2[j].x; fm[j] = f2[j].y; }
-      } else
-#endif
-      {
-        chain_rk4<NJ, NU, false, ILQR_CHAIN_FD_ROT>(P, xp, up, fp);
-        chain_rk4<NJ, NU, false, ILQR_CHAIN_FD_ROT>(P, xm, um, fm);
+      } else {
+        chain_rk4<NJ, NU>(P, xp, up, fp);
+        chain_rk4<NJ, NU>(P, xm, um, fm);
       }
       const V inv = V(1) / (zp - zm);
 #pragma unroll
@@ -1749,8 +1692,8 @@ __global__ void chain_trig_sample_kernel(ChainK<double, 2> P, double* __restrict
     double c[2] = {1.0, 0.0}, sn[2] = {0.0, 0.0};
     sincos(two_pi * k / 5.0, &sn[1], &c[1]);
     double m0[2], m1[2];
-    rnea<false, false, true>(P, c, sn, zero, e0, m0);
-    rnea<false, false, true>(P, c, sn, zero, e1, m1);
+    rnea<false, false>(P, c, sn, zero, e0, m0);
+    rnea<false, false>(P, c, sn, zero, e1, m1);
     out[3 * k] = m0[0];
     out[3 * k + 1] = 0.5 * (m1[0] + m0[1]);  // symmetric up to rounding
     out[3 * k + 2] = m1[1];
@@ -1760,7 +1703,7 @@ __global__ void chain_trig_sample_kernel(ChainK<double, 2> P, double* __restrict
       double c[2], sn[2], g[2];
       sincos(two_pi * a / 3.0, &sn[0], &c[0]);
       sincos(two_pi * b / 3.0, &sn[1], &c[1]);
-      rnea<false, true, true>(P, c, sn, zero, zero, g);
+      rnea<false, true>(P, c, sn, zero, zero, g);
       out[15 + 2 * (3 * a + b)] = g[0];
       out[15 + 2 * (3 * a + b) + 1] = g[1];
     }
@@ -1778,7 +1721,7 @@ __global__ void chain_trig_check_kernel(ChainK<double, 2> P, ChainTrig<double> Q
   };
   double x[4] = {rnd(-4, 4), rnd(-4, 4), rnd(-6, 6), rnd(-6, 6)}, u[2] = {rnd(-3, 3), rnd(-3, 3)};
   double a[4], b[4];
-  chain_xdot<2, 2, true>(P, x, u, a);
+  chain_xdot<2, 2>(P, x, u, a);
   chain_xdot_trig<2>(Q, x, u, b);
   double e = 0.0, m = 1.0;
   for (int k = 0; k < 4; ++k) {

@@ -9,7 +9,7 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 typedef unsigned u2v __attribute__((ext_vector_type(2)));
 
 constexpr int WAVES_PER_WG = 4;   // trajectories per workgroup
-constexpr int YT_OFF = 96 + 16 * 17 + 64;  // Y all-gather tile (VALU products): 16 columns × 14
+constexpr int YT_OFF = 96 + 16 * 17 + 64;  // (the VALU-product variant's Y tile: kept, the LDS size measured)
 constexpr int BW_LDS = YT_OFF + 16 * 14;   // doubles of backward scratch per wave: [G|H] rows, g row, zero, S tile, junk row, Y tile
 constexpr int SYM_EVERY = 8;          // symmetrise S every this many steps
 
@@ -147,45 +147,5 @@ struct LDLT {
   }
 };
 
-}  // namespace
-}  // namespace ilqr
-
-namespace ilqr {
-namespace {
-// (H + μI)⁻¹ r for NU = 4 by 2×2 blocks: H = [[P, Q], [Qᵀ, R]], Schur complement
-// S = R − QᵀP⁻¹Q; two reciprocals (of det P, det S) instead of LDLᵀ's four, and a
-// shorter dependent chain. H symmetric, lower triangle read.
-struct Schur4 {
-  double pi00, pi01, pi11;          // P⁻¹
-  double w00, w01, w10, w11;        // W = P⁻¹Q
-  double si00, si01, si11;          // S⁻¹
-  double q00, q01, q10, q11;        // Q (rows 0..1, cols 2..3)
-  template <int NEWTON>
-  __device__ __forceinline__ void factor(const double (&h)[4][4], double mu) {
-    const double p00 = h[0][0] + mu, p01 = h[1][0], p11 = h[1][1] + mu;
-    q00 = h[2][0]; q01 = h[3][0]; q10 = h[2][1]; q11 = h[3][1];
-    const double ip = rcp<NEWTON>(fma(p00, p11, -p01 * p01));
-    pi00 = p11 * ip; pi01 = -p01 * ip; pi11 = p00 * ip;
-    w00 = fma(pi00, q00, pi01 * q10); w01 = fma(pi00, q01, pi01 * q11);
-    w10 = fma(pi01, q00, pi11 * q10); w11 = fma(pi01, q01, pi11 * q11);
-    const double s00 = h[2][2] + mu - fma(q00, w00, q10 * w10);
-    const double s01 = h[3][2] - fma(q00, w01, q10 * w11);
-    const double s11 = h[3][3] + mu - fma(q01, w01, q11 * w11);
-    const double is = rcp<NEWTON>(fma(s00, s11, -s01 * s01));
-    si00 = s11 * is; si01 = -s01 * is; si11 = s00 * is;
-  }
-  __device__ __forceinline__ d4 solve(d4 b) const {
-    const double y0 = fma(pi00, b[0], pi01 * b[1]);
-    const double y1 = fma(pi01, b[0], pi11 * b[1]);
-    const double c0 = b[2] - fma(q00, y0, q10 * y1);
-    const double c1 = b[3] - fma(q01, y0, q11 * y1);
-    d4 x;
-    x[2] = fma(si00, c0, si01 * c1);
-    x[3] = fma(si01, c0, si11 * c1);
-    x[0] = y0 - fma(w00, x[2], w01 * x[3]);
-    x[1] = y1 - fma(w10, x[2], w11 * x[3]);
-    return x;
-  }
-};
 }  // namespace
 }  // namespace ilqr

@@ -29,10 +29,7 @@
 namespace ilqr {
 namespace {
 
-#ifndef ILQR_FW_GROUP_PF
-#define ILQR_FW_GROUP_PF 2
-#endif
-constexpr int FG_PF = ILQR_FW_GROUP_PF;  // input prefetch depth (steps)
+constexpr int FG_PF = 2;  // input prefetch depth (steps; 4 measured no faster, tools/tl_fw_probe)
 
 template <bool ROBUST>
 struct FgPath {

@@ -126,122 +126,16 @@ __device__ __forceinline__ double dpp_dot16_bd(double src, const double (&c)[12]
   return (a0 + a1) + (a2 + a3);
 }
 
-#ifndef ILQR_FW_ABLATE
-#define ILQR_FW_ABLATE 0
-#endif
-// cache policy of the ring forward's memory traffic (tools/fw_alt.sh): the aux bits of
-// the x̄/ū result stores (gfx950: 1 sc0, 2 nt, 16 sc1: both slower) and a " nt" hint on
-// the slot loads — on all three (1: +10 µs, the x_traj = NULL re-reads of x then miss)
-// or on the first alone (2, the default: 64 of the step's 96 K-row chunks, read once;
-// forward 52.6 → 48.9 µs at B = 4096, bench 6,530 → 6,650 batched it/s,
-// profiles/r02/bench_ab_k_nt.log). A slot layout with both K loads pure and hinted
-// measured slower (52.6 µs, bench_ab_k_pure.log).
-#ifndef ILQR_FW_ST_AUX
-#define ILQR_FW_ST_AUX 0
-#endif
-#ifndef ILQR_FW_LD_NT
-#define ILQR_FW_LD_NT 2
-#endif
-#if ILQR_FW_LD_NT == 1
-#define ILQR_FW_LDS_OP "global_load_lds_dwordx4 %0, off nt"
-#else
-#define ILQR_FW_LDS_OP "global_load_lds_dwordx4 %0, off"
-#endif
-// ILQR_FW_LD_NT = 2: the hint on the first slot load only (K rows alone: dead after
-// the step, never re-read from cache)
-#if ILQR_FW_LD_NT == 2
+// Cache policy of the ring forward's memory traffic (measured, round 2): the slot loads
+// carry a " nt" hint on the first load alone (64 of the step's 96 K-row chunks, read
+// once, dead after the step: forward 52.6 → 48.9 µs at B = 4096, bench 6,530 → 6,650
+// batched it/s, profiles/r02/bench_ab_k_nt.log); on all three loads it cost 10 µs (the
+// x_traj = NULL re-reads of x then miss), nt/sc0/sc1 result stores were slower and a
+// slot layout with both K loads pure and hinted measured 52.6 µs. Row broadcasts
+// through LDS instead of DPP gave the same bits and measured slower. (These alternates
+// and the forward's timing-only ablations live in tools/ablation/restore_alternates.patch.)
 #define ILQR_FW_LDS_OP1 "global_load_lds_dwordx4 %0, off nt"
-#else
-#define ILQR_FW_LDS_OP1 ILQR_FW_LDS_OP
-#endif
-
-// Row broadcasts through LDS instead of DPP: every lane writes its value to the wave's
-// scratch, each lane reads its row's 16 values back (ds_read_b128, a broadcast per
-// row) and accumulates with plain FMAs — the same four accumulators, operands and
-// order as the DPP helpers above, so the same bits. A v_fmac_f64_dpp row_newbcast
-// issues in ≈18 cycles at one wave per SIMD against ≈8 for a plain f64 FMA
-// (tools/fw_alt.sh ablations, profiles/r02/fw_ablate.log).
-#ifndef ILQR_FW_LDS_BCAST
-#define ILQR_FW_LDS_BCAST 0
-#endif
-struct RowBcast {
-  double* buf;  // this wave's 64-double scratch vector
-  int l, row;   // lane, first lane of its 16-lane row
-  __device__ __forceinline__ void put(double v) const {
-    buf[l] = v;
-    wave_lds_fence();
-  }
-  template <int K0, int N>
-  __device__ __forceinline__ void get(double (&w)[N]) const {
-    static_assert(K0 % 2 == 0 && N % 2 == 0, "16-byte reads");
-    const double2* p = reinterpret_cast<const double2*>(buf + row + K0);
-#pragma unroll
-    for (int k = 0; k < N / 2; ++k) {
-      const double2 v = p[k];
-      w[2 * k] = v.x;
-      w[2 * k + 1] = v.y;
-    }
-  }
-};
-// Σ_k<12 bcast_k(src)·c[k] (dpp_dot12's bits)
-__device__ __forceinline__ double lds_dot12(const RowBcast& rb, double src, const double (&c)[12]) {
-  rb.put(src);
-  double w[12];
-  rb.get<0>(w);
-  Acc4 r;
-#pragma unroll
-  for (int k = 0; k < 12; k += 4) {
-    r.a0 = fma(w[k], c[k], r.a0);
-    r.a1 = fma(w[k + 1], c[k + 1], r.a1);
-    r.a2 = fma(w[k + 2], c[k + 2], r.a2);
-    r.a3 = fma(w[k + 3], c[k + 3], r.a3);
-  }
-  return r.sum();
-}
-// dpp_acc16_head / dpp_acc16_tail
-__device__ __forceinline__ void lds_acc16_head(const RowBcast& rb, Acc4& r, double src, const double (&c)[16]) {
-  rb.put(src);
-  double w[12];
-  rb.get<0>(w);
-#pragma unroll
-  for (int k = 0; k < 12; k += 4) {
-    r.a0 = fma(w[k], c[k], r.a0);
-    r.a1 = fma(w[k + 1], c[k + 1], r.a1);
-    r.a2 = fma(w[k + 2], c[k + 2], r.a2);
-    r.a3 = fma(w[k + 3], c[k + 3], r.a3);
-  }
-}
-__device__ __forceinline__ void lds_acc16_tail(const RowBcast& rb, Acc4& r, double src2, const double (&c)[16]) {
-  rb.put(src2);
-  double w[4];
-  rb.get<12>(w);
-  r.a0 = fma(w[0], c[12], r.a0);
-  r.a1 = fma(w[1], c[13], r.a1);
-  r.a2 = fma(w[2], c[14], r.a2);
-  r.a3 = fma(w[3], c[15], r.a3);
-}
-// dpp_dot16_bd: lanes 0..11 of a row Σ_k<12 bcast_k·c[k], lanes 12..15 Σ_m<4 bcast_{12+m}·c[m]
-__device__ __forceinline__ double lds_dot16_bd(const RowBcast& rb, double src, const double (&c)[12], bool x_lane) {
-  rb.put(src);
-  double w[16];
-  rb.get<0>(w);
-  Acc4 r;
-  if (x_lane) {
-#pragma unroll
-    for (int k = 0; k < 12; k += 4) {
-      r.a0 = fma(w[k], c[k], r.a0);
-      r.a1 = fma(w[k + 1], c[k + 1], r.a1);
-      r.a2 = fma(w[k + 2], c[k + 2], r.a2);
-      r.a3 = fma(w[k + 3], c[k + 3], r.a3);
-    }
-  } else {
-    r.a0 = fma(w[12], c[0], r.a0);
-    r.a1 = fma(w[13], c[1], r.a1);
-    r.a2 = fma(w[14], c[2], r.a2);
-    r.a3 = fma(w[15], c[3], r.a3);
-  }
-  return r.sum();
-}
+#define ILQR_FW_LDS_OP "global_load_lds_dwordx4 %0, off"
 
 struct FwdOut {
   double cost;
@@ -277,8 +171,9 @@ struct CandPass {
 // storing). One slot (3 KB): K rows [0,192), x [192,240), u [240,256), x_traj
 // [256,304), δu [304,320) doubles; group g at K + 48g, x/x_traj + 12g, u/δu + 4g.
 constexpr int RING_SLOT = 384;  // doubles per ring slot
-// Q, R of the wave's 4 trajectories (+ read overhang), then the row-broadcast scratch
-// (four 64-double vectors, ILQR_FW_LDS_BCAST)
+// Q, R of the wave's 4 trajectories (+ read overhang), then four 64-double vectors of
+// scratch (unused since the LDS row broadcasts went; kept so the kernels' LDS size and
+// occupancy stay those measured)
 constexpr int RING_LAREA = 4 * 160 + 16 + 4 * 64;
 
 // LR_REGS: the wave's Q/R cost rows live in registers for the whole pass (kernels with
@@ -342,9 +237,6 @@ __device__ FwdOut lq_forward_wave_ring(const LQParams& P, int b0, int B, int T, 
       Lk[2 * k + 1] = q.y;
     }
   }
-  double* const bc = Ls + 4 * 160 + 16;  // row-broadcast scratch: x̄, δx, ū, v
-  [[maybe_unused]] const RowBcast rbx{bc, l, g * 16}, rbd{bc + 64, l, g * 16}, rbu{bc + 128, l, g * 16},
-      rbv{bc + 192, l, g * 16};
   wave_lds_fence();
 
   // producer: lane l moves 16 B per instruction; three instructions fill one slot
@@ -372,24 +264,10 @@ __device__ FwdOut lq_forward_wave_ring(const LQParams& P, int b0, int B, int T, 
       p2 = reinterpret_cast<const char*>(u + tr(m / 2) * T * NU + 2 * (m % 2));
       s2 = NU * 8;
     }
-#if ILQR_FW_ABLATE & 16  // probe only: every step reads step 0's K rows (cache)
-    s1 = 0;
-    if (l < 32) s2 = 0;
-#endif
-#if ILQR_FW_ABLATE & 8  // probe only: x / u / x_traj reads served from the K rows (cache)
-    if (l >= 32) {
-      p2 = reinterpret_cast<const char*>(Kg + tr(0) * T * NU * NX + 2 * (l % 24));
-      s2 = NU * NX * 8;
-    }
-#endif
     const int l3 = l & 31;
     if (l3 < 24) {
       p3 = reinterpret_cast<const char*>(xt0 + tr(l3 / 6) * (T + 1) * NX + 2 * (l3 % 6));
       s3 = NX * 8;
-#if ILQR_FW_ABLATE & 8
-      p3 = reinterpret_cast<const char*>(Kg + tr(0) * T * NU * NX + 2 * (l3 % 24));
-      s3 = NU * NX * 8;
-#endif
     } else {
       const int m = l3 - 24;
       p3 = reinterpret_cast<const char*>(dg + tr(m / 2) * T * NU + 2 * (m % 2));
@@ -467,31 +345,17 @@ __device__ FwdOut lq_forward_wave_ring(const LQParams& P, int b0, int B, int T, 
     auto step = [&](int t, auto next_wait) {
       // x̄ₖ₊₁ = A x̄ₖ + B ūₖ: the A part (broadcasts from the x lanes) does not need ūₖ
       Acc4 xa;
-#if ILQR_FW_LDS_BCAST
-      lds_acc16_head(rbx, xa, xb, Fr);
-#else
       dpp_acc16_head(xa, xb, Fr);
-#endif
       // δx = x̄ₖ − xₖ (:72); ūₖ = uₖ + α δuₖ + Kₖ δx (:73)
       const double dx = is_x ? xb - cur.a : 0.0;
-#if ILQR_FW_ABLATE & 4  // probe only: no K δx product (the c-form's saving)
-      const double kdx = dx;
-#elif ILQR_FW_LDS_BCAST
-      const double kdx = lds_dot12(rbd, dx, cur.Kr);
-#else
       const double kdx = dpp_dot12(dx, cur.Kr);
-#endif
       const double ua = fma(alpha, cur.bq, cur.a);
       const double ub = ua + kdx;
       if constexpr (CAND) eo = eo && (is_x || ua == cur.a);
       const double z = is_x ? xb : ub;
       const double v = is_x ? fma(-xtw, cur.bq, xb) : ub;
       const double e = is_x ? 0.0 : ub - cur.a;
-#if ILQR_FW_LDS_BCAST
-      lds_acc16_tail(rbu, xa, ub, Fr);  // the B part: broadcasts from the u lanes
-#else
       dpp_acc16_tail(xa, ub, Fr);  // the B part: broadcasts from the u lanes
-#endif
       produce(t + PF);  // slot (t+PF)%R was last read at step t+PF−R < t
       double Lr[NX];  // Q row (x lanes); R row in slots 0..NU-1 (u lanes), rest unused
       if constexpr (LR_REGS) {
@@ -506,19 +370,10 @@ __device__ FwdOut lq_forward_wave_ring(const LQParams& P, int b0, int B, int T, 
           Lr[2 * k + 1] = q.y;
         }
       }
-#if ILQR_FW_ABLATE & 1  // probe only (tools/fw_alt.sh): no cost row
-      const double lv = Lr[0];
-#elif ILQR_FW_LDS_BCAST
-      const double lv = lds_dot16_bd(rbv, v, Lr, is_x);
-#else
       const double lv = dpp_dot16_bd(v, Lr);
-#endif
       cost = fma(v, lv, cost);
-#if ILQR_FW_ABLATE & 2  // probe only: no result stores
-      if (t < 0)
-#endif
-      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, z), rXN, ox, (uint32_t)t * NX * 8, ILQR_FW_ST_AUX);
-      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, z), rUN, ou, (uint32_t)t * NU * 8, ILQR_FW_ST_AUX);
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, z), rXN, ox, (uint32_t)t * NX * 8, 0);
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, z), rUN, ou, (uint32_t)t * NU * 8, 0);
       du2 = fma(e, e, du2);
       xb = xa.sum();
       // slot t + 1 (past the horizon: a clamped step's slot, read and never used)
@@ -528,7 +383,7 @@ __device__ FwdOut lq_forward_wave_ring(const LQParams& P, int b0, int B, int T, 
     const int tp = T < PF ? T : PF;
     for (int t = 0; t < tp - 1; ++t) step(t, std::integral_constant<int, N_PRO>{});
     for (int t = tp - 1; t < T; ++t) step(t, std::integral_constant<int, N_SS>{});
-    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, xb), rXN, ox, (uint32_t)T * NX * 8, ILQR_FW_ST_AUX);
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, xb), rXN, ox, (uint32_t)T * NX * 8, 0);
     // Qf row (x lanes; u lanes read row 0 and zero it): one base address, 6 × 16 B
     const double2* qrow = reinterpret_cast<const double2*>(Qfb + jx * NX);
     asm volatile("" : "+v"(qrow));  // keep the row address from being hoisted as 12 pointers
@@ -740,8 +595,8 @@ __device__ FwdOut lq_forward_wave_mfma(const LQParams& P, int b0, int B, int T, 
 #pragma unroll
       for (int I = 0; I < 3; ++I)
         __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, xb[I]), rXN, ox,
-                                              (uint32_t)(t * NX * 8 + 32 * I), ILQR_FW_ST_AUX);
-      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, ub), rUN, ou, (uint32_t)t * NU * 8, ILQR_FW_ST_AUX);
+                                              (uint32_t)(t * NX * 8 + 32 * I), 0);
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, ub), rUN, ou, (uint32_t)t * NU * 8, 0);
       const double e = ub - uk;
       du2 = fma(e, e, du2);
       // x̄ₖ₊₁ = A x̄ₖ + B ūₖ (:74)
@@ -757,7 +612,7 @@ __device__ FwdOut lq_forward_wave_mfma(const LQParams& P, int b0, int B, int T, 
 #pragma unroll
     for (int I = 0; I < 3; ++I)
       __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, xb[I]), rXN, ox,
-                                            (uint32_t)(T * NX * 8 + 32 * I), ILQR_FW_ST_AUX);
+                                            (uint32_t)(T * NX * 8 + 32 * I), 0);
     // final_cost(x̄_N) = x̄ᵀQf x̄ on the raw state (:192)
     {
       const double* Qfb = P.Qf + (size_t)bb * NX * NX;

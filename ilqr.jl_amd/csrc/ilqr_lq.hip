@@ -39,157 +39,16 @@
 namespace ilqr {
 namespace {
 
-// VALU replacement of the Y = Sp·F and Z = L + FᵀY MFMAs:
-// on gfx950 f64 VALU FMAs with a DPP64 row broadcast sustain 58 TF/s at 4 waves/SIMD
-// against 42 TF/s for v_mfma_f64_16x16x4 (profiles/r01/ubench_{f64,dpp}.log).
-// y[r] += Σ_k bcast_k(s[r]) · f[k]: lane (q, c) holds Sp[q+4r][c] in s[r] and
-// F[k][c] in f[k], so y[r] = (Sp F)[q+4r][c] — the MFMA accumulator layout.
-// The leading s_nops give the f64 MFMA that produced s[] its VALU-read wait states.
-[[maybe_unused]] __device__ __forceinline__ void dpp_sf4(double& y0, double& y1, double& y2, double& y3, double s0,
-                                        double s1, double s2, double s3, const double (&f)[12]) {
-  asm volatile(
-      "s_nop 7\n\t"
-      "s_nop 7\n\t"
-      "s_nop 4\n\t"
-      "v_fmac_f64_dpp %[y0], %[s0], %[f0] row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[y1], %[s1], %[f0] row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[y2], %[s2], %[f0] row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[y3], %[s3], %[f0] row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[y0], %[s0], %[f1] row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[y1], %[s1], %[f1] row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[y2], %[s2], %[f1] row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[y3], %[s3], %[f1] row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[y0], %[s0], %[f2] row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[y1], %[s1], %[f2] row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[y2], %[s2], %[f2] row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[y3], %[s3], %[f2] row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[y0], %[s0], %[f3] row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[y1], %[s1], %[f3] row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[y2], %[s2], %[f3] row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[y3], %[s3], %[f3] row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[y0], %[s0], %[f4] row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[y1], %[s1], %[f4] row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[y2], %[s2], %[f4] row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[y3], %[s3], %[f4] row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[y0], %[s0], %[f5] row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[y1], %[s1], %[f5] row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[y2], %[s2], %[f5] row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[y3], %[s3], %[f5] row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[y0], %[s0], %[f6] row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[y1], %[s1], %[f6] row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[y2], %[s2], %[f6] row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[y3], %[s3], %[f6] row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[y0], %[s0], %[f7] row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[y1], %[s1], %[f7] row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[y2], %[s2], %[f7] row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[y3], %[s3], %[f7] row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[y0], %[s0], %[f8] row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[y1], %[s1], %[f8] row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[y2], %[s2], %[f8] row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[y3], %[s3], %[f8] row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[y0], %[s0], %[f9] row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[y1], %[s1], %[f9] row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[y2], %[s2], %[f9] row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[y3], %[s3], %[f9] row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[y0], %[s0], %[f10] row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[y1], %[s1], %[f10] row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[y2], %[s2], %[f10] row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[y3], %[s3], %[f10] row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[y0], %[s0], %[f11] row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[y1], %[s1], %[f11] row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[y2], %[s2], %[f11] row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[y3], %[s3], %[f11] row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
-      : [y0] "+v"(y0), [y1] "+v"(y1), [y2] "+v"(y2), [y3] "+v"(y3)
-      : [s0] "v"(s0), [s1] "v"(s1), [s2] "v"(s2), [s3] "v"(s3), [f0] "v"(f[0]), [f1] "v"(f[1]), [f2] "v"(f[2]), [f3] "v"(f[3]), [f4] "v"(f[4]), [f5] "v"(f[5]), [f6] "v"(f[6]), [f7] "v"(f[7]), [f8] "v"(f[8]), [f9] "v"(f[9]), [f10] "v"(f[10]), [f11] "v"(f[11]));
-}
-// z[r] += Σ_k bcast_{4r}(p[k]) · f[k] where lane (q, m) holds column (m + q) mod 16 of Y
-// in p[] (so lane 4r of row q holds column q + 4r) and F[k][c] in f[k]:
-// z[r] = (FᵀY)[c][q+4r] = Z[q+4r][c] by the symmetry of Z = FᵀSF (rounding aside).
-[[maybe_unused]] __device__ __forceinline__ void dpp_fy4(double& z0, double& z1, double& z2, double& z3,
-                                        const double (&p)[12], const double (&f)[12]) {
-  asm volatile(
-      "s_nop 4\n\t"
-      "v_fmac_f64_dpp %[z0], %[p0], %[f0] row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[z1], %[p0], %[f0] row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[z2], %[p0], %[f0] row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[z3], %[p0], %[f0] row_newbcast:12 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[z0], %[p1], %[f1] row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[z1], %[p1], %[f1] row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[z2], %[p1], %[f1] row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[z3], %[p1], %[f1] row_newbcast:12 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[z0], %[p2], %[f2] row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[z1], %[p2], %[f2] row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[z2], %[p2], %[f2] row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[z3], %[p2], %[f2] row_newbcast:12 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[z0], %[p3], %[f3] row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[z1], %[p3], %[f3] row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[z2], %[p3], %[f3] row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[z3], %[p3], %[f3] row_newbcast:12 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[z0], %[p4], %[f4] row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[z1], %[p4], %[f4] row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[z2], %[p4], %[f4] row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[z3], %[p4], %[f4] row_newbcast:12 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[z0], %[p5], %[f5] row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[z1], %[p5], %[f5] row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[z2], %[p5], %[f5] row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[z3], %[p5], %[f5] row_newbcast:12 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[z0], %[p6], %[f6] row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[z1], %[p6], %[f6] row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[z2], %[p6], %[f6] row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[z3], %[p6], %[f6] row_newbcast:12 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[z0], %[p7], %[f7] row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[z1], %[p7], %[f7] row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[z2], %[p7], %[f7] row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[z3], %[p7], %[f7] row_newbcast:12 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[z0], %[p8], %[f8] row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[z1], %[p8], %[f8] row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[z2], %[p8], %[f8] row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[z3], %[p8], %[f8] row_newbcast:12 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[z0], %[p9], %[f9] row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[z1], %[p9], %[f9] row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[z2], %[p9], %[f9] row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[z3], %[p9], %[f9] row_newbcast:12 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[z0], %[p10], %[f10] row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[z1], %[p10], %[f10] row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[z2], %[p10], %[f10] row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[z3], %[p10], %[f10] row_newbcast:12 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[z0], %[p11], %[f11] row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[z1], %[p11], %[f11] row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[z2], %[p11], %[f11] row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[z3], %[p11], %[f11] row_newbcast:12 row_mask:0xf bank_mask:0xf\n\t"
-      : [z0] "+v"(z0), [z1] "+v"(z1), [z2] "+v"(z2), [z3] "+v"(z3)
-      : [p0] "v"(p[0]), [p1] "v"(p[1]), [p2] "v"(p[2]), [p3] "v"(p[3]), [p4] "v"(p[4]), [p5] "v"(p[5]), [p6] "v"(p[6]), [p7] "v"(p[7]), [p8] "v"(p[8]), [p9] "v"(p[9]), [p10] "v"(p[10]), [p11] "v"(p[11]), [f0] "v"(f[0]), [f1] "v"(f[1]), [f2] "v"(f[2]), [f3] "v"(f[3]), [f4] "v"(f[4]), [f5] "v"(f[5]), [f6] "v"(f[6]), [f7] "v"(f[7]), [f8] "v"(f[8]), [f9] "v"(f[9]), [f10] "v"(f[10]), [f11] "v"(f[11]));
-}
-
-// Σ_j<4 bcast_j(src)·c[j]: src broadcast from lane j of each 16-lane row, two
-// accumulators. `s_nop 4` covers the VALU→DPP read hazard.
-[[maybe_unused]] __device__ __forceinline__ double dpp_dot4(double src, double c0, double c1, double c2, double c3) {
-  double a0 = 0.0, a1 = 0.0;
-  asm("s_nop 4\n\t"
-      "v_fmac_f64_dpp %[a0], %[s], %[c0] row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[a1], %[s], %[c1] row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[a0], %[s], %[c2] row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[a1], %[s], %[c3] row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
-      : [a0] "+v"(a0), [a1] "+v"(a1)
-      : [s] "v"(src), [c0] "v"(c0), [c1] "v"(c1), [c2] "v"(c2), [c3] "v"(c3));
-  return a0 + a1;
-}
-
 // ---------------------------------------------------------------------------
 // Backward pass of one trajectory by one wave (backward_pass.jl:324-357).
 // Writes d (T,NU) and K (T,NU,NX) of trajectory b. Returns true if any gain is NaN
 // (the reference's @assert !any(isnan, δu/K), :353-354).
 // ---------------------------------------------------------------------------
-// ABL: ablation bits for tools/ablate_bw.hip only (0 in the product): 1 skip the
-// factor/solve, 2 skip symmetrisation, 4 skip the LDS hand-off, 8 skip gain stores,
-// 16 skip the gradient reduction (ablated variants compute wrong gains); variant
-// bits (correct gains): 32 two Newton steps per reciprocal (product: one), 64
-// symmetrise every SYM_EVERY/2 steps, 128 Schur-complement 2×2-block solve instead
-// of LDLᵀ (NU = 4), 256 round-1 gradient (one 4-lane reduction of Lz + Fᵀs after
-// the MFMAs), 512 round-1 gain stores (exec-masked branch), 2048 the gain solve by
-// cofactors spread over the lanes (COF) instead of the redundant LDLᵀ per lane,
-// 8192 COF without its refinement step.
-template <int NX, int NU, int ABL = 0>
+// (Measured variants — Y/Z on the VALU, a Schur-complement or cofactor gain solve, two
+// Newton steps per reciprocal, other symmetrisation periods, the round-1 gradient and
+// gain stores — and tools/ablate_bw.hip's ablation bits live in
+// tools/ablation/restore_alternates.patch)
+template <int NX, int NU>
 __device__ bool lq_backward_wave(const LQParams& P, int b, int T, const double* __restrict__ x,
                                  const double* __restrict__ u, double* __restrict__ d_out,
                                  double* __restrict__ K_out, double mu, double* lds) {
@@ -222,22 +81,6 @@ __device__ bool lq_backward_wave(const LQParams& P, int b, int T, const double* 
     const double bb = ldz(ri && cu, Bb + ii * NU + cj, Bb);
     fB[kk] = a + bb;
   }
-  // VYZ (ABL bit 1024): the Y and Z products on the VALU (dpp_sf4 / dpp_fy4); this
-  // lane keeps its whole column of F, Fo[k] = F[k][c]
-  constexpr bool VYZ = (ABL & 1024) != 0;
-  // VY (ABL bit 4096): only Y = Sp·F on the VALU (row-local: lane (q, k) holds
-  // Sp[q+4r][k]), Z = L + FᵀY stays on the MFMA, reading Y as its B operand
-  constexpr bool VY = (ABL & 4096) != 0 && !VYZ;
-  static_assert(!(VYZ || VY) || NX == 12, "dpp_sf4/dpp_fy4 are written for nx = 12");
-  double Fo[(VYZ || VY) ? NX : 1];
-  if constexpr (VYZ || VY) {
-#pragma unroll
-    for (int k = 0; k < NX; ++k) {
-      const double a = ldz(cx, Ab + k * NX + ci, Ab);
-      const double bb = ldz(cu, Bb + k * NU + cj, Bb);
-      Fo[k] = a + bb;
-    }
-  }
   // Cost Hessian L = blockdiag(Q+Qᵀ, R+Rᵀ) in accumulator layout: Lc[r] = L[q+4r][c]
   // (immediate_cost_quadratization :101-106 of ℓ = xᵀQx + uᵀRu: 𝐐 = Q+Qᵀ, 𝐑 = R+Rᵀ, 𝐏 = 0)
   d4 Lc;
@@ -264,31 +107,6 @@ __device__ bool lq_backward_wave(const LQParams& P, int b, int T, const double* 
   int qv_at[KS];
 #pragma unroll
   for (int r = 0; r < KS; ++r) qv_at[r] = (c == SROW && q + 4 * r < NX) ? 64 + q + 4 * r : ZERO;
-  // COF: lane (q, c) forms the cofactor C[q][c&3] of H_reg = H + μI (stored in LDS
-  // with μ on its diagonal) from the 3×3 minor without row q and column c&3, read
-  // from the lower triangle; row q of H_reg feeds the determinant.
-  constexpr bool COF = NU == 4 && (ABL & 2048) != 0;  // ablation variant
-  int m_at[COF ? 9 : 1], hrow_at[COF ? 4 : 1];
-  double csign = 1.0;
-  if constexpr (COF) {
-    const int bq = c & 3;
-    int rr[3], cc[3];
-#pragma unroll
-    for (int k = 0, n = 0; k < 4; ++k)
-      if (k != q) rr[n++] = k;
-#pragma unroll
-    for (int k = 0, n = 0; k < 4; ++k)
-      if (k != bq) cc[n++] = k;
-    auto at = [](int i, int j) { return (i > j ? i : j) * 16 + NX + (i > j ? j : i); };
-#pragma unroll
-    for (int i = 0; i < 3; ++i)
-#pragma unroll
-      for (int j = 0; j < 3; ++j) m_at[3 * i + j] = at(rr[i], cc[j]);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) hrow_at[j] = at(q, j);
-    csign = ((q + bq) & 1) ? -1.0 : 1.0;
-  }
-
   // Terminal value function (final_cost_quadratization :134-153, ℓ_f = xᵀQf x):
   // S = Qf+Qfᵀ, s = (Qf+Qfᵀ) x_N.
   const double* xN = x + ((size_t)b * (T + 1) + T) * NX;
@@ -347,176 +165,52 @@ __device__ bool lq_backward_wave(const LQParams& P, int b, int T, const double* 
     // Z = L + Fᵀ Y = [[lxx + AᵀSA, AᵀSB], [BᵀSA, luu + BᵀSB]]  (:182-183, first terms of :270)
     d4 Y = {0.0, 0.0, 0.0, 0.0};
     d4 Z = Lc;
-    if constexpr (VYZ) {
-      double y0 = 0.0, y1 = 0.0, y2 = 0.0, y3 = 0.0;
-      dpp_sf4(y0, y1, y2, y3, Sp[0], Sp[1], Sp[2], Sp[3], Fo);
-      Y = d4{y0, y1, y2, y3};
-      // all-gather Y's columns through LDS: column-major, stride 14 (16-B aligned rows
-      // 0..12 + one junk slot taking the nonexistent rows 13..15)
-      double* yt = lds + YT_OFF;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int i = q + 4 * r;
-        yt[c * 14 + (i <= SROW ? i : 13)] = Y[r];
-      }
-      wave_lds_fence();
-      const double2* col = reinterpret_cast<const double2*>(yt + ((c + q) & 15) * 14);
-      double Yp[NX];
+    for (int kk = 0; kk < KS; ++kk) Y = mfma(Sp[kk], fB[kk], Y);
 #pragma unroll
-      for (int k = 0; k < NX / 2; ++k) {
-        const double2 v = col[k];
-        Yp[2 * k] = v.x;
-        Yp[2 * k + 1] = v.y;
-      }
-      double z0 = Lc[0], z1 = Lc[1], z2 = Lc[2], z3 = Lc[3];
-      dpp_fy4(z0, z1, z2, z3, Yp, Fo);
-      Z = d4{z0, z1, z2, z3};
-    } else if constexpr (VY) {
-      double y0 = 0.0, y1 = 0.0, y2 = 0.0, y3 = 0.0;
-      dpp_sf4(y0, y1, y2, y3, Sp[0], Sp[1], Sp[2], Sp[3], Fo);
-      asm volatile("s_nop 4" ::: );  // VALU write → MFMA operand read
-      Y = d4{y0, y1, y2, y3};
-#pragma unroll
-      for (int kk = 0; kk < KS; ++kk) Z = mfma(fB[kk], Y[kk], Z);
-    } else {
-#pragma unroll
-      for (int kk = 0; kk < KS; ++kk) Y = mfma(Sp[kk], fB[kk], Y);
-#pragma unroll
-      for (int kk = 0; kk < KS; ++kk) Z = mfma(fB[kk], Y[kk], Z);
-    }
+    for (int kk = 0; kk < KS; ++kk) Z = mfma(fB[kk], Y[kk], Z);
 
     // gq[c] = (L z)[c] + (Fᵀ s)[c]: lx + Aᵀs (c < NX), g = lu + Bᵀs (c ≥ NX)  (:181, :269).
     // (L z)[c] does not depend on the recursion: its 4-lane reduction overlaps the
     // MFMAs; (Fᵀ s)[c] = Y[SROW][c] sits in lane q = SROW%4 only, which alone
     // publishes g (the other lanes write a junk LDS row), so no reduction waits on Y.
-    double gq;
-    if constexpr ((ABL & 256) != 0) {
-      double part = 0.0;
+    double part = 0.0;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        part = fma(Lc[r], zc[r], part);
-        if (r == SROW / 4) part += (q == SROW % 4) ? Y[r] : 0.0;
-      }
-      gq = (ABL & 16) ? part : colsum4(part);
-    } else {
-      double part = 0.0;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) part = fma(Lc[r], zc[r], part);
-      gq = ((ABL & 16) ? part : colsum4(part)) + Y[SROW / 4];  // exact in lane q = SROW%4
-    }
+    for (int r = 0; r < 4; ++r) part = fma(Lc[r], zc[r], part);
+    const double gq = colsum4(part) + Y[SROW / 4];  // exact in lane q = SROW%4
 
     // hand the NU rows [G | H] and g to every lane
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int i = q + 4 * r;
-      if (i >= NX && i < NX + NU) Gl[(i - NX) * 16 + c] = COF && c == i ? Z[r] + mu : Z[r];
+      if (i >= NX && i < NX + NU) Gl[(i - NX) * 16 + c] = Z[r];
     }
-    if constexpr ((ABL & 256) != 0)
-      gl[c] = gq;  // the four lanes of column c hold the same value
-    else
-      lds[(q == SROW % 4) ? 64 + c : JUNK + l] = gq;
+    lds[(q == SROW % 4) ? 64 + c : JUNK + l] = gq;
     double h[NU][NU];
-    double mn[COF ? 9 : 1], hr[COF ? 4 : 1];
     d4 col = {0.0, 0.0, 0.0, 0.0};
-    double colq;
     double qv[KS];
-    if constexpr ((ABL & 4) != 0) {
+    wave_lds_fence();
 #pragma unroll
-      for (int i = 0; i < NU; ++i)
+    for (int i = 0; i < NU; ++i)
 #pragma unroll
-        for (int k = 0; k <= i; ++k) h[i][k] = Z[(i + k) & 3] + (i == k ? 10.0 : 0.0);
+      for (int k = 0; k <= i; ++k) h[i][k] = Gl[i * 16 + NX + k];
 #pragma unroll
-      for (int j = 0; j < NU; ++j) col[j] = Z[j] * gq;
-      colq = Z[3];
+    for (int j = 0; j < NU; ++j) col[j] = lds[col_at[j]];     // [G | g][j][c], 0 for c > NX
+    const double colq = lds[colq_at];                         // [G | g][q][c]
 #pragma unroll
-      for (int r = 0; r < KS; ++r) qv[r] = gq;
-    } else {
-      wave_lds_fence();
-      if constexpr (COF) {
-#pragma unroll
-        for (int k = 0; k < 9; ++k) mn[k] = lds[m_at[k]];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) hr[j] = lds[hrow_at[j]];
-      } else {
-#pragma unroll
-        for (int i = 0; i < NU; ++i)
-#pragma unroll
-          for (int k = 0; k <= i; ++k) h[i][k] = Gl[i * 16 + NX + k];
-      }
-#pragma unroll
-      for (int j = 0; j < NU; ++j) col[j] = lds[col_at[j]];     // [G | g][j][c], 0 for c > NX
-      colq = lds[colq_at];                                      // [G | g][q][c]
-#pragma unroll
-      for (int r = 0; r < KS; ++r) qv[r] = lds[qv_at[r]];       // (lx + Aᵀs)[q+4r] in column NX
-      wave_lds_fence();
-    }
+    for (int r = 0; r < KS; ++r) qv[r] = lds[qv_at[r]];       // (lx + Aᵀs)[q+4r] in column NX
+    wave_lds_fence();
 
     // feedback_parameters (:207-218): K_aug[:,c] = -(H + μI)⁻¹ [G | g][:,c]
-    double sol;  // ((H + μI)⁻¹ [G | g])[q][c]
-    if constexpr ((ABL & 1) != 0) {
-      asm volatile("" ::"v"(h[0][0]), "v"(h[1][0]), "v"(h[2][1]), "v"(h[3][3]));
-      sol = col[qq] * 1e-3;
-    } else if constexpr (COF) {
-      // C[q][c&3] = ±det(minor), det(H_reg) by row q's expansion (lane (q, j) holds
-      // C[q][j]), (H_reg)⁻¹[q][j] = C[q][j] / det (symmetric), then the row times
-      // [G | g][:, c] with the inverse row broadcast from lanes (q, 0..3)
-      double t0 = mn[4] * mn[8];
-      t0 = fma(-mn[5], mn[7], t0);
-      double t1 = mn[3] * mn[8];
-      t1 = fma(-mn[5], mn[6], t1);
-      double t2 = mn[3] * mn[7];
-      t2 = fma(-mn[4], mn[6], t2);
-      double cf = mn[0] * t0;
-      cf = fma(-mn[1], t1, cf);
-      cf = fma(mn[2], t2, cf);
-      cf *= csign;
-      const double det = dpp_dot4(cf, hr[0], hr[1], hr[2], hr[3]);
-      const double hinv = cf * rcp<(ABL & 32) ? 2 : 1>(det);
-      sol = dpp_dot4(hinv, col[0], col[1], col[2], col[3]);
-      if constexpr ((ABL & 8192) == 0) {
-        // one step of iterative refinement: cofactors of a near-rank-1 H lose ~2
-        // digits (3e-12 per step against 5e-14 for LDLᵀ on the quadrotor H, which
-        // the recursion amplifies); r = [G|g] − H_reg·sol, sol += (H_reg)⁻¹ r. The
-        // columns of sol and r cross rows, so they go through LDS (column-major,
-        // the symmetrisation tile, free at this point of the step)
-        double* xc = lds + 96;
-        xc[c * 4 + q] = sol;
-        wave_lds_fence();
-        const double2 s01 = reinterpret_cast<const double2*>(xc + c * 4)[0];
-        const double2 s23 = reinterpret_cast<const double2*>(xc + c * 4)[1];
-        double r = colq;
-        r = fma(-hr[0], s01.x, r);
-        r = fma(-hr[1], s01.y, r);
-        r = fma(-hr[2], s23.x, r);
-        r = fma(-hr[3], s23.y, r);
-        xc[64 + c * 4 + q] = r;
-        wave_lds_fence();
-        const double2 r01 = reinterpret_cast<const double2*>(xc + 64 + c * 4)[0];
-        const double2 r23 = reinterpret_cast<const double2*>(xc + 64 + c * 4)[1];
-        sol += dpp_dot4(hinv, r01.x, r01.y, r23.x, r23.y);
-        wave_lds_fence();
-      }
-    } else if constexpr ((ABL & 128) != 0 && NU == 4) {
-      Schur4 f;
-      f.factor<(ABL & 32) ? 2 : 1>(h, mu);
-      sol = f.solve(col)[qq];
-    } else {
-      LDLT<NU, (ABL & 32) ? 2 : 1> f;
-      f.factor(h, mu);
-      sol = f.solve(col)[qq];
-    }
+    LDLT<NU, 1> f;
+    f.factor(h, mu);
+    const double sol = f.solve(col)[qq];  // ((H + μI)⁻¹ [G | g])[q][c]
     const double kq = (q < NU) ? -sol : 0.0;              // K_aug[q][c]
     const double wk = (q < NU) ? fma(mu, kq, -colq) : 0.0;   // ((H + 2μI) K_aug)[q][c]
     nan |= __builtin_isnan(kq);
 
-    if constexpr ((ABL & 8) != 0) {
-    } else if constexpr ((ABL & 512) != 0) {
-      double* dst = cx ? Kb + ((size_t)t * NU + qq) * NX + c : db + (size_t)t * NU + qq;
-      if (q < NU && c <= SROW) *dst = kq;
-    } else {
-      store_or_drop(kq, rK, q < NU && cx, (uint32_t)(((t * NU + qq) * NX + ci) * 8));
-      store_or_drop(kq, rD, q < NU && c == SROW, (uint32_t)((t * NU + qq) * 8));
-    }
+    store_or_drop(kq, rK, q < NU && cx, (uint32_t)(((t * NU + qq) * NX + ci) * 8));
+    store_or_drop(kq, rD, q < NU && c == SROW, (uint32_t)((t * NU + qq) * 8));
 
     // step_back (:269-270): Sp ← [Qxx | lx + Aᵀs] − K_augᵀ (H + 2μI) K_aug
     d4 Cin;
@@ -533,7 +227,7 @@ __device__ bool lq_backward_wave(const LQParams& P, int b, int T, const double* 
     // accumulator tile feeds the next Y MFMA as its own transpose, so rounding
     // asymmetry E evolves as E ← −AᵀEA and grows like ρ(A)^2t on unstable A;
     // a periodic projection bounds it at negligible cost.
-    if ((ABL & 2) == 0 && (t % ((ABL & 64) ? SYM_EVERY / 2 : SYM_EVERY)) == 0) {
+    if ((t % SYM_EVERY) == 0) {
       double* tile = lds + 96;  // 16 × 17 (padded) doubles
 #pragma unroll
       for (int r = 0; r < 4; ++r) tile[(q + 4 * r) * 17 + c] = Sp[r];
@@ -796,10 +490,7 @@ __host__ __device__ __forceinline__ bool pipe_role_a(int g) { return (((g >> 8) 
 // Four waves per workgroup, each with its own ring (116 KB of LDS: one workgroup per
 // CU, one wave per SIMD); one-wave workgroups let the dispatcher pack two waves onto a
 // SIMD (the fused kernel).
-#ifndef ILQR_FW_WAVES
-#define ILQR_FW_WAVES 4
-#endif
-constexpr int FW_WAVES = ILQR_FW_WAVES;
+constexpr int FW_WAVES = 4;
 template <int NX, int NU, bool MF = false>
 __global__ __launch_bounds__(64 * FW_WAVES) void lq_forward_ring_kernel(
     LQParams P, int B, int T, const double* __restrict__ x, const double* __restrict__ u,

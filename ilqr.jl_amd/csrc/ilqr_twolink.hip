@@ -428,11 +428,7 @@ __device__ unsigned tl_backward4_wave(const TwoLinkParams& P, int b0, int B, uns
 //    0.2 ulp); a rollout that meets a larger h is redone on rk4<double>.
 // Mathematically the reference's dynamicsf (2_link_helper_functions.jl:49-79); the
 // rounding differs from rk4<double>'s by a few ulp per step (tests/test_gpu_twolink.py).
-// ILQR_TL_RK4_SHIFT=0 builds the forward on rk4<double> instead (tools/tl_fw_probe.hip).
 // ---------------------------------------------------------------------------
-#ifndef ILQR_TL_RK4_SHIFT
-#define ILQR_TL_RK4_SHIFT 1
-#endif
 
 struct TLRoll {
   double alpha, beta, delta, beta2, det0, bsq, dt;
@@ -516,7 +512,7 @@ template <int NU_>
 struct TwoLinkModel {
   using V = double;
   static constexpr int NU = NU_;
-  static constexpr bool HAS_FAST = ILQR_TL_RK4_SHIFT != 0;
+  static constexpr bool HAS_FAST = true;
   TwoLinkParams P;
   TLRoll R;
   __device__ __forceinline__ void rk4_fast(const double (&x)[4], const double (&u)[NU], double (&o)[4],

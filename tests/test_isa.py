@@ -69,7 +69,7 @@ def test_headline_kernels_have_no_waterfall_loops_or_scratch(tmp_path):
     # the default (row-form forward) fused iteration, the fit's backward leg and the
     # ilqr_backward kernel
     checked = [n for n in funcs if re.search(r"lq_iter_fused4_kernelILb0E|lq_iter_backward4_kernel|"
-                                             r"lq_backward4_kernelILi0E", n)]
+                                             r"lq_backward4_kernelE", n)]
     assert len(checked) == 3, sorted(funcs)
     for n in checked:
         body = funcs[n]

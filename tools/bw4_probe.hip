@@ -1,3 +1,5 @@
+// (Round 3: the ABL bits / -DILQR_* switches this probe uses exist only in the tree
+// tools/ablation/restore_tree.sh restores; build it there.)
 // Probe for the four-trajectories-per-wave backward (not part of the product):
 // times lq_backward4_kernel against the one-trajectory-per-wave lq_backward_kernel
 // at B=4096, T=100 (random stable LQ problems, as tools/ablate_bw.hip) and reports

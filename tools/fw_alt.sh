@@ -1,4 +1,6 @@
 #!/bin/bash
+# (Round 3: the -DILQR_* switches below exist only in the restored tree: run this from
+# the directory tools/ablation/restore_tree.sh makes.)
 # Alternate builds of libilqr_hip.so with flags on BOTH files that hold the ring
 # forward (ilqr_lq.hip: the split schedule's forward; ilqr_bw4.hip: the fused
 # iteration), for A/B timing with tools/fused_probe.py <lib> / tools/gpu_bwab.sh:
