@@ -44,6 +44,9 @@ case $WHAT in
   rcp) step rcp 60 ./tools/rcp_test ;;
   fit5) step tail_probe 200 python tools/tail_probe.py
         step rocprof_fit5 200 rocprofv3 --kernel-trace -d gpurun_out/prof_fit5 -o run --output-format csv -- python tools/fit5_trace.py ;;
+  tailcap) MODES=coop MAXT=16 step tail_cap16 200 python tools/tail_probe.py
+           MODES=coop MAXT=32 step tail_cap32 200 python tools/tail_probe.py
+           MODES=coop MAXT=64 step tail_cap64 200 python tools/tail_probe.py ;;
   ubench) step ubench 120 ./tools/ubench_f64 ;;
 esac
 done

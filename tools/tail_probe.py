@@ -9,13 +9,15 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "ilqr.jl_amd")]
 from ilqr_amd import _lib
 from ilqr_amd.problems import quadrotor_batch
 from ilqr_amd.solver import Solver
+if os.environ.get("ILQR_LIB"):  # A/B against another build of the library
+    _lib._lib = _lib.load(os.environ["ILQR_LIB"])
 
 B, T, N = 4096, 100, int(os.environ.get("ITERS", 6))
 lq, x0, u0 = quadrotor_batch(B, T=T, seed0=0)
 s = Solver(12, 4, T, B)
 s.set_problem(lq)
 s._bind_stream()
-o = _lib.default_options(tol=-1.0)
+o = _lib.default_options(tol=-1.0, max_trials=int(os.environ.get("MAXT", 64)))
 
 def run(seq, reps=5):
     s.set_schedule(sequential_search=seq)
@@ -36,7 +38,9 @@ def run(seq, reps=5):
             times[r, it] = e0.elapsed_time(e1) * 1000
             t = tr.cpu().numpy(); stn = st.cpu().numpy()
             ran = t > 0
-            stats.append((int((t > 1).sum()), int((stn == _lib.TRAJ_LS_EXHAUSTED).sum()), float(t.mean())))
+            srch = t[t > 1]
+            q = np.percentile(srch, [50, 90, 100]).astype(int).tolist() if srch.size else []
+            stats.append((int((t > 1).sum()), int((stn == _lib.TRAJ_LS_EXHAUSTED).sum()), float(t.mean()), q))
             keep = st != _lib.TRAJ_OK
             xn[keep] = xi[keep]; un[keep] = ui[keep]
             tr.zero_()
@@ -46,7 +50,10 @@ def run(seq, reps=5):
           f"{med.sum():.0f}", flush=True)
     return stats
 
+MODES = os.environ.get("MODES", "seq,coop").split(",")
 for _ in range(2):
-    st = run(True)
-    run(False)
-print("per iteration (searches past trial 1, exhausted so far, mean trials):", st)
+    if "seq" in MODES:
+        st = run(True)
+    if "coop" in MODES:
+        st = run(False)
+print("per iteration (searches past trial 1, exhausted so far, mean trials, trials p50/p90/max of the searches):", st)
