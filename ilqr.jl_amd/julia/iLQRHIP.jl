@@ -442,6 +442,61 @@ function solve!(prob::iLQRProblem, devices::Vector{Int}; max_iter::Int64=100, to
     return prob
 end
 
+"""MultiSolver(prob, devices): a device-resident multi-GPU solver for an MPC loop over
+many instances (ilqr_multi_set_problem once: A…Qf stay on their devices; then per call
+only x/u go up and the results come down — ilqr_multi_load / ilqr_multi_fit_resident /
+ilqr_multi_gather). close(ms) frees it."""
+mutable struct MultiSolver
+    ptr::Ptr{Cvoid}
+    nx::Int; nu::Int; M::Int; nb::Int
+end
+
+const ILQR_MULTI_WARM_START = Cint(1)
+
+function MultiSolver(prob::iLQRProblem, devices::Vector{Int})
+    nx, N, nb = size(prob.x); nu = size(prob.u, 1); M = N - 1
+    r = Ref{Ptr{Cvoid}}(C_NULL)
+    check(ccall((:ilqr_multi_create, libilqr), Cint,
+                (Ref{Ptr{Cvoid}}, Ptr{Cint}, Cint, Cint, Cint, Cint, Cint),
+                r, Cint.(devices), length(devices), nx, nu, M, nb), "ilqr_multi_create")
+    ms = MultiSolver(r[], nx, nu, M, nb)
+    A, B, Q, R, Qf = rowmajor3(prob.A), rowmajor3(prob.B), rowmajor3(prob.Q), rowmajor3(prob.R), rowmajor3(prob.Qf)
+    GC.@preserve A B Q R Qf begin
+        p = Ref(Problem(ILQR_PROBLEM_LQ, 0, pointer(A), pointer(B), pointer(Q), pointer(R), pointer(Qf)))
+        check(ccall((:ilqr_multi_set_problem, libilqr), Cint, (Ptr{Cvoid}, Ref{Problem}), ms.ptr, p),
+              "ilqr_multi_set_problem")
+    end
+    return ms
+end
+
+function Base.close(ms::MultiSolver)
+    ms.ptr == C_NULL && return
+    ccall((:ilqr_multi_destroy, libilqr), Cint, (Ptr{Cvoid},), ms.ptr)
+    ms.ptr = C_NULL
+end
+
+"""solve!(ms::MultiSolver, prob; max_iter, tol, warm_start) -> prob: fit every instance
+on the resident problem. warm_start = false uploads prob.x / prob.u first (the usual
+fit from (x_init, u_init)); true starts from the previous call's results, which never
+left the devices. prob.x / prob.u receive the results (ilqr_multi_gather)."""
+function solve!(ms::MultiSolver, prob::iLQRProblem; max_iter::Int64=100, tol::Float64=1e-6,
+                warm_start::Bool=false)
+    size(prob.x) == (ms.nx, ms.M + 1, ms.nb) && size(prob.u) == (ms.nu, ms.M, ms.nb) ||
+        throw(AssertionError("problem shape differs from the MultiSolver's"))
+    if !warm_start
+        check(ccall((:ilqr_multi_load, libilqr), Cint, (Ptr{Cvoid}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}),
+                    ms.ptr, prob.x, prob.u, C_NULL), "ilqr_multi_load")
+    end
+    o = default_options(); o.max_iter = max_iter; o.tol = tol
+    st = ccall((:ilqr_multi_fit_resident, libilqr), Cint, (Ptr{Cvoid}, Ref{Options}, Cint, Ptr{Cvoid}),
+               ms.ptr, o, warm_start ? ILQR_MULTI_WARM_START : Cint(0), C_NULL)
+    st in (ILQR_OK, ILQR_ERR_LS_EXHAUSTED) || check(st, "ilqr_multi_fit_resident")
+    check(ccall((:ilqr_multi_gather, libilqr), Cint,
+                (Ptr{Cvoid}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Int32}, Ptr{Int32}),
+                ms.ptr, prob.x, prob.u, C_NULL, C_NULL, C_NULL), "ilqr_multi_gather")
+    return prob
+end
+
 # -- RBD family (ILQR_PROBLEM_CHAIN): test/RBD_2_link_example with a fixed base --------
 const ILQR_F64 = Int32(0)
 const ILQR_F32 = Int32(1)

@@ -100,7 +100,8 @@ def test_julia_shim_ccalls_declared_symbols():
     src = open(os.path.join(ROOT, "ilqr.jl_amd", "julia", "iLQRHIP.jl")).read()
     called = set(re.findall(r"ccall\(\(:(ilqr_[a-z0-9_]+),\s*libilqr\)", src))
     assert {"ilqr_fit_ex", "ilqr_backward", "ilqr_forward", "ilqr_backward_tiles",
-            "ilqr_chain_fit", "ilqr_chain_set_dynamics"} <= called, called
+            "ilqr_chain_fit", "ilqr_chain_set_dynamics", "ilqr_multi_set_problem", "ilqr_multi_load",
+            "ilqr_multi_fit_resident", "ilqr_multi_gather"} <= called, called
     declared = set(declared_functions())
     assert called <= declared, called - declared
     lib = _lib.load()

@@ -249,3 +249,52 @@ def test_shim_solve_batched(gpu):
         k = int(g["fit_iters"][b])
         assert (trials[b, :k] > 0).all() and (trials[b, k:] == 0).all()
         assert rel(cost[b, :k], g["fit_cost"][b, :k]) < 1e-9
+
+
+@pytest.mark.gpu
+def test_shim_multisolver_resident(gpu):
+    """MultiSolver(prob, devices) + solve!(ms, prob; warm_start): ilqr_multi_set_problem
+    with the (2,1,3)-permuted per-instance matrices (host arrays, once), ilqr_multi_load of
+    the (nx, N, B) trajectories as they are, ilqr_multi_fit_resident, ilqr_multi_gather into
+    the same Julia arrays — two shards on the test box's GPU; equal to the batched fit
+    (solve!) above, and a warm-started second call equals a fit from the first's result."""
+    g = load("dense_t16")
+    nb = g["A"].shape[0]
+    T = g["u"].shape[1]
+    nx, nu = g["A"].shape[1], g["B"].shape[2]
+    mats = [np.ascontiguousarray(J.memory(J.rowmajor3(J.jl(np.moveaxis(g[k], 0, -1)))))
+            for k in ("A", "B", "Q", "R", "Qf")]
+    jx = J.jl(np.transpose(g["x"], (2, 1, 0)))
+    ju = J.jl(np.transpose(g["u"], (2, 1, 0)))
+    lib = _lib.load()
+    m = C.c_void_p()
+    devs = (C.c_int * 2)(0, 0)
+    _lib.check(lib.ilqr_multi_create(C.byref(m), devs, 2, nx, nu, T, nb), "ilqr_multi_create")
+    try:
+        p = _lib.Problem(_lib.PROBLEM_LQ, 0, *(a.ctypes.data for a in mats))
+        _lib.check(lib.ilqr_multi_set_problem(m, C.byref(p)), "ilqr_multi_set_problem")
+        xm = np.ascontiguousarray(J.memory(jx))
+        um = np.ascontiguousarray(J.memory(ju))
+        _lib.check(lib.ilqr_multi_load(m, xm.ctypes.data_as(C.c_void_p), um.ctypes.data_as(C.c_void_p), None),
+                   "ilqr_multi_load")
+
+        def fit_gather(flags, max_iter):
+            o = _lib.default_options(max_iter=max_iter, tol=1e-6)
+            assert lib.ilqr_multi_fit_resident(m, C.byref(o), flags, None) in (_lib.OK, _lib.ERR_LS_EXHAUSTED)
+            xo, uo = np.empty_like(xm), np.empty_like(um)
+            _lib.check(lib.ilqr_multi_gather(m, xo.ctypes.data_as(C.c_void_p), uo.ctypes.data_as(C.c_void_p),
+                                             None, None, None), "ilqr_multi_gather")
+            return J.from_memory(xo, jx.shape), J.from_memory(uo, ju.shape)
+
+        x, u = fit_gather(0, 30)
+        for b in range(nb):
+            assert rel(x[:, :, b].T, g["fit_x"][b]) < 1e-8 and rel(u[:, :, b].T, g["fit_u"][b]) < 1e-8
+        # warm start: 2 more iterations from the resident result = a fit from it
+        xw, uw = fit_gather(1, 2)
+        for b in range(nb):
+            A, B, Q, R, Qf = (g[k][b] for k in ("A", "B", "Q", "R", "Qf"))
+            xr, ur = O.fit(x[:, :, b].T, u[:, :, b].T, *O.lq_closures(A, B, Q, R, Qf), max_iter=2, tol=1e-6,
+                           symmetrize=True)[:2]
+            assert rel(xw[:, :, b].T, xr) < 1e-8 and rel(uw[:, :, b].T, ur) < 1e-8
+    finally:
+        lib.ilqr_multi_destroy(m)
