@@ -846,6 +846,7 @@ struct ChainTrigModel {
   using V = V_;
   static constexpr int NU = NU_;
   static constexpr bool HAS_FAST = true;
+  static constexpr bool HAS_CARRY = false;
   ChainTrig<V> P;
   __device__ __forceinline__ void rk4_fast(const V (&x)[4], const V (&u)[NU], V (&o)[4], bool& bad) const {
     // fp32: the joints packed (v_pk_* pairs)

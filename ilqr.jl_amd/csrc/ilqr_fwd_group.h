@@ -16,7 +16,9 @@
 //
 // A Model supplies the arithmetic of one family (value type V, NU inputs):
 //   rk4_fast(x, u, out, bad)  one RK4 step without a branch; sets `bad` when an argument
-//                             left the ranges its branch-free forms cover
+//                             left the ranges its branch-free forms cover (HAS_CARRY:
+//                             rk4_fast(x, u, out, bad, carry) after carry_init(x̄₁), a
+//                             value the model hands from step to step)
 //   rk4_robust(x, u, out)     the same step for every argument (the rollout is redone on
 //                             it when a fast pass flagged `bad`)
 //   stage_cost(xb, xt, xtw, ub), final_cost(xb)   ℓ(x̄ₖ − x_trajₖ, ūₖ) and ℓ_f(x̄_N)
@@ -44,6 +46,21 @@ struct FgOut {
   int accepted;
   bool owner;  // this lane holds the trajectory's result
 };
+
+// a model's per-rollout carry (HAS_CARRY: carry_init(x̄₁), then rk4_fast(…, carry) per
+// step), or nothing
+template <class M, bool = M::HAS_CARRY> struct FgCarry { struct T {}; };
+template <class M> struct FgCarry<M, true> { using T = typename M::Carry; };
+template <class M, class X>
+__device__ __forceinline__ typename FgCarry<M>::T fg_carry_init(const M& m, const X& x) {
+  if constexpr (M::HAS_CARRY) return m.carry_init(x);
+  else return {};
+}
+template <class M, class X, class U, class O, class C>
+__device__ __forceinline__ void fg_rk4_fast(const M& m, const X& x, const U& u, O& o, bool& bad, C& cy) {
+  if constexpr (M::HAS_CARRY) m.rk4_fast(x, u, o, bad, cy);
+  else m.rk4_fast(x, u, o, bad);
+}
 
 template <class V> struct Fg4;
 template <> struct Fg4<double> { using T = double4; };
@@ -142,6 +159,8 @@ __device__ FgOut<typename Model::V> fwd_group(const Model& m, int b, int B, int 
       xb[0] = xv.x; xb[1] = xv.y; xb[2] = xv.z; xb[3] = xv.w;
     }
     Pass p{V(0), V(0), false};
+    [[maybe_unused]] typename FgCarry<Model>::T cy{};
+    if constexpr (!ROBUST) cy = fg_carry_init(m, xb);
     auto step = [&](int t, const StepIn& in) {
       // δx = x̄ₖ − xₖ (:72); ūₖ = uₖ + α δuₖ + Kₖ δx (:73)
       V dx[4];
@@ -167,7 +186,7 @@ __device__ FgOut<typename Model::V> fwd_group(const Model& m, int b, int B, int 
       // x̄ₖ₊₁ = f(x̄ₖ, ūₖ) (:74)
       V xn[4];
       if constexpr (ROBUST) m.rk4_robust(xb, ubar, xn);
-      else m.rk4_fast(xb, ubar, xn, p.bad);
+      else fg_rk4_fast(m, xb, ubar, xn, p.bad, cy);
 #pragma unroll
       for (int i = 0; i < 4; ++i) xb[i] = xn[i];
     };

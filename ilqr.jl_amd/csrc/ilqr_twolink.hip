@@ -468,39 +468,65 @@ __device__ __forceinline__ void sincos_shift(double s0, double c0, double h, dou
   c = fma(c0, ch, -(s0 * sh));
 }
 
+// dt·θ̈ at (θ₂ with sin s2 / cos c2, θ̇ = (w1, w2), u): tl_accel with dt folded into the
+// reciprocal of det M (one product fewer per stage than dt·a, dt·b)
+template <int NU>
+__device__ __forceinline__ void tl_kdot(const TLRoll& R, double s2, double c2, double w1, double w2,
+                                        const double (&u)[NU], double& ka, double& kb) {
+  const double g = (R.beta * s2) * w2;
+  const double r0 = fma(g, fma(0.5, w2, w1), u[0]);  // u₁ − (Cθ̇)₁
+  const double hg = 0.5 * g;
+  const double r1 = NU > 1 ? fma(hg, w1, u[NU - 1]) : hg * w1;  // u₂ − (Cθ̇)₂
+  const double m00 = fma(R.beta2, c2, R.alpha);
+  const double m01 = fma(R.beta, c2, R.delta);
+  const double idt = R.dt * tl_recip(fma(-(R.bsq * c2), c2, R.det0));
+  ka = fma(R.delta, r0, -(m01 * r1)) * idt;
+  kb = fma(m00, r1, -(m01 * r0)) * idt;
+}
+
+// sin/cos of the state's θ₂, carried from step to step: the step's stage 1 reads it and
+// leaves sin/cos(θ₂') of the new state by the same angle shift the stages use,
+// h = θ₂' − θ₂ — the range reduction runs once per rollout instead of once per step
+struct TLCarry {
+  double s, c;
+};
+
 // One RK4 step without a branch (one basic block, so the scheduler can overlap the
 // stages' independent chains and the next step's reduction). `bad` is set when an
-// argument left the ranges the branch-free forms cover (|θ₂| > 1e5, |h| > 1/8); the
-// caller then redoes the rollout on rk4<double>.
+// argument left the ranges the branch-free forms cover (|θ₂| > 1e5, a shift |h| > 1/8);
+// the caller then redoes the rollout on rk4<double>. θ₁'s update sums the stage
+// velocities and scales once: θ₁ feeds nothing else.
 template <int NU>
 __device__ __forceinline__ void rk4_roll(const TLRoll& R, const double (&x)[4], const double (&u)[NU],
-                                         double (&out)[4], bool& bad) {
-  double s1, c1, s, c, a, b;
-  sincos_reduced(x[1], s1, c1);
-  tl_accel<NU>(R, s1, c1, x[2], x[3], u, a, b);
-  const double k10 = R.dt * x[2], k11 = R.dt * x[3], k12 = R.dt * a, k13 = R.dt * b;
+                                         double (&out)[4], bool& bad, TLCarry& cy) {
+  const double s1 = cy.s, c1 = cy.c;
+  double s, c, k12, k13, k22, k23, k32, k33, k42, k43;
+  tl_kdot<NU>(R, s1, c1, x[2], x[3], u, k12, k13);
+  const double k11 = R.dt * x[3];
   double y2 = x[2] + 0.5 * k12, y3 = x[3] + 0.5 * k13;
   sincos_shift(s1, c1, 0.5 * k11, s, c);
-  tl_accel<NU>(R, s, c, y2, y3, u, a, b);
-  const double k20 = R.dt * y2, k21 = R.dt * y3, k22 = R.dt * a, k23 = R.dt * b;
+  tl_kdot<NU>(R, s, c, y2, y3, u, k22, k23);
+  const double v2 = y2, k21 = R.dt * y3;
   y2 = x[2] + 0.5 * k22;
   y3 = x[3] + 0.5 * k23;
   sincos_shift(s1, c1, 0.5 * k21, s, c);
-  tl_accel<NU>(R, s, c, y2, y3, u, a, b);
-  const double k30 = R.dt * y2, k31 = R.dt * y3, k32 = R.dt * a, k33 = R.dt * b;
+  tl_kdot<NU>(R, s, c, y2, y3, u, k32, k33);
+  const double v3 = y2, k31 = R.dt * y3;
   y2 = x[2] + k32;
   y3 = x[3] + k33;
   sincos_shift(s1, c1, k31, s, c);
-  tl_accel<NU>(R, s, c, y2, y3, u, a, b);
-  const double k40 = R.dt * y2, k41 = R.dt * y3, k42 = R.dt * a, k43 = R.dt * b;
+  tl_kdot<NU>(R, s, c, y2, y3, u, k42, k43);
+  const double k41 = R.dt * y3;
   constexpr double sixth = 1.0 / 6.0;
-  out[0] = x[0] + sixth * (((k10 + 2.0 * k20) + 2.0 * k30) + k40);
+  out[0] = x[0] + (R.dt * sixth) * (((x[2] + 2.0 * v2) + 2.0 * v3) + y2);
   out[1] = x[1] + sixth * (((k11 + 2.0 * k21) + 2.0 * k31) + k41);
   out[2] = x[2] + sixth * (((k12 + 2.0 * k22) + 2.0 * k32) + k42);
   out[3] = x[3] + sixth * (((k13 + 2.0 * k23) + 2.0 * k33) + k43);
-  // |h| ≤ 1/8 for h = ½k₁₁, ½k₂₁, k₃₁ ⇐ max(|k₁₁|, |k₂₁|, 2|k₃₁|) ≤ 1/4 (NaN: not flagged,
-  // the rollout is NaN on either path)
-  const double hm = fmax(fmax(fabs(k11), fabs(k21)), 2.0 * fabs(k31));
+  const double h = out[1] - x[1];
+  sincos_shift(s1, c1, h, cy.s, cy.c);
+  // |h| ≤ 1/8 for h = ½k₁₁, ½k₂₁, k₃₁ ⇐ max(|k₁₁|, |k₂₁|, 2|k₃₁|) ≤ 1/4, and the carry's
+  // shift (NaN: not flagged, the rollout is NaN on either path)
+  const double hm = fmax(fmax(fabs(k11), fabs(k21)), fmax(2.0 * fabs(k31), 2.0 * fabs(h)));
   bad |= (hm > 0.25) | (fabs(x[1]) > 1e5);
 }
 
@@ -513,11 +539,18 @@ struct TwoLinkModel {
   using V = double;
   static constexpr int NU = NU_;
   static constexpr bool HAS_FAST = true;
+  static constexpr bool HAS_CARRY = true;
+  using Carry = TLCarry;
   TwoLinkParams P;
   TLRoll R;
+  __device__ __forceinline__ Carry carry_init(const double (&x)[4]) const {
+    Carry k;
+    sincos_reduced(x[1], k.s, k.c);
+    return k;
+  }
   __device__ __forceinline__ void rk4_fast(const double (&x)[4], const double (&u)[NU], double (&o)[4],
-                                           bool& bad) const {
-    rk4_roll<NU>(R, x, u, o, bad);
+                                           bool& bad, Carry& k) const {
+    rk4_roll<NU>(R, x, u, o, bad, k);
   }
   __device__ __forceinline__ void rk4_robust(const double (&x)[4], const double (&u)[NU], double (&o)[4]) const {
     rk4<double, NU>(P, x, u, o);
