@@ -704,13 +704,19 @@ __device__ __forceinline__ void chain_xdot_trig(const ChainTrig<V>& P, const S (
 // 2-link's rk4_roll): stage 1 reduces both angles, stages 2-4 shift their sin/cos by
 // h = ½k₁, ½k₂, k₃ (|h| ≤ 1/8); `bad` flags |h| > 1/8 or an angle past the reduction's
 // range, and the caller redoes the rollout on chain_rk4 (NaN: not flagged, NaN either way)
+// sin/cos of both joint angles carried from step to step (the forward group's carry): the
+// step's stage 1 reads them and leaves those of the new state by the stages' angle shift
+template <class V>
+struct ChainCarry {
+  V s[2], c[2];
+};
+
 template <int NU, class V>
 __device__ __forceinline__ void chain_trig_rk4_fast(const ChainTrig<V>& P, const V (&x)[4], const V (&u)[NU],
-                                                    V (&out)[4], bool& bad) {
+                                                    V (&out)[4], bool& bad, ChainCarry<V>& cy) {
   const V h = V(0.5);
-  V s10, c10, s20, c20, s1, c1, s2, c2, a0, a1;
-  sincos_red_t(x[0], s10, c10);
-  sincos_red_t(x[1], s20, c20);
+  V s1, c1, s2, c2, a0, a1;
+  const V s10 = cy.s[0], c10 = cy.c[0], s20 = cy.s[1], c20 = cy.c[1];
   chain_qdd_trig<NU>(P, s10, c10, s20, c20, x[2], x[3], u, a0, a1);
   const V k10 = P.dt * x[2], k11 = P.dt * x[3], k12 = P.dt * a0, k13 = P.dt * a1;
   V y2 = x[2] + h * k12, y3 = x[3] + h * k13;
@@ -735,8 +741,11 @@ __device__ __forceinline__ void chain_trig_rk4_fast(const ChainTrig<V>& P, const
   out[1] = x[1] + sixth * (((k11 + V(2) * k21) + V(2) * k31) + k41);
   out[2] = x[2] + sixth * (((k12 + V(2) * k22) + V(2) * k32) + k42);
   out[3] = x[3] + sixth * (((k13 + V(2) * k23) + V(2) * k33) + k43);
+  const V h0 = out[0] - x[0], h1 = out[1] - x[1];
+  sincos_shift_t(s10, c10, h0, cy.s[0], cy.c[0]);
+  sincos_shift_t(s20, c20, h1, cy.s[1], cy.c[1]);
   const V hm = fmax(fmax(fmax(fabs(k10), fabs(k11)), fmax(fabs(k20), fabs(k21))),
-                    V(2) * fmax(fabs(k30), fabs(k31)));
+                    V(2) * fmax(fmax(fabs(k30), fabs(k31)), fmax(fabs(h0), fabs(h1))));
   bad |= ((int)(hm > V(0.25)) | (int)(fabs(x[0]) > ReducedRange<V>::v) | (int)(fabs(x[1]) > ReducedRange<V>::v)) != 0;
 }
 
@@ -748,26 +757,6 @@ __device__ __forceinline__ void chain_trig_rk4_fast(const ChainTrig<V>& P, const
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ F2 f2fma(F2 a, F2 b, F2 c) { return __builtin_elementwise_fma(a, b, c); }
 
-// sincosf_reduced on both components
-__device__ __forceinline__ void sincos2_reduced(F2 x, F2& s, F2& c) {
-  const F2 kx = x * 0.63661977236758134f;
-  const F2 k = F2{rintf(kx.x), rintf(kx.y)};
-  F2 r = f2fma(-k, F2(1.5703125f), x);
-  r = f2fma(-k, F2(4.837512969970703125e-4f), r);
-  r = f2fma(-k, F2(7.54978995489188216e-8f), r);
-  const F2 z = r * r;
-  F2 ps = f2fma(z, F2(-1.9515295891e-4f), F2(8.3321608736e-3f));
-  ps = f2fma(z, ps, F2(-1.6666654611e-1f));
-  const F2 sr = f2fma(r * z, ps, r);
-  F2 pc = f2fma(z, F2(2.443315711809948e-5f), F2(-1.388731625493765e-3f));
-  pc = f2fma(z, pc, F2(4.166664568298827e-2f));
-  const F2 cr = f2fma(z * z, pc, f2fma(F2(-0.5f), z, F2(1.0f)));
-  const int q0 = (int)k.x & 3, q1 = (int)k.y & 3;
-  const float a0 = (q0 & 1) ? cr.x : sr.x, b0 = (q0 & 1) ? sr.x : cr.x;
-  const float a1 = (q1 & 1) ? cr.y : sr.y, b1 = (q1 & 1) ? sr.y : cr.y;
-  s = F2{(q0 & 2) ? -a0 : a0, (q1 & 2) ? -a1 : a1};
-  c = F2{((q0 + 1) & 2) ? -b0 : b0, ((q1 + 1) & 2) ? -b1 : b1};
-}
 // sincos_shift_t (fp32) on both components
 __device__ __forceinline__ void sincos2_shift(F2 s0, F2 c0, F2 h, F2& s, F2& c) {
   const F2 z = h * h;
@@ -811,11 +800,12 @@ __device__ __forceinline__ F2 chain_qdd_trig2(const ChainTrig<float>& P, F2 sn, 
 
 template <int NU>
 __device__ __forceinline__ void chain_trig_rk4_fast2(const ChainTrig<float>& P, const float (&x)[4],
-                                                     const float (&u)[NU], float (&out)[4], bool& bad) {
+                                                     const float (&u)[NU], float (&out)[4], bool& bad,
+                                                     ChainCarry<float>& cy) {
   const F2 q{x[0], x[1]}, w{x[2], x[3]};
   const float dt = P.dt;
-  F2 s0, c0, sn, cs;
-  sincos2_reduced(q, s0, c0);
+  const F2 s0{cy.s[0], cy.s[1]}, c0{cy.c[0], cy.c[1]};
+  F2 sn, cs;
   F2 a = chain_qdd_trig2<NU>(P, s0, c0, w, u);
   const F2 k1p = dt * w, k1v = dt * a;
   F2 y = w + 0.5f * k1v;
@@ -834,8 +824,13 @@ __device__ __forceinline__ void chain_trig_rk4_fast2(const ChainTrig<float>& P, 
   const F2 op = q + sixth * (((k1p + 2.0f * k2p) + 2.0f * k3p) + k4p);
   const F2 ov = w + sixth * (((k1v + 2.0f * k2v) + 2.0f * k3v) + k4v);
   out[0] = op.x; out[1] = op.y; out[2] = ov.x; out[3] = ov.y;
+  const F2 hq = op - q;  // the carry: sin/cos of the new angles
+  F2 sq, cq;
+  sincos2_shift(s0, c0, hq, sq, cq);
+  cy.s[0] = sq.x; cy.s[1] = sq.y; cy.c[0] = cq.x; cy.c[1] = cq.y;
   const F2 m1 = __builtin_elementwise_max(__builtin_elementwise_abs(k1p), __builtin_elementwise_abs(k2p));
-  const F2 m2 = __builtin_elementwise_max(m1, 2.0f * __builtin_elementwise_abs(k3p));
+  const F2 m2 = __builtin_elementwise_max(__builtin_elementwise_max(m1, 2.0f * __builtin_elementwise_abs(k3p)),
+                                          2.0f * __builtin_elementwise_abs(hq));
   const float hm = fmaxf(m2.x, m2.y);
   bad |= ((int)(hm > 0.25f) | (int)(fabsf(x[0]) > 8192.0f) | (int)(fabsf(x[1]) > 8192.0f)) != 0;
 }
@@ -846,12 +841,20 @@ struct ChainTrigModel {
   using V = V_;
   static constexpr int NU = NU_;
   static constexpr bool HAS_FAST = true;
-  static constexpr bool HAS_CARRY = false;
+  static constexpr bool HAS_CARRY = true;
+  using Carry = ChainCarry<V>;
   ChainTrig<V> P;
-  __device__ __forceinline__ void rk4_fast(const V (&x)[4], const V (&u)[NU], V (&o)[4], bool& bad) const {
+  __device__ __forceinline__ Carry carry_init(const V (&x)[4]) const {
+    Carry k;
+    sincos_red_t(x[0], k.s[0], k.c[0]);
+    sincos_red_t(x[1], k.s[1], k.c[1]);
+    return k;
+  }
+  __device__ __forceinline__ void rk4_fast(const V (&x)[4], const V (&u)[NU], V (&o)[4], bool& bad,
+                                           Carry& k) const {
     // fp32: the joints packed (v_pk_* pairs)
-    if constexpr (std::is_same_v<V, float>) chain_trig_rk4_fast2<NU>(P, x, u, o, bad);
-    else chain_trig_rk4_fast<NU>(P, x, u, o, bad);
+    if constexpr (std::is_same_v<V, float>) chain_trig_rk4_fast2<NU>(P, x, u, o, bad, k);
+    else chain_trig_rk4_fast<NU>(P, x, u, o, bad, k);
   }
   __device__ __forceinline__ void rk4_robust(const V (&x)[4], const V (&u)[NU], V (&o)[4]) const;
   // ℓ(x̄ₖ − x_trajₖ, ūₖ) on the joints (forward_pass.jl:187-190; RBD_helper_functions.jl:85-99)

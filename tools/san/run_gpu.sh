@@ -7,9 +7,10 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 run() {  # run <name> <cmd...>
-  timeout -k 10 240 "$@" > "gpurun_out/$1.log" 2>&1
+  local name=$1; shift
+  timeout -k 10 240 "$@" > "gpurun_out/$name.log" 2>&1
   local rc=$?
-  echo "== $1 rc=$rc"; tail -3 "gpurun_out/$1.log"
+  echo "== $name rc=$rc"; tail -3 "gpurun_out/$name.log"
   return $rc
 }
 # the HIP runtime is not instrumented: its allocations are not leaks of ours
