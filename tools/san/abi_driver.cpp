@@ -171,6 +171,10 @@ static void gpu_paths(int ndev) {
   for (int i = 0; i < 4; ++i) devs[i] = i % ndev;
   ilqr_multi* m = nullptr;
   CHECK(ilqr_multi_create(&m, devs.data(), 4, 12, 4, T, B) == ILQR_OK, "multi create");
+  // the single handle's schedule: its shards (B / 4 below BW4_MIN_BATCH) would otherwise
+  // take the one-trajectory-per-wave backward, whose bits differ
+  CHECK(ilqr_multi_set_schedule(m, ILQR_SCHED_RING_FORWARD | ILQR_SCHED_FUSED | ILQR_SCHED_BACKWARD_BLOCK) ==
+            ILQR_OK, "multi schedule");
   ilqr_problem hp{ILQR_PROBLEM_LQ, 0, lq.A.data(), lq.Bm.data(), lq.Q.data(), lq.R.data(), lq.Qf.data()};
   std::vector<double> xo(lq.x.size()), uo(lq.u.size()), co(B);
   std::vector<int32_t> io(B), so(B);
