@@ -952,6 +952,49 @@ __global__ __launch_bounds__(256) void chain_dynamics_kernel(PK P, int n,
   for (int k = 0; k < NX; ++k) xo[(size_t)i * NX + k] = o[k];
 }
 
+// The central-difference pair f(z + h e_k), f(z − h e_k) of the fp32 closed form in one
+// packed RK4 (F2 = (+, −)): stage 1 takes both angles' sin/cos in full, stages 2-4 shift
+// them by ½k₁, ½k₂, k₃ (sincos2_shift, |h| ≤ 1/8) instead of reducing the stage's angle
+// again. `bad` flags a larger shift; the caller then evaluates the pair on chain_rk4.
+template <int NU>
+__device__ __forceinline__ void chain_trig_rk4_pm(const ChainTrig<float>& P, const F2 (&x)[4], const F2 (&u)[NU],
+                                                  F2 (&out)[4], bool& bad) {
+  const float dt = P.dt;
+  F2 s10, c10, s20, c20, s1, c1, s2, c2, a0, a1;
+  scs(x[0], s10, c10);
+  scs(x[1], s20, c20);
+  chain_qdd_trig<NU>(P, s10, c10, s20, c20, x[2], x[3], u, a0, a1);
+  const F2 k10 = dt * x[2], k11 = dt * x[3], k12 = dt * a0, k13 = dt * a1;
+  F2 y2 = x[2] + 0.5f * k12, y3 = x[3] + 0.5f * k13;
+  sincos2_shift(s10, c10, 0.5f * k10, s1, c1);
+  sincos2_shift(s20, c20, 0.5f * k11, s2, c2);
+  chain_qdd_trig<NU>(P, s1, c1, s2, c2, y2, y3, u, a0, a1);
+  const F2 k20 = dt * y2, k21 = dt * y3, k22 = dt * a0, k23 = dt * a1;
+  y2 = x[2] + 0.5f * k22;
+  y3 = x[3] + 0.5f * k23;
+  sincos2_shift(s10, c10, 0.5f * k20, s1, c1);
+  sincos2_shift(s20, c20, 0.5f * k21, s2, c2);
+  chain_qdd_trig<NU>(P, s1, c1, s2, c2, y2, y3, u, a0, a1);
+  const F2 k30 = dt * y2, k31 = dt * y3, k32 = dt * a0, k33 = dt * a1;
+  y2 = x[2] + k32;
+  y3 = x[3] + k33;
+  sincos2_shift(s10, c10, k30, s1, c1);
+  sincos2_shift(s20, c20, k31, s2, c2);
+  chain_qdd_trig<NU>(P, s1, c1, s2, c2, y2, y3, u, a0, a1);
+  const F2 k40 = dt * y2, k41 = dt * y3, k42 = dt * a0, k43 = dt * a1;
+  const float sixth = 1.0f / 6.0f;
+  out[0] = x[0] + sixth * (((k10 + 2.0f * k20) + 2.0f * k30) + k40);
+  out[1] = x[1] + sixth * (((k11 + 2.0f * k21) + 2.0f * k31) + k41);
+  out[2] = x[2] + sixth * (((k12 + 2.0f * k22) + 2.0f * k32) + k42);
+  out[3] = x[3] + sixth * (((k13 + 2.0f * k23) + 2.0f * k33) + k43);
+  const F2 m1 = __builtin_elementwise_max(
+      __builtin_elementwise_max(__builtin_elementwise_abs(k10), __builtin_elementwise_abs(k11)),
+      __builtin_elementwise_max(__builtin_elementwise_abs(k20), __builtin_elementwise_abs(k21)));
+  const F2 m2 = __builtin_elementwise_max(
+      m1, 2.0f * __builtin_elementwise_max(__builtin_elementwise_abs(k30), __builtin_elementwise_abs(k31)));
+  bad |= fmaxf(m2.x, m2.y) > 0.25f;
+}
+
 // ---------------------------------------------------------------------------
 // Linearisation record per (b, t): [A | B] (NX × (NX+NU), row-major), x_t, u_t
 // ---------------------------------------------------------------------------
@@ -1046,7 +1089,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LIN == ILQR
         for (int j = 0; j < NX; ++j) x2[j] = F2{(float)xp[j], (float)xm[j]};
 #pragma unroll
         for (int j = 0; j < NU; ++j) u2[j] = F2{(float)up[j], (float)um[j]};
-        chain_rk4<NJ, NU>(P, x2, u2, f2);
+        if constexpr (std::is_same_v<PK, ChainTrig<float>>) {
+          bool bad = false;
+          chain_trig_rk4_pm<NU>(P, x2, u2, f2, bad);
+          if (bad) chain_rk4<NJ, NU>(P, x2, u2, f2);
+        } else {
+          chain_rk4<NJ, NU>(P, x2, u2, f2);
+        }
 #pragma unroll
         for (int j = 0; j < NX; ++j) { fp[j] = f2[j].x; fm[j] = f2[j].y; }
       } else {

@@ -223,7 +223,7 @@ def test_chain_api_mirror_keeps_eltype(gpu, g2):
 # The 2Dof_arm's fixed-base M is the constant diag(4, 0.5) with zero bias, so the tests
 # above cannot see a wrong joint angle, permutation sign or rotation in the 16-lane
 # Newton-Euler forward (per-lane sin/cos + DPP quad broadcasts, row_newbcast b/M
-# gathers), nor in the rotation-form central differences. These run the same kernels on
+# gathers), nor in the central differences' joint rotations. These run the same kernels on
 # ilqr_amd.chain.coupled_2dof_problem against the oracle (tests/golden/chain2c_*.npz).
 @pytest.fixture(scope="module")
 def gc():
@@ -281,7 +281,8 @@ def test_coupled_chain_forward_rollout(gpu, gc, dtype):
 @pytest.mark.parametrize("dtype,lin", CASES)
 def test_coupled_chain_linearize(gpu, gc, dtype, lin):
     """linearize_dynamics at every (b, t) of the coupled chain: dual numbers and the
-    rotation-form central differences (ILQR_CHAIN_FD_ROT), fp64 and fp32."""
+    central differences (fp32: the ± pair packed, stages 2-4 by shifted sin/cos), fp64
+    and fp32."""
     s = coupled_solver(gc, dtype, lin)
     A, B = s.linearize(dev(gc["x"], dtype), dev(gc["u"], dtype))
     t = TOL[(dtype, lin)]["AB"]
