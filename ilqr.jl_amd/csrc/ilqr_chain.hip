@@ -775,10 +775,12 @@ __device__ __forceinline__ F2 chain_qdd_trig2(const ChainTrig<float>& P, F2 sn, 
   const F2 md = F2{P.Mc[0][0], P.Mc[2][0]} +
                 (((F2{P.Mc[0][1], P.Mc[2][1]} * c2 + F2{P.Mc[0][2], P.Mc[2][2]} * s2) +
                   F2{P.Mc[0][3], P.Mc[2][3]} * C2) + F2{P.Mc[0][4], P.Mc[2][4]} * S2);
-  const float m01 = P.Mc[1][0] + (((P.Mc[1][1] * c2 + P.Mc[1][2] * s2) + P.Mc[1][3] * C2) + P.Mc[1][4] * S2);
+  // (M₀₁, dM₀₁/dq₂) packed
+  const F2 mo = F2{P.Mc[1][0], 0.0f} +
+                (((F2{P.Mc[1][1], P.Mc[1][2]} * c2 + F2{P.Mc[1][2], -P.Mc[1][1]} * s2) +
+                  F2{P.Mc[1][3], 2.0f * P.Mc[1][4]} * C2) + F2{P.Mc[1][4], -2.0f * P.Mc[1][3]} * S2);
   const F2 dmd = (F2{P.Mc[0][2], P.Mc[2][2]} * c2 - F2{P.Mc[0][1], P.Mc[2][1]} * s2) +
                  2.0f * (F2{P.Mc[0][4], P.Mc[2][4]} * C2 - F2{P.Mc[0][3], P.Mc[2][3]} * S2);
-  const float dm01 = (P.Mc[1][2] * c2 - P.Mc[1][1] * s2) + 2.0f * (P.Mc[1][4] * C2 - P.Mc[1][3] * S2);
   // g (both components): h_a = G[·][a][0] + G[·][a][1] cos q₂ + G[·][a][2] sin q₂
   F2 h[3];
 #pragma unroll
@@ -786,16 +788,19 @@ __device__ __forceinline__ F2 chain_qdd_trig2(const ChainTrig<float>& P, F2 sn, 
     h[a] = F2{P.Gc[0][a][0], P.Gc[1][a][0]} +
            (F2{P.Gc[0][a][1], P.Gc[1][a][1]} * c2 + F2{P.Gc[0][a][2], P.Gc[1][a][2]} * s2);
   const F2 g = h[0] + (h[1] * cs.x + h[2] * sn.x);
-  // M′q̇ = (dM₀₀ w₀ + dM₀₁ w₁, dM₀₁ w₀ + dM₁₁ w₁)
-  const F2 p = F2{dmd.x * w.x + dm01 * w.y, dm01 * w.x + dmd.y * w.y};
+  // M′q̇ = (dM₀₀ w₀ + dM₀₁ w₁, dM₀₁ w₀ + dM₁₁ w₁), packed
+  const F2 p = f2fma(F2{mo.y, mo.y}, w.yx, dmd * w);
   const float qq = w.x * p.x + w.y * p.y;
-  const float r0 = u[0] - (w.y * p.x + g.x);
-  float r1 = (w.y * p.y - 0.5f * qq) + g.y;
+  const F2 t = f2fma(F2{w.y, w.y}, p, g);  // (w₁p₀ + g₀, w₁p₁ + g₁)
+  const float r0 = u[0] - t.x;
+  float r1 = t.y - 0.5f * qq;
   if constexpr (NU > 1) r1 = u[NU - 1] - r1;
   else r1 = -r1;
-  const float det = md.x * md.y - m01 * m01;
+  const float det = md.x * md.y - mo.x * mo.x;
   const float id = crecip(det);
-  return F2{(md.y * r0 - m01 * r1) * id, (md.x * r1 - m01 * r0) * id};
+  // M⁻¹r = (M₁₁ r₀ − M₀₁ r₁, M₀₀ r₁ − M₀₁ r₀) / det, packed
+  const F2 r{r0, r1};
+  return (md.yx * r - F2{mo.x, mo.x} * r.yx) * id;
 }
 
 template <int NU>
