@@ -660,14 +660,15 @@ template <int NU, class S, class V>
 __device__ __forceinline__ void chain_qdd_trig(const ChainTrig<V>& P, const S& s1, const S& c1, const S& s2,
                                                const S& c2, const S& w0, const S& w1, const S (&u)[NU],
                                                S& a0, S& a1) {
-  const S C2 = c2 * c2 - s2 * s2, S2 = V(2) * (s2 * c2);
   S m[3], dm[3];
 #pragma unroll
   for (int e = 0; e < 3; ++e) {
-    m[e] = P.Mc[e][0] + (((P.Mc[e][1] * c2 + P.Mc[e][2] * s2) + P.Mc[e][3] * C2) + P.Mc[e][4] * S2);
-    // dM/dq₂ = b₁ cos − a₁ sin + 2(b₂ cos 2q − a₂ sin 2q) (the kernel argument holds M's
-    // coefficients only: fewer scalar registers than a second table)
-    dm[e] = (P.Mc[e][2] * c2 - P.Mc[e][1] * s2) + V(2) * (P.Mc[e][4] * C2 - P.Mc[e][3] * S2);
+    // M_e = a₀ + a₁ cos + b₁ sin + a₂ cos 2q + b₂ sin 2q and dM_e/dq₂ = b₁ cos − a₁ sin +
+    // 2(b₂ cos 2q − a₂ sin 2q) in Horner form in (cos q₂, sin q₂), as chain_qdd_trig2 (the
+    // kernel argument holds M's coefficients only: fewer scalar registers than a second table)
+    const V a0 = P.Mc[e][0], a1 = P.Mc[e][1], b1 = P.Mc[e][2], a2 = P.Mc[e][3], b2 = P.Mc[e][4];
+    m[e] = (a0 - a2) + c2 * ((a1 + (V(2) * a2) * c2) + (V(2) * b2) * s2) + b1 * s2;
+    dm[e] = V(-2) * b2 + c2 * ((b1 + (V(4) * b2) * c2) - (V(4) * a2) * s2) - a1 * s2;
   }
   S g[2];
 #pragma unroll
@@ -770,17 +771,26 @@ __device__ __forceinline__ void sincos2_shift(F2 s0, F2 c0, F2 h, F2& s, F2& c) 
 template <int NU>
 __device__ __forceinline__ F2 chain_qdd_trig2(const ChainTrig<float>& P, F2 sn, F2 cs, F2 w, const float (&u)[NU]) {
   const float s2 = sn.y, c2 = cs.y;
-  const float C2 = c2 * c2 - s2 * s2, S2 = 2.0f * (s2 * c2);
-  // (M₀₀, M₁₁) packed, M₀₁ alone; dM/dq₂ likewise
-  const F2 md = F2{P.Mc[0][0], P.Mc[2][0]} +
-                (((F2{P.Mc[0][1], P.Mc[2][1]} * c2 + F2{P.Mc[0][2], P.Mc[2][2]} * s2) +
-                  F2{P.Mc[0][3], P.Mc[2][3]} * C2) + F2{P.Mc[0][4], P.Mc[2][4]} * S2);
-  // (M₀₁, dM₀₁/dq₂) packed
-  const F2 mo = F2{P.Mc[1][0], 0.0f} +
-                (((F2{P.Mc[1][1], P.Mc[1][2]} * c2 + F2{P.Mc[1][2], -P.Mc[1][1]} * s2) +
-                  F2{P.Mc[1][3], 2.0f * P.Mc[1][4]} * C2) + F2{P.Mc[1][4], -2.0f * P.Mc[1][3]} * S2);
-  const F2 dmd = (F2{P.Mc[0][2], P.Mc[2][2]} * c2 - F2{P.Mc[0][1], P.Mc[2][1]} * s2) +
-                 2.0f * (F2{P.Mc[0][4], P.Mc[2][4]} * C2 - F2{P.Mc[0][3], P.Mc[2][3]} * S2);
+  // M's entries a₀ + a₁ cos q₂ + b₁ sin q₂ + a₂ cos 2q₂ + b₂ sin 2q₂ and their derivatives
+  // b₁ cos − a₁ sin + 2(b₂ cos 2q − a₂ sin 2q), in Horner form in (cos q₂, sin q₂):
+  // k₀ + c·(k₁ + k₂ c + k₃ s) + k₄ s, with M: (a₀ − a₂, a₁, 2a₂, 2b₂, b₁) and
+  // dM: (−2b₂, b₁, 4b₂, −4a₂, −a₁) (loop-invariant coefficient pairs)
+  auto horner = [&](F2 k0, F2 k1, F2 k2, F2 k3, F2 k4) {
+    const F2 in = f2fma(k3, F2(s2), f2fma(k2, F2(c2), k1));
+    return f2fma(k4, F2(s2), f2fma(in, F2(c2), k0));
+  };
+  auto a0 = [&](int e) { return P.Mc[e][0]; };
+  auto a1 = [&](int e) { return P.Mc[e][1]; };
+  auto b1 = [&](int e) { return P.Mc[e][2]; };
+  auto a2 = [&](int e) { return P.Mc[e][3]; };
+  auto b2 = [&](int e) { return P.Mc[e][4]; };
+  // (M₀₀, M₁₁), (M₀₁, dM₀₁/dq₂), (dM₀₀, dM₁₁) as pairs
+  const F2 md = horner(F2{a0(0) - a2(0), a0(2) - a2(2)}, F2{a1(0), a1(2)}, F2{2.0f * a2(0), 2.0f * a2(2)},
+                       F2{2.0f * b2(0), 2.0f * b2(2)}, F2{b1(0), b1(2)});
+  const F2 mo = horner(F2{a0(1) - a2(1), -2.0f * b2(1)}, F2{a1(1), b1(1)}, F2{2.0f * a2(1), 4.0f * b2(1)},
+                       F2{2.0f * b2(1), -4.0f * a2(1)}, F2{b1(1), -a1(1)});
+  const F2 dmd = horner(F2{-2.0f * b2(0), -2.0f * b2(2)}, F2{b1(0), b1(2)}, F2{4.0f * b2(0), 4.0f * b2(2)},
+                        F2{-4.0f * a2(0), -4.0f * a2(2)}, F2{-a1(0), -a1(2)});
   // g (both components): h_a = G[·][a][0] + G[·][a][1] cos q₂ + G[·][a][2] sin q₂
   F2 h[3];
 #pragma unroll
