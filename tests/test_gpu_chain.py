@@ -292,6 +292,31 @@ def test_coupled_chain_linearize(gpu, gc, dtype, lin):
     assert rel(A[..., 2:, :2], gc["A"][..., 2:, :2]) < ta
 
 
+def test_coupled_chain_fd_large_steps(gpu):
+    """fp32 central differences where the RK4 stages' angle shifts leave |h| ≤ 1/8
+    (fast velocities: chain_trig_rk4_pm flags the pair and re-evaluates it on the general
+    step) mixed lane by lane with ordinary states, against the fp64 dual-number Jacobian
+    of the same states."""
+    from ilqr_amd.chain import coupled_2dof_problem
+    pr = coupled_2dof_problem(2)
+    nb, T = 64, 8
+    rng = np.random.default_rng(11)
+    x = np.concatenate([rng.uniform(-3, 3, (nb, T + 1, 2)), rng.uniform(-2, 2, (nb, T + 1, 2))], axis=2)
+    fast = rng.random((nb, T + 1)) < 0.5
+    x[..., 2:] += np.where(fast, 1.0, 0.0)[..., None] * rng.choice([-1, 1], (nb, T + 1, 2)) * (40.0 / (pr.dt / 0.01))
+    u = rng.uniform(-5, 5, (nb, T, 2))
+    A64, B64 = ChainSolver(pr, T, nb, dtype=torch.float64, linearization="dual").linearize(
+        dev(x, torch.float64), dev(u, torch.float64))
+    A32, B32 = ChainSolver(pr, T, nb, dtype=torch.float32, linearization="fd").linearize(
+        dev(x, torch.float32), dev(u, torch.float32))
+    assert torch.isfinite(A32).all() and torch.isfinite(B32).all()
+    # A at the fp32 central-difference tolerance; B's small entries carry the fp32 rounding
+    # of f at |q̇| ≈ 40 rad/s over 2h: 2.8e-2 on the recursion's general step, 2.7e-2 on the
+    # closed form's general step, 3.6e-2 with its shifted stages (measured): 1e-1
+    assert rel(A32, A64) < TOL[(torch.float32, "fd")]["AB"], rel(A32, A64)
+    assert rel(B32, B64) < 1e-1, rel(B32, B64)
+
+
 @pytest.mark.parametrize("dtype,lin", CASES)
 def test_coupled_chain_backward(gpu, gc, dtype, lin):
     s = coupled_solver(gc, dtype, lin)
