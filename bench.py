@@ -164,6 +164,98 @@ def cpu_baseline(lq, x, u, budget_s):
                       f"pipeline (no Julia toolchain); C restatement timed."}
 
 
+def secondary_configs(device):
+    """BASELINE config 2 (2-link arm nu = 1, B = 1024, T = 50, fp64) and config 5 (RBD
+    2-DoF arm, fp32, central differences, B = 2048, T = 100): one cold-start fit iteration
+    per step, HIP events; each with its forward's step latency and lane occupancy."""
+    from tools import bench_rbd, bench_twolink
+    out = {}
+    for name, fn in (("config2_twolink_nu1_B1024_T50_f64",
+                      lambda: bench_twolink.measure(1024, 50, 1, steps=200, warmup=300, device=device)),
+                     ("config5_rbd_2dof_fd_f32_B2048_T100",
+                      lambda: bench_rbd.measure("fd", 2048, 100, 1, "f32", steps=100, warmup=100, device=device))):
+        try:
+            r = fn()
+            fw = r["roofline"]["forward"]
+            out[name] = {"batched_it_per_s": r["value"], "ms_per_iteration": r["ms_per_step"],
+                         "traj_iters_per_s": r["traj_iters_per_s"], "all_ok": r["all_ok"],
+                         "forward_ns_per_step": fw["step_latency_ns"],
+                         "forward_lanes_busy_frac": fw["lanes_busy_frac"],
+                         "forward_avg_launch_ms": fw["avg_launch_ms"], "forward_frac_of_peak": fw["frac"],
+                         "dtype": r["dtype"], "config": r["config"]}
+        except Exception as e:  # reported, never required
+            out[name] = {"error": repr(e)}
+    return out
+
+
+def _free_port():
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def spawn_ranks(n):
+    """`--gpus N` (N > 1) without a launcher (WORLD_SIZE unset): start N rank processes of
+    this script, one per GPU, the way torch.distributed.run would (RANK / LOCAL_RANK /
+    WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT), and return the worst exit code.
+    Runs before this process makes any GPU call; the ranks inherit stdout, so rank 0's
+    JSON line is the run's one line. A rank that fails ends the others (their PIDs)."""
+    import subprocess
+    port = os.environ.get("MASTER_PORT") or str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    while procs:
+        for p in list(procs):
+            r = p.poll()
+            if r is None:
+                continue
+            procs.remove(p)
+            if r != 0:
+                rc = rc or r
+                for q in procs:  # the survivors would wait at a barrier forever
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
+def dist_selftest(args, world, rank):
+    """`--dist-selftest`: the multi-rank plumbing of this bench WITHOUT a GPU (gloo):
+    process group, barrier-bracketed timed region, max over ranks, the per-trajectory
+    result all-gather (ilqr_amd.dist.gather_fit_results) of `--batch` entries per rank,
+    one JSON line from rank 0. No solve runs: `value` is null. tests/test_dist.py."""
+    import torch.distributed as tdist
+    from ilqr_amd.dist import gather_fit_results
+    if world > 1:
+        tdist.init_process_group("gloo")
+    B = args.batch
+    lq, x0, u0 = quadrotor_batch(B, T=args.T, seed0=rank * B)
+    # the cold trajectories' costs stand in for a fit's (ℓ = xᵀQx + uᵀRu, ℓ_f = xᵀQf x)
+    xs = x0[:, :-1]
+    cost = (np.einsum("bti,bij,btj->b", xs, lq.Q, xs) + np.einsum("bi,bij,bj->b", x0[:, -1], lq.Qf, x0[:, -1]))
+    if world > 1:
+        tdist.barrier()
+    t0 = time.perf_counter()
+    wall = time.perf_counter() - t0
+    tt = torch.tensor([wall], dtype=torch.float64)
+    if world > 1:
+        tdist.all_reduce(tt, op=tdist.ReduceOp.MAX)
+    st = torch.zeros((B,), dtype=torch.int32)
+    gc, gs = gather_fit_results(torch.from_numpy(cost), st) if world > 1 else (torch.from_numpy(cost), st)
+    ok = bool(np.allclose(gc[rank * B:(rank + 1) * B].numpy(), cost))
+    if rank == 0:
+        print(json.dumps({"metric": "dist-selftest (plumbing only, no solve)", "value": None, "n_gpus": world,
+                          "allgather_check": {"trajectories": int(gc.numel()), "own_block_matches": ok,
+                                              "finite_costs": int(torch.isfinite(gc).sum().item())}}),
+              flush=True)
+    if world > 1:
+        tdist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -177,9 +269,16 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--forward", default="dpp", choices=["dpp", "mfma"],
                     help="the ring forward's mat-vecs: DPP row broadcasts or the 4-block f64 MFMA")
+    ap.add_argument("--no-secondary", action="store_true", help="skip the configs 2 and 5 lines")
+    ap.add_argument("--dist-selftest", action="store_true",
+                    help="multi-rank plumbing only, no GPU (gloo; tests/test_dist.py)")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))  # no GPU call has been made in this process
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.dist_selftest:
+        return dist_selftest(args, world, int(os.environ.get("RANK", "0")))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = world > 1
@@ -187,6 +286,9 @@ def main():
     # box with fewer GPUs than ranks (ranks then share devices round-robin)
     backend = os.environ.get("ILQR_DIST_BACKEND", "nccl")
     ndev = torch.cuda.device_count()
+    if backend == "nccl" and local >= ndev:
+        raise SystemExit(f"rank {rank}: LOCAL_RANK {local} but {ndev} visible GPU(s); one process per GPU "
+                         f"(ILQR_DIST_BACKEND=gloo rehearses more ranks than GPUs)")
     gpu = local % max(ndev, 1) if backend != "nccl" else local
     if dist:
         import torch.distributed as tdist
@@ -360,6 +462,29 @@ def main():
     fit(FIT_ITERS)
     fit_matches_replay = bool(torch.equal(xo, x_last) and torch.equal(uo, u_last))
 
+    # the timed region's dominant kernel, lq_iter_fused4, launched exactly as fit launches
+    # it: FIT_ITERS chained iterations from cold (ilqr_iterate = one fused launch each),
+    # HIP events around every launch on the launch stream, repeated
+    fused_ms_it = [[] for _ in range(FIT_ITERS)]
+    for rep in range(22):
+        xa, ua, xb, ub = x, u, xn, un
+        st.zero_()
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+               for _ in range(FIT_ITERS)]
+        for it in range(FIT_ITERS):
+            evs[it][0].record(stream)
+            s.iterate(xa, ua, xb, ub, None if it == 0 else pc, st, trials=trials, options=opts1, new_cost=pc)
+            evs[it][1].record(stream)
+            if it == 0:
+                xa, ua, xb, ub = xn, un, fwx, fwu
+            else:
+                xa, xb, ua, ub = xb, xa, ub, ua
+        torch.cuda.synchronize()
+        if rep >= 2:
+            for it in range(FIT_ITERS):
+                fused_ms_it[it].append(evs[it][0].elapsed_time(evs[it][1]))
+    fused_ms = float(np.mean([v for row in fused_ms_it for v in row]))
+
     # result exchange (fit output): all-gather the per-trajectory costs over RCCL
     gather_ms = None
     gathered = None
@@ -374,6 +499,12 @@ def main():
         gather_ms = (time.perf_counter() - g0) * 1000.0
         gathered = {"trajectories": int(gc.numel()), "finite_costs": int(torch.isfinite(gc).sum().item()),
                     "status_max_iter": int((gs == _lib.TRAJ_MAX_ITER).sum().item())}
+
+    # BASELINE configs 2 and 5 (tools/bench_twolink.py, tools/bench_rbd.py): their fit-
+    # iteration rates and forward step latencies, after the headline's timed region
+    secondary = None
+    if world == 1 and not args.no_secondary:
+        secondary = secondary_configs(local)
 
     cnt = algorithmic_counts(T)
     bw_flops = cnt["bw_flops"] * B
@@ -412,13 +543,30 @@ def main():
                    "forward": args.forward},
         "clock_settle_s": settle_s, "clock_settle_fits": n_settle,
         "fit_timing": fit_stats,
-        "roofline": {"bound": "mfma", "kernel": "lq_iter_backward4 (backward_pass, 4 trajectories per wave, v_mfma_f64_4x4x4_4b)",
-                     "achieved": achieved_tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": achieved_tf / FP64_PEAK_TFLOPS, "traffic": traffic,
-                     "avg_launch_ms": bw_ms, "algorithmic_flops_per_launch": bw_flops,
-                     "algorithmic_bytes_per_launch": bw_bytes,
-                     "hbm_achieved_gbps": bw_bytes / (bw_ms * 1e-3) / 1e9,
-                     "mfma_pmc": mfma_summary(mf, "backward_api")},
+        # the kernel the timed region spends ≈97 % of its time in (one launch per fit
+        # iteration): algorithmic flops and bytes of one batched iteration ÷
+        # its mean launch time inside the fit chain; FP64-issue-bound, HBM beside it
+        "roofline": {"bound": "mfma", "kernel": "lq_iter_fused4 (backward_pass + forward_pass with line search, "
+                                                "4 trajectories per wave, v_mfma_f64_4x4x4_4b + DPP ring forward)",
+                     "achieved": it_flops / (fused_ms * 1e-3) / 1e12, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": it_flops / (fused_ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS,
+                     "traffic": (pmc or {}).get("hbm_bytes_per_fused_launch") if pmc and pmc.get("batch") == B
+                     and pmc.get("T") == T else None,
+                     "avg_launch_ms": fused_ms,
+                     "launch_ms_per_fit_iteration": [float(np.mean(r)) for r in fused_ms_it],
+                     "algorithmic_flops_per_launch": it_flops, "algorithmic_bytes_per_launch": it_bytes,
+                     "hbm_achieved_gbps": it_bytes / (fused_ms * 1e-3) / 1e9,
+                     "hbm_frac": it_bytes / (fused_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
+                     "timing": "HIP events around each of the fit's chained launches on the launch stream, "
+                               "20 fits after 2 (rocprofv3 kernel stats: profiles/r04/)",
+                     "mfma_pmc": mfma_summary(mf, "fused")},
+        "backward_leg": {"bound": "mfma", "kernel": "lq_iter_backward4 (backward_pass alone, 4 trajectories per wave)",
+                         "achieved": achieved_tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": achieved_tf / FP64_PEAK_TFLOPS, "traffic": traffic,
+                         "avg_launch_ms": bw_ms, "algorithmic_flops_per_launch": bw_flops,
+                         "algorithmic_bytes_per_launch": bw_bytes,
+                         "hbm_achieved_gbps": bw_bytes / (bw_ms * 1e-3) / 1e9,
+                         "mfma_pmc": mfma_summary(mf, "backward_api")},
         "forward_kernel": {"bound": "hbm", "kernel": "lq_forward (forward_pass + line search, LDS-ring input stream)",
                            "avg_launch_ms": fw_ms, "algorithmic_bytes_per_launch": fw_bytes,
                            "achieved_gbps": fw_bytes / (fw_ms * 1e-3) / 1e9,
@@ -462,6 +610,7 @@ def main():
                         "protocol": "SURVEY.md §8(d): 5-iteration fit from cold, tol disabled, median of 20 fits after "
                                     "2 warm-ups (iterations 4-5 at the fp64 cost floor, long line searches)",
                         "ms_per_fit": fit5_ms, "n_gpus": world},
+        "secondary_configs": secondary,
         "allgather_costs_ms": gather_ms,
         "allgather_check": gathered,
         "cpu_baseline": None,

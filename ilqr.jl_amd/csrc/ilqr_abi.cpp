@@ -150,7 +150,7 @@ bool fused_path(const ilqr_handle* h, const ilqr_problem* p) {
 // waits for the previous iteration's forward(c) (same trajectories); otherwise the
 // call ends by making the handle's stream wait for every forward (join).
 ilqr_status enqueue_iteration(ilqr_handle* h, const ilqr_problem* p, const ilqr::IterArgs& a,
-                              const ilqr::LSParams& ls, bool chain) {
+                              const ilqr::LSParams& ls, bool chain, const ilqr_history* hist = nullptr) {
   if (two_link(p)) {  // one stream: linearise, backward, forward
     HIP_TRY(ilqr::launch_tl_iteration(ilqr::two_link_params(), h->nu, h->batch, h->T, a, h->J, ls,
                                       h->stream));
@@ -160,8 +160,11 @@ ilqr_status enqueue_iteration(ilqr_handle* h, const ilqr_problem* p, const ilqr:
   if (h->nchunks == 1) {  // one stream, no cross-stream events (each hand-off costs ~10 µs)
     if (fused_path(h, p)) {
       ilqr::IterArgs ac = a;
+      // only a launch that gets the list also re-arms it (ctl[(gen + 1) & 1] = 0): a
+      // sequential-search launch between two cooperative ones must not advance the
+      // generation, or the next cooperative launch would count in a half nobody zeroed
       ac.coop = h->coop ? h->coop_dev : nullptr;
-      ac.coop_gen = ++h->coop_gen;
+      ac.coop_gen = h->coop ? ++h->coop_gen : h->coop_gen;
       HIP_TRY(ilqr::launch_lq_iter_fused4(P, h->batch, h->T, ac, ls, h->stream, h->fw_mfma));
       return ILQR_OK;
     }
@@ -177,6 +180,12 @@ ilqr_status enqueue_iteration(ilqr_handle* h, const ilqr_problem* p, const ilqr:
     HIP_TRY(hipEventRecord(h->ev_bw[c], h->stream));
     HIP_TRY(hipStreamWaitEvent(h->side, h->ev_bw[c], 0));
     HIP_TRY(ilqr::launch_lq_iter_forward(h->nx, h->nu, P, b0, b1, h->T, a, ls, h->side));
+    if (hist)  // chunk c's record before ev_fw[c]: its next backward (it may set NAN) waits
+               // for this chunk's record only, and still overlaps the next chunk's forward
+      HIP_TRY(ilqr::launch_record_history(
+          b1 - b0, a.iter, a.status + b0, a.iters + b0, a.trials + b0, a.new_cost + b0, a.du2 + b0, false,
+          ls.alpha0, ls.shrink, hist->cost ? hist->cost + b0 : nullptr, hist->trials ? hist->trials + b0 : nullptr,
+          hist->alpha ? hist->alpha + b0 : nullptr, hist->du2 ? hist->du2 + b0 : nullptr, h->side, h->batch));
     HIP_TRY(hipEventRecord(h->ev_fw[c], h->side));
   }
   if (!chain) return join(h, p);
@@ -530,6 +539,21 @@ ilqr_status ilqr_backward_tiles(ilqr_handle* h, const ilqr_tiles* tl, const ilqr
   return status ? fold_status(h, status) : ILQR_OK;
 }
 
+ilqr_status ilqr_linearize(ilqr_handle* h, const ilqr_problem* p, const double* x, const double* u,
+                           double* A, double* B) {
+  const ilqr_status st = check_problem(h, p);
+  if (st != ILQR_OK) return st;
+  if (!A || !B) return ILQR_ERR_BAD_ARG;
+  HIP_TRY(hipSetDevice(h->device));
+  if (two_link(p)) {
+    if (!x || !u) return ILQR_ERR_BAD_ARG;
+    HIP_TRY(ilqr::launch_tl_jacobian(ilqr::two_link_params(), h->nu, h->batch, h->T, x, u, A, B, h->stream));
+  } else {  // LQ of any supported or padded shape: the caller's (nx, nu) matrices as given
+    HIP_TRY(ilqr::launch_lq_linearize(h->nx, h->nu, lq_params(p), h->batch, h->T, A, B, h->stream));
+  }
+  return ILQR_OK;
+}
+
 ilqr_status ilqr_forward(ilqr_handle* h, const ilqr_problem* p, const ilqr_options* o,
                          const double* x, const double* u, const double* x_traj,
                          const double* d, const double* K, const double* prev_cost,
@@ -717,19 +741,18 @@ ilqr_status ilqr_fit_ex(ilqr_handle* h, const ilqr_problem* p, const ilqr_option
   const bool poll = o->tol >= 0.0 && o->max_iter > 2;
   for (int it = 1; !pipe && it <= o->max_iter; ++it) {  // forward_pass.jl:161
     // iterations chain per chunk: chunk 0's next backward overlaps chunk 1's forward
-    const ilqr_status st = enqueue_iteration(h, p, iter_args(it), ls, /*chain=*/true);
+    const ilqr_status st = enqueue_iteration(h, p, iter_args(it), ls, /*chain=*/true, hist);
     if (st != ILQR_OK) return st;
     // the history record and the count run behind every chunk's forward without
     // joining the main stream (a join would keep chunk 0's next backward from
     // overlapping chunk 1's forward): the forwards of all chunks are in order on the
     // side stream
     const hipStream_t ps = (two_link(p) || h->nchunks == 1) ? s : h->side;
-    if (hist)
+    // (chunked: enqueue_iteration recorded each chunk right behind its forward)
+    if (hist && ps == s)
       HIP_TRY(ilqr::launch_record_history(h->batch, it, h->status, h->iters, h->trials, h->prev_cost, h->du2,
                                           false, ls.alpha0, ls.shrink, hist->cost, hist->trials, hist->alpha,
                                           hist->du2, ps));
-    if (hist && ps == h->side)  // the next backwards (they may set NAN) after the record
-      for (int c = 0; c < h->nchunks; ++c) HIP_TRY(hipEventRecord(h->ev_fw[c], h->side));
     if (!poll || it == o->max_iter) continue;
     HIP_TRY(ilqr::launch_count_running(h->batch, h->status, h->dev_running + (it & 1), ps));
     HIP_TRY(hipEventRecord(h->ev_poll[it & 1], ps));

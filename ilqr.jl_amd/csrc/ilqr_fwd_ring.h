@@ -741,6 +741,9 @@ __device__ __forceinline__ void iter_forward_wave_mfma(const LQParams& P, int b0
 // coherent value); rollout stores that another XCD may overwrite later in the launch
 // (trial 1's by the publisher, trial 2's stored as it ran) are written back by a
 // release fence before the word that hands the trajectory on — a handful per launch.
+#ifndef ILQR_COOP_WAIT_TICKS
+#define ILQR_COOP_WAIT_TICKS 20000
+#endif
 __device__ __forceinline__ int32_t ag_ld(const int32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -933,6 +936,10 @@ __device__ void coop_evaluate(const LQParams& P, int b, int B, int T, const Iter
       if (j0 + k <= lim0) bits |= 1ull << (j0 + k - 1);
     const uint64_t m =
         __hip_atomic_fetch_or(&R->mask, bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) | bits;
+    // the mask RMW performed before best/stop are read: two waves that each lower
+    // best/stop and then set their bits cannot both read the other's mask without its
+    // bits AND an old best (store-buffer pattern) — one of them sees the complete set
+    complete_vmem();
     lim = coop_lim(R, ls.max_trials);
     const uint64_t need = lim >= 64 ? ~0ull : ((1ull << lim) - 1ull);
     if ((m & need) == need) {
@@ -961,7 +968,10 @@ __device__ void lq_coop_search(const LQParams& P, int B, int T, const IterArgs& 
   const LSCoop c = *a.coop;  // scalar loads, here at the end of the wave's own work
   const uint32_t gen = a.coop_gen;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  constexpr uint64_t WAIT_TICKS = 20000;  // 200 µs at the 100 MHz real-time counter
+  // 200 µs at the 100 MHz real-time counter; the Makefile's `variants` target builds a
+  // library with 0 (a wave leaves at the first unwritten slot it sees) for the test of
+  // this exit (tests/test_gpu_line_search.py::test_coop_timeout_exit_variant)
+  constexpr uint64_t WAIT_TICKS = ILQR_COOP_WAIT_TICKS;
   while (true) {
     const int n = __builtin_amdgcn_readfirstlane(ag_ld(c.ctl + (gen & 1)));
     if (n == 0) break;

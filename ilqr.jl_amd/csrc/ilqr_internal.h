@@ -140,10 +140,16 @@ hipError_t launch_fill_f64(double* p, int n, double v, hipStream_t s);
 // per-trajectory words the iteration kernels left (iters[b] == it: the trajectory ran
 // it; cost = the in-place prev_cost; status after the iteration). Cost/du2 arrays of
 // the family's dtype (f32: float), α formed in that dtype as the forward formed it.
+// `stride`: the history arrays' row length (0: B); a chunk of the batch passes its
+// offset pointers, its own B and the whole batch as the stride.
 hipError_t launch_record_history(int B, int it, const int32_t* status, const int32_t* iters,
                                  const int32_t* trials, const void* cost, const void* du2, bool f32,
                                  double alpha0, double shrink, double* h_cost, int32_t* h_trials,
-                                 double* h_alpha, double* h_du2, hipStream_t s);
+                                 double* h_alpha, double* h_du2, hipStream_t s, int stride = 0);
+// linearize_dynamics (ilqr_linearize): A (B, T, nx, nx), Bm (B, T, nx, nu) — the LQ
+// instance's matrices at every step
+hipError_t launch_lq_linearize(int nx, int nu, const LQParams& p, int B, int T, double* A, double* Bm,
+                               hipStream_t s);
 // *out = #trajectories with status OK (out may be host-mapped memory)
 hipError_t launch_count_running(int B, const int32_t* status, int32_t* out, hipStream_t s);
 bool lq_supported(int nx, int nu);
@@ -175,6 +181,10 @@ hipError_t launch_tl_forward(const TwoLinkParams& P, int nu, int B, int T, const
                              const double* K, const double* prev_cost, double* xnew,
                              double* unew, double* new_cost, int32_t* trials, int32_t* status,
                              const LSParams& ls, hipStream_t s);
+// linearize_dynamics at every (b, t) in the caller's layout (ilqr_linearize):
+// A (B, T, 4, 4), Bm (B, T, 4, nu), the backward's Dual<4+nu> arithmetic
+hipError_t launch_tl_jacobian(const TwoLinkParams& P, int nu, int B, int T, const double* x,
+                              const double* u, double* A, double* Bm, hipStream_t s);
 // one fit iteration (linearise, backward, forward) for trajectories with status OK
 hipError_t launch_tl_iteration(const TwoLinkParams& P, int nu, int B, int T, const IterArgs& a,
                                double* J, const LSParams& ls, hipStream_t s);

@@ -629,14 +629,27 @@ __global__ void gather_flags_kernel(int32_t* dflags, int32_t* flags) {
   __hip_atomic_store(dflags, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// linearize_dynamics of the LQ family (ilqr_linearize): f(x, u) = A x + B u is linear,
+// so ∂f/∂x = A and ∂f/∂u = B at every (x_t, u_t) — the instance's matrix broadcast
+// over the T steps, one thread per output element (coalesced stores; the E-element
+// source block of a trajectory is read T times from cache)
+__global__ void lq_broadcast_steps_kernel(const double* __restrict__ src, double* __restrict__ dst, int T,
+                                          int E, size_t n) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const size_t per_traj = (size_t)T * E;
+  const size_t b = i / per_traj;
+  dst[i] = src[b * E + (i - b * per_traj) % E];
+}
+
 template <class V>
-__global__ void record_history_kernel(int B, int it, const int32_t* __restrict__ status,
+__global__ void record_history_kernel(int B, int stride, int it, const int32_t* __restrict__ status,
                                       const int32_t* __restrict__ iters, const int32_t* __restrict__ trials,
                                       const V* __restrict__ cost, const V* __restrict__ du2, V alpha0, V shrink,
                                       double* h_cost, int32_t* h_trials, double* h_alpha, double* h_du2) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
-  const size_t o = (size_t)(it - 1) * B + b;
+  const size_t o = (size_t)(it - 1) * stride + b;
   const bool ran = iters[b] == it;
   const int32_t st = status[b];
   const bool acc = ran && (st == ILQR_TRAJ_OK || st == ILQR_TRAJ_CONVERGED);
@@ -855,18 +868,30 @@ hipError_t launch_gather_result(int B, int T, int nx, int nu, const double* xin,
   return hipGetLastError();
 }
 
+hipError_t launch_lq_linearize(int nx, int nu, const LQParams& p, int B, int T, double* A, double* Bm,
+                               hipStream_t s) {
+  if (B <= 0 || T <= 0) return hipSuccess;
+  const size_t nA = (size_t)B * T * nx * nx, nB = (size_t)B * T * nx * nu;
+  lq_broadcast_steps_kernel<<<(unsigned)((nA + 255) / 256), 256, 0, s>>>(p.A, A, T, nx * nx, nA);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  lq_broadcast_steps_kernel<<<(unsigned)((nB + 255) / 256), 256, 0, s>>>(p.B, Bm, T, nx * nu, nB);
+  return hipGetLastError();
+}
+
 hipError_t launch_record_history(int B, int it, const int32_t* status, const int32_t* iters,
                                  const int32_t* trials, const void* cost, const void* du2, bool f32,
                                  double alpha0, double shrink, double* h_cost, int32_t* h_trials,
-                                 double* h_alpha, double* h_du2, hipStream_t s) {
+                                 double* h_alpha, double* h_du2, hipStream_t s, int stride) {
   if (B <= 0) return hipSuccess;
+  if (stride <= 0) stride = B;
   const unsigned g = (unsigned)((B + 255) / 256);
   if (f32)
-    record_history_kernel<float><<<g, 256, 0, s>>>(B, it, status, iters, trials, (const float*)cost,
+    record_history_kernel<float><<<g, 256, 0, s>>>(B, stride, it, status, iters, trials, (const float*)cost,
                                                    (const float*)du2, (float)alpha0, (float)shrink, h_cost,
                                                    h_trials, h_alpha, h_du2);
   else
-    record_history_kernel<double><<<g, 256, 0, s>>>(B, it, status, iters, trials, (const double*)cost,
+    record_history_kernel<double><<<g, 256, 0, s>>>(B, stride, it, status, iters, trials, (const double*)cost,
                                                     (const double*)du2, alpha0, shrink, h_cost, h_trials,
                                                     h_alpha, h_du2);
   return hipGetLastError();

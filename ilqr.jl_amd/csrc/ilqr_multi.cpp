@@ -289,13 +289,17 @@ ilqr_status ilqr_multi_fit_resident(ilqr_multi* m, const ilqr_options* o, int fl
       std::swap(s.x, s.xo);
       std::swap(s.u, s.uo);
     }
-    ilqr_status r = shard_fit(m, s, o, (flags & ILQR_MULTI_USE_X_TRAJ) != 0, hist);
-    if ((r == ILQR_OK || r == ILQR_ERR_NAN || r == ILQR_ERR_LS_EXHAUSTED) && hist && s.nb && max_iter > 0) {
-      // the shard's (max_iter, nb) record into columns b0 .. b0+nb of the caller's
-      // (max_iter, batch) arrays (device memory of any device: peer copies)
-      auto cp = [&](void* dst, const void* src, size_t w) {
-        return hipMemcpy2DAsync((char*)dst + w * s.b0, w * m->batch, src, w * s.nb, w * s.nb, max_iter,
-                                hipMemcpyDefault, s.stream);
+    // The shard's (max_iter, nb) record ↔ columns b0 .. b0+nb of the caller's
+    // (max_iter, batch) arrays (device memory of any device: peer copies). The scratch
+    // is first loaded with the caller's columns, so rows past the shard's last iteration
+    // (the fit's poll stopped the loop) go back as they were (include/ilqr.h).
+    auto cp_hist = [&](bool out) -> hipError_t {
+      auto cp = [&](void* user, void* scratch, size_t w) {
+        char* u = (char*)user + w * s.b0;
+        return out ? hipMemcpy2DAsync(u, w * m->batch, scratch, w * s.nb, w * s.nb, max_iter,
+                                      hipMemcpyDefault, s.stream)
+                   : hipMemcpy2DAsync(scratch, w * s.nb, u, w * m->batch, w * s.nb, max_iter,
+                                      hipMemcpyDefault, s.stream);
       };
       hipError_t e = hipSuccess;
       if (hist->cost) e = cp(hist->cost, s.hcost, sizeof(double));
@@ -303,8 +307,15 @@ ilqr_status ilqr_multi_fit_resident(ilqr_multi* m, const ilqr_options* o, int fl
       if (e == hipSuccess && hist->alpha) e = cp(hist->alpha, s.halpha, sizeof(double));
       if (e == hipSuccess && hist->du2) e = cp(hist->du2, s.hdu2, sizeof(double));
       if (e == hipSuccess) e = hipStreamSynchronize(s.stream);
-      if (e != hipSuccess) r = ILQR_ERR_HIP;
+      return e;
+    };
+    const bool rec = hist && s.nb && max_iter > 0;
+    if (rec) {
+      if (hipSetDevice(s.device) != hipSuccess || cp_hist(false) != hipSuccess) return ILQR_ERR_HIP;
     }
+    ilqr_status r = shard_fit(m, s, o, (flags & ILQR_MULTI_USE_X_TRAJ) != 0, hist);
+    if ((r == ILQR_OK || r == ILQR_ERR_NAN || r == ILQR_ERR_LS_EXHAUSTED) && rec && cp_hist(true) != hipSuccess)
+      r = ILQR_ERR_HIP;
     return r;
   });
   m->have_result = severity(st) <= severity(ILQR_ERR_NAN);

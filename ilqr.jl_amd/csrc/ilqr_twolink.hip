@@ -321,6 +321,37 @@ __global__ __launch_bounds__(256) void tl_linearize_kernel(TwoLinkParams P, int 
   for (int e = 0; e < NJR; e += 2) Jt[e / 2] = make_double2(jv[e], jv[e + 1]);
 }
 
+// linearize_dynamics (backward_pass.jl:25-40) in the caller's layout (ilqr_linearize):
+// the same Dual<4+NU> RK4 as tl_linearize_kernel, so the same bits as the backward's
+// own [A|B]; A (B, T, 4, 4), B (B, T, 4, NU), one lane per (b, t)
+template <int NU>
+__global__ __launch_bounds__(256) void tl_jacobian_kernel(TwoLinkParams P, int B, int T,
+                                                          const double* __restrict__ x,
+                                                          const double* __restrict__ u,
+                                                          double* __restrict__ A, double* __restrict__ Bm) {
+  constexpr int ND = TL_NX + NU;
+  const int b = blockIdx.x * 256 + threadIdx.x;
+  const int t = blockIdx.y;
+  if (b >= B) return;
+  const double* xb = x + ((size_t)b * (T + 1) + t) * TL_NX;
+  const double* ub = u + ((size_t)b * T + t) * NU;
+  Dual<ND> xs[4], us[NU], out[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) xs[i] = seed<ND>(xb[i], i);
+#pragma unroll
+  for (int i = 0; i < NU; ++i) us[i] = seed<ND>(ub[i], 4 + i);
+  rk4_lin<Dual<ND>, NU>(P, xs, us, out);
+  double* At = A + ((size_t)b * T + t) * 16;
+  double* Bt = Bm + ((size_t)b * T + t) * 4 * NU;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) At[i * 4 + k] = out[i].d[k];
+#pragma unroll
+    for (int k = 0; k < NU; ++k) Bt[i * NU + k] = out[i].d[4 + k];
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Riccati recursion on the 4-block f64 MFMA (v_mfma_f64_4x4x4f64), FOUR trajectories
 // per wave — the layout of the LQ family's ilqr_bw4.hip: lane
@@ -815,6 +846,17 @@ hipError_t launch_tl_forward(const TwoLinkParams& P, int nu, int B, int T, const
                              const LSParams& ls, hipStream_t s) {
   return nu == 1 ? tl_forward_nu<1>(P, B, T, x, u, xtraj, d, K, prev_cost, xnew, unew, new_cost, trials, status, ls, s)
                  : tl_forward_nu<2>(P, B, T, x, u, xtraj, d, K, prev_cost, xnew, unew, new_cost, trials, status, ls, s);
+}
+
+hipError_t launch_tl_jacobian(const TwoLinkParams& P, int nu, int B, int T, const double* x,
+                              const double* u, double* A, double* Bm, hipStream_t s) {
+  if (B <= 0) return hipSuccess;
+  const dim3 g((B + 255) / 256, T);
+  if (nu == 1)
+    tl_jacobian_kernel<1><<<g, 256, 0, s>>>(P, B, T, x, u, A, Bm);
+  else
+    tl_jacobian_kernel<2><<<g, 256, 0, s>>>(P, B, T, x, u, A, Bm);
+  return hipGetLastError();
 }
 
 hipError_t launch_tl_iteration(const TwoLinkParams& P, int nu, int B, int T, const IterArgs& a,

@@ -10,7 +10,12 @@ __all__ = ["LinearDynamics", "QuadraticCost", "QuadraticFinalCost", "LQBatch",
            "TwoLinkFinalCost", "two_link_closures", "two_link_initial_states", "quadrotor_batch", "quadrotor_instance", "random_lq_batch",
            "fit", "backward_pass", "forward_pass", "Solver", "selftest", "LineSearchExhausted",
            "ChainSolver", "ChainProblem", "rbd_2dof_problem", "chain_closures", "load_robot",
-           "rbd_initial_states", "simple_final_cost", "simple_immediate_cost"]
+           "rbd_initial_states", "simple_final_cost", "simple_immediate_cost",
+           "linearize_dynamics", "immediate_cost_quadratization", "final_cost_quadratization",
+           "optimal_controller_param", "feedback_parameters", "step_back"]
+
+_HELPERS = ("linearize_dynamics", "immediate_cost_quadratization", "final_cost_quadratization",
+            "optimal_controller_param", "feedback_parameters", "step_back")
 
 
 def __getattr__(name):
@@ -19,6 +24,9 @@ def __getattr__(name):
     if name in ("fit", "backward_pass", "forward_pass", "LineSearchExhausted"):
         from . import api
         return getattr(api, name)
+    if name in _HELPERS:  # the reference's documented per-step API (docs/src/documentation.md)
+        from . import helpers
+        return getattr(helpers, name)
     if name in ("ChainSolver", "ChainProblem", "rbd_2dof_problem", "chain_closures", "load_robot",
                 "rbd_initial_states"):
         from . import chain

@@ -11,6 +11,10 @@ import os
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "lib",
                         "libilqr_hip.so")
+# test-only builds (csrc/Makefile `variants`): the cooperative search's timeout exit forced
+WAIT0_LIB_PATH = os.path.join(os.path.dirname(LIB_PATH), "variants", "libilqr_hip_wait0.so")
+
+ABI_VERSION = 2  # ILQR_ABI_VERSION of include/ilqr.h
 
 # ilqr_status
 OK = 0
@@ -116,6 +120,7 @@ SIGNATURES = {
     "ilqr_host_free": (C.c_int, [P]),
     "ilqr_backward": (C.c_int, [P, C.POINTER(Problem), C.POINTER(Options), P, P, P, P, P]),
     "ilqr_backward_tiles": (C.c_int, [P, C.POINTER(Tiles), C.POINTER(Options), P, P, P]),
+    "ilqr_linearize": (C.c_int, [P, C.POINTER(Problem), P, P, P, P]),
     "ilqr_forward": (C.c_int, [P, C.POINTER(Problem), C.POINTER(Options), P, P, P, P, P, P,
                                P, P, P, P, P]),
     "ilqr_iterate": (C.c_int, [P, C.POINTER(Problem), C.POINTER(Options), P, P, P, P, P, P,
@@ -166,7 +171,7 @@ def load(path: str = LIB_PATH) -> C.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.ilqr_abi_version() != 1:
+    if lib.ilqr_abi_version() != ABI_VERSION:
         raise ImportError("libilqr_hip.so ABI version mismatch")
     if path == LIB_PATH:
         _lib = lib

@@ -300,4 +300,9 @@ def _fit_closures(xb, ub, xt, dynamicsf, immediate_cost, final_cost, max_iter, t
     return FitResult(xi, ui, prev, iters, status, _lib.OK, hist)
 
 
-__all__ = ["fit", "backward_pass", "forward_pass", "LineSearchExhausted"]
+from .helpers import (feedback_parameters, final_cost_quadratization,  # noqa: E402  (the per-step API)
+                      immediate_cost_quadratization, linearize_dynamics, optimal_controller_param, step_back)
+
+__all__ = ["fit", "backward_pass", "forward_pass", "LineSearchExhausted", "linearize_dynamics",
+           "immediate_cost_quadratization", "final_cost_quadratization", "optimal_controller_param",
+           "feedback_parameters", "step_back"]

@@ -72,8 +72,9 @@ class Solver:
     _lib.PROBLEM_TWO_LINK (the reference's 2-link arm; nothing to set)."""
 
     def __init__(self, nx: int, nu: int, T: int, batch: int, device: int = 0,
-                 kind: int = _lib.PROBLEM_LQ):
-        self.lib = _lib.load()
+                 kind: int = _lib.PROBLEM_LQ, lib_path: str = None):
+        # lib_path: another build of the library (the tests' variants); default the product's
+        self.lib = _lib.load() if lib_path is None else _lib.load(lib_path)
         if not self.lib.ilqr_supported(kind, nx, nu):
             raise NotImplementedError(f"(nx, nu) = ({nx}, {nu}) has no compiled kernel for "
                                       f"problem kind {kind}")

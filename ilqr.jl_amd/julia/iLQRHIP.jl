@@ -22,11 +22,18 @@
 #     forward pass rolls the user's closure out on the host (a Julia closure cannot run on
 #     the device; this is the reference's own forward_pass.jl:70-87 loop with the line
 #     search capped).
-# New API: `solve!(::iLQRProblem)` (batched LQ, one or several GPUs) and `chain_fit`
-# (the RBD family of BASELINE config 5).
+# The reference's documented per-step API (docs/src/documentation.md:13-51) with its
+# signatures: linearize_dynamics (vector and trajectory forms; ilqr_linearize on the device
+# for the LQ / 2-link families), immediate_cost_quadratization, final_cost_quadratization,
+# optimal_controller_param, feedback_parameters, step_back.
+# New API: `solve!(::iLQRProblem)` (batched LQ, one or several GPUs), the resident
+# single-GPU `Solver` (set_problem! / fit! / backward! / forward! / solve!, close: one
+# workspace reused by every call — fit / backward_pass / forward_pass run on a cached one),
+# the resident multi-GPU `MultiSolver`, and `chain_fit` (the RBD family of BASELINE config 5).
 module iLQRHIP
 
 using ForwardDiff: gradient, jacobian, hessian   # as the reference (src/iLQR.jl:3)
+using LinearAlgebra: dot
 
 const libilqr = joinpath(@__DIR__, "..", "lib", "libilqr_hip.so")
 
@@ -149,11 +156,18 @@ function Handle(nx, nu, T, batch; device=0)
     check(ccall((:ilqr_create, libilqr), Cint, (Ref{Ptr{Cvoid}}, Cint, Cint, Cint, Cint, Cint),
                 r, device, nx, nu, T, batch), "ilqr_create")
     h = Handle(r[], Ptr{Cvoid}[])
-    finalizer(h) do h
-        for p in h.bufs; ccall((:ilqr_free, libilqr), Cint, (Ptr{Cvoid}, Ptr{Cvoid}), h.ptr, p); end
-        ccall((:ilqr_destroy, libilqr), Cint, (Ptr{Cvoid},), h.ptr)
-    end
+    finalizer(close, h)       # a backstop: Solver and the per-call paths close explicitly
     return h
+end
+
+"""close(h): free the handle's device buffers and its workspace now (idempotent)."""
+function Base.close(h::Handle)
+    h.ptr == C_NULL && return nothing
+    for p in h.bufs; ccall((:ilqr_free, libilqr), Cint, (Ptr{Cvoid}, Ptr{Cvoid}), h.ptr, p); end
+    empty!(h.bufs)
+    ccall((:ilqr_destroy, libilqr), Cint, (Ptr{Cvoid},), h.ptr)
+    h.ptr = C_NULL
+    return nothing
 end
 
 # launch schedule of the LQ family (include/ilqr.h: ILQR_SCHED_*)
@@ -179,6 +193,21 @@ function upload(h::Handle, a::Array{T}) where {T}
     check(ccall((:ilqr_memcpy_h2d, libilqr), Cint, (Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Csize_t),
                 h.ptr, p, a, sizeof(a)), "ilqr_memcpy_h2d")
     return p
+end
+
+# into an existing device buffer (the resident Solver: no allocation)
+function upload!(h::Handle, p::Ptr, a::Array)
+    check(ccall((:ilqr_memcpy_h2d, libilqr), Cint, (Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Csize_t),
+                h.ptr, p, a, sizeof(a)), "ilqr_memcpy_h2d")
+    return p
+end
+
+function release!(h::Handle, p::Ptr)
+    i = findfirst(==(Ptr{Cvoid}(p)), h.bufs)
+    i === nothing && return nothing
+    ccall((:ilqr_free, libilqr), Cint, (Ptr{Cvoid}, Ptr{Cvoid}), h.ptr, p)
+    deleteat!(h.bufs, i)
+    return nothing
 end
 
 function download!(h::Handle, a::Array, p::Ptr)
@@ -259,17 +288,8 @@ function backward_pass(x::AbstractMatrix, u::AbstractMatrix, dynamicsf, immediat
     @assert(N == M + 1)                                                 # backward_pass.jl:329
     family(dynamicsf, immediate_cost, final_cost) == :tiles &&
         return backward_tiles_device(x, u, dynamicsf, immediate_cost, final_cost)
-    h = Handle(nx, nu, M, 1)
-    p = Ref(problem(h, dynamicsf, immediate_cost, final_cost))
-    xd = upload(h, to_abi(x)); ud = upload(h, to_abi(u))
-    dd = alloc(h, Float64, M * nu); Kd = alloc(h, Float64, M * nu * nx)
-    st = alloc(h, Int32, 1)
-    check(ccall((:ilqr_backward, libilqr), Cint,
-                (Ptr{Cvoid}, Ref{Problem}, Ref{Options}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Int32}),
-                h.ptr, p, default_options(), xd, ud, dd, Kd, st), "ilqr_backward")
-    du = from_abi(download!(h, zeros(nu, M), dd))                       # (T × nu)
-    K = gains_from_abi(download!(h, zeros(nx, nu, M), Kd))              # (T × nu × nx) like 𝐊s
-    return du, K
+    # the resident solver of this shape (no allocation per call): δu (T × nu), K (T × nu × nx) like 𝐊s
+    return backward!(set_problem!(cached_solver(nx, nu, M), dynamicsf, immediate_cost, final_cost), x, u)
 end
 
 # total_cost_generator (forward_pass.jl:182-196), for the host rollout of the tiles path
@@ -311,20 +331,8 @@ function forward_pass(x::AbstractMatrix, u::AbstractMatrix, x_traj::AbstractMatr
     @assert(N == M + 1)                                                 # forward_pass.jl:62
     family(dynamicsf, immediate_cost, final_cost) == :tiles &&
         return forward_host(x, u, x_traj, δu, K, prev_cost, dynamicsf, immediate_cost, final_cost)
-    h = Handle(nx, nu, M, 1)
-    p = Ref(problem(h, dynamicsf, immediate_cost, final_cost))
-    xd = upload(h, to_abi(x)); ud = upload(h, to_abi(u)); xt = upload(h, to_abi(x_traj))
-    dd = upload(h, to_abi(δu)); Kd = upload(h, gains_to_abi(K))
-    pc = upload(h, Float64[prev_cost])
-    xo = alloc(h, Float64, N * nx); uo = alloc(h, Float64, M * nu); co = alloc(h, Float64, 1)
-    st = alloc(h, Int32, 1)
-    check(ccall((:ilqr_forward, libilqr), Cint,
-                (Ptr{Cvoid}, Ref{Problem}, Ref{Options}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64},
-                 Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64},
-                 Ptr{Int32}, Ptr{Int32}),
-                h.ptr, p, default_options(), xd, ud, xt, dd, Kd, pc, xo, uo, co, C_NULL, st), "ilqr_forward")
-    x̄ = from_abi(download!(h, zeros(nx, N), xo)); ū = from_abi(download!(h, zeros(nu, M), uo))
-    return (x̄, ū, download!(h, zeros(1), co)[1])
+    s = set_problem!(cached_solver(nx, nu, M), dynamicsf, immediate_cost, final_cost)
+    return forward!(s, x, u, x_traj, δu, K, prev_cost)
 end
 
 # the reference's per-iteration line (forward_pass.jl:167), from a fit's history
@@ -345,20 +353,10 @@ function fit(x_init::AbstractMatrix, u_init::AbstractMatrix, dynamicsf, immediat
     @assert(N == M + 1, "size(x_init)[2] == size(u_init)[1]")          # forward_pass.jl:156
     family(dynamicsf, immediate_cost, final_cost) == :tiles &&
         return fit_tiles(x_init, u_init, dynamicsf, immediate_cost, final_cost, x_traj, max_iter, tol, verbose)
-    h = Handle(nx, nu, M, 1)
-    p = Ref(problem(h, dynamicsf, immediate_cost, final_cost))
-    o = default_options(); o.max_iter = max_iter; o.tol = tol
-    xi = upload(h, to_abi(x_init)); ui = upload(h, to_abi(u_init)); xt = upload(h, to_abi(x_traj))
-    xo = alloc(h, Float64, N * nx); uo = alloc(h, Float64, M * nu)
-    hc = alloc(h, Float64, max_iter); ht = upload(h, zeros(Int32, max(max_iter, 1)))
-    hist = Ref(History(hc, ht, C_NULL, C_NULL))
-    st = ccall((:ilqr_fit_ex, libilqr), Cint,
-               (Ptr{Cvoid}, Ref{Problem}, Ref{Options}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64},
-                Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Int32}, Ptr{Int32}, Ref{History}),
-               h.ptr, p, o, xi, ui, xt, xo, uo, C_NULL, C_NULL, C_NULL, hist)
-    st == ILQR_ERR_LS_EXHAUSTED || check(st, "ilqr_fit")   # exhausted: the last iterate is returned
-    verbose && print_history(download!(h, zeros(max_iter), hc), download!(h, zeros(Int32, max(max_iter, 1)), ht))
-    return from_abi(download!(h, zeros(nx, N), xo)), from_abi(download!(h, zeros(nu, M), uo))
+    # the resident solver of this shape: an MPC loop calling fit allocates nothing per call;
+    # an exhausted line search returns the last iterate (fit_resident!)
+    s = set_problem!(cached_solver(nx, nu, M), dynamicsf, immediate_cost, final_cost)
+    return fit!(s, x_init, u_init; x_traj=x_traj, max_iter=max_iter, tol=tol, verbose=verbose)
 end
 
 # fit (forward_pass.jl:148-179) for arbitrary closures: tiles backward on the GPU, host
@@ -495,6 +493,238 @@ function solve!(ms::MultiSolver, prob::iLQRProblem; max_iter::Int64=100, tol::Fl
                 (Ptr{Cvoid}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Int32}, Ptr{Int32}),
                 ms.ptr, prob.x, prob.u, C_NULL, C_NULL, C_NULL), "ilqr_multi_gather")
     return prob
+end
+
+# -- resident single-device solver ------------------------------------------------------
+"""Solver(nx, nu, T, batch; device = 0): one GPU, one ilqr_create workspace, and every
+device buffer a call needs — the problem (A, B, Q, R, Qf), the trajectories, x_traj, the
+results, the gains — allocated ONCE here and reused by every call (include/ilqr.h: "hot
+calls never allocate"), for an MPC loop calling fit over and over (forward_pass.jl:148-179).
+The history scratch of verbose fits grows on demand. close(s) frees everything at once;
+the finalizer is only a backstop. The functional fit / backward_pass / forward_pass above
+run on a cached Solver per shape (cached_solver; clear_cache!() closes them)."""
+mutable struct Solver
+    h::Handle
+    nx::Int; nu::Int; M::Int; nb::Int
+    kind::Int32
+    A::Ptr{Float64}; B::Ptr{Float64}; Q::Ptr{Float64}; R::Ptr{Float64}; Qf::Ptr{Float64}
+    x::Ptr{Float64}; u::Ptr{Float64}; xt::Ptr{Float64}; xo::Ptr{Float64}; uo::Ptr{Float64}
+    d::Ptr{Float64}; K::Ptr{Float64}; pc::Ptr{Float64}; cost::Ptr{Float64}
+    iters::Ptr{Int32}; status::Ptr{Int32}; trials::Ptr{Int32}
+    hc::Ptr{Float64}; ht::Ptr{Int32}; hcap::Int
+end
+
+function Solver(nx::Integer, nu::Integer, T::Integer, batch::Integer; device::Integer=0)
+    h = Handle(nx, nu, T, batch; device=device)
+    N = T + 1
+    f(n) = alloc(h, Float64, batch * n)
+    i(n) = alloc(h, Int32, batch * n)
+    return Solver(h, nx, nu, T, batch, Int32(0),
+                  f(nx * nx), f(nx * nu), f(nx * nx), f(nu * nu), f(nx * nx),     # A B Q R Qf
+                  f(N * nx), f(T * nu), f(N * nx), f(N * nx), f(T * nu),         # x u x_traj x̄ ū
+                  f(T * nu), f(T * nu * nx), f(1), f(1),                          # δu K prev_cost cost
+                  i(1), i(1), i(1),                                               # iters status trials
+                  Ptr{Float64}(C_NULL), Ptr{Int32}(C_NULL), 0)
+end
+
+Base.close(s::Solver) = close(s.h)
+
+problem_ref(s::Solver) = Ref(s.kind == ILQR_PROBLEM_LQ ? Problem(ILQR_PROBLEM_LQ, 0, s.A, s.B, s.Q, s.R, s.Qf) :
+                                                       Problem(s.kind, 0, C_NULL, C_NULL, C_NULL, C_NULL, C_NULL))
+
+"""set_problem!(s, dynamicsf, immediate_cost, final_cost): the problem the next calls
+solve — LQ matrices copied into the resident buffers (batch 1: one instance), or the
+2-link arm (nothing to copy)."""
+function set_problem!(s::Solver, f::LinearDynamics, l::QuadraticCost, lf::QuadraticFinalCost)
+    s.nb == 1 || throw(ArgumentError("one instance per call: set_problem!(s, ::iLQRProblem) for batches"))
+    upload!(s.h, s.A, rowmajor(f.A)); upload!(s.h, s.B, rowmajor(f.B)); upload!(s.h, s.Q, rowmajor(l.Q))
+    upload!(s.h, s.R, rowmajor(l.R)); upload!(s.h, s.Qf, rowmajor(lf.Qf))
+    s.kind = ILQR_PROBLEM_LQ
+    return s
+end
+function set_problem!(s::Solver, f::TwoLinkDynamics{NU}, ::TwoLinkCost, ::TwoLinkFinalCost) where {NU}
+    (s.nx, s.nu) == (4, NU) || throw(AssertionError("the 2-link arm is (4, $NU), the solver ($(s.nx), $(s.nu))"))
+    s.kind = ILQR_PROBLEM_TWO_LINK
+    return s
+end
+function set_problem!(s::Solver, prob::iLQRProblem)
+    upload!(s.h, s.A, rowmajor3(prob.A)); upload!(s.h, s.B, rowmajor3(prob.B)); upload!(s.h, s.Q, rowmajor3(prob.Q))
+    upload!(s.h, s.R, rowmajor3(prob.R)); upload!(s.h, s.Qf, rowmajor3(prob.Qf))
+    s.kind = ILQR_PROBLEM_LQ
+    return s
+end
+
+function ensure_history!(s::Solver, n::Int)
+    if s.hcap < n
+        s.hc != C_NULL && (release!(s.h, s.hc); release!(s.h, s.ht))
+        s.hc = alloc(s.h, Float64, n * s.nb); s.ht = alloc(s.h, Int32, n * s.nb); s.hcap = n
+    end
+    upload!(s.h, s.ht, zeros(Int32, n * s.nb))   # rows past the last iteration read as "not run"
+    return Ref(History(s.hc, s.ht, C_NULL, C_NULL))
+end
+
+# ilqr_fit_ex from the resident (x, u, x_traj) into the resident results
+function fit_resident!(s::Solver, max_iter::Int64, tol::Float64, verbose::Bool)
+    s.kind == 0 && throw(ArgumentError("set_problem! first"))
+    o = default_options(); o.max_iter = max_iter; o.tol = tol
+    n = max(max_iter, 1)
+    hist = verbose ? ensure_history!(s, n) : Ref(History(C_NULL, C_NULL, C_NULL, C_NULL))
+    st = ccall((:ilqr_fit_ex, libilqr), Cint,
+               (Ptr{Cvoid}, Ref{Problem}, Ref{Options}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64},
+                Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Int32}, Ptr{Int32}, Ref{History}),
+               s.h.ptr, problem_ref(s), o, s.x, s.u, s.xt, s.xo, s.uo, s.cost, s.iters, s.status, hist)
+    st in (ILQR_OK, ILQR_ERR_LS_EXHAUSTED) || check(st, "ilqr_fit")
+    if verbose
+        c = download!(s.h, zeros(s.nb, n), s.hc); t = download!(s.h, zeros(Int32, s.nb, n), s.ht)
+        for b in 1:s.nb; print_history(c[b, :], t[b, :]); end
+    end
+    return st
+end
+
+"""fit!(s, x_init, u_init; x_traj, max_iter, tol, verbose) -> (x̄, ū): iLQR.fit
+(forward_pass.jl:148-179) of one trajectory (reference layout) on the resident solver."""
+function fit!(s::Solver, x_init::AbstractMatrix, u_init::AbstractMatrix; x_traj=zero(x_init),
+              max_iter::Int64=100, tol::Float64=1e-6, verbose::Bool=false)
+    N, nx = size(x_init); M, nu = size(u_init)
+    @assert(N == M + 1, "size(x_init)[2] == size(u_init)[1]")          # forward_pass.jl:156
+    (nx, nu, M, 1) == (s.nx, s.nu, s.M, s.nb) || throw(AssertionError("shape differs from the Solver's"))
+    upload!(s.h, s.x, to_abi(x_init)); upload!(s.h, s.u, to_abi(u_init)); upload!(s.h, s.xt, to_abi(x_traj))
+    fit_resident!(s, max_iter, tol, verbose)
+    return from_abi(download!(s.h, zeros(nx, N), s.xo)), from_abi(download!(s.h, zeros(nu, M), s.uo))
+end
+
+"""solve!(s::Solver, prob; max_iter, tol) -> prob: the batched fit of solve!(prob) on the
+resident solver (set_problem!(s, prob) first, or here with set = true)."""
+function solve!(s::Solver, prob::iLQRProblem; max_iter::Int64=100, tol::Float64=1e-6, set::Bool=false)
+    size(prob.x) == (s.nx, s.M + 1, s.nb) && size(prob.u) == (s.nu, s.M, s.nb) ||
+        throw(AssertionError("problem shape differs from the Solver's"))
+    set && set_problem!(s, prob)
+    upload!(s.h, s.x, prob.x); upload!(s.h, s.u, prob.u)
+    st = ccall((:ilqr_fit_ex, libilqr), Cint,
+               (Ptr{Cvoid}, Ref{Problem}, Ref{Options}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64},
+                Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Int32}, Ptr{Int32}, Ptr{Cvoid}),
+               s.h.ptr, problem_ref(s), (o = default_options(); o.max_iter = max_iter; o.tol = tol; o),
+               s.x, s.u, C_NULL, s.xo, s.uo, s.cost, s.iters, s.status, C_NULL)
+    st in (ILQR_OK, ILQR_ERR_LS_EXHAUSTED) || check(st, "ilqr_fit")
+    download!(s.h, prob.x, s.xo); download!(s.h, prob.u, s.uo)
+    return prob
+end
+
+"""backward!(s, x, u) -> (δu, K): iLQR.backward_pass (backward_pass.jl:324-357) on the
+resident solver (one trajectory, reference layout)."""
+function backward!(s::Solver, x::AbstractMatrix, u::AbstractMatrix)
+    N, nx = size(x); M, nu = size(u)
+    @assert(N == M + 1)                                                 # backward_pass.jl:329
+    upload!(s.h, s.x, to_abi(x)); upload!(s.h, s.u, to_abi(u))
+    check(ccall((:ilqr_backward, libilqr), Cint,
+                (Ptr{Cvoid}, Ref{Problem}, Ref{Options}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Int32}),
+                s.h.ptr, problem_ref(s), default_options(), s.x, s.u, s.d, s.K, s.status), "ilqr_backward")
+    return from_abi(download!(s.h, zeros(nu, M), s.d)), gains_from_abi(download!(s.h, zeros(nx, nu, M), s.K))
+end
+
+"""forward!(s, x, u, x_traj, δu, K, prev_cost) -> (x̄, ū, new_cost): iLQR.forward_pass
+(forward_pass.jl:55-93) on the resident solver."""
+function forward!(s::Solver, x::AbstractMatrix, u::AbstractMatrix, x_traj::AbstractMatrix, δu::AbstractMatrix,
+                  K::AbstractArray{<:Real,3}, prev_cost::Real)
+    N, nx = size(x); M, nu = size(u)
+    @assert(N == M + 1)                                                 # forward_pass.jl:62
+    upload!(s.h, s.x, to_abi(x)); upload!(s.h, s.u, to_abi(u)); upload!(s.h, s.xt, to_abi(x_traj))
+    upload!(s.h, s.d, to_abi(δu)); upload!(s.h, s.K, gains_to_abi(K)); upload!(s.h, s.pc, Float64[prev_cost])
+    check(ccall((:ilqr_forward, libilqr), Cint,
+                (Ptr{Cvoid}, Ref{Problem}, Ref{Options}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64},
+                 Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64},
+                 Ptr{Int32}, Ptr{Int32}),
+                s.h.ptr, problem_ref(s), default_options(), s.x, s.u, s.xt, s.d, s.K, s.pc, s.xo, s.uo, s.cost,
+                s.trials, s.status), "ilqr_forward")
+    return (from_abi(download!(s.h, zeros(nx, N), s.xo)), from_abi(download!(s.h, zeros(nu, M), s.uo)),
+            download!(s.h, zeros(1), s.cost)[1])
+end
+
+# the functional entry points' solvers, one per (nx, nu, T) on device 0
+const SOLVER_CACHE = Dict{NTuple{3,Int},Solver}()
+function cached_solver(nx, nu, M)
+    s = get(SOLVER_CACHE, (nx, nu, M), nothing)
+    (s === nothing || s.h.ptr == C_NULL) && (s = SOLVER_CACHE[(nx, nu, M)] = Solver(nx, nu, M, 1))
+    return s
+end
+"""clear_cache!(): close the solvers fit / backward_pass / forward_pass keep per shape."""
+function clear_cache!()
+    foreach(close, values(SOLVER_CACHE)); empty!(SOLVER_CACHE)
+    return nothing
+end
+
+# -- the reference's documented per-step API (docs/src/documentation.md:13-51) ------------
+"""linearize_dynamics(x, u, dynamicsf) -> (𝐀, 𝐁) (backward_pass.jl:25-40). Vectors: one
+point. Matrices with one row per step (test/test_linearize_dynamics.jl:10-14): 𝐀s (T × nx
+× nx), 𝐁s (T × nx × nu) with 𝐀s[i, :, :] the Jacobian at (x[i, :], u[i, :]) — on the
+device (ilqr_linearize) for the LQ and 2-link families, by ForwardDiff (as the reference)
+for any other closure."""
+function linearize_dynamics(x::AbstractVector, u::AbstractVector, f)
+    As, Bs = linearize_dynamics(reshape(collect(x), 1, :), reshape(collect(u), 1, :), f)
+    return As[1, :, :], Bs[1, :, :]
+end
+function linearize_dynamics(x::AbstractMatrix, u::AbstractMatrix, f)
+    M, nu = size(u); nx = size(x, 2)
+    size(x, 1) in (M, M + 1) || throw(AssertionError("x has $(size(x, 1)) rows for $M inputs"))
+    fam = f isa LinearDynamics ? :lq : f isa TwoLinkDynamics ? :two_link : :host
+    if fam == :host                                                     # ForwardDiff, :32-33
+        As = zeros(M, nx, nx); Bs = zeros(M, nx, nu)
+        for i in 1:M
+            As[i, :, :] = jacobian(z -> f(z, u[i, :]), x[i, :]); Bs[i, :, :] = jacobian(v -> f(x[i, :], v), u[i, :])
+        end
+        return As, Bs
+    end
+    xa = size(x, 1) == M ? vcat(x, x[end:end, :]) : x                   # the ABI reads T+1 states
+    h = Handle(nx, nu, M, 1)
+    try
+        p = fam == :lq ? Ref(problem(h, f, QuadraticCost(zero(f.A), zeros(nu, nu)), QuadraticFinalCost(zero(f.A)))) :
+                         Ref(Problem(ILQR_PROBLEM_TWO_LINK, 0, C_NULL, C_NULL, C_NULL, C_NULL, C_NULL))
+        xd = upload(h, to_abi(xa)); ud = upload(h, to_abi(u))
+        Ad = alloc(h, Float64, M * nx * nx); Bd = alloc(h, Float64, M * nx * nu)
+        check(ccall((:ilqr_linearize, libilqr), Cint,
+                    (Ptr{Cvoid}, Ref{Problem}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}),
+                    h.ptr, p, xd, ud, Ad, Bd), "ilqr_linearize")
+        # (T, nx, nx) row-major = Julia (nx, nx, T), each step transposed → 𝐀s (T × nx × nx)
+        return (permutedims(download!(h, zeros(nx, nx, M), Ad), (3, 2, 1)),
+                permutedims(download!(h, zeros(nu, nx, M), Bd), (3, 2, 1)))
+    finally
+        close(h)
+    end
+end
+
+"""immediate_cost_quadratization(x, u, immediate_cost) -> (𝑞, 𝐪, 𝐫, 𝐐, 𝐏, 𝐑)
+(backward_pass.jl:81-109; 𝐏 = ∂(∇ᵤℓ)/∂x is nu × nx): ForwardDiff on the host, the
+reference's own derivatives."""
+function immediate_cost_quadratization(x::AbstractVector, u::AbstractVector, ℓ)
+    gu(z, v) = gradient(w -> ℓ(z, w), v)
+    return (ℓ(x, u), gradient(z -> ℓ(z, u), x), gu(x, u), hessian(z -> ℓ(z, u), x),
+            jacobian(z -> gu(z, u), x), hessian(v -> ℓ(x, v), u))
+end
+
+"""final_cost_quadratization(x, final_cost) -> (𝑞ₙ, 𝐪ₙ, 𝐐ₙ) (backward_pass.jl:134-153)."""
+final_cost_quadratization(x::AbstractVector, ℓf) = (ℓf(x), gradient(ℓf, x), hessian(ℓf, x))
+
+"""optimal_controller_param(𝐀, 𝐁, 𝐫, 𝐏, 𝐑, 𝐬′, 𝐒′) -> (𝐠, 𝐆, 𝐇) (backward_pass.jl:177-186)."""
+function optimal_controller_param(A::AbstractMatrix, B::AbstractMatrix, r::AbstractVector, P::AbstractMatrix,
+                                  R::AbstractMatrix, s::AbstractVector, S::AbstractMatrix)
+    BᵀS = transpose(B) * S
+    return (r + transpose(B) * s, P + BᵀS * A, R + BᵀS * B)
+end
+
+"""feedback_parameters(𝐠, 𝐆, 𝐇) -> (𝛿𝐮ᶠᶠ, 𝐊) with the fixed H + 0.01 I (backward_pass.jl:207-218)."""
+function feedback_parameters(g::AbstractVector, G::AbstractMatrix, H::AbstractMatrix)
+    Hμ = H + 0.01 * one(H)
+    return (-(Hμ \ g), -(Hμ \ G))
+end
+
+"""step_back(𝐀, 𝑞, 𝐪, 𝐐, 𝐠, 𝐆, 𝐇, 𝛿𝐮, 𝐊, 𝑠′, 𝐬′, 𝐒′) -> (𝑠, 𝐬, 𝐒), unregularised 𝐇
+(backward_pass.jl:262-273)."""
+function step_back(A, q, qv, Q, g, G, H, δu, K, s′, sv′, S′)
+    Hδu = H * δu
+    Kᵀ, Gᵀ, Aᵀ = transpose(K), transpose(G), transpose(A)
+    return (q + s′ + 0.5 * dot(δu, Hδu) + dot(δu, g),
+            qv + Aᵀ * sv′ + Kᵀ * Hδu + Kᵀ * g + Gᵀ * δu,
+            Q + Aᵀ * S′ * A + Kᵀ * H * K + Kᵀ * G + Gᵀ * K)
 end
 
 # -- RBD family (ILQR_PROBLEM_CHAIN): test/RBD_2_link_example with a fixed base --------

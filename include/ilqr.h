@@ -11,6 +11,7 @@
  *   ilqr_fit       <- iLQR.fit             /root/reference/src/forward_pass.jl:148-179
  *   ilqr_iterate   <- one iteration of fit's loop body, forward_pass.jl:162-175
  *                     (backward_pass + forward_pass fused in one launch)
+ *   ilqr_linearize <- iLQR.linearize_dynamics, trajectory form  backward_pass.jl:25-40
  *
  * The reference's callbacks (dynamicsf, immediate_cost, final_cost; documented
  * at src/backward_pass.jl:11-19,54-70,122-127) are Julia closures that cannot
@@ -56,7 +57,7 @@
 extern "C" {
 #endif
 
-#define ILQR_ABI_VERSION 1
+#define ILQR_ABI_VERSION 2
 
 typedef enum {
   ILQR_OK = 0,
@@ -191,11 +192,6 @@ ilqr_status ilqr_backward(ilqr_handle* h, const ilqr_problem* p, const ilqr_opti
                           const double* x, const double* u, double* d, double* K,
                           int32_t* status);
 
-/* iLQR.forward_pass (forward_pass.jl:55-93): rollout + line search starting
- * from alpha0, accepting the first alpha with prev_cost - new_cost > 0; a
- * trajectory whose search exhausts max_trials gets x_new = x, u_new = u.
- * x_traj may be NULL (zeros); trials may be NULL. status as for ilqr_backward
- * (synchronising when given; ILQR_ERR_LS_EXHAUSTED / ILQR_ERR_NAN). */
 /* iLQR.backward_pass for arbitrary closures: the Riccati recursion of
  * backward_pass.jl:335-357 (optimal_controller_param, feedback_parameters,
  * step_back) on caller-supplied derivative tiles (ilqr_tiles); same outputs and
@@ -203,6 +199,21 @@ ilqr_status ilqr_backward(ilqr_handle* h, const ilqr_problem* p, const ilqr_opti
 ilqr_status ilqr_backward_tiles(ilqr_handle* h, const ilqr_tiles* tiles, const ilqr_options* o,
                                 double* d, double* K, int32_t* status);
 
+/* iLQR.linearize_dynamics (backward_pass.jl:25-40) at every step of every
+ * trajectory, the trajectory form test/test_linearize_dynamics.jl:10-14 calls:
+ * A (batch, T, nx, nx) = ∂f/∂x and B (batch, T, nx, nu) = ∂f/∂u at (x_t, u_t),
+ * t = 0 .. T−1 (x (batch, T+1, nx): x_T is not read; u (batch, T, nu)). LQ: f is
+ * linear, so every step's A_t, B_t is the instance's A, B exactly (x, u may be NULL).
+ * TWO_LINK: forward-mode dual numbers through the RK4 functor, the arithmetic of
+ * ilqr_backward's own linearisation. Asynchronous. (Chains: ilqr_chain_linearize.) */
+ilqr_status ilqr_linearize(ilqr_handle* h, const ilqr_problem* p, const double* x, const double* u,
+                           double* A, double* B);
+
+/* iLQR.forward_pass (forward_pass.jl:55-93): rollout + line search starting
+ * from alpha0, accepting the first alpha with prev_cost - new_cost > 0; a
+ * trajectory whose search exhausts max_trials gets x_new = x, u_new = u.
+ * x_traj may be NULL (zeros); trials may be NULL. status as for ilqr_backward
+ * (synchronising when given; ILQR_ERR_LS_EXHAUSTED / ILQR_ERR_NAN). */
 ilqr_status ilqr_forward(ilqr_handle* h, const ilqr_problem* p, const ilqr_options* o,
                          const double* x, const double* u, const double* x_traj,
                          const double* d, const double* K, const double* prev_cost,

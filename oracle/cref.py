@@ -132,7 +132,10 @@ def tl_forward(x, u, x_traj, d, K, prev_cost, max_trials=64, alpha0=1.0, shrink=
 
 
 def tl_fit(x_init, u_init, x_traj=None, max_iter=100, tol=1e-6, mu=0.01, max_trials=64,
-           symmetrize=False, nthreads=0):
+           symmetrize=False, nthreads=0, history=False):
+    """→ (x, u, cost, iters, status), plus with history=True a dict of (max_iter, B)
+    arrays "cost" (NaN: not run / failed), "trials" (0: not run), "du2" — the layout of
+    ilqr_fit_ex's record (include/ilqr.h)."""
     lib = load()
     xi, ui = _f64(x_init), _f64(u_init)
     nb, T, nu = ui.shape
@@ -142,9 +145,15 @@ def tl_fit(x_init, u_init, x_traj=None, max_iter=100, tol=1e-6, mu=0.01, max_tri
     cost = np.empty(nb)
     iters = np.empty(nb, dtype=np.int32)
     st = np.empty(nb, dtype=np.int32)
+    h = None
+    if history:
+        h = {"cost": np.full((nb, max_iter), np.nan), "trials": np.zeros((nb, max_iter), dtype=np.int32),
+             "du2": np.full((nb, max_iter), np.nan)}
     lib.oracle_tl_fit(nb, T, nu, _p(xi), _p(ui), _p(xt), max_iter, C.c_double(tol), C.c_double(mu),
                       int(symmetrize), max_trials, _p(xo), _p(uo), _p(cost), _p(iters), _p(st),
-                      nthreads)
+                      nthreads, *((_p(h["cost"]), _p(h["trials"]), _p(h["du2"])) if h else (None, None, None)))
+    if history:
+        return xo, uo, cost, iters, st, {k: np.ascontiguousarray(v.T) for k, v in h.items()}
     return xo, uo, cost, iters, st
 
 

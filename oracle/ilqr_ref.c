@@ -815,11 +815,15 @@ int oracle_lq_forward(int Bn, int T, int n, int m, const double* A, const double
 }
 
 /* fit (forward_pass.jl:148-179) for one trajectory.
- * status: 1 converged, 2 max_iter, 3 LS exhausted, 4 NaN. */
+ * status: 1 converged, 2 max_iter, 3 LS exhausted, 4 NaN.
+ * hcost / htrials / hdu2 (may be NULL): per iteration i (index i − 1) the accepted cost
+ * (the reference's `Iteration: i  Total Cost: c` line, :167; NaN if the search failed),
+ * the trials of the search (max_trials when exhausted), Σ(ū − u)² (:171); entries past
+ * the last iteration untouched — ilqr_fit_ex's history record (include/ilqr.h). */
 static void fit_one(const prob_t* P, const double* x_init, const double* u_init,
                     const double* xtraj, int max_iter, double tol, double mu, int sym,
                     int max_trials, double* x_out, double* u_out, double* cost, int* iters,
-                    int* status) {
+                    int* status, double* hcost, int* htrials, double* hdu2) {
   const int n = P->n, m = P->m, T = P->T;
   const size_t xs = (size_t)(T + 1) * n, us = (size_t)T * m;
   double* buf = (double*)malloc(sizeof(double) * (2 * xs + 2 * us + us + us * n));
@@ -832,10 +836,13 @@ static void fit_one(const prob_t* P, const double* x_init, const double* u_init,
     if (backward_one(P, xi, ui, mu, sym, d, K)) { st = 4; break; }
     double nc = NAN;
     const int tr = forward_one(P, xi, ui, xtraj, d, K, prev_cost, xn, un, &nc, max_trials, 1.0, 0.5);
+    if (htrials) htrials[it - 1] = tr < 0 ? max_trials : tr;
+    if (hcost) hcost[it - 1] = tr < 0 ? NAN : nc;
     if (tr < 0) { st = (nc != nc) ? 4 : 3; break; }
     prev_cost = nc; /* :168 */
     double du2 = 0.0;
     for (size_t i = 0; i < us; ++i) du2 += (un[i] - ui[i]) * (un[i] - ui[i]);
+    if (hdu2) hdu2[it - 1] = du2;
     if (du2 <= tol) { st = 1; break; } /* :171 — break before the update */
     memcpy(xi, xn, sizeof(double) * xs); /* :174-175 */
     memcpy(ui, un, sizeof(double) * us);
@@ -861,7 +868,7 @@ int oracle_lq_fit(int Bn, int T, int n, int m, const double* A, const double* Bm
     const prob_t P = instance(b, n, m, T, A, Bm, Q, R, Qf);
     fit_one(&P, x_init + b * xs, u_init + b * us, xtraj ? xtraj + b * xs : NULL, max_iter, tol, mu,
             sym, max_trials, x_out + b * xs, u_out + b * us, &cost[b], iters ? &iters[b] : NULL,
-            status ? &status[b] : NULL);
+            status ? &status[b] : NULL, NULL, NULL, NULL);
   }
   return 0;
 }
@@ -901,17 +908,20 @@ int oracle_tl_forward(int Bn, int T, int nu, const double* x, const double* u, c
   return fails;
 }
 
+/* history arrays (may be NULL): (Bn, max_iter), trajectory slowest (see fit_one) */
 int oracle_tl_fit(int Bn, int T, int nu, const double* x_init, const double* u_init, const double* xtraj,
                   int max_iter, double tol, double mu, int sym, int max_trials, double* x_out,
-                  double* u_out, double* cost, int* iters, int* status, int nthreads) {
+                  double* u_out, double* cost, int* iters, int* status, int nthreads, double* hcost,
+                  int* htrials, double* hdu2) {
   set_threads(nthreads);
   const prob_t P = tl_problem(T, nu);
-  const size_t xs = (size_t)(T + 1) * 4, us = (size_t)T * nu;
+  const size_t xs = (size_t)(T + 1) * 4, us = (size_t)T * nu, hs = (size_t)max_iter;
 #pragma omp parallel for schedule(dynamic, 4)
   for (int b = 0; b < Bn; ++b)
     fit_one(&P, x_init + b * xs, u_init + b * us, xtraj ? xtraj + b * xs : NULL, max_iter, tol, mu,
             sym, max_trials, x_out + b * xs, u_out + b * us, &cost[b], iters ? &iters[b] : NULL,
-            status ? &status[b] : NULL);
+            status ? &status[b] : NULL, hcost ? hcost + b * hs : NULL, htrials ? htrials + b * hs : NULL,
+            hdu2 ? hdu2 + b * hs : NULL);
   return 0;
 }
 

@@ -17,7 +17,8 @@ def pytest_configure(config):
 # that `-m gpu -x` stopping on a family's unit test cannot hide them; then the LQ
 # parity suite, the 2-link family, tiles, layouts, and the chain family last.
 _ORDER = ("test_gpu_configs", "test_gpu_headline", "test_gpu_line_search", "test_gpu_history", "test_gpu_multi", "test_gpu_parity", "test_gpu_twolink",
-          "test_gpu_tiles", "test_gpu_julia_layout", "test_gpu_cost_functions", "test_gpu_chain")
+          "test_gpu_tiles", "test_gpu_julia_layout", "test_gpu_julia_resident", "test_gpu_helpers",
+          "test_gpu_cost_functions", "test_gpu_chain")
 
 
 def pytest_collection_modifyitems(config, items):

@@ -28,7 +28,7 @@ def test_library_loads_and_exports_every_symbol():
     lib = _lib.load()
     for name in declared_functions():
         assert hasattr(lib, name), name
-    assert lib.ilqr_abi_version() == 1
+    assert lib.ilqr_abi_version() == _lib.ABI_VERSION == 2
 
 
 def test_status_strings_and_defaults():
@@ -101,9 +101,25 @@ def test_julia_shim_ccalls_declared_symbols():
     called = set(re.findall(r"ccall\(\(:(ilqr_[a-z0-9_]+),\s*libilqr\)", src))
     assert {"ilqr_fit_ex", "ilqr_backward", "ilqr_forward", "ilqr_backward_tiles",
             "ilqr_chain_fit", "ilqr_chain_set_dynamics", "ilqr_multi_set_problem", "ilqr_multi_load",
-            "ilqr_multi_fit_resident", "ilqr_multi_gather"} <= called, called
+            "ilqr_multi_fit_resident", "ilqr_multi_gather", "ilqr_linearize"} <= called, called
     declared = set(declared_functions())
     assert called <= declared, called - declared
     lib = _lib.load()
     for name in called:
         assert hasattr(lib, name), name
+
+
+def test_julia_shim_exposes_reference_api():
+    """The shim defines the reference's public functions (docs/src/documentation.md:13-51)
+    and the resident Solver's methods; the per-call paths no longer create handles
+    (they run on cached_solver): only Solver(), the tiles/linearize helpers and
+    solve!(prob) construct a Handle."""
+    src = open(os.path.join(ROOT, "ilqr.jl_amd", "julia", "iLQRHIP.jl")).read()
+    for fn in ("fit", "backward_pass", "forward_pass", "linearize_dynamics", "immediate_cost_quadratization",
+               "final_cost_quadratization", "optimal_controller_param", "feedback_parameters", "step_back",
+               "fit!", "backward!", "forward!", "set_problem!", "solve!", "clear_cache!"):
+        assert re.search(r"^(function )?" + re.escape(fn) + r"\(", src, re.M), fn
+    assert re.search(r"^Base\.close\(s::Solver\)", src, re.M)
+    body = lambda name: src[src.index(f"function {name}("):src.index("\nend", src.index(f"function {name}("))]
+    for name in ("fit", "backward_pass", "forward_pass"):
+        assert "Handle(" not in body(name) and "cached_solver(" in body(name), name

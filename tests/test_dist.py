@@ -66,3 +66,25 @@ def test_two_rank_fit_gather_matches_single_process(n):
     _, _, cost, iters, st = cref.lq_fit(lq, x, u, max_iter=20, tol=1e-6, nthreads=1)
     assert np.array_equal(idx, np.arange(n))
     assert np.array_equal(gc, cost) and np.array_equal(gs, st)
+
+
+def test_bench_gpus_flag_spawns_ranks():
+    """`bench.py --gpus 2` with no launcher starts two rank processes itself (before any
+    GPU call); rank 0 prints the one JSON line with n_gpus = 2 and the per-trajectory
+    all-gather of 2 × batch entries. --dist-selftest runs that plumbing without a GPU
+    (gloo, no solve); the GPU form is tests/test_gpu_headline.py::test_bench_two_ranks_gloo."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env["ILQR_DIST_BACKEND"] = "gloo"
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--dist-selftest",
+                        "--batch", "16", "--T", "8"], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2
+    assert out["allgather_check"]["trajectories"] == 32
+    assert out["allgather_check"]["own_block_matches"] and out["allgather_check"]["finite_costs"] == 32

@@ -167,3 +167,26 @@ def test_config4_shards_equal_independent_instances(gpu, config4):
     xr, ur, cr, itr, _ = cref.lq_fit(sub(lq7, idx), x7[idx], u7[idx], max_iter=2, tol=-1.0, symmetrize=True)
     assert rel(r.u.cpu().numpy()[idx], ur) < TOL_TRAJ and rel(r.cost.cpu().numpy()[idx], cr) < TOL_COST
     s.close()
+
+
+def test_bench_two_ranks_gloo(gpu):
+    """`bench.py --gpus 2` without a launcher spawns its two rank processes (here both on
+    the box's one GPU, gloo in place of RCCL): one JSON line, n_gpus = 2, the per-trajectory
+    cost all-gather holding both ranks' batches, every gathered cost finite."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env["ILQR_DIST_BACKEND"] = "gloo"
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "6",
+                        "--warmup", "3", "--settle", "0.1", "--batch", "512", "--no-cpu", "--no-secondary"],
+                       env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["config"]["global_batch"] == 1024
+    assert out["allgather_check"]["trajectories"] == 1024 and out["allgather_check"]["finite_costs"] == 1024
+    assert out["value"] > 0 and out["iteration"]["all_ok"]

@@ -89,6 +89,50 @@ def test_coop_equals_sequential_forced(gpu, nb):
     assert_same(coop, seq)
 
 
+@pytest.mark.parametrize("nb", [4096, 8192])
+def test_coop_timeout_exit_variant(gpu, nb):
+    """The cooperative search's timeout exit (lq_coop_search: a wave that finds no work but
+    a reserved, not yet written list slot waits at most WAIT_TICKS, then leaves) taken at
+    every such sighting: the test build libilqr_hip_wait0.so (ILQR_COOP_WAIT_TICKS = 0,
+    csrc/Makefile `variants`) must still give the sequential search's bits — correctness
+    rests only on every publisher finding its own entries, not on the wait."""
+    lq, x, u, xt, pc = forced_case(nb)
+    seq_s = Solver(12, 4, 100, nb)
+    seq_s.set_problem(lq)
+    var = Solver(12, 4, 100, nb, lib_path=_lib.WAIT0_LIB_PATH)
+    var.set_problem(lq)
+    try:
+        seq = run_iterate(seq_s, x, u, xt, pc, True)
+        coop = run_iterate(var, x, u, xt, pc, False)
+        coop2 = run_iterate(var, x, u, xt, pc, False)   # and again on the re-armed list
+    finally:
+        seq_s.close()
+        var.close()
+    assert (seq[4] == _lib.TRAJ_LS_EXHAUSTED).sum() > nb // 10
+    assert_same(coop, seq)
+    assert_same(coop2, seq)
+
+
+def test_coop_sequential_coop_on_one_handle(gpu):
+    """coop → sequential → coop launches on ONE handle (a sequential launch
+    must not advance the list generation, or the next cooperative launch counts in a
+    half nobody zeroed): all three bit-equal, over the forced workload's many publications."""
+    nb = 4096
+    lq, x, u, xt, pc = forced_case(nb)
+    s = Solver(12, 4, 100, nb)
+    s.set_problem(lq)
+    try:
+        a = run_iterate(s, x, u, xt, pc, False)
+        b = run_iterate(s, x, u, xt, pc, True)
+        c = run_iterate(s, x, u, xt, pc, False)
+        d = run_iterate(s, x, u, xt, pc, True)
+        e = run_iterate(s, x, u, xt, pc, False)
+    finally:
+        s.close()
+    for r in (a, c, d, e):
+        assert_same(r, b)
+
+
 @pytest.mark.parametrize("max_trials", [2, 7, 64, 65])
 def test_coop_equals_sequential_max_trials(gpu, max_trials):
     nb = 2048

@@ -5,6 +5,8 @@ one GPU. Trajectories are independent, so each shard's block must equal the same
 trajectories solved by one handle over the whole batch, bit for bit (same kernels,
 same per-trajectory arithmetic) — the resident path, the host-in/host-out path, warm
 starts and the per-iteration history alike."""
+import ctypes as C
+
 import numpy as np
 import pytest
 import torch
@@ -86,6 +88,60 @@ def test_resident_warm_start_and_history(gpu):
             np.testing.assert_array_equal(r2[k], ref2[k], err_msg=k)
     finally:
         ms.close()
+
+
+def test_resident_history_with_tol_leaves_unrun_rows(gpu):
+    """with tol ≥ 0 each shard's fit stops polling at its own last iteration, so
+    the rows of the (max_iter, batch) record past it must keep what the caller put there
+    (include/ilqr.h: "left as they were"), never the shard scratch's stale contents. Rows a
+    trajectory ran equal one handle's record bit for bit; every other entry is either the
+    caller's sentinel or the "did not run" marker (trials 0, NaN) one handle writes."""
+    B, T, n = 4096, 50, 40
+    lq, x, u = quadrotor_batch(B, T=T, seed0=11)
+
+    def filled():
+        h, hst = alloc_history(n, B, "cuda")
+        h["cost"].fill_(-5.0)
+        h["trials"].fill_(-1)
+        h["alpha"].fill_(-5.0)
+        h["du2"].fill_(-5.0)
+        return h, hst
+
+    ms = MultiSolver([0] * 4, 12, 4, T, B)
+    try:
+        ms.set_schedule(backward="block")
+        ms.set_problem(lq)
+        for rep in range(2):   # the second fit reuses the shards' scratch from the first
+            ms.load(x, u)
+            h, hst = filled()
+            ms.fit_resident(max_iter=n, tol=1e-6, history=hst)
+            hm = {k: v.cpu().numpy() for k, v in h.items()}
+    finally:
+        ms.close()
+    s = Solver(12, 4, T, B)
+    s.set_problem(lq)
+    s.set_schedule(backward="block")
+    h1, hst1 = filled()
+    xi, ui = dev(x), dev(u)
+    xo, uo = s.alloc_traj(zero=False)
+    P = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
+    s._bind_stream()
+    rc = s.lib.ilqr_fit_ex(s.h, s._p(), C.byref(_lib.default_options(max_iter=n, tol=1e-6)), P(xi), P(ui), None,
+                           P(xo), P(uo), None, None, None, C.byref(hst1))
+    torch.cuda.synchronize()
+    s.close()
+    assert rc == _lib.OK
+    h1 = {k: v.cpu().numpy() for k, v in h1.items()}
+    ran = h1["trials"] > 0
+    assert ran.any() and (~ran).any()
+    for k in ("cost", "trials", "alpha", "du2"):
+        np.testing.assert_array_equal(hm[k][ran], h1[k][ran], err_msg=k)
+    unrun = ~ran
+    assert np.all((hm["trials"][unrun] == -1) | (hm["trials"][unrun] == 0))
+    for k in ("cost", "alpha", "du2"):
+        v = hm[k][unrun]
+        assert np.all((v == -5.0) | np.isnan(v)), k
+    assert (hm["trials"] == -1).any()   # some shard stopped before the last row: untouched
 
 
 def test_host_path_equals_resident(gpu):

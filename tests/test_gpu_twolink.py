@@ -168,20 +168,69 @@ def test_tl_config2_batch(gpu):
         assert abs(float(r.cost[b]) - h[-1]["cost"]) / h[-1]["cost"] < 1e-11
 
 
-def test_tl_long_horizon_reaches_target(gpu):
-    """The reference's end-to-end example (animate_2_link.jl:7-25: x₀ = [.1,-.1,0,0],
-    u₀ = 0, T = 900, tol = 1e-6) and the repaired check of test_iLQR.jl:19:
-    final_cost(x̄_N) < 0.01. Parity here is a property, not a fixture: the oracle
-    is too slow at T = 900."""
+def _fit_vs_c_oracle(x, u, max_iter, tol=1e-6):
+    """fit_ex on the device against the C restatement's fit (oracle/ilqr_ref.c, symmetrised
+    step_back): status and iteration count exactly, the returned iterate at TOL_FIT, the
+    cost at 1e-11, and the per-iteration record — every iteration's accepted cost (the
+    reference's `Iteration: i  Total Cost: c` line, forward_pass.jl:167) at 1e-11 and its
+    line-search trial count exactly."""
+    from oracle import cref
+    B, T, nu = u.shape
+    s = Solver(4, nu, T, B, kind=_lib.PROBLEM_TWO_LINK)
+    try:
+        r = s.fit(dev(x), dev(u), max_iter=max_iter, tol=tol, history=True)
+    finally:
+        s.close()
+    xo, uo, co, it, st, h = cref.tl_fit(x, u, max_iter=max_iter, tol=tol, symmetrize=True, history=True)
+    np.testing.assert_array_equal(r.status.cpu().numpy(), st)
+    np.testing.assert_array_equal(r.iters.cpu().numpy(), it)
+    assert rel(r.x, xo) < TOL_FIT and rel(r.u, uo) < TOL_FIT, (rel(r.x, xo), rel(r.u, uo))
+    assert rel(r.cost, co) < 1e-11
+    n = int(it.max())
+    hc, ht = r.history["cost"][:n].cpu().numpy(), r.history["trials"][:n].cpu().numpy()
+    np.testing.assert_array_equal(ht, h["trials"][:n])
+    ran = ht > 0
+    assert np.isfinite(hc[ran]).all() and np.isnan(hc[~ran]).all()
+    assert float(np.max(np.abs(hc[ran] - h["cost"][:n][ran]) / np.abs(h["cost"][:n][ran]))) < 1e-11
+    return r, it, h
+
+
+def test_tl_animate_workload_vs_c_oracle(gpu):
+    """The reference's end-to-end example, animate_2_link.jl:7-25: x₀ = [.1, −.1, 0, 0],
+    u₀ = 0, x_init the rollout of u₀, T = 900, tol = 1e-6, max_iter = 10⁶ — fit on the
+    device against the C restatement's fit (iteration count, iterates, per-iteration cost
+    history), plus the repaired check of test_iLQR.jl:19: final_cost(x̄_N) < 0.01."""
     T = 900
     s = tl_solver(T, 1)
-    u0 = torch.zeros((1, T, 2), dtype=torch.float64, device="cuda")
-    x = s.rollout(dev(np.array([[0.1, -0.1, 0.0, 0.0]])), u0)
-    r = s.fit(x, u0, max_iter=1000, tol=1e-6)
-    assert int(r.status[0]) == _lib.TRAJ_CONVERGED
+    u0 = np.zeros((1, T, 2))
+    x = s.rollout(dev(np.array([[0.1, -0.1, 0.0, 0.0]])), dev(u0)).cpu().numpy()
+    s.close()
+    f, _, _ = two_link_closures()
+    assert rel(x[0], O.rollout(np.array([0.1, -0.1, 0.0, 0.0]), u0[0], f)) < TOL_ROLL
+    r, it, h = _fit_vs_c_oracle(x, u0, max_iter=10**6)
+    assert int(r.status[0]) == _lib.TRAJ_CONVERGED and int(it[0]) >= 3
     th = TwoLinkArm.inverse_kinematics()
     xN = r.x[0, -1].cpu().numpy()
     assert float(np.sum((th - xN[:2]) ** 2)) < 0.01
+
+
+def test_tl_test_iLQR_workload_vs_c_oracle(gpu):
+    """test/test_iLQR.jl:8-19 as intended: x_init with every state the random x₀, u_init =
+    zeros(100, 2), T = 100, tol = 1e-6 — eight seeded x₀ (default_rng(seed).random(4),
+    seeds 0..7) on the device against the C restatement's fit (iteration counts, iterates,
+    per-iteration cost history). As written the reference test cannot run: `repeat(x₀,
+    101, 1)'` is 1×404, so fit's `@assert N == M + 1` fails, and `max_iter = 1e5` is a
+    Float64 that `max_iter::Int64` rejects (the integer 10⁵ is used here). Its check
+    final_cost(x̄_N) < 0.01 does NOT hold for this workload: from these x₀ a 1 s horizon
+    ends 2.3-8.6 rad² from θ* — the oracle's fit and the device's agree on that, which is
+    what is asserted (the check holds for the T = 900 example above)."""
+    B, T = 8, 100
+    x0 = np.stack([np.random.default_rng(b).random(4) for b in range(B)])
+    x = np.repeat(x0[:, None, :], T + 1, axis=1)
+    u = np.zeros((B, T, 2))
+    r, it, h = _fit_vs_c_oracle(x, u, max_iter=10**5)
+    assert (r.status.cpu().numpy() == _lib.TRAJ_CONVERGED).all()
+    assert (it >= 8).all()
 
 
 def test_tl_bad_problem_args(gpu):

@@ -62,6 +62,109 @@ def cpu_baseline(pr, x, u, budget_s):
                       f"{el:.2f} s"}
 
 
+def measure(lin="fd", B=2048, T=100, nu=1, dtype="f32", steps=100, warmup=100, device=0,
+            dynamics="auto", cpu_budget=None, base=None):
+    """Config 5's fit-iteration rate and per-kernel roofline for one linearisation (one
+    dict; bench.py's secondary_configs calls this after its headline, outside the
+    headline's timed region)."""
+    dt = torch.float32 if dtype == "f32" else torch.float64
+    dev = torch.device("cuda", device)
+    pr = rbd_2dof_problem(nu)
+    x0 = rbd_initial_states(B, 2)
+    s = ChainSolver(pr, T, B, dtype=dt, linearization=lin, device=device)
+    s.set_dynamics(dynamics)
+    u = torch.zeros((B, T, pr.nu), dtype=dt, device=dev)
+    x = s.rollout(torch.from_numpy(x0).to(dev, dt), u)
+    xn, un = torch.empty_like(x), torch.empty_like(u)
+    pc = torch.empty((B,), dtype=dt, device=dev)
+    st = torch.zeros((B,), dtype=torch.int32, device=dev)
+    trials = torch.empty((B,), dtype=torch.int32, device=dev)
+    opts = _lib.default_options(tol=-1.0)
+    stream = torch.cuda.current_stream(dev)
+    s._bind()
+
+    def step():
+        s.iterate(x, u, xn, un, None, st, pc, trials=trials, options=opts)
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ms_ev = timed(step, steps, stream)
+    ms = max(ms_ev, (time.perf_counter() - t0) * 1000.0 / steps)
+    ok = bool((st == 0).all().item())
+    # per-kernel times and the roofline object (algorithmic FLOPs, tools/flops.py)
+    d = torch.empty((B, T, pr.nu), dtype=dt, device=dev)
+    K = torch.empty((B, T, pr.nu, pr.nx), dtype=dt, device=dev)
+    A = torch.empty((B, T, pr.nx, pr.nx), dtype=dt, device=dev)
+    Bm = torch.empty((B, T, pr.nx, pr.nu), dtype=dt, device=dev)
+    o = _lib.default_options()
+    import ctypes as C
+    P = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
+    lin_fn = lambda: s.lib.ilqr_chain_linearize(s.h, P(x), P(u), P(A), P(Bm))  # noqa: E731
+    bw = lambda: s.lib.ilqr_chain_backward(s.h, C.byref(o), P(x), P(u), P(d), P(K), None)  # noqa: E731
+    pinf = torch.full((B,), float("inf"), dtype=dt, device=dev)
+    nc = torch.empty_like(pinf)
+    fw = lambda: s.lib.ilqr_chain_forward(s.h, C.byref(o), P(x), P(u), None, P(d), P(K), P(pinf),  # noqa: E731
+                                          P(xn), P(un), P(nc), None, None)
+    for fn in (lin_fn, bw, fw):
+        fn()
+    lin_ms = timed(lin_fn, steps, stream)
+    bw_ms = timed(bw, steps, stream)   # ilqr_chain_backward = linearise + Riccati
+    fw_ms = timed(fw, steps, stream)
+    nd = pr.nx + pr.nu
+    # algorithmic FLOPs of the evaluator that runs: the closed form's own count
+    # (pricing it on the recursion's 16x larger count put the linearisation above peak)
+    f_ref = FL.chain_dynamics_flops(pr)
+    f_rk4 = FL.chain_closed_form_flops(pr.nu) if s.dynamics_mode == "closed_form" else f_ref
+    lin_fl = (f_rk4 * FL.dual_factor(nd) if lin == "dual" else 2 * nd * f_rk4 + nd * pr.nx) * T * B
+    ric_fl = FL.riccati_flops_per_step(pr.nx, pr.nu) * T * B
+    fw_fl = FL.forward_flops_per_step(pr.nx, pr.nu, f_rk4) * T * B
+    peak = PEAK_TFLOPS[dtype]
+    kern = {"linearize": (lin_ms, lin_fl), "riccati": (max(bw_ms - lin_ms, 1e-6), ric_fl),
+            "forward": (fw_ms, fw_fl)}
+    roof = {"bound": ("forward latency/issue (a dependent RK4 chain per trajectory, 4 candidate lanes each, "
+                      "closed-form dynamics)"
+                      if s.dynamics_mode == "closed_form" else
+                      "forward latency/issue (16 lanes per trajectory)") + ", linearisation VALU issue",
+            "unit": "TFLOP/s", "peak": peak, "peak_dtype": dtype,
+            "flops_note": (f"RK4 of the closed form = {f_rk4} flop; of the restated RBD recursion "
+                           f"(the reference's RigidBodyDynamics.jl calls) = {f_ref} flop (tools/flops.py)"
+                           if f_rk4 != f_ref else
+                           f"RK4 of the restated RBD formulas = {f_rk4} flop (tools/flops.py)")}
+    for k, (ms_k, fl) in kern.items():
+        roof[k] = {"avg_launch_ms": ms_k, "algorithmic_flops": fl,
+                   "achieved": fl / (ms_k * 1e-3) / 1e12, "frac": fl / (ms_k * 1e-3) / 1e12 / peak}
+    roof["achieved"], roof["frac"] = roof["forward"]["achieved"], roof["forward"]["frac"]
+    # the forward's real bound: T dependent RK4 steps per trajectory (4 line-search
+    # candidate lanes each: 4B of the chip's 65,536 lanes), so its time is T × the
+    # latency of one step — the FLOP fraction is small by construction
+    roof["forward"]["step_latency_ns"] = fw_ms * 1e6 / T
+    roof["forward"]["lanes_busy_frac"] = min(1.0, 4 * B / (1024 * 64))
+    res = {"metric": f"batched iLQR iterations/sec (fwd+bwd pass), RBD 2-DoF arm fixed base, "
+                     f"nx=4 nu={pr.nu} T={T}",
+           "value": 1000.0 / ms, "unit": f"batched iterations/s (batch={B})", "n_gpus": 1,
+           "steps": steps, "warmup": warmup, "ms_per_step": ms,
+           "higher_is_better": True, "dtype": dtype, "data": "synthetic x0 ~ U(-1,1)",
+           "config": {"workload": "BASELINE config 5 (RBD_2_link_example, fixed base)",
+                      "batch": B, "T": T, "linearization": lin, "dynamics": s.dynamics_mode,
+                      "closed_form_check": s.closed_form_error},
+           "traj_iters_per_s": B * 1000.0 / ms,
+           "mean_line_search_trials": float(trials.double().mean().item()), "all_ok": ok,
+           "roofline": roof,
+           "cpu_baseline": None}
+    if cpu_budget:
+        if base is None:
+            xs = x[: min(B, 256)].double().cpu().numpy()
+            us = u[: min(B, 256)].double().cpu().numpy()
+            base = cpu_baseline(pr, xs, us, cpu_budget)
+            base["value"] = base["value"] / B  # trajectory-iterations/s → batched it/s
+            base["unit"] = f"batched iterations/s (batch={B})"
+        res["cpu_baseline"] = base
+    s.close()
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=100)
@@ -77,105 +180,12 @@ def main():
     ap.add_argument("--dynamics", default="auto", choices=["auto", "rnea", "closed_form"],
                     help="the chain handle's dynamics evaluator (ilqr_chain_set_dynamics)")
     args = ap.parse_args()
-    B, T = args.batch, args.T
-    dt = torch.float32 if args.dtype == "f32" else torch.float64
-    dev = torch.device("cuda", 0)
-    pr = rbd_2dof_problem(args.nu)
-    x0 = rbd_initial_states(B, 2)
     base = None
     for lin in args.lin.split(","):
-        s = ChainSolver(pr, T, B, dtype=dt, linearization=lin)
-        s.set_dynamics(args.dynamics)
-        u = torch.zeros((B, T, pr.nu), dtype=dt, device=dev)
-        x = s.rollout(torch.from_numpy(x0).to(dev, dt), u)
-        xn, un = torch.empty_like(x), torch.empty_like(u)
-        pc = torch.empty((B,), dtype=dt, device=dev)
-        st = torch.zeros((B,), dtype=torch.int32, device=dev)
-        trials = torch.empty((B,), dtype=torch.int32, device=dev)
-        opts = _lib.default_options(tol=-1.0)
-        stream = torch.cuda.current_stream(dev)
-        s._bind()
-
-        def step():
-            s.iterate(x, u, xn, un, None, st, pc, trials=trials, options=opts)
-
-        for _ in range(args.warmup):
-            step()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        ms_ev = timed(step, args.steps, stream)
-        ms = max(ms_ev, (time.perf_counter() - t0) * 1000.0 / args.steps)
-        ok = bool((st == 0).all().item())
-        # per-kernel times and the roofline object (algorithmic FLOPs, tools/flops.py)
-        d = torch.empty((B, T, pr.nu), dtype=dt, device=dev)
-        K = torch.empty((B, T, pr.nu, pr.nx), dtype=dt, device=dev)
-        A = torch.empty((B, T, pr.nx, pr.nx), dtype=dt, device=dev)
-        Bm = torch.empty((B, T, pr.nx, pr.nu), dtype=dt, device=dev)
-        o = _lib.default_options()
-        import ctypes as C
-        P = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
-        lin_fn = lambda: s.lib.ilqr_chain_linearize(s.h, P(x), P(u), P(A), P(Bm))  # noqa: E731
-        bw = lambda: s.lib.ilqr_chain_backward(s.h, C.byref(o), P(x), P(u), P(d), P(K), None)  # noqa: E731
-        pinf = torch.full((B,), float("inf"), dtype=dt, device=dev)
-        nc = torch.empty_like(pinf)
-        fw = lambda: s.lib.ilqr_chain_forward(s.h, C.byref(o), P(x), P(u), None, P(d), P(K), P(pinf),  # noqa: E731
-                                              P(xn), P(un), P(nc), None, None)
-        for fn in (lin_fn, bw, fw):
-            fn()
-        lin_ms = timed(lin_fn, args.steps, stream)
-        bw_ms = timed(bw, args.steps, stream)   # ilqr_chain_backward = linearise + Riccati
-        fw_ms = timed(fw, args.steps, stream)
-        nd = pr.nx + pr.nu
-        # algorithmic FLOPs of the evaluator that runs: the closed form's own count
-        # (pricing it on the recursion's 16x larger count put the linearisation above peak)
-        f_ref = FL.chain_dynamics_flops(pr)
-        f_rk4 = FL.chain_closed_form_flops(pr.nu) if s.dynamics_mode == "closed_form" else f_ref
-        lin_fl = (f_rk4 * FL.dual_factor(nd) if lin == "dual" else 2 * nd * f_rk4 + nd * pr.nx) * T * B
-        ric_fl = FL.riccati_flops_per_step(pr.nx, pr.nu) * T * B
-        fw_fl = FL.forward_flops_per_step(pr.nx, pr.nu, f_rk4) * T * B
-        peak = PEAK_TFLOPS[args.dtype]
-        kern = {"linearize": (lin_ms, lin_fl), "riccati": (max(bw_ms - lin_ms, 1e-6), ric_fl),
-                "forward": (fw_ms, fw_fl)}
-        roof = {"bound": ("forward latency/issue (a dependent RK4 chain per trajectory, 4 candidate lanes each, "
-                          "closed-form dynamics)"
-                          if s.dynamics_mode == "closed_form" else
-                          "forward latency/issue (16 lanes per trajectory)") + ", linearisation VALU issue",
-                "unit": "TFLOP/s", "peak": peak, "peak_dtype": args.dtype,
-                "flops_note": (f"RK4 of the closed form = {f_rk4} flop; of the restated RBD recursion "
-                               f"(the reference's RigidBodyDynamics.jl calls) = {f_ref} flop (tools/flops.py)"
-                               if f_rk4 != f_ref else
-                               f"RK4 of the restated RBD formulas = {f_rk4} flop (tools/flops.py)")}
-        for k, (ms_k, fl) in kern.items():
-            roof[k] = {"avg_launch_ms": ms_k, "algorithmic_flops": fl,
-                       "achieved": fl / (ms_k * 1e-3) / 1e12, "frac": fl / (ms_k * 1e-3) / 1e12 / peak}
-        roof["achieved"], roof["frac"] = roof["forward"]["achieved"], roof["forward"]["frac"]
-        # the forward's real bound: T dependent RK4 steps per trajectory (4 line-search
-        # candidate lanes each: 4B of the chip's 65,536 lanes), so its time is T × the
-        # latency of one step — the FLOP fraction is small by construction
-        roof["forward"]["step_latency_ns"] = fw_ms * 1e6 / T
-        roof["forward"]["lanes_busy_frac"] = min(1.0, 4 * B / (1024 * 64))
-        res = {"metric": f"batched iLQR iterations/sec (fwd+bwd pass), RBD 2-DoF arm fixed base, "
-                         f"nx=4 nu={pr.nu} T={T}",
-               "value": 1000.0 / ms, "unit": f"batched iterations/s (batch={B})", "n_gpus": 1,
-               "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms,
-               "higher_is_better": True, "dtype": args.dtype, "data": "synthetic x0 ~ U(-1,1)",
-               "config": {"workload": "BASELINE config 5 (RBD_2_link_example, fixed base)",
-                          "batch": B, "T": T, "linearization": lin, "dynamics": s.dynamics_mode,
-                          "closed_form_check": s.closed_form_error},
-               "traj_iters_per_s": B * 1000.0 / ms,
-               "mean_line_search_trials": float(trials.double().mean().item()), "all_ok": ok,
-               "roofline": roof,
-               "cpu_baseline": None}
-        if not args.no_cpu:
-            if base is None:
-                xs = x[: min(B, 256)].double().cpu().numpy()
-                us = u[: min(B, 256)].double().cpu().numpy()
-                base = cpu_baseline(pr, xs, us, args.cpu_budget)
-                base["value"] = base["value"] / B  # trajectory-iterations/s → batched it/s
-                base["unit"] = f"batched iterations/s (batch={B})"
-            res["cpu_baseline"] = base
+        res = measure(lin, args.batch, args.T, args.nu, args.dtype, args.steps, args.warmup,
+                      dynamics=args.dynamics, cpu_budget=None if args.no_cpu else args.cpu_budget, base=base)
+        base = res["cpu_baseline"]
         print(json.dumps(res), flush=True)
-        s.close()
 
 
 if __name__ == "__main__":

@@ -40,20 +40,11 @@ def timed(fn, n, stream):
     return e0.elapsed_time(e1) / n
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=500)
-    ap.add_argument("--batch", type=int, default=1024)
-    ap.add_argument("--T", type=int, default=50)
-    ap.add_argument("--nu", type=int, default=1, choices=[1, 2],
-                    help="1 = BASELINE config 2 as stated (f(x, [u1, 0])); 2 = the reference's shape")
-    ap.add_argument("--cpu-budget", type=float, default=10.0)
-    ap.add_argument("--no-cpu", action="store_true")
-    args = ap.parse_args()
-    B, T, NU = args.batch, args.T, args.nu
-    dev = torch.device("cuda", 0)
-    s = Solver(4, NU, T, B, kind=_lib.PROBLEM_TWO_LINK)
+def measure(B=1024, T=50, NU=1, steps=200, warmup=500, device=0, cpu_budget=None):
+    """Config 2's fit-iteration rate and per-kernel roofline (one dict; bench.py's
+    secondary_configs calls this after its headline, outside the headline's timed region)."""
+    dev = torch.device("cuda", device)
+    s = Solver(4, NU, T, B, device=device, kind=_lib.PROBLEM_TWO_LINK)
     x0 = two_link_initial_states(B)
     u = torch.zeros((B, T, NU), dtype=torch.float64, device=dev)
     x = s.rollout(torch.from_numpy(x0).to(dev), u)
@@ -68,12 +59,12 @@ def main():
     def step():
         s.iterate(x, u, xn, un, None, st, trials=trials, options=opts, new_cost=pc)
 
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         step()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    ms_ev = timed(step, args.steps, stream)
-    ms_wall = (time.perf_counter() - t0) * 1000.0 / args.steps
+    ms_ev = timed(step, steps, stream)
+    ms_wall = (time.perf_counter() - t0) * 1000.0 / steps
     ms = max(ms_ev, ms_wall)
 
     d = torch.empty((B, T, NU), dtype=torch.float64, device=dev)
@@ -81,13 +72,13 @@ def main():
     o = _lib.default_options()
     bw = lambda: s.lib.ilqr_backward(s.h, s._p(), C.byref(o), _ptr(x), _ptr(u), _ptr(d), _ptr(K), None)
     bw()
-    bw_ms = timed(bw, args.steps, stream)
+    bw_ms = timed(bw, steps, stream)
     pinf = torch.full((B,), float("inf"), dtype=torch.float64, device=dev)
     nc = torch.empty_like(pinf)
     fw = lambda: s.lib.ilqr_forward(s.h, s._p(), C.byref(o), _ptr(x), _ptr(u), None, _ptr(d), _ptr(K),
                                     _ptr(pinf), _ptr(xn), _ptr(un), _ptr(nc), None, None)
     fw()
-    fw_ms = timed(fw, args.steps, stream)
+    fw_ms = timed(fw, steps, stream)
 
     # algorithmic FLOPs (tools/flops.py): linearise = dual RK4 over 4+NU directions,
     # backward = the Riccati step count, forward = one trial (1 on a cold start)
@@ -114,8 +105,8 @@ def main():
     roof["forward"]["lanes_busy_frac"] = min(1.0, 4 * B / (1024 * 64))
     out = {
         "metric": f"batched iLQR iterations/sec (fwd+bwd pass), 2-link arm nx=4 nu={NU} T={T}, batch={B}",
-        "value": 1000.0 / ms, "unit": "batched iterations/s (batch=1024)", "n_gpus": 1,
-        "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True,
+        "value": 1000.0 / ms, "unit": f"batched iterations/s (batch={B})", "n_gpus": 1,
+        "steps": steps, "warmup": warmup, "ms_per_step": ms, "higher_is_better": True,
         "dtype": "f64", "data": "synthetic: x0 = default_rng(b).random(4), u0 = 0, rollout",
         "config": {"workload": "2-link arm fit iteration (cold start)", "T": T, "batch": B, "nu": NU,
                    "variant": "reference shape" if NU == 2 else "f(x, [u1, 0]), build-defined, not reference-pinned"},
@@ -125,15 +116,30 @@ def main():
         "mean_trials": float(trials.double().mean()), "all_ok": bool((st == 0).all()),
         "cpu_baseline": None,
     }
-    if not args.no_cpu:
+    if cpu_budget:
         try:
             from oracle import cref
-            out["cpu_baseline"] = cref.twolink_cpu_baseline(x.cpu().numpy(), u.cpu().numpy(), B,
-                                                            args.cpu_budget)
+            out["cpu_baseline"] = cref.twolink_cpu_baseline(x.cpu().numpy(), u.cpu().numpy(), B, cpu_budget)
         except Exception as e:
             out["cpu_baseline"] = {"error": repr(e)}
-    print(json.dumps(out), flush=True)
     s.close()
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=500)
+    ap.add_argument("--batch", type=int, default=1024)
+    ap.add_argument("--T", type=int, default=50)
+    ap.add_argument("--nu", type=int, default=1, choices=[1, 2],
+                    help="1 = BASELINE config 2 as stated (f(x, [u1, 0])); 2 = the reference's shape")
+    ap.add_argument("--cpu-budget", type=float, default=10.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+    out = measure(args.batch, args.T, args.nu, args.steps, args.warmup,
+                  cpu_budget=None if args.no_cpu else args.cpu_budget)
+    print(json.dumps(out), flush=True)
 
 
 if __name__ == "__main__":

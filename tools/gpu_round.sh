@@ -26,13 +26,13 @@ case $WHAT in
   ls) step pytest_ls 400 python -u -m pytest tests/test_gpu_line_search.py -m gpu -x -v --timeout 200 --timeout-method thread ;;
   cfg) step pytest_cfg 400 python -u -m pytest tests/test_gpu_configs.py -m gpu -x -v -s --timeout 200 --timeout-method thread ;;
   smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
-  prof) step rocprof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 50 --warmup 300 --no-cpu ;;
+  prof) step rocprof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 50 --warmup 300 --no-cpu --no-secondary ;;
   ablate) step ablate 120 ./tools/ablate_bw ;;
   dist2) ILQR_DIST_BACKEND=gloo step dist2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 2 --steps 5 --warmup 1 --no-cpu ;;
-  pmc) step pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- python bench.py --steps 5 --warmup 1 --no-cpu
-       step pmc_write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run -- python bench.py --steps 5 --warmup 1 --no-cpu
+  pmc) step pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- python bench.py --steps 5 --warmup 1 --no-cpu --no-secondary
+       step pmc_write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run -- python bench.py --steps 5 --warmup 1 --no-cpu --no-secondary
        python profiles/collect_pmc.py gpurun_out/pmc_fetch gpurun_out/pmc_write gpurun_out/pmc.json > gpurun_out/pmc_summary.log 2>&1 ;;
-  mfma) step pmc_mfma 300 rocprofv3 --pmc MfmaUtil MfmaFlopsF64 SQ_INSTS_VALU_MFMA_F64 SQ_INSTS_VALU GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d gpurun_out/pmc_mfma -o run -- python bench.py --steps 5 --warmup 1 --no-cpu
+  mfma) step pmc_mfma 300 rocprofv3 --pmc MfmaUtil MfmaFlopsF64 SQ_INSTS_VALU_MFMA_F64 SQ_INSTS_VALU GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d gpurun_out/pmc_mfma -o run -- python bench.py --steps 5 --warmup 1 --no-cpu --no-secondary
         python profiles/collect_mfma.py gpurun_out/pmc_mfma gpurun_out/mfma.json > gpurun_out/mfma_summary.log 2>&1 ;;
   tl) step pytest_twolink 600 python -m pytest tests/test_gpu_twolink.py -x -q ;;
   tiles) step pytest_tiles 600 python -m pytest tests/test_gpu_tiles.py -x -q ;;

@@ -26,7 +26,8 @@ int oracle_lq_fit(int Bn, int T, int n, int m, const double* A, const double* Bm
                   int* iters, int* status, int nthreads);
 int oracle_tl_fit(int Bn, int T, int nu, const double* x_init, const double* u_init, const double* xtraj,
                   int max_iter, double tol, double mu, int sym, int max_trials, double* x_out, double* u_out,
-                  double* cost, int* iters, int* status, int nthreads);
+                  double* cost, int* iters, int* status, int nthreads, double* hcost, int* htrials,
+                  double* hdu2);
 int oracle_tiles_backward(int Bn, int T, int n, int m, const double* A, const double* Bm, const double* lx,
                           const double* lu, const double* lxx, const double* lux, const double* luu,
                           const double* lfx, const double* lfxx, double mu, int sym, double* d, double* K,
@@ -102,7 +103,7 @@ static void two_link_case(int Bn, int T, int nu, int nthreads) {
   int *it = (int*)calloc(Bn, sizeof(int)), *st = (int*)calloc(Bn, sizeof(int));
   for (int b = 0; b < Bn; ++b)
     for (int t = 0; t <= T; ++t) { x[b * xs + t * 4] = 0.1 * unif(); x[b * xs + t * 4 + 1] = -0.1; }
-  oracle_tl_fit(Bn, T, nu, x, u, NULL, 30, 1e-6, 0.01, 1, 64, xo, uo, cost, it, st, nthreads);
+  oracle_tl_fit(Bn, T, nu, x, u, NULL, 30, 1e-6, 0.01, 1, 64, xo, uo, cost, it, st, nthreads, NULL, NULL, NULL);
   for (int b = 0; b < Bn; ++b) CHECK(st[b] >= 1 && st[b] <= 3, "tl_fit nu=%d b=%d st=%d", nu, b, st[b]);
   free(x); free(u); free(xo); free(uo); free(cost); free(it); free(st);
 }
