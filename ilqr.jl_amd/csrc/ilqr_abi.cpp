@@ -164,6 +164,7 @@ ilqr_status enqueue_iteration(ilqr_handle* h, const ilqr_problem* p, const ilqr:
       // sequential-search launch between two cooperative ones must not advance the
       // generation, or the next cooperative launch would count in a half nobody zeroed
       ac.coop = h->coop ? h->coop_dev : nullptr;
+      ac.coop_ctl = h->coop ? h->coop_ctl : nullptr;
       ac.coop_gen = h->coop ? ++h->coop_gen : h->coop_gen;
       HIP_TRY(ilqr::launch_lq_iter_fused4(P, h->batch, h->T, ac, ls, h->stream, h->fw_mfma));
       return ILQR_OK;

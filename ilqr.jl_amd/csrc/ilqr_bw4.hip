@@ -447,8 +447,7 @@ __global__ __launch_bounds__(64 * FUSED_WAVES) void lq_iter_fused4_kernel(LQPara
   IterArgs ai = a;
   if (a.coop && wid == 0 && l == 0) {
     // the next launch's list length (this launch counts in ctl[gen & 1])
-    int32_t* ctl = a.coop->ctl;
-    __hip_atomic_store(ctl + ((a.coop_gen + 1) & 1), 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(a.coop_ctl + ((a.coop_gen + 1) & 1), 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   if (b0 < B) {
     if (a.init) {

@@ -69,7 +69,9 @@ struct IterArgs {
   const LSCoop* coop;   // the fused LQ kernel's cooperative line search (device memory, one
                         // per handle; read only when the search starts, so its pointers
                         // hold no SGPRs through the backward pass); nullptr: off
-  uint32_t coop_gen;    // the launch's generation (per handle, counts fused launches)
+  uint32_t coop_gen;    // the launch's generation (per handle, counts cooperative launches)
+  int32_t* coop_ctl;    // == coop->ctl, in the kernel arguments: a wave's exit test at the end
+                        // of its own work is ONE load (no dependent load of *coop first)
 };
 
 // Returns hipSuccess or the launch error. All launches are asynchronous on `s`.

@@ -41,12 +41,12 @@ case $WHAT in
   chain) step pytest_chain 600 python -u -m pytest tests/test_gpu_chain.py -x -v --timeout 120 --timeout-method thread ;;
   rbdbench) step bench_rbd 300 python tools/bench_rbd.py ;;
   rbdprof) step rocprof_rbd 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_rbd -o run --output-format csv -- python tools/bench_rbd.py --steps 20 --warmup 5 --no-cpu ;;
-  rcp) step rcp 60 ./tools/rcp_test ;;
   fit5) step tail_probe 200 python tools/tail_probe.py
         step rocprof_fit5 200 rocprofv3 --kernel-trace -d gpurun_out/prof_fit5 -o run --output-format csv -- python tools/fit5_trace.py ;;
   tailcap) MODES=coop MAXT=16 step tail_cap16 200 python tools/tail_probe.py
            MODES=coop MAXT=32 step tail_cap32 200 python tools/tail_probe.py
            MODES=coop MAXT=64 step tail_cap64 200 python tools/tail_probe.py ;;
   ubench) step ubench 120 ./tools/ubench_f64 ;;
+  ilp) step tl_ilp 120 ./tools/tl_ilp_probe ;;
 esac
 done
