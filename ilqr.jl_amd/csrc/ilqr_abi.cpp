@@ -163,9 +163,13 @@ ilqr_status enqueue_iteration(ilqr_handle* h, const ilqr_problem* p, const ilqr:
       // only a launch that gets the list also re-arms it (ctl[(gen + 1) & 1] = 0): a
       // sequential-search launch between two cooperative ones must not advance the
       // generation, or the next cooperative launch would count in a half nobody zeroed
-      ac.coop = h->coop ? h->coop_dev : nullptr;
-      ac.coop_ctl = h->coop ? h->coop_ctl : nullptr;
-      ac.coop_gen = h->coop ? ++h->coop_gen : h->coop_gen;
+      // Against prev_cost = +Inf (a cold iteration, fit's first) trial 1 accepts every
+      // finite cost (forward_pass.jl:77-80): nothing would be published, so the launch
+      // runs the sequential search (the same bits) without the search's exit test.
+      const bool coop = h->coop && a.prev_cost && !a.init;
+      ac.coop = coop ? h->coop_dev : nullptr;
+      ac.coop_ctl = coop ? h->coop_ctl : nullptr;
+      ac.coop_gen = coop ? ++h->coop_gen : h->coop_gen;
       HIP_TRY(ilqr::launch_lq_iter_fused4(P, h->batch, h->T, ac, ls, h->stream, h->fw_mfma));
       return ILQR_OK;
     }

@@ -157,6 +157,11 @@ def tl_fit(x_init, u_init, x_traj=None, max_iter=100, tol=1e-6, mu=0.01, max_tri
     return xo, uo, cost, iters, st
 
 
+def tl_set_target(x=0.6, y=-0.5):
+    """The 2-link target_tool_loc of the C restatement (test-only; default the script's)."""
+    load().oracle_tl_set_target(C.c_double(x), C.c_double(y))
+
+
 def twolink_cpu_baseline(x, u, batch, budget_s):
     """bench_twolink's cpu_baseline leg: one cold-start iteration (backward +
     forward) per trajectory of the 2-link workload (nu from u), OpenMP over trajectories."""

@@ -5,14 +5,21 @@ or shipped. Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline
 leg may import it.
 
 Parity status: the reference is pure Julia and no Julia toolchain exists in
-this container or on the GPU box, so this restatement cannot be checked
-against executed reference output ("parity unpinned" against the reference
-binary). It is pinned instead by known-answer tests derived from the
-reference's own tests and algebra (tests/test_oracle.py): the repaired
-linear-f linearisation property of test/test_linearize_dynamics.jl:24-25, the
-LQ closed-form (KKT) fixed point, the 2-link IK constants of
-test/2_link_example/2_link_helper_functions.jl:16-26 and the convergence
-property `final_cost(x̄_N) < 0.01` of test/test_iLQR.jl:19.
+this container or on the GPU box, so the reference cannot be run here. Its one
+recorded EXECUTED output is pinned instead: the animations
+test/2_link_example/animate_2_link.jl saved when its authors ran it (shipped in
+test/2_link_example/figures/, 91 frames of the T = 900 2-link fit each; frames
+extracted into tests/golden/reference_gifs.npz by tests/golden/make_gif_golden.py).
+The C restatement's fit of that workload reproduces every frame of the shipped
+script's GIF within a third of a pixel (elbow and tool ≤ 0.0035 data units,
+tests/test_reference_gifs.py), and this Python restatement equals the C one on the
+same workload (1e-9). Beyond that the restatements are pinned by known-answer tests
+derived from the reference's own tests and algebra (tests/test_oracle.py): the
+repaired linear-f linearisation property of test/test_linearize_dynamics.jl:24-25,
+the LQ closed-form (KKT) fixed point, the 2-link IK constants of
+test/2_link_example/2_link_helper_functions.jl:16-26 and the convergence property
+`final_cost(x̄_N) < 0.01` of test/test_iLQR.jl:19. The LQ family (the headline) has
+no executed reference output anywhere: there the pin is the algebra (KKT) only.
 
 Layout: one trajectory per call, row-per-timestep exactly like the reference:
 x is (N, n), u is (T, m) with N = T + 1, δu is (T, m), K is (T, m, n).

@@ -205,6 +205,17 @@ static void tl_init(void) {
   done = 1;
 }
 
+/* test-only: another target_tool_loc (2_link_helper_functions.jl:16) — the reference's
+ * shipped animations of the other quadrants (tests/test_reference_gifs.py); the script's
+ * own (0.6, −0.5) is the default. Not thread-safe against running fits. */
+void oracle_tl_set_target(double x, double y) {
+  tl_init();
+  const double l1 = sqrt(2.) / 2., l2 = sqrt(2.) / 2.;
+  const double q2 = acos((x * x + y * y - l1 * l1 - l2 * l2) / (2 * l1 * l2));  /* :22-23 */
+  TL.tgt0 = atan2(y, x) - atan2(l2 * sin(q2), l1 + l2 * cos(q2));
+  TL.tgt1 = q2;
+}
+
 /* continuous_dynamics (:51-69) on duals */
 static void tl_cd_dual(const dual6* x, const dual6* u, dual6* xd) {
   const dual6 c2 = dcos(x[1]), s2 = dsin(x[1]);

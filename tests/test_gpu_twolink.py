@@ -199,7 +199,9 @@ def test_tl_animate_workload_vs_c_oracle(gpu):
     """The reference's end-to-end example, animate_2_link.jl:7-25: x₀ = [.1, −.1, 0, 0],
     u₀ = 0, x_init the rollout of u₀, T = 900, tol = 1e-6, max_iter = 10⁶ — fit on the
     device against the C restatement's fit (iteration count, iterates, per-iteration cost
-    history), plus the repaired check of test_iLQR.jl:19: final_cost(x̄_N) < 0.01."""
+    history), the repaired check of test_iLQR.jl:19 (final_cost(x̄_N) < 0.01), and every
+    frame of the animation the reference saved from this run (elbow and tool within
+    0.01, under a pixel)."""
     T = 900
     s = tl_solver(T, 1)
     u0 = np.zeros((1, T, 2))
@@ -212,6 +214,12 @@ def test_tl_animate_workload_vs_c_oracle(gpu):
     th = TwoLinkArm.inverse_kinematics()
     xN = r.x[0, -1].cpu().numpy()
     assert float(np.sum((th - xN[:2]) ** 2)) < 0.01
+    # and against the reference's EXECUTED output: the animation this very script saved
+    # (figures/iLQR_2_link_quad_4.gif, 91 frames t = 1:10:901; tests/test_reference_gifs.py)
+    import test_reference_gifs as G
+    z = np.load(G.GOLD, allow_pickle=False)
+    de, dt = G.frame_error(r.x[0, ::10, :2].cpu().numpy(), z["quad_4_theta"])
+    assert de < G.TOL and dt < G.TOL, (de, dt)
 
 
 def test_tl_test_iLQR_workload_vs_c_oracle(gpu):

@@ -1,0 +1,127 @@
+"""The oracle pinned against the reference's EXECUTED output: the animations
+test/2_link_example/animate_2_link.jl saved when its authors ran it (shipped in
+/root/reference/test/2_link_example/figures/; frames extracted into
+tests/golden/reference_gifs.npz by tests/golden/make_gif_golden.py).
+
+Each GIF is iLQR.fit's result for the 2-link arm — T = 900, x₀ = [.1, −.1, 0, 0], u₀ = 0
+and its rollout, tol = 1e-6 (animate_2_link.jl:7-25) — drawn at every 10th state
+(t = 1:10:901, 91 frames). quad_4 is the script as shipped (its save_loc; target_tool_loc
+= [0.6, −0.5], 2_link_helper_functions.jl:16): the C restatement's fit (oracle/ilqr_ref.c,
+the checker of every GPU test) must reproduce every frame — elbow and tool within TOL =
+0.01 data units ≈ 0.9 px; measured ≤ 0.0035, a third of a pixel. quad_1..3 (the target in
+the other quadrants) and iLQR_2_link.gif (an earlier copy) come from edited copies of the
+script whose other settings are not recorded: they end on their targets and follow the
+oracle's fits within TOL_EDITED = 0.025 (measured ≤ 0.019, ≈1.7 px, during the fast first
+second; ≤ 0.0073 for iLQR_2_link.gif). The pin discriminates: the open-loop rollout misses
+by 1.0 and the fit stopped after two of its iterations by several pixels.
+
+The GPU path is checked against the same frames in tests/test_gpu_twolink.py.
+"""
+import json
+import math
+import os
+
+import numpy as np
+import pytest
+
+from oracle import cref
+from oracle import ilqr_oracle as O
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden", "reference_gifs.npz")
+TOL = 0.01  # data units (the plot's 4 units span ≈353 px: 0.01 ≈ 0.9 px)
+TOL_EDITED = 0.025
+L = math.sqrt(2.0) / 2.0
+TARGETS = {"quad_4": (0.6, -0.5), "quad_1": (0.6, 0.5), "quad_2": (-0.6, 0.5), "quad_3": (-0.6, -0.5)}
+
+
+@pytest.fixture(scope="module")
+def gifs():
+    z = np.load(GOLD, allow_pickle=False)
+    return {k: z[k] for k in z.files}, json.loads(str(z["meta"]))
+
+
+def arm_points(th):
+    e = np.stack([L * np.cos(th[:, 0]), L * np.sin(th[:, 0])], 1)
+    t = e + np.stack([L * np.cos(th[:, 0] + th[:, 1]), L * np.sin(th[:, 0] + th[:, 1])], 1)
+    return e, t
+
+
+def frame_error(theta_fit, theta_gif):
+    """Max over frames of the elbow / tool distance (data units) between a fit's states
+    t = 1:10:901 and the GIF's."""
+    e1, t1 = arm_points(theta_fit)
+    e2, t2 = arm_points(theta_gif)
+    return float(np.hypot(*(e1 - e2).T).max()), float(np.hypot(*(t1 - t2).T).max())
+
+
+def animate_x_init(T=900):
+    x = np.zeros((1, T + 1, 4))
+    x[0, 0] = [0.1, -0.1, 0.0, 0.0]
+    for t in range(T):   # animate_2_link.jl:11-16: the rollout of u = 0
+        x[0, t + 1] = O.TwoLink.dynamicsf(x[0, t], np.zeros(2))
+    return x
+
+
+def c_oracle_fit(target=(0.6, -0.5)):
+    cref.tl_set_target(*target)
+    try:
+        x = animate_x_init()
+        xo, uo, co, it, st = cref.tl_fit(x, np.zeros((1, 900, 2)), max_iter=10**6, tol=1e-6, symmetrize=True)
+    finally:
+        cref.tl_set_target()
+    assert st[0] == 1, st   # converged
+    return xo[0]
+
+
+def test_fixture_is_the_shipped_script(gifs):
+    g, meta = gifs
+    assert meta["T"] == 900 and meta["stride"] == 10
+    for key, tgt in TARGETS.items():
+        assert g[key + "_theta"].shape == (91, 2)
+        # each animation ends at its target (the fit's final tool position)
+        assert np.hypot(*(np.array(meta["gifs"][key]["final_tool"]) - tgt)) < TOL, key
+        # the polyline fits the drawn arm to ~1.5 px RMS (the stroke is 5 px wide)
+        assert g[key + "_rms_px"].max() < 2.5, key
+
+
+def test_c_oracle_fit_reproduces_reference_animation(gifs):
+    """The shipped script's own output, every frame within a pixel."""
+    g, _ = gifs
+    xo = c_oracle_fit(TARGETS["quad_4"])
+    de, dt = frame_error(xo[::10, :2], g["quad_4_theta"])
+    assert de < TOL and dt < TOL, (de, dt)
+
+
+@pytest.mark.parametrize("key", ["quad_1", "quad_2", "quad_3", "ilqr_2_link"])
+def test_c_oracle_fit_follows_edited_script_animations(gifs, key):
+    g, _ = gifs
+    xo = c_oracle_fit(TARGETS.get(key, (0.6, -0.5)))
+    de, dt = frame_error(xo[::10, :2], g[key + "_theta"])
+    assert de < TOL_EDITED and dt < TOL_EDITED, (key, de, dt)
+
+
+def test_gif_pin_discriminates(gifs):
+    """The frames tell the script's own fit apart from nearby alternatives."""
+    g, _ = gifs
+    ref = g["quad_4_theta"]
+    x = animate_x_init()
+    de, dt = frame_error(x[0, ::10, :2], ref)               # no fit: the open-loop rollout
+    assert dt > 50 * TOL
+    xo = c_oracle_fit((0.6, -0.5))
+    # a different fit: stopped after 2 of its iterations
+    x2, _, _, _, _ = cref.tl_fit(x, np.zeros((1, 900, 2)), max_iter=2, tol=1e-6, symmetrize=True)
+    assert max(frame_error(x2[0, ::10, :2], ref)) > 3 * TOL
+    assert max(frame_error(xo[::10, :2], ref)) < TOL
+
+
+def test_python_oracle_agrees_with_c_on_the_animation(gifs):
+    """The literal Python restatement (ForwardDiff restated by oracle.dual) on the same
+    workload, first iterations: its iterates equal the C restatement's — so both
+    restatements inherit the pin (the full fit is minutes in pure Python)."""
+    x = animate_x_init(T=900)
+    u = np.zeros((900, 2))
+    TL = O.TwoLink
+    xp, up = O.fit(x[0], u, TL.dynamicsf, TL.immediate_cost, TL.final_cost, max_iter=1, tol=1e-6,
+                   symmetrize=True)[:2]
+    xc, uc, _, _, _ = cref.tl_fit(x, u[None], max_iter=1, tol=1e-6, symmetrize=True)
+    assert np.abs(up - uc[0]).max() < 1e-9 * max(1.0, np.abs(uc).max())
