@@ -615,7 +615,7 @@ def main():
         "allgather_check": gathered,
         "cpu_baseline": None,
     }
-    if rank == 0 and not args.no_cpu:
+    if rank == 0 and world == 1 and not args.no_cpu:  # the CPU baseline: rank 0 at N = 1 only
         try:
             result["cpu_baseline"] = cpu_baseline(lq, x0, u0, args.cpu_budget)
         except Exception as e:  # the baseline is reported, never required
