@@ -168,12 +168,19 @@ def secondary_configs(device):
     """BASELINE config 2 (2-link arm nu = 1, B = 1024, T = 50, fp64) and config 5 (RBD
     2-DoF arm, fp32, central differences, B = 2048, T = 100): one cold-start fit iteration
     per step, HIP events; each with its forward's step latency and lane occupancy."""
+    from ilqr_amd.chain import coupled_2dof_problem
     from tools import bench_rbd, bench_twolink
     out = {}
     for name, fn in (("config2_twolink_nu1_B1024_T50_f64",
                       lambda: bench_twolink.measure(1024, 50, 1, steps=200, warmup=300, device=device)),
                      ("config5_rbd_2dof_fd_f32_B2048_T100",
-                      lambda: bench_rbd.measure("fd", 2048, 100, 1, "f32", steps=100, warmup=100, device=device))):
+                      lambda: bench_rbd.measure("fd", 2048, 100, 1, "f32", steps=100, warmup=100, device=device)),
+                     # the same step on the coupled 2-joint chain (tilted joint, offset COMs,
+                     # gravity): the reference's 2Dof_arm.urdf has a constant mass matrix and
+                     # no bias, so config 5 alone does not exercise q-dependent dynamics
+                     ("config5_shape_coupled_chain_fd_f32_B2048_T100",
+                      lambda: bench_rbd.measure("fd", 2048, 100, 1, "f32", steps=100, warmup=100, device=device,
+                                                problem=coupled_2dof_problem(1)))):
         try:
             r = fn()
             fw = r["roofline"]["forward"]

@@ -63,13 +63,15 @@ def cpu_baseline(pr, x, u, budget_s):
 
 
 def measure(lin="fd", B=2048, T=100, nu=1, dtype="f32", steps=100, warmup=100, device=0,
-            dynamics="auto", cpu_budget=None, base=None):
+            dynamics="auto", cpu_budget=None, base=None, problem=None):
     """Config 5's fit-iteration rate and per-kernel roofline for one linearisation (one
     dict; bench.py's secondary_configs calls this after its headline, outside the
     headline's timed region)."""
     dt = torch.float32 if dtype == "f32" else torch.float64
     dev = torch.device("cuda", device)
-    pr = rbd_2dof_problem(nu)
+    # problem: another chain (the coupled 2-joint test chain: q-dependent M and bias, which
+    # the reference's 2Dof_arm.urdf parses without — constant M, zero bias)
+    pr = rbd_2dof_problem(nu) if problem is None else problem
     x0 = rbd_initial_states(B, 2)
     s = ChainSolver(pr, T, B, dtype=dt, linearization=lin, device=device)
     s.set_dynamics(dynamics)
