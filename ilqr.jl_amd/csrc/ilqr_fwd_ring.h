@@ -968,16 +968,15 @@ __device__ void lq_coop_search(const LQParams& P, int B, int T, const IterArgs& 
   const uint32_t gen = a.coop_gen;
   // the no-publication launch (every iteration from cold, most of a fit's) leaves after
   // ONE load: the list length straight from the kernel arguments
-  int n = __builtin_amdgcn_readfirstlane(ag_ld(a.coop_ctl + (gen & 1)));
-  if (n == 0) return;
+  if (__builtin_amdgcn_readfirstlane(ag_ld(a.coop_ctl + (gen & 1))) == 0) return;
   const LSCoop c = *a.coop;  // scalar loads, only once there is work
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   // 200 µs at the 100 MHz real-time counter; the Makefile's `variants` target builds a
   // library with 0 (a wave leaves at the first unwritten slot it sees) for the test of
   // this exit (tests/test_gpu_line_search.py::test_coop_timeout_exit_variant)
   constexpr uint64_t WAIT_TICKS = ILQR_COOP_WAIT_TICKS;
-  for (bool first = true;; first = false) {
-    if (!first) n = __builtin_amdgcn_readfirstlane(ag_ld(c.ctl + (gen & 1)));
+  while (true) {
+    const int n = __builtin_amdgcn_readfirstlane(ag_ld(c.ctl + (gen & 1)));
     if (n == 0) break;
     bool unwritten = false;
     const int b = coop_find(c, gen, n, ls.max_trials, (int)(((uint64_t)wid * 2654435761u) % (uint32_t)n),
