@@ -3,8 +3,10 @@
 // fit driver (src/forward_pass.jl:148-179) on top of the fused iteration kernel.
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -76,6 +78,7 @@ struct ilqr_handle {
   uint64_t* coop_list = nullptr;
   int32_t* coop_ctl = nullptr;
   uint32_t coop_gen = 0;  // fused launches so far (the list's generation tag)
+  uint32_t fit_seq = 0;   // fits so far (tags the host call-status word, wait_fit)
   ilqr::LSCoop* coop_dev = nullptr;  // the struct of the above, in device memory
   int bound[3] = {0, 0, 0};
   hipEvent_t ev_bw[2] = {nullptr, nullptr};
@@ -304,6 +307,34 @@ ilqr_status unpad_x(ilqr_handle* h, const double* px, double* x) {
 }
 ilqr_status unpad_u(ilqr_handle* h, const double* pu, double* u) {
   return unpad3(h, pu, u, (size_t)h->batch, h->T, h->nu, h->T, PAD_NU);
+}
+
+// The end of a fit. The stream's last kernel (gather_flags_kernel) stores this fit's number
+// into the host-mapped call-status word as it runs, so the host spins on that word (no
+// runtime wake-up: the blocking stream sync cost ≈20 µs of host turnaround per fit at the
+// headline, profiles/r04/trace_fit_gaps_second_r04.txt), then synchronises the stream —
+// already drained, that returns at once — so the runtime's view is exact before the call
+// returns. A long fit spins at most FIT_SPIN_US before the plain sync. ILQR_FIT_WAIT=sync
+// in the environment restores the blocking sync alone (A/B).
+hipError_t wait_fit(ilqr_handle* h, uint32_t seq, hipStream_t s) {
+  static const bool spin = [] {
+    const char* e = getenv("ILQR_FIT_WAIT");
+    return !(e && strcmp(e, "sync") == 0);
+  }();
+  if (spin) {
+    constexpr int64_t FIT_SPIN_US = 20000;
+    const volatile int32_t* w = h->host_running + 2;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t k = 0;; ++k) {
+      if (((uint32_t)__atomic_load_n(w, __ATOMIC_ACQUIRE) >> 2) == seq) break;
+      if ((k & 255u) == 255u &&
+          std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0).count() >
+              FIT_SPIN_US)
+        break;
+      __builtin_ia32_pause();
+    }
+  }
+  return hipStreamSynchronize(s);
 }
 
 }  // namespace
@@ -773,11 +804,13 @@ ilqr_status ilqr_fit_ex(ilqr_handle* h, const ilqr_problem* p, const ilqr_option
   // still-running trajectories (max_iter reached) return the last accepted iterate,
   // the one the last iteration wrote (the input when max_iter = 0)
   const int last = o->max_iter == 0 ? ilqr::PARITY_INPUT : (direct ? ilqr::PARITY_OUT : (o->max_iter & 1));
+  uint32_t seq = (++h->fit_seq) & 0x3fffffffu;
+  if (seq == 0) seq = h->fit_seq = 1;  // 0 is the word's cleared value
   HIP_TRY(ilqr::launch_gather_result(h->batch, h->T, h->nx, h->nu, x_init, u_init, h->xbuf[0],
                                      h->ubuf[0], h->xbuf[1], h->ubuf[1], h->res_parity, h->status,
                                      last, h->prev_cost, h->iters, x_out, u_out, cost, iters,
-                                     status, h->dev_flags, h->dev_running + 2, s));
-  HIP_TRY(hipStreamSynchronize(s));
+                                     status, h->dev_flags, h->dev_running + 2, s, seq));
+  HIP_TRY(wait_fit(h, seq, s));
   const int32_t f = __atomic_load_n(h->host_running + 2, __ATOMIC_ACQUIRE);
   return (f & 1) ? ILQR_ERR_NAN : ((f & 2) ? ILQR_ERR_LS_EXHAUSTED : ILQR_OK);
 }

@@ -123,14 +123,14 @@ hipError_t launch_fit_init(int B, double* prev_cost, int32_t* status, int32_t* r
 // x_out[b] = the buffer res_parity[b] names (final_parity for still-running ones,
 // whose status becomes MAX_ITER), and u; cost/iters/status copied out (each may be
 // null). The call-status bits go through dflags (two zeroed device words, re-armed by
-// the kernel) into `flags` (host-mapped, may be null).
+// the kernel) into `flags` (host-mapped, may be null) as (seq << 2) | bits.
 hipError_t launch_gather_result(int B, int T, int nx, int nu, const double* xin, const double* uin,
                                 const double* x0, const double* u0, const double* x1,
                                 const double* u1, const int32_t* res_parity, int32_t* status,
                                 int final_parity, const double* fit_cost, const int32_t* fit_iters,
                                 double* x_out, double* u_out, double* cost_out,
                                 int32_t* iters_out, int32_t* status_out, int32_t* dflags,
-                                int32_t* flags, hipStream_t s);
+                                int32_t* flags, hipStream_t s, uint32_t seq = 0);
 // (N, R, C) row-major → (N, R2, C2) zero-padded (R2 ≥ R, C2 ≥ C), and back.
 hipError_t launch_pad3(const double* src, double* dst, size_t N, int R, int C, int R2, int C2,
                        hipStream_t s);

@@ -623,9 +623,11 @@ __global__ __launch_bounds__(256) void gather_kernel(int B, int T, int nx, int n
 
 // the gather's call-status word to the host-mapped `flags` (after gather_kernel on the
 // same stream: its atomics are complete and visible at the kernel boundary), re-armed
-__global__ void gather_flags_kernel(int32_t* dflags, int32_t* flags) {
+// `seq` tags the host word (bits 2..31): the host knows the fit's last kernel ran when
+// the word carries its fit's number (ilqr_fit_ex waits on it)
+__global__ void gather_flags_kernel(int32_t* dflags, int32_t* flags, uint32_t seq) {
   const int32_t v = __hip_atomic_load(dflags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (flags) *(volatile int32_t*)flags = v;
+  if (flags) *(volatile int32_t*)flags = (int32_t)((seq << 2) | ((uint32_t)v & 3u));
   __hip_atomic_store(dflags, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
@@ -857,14 +859,14 @@ hipError_t launch_gather_result(int B, int T, int nx, int nu, const double* xin,
                                 int final_parity, const double* fit_cost, const int32_t* fit_iters,
                                 double* x_out, double* u_out, double* cost_out,
                                 int32_t* iters_out, int32_t* status_out, int32_t* dflags,
-                                int32_t* flags, hipStream_t s) {
+                                int32_t* flags, hipStream_t s, uint32_t seq) {
   if (B <= 0) return hipSuccess;
   gather_kernel<<<(B + 3) / 4, 256, 0, s>>>(B, T, nx, nu, xin, uin, x0, u0, x1, u1, res_parity, status,
                                             final_parity, fit_cost, fit_iters, x_out, u_out, cost_out,
                                             iters_out, status_out, dflags);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  gather_flags_kernel<<<1, 1, 0, s>>>(dflags, flags);
+  gather_flags_kernel<<<1, 1, 0, s>>>(dflags, flags, seq);
   return hipGetLastError();
 }
 

@@ -48,5 +48,10 @@ case $WHAT in
            MODES=coop MAXT=64 step tail_cap64 200 python tools/tail_probe.py ;;
   ubench) step ubench 120 ./tools/ubench_f64 ;;
   ilp) step tl_ilp 120 ./tools/tl_ilp_probe ;;
+  waitab) for i in 1 2; do
+            ILQR_FIT_WAIT=sync step bench_wait_sync_$i 300 python bench.py --no-cpu --no-secondary
+            step bench_wait_spin_$i 300 python bench.py --no-cpu --no-secondary
+          done
+          for f in gpurun_out/bench_wait_*.log; do python -c "import json,sys; d=[json.loads(l) for l in open(sys.argv[1]) if l.startswith('{')][-1]; print(sys.argv[1], round(d['value'],1), round(d['fit_timing']['median_fit_ms']*1000,1), round(d['roofline']['avg_launch_ms']*1000,1))" $f; done ;;
 esac
 done
