@@ -310,12 +310,13 @@ ilqr_status unpad_u(ilqr_handle* h, const double* pu, double* u) {
 }
 
 // The end of a fit. The stream's last kernel (gather_flags_kernel) stores this fit's number
-// into the host-mapped call-status word as it runs, so the host spins on that word (no
-// runtime wake-up: the blocking stream sync cost ≈20 µs of host turnaround per fit at the
-// headline, profiles/r04/trace_fit_gaps_second_r04.txt), then synchronises the stream —
-// already drained, that returns at once — so the runtime's view is exact before the call
-// returns. A long fit spins at most FIT_SPIN_US before the plain sync. ILQR_FIT_WAIT=sync
-// in the environment restores the blocking sync alone (A/B).
+// into the host-mapped call-status word as it runs, after every earlier kernel of the
+// stream completed (in-order stream): when the word carries the number, the outputs are
+// written. The host spins on that word and returns — the runtime's blocking stream sync
+// costs ≈8 µs more per fit after the work is done (A/B in bench.py, 455 → 447 µs per
+// 3-iteration headline fit, profiles/r04/fit_wait_ab_r04.log). A fit longer than
+// FIT_SPIN_US falls back to the stream sync; ILQR_FIT_WAIT=sync in the environment forces
+// the sync (A/B).
 hipError_t wait_fit(ilqr_handle* h, uint32_t seq, hipStream_t s) {
   static const bool spin = [] {
     const char* e = getenv("ILQR_FIT_WAIT");
@@ -326,7 +327,7 @@ hipError_t wait_fit(ilqr_handle* h, uint32_t seq, hipStream_t s) {
     const volatile int32_t* w = h->host_running + 2;
     const auto t0 = std::chrono::steady_clock::now();
     for (uint32_t k = 0;; ++k) {
-      if (((uint32_t)__atomic_load_n(w, __ATOMIC_ACQUIRE) >> 2) == seq) break;
+      if (((uint32_t)__atomic_load_n(w, __ATOMIC_ACQUIRE) >> 2) == seq) return hipSuccess;
       if ((k & 255u) == 255u &&
           std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0).count() >
               FIT_SPIN_US)

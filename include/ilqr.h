@@ -241,7 +241,9 @@ ilqr_status ilqr_iterate(ilqr_handle* h, const ilqr_problem* p, const ilqr_optio
  * x_traj may be NULL. cost (batch) receives the cost of the returned iterate's
  * successor (the reference's last new_cost); iters/status (batch) may be NULL.
  * Returns ILQR_ERR_NAN / ILQR_ERR_LS_EXHAUSTED if any trajectory stopped that
- * way (others still complete). Synchronises the stream. */
+ * way (others still complete). Returns once the fit's last kernel has run: every
+ * output is written and the stream holds no more of the fit's work (the host waits
+ * on a word that kernel writes, not on the runtime's stream sync). */
 ilqr_status ilqr_fit(ilqr_handle* h, const ilqr_problem* p, const ilqr_options* o,
                      const double* x_init, const double* u_init, const double* x_traj,
                      double* x_out, double* u_out, double* cost, int32_t* iters,
