@@ -581,6 +581,24 @@ __global__ __launch_bounds__(256, 4) void lq_iter_pipe_kernel(LQParams P, int B,
   }
 }
 
+// dst[0, n) = src[0, n) by one wave: eight loads per lane in flight before their stores
+// (a load-store pair per element waits out the memory latency once per 64 elements)
+__device__ inline void wave_copy(double* __restrict__ dst, const double* __restrict__ src, int n, int l) {
+  for (int i0 = 0; i0 < n; i0 += 64 * 8) {
+    double v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int i = i0 + j * 64 + l;
+      if (i < n) v[j] = src[i];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int i = i0 + j * 64 + l;
+      if (i < n) dst[i] = v[j];
+    }
+  }
+}
+
 // One wave per trajectory (four per block). The call status (bit 0 a NaN trajectory,
 // bit 1 an exhausted line search) is OR-ed into a DEVICE word, dflags[0], with
 // relaxed device-scope atomics (only by trajectories that set a bit);
@@ -606,8 +624,8 @@ __global__ __launch_bounds__(256) void gather_kernel(int B, int T, int nx, int n
     if (par != PARITY_OUT) {  // PARITY_OUT: the last iteration wrote x_out / u_out itself
       const double* xs = (par == PARITY_INPUT ? xin : (par ? x1 : x0)) + (size_t)b * (T + 1) * nx;
       const double* us = (par == PARITY_INPUT ? uin : (par ? u1 : u0)) + (size_t)b * T * nu;
-      for (int i = l; i < (T + 1) * nx; i += 64) x_out[(size_t)b * (T + 1) * nx + i] = xs[i];
-      for (int i = l; i < T * nu; i += 64) u_out[(size_t)b * T * nu + i] = us[i];
+      wave_copy(x_out + (size_t)b * (T + 1) * nx, xs, (T + 1) * nx, l);
+      wave_copy(u_out + (size_t)b * T * nu, us, T * nu, l);
     }
     if (l == 0) {  // the lane that read status[b] is the one that rewrites it
       const int32_t st = running ? ILQR_TRAJ_MAX_ITER : st0;

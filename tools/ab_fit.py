@@ -25,5 +25,6 @@ for _ in range(300):
     t0 = time.perf_counter()
     r = s.fit(x, u, max_iter=3, tol=-1.0)
     ts.append(time.perf_counter() - t0)
-print(f"{os.path.basename(os.environ.get('ILQR_LIB', 'product'))}: 3-iteration fit median "
+print(f"{os.path.basename(os.environ.get('ILQR_LIB', 'product'))} ILQR_GATHER_WG="
+      f"{os.environ.get('ILQR_GATHER_WG', '-')}: 3-iteration fit median "
       f"{np.median(ts) * 1e3:.4f} ms (p10 {np.percentile(ts, 10) * 1e3:.4f}), call status {r.call_status}", flush=True)

@@ -53,5 +53,14 @@ case $WHAT in
             step bench_wait_spin_$i 300 python bench.py --no-cpu --no-secondary
           done
           for f in gpurun_out/bench_wait_*.log; do python -c "import json,sys; d=[json.loads(l) for l in open(sys.argv[1]) if l.startswith('{')][-1]; print(sys.argv[1], round(d['value'],1), round(d['fit_timing']['median_fit_ms']*1000,1), round(d['roofline']['avg_launch_ms']*1000,1))" $f; done ;;
+  gatherab) for i in 1 2 3; do for wg in 0 1 4 16; do
+              ILQR_GATHER_WG=$wg step ab_fit_wg${wg}_$i 120 python tools/ab_fit.py
+            done; done
+            grep -h "fit median" gpurun_out/ab_fit_wg*.log > gpurun_out/gather_ab.log; cat gpurun_out/gather_ab.log ;;
+  gathertrace) for wg in 0 4; do
+                 ILQR_GATHER_WG=$wg step trace_wg$wg 200 rocprofv3 --kernel-trace -d gpurun_out/trace_wg$wg -o run --output-format csv -- python tools/ab_fit.py
+                 python tools/trace_fit_gaps.py gpurun_out/trace_wg$wg/run_kernel_trace.csv > gpurun_out/trace_fit_gaps_wg$wg.txt 2>&1
+               done ;;
+  gtest) step pytest_gather 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_line_search.py tests/test_gpu_multi.py -m gpu -x -q --timeout 120 --timeout-method thread ;;
 esac
 done

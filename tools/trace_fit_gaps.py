@@ -38,6 +38,14 @@ def main(path):
     # per-fit tail: gather, flags, and the gap to the next fused launch
     gaps, gath, flags = [], [], []
     for i, r in enumerate(rows[:-1]):
+        if "gather_wg_kernel" in r["Kernel_Name"] and "lq_iter_fused4" in rows[i + 1]["Kernel_Name"]:
+            g = (int(rows[i + 1]["Start_Timestamp"]) - int(r["End_Timestamp"])) / 1000
+            if g < 200:
+                gaps.append(g)
+                flags.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000)
+                p = rows[i - 1]
+                gath.append((int(r["Start_Timestamp"]) - int(p["End_Timestamp"])) / 1000)  # gap after the last fused
+            continue
         if "gather_flags_kernel" in r["Kernel_Name"] and "lq_iter_fused4" in rows[i + 1]["Kernel_Name"]:
             g = (int(rows[i + 1]["Start_Timestamp"]) - int(r["End_Timestamp"])) / 1000
             if g < 200:   # inside a run of fits (not a section boundary)
@@ -46,7 +54,11 @@ def main(path):
                 p = rows[i - 1]
                 if "gather_kernel" in p["Kernel_Name"]:
                     gath.append((int(p["End_Timestamp"]) - int(p["Start_Timestamp"])) / 1000)
-    if gaps:
+    if gaps and any("gather_wg_kernel" in r["Kernel_Name"] for r in rows):
+        print(f"per fit (one-launch gather): gap after the last fused launch {np.median(gath):.1f} µs, "
+              f"gather_wg {np.median(flags):.1f} µs, host turnaround {np.median(gaps):.1f} µs "
+              f"(median over {len(gaps)} fits)")
+    elif gaps:
         print(f"per fit: gather {np.median(gath):.1f} µs, flags {np.median(flags):.1f} µs, host turnaround "
               f"{np.median(gaps):.1f} µs (median over {len(gaps)} fits)")
 
