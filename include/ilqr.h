@@ -242,8 +242,10 @@ ilqr_status ilqr_iterate(ilqr_handle* h, const ilqr_problem* p, const ilqr_optio
  * successor (the reference's last new_cost); iters/status (batch) may be NULL.
  * Returns ILQR_ERR_NAN / ILQR_ERR_LS_EXHAUSTED if any trajectory stopped that
  * way (others still complete). Returns once the fit's last kernel has run: every
- * output is written and the stream holds no more of the fit's work (the host waits
- * on a word that kernel writes, not on the runtime's stream sync). */
+ * output is written (the host thread spins, up to 20 ms, then falls back to the
+ * stream sync, on a host-mapped word that one-thread kernel writes after every earlier
+ * kernel of the stream completed; the runtime may still be retiring that kernel, so
+ * work the caller enqueues next on the same stream runs after it as usual). */
 ilqr_status ilqr_fit(ilqr_handle* h, const ilqr_problem* p, const ilqr_options* o,
                      const double* x_init, const double* u_init, const double* x_traj,
                      double* x_out, double* u_out, double* cost, int32_t* iters,
