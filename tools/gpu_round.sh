@@ -61,6 +61,7 @@ case $WHAT in
                  ILQR_GATHER_WG=$wg step trace_wg$wg 200 rocprofv3 --kernel-trace -d gpurun_out/trace_wg$wg -o run --output-format csv -- python tools/ab_fit.py
                  python tools/trace_fit_gaps.py gpurun_out/trace_wg$wg/run_kernel_trace.csv > gpurun_out/trace_fit_gaps_wg$wg.txt 2>&1
                done ;;
+  spread) step wave_spread 200 python tools/wave_spread.py ;;
   gtest) step pytest_gather 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_line_search.py tests/test_gpu_multi.py -m gpu -x -q --timeout 120 --timeout-method thread ;;
 esac
 done
