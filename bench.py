@@ -190,6 +190,10 @@ def secondary_configs(device):
                          "forward_lanes_busy_frac": fw["lanes_busy_frac"],
                          "forward_avg_launch_ms": fw["avg_launch_ms"], "forward_frac_of_peak": fw["frac"],
                          "dtype": r["dtype"], "config": r["config"]}
+            if "fit" in r:  # ChainSolver.fit end to end (config 5)
+                out[name]["fit3_ms"] = r["fit"]["fit3"]["median_ms"]
+                out[name]["fit_default_ms"] = r["fit"]["fit_default"]["median_ms"]
+                out[name]["fit_default_mean_iterations"] = r["fit"]["fit_default"]["mean_iterations"]
         except Exception as e:  # reported, never required
             out[name] = {"error": repr(e)}
     return out

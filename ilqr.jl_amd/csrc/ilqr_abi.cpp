@@ -309,22 +309,26 @@ ilqr_status unpad_u(ilqr_handle* h, const double* pu, double* u) {
   return unpad3(h, pu, u, (size_t)h->batch, h->T, h->nu, h->T, PAD_NU);
 }
 
-// The end of a fit. The stream's last kernel (gather_flags_kernel) stores this fit's number
-// into the host-mapped call-status word as it runs, after every earlier kernel of the
-// stream completed (in-order stream): when the word carries the number, the outputs are
-// written. The host spins on that word and returns — the runtime's blocking stream sync
-// costs ≈8 µs more per fit after the work is done (A/B in bench.py, 455 → 447 µs per
-// 3-iteration headline fit, profiles/r04/fit_wait_ab_r04.log). A fit longer than
-// FIT_SPIN_US falls back to the stream sync; ILQR_FIT_WAIT=sync in the environment forces
-// the sync (A/B).
-hipError_t wait_fit(ilqr_handle* h, uint32_t seq, hipStream_t s) {
+// The end of a fit: the stream's last kernel stores this fit's number into a wait word
+// (ilqr::wait_host_seq below).
+hipError_t wait_fit(ilqr_handle* h, uint32_t seq, hipStream_t s) { return ilqr::wait_host_seq(h->host_running + 2, seq, s); }
+
+}  // namespace
+
+// The stream's last kernel of a fit (gather_flags_kernel) stores the fit's number into
+// the host-mapped call-status word as it runs, after every earlier kernel of the stream
+// completed (in-order stream): when the word carries the number, the outputs are written.
+// The host spins on that word and returns — the runtime's blocking stream sync costs
+// ≈8 µs more per fit after the work is done (A/B in bench.py, 455 → 447 µs per 3-iteration
+// headline fit, profiles/r04/fit_wait_ab_r04.log). A fit longer than FIT_SPIN_US falls
+// back to the stream sync; ILQR_FIT_WAIT=sync in the environment forces the sync (A/B).
+hipError_t ilqr::wait_host_seq(const volatile int32_t* w, uint32_t seq, hipStream_t s) {
   static const bool spin = [] {
     const char* e = getenv("ILQR_FIT_WAIT");
     return !(e && strcmp(e, "sync") == 0);
   }();
   if (spin) {
     constexpr int64_t FIT_SPIN_US = 20000;
-    const volatile int32_t* w = h->host_running + 2;
     const auto t0 = std::chrono::steady_clock::now();
     for (uint32_t k = 0;; ++k) {
       if (((uint32_t)__atomic_load_n(w, __ATOMIC_ACQUIRE) >> 2) == seq) return hipSuccess;
@@ -337,8 +341,6 @@ hipError_t wait_fit(ilqr_handle* h, uint32_t seq, hipStream_t s) {
   }
   return hipStreamSynchronize(s);
 }
-
-}  // namespace
 
 extern "C" {
 

@@ -1849,32 +1849,56 @@ __global__ __launch_bounds__(64 * W) void chain_iter_forward_trig_kernel(ChainTr
   }
 }
 
-// x_out[b] = (res_parity[b] ? x1 : x0)[b]; still-running trajectories → MAX_ITER
+// The end of a chain fit (the LQ driver's gather_kernel for V = float / double): x_out[b]
+// = the buffer res_parity[b] names — x0 / x1 the handle's, PARITY_INPUT the caller's
+// x_init, PARITY_OUT nothing to copy (the last iteration wrote x_out) — with
+// final_parity for still-running trajectories, whose status becomes MAX_ITER; cost /
+// iterations / status copied out (each may be null); the call-status bits (1 NaN,
+// 2 exhausted search) OR-ed into dflags[0] by the trajectories that set one. One block
+// per trajectory: status is read by every thread before thread 0 rewrites it.
 template <class V>
-__global__ __launch_bounds__(256) void chain_gather_kernel(int B, int nxe, int nue, const V* x0,
-                                                           const V* u0, const V* x1, const V* u1,
-                                                           const int32_t* res_parity,
-                                                           int32_t* status, int final_parity,
-                                                           V* x_out, V* u_out) {
+__global__ __launch_bounds__(256) void chain_gather_kernel(int B, int nxe, int nue, const V* xin, const V* uin,
+                                                           const V* x0, const V* u0, const V* x1, const V* u1,
+                                                           const int32_t* res_parity, int32_t* status,
+                                                           int final_parity, const V* fit_cost,
+                                                           const int32_t* fit_iters, V* x_out, V* u_out,
+                                                           V* cost_out, int32_t* iters_out, int32_t* status_out,
+                                                           int32_t* dflags) {
   const int b = blockIdx.y;
   if (b >= B) return;
-  const bool running = status[b] == ILQR_TRAJ_OK;
+  const int32_t st0 = status[b];
+  const bool running = st0 == ILQR_TRAJ_OK;
   const int par = running ? final_parity : res_parity[b];
-  const V* xs = (par ? x1 : x0) + (size_t)b * nxe;
-  const V* us = (par ? u1 : u0) + (size_t)b * nue;
-  for (int i = threadIdx.x; i < nxe + nue; i += 256) {  // one block per trajectory: status is
-                                                         // read by all threads before it is set
-    if (i < nxe) x_out[(size_t)b * nxe + i] = xs[i];
-    else u_out[(size_t)b * nue + (i - nxe)] = us[i - nxe];
+  if (par != PARITY_OUT) {
+    const V* xs = (par == PARITY_INPUT ? xin : (par ? x1 : x0)) + (size_t)b * nxe;
+    const V* us = (par == PARITY_INPUT ? uin : (par ? u1 : u0)) + (size_t)b * nue;
+    for (int i = threadIdx.x; i < nxe + nue; i += 256) {
+      if (i < nxe) x_out[(size_t)b * nxe + i] = xs[i];
+      else u_out[(size_t)b * nue + (i - nxe)] = us[i - nxe];
+    }
   }
   __syncthreads();
-  if (running && threadIdx.x == 0) status[b] = ILQR_TRAJ_MAX_ITER;
+  if (threadIdx.x == 0) {
+    const int32_t st = running ? ILQR_TRAJ_MAX_ITER : st0;
+    status[b] = st;
+    if (status_out) status_out[b] = st;
+    if (cost_out) cost_out[b] = fit_cost[b];
+    if (iters_out) iters_out[b] = fit_iters[b];
+    const int f = (st == ILQR_TRAJ_NAN ? 1 : 0) | (st == ILQR_TRAJ_LS_EXHAUSTED ? 2 : 0);
+    if (f) __hip_atomic_fetch_or(dflags, f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
+// fit's per-trajectory state (forward_pass.jl:159): prev_cost = +Inf, status OK, result
+// "the input" (iteration 1 reads x_init / u_init in place), iterations 0 — one launch
 template <class V>
-__global__ void chain_fill_kernel(V* p, int n, V v) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i < n) p[i] = v;
+__global__ void chain_fit_init_kernel(int B, V* prev_cost, int32_t* status, int32_t* res_parity, int32_t* iters) {
+  const int b = blockIdx.x * 256 + threadIdx.x;
+  if (b >= B) return;
+  prev_cost[b] = V(INFINITY);
+  status[b] = ILQR_TRAJ_OK;
+  res_parity[b] = PARITY_INPUT;
+  iters[b] = 0;
 }
 
 }  // namespace
@@ -1901,6 +1925,14 @@ struct ilqr_chain_handle {
   int32_t* status = nullptr;
   int32_t* res_parity = nullptr;
   int32_t* iters = nullptr;
+  // the fit driver's host-mapped words ([0], [1] running counts of the poll, [2] the
+  // call status tagged with the fit's number), their device alias, the gather's device
+  // call-status word, the poll's events
+  int32_t* host_words = nullptr;
+  int32_t* dev_words = nullptr;
+  int32_t* dev_flags = nullptr;
+  hipEvent_t ev_poll[2] = {nullptr, nullptr};
+  uint32_t fit_seq = 0;
   // closed-form dynamics of 2-joint chains (ilqr_chain_set_dynamics): available once
   // sampled and checked against the recursion at creation, used unless RNEA is asked for
   bool trig_ok = false;
@@ -2310,6 +2342,8 @@ ilqr::ChainIter<V> iter_args(const ilqr_chain_handle* h, const void* x, const vo
   return a;
 }
 
+// Reduce per-trajectory status to the call status (host copy, synchronising):
+// ilqr_chain_backward / ilqr_chain_forward
 ilqr_status chain_fold_status(ilqr_chain_handle* h, const int32_t* dev_status) {
   std::vector<int32_t> st(h->batch);
   CH_TRY(hipMemcpyAsync(st.data(), dev_status, sizeof(int32_t) * h->batch, hipMemcpyDeviceToHost,
@@ -2327,43 +2361,68 @@ template <class V>
 ilqr_status chain_fit_t(ilqr_chain_handle* h, const ilqr_options* o, const void* x_init,
                         const void* u_init, const void* x_traj, void* x_out, void* u_out,
                         void* cost, int32_t* iters, int32_t* status, const ilqr_history* hist) {
+  // The LQ fit driver's structure (ilqr_abi.cpp ilqr_fit_ex, DESIGN.md §4 fit driver):
+  // iteration 1 reads x_init / u_init in place (no copy-in), the last iteration writes
+  // x_out / u_out directly unless they overlap an input, a tol ≥ 0 fit stops enqueueing
+  // once every trajectory has stopped (the running count one iteration behind), and the
+  // call ends with one gather + a one-thread launch that publishes the call status to a
+  // host-mapped word the host spins on (no status copy, no host fold).
   const size_t B = (size_t)h->batch, nx = 2 * (size_t)h->nj;
   const size_t nxe = (h->T + 1) * nx, nue = (size_t)h->T * h->nu;
   hipStream_t s = h->stream;
-  CH_TRY(hipMemcpyAsync(h->xbuf[0], x_init, sizeof(V) * B * nxe, hipMemcpyDeviceToDevice, s));
-  CH_TRY(hipMemcpyAsync(h->ubuf[0], u_init, sizeof(V) * B * nue, hipMemcpyDeviceToDevice, s));
-  const unsigned g = (unsigned)((B + 255) / 256);
-  ilqr::chain_fill_kernel<V><<<g, 256, 0, s>>>((V*)h->prev_cost, h->batch, V(INFINITY));  // :159
-  ilqr::chain_fill_kernel<int32_t><<<g, 256, 0, s>>>(h->status, h->batch, ILQR_TRAJ_OK);
-  ilqr::chain_fill_kernel<int32_t><<<g, 256, 0, s>>>(h->res_parity, h->batch, 0);
-  ilqr::chain_fill_kernel<int32_t><<<g, 256, 0, s>>>(h->iters, h->batch, 0);
-  CH_TRY(hipGetLastError());
   const ilqr::LSParams ls = chain_ls(o);
   const int max_iter = o ? o->max_iter : 100;
-  int par = 0;
+  const unsigned g = (unsigned)((B + 255) / 256);
+  ilqr::chain_fit_init_kernel<V><<<g, 256, 0, s>>>(h->batch, (V*)h->prev_cost, h->status, h->res_parity, h->iters);
+  CH_TRY(hipGetLastError());
+  volatile int32_t* flags = h->host_words + 2;
+  *flags = 0;
+  const size_t xb = sizeof(V) * B * nxe, ub = sizeof(V) * B * nue;
+  auto overlap = [](const void* p, size_t np, const void* q, size_t nq) {
+    const char *a = (const char*)p, *b = (const char*)q;
+    return q && a < b + nq && b < a + np;
+  };
+  const bool direct = max_iter > 0 && !overlap(x_out, xb, x_init, xb) && !overlap(x_out, xb, x_traj, xb) &&
+                      !overlap(x_out, xb, u_init, ub) && !overlap(u_out, ub, u_init, ub) &&
+                      !overlap(u_out, ub, x_init, xb) && !overlap(u_out, ub, x_traj, xb);
+  const bool poll = ls.tol >= 0.0 && max_iter > 2;
   for (int it = 1; it <= max_iter; ++it) {  // forward_pass.jl:161
-    auto a = iter_args<V>(h, h->xbuf[par], h->ubuf[par], x_traj, h->xbuf[par ^ 1], h->ubuf[par ^ 1],
-                          h->prev_cost, h->prev_cost, h->du2, h->trials, h->status);
+    const int par = (it - 1) & 1;
+    const bool last = direct && it == max_iter;
+    auto a = iter_args<V>(h, it == 1 ? x_init : h->xbuf[par], it == 1 ? u_init : h->ubuf[par], x_traj,
+                          last ? x_out : h->xbuf[par ^ 1], last ? u_out : h->ubuf[par ^ 1], h->prev_cost,
+                          h->prev_cost, h->du2, h->trials, h->status);
     a.res_parity = h->res_parity;
     a.iters = h->iters;
-    a.parity = par;
+    a.parity = it == 1 ? ilqr::PARITY_INPUT : par;  // where the input x̄ⁱ, ūⁱ lie (:174-175)
     a.iter = it;
     CH_TRY(dispatch<V>(h, [&](auto ops) { return decltype(ops)::iteration(h, a, ls); }));
     if (hist)  // the per-iteration record (ilqr_history)
       CH_TRY(ilqr::launch_record_history(h->batch, it, h->status, h->iters, h->trials, h->prev_cost, h->du2,
                                          sizeof(V) == 4, ls.alpha0, ls.shrink, hist->cost, hist->trials,
                                          hist->alpha, hist->du2, s));
-    par ^= 1;  // x̄ⁱ, ūⁱ = x̄ⁱ⁺¹, ūⁱ⁺¹ (:174-175)
+    if (!poll || it == max_iter) continue;
+    CH_TRY(ilqr::launch_count_running(h->batch, h->status, h->dev_words + (it & 1), s));
+    CH_TRY(hipEventRecord(h->ev_poll[it & 1], s));
+    if (it >= 2) {  // iteration it−1's count, read while iteration it runs (:171's break)
+      CH_TRY(hipEventSynchronize(h->ev_poll[(it - 1) & 1]));
+      if (__atomic_load_n(h->host_words + ((it - 1) & 1), __ATOMIC_ACQUIRE) == 0) break;
+    }
   }
+  // still-running trajectories (max_iter reached) return the last accepted iterate
+  const int final_parity =
+      max_iter == 0 ? ilqr::PARITY_INPUT : (direct ? ilqr::PARITY_OUT : (max_iter & 1));
   ilqr::chain_gather_kernel<V><<<dim3(1, h->batch), 256, 0, s>>>(
-      h->batch, (int)nxe, (int)nue, (const V*)h->xbuf[0], (const V*)h->ubuf[0],
-      (const V*)h->xbuf[1], (const V*)h->ubuf[1], h->res_parity, h->status, par, (V*)x_out,
-      (V*)u_out);
+      h->batch, (int)nxe, (int)nue, (const V*)x_init, (const V*)u_init, (const V*)h->xbuf[0],
+      (const V*)h->ubuf[0], (const V*)h->xbuf[1], (const V*)h->ubuf[1], h->res_parity, h->status, final_parity,
+      (const V*)h->prev_cost, h->iters, (V*)x_out, (V*)u_out, (V*)cost, iters, status, h->dev_flags);
   CH_TRY(hipGetLastError());
-  if (cost) CH_TRY(hipMemcpyAsync(cost, h->prev_cost, sizeof(V) * B, hipMemcpyDeviceToDevice, s));
-  if (iters) CH_TRY(hipMemcpyAsync(iters, h->iters, sizeof(int32_t) * B, hipMemcpyDeviceToDevice, s));
-  if (status) CH_TRY(hipMemcpyAsync(status, h->status, sizeof(int32_t) * B, hipMemcpyDeviceToDevice, s));
-  return chain_fold_status(h, h->status);
+  uint32_t seq = (++h->fit_seq) & 0x3fffffffu;
+  if (seq == 0) seq = h->fit_seq = 1;  // 0 is the word's cleared value
+  CH_TRY(ilqr::launch_publish_flags(h->dev_flags, h->dev_words + 2, seq, s));
+  CH_TRY(ilqr::wait_host_seq(h->host_words + 2, seq, s));
+  const int32_t f = __atomic_load_n(h->host_words + 2, __ATOMIC_ACQUIRE);
+  return (f & 1) ? ILQR_ERR_NAN : ((f & 2) ? ILQR_ERR_LS_EXHAUSTED : ILQR_OK);
 }
 
 }  // namespace
@@ -2413,6 +2472,12 @@ ilqr_status ilqr_chain_create(ilqr_chain_handle** out, int device, const ilqr_ch
     if (e == hipSuccess) e = hipMalloc(&h->status, sizeof(int32_t) * B);
     if (e == hipSuccess) e = hipMalloc(&h->res_parity, sizeof(int32_t) * B);
     if (e == hipSuccess) e = hipMalloc(&h->iters, sizeof(int32_t) * B);
+    if (e == hipSuccess)
+      e = hipHostMalloc(&h->host_words, sizeof(int32_t) * 4, hipHostMallocMapped | hipHostMallocCoherent);
+    if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&h->dev_words, h->host_words, 0);
+    if (e == hipSuccess) e = hipMalloc(&h->dev_flags, sizeof(int32_t) * 2);
+    if (e == hipSuccess) e = hipMemset(h->dev_flags, 0, sizeof(int32_t) * 2);
+    for (int c = 0; c < 2 && e == hipSuccess; ++c) e = hipEventCreateWithFlags(&h->ev_poll[c], hipEventDisableTiming);
   }
   if (e != hipSuccess) {
     ilqr_chain_destroy(h);
@@ -2500,7 +2565,10 @@ ilqr_status ilqr_chain_destroy(ilqr_chain_handle* h) {
     (void)hipFree(h->ubuf[i]);
   }
   for (void* p : {h->K, h->d, h->J, h->prev_cost, h->du2}) (void)hipFree(p);
-  for (int32_t* p : {h->trials, h->status, h->res_parity, h->iters}) (void)hipFree(p);
+  for (int32_t* p : {h->trials, h->status, h->res_parity, h->iters, h->dev_flags}) (void)hipFree(p);
+  if (h->host_words) (void)hipHostFree(h->host_words);
+  for (hipEvent_t ev : h->ev_poll)
+    if (ev) (void)hipEventDestroy(ev);
   (void)hipFree(h->task_dev);
   delete h;
   return ILQR_OK;

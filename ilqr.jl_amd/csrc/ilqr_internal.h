@@ -154,6 +154,12 @@ hipError_t launch_lq_linearize(int nx, int nu, const LQParams& p, int B, int T, 
                                hipStream_t s);
 // *out = #trajectories with status OK (out may be host-mapped memory)
 hipError_t launch_count_running(int B, const int32_t* status, int32_t* out, hipStream_t s);
+// The last launch of a fit (gather_flags_kernel): dflags[0] (a gather's call-status
+// bits, re-armed) into the host-mapped word `flags` as (seq << 2) | bits.
+hipError_t launch_publish_flags(int32_t* dflags, int32_t* flags, uint32_t seq, hipStream_t s);
+// The host's end of a fit: spin (≤ 20 ms, then the stream sync) until the host-mapped
+// word carries `seq` in bits 2..31 (ilqr_abi.cpp; ILQR_FIT_WAIT=sync forces the sync).
+hipError_t wait_host_seq(const volatile int32_t* word, uint32_t seq, hipStream_t s);
 bool lq_supported(int nx, int nu);
 
 // Caller-supplied derivative tiles (ilqr_tiles in include/ilqr.h), device pointers.

@@ -965,6 +965,11 @@ __global__ __launch_bounds__(256) void count_running_kernel(int B, const int32_t
   if (threadIdx.x == 0) *out = total;
 }
 
+hipError_t launch_publish_flags(int32_t* dflags, int32_t* flags, uint32_t seq, hipStream_t s) {
+  gather_flags_kernel<<<1, 1, 0, s>>>(dflags, flags, seq);
+  return hipGetLastError();
+}
+
 hipError_t launch_count_running(int B, const int32_t* status, int32_t* out, hipStream_t s) {
   count_running_kernel<<<1, 256, 0, s>>>(B, status, out);
   return hipGetLastError();

@@ -429,3 +429,83 @@ def test_closed_form_equals_recursion(gpu, name, nu):
     assert s.dynamics_mode == "rnea"
     s.set_dynamics("auto")
     assert s.dynamics_mode == "closed_form"
+
+
+def chain_fit_replay(s, x0, u0, max_iter, tol, max_trials):
+    """fit (forward_pass.jl:148-179) restated as ilqr_chain_iterate calls: prev_cost = Inf,
+    each iteration on the still-running trajectories, a trajectory that stops keeps the
+    iteration's INPUT (converged: the pre-update iterate, :171; NaN / exhausted search:
+    the last accepted one), the running ones the last accepted iterate and MAX_ITER."""
+    nb = x0.shape[0]
+    dt = x0.dtype
+    s._bind()
+    o = _lib.default_options(max_iter=max_iter, tol=tol, max_trials=max_trials)
+    x, u = x0.clone(), u0.clone()
+    pc = torch.full((nb,), float("inf"), dtype=dt, device="cuda")
+    st = torch.zeros((nb,), dtype=torch.int32, device="cuda")
+    tr = torch.zeros((nb,), dtype=torch.int32, device="cuda")
+    it_out = torch.zeros((nb,), dtype=torch.int32, device="cuda")
+    rx, ru = x0.clone(), u0.clone()
+    for it in range(1, max_iter + 1):
+        run = st == 0
+        if not bool(run.any()):
+            break
+        xn, un = torch.empty_like(x), torch.empty_like(u)
+        tr.fill_(-1)
+        s.iterate(x, u, xn, un, pc, st, pc, trials=tr, options=o)
+        it_out[run & (tr != -1)] = it   # the forward ran it (a NaN backward stops before)
+        stopped = run & (st != 0)
+        rx[stopped], ru[stopped] = x[stopped], u[stopped]
+        keep = run & (st == 0)
+        x = torch.where(keep[:, None, None], xn, x)
+        u = torch.where(keep[:, None, None], un, u)
+    run = st == 0
+    rx[run], ru[run] = x[run], u[run]
+    st = torch.where(run, torch.full_like(st, _lib.TRAJ_MAX_ITER), st)
+    s_np = st.cpu().numpy()
+    cs = _lib.ERR_NAN if (s_np == _lib.TRAJ_NAN).any() else (
+        _lib.ERR_LS_EXHAUSTED if (s_np == _lib.TRAJ_LS_EXHAUSTED).any() else _lib.OK)
+    return rx, ru, pc, it_out, st, cs
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+@pytest.mark.parametrize("max_iter,tol,max_trials,nan,inplace", [
+    (20, 1e-6, None, True, False),     # early convergence: the poll stops the loop
+    (6, -1.0, 2, True, False),         # exhausted searches and a NaN, to max_iter
+    (5, 1e-6, None, False, True),      # x_out = x_init: no direct output, copies
+    (1, -1.0, None, False, False),
+    (0, -1.0, None, False, False),     # the input is the result
+])
+def test_chain_fit_equals_iterate_replay(gpu, g2, dtype, max_iter, tol, max_trials, nan, inplace):
+    """The chain fit driver (one init launch, iteration 1 on the caller's x_init in place,
+    the last iteration into x_out, the running-count poll, one gather + the published
+    call status) returns exactly what the same iterations through ilqr_chain_iterate do:
+    x, u, cost, iterations, status and call status, bit for bit."""
+    import ctypes as C
+    s = solver(g2, dtype, "fd" if dtype == torch.float32 else "dual")
+    x0, u0 = dev(g2["x"], dtype), dev(g2["u"], dtype)
+    if nan:
+        x0[1, 3, 2] = float("nan")
+    ref = chain_fit_replay(s, x0, u0, max_iter, tol, max_trials)
+    for _ in range(2):   # twice: the re-armed call-status words
+        xi, ui = x0.clone(), u0.clone()
+        if inplace:
+            nb = xi.shape[0]
+            cost = torch.empty((nb,), dtype=dtype, device="cuda")
+            it = torch.empty((nb,), dtype=torch.int32, device="cuda")
+            st = torch.empty((nb,), dtype=torch.int32, device="cuda")
+            s._bind()
+            o = _lib.default_options(max_iter=max_iter, tol=tol, max_trials=max_trials)
+            p = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
+            cs = s.lib.ilqr_chain_fit(s.h, C.byref(o), p(xi), p(ui), None, p(xi), p(ui), p(cost), p(it), p(st))
+            got = (xi, ui, cost, it, st, cs)
+        else:
+            r = s.fit(xi, ui, max_iter=max_iter, tol=tol,
+                      options=_lib.default_options(max_iter=max_iter, tol=tol, max_trials=max_trials))
+            got = (r.x, r.u, r.cost, r.iters, r.status, r.call_status)
+        assert got[5] == ref[5]
+        for a, b in zip(got[:4], ref[:4]):
+            torch.testing.assert_close(a, b, rtol=0, atol=0, equal_nan=True)
+        assert torch.equal(got[4], ref[4])
+    if nan and max_iter > 0:
+        assert ref[4][1].item() == _lib.TRAJ_NAN

@@ -163,8 +163,28 @@ def measure(lin="fd", B=2048, T=100, nu=1, dtype="f32", steps=100, warmup=100, d
             base["value"] = base["value"] / B  # trajectory-iterations/s → batched it/s
             base["unit"] = f"batched iterations/s (batch={B})"
         res["cpu_baseline"] = base
+    res["fit"] = fit_timing(s, x, u)
     s.close()
     return res
+
+
+def fit_timing(s, x, u, n=40):
+    """ChainSolver.fit end to end (synchronous, wall clock, median of n): the 3-iteration
+    fit from cold (tol disabled) and the reference's default call (tol = 1e-6,
+    max_iter = 100)."""
+    out = {}
+    for name, kw in (("fit3", dict(max_iter=3, tol=-1.0)), ("fit_default", dict(max_iter=100, tol=1e-6))):
+        for _ in range(5):
+            r = s.fit(x, u, **kw)
+        ts = []
+        for _ in range(n):
+            t0 = time.perf_counter()
+            r = s.fit(x, u, **kw)
+            ts.append(time.perf_counter() - t0)
+        ms = float(np.median(ts)) * 1e3
+        it = float(r.iters.double().mean().item())
+        out[name] = {"median_ms": ms, "mean_iterations": it, "batched_it_per_s": it * 1e3 / ms}
+    return out
 
 
 def main():
