@@ -155,8 +155,11 @@ def test_coop_nan_and_unreachable(gpu):
     nb = 4096
     lq, x, u, xt, pc = forced_case(nb)
     pc[::7] = -1.0
-    x = x.copy()
+    x, u, xt = x.copy(), u.copy(), xt.copy()
     x[5, 3, 2] = np.nan
+    # trajectory 9 at rest on its target: gradient and δu exactly 0, so α·δu vanishes at
+    # trial 1 itself (the published `stop` is clamped to 2: trial 2 repeats trial 1)
+    x[9], u[9], xt[9], pc[9] = 0.0, 0.0, 0.0, -1.0
     s = Solver(12, 4, 100, nb)
     s.set_problem(lq)
     try:
@@ -166,6 +169,7 @@ def test_coop_nan_and_unreachable(gpu):
         s.close()
     assert seq[4][5] == _lib.TRAJ_NAN
     assert (seq[4][::7][1:] == _lib.TRAJ_LS_EXHAUSTED).all() and (seq[5][::7][1:] == 64).all()
+    assert seq[4][9] == _lib.TRAJ_LS_EXHAUSTED and seq[5][9] == 64
     assert_same(coop, seq)
 
 

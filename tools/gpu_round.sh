@@ -67,6 +67,11 @@ case $WHAT in
              step rbd_new_$i 200 python tools/bench_rbd.py --lin fd --no-cpu --steps 50 --warmup 50
            done
            for f in gpurun_out/rbd_prev_*.log gpurun_out/rbd_new_*.log; do python -c "import json,sys; d=[json.loads(l) for l in open(sys.argv[1]) if l.startswith('{')][-1]; f=d['fit']; print(sys.argv[1], round(d['value'],1), 'fit3', round(f['fit3']['median_ms'],4), 'default', round(f['fit_default']['median_ms'],4), round(f['fit_default']['mean_iterations'],2))" $f; done > gpurun_out/chain_fit_ab.log; cat gpurun_out/chain_fit_ab.log ;;
+  vanishab) for i in 1 2; do
+              ILQR_LIB=ilqr.jl_amd/lib/variants/libilqr_hip_prev.so MODES=coop step tail_prev_$i 200 python tools/tail_probe.py
+              MODES=coop step tail_new_$i 200 python tools/tail_probe.py
+            done
+            grep -h "coop \|per iteration" gpurun_out/tail_prev_*.log gpurun_out/tail_new_*.log > gpurun_out/vanish_ab.log; cat gpurun_out/vanish_ab.log ;;
   gtest) step pytest_gather 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_line_search.py tests/test_gpu_multi.py -m gpu -x -q --timeout 120 --timeout-method thread ;;
 esac
 done
