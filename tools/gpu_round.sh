@@ -72,6 +72,7 @@ case $WHAT in
               MODES=coop step tail_new_$i 200 python tools/tail_probe.py
             done
             grep -h "coop \|per iteration" gpurun_out/tail_prev_*.log gpurun_out/tail_new_*.log > gpurun_out/vanish_ab.log; cat gpurun_out/vanish_ab.log ;;
+  tail5) step coop_tail 200 python tools/coop_tail_analysis.py ;;
   gtest) step pytest_gather 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_line_search.py tests/test_gpu_multi.py -m gpu -x -q --timeout 120 --timeout-method thread ;;
 esac
 done
