@@ -79,6 +79,8 @@ struct ilqr_handle {
   int32_t* coop_ctl = nullptr;
   uint32_t coop_gen = 0;  // fused launches so far (the list's generation tag)
   uint32_t fit_seq = 0;   // fits so far (tags the host call-status word, wait_fit)
+  double* coop_sx = nullptr;  // the search's scratch rollouts (LSCoop::sx / su)
+  double* coop_su = nullptr;
   ilqr::LSCoop* coop_dev = nullptr;  // the struct of the above, in device memory
   int bound[3] = {0, 0, 0};
   hipEvent_t ev_bw[2] = {nullptr, nullptr};
@@ -421,8 +423,17 @@ ilqr_status ilqr_create(ilqr_handle** out, int device, int nx, int nu, int T, in
     if (e == hipSuccess) e = hipMemset(h->coop_list, 0, sizeof(uint64_t) * B);  // generation 0: stale
     if (e == hipSuccess) e = hipMemset(h->coop_ctl, 0, sizeof(int32_t) * 2);
     if (e == hipSuccess) e = hipMalloc(&h->coop_dev, sizeof(ilqr::LSCoop));
+    // scratch rollouts for the first searches of a launch (32-bit buffer offsets: the
+    // x part must stay under 2 GiB, else no scratch)
+    const int nsl = std::min(batch, ilqr::COOP_SCRATCH_SLOTS);
+    const size_t sxb = sizeof(double) * nsl * ilqr::COOP_MAX_TRIALS * (size_t)(T + 1) * nx;
+    const size_t sub = sizeof(double) * nsl * ilqr::COOP_MAX_TRIALS * (size_t)T * nu;
+    const bool scratch = sxb < (size_t(1) << 31);
+    if (e == hipSuccess && scratch) e = hipMalloc(&h->coop_sx, sxb);
+    if (e == hipSuccess && scratch) e = hipMalloc(&h->coop_su, sub);
     if (e == hipSuccess) {
-      const ilqr::LSCoop c{h->coop_rec, h->coop_cost, h->coop_du2, h->coop_list, h->coop_ctl};
+      const ilqr::LSCoop c{h->coop_rec, h->coop_cost, h->coop_du2, h->coop_list, h->coop_ctl,
+                           h->coop_sx,  h->coop_su,   scratch ? nsl : 0};
       e = hipMemcpy(h->coop_dev, &c, sizeof(c), hipMemcpyHostToDevice);
     }
     if (e == hipSuccess) e = hipDeviceSynchronize();
@@ -477,6 +488,8 @@ ilqr_status ilqr_destroy(ilqr_handle* h) {
   (void)hipFree(h->coop_cost);
   (void)hipFree(h->coop_du2);
   (void)hipFree(h->coop_list);
+  (void)hipFree(h->coop_sx);
+  (void)hipFree(h->coop_su);
   (void)hipFree(h->coop_ctl);
   (void)hipFree(h->coop_dev);
   for (int c = 0; c < 2; ++c)

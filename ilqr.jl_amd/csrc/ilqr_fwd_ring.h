@@ -157,6 +157,12 @@ struct FwdOut {
 struct CandPass {
   double alpha;     // this lane's group's α
   int store_group;  // group that stores its rollout into x_new/u_new of the trajectory
+  // scratch rollouts (LSCoop::sx / su, byte sizes): when set, EVERY group stores its
+  // rollout there, group g at trial index sidx + g, instead of into x_new / u_new
+  double* sx = nullptr;
+  double* su = nullptr;
+  int sidx = 0;
+  uint32_t sx_bytes = 0, su_bytes = 0;
 };
 
 
@@ -301,11 +307,16 @@ __device__ FwdOut lq_forward_wave_ring(const LQParams& P, int b0, int B, int T, 
   // the resources' words made provably wave-uniform (the candidate passes run inside
   // the cooperative search's loops, where the compiler loses track of it: a divergent
   // resource is a readfirstlane waterfall loop around every store)
-  const auto rXN = buffer_rsrc(uniform_ptr(xnew + (size_t)b0 * (T + 1) * NX),
-                               (uint32_t)__builtin_amdgcn_readfirstlane(nt * (T + 1) * NX * 8));
-  const auto rUN = buffer_rsrc(uniform_ptr(unew + (size_t)b0 * T * NU),
-                               (uint32_t)__builtin_amdgcn_readfirstlane(nt * T * NU * 8));
-  const int gs = CAND ? 0 : g;  // this group's trajectory within the stored span
+  const bool scr = CAND && cand.sx != nullptr;  // wave-uniform
+  const auto rXN = scr ? buffer_rsrc(uniform_ptr(cand.sx), (uint32_t)__builtin_amdgcn_readfirstlane(cand.sx_bytes))
+                       : buffer_rsrc(uniform_ptr(xnew + (size_t)b0 * (T + 1) * NX),
+                                     (uint32_t)__builtin_amdgcn_readfirstlane(nt * (T + 1) * NX * 8));
+  const auto rUN = scr ? buffer_rsrc(uniform_ptr(cand.su), (uint32_t)__builtin_amdgcn_readfirstlane(cand.su_bytes))
+                       : buffer_rsrc(uniform_ptr(unew + (size_t)b0 * T * NU),
+                                     (uint32_t)__builtin_amdgcn_readfirstlane(nt * T * NU * 8));
+  // this group's rollout within the stored span: its trajectory (g), the candidate pass's
+  // one trajectory (0), or its trial's scratch slot
+  const int gs = scr ? cand.sidx + g : (CAND ? 0 : g);
   const uint32_t oxs = is_x ? (uint32_t)(gs * (T + 1) * NX + jx) * 8 : OOR;
   const uint32_t ous = is_u ? (uint32_t)(gs * T * NU + iu) * 8 : OOR;
 
@@ -319,7 +330,7 @@ __device__ FwdOut lq_forward_wave_ring(const LQParams& P, int b0, int B, int T, 
     for (int t = 0; t < PF; ++t) produce(t);
     double cost = 0.0, du2 = 0.0;
     bool eo = true;  // CAND: fma(α, δuₖ, uₖ) == uₖ so far (u lanes)
-    const bool st = open && (!CAND || g == cand.store_group);
+    const bool st = open && (!CAND || scr || g == cand.store_group);
     const uint32_t ox = st ? oxs : OOR, ou = st ? ous : OOR;  // closed groups store nothing
     // slot t's operands are read into registers at the end of step t − 1 (software
     // pipelining of the LDS reads: their latency is off the step's dependent chain)
@@ -792,8 +803,9 @@ __device__ __forceinline__ void coop_publish(const LSCoop& c, uint32_t gen, int 
   ag_st(&R->stop, max_trials + 1);
   ag_st(&R->fin, 0);
   __hip_atomic_store(&R->mask, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // trial 1 done
-  release_agent();  // the record, and trial 1's rollout stores, before the entry
   const int slot = __hip_atomic_fetch_add(c.ctl + (gen & 1), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  ag_st(&R->slot, slot);
+  release_agent();  // the record (its slot too), and trial 1's rollout stores, before the entry
   __hip_atomic_store(c.list + slot, ((uint64_t)gen << 32) | (uint32_t)b, __ATOMIC_RELAXED,
                      __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -853,9 +865,34 @@ __device__ __attribute__((unused)) int coop_find(const LSCoop& c, uint32_t gen, 
 }
 
 // Trajectory b's outcome, once trials 1..lim are evaluated (whole wave).
+// dst[0, n) = src[0, n) by the whole wave, the source read coherently at agent scope (it
+// was written by another wave, possibly on another XCD, and released before the mask
+// bits that let this wave finalise; a plain load could hit a line this XCD's L2 kept from
+// an earlier launch), eight loads per lane in flight
+__device__ __forceinline__ void coop_copy(double* __restrict__ dst, const double* src, int n) {
+  const int l = threadIdx.x & 63;
+  for (int i0 = 0; i0 < n; i0 += 64 * 8) {
+    uint64_t v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int i = i0 + 64 * k + l;
+      v[k] = i < n ? __hip_atomic_load(reinterpret_cast<const uint64_t*>(src + i), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT)
+                   : 0ull;
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int i = i0 + 64 * k + l;
+      if (i < n) dst[i] = __builtin_bit_cast(double, v[k]);
+    }
+  }
+}
+
+// `sl`: the search's list position; below c.nslots every evaluated trial's rollout is in
+// the scratch and the final one is copied from there instead of rolled out again.
 template <int NX, int NU>
 __device__ void coop_finalize(const LQParams& P, int b, int B, int T, const IterArgs& a, const LSCoop& c,
-                              const LSParams& ls, double* ring, int lim) {
+                              const LSParams& ls, double* ring, int lim, int sl) {
   LSCoopRec* R = c.rec + b;
   int best = 0;
   double cost = 0.0, du2 = 0.0;
@@ -866,8 +903,14 @@ __device__ void coop_finalize(const LQParams& P, int b, int B, int T, const Iter
   }
   const bool accepted = __builtin_amdgcn_readfirstlane(best) <= ls.max_trials;  // then best == lim
   // trial 2's group stored as it ran; any other final rollout is rolled out again,
-  // storing (an exhausted one only for ilqr_iterate: fit keeps the previous iterate)
-  if (lim != 2 && (accepted || !a.res_parity)) {
+  // storing (an exhausted one only for ilqr_iterate: fit keeps the previous iterate) —
+  // or, for a search with a scratch slot, copied from the trial's scratch rollout
+  const bool scr = sl < c.nslots;
+  if (scr && (accepted || !a.res_parity)) {
+    const int s0 = sl * COOP_MAX_TRIALS + lim - 1;
+    coop_copy(a.xnew + (size_t)b * (T + 1) * NX, c.sx + (size_t)s0 * (T + 1) * NX, (T + 1) * NX);
+    coop_copy(a.unew + (size_t)b * T * NU, c.su + (size_t)s0 * T * NU, T * NU);
+  } else if (!scr && lim != 2 && (accepted || !a.res_parity)) {
     const int g = (threadIdx.x & 63) >> 4;
     double scratch = 0.0;
     (void)lq_forward_wave_ring<NX, NU, PIPE_R, PIPE_PF, true, true>(
@@ -898,13 +941,16 @@ __device__ void coop_evaluate(const LQParams& P, int b, int B, int T, const Iter
                               const LSParams& ls, double* ring) {
   LSCoopRec* R = c.rec + b;
   const int l = threadIdx.x & 63, g = l >> 4;
-  int j0 = 0, lim0 = 0;
+  int j0 = 0, lim0 = 0, sl = 0;
   if (l == 0) {
     j0 = __hip_atomic_fetch_add(&R->next, 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     lim0 = coop_lim(R, ls.max_trials);
+    sl = ag_ld(&R->slot);
   }
   j0 = __builtin_amdgcn_readfirstlane(j0);
   lim0 = __builtin_amdgcn_readfirstlane(lim0);
+  sl = __builtin_amdgcn_readfirstlane(sl);
+  const bool scr = sl < c.nslots;  // every trial's rollout to the scratch
   if (j0 > lim0) return;  // raced past the needed set: nothing to do
   const int j = j0 + g;   // this group's trial
   const bool mine = j <= lim0;
@@ -912,9 +958,16 @@ __device__ void coop_evaluate(const LQParams& P, int b, int B, int T, const Iter
   // once no trial of b is needed any more)
   const double pc = a.prev_cost ? a.prev_cost[b] : INFINITY;
   double du2 = 0.0;
+  CandPass cp{trial_alpha(ls, j), j0 == 2 ? 0 : -1};
+  if (scr) {
+    cp.sx = c.sx;
+    cp.su = c.su;
+    cp.sidx = sl * COOP_MAX_TRIALS + j0 - 1;
+    cp.sx_bytes = (uint32_t)(c.nslots * COOP_MAX_TRIALS * (T + 1) * NX * 8);
+    cp.su_bytes = (uint32_t)(c.nslots * COOP_MAX_TRIALS * T * NU * 8);
+  }
   const FwdOut r = lq_forward_wave_ring<NX, NU, PIPE_R, PIPE_PF, true, true>(
-      P, b, B, T, mine, a.x, a.u, a.xtraj, a.d, a.K, pc, a.xnew, a.unew, &du2, ls, ring,
-      CandPass{trial_alpha(ls, j), j0 == 2 ? 0 : -1});
+      P, b, B, T, mine, a.x, a.u, a.xtraj, a.d, a.K, pc, a.xnew, a.unew, &du2, ls, ring, cp);
   if ((l & 15) == 0 && mine) {
     ag_std(c.cost + (size_t)b * COOP_MAX_TRIALS + j - 1, r.cost);
     ag_std(c.du2 + (size_t)b * COOP_MAX_TRIALS + j - 1, du2);
@@ -924,8 +977,8 @@ __device__ void coop_evaluate(const LQParams& P, int b, int B, int T, const Iter
       __hip_atomic_fetch_min(&R->stop, j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   // costs and best/stop complete before the mask bits; trial 2's rollout (stored as it
-  // ran) also written back from this XCD's L2
-  if (j0 == 2)
+  // ran) and scratch rollouts also written back from this XCD's L2
+  if (j0 == 2 || scr)
     release_agent();
   else
     complete_vmem();
@@ -950,7 +1003,7 @@ __device__ void coop_evaluate(const LQParams& P, int b, int B, int T, const Iter
   }
   fin = __builtin_amdgcn_readfirstlane(fin);
   lim = __builtin_amdgcn_readfirstlane(lim);
-  if (fin) coop_finalize<NX, NU>(P, b, B, T, a, c, ls, ring, lim);
+  if (fin) coop_finalize<NX, NU>(P, b, B, T, a, c, ls, ring, lim, sl);
 }
 
 // The work loop every wave of the launch enters once it is done with its own

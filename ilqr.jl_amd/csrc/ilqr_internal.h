@@ -34,7 +34,8 @@ struct LSCoopRec {  // per trajectory, agent-scope atomics only
   int32_t stop;     // smallest rejected trial whose α·δu vanished (max_trials + 1: none)
   int32_t fin;      // 0 → 1 by the wave that finalises the trajectory
   uint64_t mask;    // bit j − 1: trial j evaluated
-  uint64_t pad;
+  int32_t slot;     // its position in the launch's list (written before the entry)
+  int32_t pad;
 };
 struct LSCoop {
   LSCoopRec* rec;     // (B); nullptr: the sequential search of the ring forward
@@ -43,7 +44,14 @@ struct LSCoop {
   uint64_t* list;     // (B) published trajectories: launch generation << 32 | trajectory
                       // (an entry of another generation is stale: not written yet)
   int32_t* ctl;       // [gen & 1]: list length of launch `gen` (the launch zeroes the other)
+  // Rollouts of every evaluated trial of the first `nslots` searches of a launch (list
+  // positions < nslots): (nslots, 64, T+1, nx) and (nslots, 64, T, nu). Their finaliser
+  // copies the accepted trial's instead of rolling it out again.
+  double* sx;
+  double* su;
+  int32_t nslots;     // 0: no scratch (every finaliser rolls out)
 };
+constexpr int COOP_SCRATCH_SLOTS = 32;
 constexpr int COOP_MAX_TRIALS = 64;
 
 // Buffers of one fused iteration (fit loop body).

@@ -73,6 +73,11 @@ case $WHAT in
             done
             grep -h "coop \|per iteration" gpurun_out/tail_prev_*.log gpurun_out/tail_new_*.log > gpurun_out/vanish_ab.log; cat gpurun_out/vanish_ab.log ;;
   tail5) step coop_tail 200 python tools/coop_tail_analysis.py ;;
+  headab) for i in 1 2; do
+            ILQR_LIB=ilqr.jl_amd/lib/variants/libilqr_hip_prev.so step ab_fit_prev_$i 120 python tools/ab_fit.py
+            step ab_fit_new_$i 120 python tools/ab_fit.py
+          done
+          grep -h "fit median" gpurun_out/ab_fit_prev_*.log gpurun_out/ab_fit_new_*.log > gpurun_out/head_ab.log; cat gpurun_out/head_ab.log ;;
   gtest) step pytest_gather 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_line_search.py tests/test_gpu_multi.py -m gpu -x -q --timeout 120 --timeout-method thread ;;
 esac
 done
