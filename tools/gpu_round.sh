@@ -78,6 +78,11 @@ case $WHAT in
             step ab_fit_new_$i 120 python tools/ab_fit.py
           done
           grep -h "fit median" gpurun_out/ab_fit_prev_*.log gpurun_out/ab_fit_new_*.log > gpurun_out/head_ab.log; cat gpurun_out/head_ab.log ;;
+  tlab) for i in 1 2; do
+          ILQR_LIB=ilqr.jl_amd/lib/variants/libilqr_hip_prev.so step tl_prev_$i 200 python tools/ab_lib.py tools/bench_twolink.py --no-cpu
+          step tl_new_$i 200 python tools/bench_twolink.py --no-cpu
+        done
+        for f in gpurun_out/tl_prev_*.log gpurun_out/tl_new_*.log; do python -c "import json,sys; d=[json.loads(l) for l in open(sys.argv[1]) if l.startswith('{')][-1]; r=d['roofline']; print(sys.argv[1], round(d['value'],1), {k: round(v['avg_launch_ms']*1000,2) for k,v in r.items() if isinstance(v, dict) and 'avg_launch_ms' in v})" $f; done > gpurun_out/tl_ab.log; cat gpurun_out/tl_ab.log ;;
   gtest) step pytest_gather 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_line_search.py tests/test_gpu_multi.py -m gpu -x -q --timeout 120 --timeout-method thread ;;
 esac
 done
