@@ -431,7 +431,7 @@ def test_closed_form_equals_recursion(gpu, name, nu):
     assert s.dynamics_mode == "closed_form"
 
 
-def chain_fit_replay(s, x0, u0, max_iter, tol, max_trials):
+def chain_fit_replay(s, x0, u0, max_iter, tol, max_trials, x_traj=None):
     """fit (forward_pass.jl:148-179) restated as ilqr_chain_iterate calls: prev_cost = Inf,
     each iteration on the still-running trajectories, a trajectory that stops keeps the
     iteration's INPUT (converged: the pre-update iterate, :171; NaN / exhausted search:
@@ -452,7 +452,7 @@ def chain_fit_replay(s, x0, u0, max_iter, tol, max_trials):
             break
         xn, un = torch.empty_like(x), torch.empty_like(u)
         tr.fill_(-1)
-        s.iterate(x, u, xn, un, pc, st, pc, trials=tr, options=o)
+        s.iterate(x, u, xn, un, pc, st, pc, trials=tr, x_traj=x_traj, options=o)
         it_out[run & (tr != -1)] = it   # the forward ran it (a NaN backward stops before)
         stopped = run & (st != 0)
         rx[stopped], ru[stopped] = x[stopped], u[stopped]
@@ -473,6 +473,8 @@ def chain_fit_replay(s, x0, u0, max_iter, tol, max_trials):
     (20, 1e-6, None, True, False),     # early convergence: the poll stops the loop
     (6, -1.0, 2, True, False),         # exhausted searches and a NaN, to max_iter
     (5, 1e-6, None, False, True),      # x_out = x_init: no direct output, copies
+    (4, -1.0, None, False, "xtraj"),   # x_out = x_traj (a tracking target): read by every
+                                       # iteration, written only by the gather
     (1, -1.0, None, False, False),
     (0, -1.0, None, False, False),     # the input is the result
 ])
@@ -486,10 +488,25 @@ def test_chain_fit_equals_iterate_replay(gpu, g2, dtype, max_iter, tol, max_tria
     x0, u0 = dev(g2["x"], dtype), dev(g2["u"], dtype)
     if nan:
         x0[1, 3, 2] = float("nan")
-    ref = chain_fit_replay(s, x0, u0, max_iter, tol, max_trials)
+    xt0 = None
+    if inplace == "xtraj":
+        xt0 = x0.flip(1).contiguous()  # some other trajectory of states as the target
+    ref = chain_fit_replay(s, x0, u0, max_iter, tol, max_trials, x_traj=xt0)
     for _ in range(2):   # twice: the re-armed call-status words
         xi, ui = x0.clone(), u0.clone()
-        if inplace:
+        if inplace == "xtraj":
+            nb = xi.shape[0]
+            xt = xt0.clone()
+            uo = torch.empty_like(ui)
+            cost = torch.empty((nb,), dtype=dtype, device="cuda")
+            it = torch.empty((nb,), dtype=torch.int32, device="cuda")
+            st = torch.empty((nb,), dtype=torch.int32, device="cuda")
+            s._bind()
+            o = _lib.default_options(max_iter=max_iter, tol=tol, max_trials=max_trials)
+            p = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
+            cs = s.lib.ilqr_chain_fit(s.h, C.byref(o), p(xi), p(ui), p(xt), p(xt), p(uo), p(cost), p(it), p(st))
+            got = (xt, uo, cost, it, st, cs)
+        elif inplace:
             nb = xi.shape[0]
             cost = torch.empty((nb,), dtype=dtype, device="cuda")
             it = torch.empty((nb,), dtype=torch.int32, device="cuda")

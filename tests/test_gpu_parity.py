@@ -559,6 +559,34 @@ def test_fit_output_aliasing_input(gpu, max_iter, tol):
     assert torch.equal(st, ref.status) and torch.equal(cost, ref.cost)
 
 
+@pytest.mark.parametrize("max_iter,tol", [(1, -1.0), (3, -1.0), (6, 1e-8)])
+def test_fit_output_aliasing_x_traj(gpu, max_iter, tol):
+    """x_out = x_traj (a tracking target the caller overwrites with the result): every
+    iteration reads x_traj, so the last one must not write x_out directly — the gather
+    does, after the iterations. Same bits as the call with separate buffers."""
+    import ctypes as C
+    nb, T = 37, 20
+    lq, x, u = random_lq_batch(nb, 12, 4, T, seed=23)
+    xt_np = np.ascontiguousarray(x[:, ::-1]) * 0.5
+    s = Solver(12, 4, T, nb)
+    s.set_problem(lq)
+    ref = s.fit(dev(x), dev(u), x_traj=dev(xt_np), max_iter=max_iter, tol=tol)
+    xi, ui, xt = dev(x), dev(u), dev(xt_np)
+    uo = torch.empty_like(ui)
+    cost = torch.empty((nb,), dtype=torch.float64, device="cuda")
+    it = torch.empty((nb,), dtype=torch.int32, device="cuda")
+    st = torch.empty((nb,), dtype=torch.int32, device="cuda")
+    s._bind_stream()
+    o = _lib.default_options(max_iter=max_iter, tol=tol)
+    p = C.c_void_p
+    rc = s.lib.ilqr_fit(s.h, s._p(), C.byref(o), p(xi.data_ptr()), p(ui.data_ptr()), p(xt.data_ptr()),
+                        p(xt.data_ptr()), p(uo.data_ptr()), p(cost.data_ptr()), p(it.data_ptr()),
+                        p(st.data_ptr()))
+    assert rc == ref.call_status
+    assert torch.equal(xt, ref.x) and torch.equal(uo, ref.u) and torch.equal(it, ref.iters)
+    assert torch.equal(st, ref.status) and torch.equal(cost, ref.cost)
+
+
 @pytest.mark.parametrize("nb,T", [(4096, 100), (37, 17), (5, 3), (2051, 9)])
 def test_fused_iteration_equals_two_launches(gpu, nb, T):
     """ILQR_SCHED_FUSED (one kernel: the block backward then the ring forward per wave)
