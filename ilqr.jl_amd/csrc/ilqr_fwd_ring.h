@@ -832,19 +832,39 @@ __device__ __attribute__((unused)) int coop_find(const LSCoop& c, uint32_t gen, 
       e[k] = pos < n ? __hip_atomic_load(c.list + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                      : ((uint64_t)gen << 32) | 0xFFFFFFFFull;  // past the list: no entry
     }
-    int nx[CH], lim[CH];
+    int nx[CH], lim[CH], dist[CH];
 #pragma unroll
     for (int k = 0; k < CH; ++k) {
       const uint32_t bb = (uint32_t)e[k];
       const bool ok = (uint32_t)(e[k] >> 32) == gen && bb != 0xFFFFFFFFu;
       const LSCoopRec* R = c.rec + (ok ? bb : 0);
-      nx[k] = ok ? ag_ld(&R->next) : 0x7fffffff;
-      lim[k] = ok ? coop_lim_hint(R, max_trials) : 0;
+      // the record's words as three 64-bit relaxed loads (hints; the grab is exact): every
+      // idle wave scans the list, and with few searches they all hit the same few records
+      const uint64_t nb = ok ? __hip_atomic_load(reinterpret_cast<const uint64_t*>(&R->next), __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT)
+                             : 0;
+      const uint64_t sf = ok ? __hip_atomic_load(reinterpret_cast<const uint64_t*>(&R->stop), __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT)
+                             : 0;
+      const uint64_t m = ok ? __hip_atomic_load(&R->mask, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+      nx[k] = ok ? (int32_t)(uint32_t)nb : 0x7fffffff;
+      {
+        const int be = (int32_t)(uint32_t)(nb >> 32), st = (int32_t)(uint32_t)sf;
+        const int mn = be < st ? be : st;
+        lim[k] = ok ? (mn < max_trials ? mn : max_trials) : 0;
+      }
+      // how far its next quad lies past the trials known so far (1..front evaluated):
+      // the least speculative quad first — a search's first quad, or the next quad of a
+      // deep search whose handed-out trials have all come back rejected
+      const int front = ~m ? __builtin_ctzll(~m) : 64;
+      dist[k] = nx[k] - front;
       if ((uint32_t)(e[k] >> 32) != gen) unwritten = true;  // reserved, not yet written
     }
 #pragma unroll
     for (int k = 0; k < CH; ++k) {
-      const uint64_t key = ((uint64_t)(uint32_t)nx[k] << 32) | (uint32_t)(base + 64 * k + l);
+      const uint32_t dk = dist[k] < 1 ? 1u : (dist[k] > 127 ? 127u : (uint32_t)dist[k]);
+      const uint64_t key = ((uint64_t)dk << 56) | ((uint64_t)((uint32_t)nx[k] & 0xFFFFFFu) << 32) |
+                           (uint32_t)(base + 64 * k + l);
       if (nx[k] <= lim[k] && key < best) best = key;
     }
     // wave minimum
@@ -853,7 +873,7 @@ __device__ __attribute__((unused)) int coop_find(const LSCoop& c, uint32_t gen, 
       const uint64_t q = __shfl_xor(best, o);
       best = q < best ? q : best;
     }
-    if ((best >> 32) <= 2) break;  // nothing is fresher than an untouched trajectory
+    if ((best >> 56) <= 1) break;  // a quad right at its search's frontier: nothing ranks before it
   }
   unwritten = __any(unwritten);
   if (best == ~0ull) return -1;

@@ -2,6 +2,7 @@
 // (ilqr_lq.hip). Not installed; see include/ilqr.h for the public ABI.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <stddef.h>
 #include <stdint.h>
 
 namespace ilqr {
@@ -52,6 +53,10 @@ struct LSCoop {
   int32_t nslots;     // 0: no scratch (every finaliser rolls out)
 };
 constexpr int COOP_SCRATCH_SLOTS = 32;
+// coop_find reads (next, best) and (stop, fin) as one 64-bit word each
+static_assert(sizeof(LSCoopRec) == 32 && offsetof(LSCoopRec, best) == 4 && offsetof(LSCoopRec, stop) == 8 &&
+                  offsetof(LSCoopRec, fin) == 12 && offsetof(LSCoopRec, mask) == 16,
+              "LSCoopRec layout");
 constexpr int COOP_MAX_TRIALS = 64;
 
 // Buffers of one fused iteration (fit loop body).
