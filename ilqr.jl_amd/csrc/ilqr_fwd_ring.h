@@ -810,8 +810,10 @@ __device__ __forceinline__ void coop_publish(const LSCoop& c, uint32_t gen, int 
                      __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// A published trajectory with trials left to hand out, breadth first (smallest `next`,
-// ties to the first entry at or after this wave's rotated start); -1 if none. Relaxed
+// A published trajectory with trials left to hand out, the least speculative first (the
+// smallest distance of `next` past the trials its search has evaluated, then the smallest
+// `next`, then the first entry at or after this wave's rotated start); -1
+// if none. Relaxed
 // reads: a hint, the grab itself is exact. `unwritten`: a reserved list slot is not
 // written yet (its publisher is mid-way: the slot still holds another launch's entry).
 __device__ __attribute__((unused)) int coop_find(const LSCoop& c, uint32_t gen, int n, int max_trials,
