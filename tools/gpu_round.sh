@@ -1,6 +1,14 @@
 #!/bin/bash
 # One GPU session: tests, smoke, bench, kernel-trace profile, diagnostics. Each GPU
 # step has its own time limit; a crash-class exit (fault/abort/segv/timeout) stops.
+# The A/B steps (vanishab, headab, chainab, tlab) compare the product library with
+# ilqr.jl_amd/lib/variants/libilqr_hip_prev.so — the previous commit's build, made on the
+# CPU before the call:
+#   git archive HEAD ilqr.jl_amd/csrc include | tar -x -C /tmp/prev &&
+#   make -C /tmp/prev/ilqr.jl_amd/csrc ../lib/libilqr_hip.so &&
+#   cp /tmp/prev/ilqr.jl_amd/lib/libilqr_hip.so ilqr.jl_amd/lib/variants/libilqr_hip_prev.so
+# (chainab names it libilqr_hip_prevchain.so); spread and tail5 need the instrumented
+# build of tools/ablation/build_trace_lib.sh.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
