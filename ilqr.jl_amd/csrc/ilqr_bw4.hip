@@ -444,6 +444,7 @@ __global__ __launch_bounds__(64 * FUSED_WAVES) void lq_iter_fused4_kernel(LQPara
   const bool owner = MF ? (l < 16 && (l & 3) == 0) : (l & 15) == 0;
   const int q = MF ? (l >> 2) & 3 : l >> 4;
   unsigned active = 0;
+  unsigned own = 0;  // the wave's published trajectories (iter_forward_wave_coop)
   IterArgs ai = a;
   if (a.coop && wid == 0 && l == 0) {
     // the next launch's list length (this launch counts in ctl[gen & 1])
@@ -483,11 +484,11 @@ __global__ __launch_bounds__(64 * FUSED_WAVES) void lq_iter_fused4_kernel(LQPara
     if constexpr (MF)
       iter_forward_wave_mfma(P, b0, B, T, ai, ls, lds, run);
     else if (coop)
-      iter_forward_wave_coop<12, 4>(P, b0, B, T, ai, ls, lds, ((run >> (l >> 4)) & 1u) != 0);
+      own = iter_forward_wave_coop<12, 4>(P, b0, B, T, ai, ls, lds, ((run >> (l >> 4)) & 1u) != 0);
     else
       iter_forward_wave_active<12, 4>(P, b0, B, T, ai, ls, lds, ((run >> (l >> 4)) & 1u) != 0);
   }
-  if (coop) lq_coop_search<12, 4>(P, B, T, ai, ls, lds, wid);
+  if (coop) lq_coop_search<12, 4>(P, B, T, ai, ls, lds, wid, b0, own);
 }
 
 }  // namespace

@@ -1039,12 +1039,19 @@ __device__ void coop_evaluate(const LQParams& P, int b, int B, int T, const Iter
 // for the next launch; stale entries carry another generation.
 template <int NX, int NU>
 __device__ void lq_coop_search(const LQParams& P, int B, int T, const IterArgs& a, const LSParams& ls,
-                               double* ring, int wid) {
+                               double* ring, int wid, int b0, unsigned own) {
   const uint32_t gen = a.coop_gen;
   // the no-publication launch (every iteration from cold, most of a fit's) leaves after
   // ONE load: the list length straight from the kernel arguments
   if (__builtin_amdgcn_readfirstlane(ag_ld(a.coop_ctl + (gen & 1))) == 0) return;
   const LSCoop c = *a.coop;  // scalar loads, only once there is work
+  // first the quads of the wave's own published trajectories (`own`, bit q: b0 + q): a
+  // search's first quad then starts as its trial 1 ends, not when some wave frees up
+  // (≈50 µs later in the at-floor iteration, §4); a quad another wave took already
+  // makes this grab the next one, or nothing
+#pragma unroll 1
+  for (int q = 0; q < 4; ++q)
+    if ((own >> q) & 1u) coop_evaluate<NX, NU>(P, b0 + q, B, T, a, c, ls, ring);
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   // 200 µs at the 100 MHz real-time counter; the Makefile's `variants` target builds a
   // library with 0 (a wave leaves at the first unwritten slot it sees) for the test of
@@ -1070,9 +1077,9 @@ __device__ void lq_coop_search(const LQParams& P, int B, int T, const IterArgs& 
 // groups (the ring forward's sequential code at max_trials = 1); an accepted trajectory
 // is done as in iter_forward_wave_active, an open one is published.
 template <int NX, int NU>
-__device__ __forceinline__ void iter_forward_wave_coop(const LQParams& P, int b0, int B, int T,
-                                                       const IterArgs& a, const LSParams& ls,
-                                                       double* ring, bool active) {
+__device__ __forceinline__ unsigned iter_forward_wave_coop(const LQParams& P, int b0, int B, int T,
+                                                           const IterArgs& a, const LSParams& ls,
+                                                           double* ring, bool active) {
   const int j = threadIdx.x & 15;
   const int b = b0 + ((threadIdx.x & 63) >> 4);
   LSParams ls1 = ls;
@@ -1095,6 +1102,12 @@ __device__ __forceinline__ void iter_forward_wave_coop(const LQParams& P, int b0
       }
     }
   }
+  // the published groups, bit q (wave-uniform)
+  const uint64_t pub = __ballot(j == 0 && active && !r.accepted);
+  unsigned own = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) own |= ((pub >> (16 * q)) & 1ull) ? (1u << q) : 0u;
+  return own;
 }
 
 template <int NX, int NU, bool LR_REGS = true>
