@@ -959,7 +959,7 @@ __device__ void coop_finalize(const LQParams& P, int b, int B, int T, const Iter
 // Grab trials j0 .. j0+3 of trajectory b, evaluate them, and finalise b if these were
 // the last needed (whole wave).
 template <int NX, int NU>
-__device__ void coop_evaluate(const LQParams& P, int b, int B, int T, const IterArgs& a, const LSCoop& c,
+__device__ int coop_evaluate(const LQParams& P, int b, int B, int T, const IterArgs& a, const LSCoop& c,
                               const LSParams& ls, double* ring) {
   LSCoopRec* R = c.rec + b;
   const int l = threadIdx.x & 63, g = l >> 4;
@@ -973,7 +973,7 @@ __device__ void coop_evaluate(const LQParams& P, int b, int B, int T, const Iter
   lim0 = __builtin_amdgcn_readfirstlane(lim0);
   sl = __builtin_amdgcn_readfirstlane(sl);
   const bool scr = sl < c.nslots;  // every trial's rollout to the scratch
-  if (j0 > lim0) return;  // raced past the needed set: nothing to do
+  if (j0 > lim0) return 0;  // raced past the needed set: nothing to do
   const int j = j0 + g;   // this group's trial
   const bool mine = j <= lim0;
   // the cost to beat: written before this launch (in place by fit's finaliser of b only,
@@ -1026,6 +1026,7 @@ __device__ void coop_evaluate(const LQParams& P, int b, int B, int T, const Iter
   fin = __builtin_amdgcn_readfirstlane(fin);
   lim = __builtin_amdgcn_readfirstlane(lim);
   if (fin) coop_finalize<NX, NU>(P, b, B, T, a, c, ls, ring, lim, sl);
+  return fin ? 2 : 1;  // 1: a quad evaluated, the search not finalised here; 2: finalised
 }
 
 // The work loop every wave of the launch enters once it is done with its own
@@ -1052,6 +1053,13 @@ __device__ void lq_coop_search(const LQParams& P, int B, int T, const IterArgs& 
 #pragma unroll 1
   for (int q = 0; q < 4; ++q)
     if ((own >> q) & 1u) coop_evaluate<NX, NU>(P, b0 + q, B, T, a, c, ls, ring);
+  // then stay on them: each further quad of an own search that is still open (the wave
+  // knows its last quad's outcome first), up to the first one with nothing left to grab
+#pragma unroll 1
+  for (int q = 0; q < 4; ++q)
+    if ((own >> q) & 1u)
+      for (int k = 0; k < COOP_MAX_TRIALS / 4; ++k)
+        if (coop_evaluate<NX, NU>(P, b0 + q, B, T, a, c, ls, ring) != 1) break;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   // 200 µs at the 100 MHz real-time counter; the Makefile's `variants` target builds a
   // library with 0 (a wave leaves at the first unwritten slot it sees) for the test of
