@@ -145,6 +145,19 @@ struct LDLT {
       for (int p = i + 1; p < NU; ++p) x[i] = fma(-l[p][i], x[p], x[i]);
     return x;
   }
+  // in place, a right-hand side of NU entries (the wide tiles kernel, NU = 8)
+  __device__ __forceinline__ void solve_n(double (&x)[NU]) const {
+#pragma unroll
+    for (int i = 0; i < NU; ++i)
+#pragma unroll
+      for (int p = 0; p < i; ++p) x[i] = fma(-l[i][p], x[p], x[i]);
+#pragma unroll
+    for (int i = 0; i < NU; ++i) x[i] *= dinv[i];
+#pragma unroll
+    for (int i = NU - 1; i >= 0; --i)
+#pragma unroll
+      for (int p = i + 1; p < NU; ++p) x[i] = fma(-l[p][i], x[p], x[i]);
+  }
 };
 
 }  // namespace

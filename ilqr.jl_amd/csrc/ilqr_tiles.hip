@@ -212,14 +212,221 @@ __global__ __launch_bounds__(256) void tiles_backward_kernel(TileParams P, int B
   if (status && (threadIdx.x & 63) == 0) status[b] = nan ? ILQR_TRAJ_NAN : ILQR_TRAJ_OK;
 }
 
+// ---------------------------------------------------------------------------------
+// WIDE shapes: nx ≤ 16, nu ≤ 8 (the reference's RBD caller is nx = 16, nu = 8, T = 1000:
+// test/RBD_2_link_example/animate_RBD_2_link.jl:8,19-20,31). F = [A | B] no longer fits
+// one 16×16 tile beside the value gradient, so the recursion is split over 16×16 tiles
+// of v_mfma_f64_16x16x4_f64 (lane 16q + c holds row q + 4r, column c of an accumulator):
+//   Y_A = S·A,  Y_B = S·B + s·e₈ᵀ          (B in columns 0..7, s rides in column 8)
+//   Z_xx = lxx + AᵀY_A                     (:270's AᵀSA part)
+//   Z_xe = [· | lx] + AᵀY_B                (column 8: 𝐪 + Aᵀ𝐬, :269)
+//   Z_ux = lux + BᵀY_A = G                 (:182)
+//   Z_ue = [luu | lu] + BᵀY_B = [H | g]    (:181, :183)
+// one LDS hand-off of G, H, g; every lane factors H + μI (LDLᵀ, 8×8) and solves its
+// column of G and g; the exact rank-nu step_back (as the narrow kernel):
+//   S ← Z_xx − Kᵀ(H + 2μI)K,  s ← (Z_xe − Kᵀ(H + 2μI)·[· | d]) column 8.
+// 28 MFMAs per step. The dimensions are run-time values zero-padded to 16 × 8: padded
+// rows/columns of A, B and the cost tiles are zero, so the padded gains are zero and the
+// real ones are unchanged (the LDLᵀ pivots of the padding come last and are exactly μ).
+// ---------------------------------------------------------------------------------
+constexpr int TW_NX = 16, TW_NU = 8;
+constexpr int TW_LDS = 128 + 128 + 16 * 17;  // G rows, [H | g] rows, symmetrisation tile
+
+__device__ __forceinline__ double pick4(const double (&v)[TW_NU], int q, int base) {
+  const double a = (q & 1) ? v[base + 1] : v[base];
+  const double b = (q & 1) ? v[base + 3] : v[base + 2];
+  return (q & 2) ? b : a;
+}
+
+struct WideTile {
+  double fA[4];  // A[4kk+q][c]
+  double fB[4];  // B[4kk+q][c]
+  d4 Lxx;        // lxx[q+4r][c]
+  d4 Lux;        // lux[q+4r][c] (rows < nu)
+  d4 Lue;        // [luu | lu][q+4r][c]
+  d4 Lxe;        // lx[q+4r] in column 8
+};
+
+__device__ bool tiles_backward_wide_wave(const TileParams& P, int b, int T, int nx, int nu,
+                                         double* __restrict__ d_out, double* __restrict__ K_out,
+                                         double mu, double* lds) {
+  const int l = threadIdx.x & 63;
+  const int c = l & 15;
+  const int q = l >> 4;
+  const bool cx = c < nx;
+  const bool cu = c < nu;
+  const bool c8 = c == 8;
+  const size_t bt = (size_t)b * T;
+  const size_t sxx = (size_t)nx * nx, sxu = (size_t)nx * nu, suu = (size_t)nu * nu;
+  const double* A0 = P.A + bt * sxx;
+  const double* B0 = P.B + bt * sxu;
+  const double* lx0 = P.lx + bt * nx;
+  const double* lu0 = P.lu + bt * nu;
+  const double* lxx0 = P.lxx + bt * sxx;
+  const double* lux0 = P.lux ? P.lux + bt * sxu : nullptr;
+  const double* luu0 = P.luu + bt * suu;
+
+  auto load = [&](int t, WideTile& s) {
+    const double* A = A0 + (size_t)t * sxx;
+    const double* Bm = B0 + (size_t)t * sxu;
+    const double* lxx = lxx0 + (size_t)t * sxx;
+    const double* luu = luu0 + (size_t)t * suu;
+    const double* lx = lx0 + (size_t)t * nx;
+    const double* lu = lu0 + (size_t)t * nu;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const int i = 4 * kk + q;
+      const bool ri = i < nx;
+      s.fA[kk] = ldz(ri && cx, A + i * nx + c, A);
+      s.fB[kk] = ldz(ri && cu, Bm + i * nu + c, Bm);
+      s.Lxx[kk] = ldz(ri && cx, lxx + i * nx + c, lxx);
+      s.Lxe[kk] = ldz(ri && c8, lx + i, lx);
+    }
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int i = q + 4 * r;
+      const bool ru = i < nu;
+      if (lux0) {
+        const double* lux = lux0 + (size_t)t * sxu;
+        s.Lux[r] = ldz(ru && cx, lux + i * nx + c, lux);
+      } else {
+        s.Lux[r] = 0.0;
+      }
+      s.Lue[r] = ldz(ru && cu, luu + i * nu + c, luu) + ldz(ru && c8, lu + i, lu);
+    }
+    s.Lux[2] = s.Lux[3] = s.Lue[2] = s.Lue[3] = 0.0;
+  };
+
+  double* Gl = lds;        // G[j][c], j < 8
+  double* Hl = lds + 128;  // [H | g][j][c], j < 8, c ≤ 8
+  double* tile = lds + 256;
+
+  // terminal value function (:335-336): S = ∇²ℓ_f, s = ∇ℓ_f (column 8 of Sx)
+  d4 S, Sx;
+  {
+    const double* lfxx = P.lfxx + (size_t)b * sxx;
+    const double* lfx = P.lfx + (size_t)b * nx;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = q + 4 * r;
+      S[r] = ldz(i < nx && cx, lfxx + i * nx + c, lfxx);
+      Sx[r] = ldz(i < nx && c8, lfx + i, lfx);
+    }
+  }
+
+  bool nan = false;
+  double* Kb = K_out + bt * nu * nx;
+  double* db = d_out + bt * nu;
+  WideTile cur, nxt;
+  load(T - 1, cur);
+  for (int t = T - 1; t >= 0; --t) {
+    load(t > 0 ? t - 1 : 0, nxt);  // prefetch
+
+    d4 YA = {0.0, 0.0, 0.0, 0.0};
+    d4 YB;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) YB[r] = c8 ? Sx[r] : 0.0;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      YA = mfma(S[kk], cur.fA[kk], YA);
+      YB = mfma(S[kk], cur.fB[kk], YB);
+    }
+    d4 Zxx = cur.Lxx, Zxe = cur.Lxe, Zux = cur.Lux, Zue = cur.Lue;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      Zxx = mfma(cur.fA[kk], YA[kk], Zxx);
+      Zxe = mfma(cur.fA[kk], YB[kk], Zxe);
+      Zux = mfma(cur.fB[kk], YA[kk], Zux);
+      Zue = mfma(cur.fB[kk], YB[kk], Zue);
+    }
+
+    // hand-off: G (rows q, q+4) and [H | g] (rows q, q+4)
+    Gl[q * 16 + c] = Zux[0];
+    Gl[(q + 4) * 16 + c] = Zux[1];
+    Hl[q * 16 + c] = Zue[0];
+    Hl[(q + 4) * 16 + c] = Zue[1];
+    wave_lds_fence();
+    double h[TW_NU][TW_NU];
+#pragma unroll
+    for (int i = 0; i < TW_NU; ++i)
+#pragma unroll
+      for (int k = 0; k <= i; ++k) h[i][k] = Hl[i * 16 + k];
+    double xs[TW_NU], xd[TW_NU];
+#pragma unroll
+    for (int j = 0; j < TW_NU; ++j) {
+      xs[j] = Gl[j * 16 + c];
+      xd[j] = Hl[j * 16 + 8];
+    }
+    wave_lds_fence();
+
+    // feedback_parameters (:207-218): (H + μI) x = [G[:, c] | g]
+    LDLT<TW_NU> f;
+    f.factor(h, mu);
+    f.solve_n(xs);
+    f.solve_n(xd);
+    const double a0 = pick4(xs, q, 0), a1 = pick4(xs, q, 4);  // −K[q][c], −K[q+4][c]
+    const double e0 = pick4(xd, q, 0), e1 = pick4(xd, q, 4);  // −d[q], −d[q+4]
+    nan |= __builtin_isnan(a0) | __builtin_isnan(a1) | __builtin_isnan(e0) | __builtin_isnan(e1);
+    {
+      double* Kt = Kb + (size_t)t * nu * nx;
+      double* dt = db + (size_t)t * nu;
+      if (cx && q < nu) Kt[q * nx + c] = -a0;
+      if (cx && q + 4 < nu) Kt[(q + 4) * nx + c] = -a1;
+      if (c == 0 && q < nu) dt[q] = -e0;
+      if (c == 0 && q + 4 < nu) dt[q + 4] = -e1;
+    }
+
+    // step_back (:269-270), exact rewrite: W = (H + 2μI)K = μK − G, w = μd − g
+    const double w0 = fma(-mu, a0, -Zux[0]), w1 = fma(-mu, a1, -Zux[1]);
+    const double v0 = c8 ? fma(-mu, e0, -Zue[0]) : 0.0;  // lane (8, q) holds g[q], g[q+4]
+    const double v1 = c8 ? fma(-mu, e1, -Zue[1]) : 0.0;
+    S = mfma(a1, w1, mfma(a0, w0, Zxx));
+    Sx = mfma(a1, v1, mfma(a0, v0, Zxe));
+    cur = nxt;
+
+    if ((t % TB_SYM_EVERY) == 0) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) tile[(q + 4 * r) * 17 + c] = S[r];
+      wave_lds_fence();
+#pragma unroll
+      for (int r = 0; r < 4; ++r) S[r] = 0.5 * (S[r] + tile[c * 17 + q + 4 * r]);
+      wave_lds_fence();
+    }
+  }
+  return __any(nan);
+}
+
+__global__ __launch_bounds__(256) void tiles_backward_wide_kernel(TileParams P, int B, int T, int nx,
+                                                                  int nu, double* __restrict__ d,
+                                                                  double* __restrict__ K,
+                                                                  int32_t* __restrict__ status,
+                                                                  double mu) {
+  __shared__ __attribute__((aligned(16))) double lds[4 * TW_LDS];
+  const int w = threadIdx.x >> 6;
+  const int b = blockIdx.x * 4 + w;
+  if (b >= B) return;
+  const bool nan = tiles_backward_wide_wave(P, b, T, nx, nu, d, K, mu, lds + w * TW_LDS);
+  if (status && (threadIdx.x & 63) == 0) status[b] = nan ? ILQR_TRAJ_NAN : ILQR_TRAJ_OK;
+}
+
+bool tiles_narrow(int nx, int nu) { return nx >= 1 && nx <= 12 && nu >= 1 && nu <= 4; }
+
 }  // namespace
 
-// every state dimension 1..12 with 1..4 inputs (nx + nu ≤ 16, nu ≤ 4: one MFMA tile)
-bool tiles_supported(int nx, int nu) { return nx >= 1 && nx <= 12 && nu >= 1 && nu <= 4; }
+// every state dimension 1..12 with 1..4 inputs in one MFMA tile (compiled per shape);
+// up to nx = 16, nu = 8 on the tiled wide kernel (run-time dimensions)
+bool tiles_supported(int nx, int nu) {
+  return tiles_narrow(nx, nu) || (nx >= 1 && nx <= TW_NX && nu >= 1 && nu <= TW_NU);
+}
 
 hipError_t launch_tiles_backward(int nx, int nu, const TileParams& p, int B, int T, double* d,
                                  double* K, int32_t* status, double mu, hipStream_t s) {
   const int grid = (B + 3) / 4;
+  if (!tiles_narrow(nx, nu)) {
+    if (!tiles_supported(nx, nu)) return hipErrorInvalidValue;
+    tiles_backward_wide_kernel<<<grid, 256, 0, s>>>(p, B, T, nx, nu, d, K, status, mu);
+    return hipGetLastError();
+  }
 #define ILQR_TILES_CASE(NXV, NUV)                                                              \
   if (nx == NXV && nu == NUV) {                                                                \
     tiles_backward_kernel<NXV, NUV><<<grid, 256, 0, s>>>(p, B, T, d, K, status, mu);          \

@@ -28,6 +28,8 @@ forward_pass and, in fit, stops that trajectory at its current iterate.
 """
 from __future__ import annotations
 
+import contextlib
+import threading
 import warnings
 
 import numpy as np
@@ -109,11 +111,48 @@ def _chain_solver(xb, ub, dynamicsf, immediate_cost, final_cost, dtype):
     return s
 
 
+# The closure path's tiles handles, one per (device, nx, nu, T, batch), kept between
+# calls (an MPC loop calling fit allocates no device workspace per call). A call checks
+# its handle OUT of the cache and back in when done, so two threads fitting the same
+# shape at once never share one (the second builds its own; the surplus is closed on
+# check-in). At most _TILES_MAX shapes stay cached, least recently used evicted.
+_TILES_CACHE: dict = {}
+_TILES_LOCK = threading.Lock()
+_TILES_MAX = 8
+
+
+@contextlib.contextmanager
 def _tiles_solver(xb, ub):
     nb, N, nx = xb.shape
     _, M, nu = ub.shape
     assert N == M + 1, "size(x)[1] == size(u)[1] + 1"   # backward_pass.jl:329
-    return Solver(nx, nu, M, nb, device=_device(), kind=_lib.PROBLEM_TILES)
+    key = (_device(), nx, nu, M, nb)
+    with _TILES_LOCK:
+        s = _TILES_CACHE.pop(key, None)
+    if s is None:
+        s = Solver(nx, nu, M, nb, device=key[0], kind=_lib.PROBLEM_TILES)
+    try:
+        yield s
+    finally:
+        evicted = []
+        with _TILES_LOCK:
+            if key in _TILES_CACHE:
+                evicted.append(s)
+            else:
+                _TILES_CACHE[key] = s
+                while len(_TILES_CACHE) > _TILES_MAX:
+                    evicted.append(_TILES_CACHE.pop(next(iter(_TILES_CACHE))))
+        for e in evicted:
+            e.close()
+
+
+def clear_cache():
+    """Close the tiles handles fit / backward_pass keep per shape for closures."""
+    with _TILES_LOCK:
+        ss = list(_TILES_CACHE.values())
+        _TILES_CACHE.clear()
+    for s in ss:
+        s.close()
 
 
 def _solver(xb, ub, dynamicsf, immediate_cost, final_cost):
@@ -139,18 +178,19 @@ def backward_pass(x, u, dynamicsf, immediate_cost, final_cost):
     ub, _, _ = _as_batch(u, "u", 2)
     fam = _family(dynamicsf, immediate_cost, final_cost)
     if fam == "closures":
-        s = _tiles_solver(xb, ub)
-        tl = _tiles.derivative_tiles(xb, ub, dynamicsf, immediate_cost, final_cost)
-        d, K, st = s.backward_tiles(tl)
+        with _tiles_solver(xb, ub) as s:
+            tl = _tiles.derivative_tiles(xb, ub, dynamicsf, immediate_cost, final_cost)
+            d, K, st = s.backward_tiles(tl)
     elif fam == "chain":
         dt = _eltype(x)
         xb, ub = xb.to(dt), ub.to(dt)
         s = _chain_solver(xb, ub, dynamicsf, immediate_cost, final_cost, dt)
         d, K, st = s.backward(xb, ub)
+        s.close()
     else:
         s = _solver(xb, ub, dynamicsf, immediate_cost, final_cost)
         d, K, st = s.backward(xb, ub)
-    s.close()
+        s.close()
     if bool((st == _lib.TRAJ_NAN).any()):
         raise AssertionError("!any(isnan, δu/K) failed")   # backward_pass.jl:353-354
     return _out(d, batched, is_t), _out(K, batched, is_t)
@@ -252,9 +292,14 @@ def _fit_closures(xb, ub, xt, dynamicsf, immediate_cost, final_cost, max_iter, t
     derivative tiles (torch.func on the device) → ilqr_backward_tiles (HIP) →
     forward_pass rollout of the user dynamics (torch on the device). Trajectories
     that converge, exhaust their line search or hit NaN stop; the rest continue."""
+    with _tiles_solver(xb, ub) as s:
+        return _fit_closures_on(s, xb, ub, xt, dynamicsf, immediate_cost, final_cost, max_iter, tol,
+                                history)
+
+
+def _fit_closures_on(s, xb, ub, xt, dynamicsf, immediate_cost, final_cost, max_iter, tol, history):
     from .solver import FitResult
     nb = xb.shape[0]
-    s = _tiles_solver(xb, ub)
     dev = xb.device
     xi, ui = xb.clone(), ub.clone()
     prev = torch.full((nb,), float("inf"), dtype=torch.float64, device=dev)   # :159
@@ -295,7 +340,6 @@ def _fit_closures(xb, ub, xt, dynamicsf, immediate_cost, final_cost, max_iter, t
         step = acc & ~conv
         xi = torch.where(step[:, None, None], xn, xi)                            # :174-175
         ui = torch.where(step[:, None, None], un, ui)
-    s.close()
     status = torch.where(status == _lib.TRAJ_OK, _lib.TRAJ_MAX_ITER, status).to(torch.int32)
     return FitResult(xi, ui, prev, iters, status, _lib.OK, hist)
 
@@ -303,6 +347,6 @@ def _fit_closures(xb, ub, xt, dynamicsf, immediate_cost, final_cost, max_iter, t
 from .helpers import (feedback_parameters, final_cost_quadratization,  # noqa: E402  (the per-step API)
                       immediate_cost_quadratization, linearize_dynamics, optimal_controller_param, step_back)
 
-__all__ = ["fit", "backward_pass", "forward_pass", "LineSearchExhausted", "linearize_dynamics",
+__all__ = ["fit", "backward_pass", "forward_pass", "LineSearchExhausted", "clear_cache", "linearize_dynamics",
            "immediate_cost_quadratization", "final_cost_quadratization", "optimal_controller_param",
            "feedback_parameters", "step_back"]

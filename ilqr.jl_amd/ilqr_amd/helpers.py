@@ -106,11 +106,12 @@ def _linearize(x, u, dynamicsf, nb, nx, nu, T):
         finally:
             s.close()
         return A, Bm
-    from torch.func import jacfwd, vmap  # any other torch closure: ForwardDiff's role
+    # any other torch closure: ForwardDiff's role, in reverse mode (tiles.py: PyTorch's
+    # vmapped forward-mode derivative of linalg.solve is wrong)
+    from torch.func import jacrev, vmap
     xs, us = x[:, :T].reshape(-1, nx), u.reshape(-1, nu)
     try:
-        A = vmap(jacfwd(dynamicsf, argnums=0))(xs, us)   # :32
-        Bm = vmap(jacfwd(dynamicsf, argnums=1))(xs, us)  # :33
+        A, Bm = vmap(jacrev(dynamicsf, argnums=(0, 1)))(xs, us)   # :32-33
     except (TypeError, RuntimeError, ValueError) as e:
         raise NotImplementedError("closures must be written with torch operations on 1-D tensors "
                                   f"(torch.func could not differentiate them: {e})") from e

@@ -3,9 +3,13 @@
 The reference differentiates its user callbacks with ForwardDiff
 (src/backward_pass.jl:25-40 linearize_dynamics, :81-109
 immediate_cost_quadratization, :134-153 final_cost_quadratization). Here the
-same derivatives are taken with torch.func forward-mode AD (jacfwd), vmapped
-over every (trajectory, time step) at once ON THE GPU; the Riccati recursion
-then runs in the HIP kernel behind ilqr_backward_tiles.
+same derivatives are taken with torch.func, vmapped over every (trajectory, time
+step) at once ON THE GPU; the Riccati recursion then runs in the HIP kernel behind
+ilqr_backward_tiles. The derivatives are exact like ForwardDiff's, but taken in
+REVERSE mode (jacrev): PyTorch 2.10's batching rule for the forward-mode derivative
+of linalg.solve / lu_solve under vmap returns wrong values (off by O(1) relative;
+tests/test_closures.py keeps the counter-example), and a dynamics closure solving
+M v̇ = τ − b — the reference's RBD example, RBD_helper_functions.jl:64 — hits it.
 
 Closures must be written with torch operations on 1-D tensors — the analogue of
 the reference's eltype-generic Julia closures:
@@ -24,30 +28,28 @@ TILE_NAMES = ("A", "B", "lx", "lu", "lxx", "lux", "luu", "lfx", "lfxx")
 
 def derivative_tiles(x, u, dynamicsf, immediate_cost, final_cost):
     """x (B, T+1, nx), u (B, T, nu) CUDA float64 → dict of ilqr_tiles tensors."""
-    from torch.func import jacfwd, vmap
+    from torch.func import jacrev, vmap
     nb, N, nx = x.shape
     T, nu = u.shape[1], u.shape[2]
     try:
-        return _tiles(x, u, dynamicsf, immediate_cost, final_cost, jacfwd, vmap, nb, nx, T, nu)
+        return _tiles(x, u, dynamicsf, immediate_cost, final_cost, jacrev, vmap, nb, nx, T, nu)
     except (TypeError, RuntimeError, ValueError) as e:
         raise NotImplementedError(
             "generic closures must be written with torch operations on 1-D tensors "
             f"(torch.func could not differentiate them: {e})") from e
 
 
-def _tiles(x, u, dynamicsf, immediate_cost, final_cost, jacfwd, vmap, nb, nx, T, nu):
+def _tiles(x, u, dynamicsf, immediate_cost, final_cost, jac, vmap, nb, nx, T, nu):
     xs = x[:, :T].reshape(-1, nx)
     us = u.reshape(-1, nu)
-    A = vmap(jacfwd(dynamicsf, argnums=0))(xs, us)                      # :32
-    Bm = vmap(jacfwd(dynamicsf, argnums=1))(xs, us)                     # :33
-    lx = vmap(jacfwd(immediate_cost, argnums=0))(xs, us)                # :95,102
-    lu = vmap(jacfwd(immediate_cost, argnums=1))(xs, us)                # :96,103
-    lxx = vmap(jacfwd(jacfwd(immediate_cost, argnums=0), argnums=0))(xs, us)  # :97,104
-    lux = vmap(jacfwd(jacfwd(immediate_cost, argnums=1), argnums=0))(xs, us)  # :98,105 (m×n)
-    luu = vmap(jacfwd(jacfwd(immediate_cost, argnums=1), argnums=1))(xs, us)  # :99,106
+    A, Bm = vmap(jac(dynamicsf, argnums=(0, 1)))(xs, us)                # :32-33
+    lx, lu = vmap(jac(immediate_cost, argnums=(0, 1)))(xs, us)          # :95-96,102-103
+    lxx = vmap(jac(jac(immediate_cost, argnums=0), argnums=0))(xs, us)  # :97,104
+    lux = vmap(jac(jac(immediate_cost, argnums=1), argnums=0))(xs, us)  # :98,105 (m×n)
+    luu = vmap(jac(jac(immediate_cost, argnums=1), argnums=1))(xs, us)  # :99,106
     xN = x[:, T]
-    lfx = vmap(jacfwd(final_cost))(xN)                                  # :142
-    lfxx = vmap(jacfwd(jacfwd(final_cost)))(xN)                         # :143
+    lfx = vmap(jac(final_cost))(xN)                                     # :142
+    lfxx = vmap(jac(jac(final_cost)))(xN)                               # :143
     out = {"A": A.reshape(nb, T, nx, nx), "B": Bm.reshape(nb, T, nx, nu),
            "lx": lx.reshape(nb, T, nx), "lu": lu.reshape(nb, T, nu),
            "lxx": lxx.reshape(nb, T, nx, nx), "lux": lux.reshape(nb, T, nu, nx),

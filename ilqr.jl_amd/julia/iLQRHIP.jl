@@ -269,17 +269,22 @@ function derivative_tiles(x::AbstractMatrix, u::AbstractMatrix, f, ℓ, ℓf)
     return (A=A, B=B, lx=lx, lu=lu, lxx=lxx, lux=lux, luu=luu, lfx=lfx, lfxx=lfxx)
 end
 
+# backward_pass on the resident tiles workspace of this shape (TilesSolver, cached): the
+# host tiles go into buffers allocated once, so fit_tiles' iterations allocate nothing
+# on the device
 function backward_tiles_device(x::AbstractMatrix, u::AbstractMatrix, f, ℓ, ℓf)
     N, nx = size(x); M, nu = size(u)
-    h = Handle(nx, nu, M, 1)
     t = derivative_tiles(x, u, f, ℓ, ℓf)
-    tl = Ref(Tiles(upload(h, t.A), upload(h, t.B), upload(h, t.lx), upload(h, t.lu), upload(h, t.lxx),
-                   upload(h, t.lux), upload(h, t.luu), upload(h, t.lfx), upload(h, t.lfxx)))
-    dd = alloc(h, Float64, M * nu); Kd = alloc(h, Float64, M * nu * nx); st = alloc(h, Int32, 1)
-    check(ccall((:ilqr_backward_tiles, libilqr), Cint,
-                (Ptr{Cvoid}, Ref{Tiles}, Ref{Options}, Ptr{Float64}, Ptr{Float64}, Ptr{Int32}),
-                h.ptr, tl, default_options(), dd, Kd, st), "ilqr_backward_tiles")
-    return from_abi(download!(h, zeros(nu, M), dd)), gains_from_abi(download!(h, zeros(nx, nu, M), Kd))
+    return with_cached(TILES_CACHE, () -> TilesSolver(nx, nu, M), (nx, nu, M)) do s
+        for (p, a) in ((s.tl.A, t.A), (s.tl.B, t.B), (s.tl.lx, t.lx), (s.tl.lu, t.lu), (s.tl.lxx, t.lxx),
+                       (s.tl.lux, t.lux), (s.tl.luu, t.luu), (s.tl.lfx, t.lfx), (s.tl.lfxx, t.lfxx))
+            upload!(s.h, p, a)
+        end
+        check(ccall((:ilqr_backward_tiles, libilqr), Cint,
+                    (Ptr{Cvoid}, Ref{Tiles}, Ref{Options}, Ptr{Float64}, Ptr{Float64}, Ptr{Int32}),
+                    s.h.ptr, Ref(s.tl), default_options(), s.d, s.K, s.status), "ilqr_backward_tiles")
+        (from_abi(download!(s.h, zeros(nu, M), s.d)), gains_from_abi(download!(s.h, zeros(nx, nu, M), s.K)))
+    end
 end
 
 """backward_pass(x, u, dynamicsf, immediate_cost, final_cost) -> (δu::T×nu, K::T×nu×nx)"""
@@ -289,7 +294,9 @@ function backward_pass(x::AbstractMatrix, u::AbstractMatrix, dynamicsf, immediat
     family(dynamicsf, immediate_cost, final_cost) == :tiles &&
         return backward_tiles_device(x, u, dynamicsf, immediate_cost, final_cost)
     # the resident solver of this shape (no allocation per call): δu (T × nu), K (T × nu × nx) like 𝐊s
-    return backward!(set_problem!(cached_solver(nx, nu, M), dynamicsf, immediate_cost, final_cost), x, u)
+    return with_cached(SOLVER_CACHE, () -> Solver(nx, nu, M, 1), (nx, nu, M)) do s
+        backward!(set_problem!(s, dynamicsf, immediate_cost, final_cost), x, u)
+    end
 end
 
 # total_cost_generator (forward_pass.jl:182-196), for the host rollout of the tiles path
@@ -331,8 +338,9 @@ function forward_pass(x::AbstractMatrix, u::AbstractMatrix, x_traj::AbstractMatr
     @assert(N == M + 1)                                                 # forward_pass.jl:62
     family(dynamicsf, immediate_cost, final_cost) == :tiles &&
         return forward_host(x, u, x_traj, δu, K, prev_cost, dynamicsf, immediate_cost, final_cost)
-    s = set_problem!(cached_solver(nx, nu, M), dynamicsf, immediate_cost, final_cost)
-    return forward!(s, x, u, x_traj, δu, K, prev_cost)
+    return with_cached(SOLVER_CACHE, () -> Solver(nx, nu, M, 1), (nx, nu, M)) do s
+        forward!(set_problem!(s, dynamicsf, immediate_cost, final_cost), x, u, x_traj, δu, K, prev_cost)
+    end
 end
 
 # the reference's per-iteration line (forward_pass.jl:167), from a fit's history
@@ -355,8 +363,10 @@ function fit(x_init::AbstractMatrix, u_init::AbstractMatrix, dynamicsf, immediat
         return fit_tiles(x_init, u_init, dynamicsf, immediate_cost, final_cost, x_traj, max_iter, tol, verbose)
     # the resident solver of this shape: an MPC loop calling fit allocates nothing per call;
     # an exhausted line search returns the last iterate (fit_resident!)
-    s = set_problem!(cached_solver(nx, nu, M), dynamicsf, immediate_cost, final_cost)
-    return fit!(s, x_init, u_init; x_traj=x_traj, max_iter=max_iter, tol=tol, verbose=verbose)
+    return with_cached(SOLVER_CACHE, () -> Solver(nx, nu, M, 1), (nx, nu, M)) do s
+        fit!(set_problem!(s, dynamicsf, immediate_cost, final_cost), x_init, u_init;
+             x_traj=x_traj, max_iter=max_iter, tol=tol, verbose=verbose)
+    end
 end
 
 # fit (forward_pass.jl:148-179) for arbitrary closures: tiles backward on the GPU, host
@@ -502,7 +512,7 @@ results, the gains — allocated ONCE here and reused by every call (include/ilq
 calls never allocate"), for an MPC loop calling fit over and over (forward_pass.jl:148-179).
 The history scratch of verbose fits grows on demand. close(s) frees everything at once;
 the finalizer is only a backstop. The functional fit / backward_pass / forward_pass above
-run on a cached Solver per shape (cached_solver; clear_cache!() closes them)."""
+run on a cached Solver per shape (with_cached; clear_cache!() closes them)."""
 mutable struct Solver
     h::Handle
     nx::Int; nu::Int; M::Int; nb::Int
@@ -512,6 +522,7 @@ mutable struct Solver
     d::Ptr{Float64}; K::Ptr{Float64}; pc::Ptr{Float64}; cost::Ptr{Float64}
     iters::Ptr{Int32}; status::Ptr{Int32}; trials::Ptr{Int32}
     hc::Ptr{Float64}; ht::Ptr{Int32}; hcap::Int
+    lock::ReentrantLock      # held by the functional entry points for a whole call (with_cached)
 end
 
 function Solver(nx::Integer, nu::Integer, T::Integer, batch::Integer; device::Integer=0)
@@ -524,10 +535,34 @@ function Solver(nx::Integer, nu::Integer, T::Integer, batch::Integer; device::In
                   f(N * nx), f(T * nu), f(N * nx), f(N * nx), f(T * nu),         # x u x_traj x̄ ū
                   f(T * nu), f(T * nu * nx), f(1), f(1),                          # δu K prev_cost cost
                   i(1), i(1), i(1),                                               # iters status trials
-                  Ptr{Float64}(C_NULL), Ptr{Int32}(C_NULL), 0)
+                  Ptr{Float64}(C_NULL), Ptr{Int32}(C_NULL), 0, ReentrantLock())
 end
 
-Base.close(s::Solver) = close(s.h)
+Base.close(s::Solver) = lock(() -> close(s.h), s.lock)
+
+"""TilesSolver(nx, nu, T): the resident workspace of the arbitrary-closure path — a handle
+and the device buffers of one trajectory's derivative tiles (ilqr_tiles: A, B, lx, lu,
+lxx, lux, luu, lfx, lfxx) and its gains (δu, K, status), allocated once per shape and
+reused by every backward_pass / fit iteration (include/ilqr.h: "hot calls never
+allocate"). Shapes: every nx ≤ 16, nu ≤ 8 — the reference's RBD caller is 16 × 8 at
+T = 1000 (test/RBD_2_link_example/animate_RBD_2_link.jl:8,19-20,31)."""
+mutable struct TilesSolver
+    h::Handle
+    nx::Int; nu::Int; M::Int
+    tl::Tiles
+    d::Ptr{Float64}; K::Ptr{Float64}; status::Ptr{Int32}
+    lock::ReentrantLock
+end
+
+function TilesSolver(nx::Integer, nu::Integer, T::Integer; device::Integer=0)
+    h = Handle(nx, nu, T, 1; device=device)
+    f(n) = alloc(h, Float64, n)
+    tl = Tiles(f(T * nx * nx), f(T * nx * nu), f(T * nx), f(T * nu), f(T * nx * nx),   # A B lx lu lxx
+               f(T * nu * nx), f(T * nu * nu), f(nx), f(nx * nx))                      # lux luu lfx lfxx
+    return TilesSolver(h, nx, nu, T, tl, f(T * nu), f(T * nu * nx), alloc(h, Int32, 1), ReentrantLock())
+end
+
+Base.close(s::TilesSolver) = lock(() -> close(s.h), s.lock)
 
 problem_ref(s::Solver) = Ref(s.kind == ILQR_PROBLEM_LQ ? Problem(ILQR_PROBLEM_LQ, 0, s.A, s.B, s.Q, s.R, s.Qf) :
                                                        Problem(s.kind, 0, C_NULL, C_NULL, C_NULL, C_NULL, C_NULL))
@@ -640,16 +675,60 @@ function forward!(s::Solver, x::AbstractMatrix, u::AbstractMatrix, x_traj::Abstr
             download!(s.h, zeros(1), s.cost)[1])
 end
 
-# the functional entry points' solvers, one per (nx, nu, T) on device 0
+# The functional entry points' workspaces, one per (nx, nu, T) on device 0: Solvers for the
+# LQ / 2-link families, TilesSolvers for arbitrary closures. The reference's fit is a pure
+# function, so two tasks calling fit with one shape must not share buffers: with_cached
+# holds the workspace's lock for the whole call (the second task waits for it), and the
+# dictionaries change only under CACHE_LOCK. At most MAX_CACHED shapes per family stay
+# resident; a new shape evicts an idle one (its device memory freed at once).
 const SOLVER_CACHE = Dict{NTuple{3,Int},Solver}()
-function cached_solver(nx, nu, M)
-    s = get(SOLVER_CACHE, (nx, nu, M), nothing)
-    (s === nothing || s.h.ptr == C_NULL) && (s = SOLVER_CACHE[(nx, nu, M)] = Solver(nx, nu, M, 1))
-    return s
+const TILES_CACHE = Dict{NTuple{3,Int},TilesSolver}()
+const CACHE_LOCK = ReentrantLock()
+const MAX_CACHED = 8
+
+function evict_idle!(cache::Dict)
+    for (k, c) in cache
+        if trylock(c.lock)
+            try
+                close(c.h)
+            finally
+                unlock(c.lock)
+            end
+            delete!(cache, k)
+            return true
+        end
+    end
+    return false
 end
-"""clear_cache!(): close the solvers fit / backward_pass / forward_pass keep per shape."""
+
+"""with_cached(f, cache, make, key): f(s) on the cached workspace `key` (built by make()
+on first use), holding s.lock for the call."""
+function with_cached(f, cache::Dict, make, key)
+    while true
+        s = lock(CACHE_LOCK) do
+            c = get(cache, key, nothing)
+            if c === nothing || c.h.ptr == C_NULL
+                length(cache) >= MAX_CACHED && evict_idle!(cache)
+                c = cache[key] = make()
+            end
+            c
+        end
+        lock(s.lock)
+        try
+            s.h.ptr == C_NULL && continue      # evicted between the two locks: take a fresh one
+            return f(s)
+        finally
+            unlock(s.lock)
+        end
+    end
+end
+
+"""clear_cache!(): close the workspaces fit / backward_pass / forward_pass keep per shape."""
 function clear_cache!()
-    foreach(close, values(SOLVER_CACHE)); empty!(SOLVER_CACHE)
+    lock(CACHE_LOCK) do
+        foreach(close, values(SOLVER_CACHE)); empty!(SOLVER_CACHE)
+        foreach(close, values(TILES_CACHE)); empty!(TILES_CACHE)
+    end
     return nothing
 end
 

@@ -195,7 +195,9 @@ ilqr_status ilqr_backward(ilqr_handle* h, const ilqr_problem* p, const ilqr_opti
 /* iLQR.backward_pass for arbitrary closures: the Riccati recursion of
  * backward_pass.jl:335-357 (optimal_controller_param, feedback_parameters,
  * step_back) on caller-supplied derivative tiles (ilqr_tiles); same outputs and
- * status behaviour as ilqr_backward. Shapes: ilqr_supported(ILQR_PROBLEM_TILES, nx, nu). */
+ * status behaviour as ilqr_backward. Shapes: ilqr_supported(ILQR_PROBLEM_TILES, nx, nu):
+ * every nx ≤ 16, nu ≤ 8 (the reference's RBD caller, animate_RBD_2_link.jl:31, is 16 × 8
+ * at T = 1000), any T. */
 ilqr_status ilqr_backward_tiles(ilqr_handle* h, const ilqr_tiles* tiles, const ilqr_options* o,
                                 double* d, double* K, int32_t* status);
 

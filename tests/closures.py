@@ -80,3 +80,216 @@ def two_link_torch():
         return ((q1 - x[0]) ** 2 + (q2 - x[1]) ** 2) * 1.0
 
     return dynamicsf, immediate_cost, final_cost
+
+
+# -- the reference's RBD example, floating base -------------------------------------
+def jet_ns():
+    """numpy arrays and oracle.jet Jets (array-valued forward-mode AD)."""
+    from oracle import jet
+    return types.SimpleNamespace(sin=jet.sin, cos=jet.cos, cat=jet.cat, solve=jet.solve, tr=jet.tr,
+                                 const=lambda a: np.asarray(a, dtype=np.float64))
+
+
+def torch_arr_ns(device="cuda"):
+    import torch
+    return types.SimpleNamespace(
+        sin=torch.sin, cos=torch.cos, cat=lambda parts, axis=-1: torch.cat(parts, dim=axis),
+        solve=lambda M, b: torch.linalg.solve(M, b.unsqueeze(-1)).squeeze(-1),
+        tr=lambda a: a.transpose(-1, -2),
+        const=lambda a: torch.as_tensor(np.asarray(a, dtype=np.float64), device=device))
+
+
+def _skew(a):
+    return np.array([[0.0, -a[2], a[1]], [a[2], 0.0, -a[0]], [-a[1], a[0], 0.0]])
+
+
+def _skew_basis():
+    """E (9, 3) with (E @ a).reshape(3, 3) = [a×]."""
+    return np.stack([_skew(e).ravel() for e in np.eye(3)], axis=1)
+
+
+def _crm_basis():
+    """E (36, 6) with (E @ v).reshape(6, 6) = crm(v) = [[ω×, 0], [v×, ω×]] (Featherstone)."""
+    cols = []
+    for e in np.eye(6):
+        m = np.zeros((6, 6))
+        m[:3, :3] = m[3:, 3:] = _skew(e[:3])
+        m[3:, :3] = _skew(e[3:])
+        cols.append(m.ravel())
+    return np.stack(cols, axis=1)
+
+
+def rbd_floating_arm(ns, dt=0.01):
+    """test/RBD_2_link_example/RBD_helper_functions.jl:48-116 written with array ops —
+    the closures a user of the generic path would write for animate_RBD_2_link.jl:
+    nx = 16 ([MRP p (3); base position r (3); θ (2); ω (3); v (3); θ̇ (2)]), nu = 8
+    (base torque (3), base force (3), joint torques (2)).
+
+    The mechanism is test/urdf/2Dof_arm.urdf parsed floating with zero gravity (:6-8):
+    a 30 kg base (I = 50·1), link_1 at (.5, .5, 0) about z, link_2 at (1, 0, 0) of
+    link_1 about y, 3 kg and I = .5·1 each, COMs on the joint origins. RigidBodyDynamics.jl
+    (absent) is restated with Featherstone's algorithms in body coordinates: the mass
+    matrix by the composite-rigid-body algorithm, dynamics_bias by recursive
+    Newton-Euler at zero acceleration; the base twist (ω, v) is body-frame, angular
+    first (RBD.jl's QuaternionFloating). The reference's kinematics (:64) are kept as
+    written: q̇ = [pdot_from_w(p, ω); v; θ̇] (Attitude.jl's MRP rate; the base position
+    integrates v as is). Parity vs RigidBodyDynamics.jl: unpinned (not runnable here).
+    Works on 1-D tensors (torch.func) and on (P, n) numpy arrays / oracle.jet Jets."""
+    I0 = np.diag([50.0, 50.0, 50.0, 30.0, 30.0, 30.0])
+    I1 = I2 = np.diag([0.5, 0.5, 0.5, 3.0, 3.0, 3.0])
+
+    def joint(r, a):
+        r, a = np.asarray(r, float), np.asarray(a, float)
+        Xt = np.eye(6)
+        Xt[3:, :3] = -_skew(r)
+        aa = np.outer(a, a)
+        bd = lambda m: np.block([[m, np.zeros((3, 3))], [np.zeros((3, 3)), m]])  # noqa: E731
+        S = np.concatenate([a, np.zeros(3)])
+        # X(θ) = blockdiag(E, E)·Xt, E = Rot(a, θ)ᵀ = cos θ (1 − aaᵀ) − sin θ [a×] + aaᵀ
+        return bd(np.eye(3) - aa) @ Xt, bd(-_skew(a)) @ Xt, bd(aa) @ Xt, S
+
+    C1a, C1b, C1c, S1n = joint((0.5, 0.5, 0.0), (0.0, 0.0, 1.0))
+    C2a, C2b, C2c, S2n = joint((1.0, 0.0, 0.0), (0.0, 1.0, 0.0))
+    m22 = float(S2n @ I2 @ S2n)
+    K = ns.const
+    I0c, I1c, I2c = K(I0), K(I1), K(I2)
+    C1a, C1b, C1c, C2a, C2b, C2c = (K(a) for a in (C1a, C1b, C1c, C2a, C2b, C2c))
+    S1, S2 = K(S1n), K(S2n)
+    F2 = K(I2 @ S2n)
+    ECRM, ESKEW = K(_crm_basis()), K(_skew_basis())
+    target = K([0.0, 0.0, 0.0, 5.0, 1.0, 2.0, 1.0, 0.3])             # animate_RBD_2_link.jl:10
+    Qw = K([100.0, 100.0, 100.0, 1.0, 1.0, 1.0, 10.0, 10.0])           # :89-91
+    Rw = K([1.0, 1.0, 1.0, 100.0, 100.0, 100.0, 10.0, 10.0])           # :96-97
+    Qfw = K([100.0, 100.0, 100.0, 1000.0, 1000.0, 1000.0, 10.0, 10.0])  # :111-112
+
+    def mv(M, v):
+        return (M @ v[..., None])[..., 0]
+
+    def crm(v):
+        w = mv(ECRM, v)
+        return w.reshape(tuple(w.shape[:-1]) + (6, 6))
+
+    def cross(a, b):
+        w = mv(ESKEW, a)
+        return mv(w.reshape(tuple(w.shape[:-1]) + (3, 3)), b)
+
+    def xform(c, s, Ca, Cb, Cc):
+        return c[..., None, None] * Ca + s[..., None, None] * Cb + Cc
+
+    def kinematics(x):
+        th = x[..., 6:8]
+        X1 = xform(ns.cos(th[..., 0]), ns.sin(th[..., 0]), C1a, C1b, C1c)
+        X2 = xform(ns.cos(th[..., 1]), ns.sin(th[..., 1]), C2a, C2b, C2c)
+        return X1, X2, ns.tr(X1), ns.tr(X2)
+
+    def mass_matrix(x, kin=None):                                      # :60, CRBA
+        X1, X2, X1T, X2T = kin if kin is not None else kinematics(x)
+        Ic1 = I1c + X2T @ I2c @ X2
+        Ic0 = I0c + X1T @ Ic1 @ X1
+        F1 = mv(Ic1, S1)
+        F21 = mv(X2T, F2)
+        m11 = (F1 * S1).sum(-1)[..., None, None]
+        m12 = (F21 * S1).sum(-1)[..., None, None]
+        M01, M02 = mv(X1T, F1), mv(X1T, F21)
+        top = ns.cat([Ic0, M01[..., :, None], M02[..., :, None]])
+        r6 = ns.cat([M01[..., None, :], m11, m12])
+        r7 = ns.cat([M02[..., None, :], m12, m12 * 0.0 + m22])
+        return ns.cat([top, r6, r7], axis=-2)
+
+    def dynamics_bias(x, kin=None):                                    # :64, RNEA at q̈ = 0
+        X1, X2, X1T, X2T = kin if kin is not None else kinematics(x)
+        w, vl, thd = x[..., 8:11], x[..., 11:14], x[..., 14:16]
+        v0 = ns.cat([w, vl])
+        v1 = mv(X1, v0) + S1 * thd[..., 0:1]
+        v2 = mv(X2, v1) + S2 * thd[..., 1:2]
+        a1 = mv(crm(v1), S1) * thd[..., 0:1]
+        a2 = mv(X2, a1) + mv(crm(v2), S2) * thd[..., 1:2]
+        f2 = mv(I2c, a2) - mv(ns.tr(crm(v2)), mv(I2c, v2))
+        f1 = mv(I1c, a1) - mv(ns.tr(crm(v1)), mv(I1c, v1)) + mv(X2T, f2)
+        f0 = -mv(ns.tr(crm(v0)), mv(I0c, v0)) + mv(X1T, f1)
+        return ns.cat([f0, (f1 * S1).sum(-1)[..., None], (f2 * S2).sum(-1)[..., None]])
+
+    def continuous_dynamics(x, u):                                     # :52-68
+        p, w, vl, thd = x[..., 0:3], x[..., 8:11], x[..., 11:14], x[..., 14:16]
+        kin = kinematics(x)
+        M = mass_matrix(x, kin)
+        vdot = ns.solve(M, u - dynamics_bias(x, kin))                  # :64
+        pp = (p * p).sum(-1)[..., None]
+        pw = (p * w).sum(-1)[..., None]
+        pdot = 0.25 * ((1.0 - pp) * w + 2.0 * cross(p, w) + 2.0 * pw * p)   # pdot_from_w
+        return ns.cat([pdot, vl, thd, vdot])                           # :65-67
+
+    def dynamicsf(x, u):                                               # RK4, :70-78
+        k1 = dt * continuous_dynamics(x, u)
+        k2 = dt * continuous_dynamics(x + k1 / 2, u)
+        k3 = dt * continuous_dynamics(x + k2 / 2, u)
+        k4 = dt * continuous_dynamics(x + k3, u)
+        return x + (1 / 6) * (k1 + 2 * k2 + 2 * k3 + k4)
+
+    def immediate_cost(x, u):                                          # :85-101
+        dx = target - x[..., 0:8]
+        return (dx * Qw * dx).sum(-1) * 10.0 + (u * Rw * u).sum(-1) * 1.0
+
+    def final_cost(x):                                                 # :107-116
+        dx = target - x[..., 0:8]
+        return (dx * Qfw * dx).sum(-1) * 100000.0
+
+    dynamicsf.mass_matrix, dynamicsf.dynamics_bias = mass_matrix, dynamics_bias
+    return dynamicsf, immediate_cost, final_cost
+
+
+def rbd_initial_state():
+    """RBD_to_iLQR_state of set_configuration!(state, [0,0,0,1, .5,.75,1, 0,0]) at rest
+    (RBD_helper_functions.jl:9, :26-29; animate_RBD_2_link.jl:22): quaternion (0, 0, 0, 1)
+    → MRP p = q_v / (1 + q_s) = (0, 0, 1)."""
+    return np.array([0.0, 0.0, 1.0, 0.5, 0.75, 1.0, 0.0, 0.0] + [0.0] * 8)
+
+
+def rbd_cost_quads():
+    """Exact quadratizations of rbd_floating_arm's costs (RBD_helper_functions.jl:85-116
+    are weighted sums of squares): what ForwardDiff's gradient / hessian return, batched
+    over points — lx, lu, lxx, lux (= 0), luu and lfx, lfxx."""
+    tgt = np.array([0.0, 0.0, 0.0, 5.0, 1.0, 2.0, 1.0, 0.3])
+    Qw = np.array([100.0, 100.0, 100.0, 1.0, 1.0, 1.0, 10.0, 10.0])
+    Rw = np.array([1.0, 1.0, 1.0, 100.0, 100.0, 100.0, 10.0, 10.0])
+    Qfw = np.array([100.0, 100.0, 100.0, 1000.0, 1000.0, 1000.0, 10.0, 10.0])
+
+    def quad(x, u):
+        P = x.shape[0]
+        lx = np.zeros((P, 16))
+        lx[:, :8] = -20.0 * Qw * (tgt - x[:, :8])
+        lxx = np.zeros((P, 16, 16))
+        lxx[:, np.arange(8), np.arange(8)] = 20.0 * Qw
+        luu = np.broadcast_to(np.diag(2.0 * Rw), (P, 8, 8)).copy()
+        return lx, 2.0 * Rw * u, lxx, np.zeros((P, 8, 16)), luu
+
+    def fquad(xN):
+        P = xN.shape[0]
+        lfx = np.zeros((P, 16))
+        lfx[:, :8] = -200000.0 * Qfw * (tgt - xN[:, :8])
+        lfxx = np.zeros((P, 16, 16))
+        lfxx[:, np.arange(8), np.arange(8)] = 200000.0 * Qfw
+        return lfx, lfxx
+    return quad, fquad
+
+
+def coupled_pendula_arr(ns, dt=0.05):
+    """coupled_pendula's dynamics written on arrays (x[..., i]): the same arithmetic in the
+    same order, for batched numpy / oracle.jet evaluation."""
+    def dynamicsf(x, u):
+        th1, th2, w1, w2 = x[..., 0], x[..., 1], x[..., 2], x[..., 3]
+        cpl = ns.sin(th1 - th2)
+        a1 = -9.81 * ns.sin(th1) - 0.4 * cpl * w2 * w2 - 0.1 * w1 + u[..., 0]
+        a2 = -9.81 * ns.sin(th2) + 0.4 * cpl * w1 * w1 - 0.1 * w2 + u[..., 1] * ns.cos(th2)
+        return ns.cat([(th1 + dt * w1)[..., None], (th2 + dt * w2)[..., None],
+                       (w1 + dt * a1)[..., None], (w2 + dt * a2)[..., None]])
+
+    def immediate_cost(x, u):
+        return (0.5 * (x[..., 0] * x[..., 0] + x[..., 1] * x[..., 1]) + 0.1 * (x[..., 2] * x[..., 2] + x[..., 3] * x[..., 3])
+                + u[..., 0] * u[..., 0] + u[..., 1] * u[..., 1] + 0.2 * u[..., 0] * x[..., 2]
+                + 0.1 * ns.sin(x[..., 0]) * u[..., 1])
+
+    def final_cost(x):
+        return 5.0 * (x[..., 0] * x[..., 0] + x[..., 1] * x[..., 1]) + x[..., 2] * x[..., 2] + x[..., 3] * x[..., 3]
+
+    return dynamicsf, immediate_cost, final_cost

@@ -53,7 +53,10 @@ def test_supported_shapes():
     assert lib.ilqr_supported(_lib.PROBLEM_TWO_LINK, 12, 4) == 0
     assert lib.ilqr_supported(_lib.PROBLEM_LQ, 4, 2) == 1
     assert lib.ilqr_supported(_lib.PROBLEM_TILES, 7, 3) == 1
-    assert lib.ilqr_supported(_lib.PROBLEM_TILES, 13, 1) == 0
+    assert lib.ilqr_supported(_lib.PROBLEM_TILES, 13, 1) == 1   # the wide tiles kernel
+    assert lib.ilqr_supported(_lib.PROBLEM_TILES, 16, 8) == 1   # animate_RBD_2_link.jl's shape
+    assert lib.ilqr_supported(_lib.PROBLEM_TILES, 17, 1) == 0
+    assert lib.ilqr_supported(_lib.PROBLEM_TILES, 16, 9) == 0
 
 
 def test_header_problem_kinds_match_binding():
@@ -112,8 +115,9 @@ def test_julia_shim_ccalls_declared_symbols():
 def test_julia_shim_exposes_reference_api():
     """The shim defines the reference's public functions (docs/src/documentation.md:13-51)
     and the resident Solver's methods; the per-call paths no longer create handles
-    (they run on cached_solver): only Solver(), the tiles/linearize helpers and
-    solve!(prob) construct a Handle."""
+    (they run on a cached workspace through with_cached, the closures' tiles path
+    included): only Solver(), TilesSolver(), the linearize helper and solve!(prob)
+    construct a Handle."""
     src = open(os.path.join(ROOT, "ilqr.jl_amd", "julia", "iLQRHIP.jl")).read()
     for fn in ("fit", "backward_pass", "forward_pass", "linearize_dynamics", "immediate_cost_quadratization",
                "final_cost_quadratization", "optimal_controller_param", "feedback_parameters", "step_back",
@@ -122,4 +126,9 @@ def test_julia_shim_exposes_reference_api():
     assert re.search(r"^Base\.close\(s::Solver\)", src, re.M)
     body = lambda name: src[src.index(f"function {name}("):src.index("\nend", src.index(f"function {name}("))]
     for name in ("fit", "backward_pass", "forward_pass"):
-        assert "Handle(" not in body(name) and "cached_solver(" in body(name), name
+        assert "Handle(" not in body(name) and "with_cached(SOLVER_CACHE" in body(name), name
+    assert re.search(r"^Base\.close\(s::TilesSolver\)", src, re.M)
+    assert "Handle(" not in body("backward_tiles_device")
+    assert "with_cached(TILES_CACHE" in body("backward_tiles_device")
+    # every cached workspace carries the lock with_cached holds for a call
+    assert src.count("ReentrantLock()") >= 3

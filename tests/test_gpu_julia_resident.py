@@ -170,3 +170,123 @@ def test_resident_solver_100_fits_allocate_nothing(gpu):
     assert lib.n["ilqr_free"] == lib.n["ilqr_malloc"] == 19 and lib.n["ilqr_destroy"] == 1
     s.close()                                                        # idempotent
     assert lib.n["ilqr_destroy"] == 1
+
+
+# -- the arbitrary-closure path: iLQRHIP.fit → fit_tiles → backward_tiles_device ---------
+class ShimTilesSolver:
+    """iLQRHIP.TilesSolver: one handle and the 12 resident buffers in the constructor's
+    order (A B lx lu lxx lux luu lfx lfxx, then δu K status)."""
+
+    def __init__(self, lib, nx, nu, T):
+        self.hd = h = ShimHandle(lib, nx, nu, T, 1)
+        self.nx, self.nu, self.M = nx, nu, T
+        f = lambda n: h.alloc(np.float64, n)  # noqa: E731
+        self.tl = [f(T * nx * nx), f(T * nx * nu), f(T * nx), f(T * nu), f(T * nx * nx),
+                   f(T * nu * nx), f(T * nu * nu), f(nx), f(nx * nx)]
+        self.d, self.K, self.status = f(T * nu), f(T * nu * nx), h.alloc(np.int32, 1)
+
+    def close(self):
+        self.hd.close()
+
+
+def julia_tiles(x, u, fj, quad, fquad):
+    """iLQRHIP.derivative_tiles' Julia arrays — A (nx, nx, M) with A[:, :, i] =
+    permutedims(jacobian), lx (nx, M), … — from the oracle's forward-mode Jacobians and
+    the exact cost quadratizations (ForwardDiff's values; Julia's own call per step)."""
+    from oracle import jet
+    M = u.shape[0]
+    A, B = jet.jacobians(fj, x[:M], u)
+    lx, lu, lxx, lux, luu = quad(x[:M], u)
+    lfx, lfxx = fquad(x[M:M + 1])
+    stepT = lambda a: J.jl(np.transpose(a, (2, 1, 0)))   # (M, r, c) → Julia (c, r, M)  # noqa: E731
+    return [stepT(A), stepT(B), J.jl(lx.T), J.jl(lu.T), stepT(lxx), stepT(lux), stepT(luu),
+            J.jl(lfx[0]), J.jl(lfxx[0].T)]
+
+
+def shim_backward_tiles(cache, lib, x, u, fj, quad, fquad):
+    """iLQRHIP.backward_tiles_device: the host tiles into the cached TilesSolver's buffers
+    (with_cached(TILES_CACHE, …)), ilqr_backward_tiles, download."""
+    M, nu = u.shape
+    nx = x.shape[1]
+    t = julia_tiles(x, u, fj, quad, fquad)
+    s = cache.get((nx, nu, M))
+    if s is None:
+        s = cache[(nx, nu, M)] = ShimTilesSolver(lib, nx, nu, M)
+    for p, a in zip(s.tl, t):
+        s.hd.upload_into(p, a)
+    tl = _lib.Tiles(*(p.value for p in s.tl))
+    o = _lib.default_options()
+    rc = lib.ilqr_backward_tiles(s.hd.h, C.byref(tl), C.byref(o), s.d, s.K, s.status)
+    _lib.check(rc, "ilqr_backward_tiles")
+    return (J.from_abi(s.hd.download((nu, M), s.d)), J.gains_from_abi(s.hd.download((nx, nu, M), s.K)))
+
+
+def shim_fit_tiles(cache, lib, x_init, u_init, fj, lj, lfj, quad, fquad, max_iter, tol, max_trials=64):
+    """iLQRHIP.fit_tiles with forward_host: the host rollout of the user's closure."""
+    xi, ui = np.array(x_init), np.array(u_init)
+    xt = np.zeros_like(xi)
+    prev = np.inf
+    iters = 0
+    for it in range(1, max_iter + 1):
+        iters = it
+        du, K = shim_backward_tiles(cache, lib, xi, ui, fj, quad, fquad)           # :162
+        N, M = xi.shape[0], ui.shape[0]
+        alpha, xb, ub, exhausted = 1.0, np.zeros_like(xi), np.zeros_like(ui), False
+        for trial in range(1, max_trials + 1):
+            xb[0] = xi[0]
+            for k in range(M):
+                ub[k] = ui[k] + alpha * du[k] + K[k] @ (xb[k] - xi[k])
+                xb[k + 1] = fj(xb[k][None], ub[k][None])[0]
+            c = sum(float(lj((xb[k] - xt[k])[None], ub[k][None])[0]) for k in range(M)) + float(lfj(xb[M][None])[0])
+            if prev - c > 0:
+                break
+            if trial == max_trials:
+                exhausted = True
+            alpha /= 2
+        if exhausted:
+            break
+        prev = c
+        if float(((ub - ui) ** 2).sum()) <= tol:                                   # :171
+            break
+        xi, ui = xb.copy(), ub.copy()
+    return xi, ui, iters
+
+
+def test_tiles_path_20_fits_allocate_nothing_rbd_shape(gpu):
+    """iLQRHIP.fit with the reference RBD example's closures (nx = 16, nu = 8, T = 1000):
+    the tiles workspace is created once (1 handle, 12 buffers) and reused by every
+    iteration of 20 MPC-style fits; results agree with the batched closure oracle."""
+    from closures import jet_ns, rbd_cost_quads, rbd_floating_arm, rbd_initial_state
+    from oracle import closure_fit as CF
+    fj, lj, lfj = rbd_floating_arm(jet_ns())
+    quad, fquad = rbd_cost_quads()
+    T = 1000
+    lib = CountingLib()
+    cache = {}
+    rng = np.random.default_rng(11)
+    u0 = np.zeros((T, 8))
+    counts = []
+    for call in range(20):
+        x0 = rbd_initial_state()
+        x0[8:] = 0.02 * rng.standard_normal(8)
+        x = np.zeros((T + 1, 16))
+        x[0] = x0
+        for t in range(T):
+            x[t + 1] = fj(x[t][None], u0[t][None])[0]
+        max_iter = 3 if call == 19 else 1
+        xo, uo, iters = shim_fit_tiles(cache, lib, x, u0, fj, lj, lfj, quad, fquad, max_iter, 1e-6)
+        counts.append(dict(lib.n))
+        if call in (0, 19):
+            r = CF.fit(x[None], u0[None], fj, lj, lfj, quad, fquad, max_iter=max_iter, tol=1e-6)
+            assert iters == int(r["iters"][0])
+            assert rel(xo, r["x"][0]) < 1e-8 and rel(uo, r["u"][0]) < 1e-8
+    assert counts[0] == {"ilqr_create": 1, "ilqr_destroy": 0, "ilqr_malloc": 12, "ilqr_free": 0}
+    assert all(c == counts[0] for c in counts)
+    for s in cache.values():
+        s.close()
+    assert lib.n["ilqr_free"] == 12 and lib.n["ilqr_destroy"] == 1
+
+
+def rel(a, b):
+    a, b = np.asarray(a, float), np.asarray(b, float)
+    return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-300))

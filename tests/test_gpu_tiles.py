@@ -65,10 +65,10 @@ def lq_tiles(lq, x, u):
 
 def test_tiles_supported_shapes(gpu):
     lib = _lib.load()
-    for nx in range(1, 13):
-        for nu in range(1, 5):
+    for nx in range(1, 17):
+        for nu in range(1, 9):
             assert lib.ilqr_supported(_lib.PROBLEM_TILES, nx, nu) == 1
-    for nx, nu in ((13, 1), (12, 5), (0, 1), (4, 0)):
+    for nx, nu in ((17, 1), (12, 9), (16, 9), (0, 1), (4, 0)):
         assert lib.ilqr_supported(_lib.PROBLEM_TILES, nx, nu) == 0
 
 
@@ -96,6 +96,40 @@ def test_tiles_every_shape_vs_oracle(gpu, n, m):
     assert (st.cpu().numpy() == 0).all()
     dr, Kr, _ = cref.tiles_backward(tl, symmetrize=True)
     assert rel(d, dr) < 1e-10 and rel(K, Kr) < 1e-10
+
+
+@pytest.mark.parametrize("n,m", [(13, 1), (16, 4), (4, 8), (1, 5), (12, 5), (15, 7), (16, 8)])
+def test_tiles_wide_shapes_vs_oracle(gpu, n, m):
+    """Shapes past one MFMA tile (nx ≤ 16, nu ≤ 8) run on the tiled wide kernel."""
+    nb, T = 6, 40
+    tl = random_tiles(nb, T, n, m, seed=1000 + 100 * n + m)
+    s = Solver(n, m, T, nb, kind=_lib.PROBLEM_TILES)
+    d, K, st = s.backward_tiles(to_dev(tl))
+    assert (st.cpu().numpy() == 0).all()
+    dr, Kr, _ = cref.tiles_backward(tl, symmetrize=True)
+    assert rel(d, dr) < 1e-10 and rel(K, Kr) < 1e-10
+    tl0 = dict(tl, lux=None)  # 𝐏 = NULL reads as zeros
+    d0, K0, _ = s.backward_tiles(to_dev(tl0))
+    dr0, Kr0, _ = cref.tiles_backward(tl0, symmetrize=True)
+    assert rel(d0, dr0) < 1e-10 and rel(K0, Kr0) < 1e-10
+    s.close()
+
+
+def test_tiles_wide_rbd_shape_long_horizon(gpu):
+    """The reference RBD caller's shape: nx = 16, nu = 8, T = 1000
+    (test/RBD_2_link_example/animate_RBD_2_link.jl:8,19-20)."""
+    nb, T, n, m = 3, 1000, 16, 8
+    tl = random_tiles(nb, T, n, m, seed=16008)
+    s = Solver(n, m, T, nb, kind=_lib.PROBLEM_TILES)
+    d, K, st = s.backward_tiles(to_dev(tl))
+    assert (st.cpu().numpy() == 0).all()
+    dr, Kr, _ = cref.tiles_backward(tl, symmetrize=True)
+    assert rel(d, dr) < 1e-10 and rel(K, Kr) < 1e-10
+    # a NaN tile is reported per trajectory, as backward_pass.jl:353-354 asserts
+    tl["A"][1, 500, 3, 3] = np.nan
+    _, _, st = s.backward_tiles(to_dev(tl))
+    assert st.cpu().numpy().tolist() == [0, _lib.TRAJ_NAN, 0]
+    s.close()
 
 
 def test_tiles_pendula_vs_oracle(gpu):
@@ -171,3 +205,53 @@ def test_generic_closures_fit_vs_oracle(gpu):
         xo, uo = O.fit(x[b], u[b], fo, lo, lfo, max_iter=30, tol=1e-6, max_trials=64, history=h)
         assert int(info["iters"][b]) == len(h)
         assert rel(xf[b], xo) < 1e-9 and rel(uf[b], uo) < 1e-9
+
+
+def rbd_batch(nb, T):
+    """The reference RBD script's start (animate_RBD_2_link.jl:19-27: rest state, zero
+    inputs, x_init = rollout) plus perturbed copies."""
+    from closures import jet_ns, rbd_floating_arm, rbd_initial_state
+    fj, _, _ = rbd_floating_arm(jet_ns())
+    x = np.zeros((nb, T + 1, 16))
+    x[:, 0] = rbd_initial_state()
+    x[1:, 0, 8:] = 0.05 * np.random.default_rng(7).standard_normal((nb - 1, 8))
+    u = np.zeros((nb, T, 8))
+    for t in range(T):
+        x[:, t + 1] = fj(x[:, t], u[:, t])
+    return x, u
+
+
+def test_rbd_caller_backward_pass_t1000(gpu):
+    """iLQR.backward_pass with the RBD example's 16 × 8 closures at T = 1000: tiles by
+    torch.func on the device + the wide HIP recursion, against oracle.jet tiles + the C
+    recursion."""
+    from closures import jet_ns, rbd_cost_quads, rbd_floating_arm, torch_arr_ns
+    from oracle import closure_fit as CF
+    x, u = rbd_batch(2, 1000)
+    u = u + 0.1 * np.random.default_rng(8).standard_normal(u.shape)
+    d, K = api.backward_pass(torch.from_numpy(x).cuda(), torch.from_numpy(u).cuda(),
+                             *rbd_floating_arm(torch_arr_ns()))
+    q, fq = rbd_cost_quads()
+    tl = CF.derivative_tiles(x, u, rbd_floating_arm(jet_ns())[0], q, fq)
+    dr, Kr, st = cref.tiles_backward(tl, symmetrize=True)
+    assert (st == 0).all()
+    assert rel(d, dr) < 1e-10 and rel(K, Kr) < 1e-10
+
+
+def test_rbd_caller_fit_t1000(gpu):
+    """iLQR.fit on the reference's RBD caller shape (nx = 16, nu = 8, T = 1000) through
+    the generic closure path, against the batched closure oracle: iteration counts and
+    per-iteration trials exact, iterates and costs within 1e-8."""
+    from closures import jet_ns, rbd_cost_quads, rbd_floating_arm, torch_arr_ns
+    from oracle import closure_fit as CF
+    nb, T, iters = 2, 1000, 4
+    x, u = rbd_batch(nb, T)
+    xf, uf, info = api.fit(torch.from_numpy(x).cuda(), torch.from_numpy(u).cuda(),
+                           *rbd_floating_arm(torch_arr_ns()), max_iter=iters, tol=1e-6, return_info=True)
+    fj, lj, lfj = rbd_floating_arm(jet_ns())
+    r = CF.fit(x, u, fj, lj, lfj, *rbd_cost_quads(), max_iter=iters, tol=1e-6)
+    assert info["iters"].tolist() == r["iters"].tolist()
+    assert info["status"].tolist() == r["status"].tolist()
+    assert info["history"]["trials"][:iters].tolist() == r["history"]["trials"].tolist()
+    assert rel(info["cost"], r["cost"]) < 1e-8
+    assert rel(xf, r["x"]) < 1e-8 and rel(uf, r["u"]) < 1e-8
