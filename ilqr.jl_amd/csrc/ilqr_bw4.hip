@@ -470,6 +470,19 @@ __global__ __launch_bounds__(64 * FUSED_WAVES) void lq_iter_fused4_kernel(LQPara
         if (b0 + q < B && a.status[b0 + q] == ILQR_TRAJ_OK) active |= 1u << q;
     }
   }
+#if ILQR_FUSED_DEPHASE_PROBE
+  // TIMING-ONLY probe (tools/dephase_probe.sh, not the product): half of the waves
+  // (PROBE 1: odd waves of every workgroup; 2: odd workgroups) run the forward FIRST on
+  // the gains already in K/d, then the backward — the phase mix of a de-phased schedule
+  // (forward(i−1) then backward(i) beside backward(i) then forward(i)) at one wave/SIMD.
+  if (active != 0 && ((ILQR_FUSED_DEPHASE_PROBE == 1 ? w : (int)blockIdx.x) & 1)) {
+    iter_forward_wave_active<12, 4>(P, b0, B, T, ai, ls, lds, ((active >> (l >> 4)) & 1u) != 0);
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    (void)lq_backward4_wave(P, b0, B, active, T, a.x, a.u, a.d, a.K, ls.mu, lds);
+    return;
+  }
+#endif
   if (active != 0) {
     const unsigned nan = lq_backward4_wave(P, b0, B, active, T, a.x, a.u, a.d, a.K, ls.mu, lds) & active;
     if (owner && ((nan >> q) & 1u)) {
