@@ -3,11 +3,13 @@
 // fit driver (src/forward_pass.jl:148-179) on top of the fused iteration kernel.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <ctime>
 #include <string>
 #include <vector>
 
@@ -39,6 +41,8 @@ struct ilqr_handle {
   int32_t* dev_running = nullptr;  // device alias of host_running
   int32_t* dev_flags = nullptr;    // gather_kernel's device call-status word
   hipEvent_t ev_poll[2] = {nullptr, nullptr};
+  ilqr::HostWait host_wait;        // the end-of-fit wait (wait_host_seq)
+  ilqr::HostWait poll_wait;        // the per-iteration convergence polls (wait_event)
   // LQ problems of another shape (nx ≤ 12, nu ≤ 4) run zero-padded on an inner
   // (12, 4) handle (created on the first such call): zero rows/columns of A, B, Q, R,
   // Qf, x, u decouple exactly, so the real entries are the (12, 4) kernels' bits.
@@ -313,7 +317,9 @@ ilqr_status unpad_u(ilqr_handle* h, const double* pu, double* u) {
 
 // The end of a fit: the stream's last kernel stores this fit's number into a wait word
 // (ilqr::wait_host_seq below).
-hipError_t wait_fit(ilqr_handle* h, uint32_t seq, hipStream_t s) { return ilqr::wait_host_seq(h->host_running + 2, seq, s); }
+hipError_t wait_fit(ilqr_handle* h, uint32_t seq, hipStream_t s) {
+  return ilqr::wait_host_seq(h->host_running + 2, seq, s, &h->host_wait);
+}
 
 }  // namespace
 
@@ -322,26 +328,65 @@ hipError_t wait_fit(ilqr_handle* h, uint32_t seq, hipStream_t s) { return ilqr::
 // completed (in-order stream): when the word carries the number, the outputs are written.
 // The host spins on that word and returns — the runtime's blocking stream sync costs
 // ≈8 µs more per fit after the work is done (A/B in bench.py, 455 → 447 µs per 3-iteration
-// headline fit, profiles/r04/fit_wait_ab_r04.log). A fit longer than FIT_SPIN_US falls
-// back to the stream sync; ILQR_FIT_WAIT=sync in the environment forces the sync (A/B).
-hipError_t ilqr::wait_host_seq(const volatile int32_t* w, uint32_t seq, hipStream_t s) {
+// headline fit, profiles/r04/fit_wait_ab_r04.log). The handle remembers how long its
+// previous wait took (est): a wait expected to be long naps (50 µs sleeps) until 150 µs
+// before that, then spins to 1.25 × est (50 µs at least, est + 1 ms at most), then naps
+// between stream queries until the stream is idle. A headline-size fit so spins ≈150 µs
+// of its ≈450; a long one (a config-5 default fit, 9-39 ms; every shard thread of
+// ilqr_multi) holds no core. The fit drivers' per-iteration convergence polls wait the
+// same way on their events (wait_event; the next iteration is already queued, so a nap's
+// wake-up delay idles nothing). hipEventSynchronize busy-waits on this ROCm whatever the
+// event's flags (tools/event_wait_probe.py, profiles/r05/event_wait_probe_r05.log), so
+// no runtime sync is left on these paths. ILQR_FIT_WAIT=sync in the environment forces
+// the stream sync (A/B).
+namespace {
+template <class Done, class Idle>
+hipError_t nap_spin_wait(ilqr::HostWait* hw, Done done, Idle idle) {
+  using clk = std::chrono::steady_clock;
+  const auto t0 = clk::now();
+  const int64_t est = hw->last_us;
+  auto since = [&] { return std::chrono::duration_cast<std::chrono::microseconds>(clk::now() - t0).count(); };
+  const struct timespec nap = {0, 50000};
+  if (est > 300)
+    while (!done() && since() < est - 150) nanosleep(&nap, nullptr);
+  const int64_t budget = est > 0 ? std::min<int64_t>(std::max<int64_t>(est + est / 4, 50), est + 1000) : 1000;
+  hipError_t e = hipSuccess;
+  for (uint32_t k = 0;; ++k) {
+    if (done()) break;
+    if ((k & 255u) == 255u && since() > budget) {
+      while (!done()) {  // past the estimate: nap between queries until the work is done
+        if ((e = idle()) != hipErrorNotReady) break;
+        nanosleep(&nap, nullptr);
+      }
+      if (e == hipErrorNotReady) e = hipSuccess;
+      break;
+    }
+    __builtin_ia32_pause();
+  }
+  hw->last_us = since();
+  return e;
+}
+}  // namespace
+
+hipError_t ilqr::wait_host_seq(const volatile int32_t* w, uint32_t seq, hipStream_t s, HostWait* hw) {
   static const bool spin = [] {
     const char* e = getenv("ILQR_FIT_WAIT");
     return !(e && strcmp(e, "sync") == 0);
   }();
-  if (spin) {
-    constexpr int64_t FIT_SPIN_US = 20000;
-    const auto t0 = std::chrono::steady_clock::now();
-    for (uint32_t k = 0;; ++k) {
-      if (((uint32_t)__atomic_load_n(w, __ATOMIC_ACQUIRE) >> 2) == seq) return hipSuccess;
-      if ((k & 255u) == 255u &&
-          std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0).count() >
-              FIT_SPIN_US)
-        break;
-      __builtin_ia32_pause();
-    }
-  }
-  return hipStreamSynchronize(s);
+  if (!spin) return hipStreamSynchronize(s);
+  auto done = [&] { return ((uint32_t)__atomic_load_n(w, __ATOMIC_ACQUIRE) >> 2) == seq; };
+  hipError_t e = nap_spin_wait(hw, done, [&] {
+    const hipError_t q = hipStreamQuery(s);  // idle, busy (NotReady) or an execution error
+    return q == hipSuccess && !done() ? hipErrorLaunchFailure : q;  // idle without the word: lost
+  });
+  return e != hipSuccess ? e : hipPeekAtLastError();  // a launch error of this thread
+}
+
+hipError_t ilqr::wait_event(hipEvent_t ev, HostWait* hw) {
+  hipError_t q = hipErrorNotReady;
+  auto done = [&] { return (q = hipEventQuery(ev)) != hipErrorNotReady; };
+  const hipError_t e = nap_spin_wait(hw, done, [&] { return q = hipEventQuery(ev); });
+  return e != hipSuccess ? e : q;
 }
 
 extern "C" {
@@ -809,7 +854,7 @@ ilqr_status ilqr_fit_ex(ilqr_handle* h, const ilqr_problem* p, const ilqr_option
     HIP_TRY(ilqr::launch_count_running(h->batch, h->status, h->dev_running + (it & 1), ps));
     HIP_TRY(hipEventRecord(h->ev_poll[it & 1], ps));
     if (it >= 2) {
-      HIP_TRY(hipEventSynchronize(h->ev_poll[(it - 1) & 1]));
+      HIP_TRY(ilqr::wait_event(h->ev_poll[(it - 1) & 1], &h->poll_wait));
       if (__atomic_load_n(h->host_running + ((it - 1) & 1), __ATOMIC_ACQUIRE) == 0) break;
     }
   }

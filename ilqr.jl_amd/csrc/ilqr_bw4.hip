@@ -475,7 +475,18 @@ __global__ __launch_bounds__(64 * FUSED_WAVES) void lq_iter_fused4_kernel(LQPara
   // (PROBE 1: odd waves of every workgroup; 2: odd workgroups) run the forward FIRST on
   // the gains already in K/d, then the backward — the phase mix of a de-phased schedule
   // (forward(i−1) then backward(i) beside backward(i) then forward(i)) at one wave/SIMD.
-  if (active != 0 && ((ILQR_FUSED_DEPHASE_PROBE == 1 ? w : (int)blockIdx.x) & 1)) {
+  // PROBE 3 is that schedule's first launch (odd waves: backward only), PROBE 4 its
+  // drain launch (odd waves: forward only, even waves nothing).
+  if (ILQR_FUSED_DEPHASE_PROBE == 3 && active != 0 && (w & 1)) {
+    (void)lq_backward4_wave(P, b0, B, active, T, a.x, a.u, a.d, a.K, ls.mu, lds);
+    return;
+  }
+  if (ILQR_FUSED_DEPHASE_PROBE == 4) {
+    if (active != 0 && (w & 1))
+      iter_forward_wave_active<12, 4>(P, b0, B, T, ai, ls, lds, ((active >> (l >> 4)) & 1u) != 0);
+    return;
+  }
+  if (active != 0 && ((ILQR_FUSED_DEPHASE_PROBE != 2 ? w : (int)blockIdx.x) & 1)) {
     iter_forward_wave_active<12, 4>(P, b0, B, T, ai, ls, lds, ((active >> (l >> 4)) & 1u) != 0);
     __builtin_amdgcn_s_waitcnt(0);
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");

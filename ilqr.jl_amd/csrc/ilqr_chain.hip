@@ -1929,6 +1929,8 @@ struct ilqr_chain_handle {
   // call status tagged with the fit's number), their device alias, the gather's device
   // call-status word, the poll's events
   int32_t* host_words = nullptr;
+  ilqr::HostWait host_wait;  // the end-of-fit wait (wait_host_seq)
+  ilqr::HostWait poll_wait;  // the per-iteration convergence polls (wait_event)
   int32_t* dev_words = nullptr;
   int32_t* dev_flags = nullptr;
   hipEvent_t ev_poll[2] = {nullptr, nullptr};
@@ -2405,7 +2407,7 @@ ilqr_status chain_fit_t(ilqr_chain_handle* h, const ilqr_options* o, const void*
     CH_TRY(ilqr::launch_count_running(h->batch, h->status, h->dev_words + (it & 1), s));
     CH_TRY(hipEventRecord(h->ev_poll[it & 1], s));
     if (it >= 2) {  // iteration it−1's count, read while iteration it runs (:171's break)
-      CH_TRY(hipEventSynchronize(h->ev_poll[(it - 1) & 1]));
+      CH_TRY(ilqr::wait_event(h->ev_poll[(it - 1) & 1], &h->poll_wait));
       if (__atomic_load_n(h->host_words + ((it - 1) & 1), __ATOMIC_ACQUIRE) == 0) break;
     }
   }
@@ -2420,7 +2422,7 @@ ilqr_status chain_fit_t(ilqr_chain_handle* h, const ilqr_options* o, const void*
   uint32_t seq = (++h->fit_seq) & 0x3fffffffu;
   if (seq == 0) seq = h->fit_seq = 1;  // 0 is the word's cleared value
   CH_TRY(ilqr::launch_publish_flags(h->dev_flags, h->dev_words + 2, seq, s));
-  CH_TRY(ilqr::wait_host_seq(h->host_words + 2, seq, s));
+  CH_TRY(ilqr::wait_host_seq(h->host_words + 2, seq, s, &h->host_wait));
   const int32_t f = __atomic_load_n(h->host_words + 2, __ATOMIC_ACQUIRE);
   return (f & 1) ? ILQR_ERR_NAN : ((f & 2) ? ILQR_ERR_LS_EXHAUSTED : ILQR_OK);
 }

@@ -170,9 +170,16 @@ hipError_t launch_count_running(int B, const int32_t* status, int32_t* out, hipS
 // The last launch of a fit (gather_flags_kernel): dflags[0] (a gather's call-status
 // bits, re-armed) into the host-mapped word `flags` as (seq << 2) | bits.
 hipError_t launch_publish_flags(int32_t* dflags, int32_t* flags, uint32_t seq, hipStream_t s);
-// The host's end of a fit: spin (≤ 20 ms, then the stream sync) until the host-mapped
-// word carries `seq` in bits 2..31 (ilqr_abi.cpp; ILQR_FIT_WAIT=sync forces the sync).
-hipError_t wait_host_seq(const volatile int32_t* word, uint32_t seq, hipStream_t s);
+// The host's end of a fit: wait until the host-mapped word carries `seq` in bits 2..31 —
+// nap through the bulk of a wait the handle's previous one says is long, spin around its
+// expected end, then nap between stream queries (ilqr_abi.cpp; ILQR_FIT_WAIT=sync forces
+// the stream sync). wait_event: the same for an event (the fit drivers' polls). One
+// HostWait per waiting site of a handle.
+struct HostWait {
+  int64_t last_us = 0;  // the previous wait's length
+};
+hipError_t wait_host_seq(const volatile int32_t* word, uint32_t seq, hipStream_t s, HostWait* hw);
+hipError_t wait_event(hipEvent_t ev, HostWait* hw);
 bool lq_supported(int nx, int nu);
 
 // Caller-supplied derivative tiles (ilqr_tiles in include/ilqr.h), device pointers.
