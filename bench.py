@@ -206,6 +206,40 @@ def _free_port():
         return so.getsockname()[1]
 
 
+# Every per-rank time behind an aggregate field of the JSON line. The job ends with its
+# slowest rank, so each is reduced with MAX over ranks before any field is formed; the
+# per-trajectory mean iteration count of the default-options fit is averaged over ranks.
+RANK_TIMES = ("ms_step", "fit5_ms", "dflt_ms", "single_ms", "bw_ms", "fw_ms", "fused_ms")
+
+
+def reduce_over_ranks(times, dflt_iters, world, device):
+    """→ (dict of max-over-ranks times, mean-over-ranks default-fit iterations)."""
+    if world == 1:
+        return dict(times), dflt_iters
+    import torch.distributed as tdist
+    t = torch.tensor([times[k] for k in RANK_TIMES], dtype=torch.float64, device=device)
+    tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+    it = torch.tensor([dflt_iters], dtype=torch.float64, device=device)
+    tdist.all_reduce(it, op=tdist.ReduceOp.SUM)
+    return dict(zip(RANK_TIMES, t.tolist())), float(it.item()) / world
+
+
+def aggregate_fields(tm, dflt_iters, world):
+    """The whole-job rates of the JSON line from max-over-ranks times (ms)."""
+    return {"value": world * 1000.0 / tm["ms_step"],
+            "co_headline": world * 5000.0 / tm["fit5_ms"],
+            "fit_default_batched_it_per_s": world * 1000.0 * dflt_iters / tm["dflt_ms"],
+            "single_iteration_batched_it_per_s": world * 1000.0 / tm["single_ms"],
+            "fit5_batched_it_per_s": world * 5000.0 / tm["fit5_ms"]}
+
+
+def fake_rank_times(rank):
+    """--dist-selftest's stand-in per-rank times (ms): rank r is (1 + r/4)× rank 0, so the
+    max over ranks is the last rank's (tests/test_dist.py checks every aggregate field)."""
+    f = 1.0 + rank / 4.0
+    return {k: f * v for k, v in zip(RANK_TIMES, (0.154, 3.4, 2.0, 0.15, 0.097, 0.05, 0.146))}, 4.0 + rank
+
+
 def spawn_ranks(n):
     """`--gpus N` (N > 1) without a launcher (WORLD_SIZE unset): start N rank processes of
     this script, one per GPU, the way torch.distributed.run would (RANK / LOCAL_RANK /
@@ -258,10 +292,15 @@ def dist_selftest(args, world, rank):
     st = torch.zeros((B,), dtype=torch.int32)
     gc, gs = gather_fit_results(torch.from_numpy(cost), st) if world > 1 else (torch.from_numpy(cost), st)
     ok = bool(np.allclose(gc[rank * B:(rank + 1) * B].numpy(), cost))
+    # the aggregate fields from stand-in per-rank times, reduced exactly as main() does
+    times, iters = fake_rank_times(rank)
+    tm, it_mean = reduce_over_ranks(times, iters, world, "cpu")
     if rank == 0:
         print(json.dumps({"metric": "dist-selftest (plumbing only, no solve)", "value": None, "n_gpus": world,
                           "allgather_check": {"trajectories": int(gc.numel()), "own_block_matches": ok,
-                                              "finite_costs": int(torch.isfinite(gc).sum().item())}}),
+                                              "finite_costs": int(torch.isfinite(gc).sum().item())},
+                          "rank_times_max": tm, "dflt_iters_mean": it_mean,
+                          "aggregates": aggregate_fields(tm, it_mean, world)}),
               flush=True)
     if world > 1:
         tdist.destroy_process_group()
@@ -384,11 +423,7 @@ def main():
     wall = time.perf_counter() - t0
     ms = e0.elapsed_time(e1) / args.steps
     ms_wall = wall * 1000.0 / args.steps
-    ms_step = max(ms, ms_wall)
-    if dist:  # max over ranks
-        tt = torch.tensor([ms_step], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
-        tdist.all_reduce(tt, op=tdist.ReduceOp.MAX)
-        ms_step = float(tt.item())
+    ms_step = max(ms, ms_wall)   # this rank's; reduced over ranks with the other times below
     full = [t * 1000.0 / n for t, n in fit_times if n == FIT_ITERS]
     fit_stats = None
     if full:
@@ -511,18 +546,35 @@ def main():
     fused_ok = bool((st == 0).all().item())
     fused_ms = f0.elapsed_time(f1) / (reps * FIT_ITERS)
 
-    # result exchange (fit output): all-gather the per-trajectory costs over RCCL
-    gather_ms = None
+    # every per-rank time behind an aggregate field, max over ranks (RANK_TIMES)
+    rank_times = {"ms_step": ms_step, "fit5_ms": fit5_ms, "dflt_ms": dflt_ms, "single_ms": single_ms,
+                  "bw_ms": bw_ms, "fw_ms": fw_ms, "fused_ms": fused_ms}
+    tm, dflt_iters_all = reduce_over_ranks(rank_times, dflt_iters, world,
+                                           dev if backend == "nccl" else "cpu")
+    agg = aggregate_fields(tm, dflt_iters_all, world)
+    ms_step, fit5_ms, dflt_ms, single_ms = tm["ms_step"], tm["fit5_ms"], tm["dflt_ms"], tm["single_ms"]
+    bw_ms, fw_ms, fused_ms = tm["bw_ms"], tm["fw_ms"], tm["fused_ms"]
+
+    # result exchange (fit output): all-gather the per-trajectory costs over RCCL, timed
+    # with HIP events on the launch stream (it waits for the collective's stream) and by
+    # the host clock, max over ranks
+    gather_ms = gather_ev_ms = None
     gathered = None
     if dist:
         from ilqr_amd.dist import gather_fit_results
         tdist.barrier()
         torch.cuda.synchronize()
+        g_e0, g_e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         g0 = time.perf_counter()
+        g_e0.record(stream)
         src_c, src_s = (fcost, fst) if backend == "nccl" else (fcost.cpu(), fst.cpu())
         gc, gs = gather_fit_results(src_c, src_s)
+        g_e1.record(stream)
         torch.cuda.synchronize()
-        gather_ms = (time.perf_counter() - g0) * 1000.0
+        gt = torch.tensor([(time.perf_counter() - g0) * 1000.0, g_e0.elapsed_time(g_e1)], dtype=torch.float64,
+                          device=dev if backend == "nccl" else "cpu")
+        tdist.all_reduce(gt, op=tdist.ReduceOp.MAX)
+        gather_ms, gather_ev_ms = gt.tolist()
         gathered = {"trajectories": int(gc.numel()), "finite_costs": int(torch.isfinite(gc).sum().item()),
                     "status_max_iter": int((gs == _lib.TRAJ_MAX_ITER).sum().item())}
 
@@ -551,7 +603,7 @@ def main():
 
     result = {
         "metric": "batched iLQR iterations/sec (fwd+bwd pass), nx=12 nu=4 T=100, 1/2/4/8 MI355X",
-        "value": world * 1000.0 / ms_step,
+        "value": agg["value"],
         "unit": "batched iterations/s (one batched iteration = 4096 trajectories per GPU, backward+forward "
                 f"with line search, inside a {FIT_ITERS}-iteration fit from cold)",
         "n_gpus": world,
@@ -611,15 +663,15 @@ def main():
                       "cost_strictly_decreasing": monotone, "all_ok": ok,
                       "fit_equals_replay": fit_matches_replay,
                       "event_ms": ms, "wall_ms": ms_wall},
-        "fit_5_iterations": {"ms_per_iteration": fit5_ms / 5, "batched_it_per_s": 5000.0 / fit5_ms,
+        "fit_5_iterations": {"ms_per_iteration": fit5_ms / 5, "batched_it_per_s": agg["fit5_batched_it_per_s"],
                              "line_search_trials_per_iteration": trials_per_iter, "call_status": fit5_rc,
                              "trajectory_status_counts": fit5_status,
                              "note": "iterations 4-5 at the fp64 cost floor: capped line searches (status 3 = exhausted)"},
-        "fit_default_options": {"ms_per_fit": dflt_ms, "mean_iterations": dflt_iters,
-                                "batched_it_per_s": 1000.0 * dflt_iters / dflt_ms, "call_status": dflt_rc,
+        "fit_default_options": {"ms_per_fit": dflt_ms, "mean_iterations": dflt_iters_all,
+                                "batched_it_per_s": agg["fit_default_batched_it_per_s"], "call_status": dflt_rc,
                                 "trajectory_status_counts": dflt_status,
                                 "note": "the reference's default call: tol = 1e-6, max_iter = 100 (converged trajectories leave the batch)"},
-        "single_iteration_cold": {"ms": single_ms, "batched_it_per_s": 1000.0 / single_ms,
+        "single_iteration_cold": {"ms": single_ms, "batched_it_per_s": agg["single_iteration_batched_it_per_s"],
                                   "note": "one iteration from cold per step (ilqr_iterate = one launch of "
                                           "lq_iter_fused4: every wave's backward then its forward)"},
         "iteration_kernel": {"kernel": "lq_iter_fused4 (backward_pass + forward_pass, 4 trajectories per wave)",
@@ -632,12 +684,17 @@ def main():
                              "traffic": (pmc or {}).get("hbm_bytes_per_fused_launch"),
                              "mfma_pmc": mfma_summary(mf, "fused")},
         "co_headline": {"metric": "batched iLQR iterations/sec (fwd+bwd pass), nx=12 nu=4 T=100, 1/2/4/8 MI355X",
-                        "value": world * 5000.0 / fit5_ms, "unit": "batched iterations/s",
+                        "value": agg["co_headline"], "unit": "batched iterations/s",
                         "protocol": "SURVEY.md §8(d): 5-iteration fit from cold, tol disabled, median of 20 fits after "
                                     "2 warm-ups (iterations 4-5 at the fp64 cost floor, long line searches)",
                         "ms_per_fit": fit5_ms, "n_gpus": world},
         "secondary_configs": secondary,
         "allgather_costs_ms": gather_ms,
+        "allgather_costs_event_ms": gather_ev_ms,
+        "rank_reduction": "every time in this line is the max over ranks (the per-GPU kernel legs too: "
+                          "roofline, backward_leg, forward_kernel, iteration_kernel); mean_iterations is the "
+                          "mean over ranks; rank0_times are rank 0's own",
+        "rank0_times": rank_times,
         "allgather_check": gathered,
         "cpu_baseline": None,
     }

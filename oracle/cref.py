@@ -157,6 +157,16 @@ def tl_fit(x_init, u_init, x_traj=None, max_iter=100, tol=1e-6, mu=0.01, max_tri
     return xo, uo, cost, iters, st
 
 
+def tl_set_physical_coriolis(on=False):
+    """Test-only: the textbook Coriolis matrix in place of the script's quirk (ilqr_ref.c)."""
+    load().oracle_tl_set_physical_coriolis(int(on))
+
+
+def set_fit_return_post_update(on=False):
+    """Test-only: fit returns the iterate that met tol, not the previous one (ilqr_ref.c)."""
+    load().oracle_set_fit_return_post_update(int(on))
+
+
 def tl_set_target(x=0.6, y=-0.5):
     """The 2-link target_tool_loc of the C restatement (test-only; default the script's)."""
     load().oracle_tl_set_target(C.c_double(x), C.c_double(y))

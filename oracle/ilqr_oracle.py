@@ -13,7 +13,11 @@ extracted into tests/golden/reference_gifs.npz by tests/golden/make_gif_golden.p
 The C restatement's fit of that workload reproduces every frame of the shipped
 script's GIF within a third of a pixel (elbow and tool ≤ 0.0035 data units,
 tests/test_reference_gifs.py), and this Python restatement equals the C one on the
-same workload (1e-9). Beyond that the restatements are pinned by known-answer tests
+same workload (1e-9). What the pin resolves (test_gif_pin_sensitivity): the script's
+CoriolisMatrix quirk IS visible — the textbook Coriolis matrix misses the frames by
+0.039 data units (≈3.5 px, 4× the tolerance); fit's return of the iterate before the
+update that met tol is NOT — the other choice moves the frames by < 10⁻⁵, so that quirk
+rests on the restatement's algebra and the unit tests alone. Beyond that the restatements are pinned by known-answer tests
 derived from the reference's own tests and algebra (tests/test_oracle.py): the
 repaired linear-f linearisation property of test/test_linearize_dynamics.jl:24-25,
 the LQ closed-form (KKT) fixed point, the 2-link IK constants of

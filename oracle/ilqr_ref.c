@@ -216,6 +216,15 @@ void oracle_tl_set_target(double x, double y) {
   TL.tgt1 = q2;
 }
 
+/* test-only (tests/test_reference_gifs.py::test_gif_pin_sensitivity): 1 = the textbook
+ * Coriolis matrix (Christoffel symbols summed over every k) in place of the script's
+ * CoriolisMatrix, whose `for k in length(θ)` (:42-44) leaves ½·θ̇₂·∂M/∂θ₂:
+ * C = [−βs₂θ̇₂, −βs₂(θ̇₁+θ̇₂); βs₂θ̇₁, 0] against [−βs₂θ̇₂, −½βs₂θ̇₂; −½βs₂θ̇₂, 0]. */
+static int TL_PHYSICAL_CORIOLIS = 0;
+void oracle_tl_set_physical_coriolis(int on) { TL_PHYSICAL_CORIOLIS = on; }
+
+static void tl_cd_dual_tail(const dual6* x, const dual6* u, dual6* xd, dual6 m00, dual6 m01, dual6 c00,
+                            dual6 c01, dual6 c10, dual6 c11);
 /* continuous_dynamics (:51-69) on duals */
 static void tl_cd_dual(const dual6* x, const dual6* u, dual6* xd) {
   const dual6 c2 = dcos(x[1]), s2 = dsin(x[1]);
@@ -228,6 +237,15 @@ static void tl_cd_dual(const dual6* x, const dual6* u, dual6* xd) {
   const dual6 c01 = dmul(dscale(0.5, dsub(dadd(dm01, dm01), dm01)), x[3]);
   const dual6 c10 = dmul(dscale(0.5, dsub(dadd(zero, dm01), zero)), x[3]);
   const dual6 c11 = dmul(dscale(0.5, dsub(dadd(zero, zero), zero)), x[3]);
+  if (TL_PHYSICAL_CORIOLIS) {
+    const dual6 p01 = dmul(dm01, dadd(x[2], x[3])), p10 = dneg(dmul(dm01, x[2]));
+    tl_cd_dual_tail(x, u, xd, m00, m01, c00, p01, p10, zero);
+    return;
+  }
+  tl_cd_dual_tail(x, u, xd, m00, m01, c00, c01, c10, c11);
+}
+static void tl_cd_dual_tail(const dual6* x, const dual6* u, dual6* xd, dual6 m00, dual6 m01, dual6 c00,
+                            dual6 c01, dual6 c10, dual6 c11) {
   const dual6 det = dsub(dmul(m00, dc(TL.delta)), dmul(m01, m01));
   const dual6 i00 = ddiv(dc(TL.delta), det), i01 = ddiv(dneg(m01), det);
   const dual6 i10 = ddiv(dneg(m01), det), i11 = ddiv(m00, det);
@@ -244,11 +262,13 @@ static void tl_cd(const double* x, const double* u, double* xd) {
   const double m00 = TL.alpha + 2 * TL.beta * c2, m01 = TL.delta + TL.beta * c2;
   const double dm00 = 2 * TL.beta * -s2, dm01 = TL.beta * -s2;
   const double c00 = 0.5 * dm00 * x[3], c01 = 0.5 * ((dm01 + dm01) - dm01) * x[3];
-  const double c10 = 0.5 * dm01 * x[3], c11 = 0.0 * x[3];
+  double c10 = 0.5 * dm01 * x[3], c11 = 0.0 * x[3];
+  const double c01p = TL_PHYSICAL_CORIOLIS ? dm01 * (x[2] + x[3]) : c01;
+  if (TL_PHYSICAL_CORIOLIS) { c10 = -(dm01 * x[2]); c11 = 0.0; }
   const double det = m00 * TL.delta - m01 * m01;
   const double i00 = TL.delta / det, i01 = -m01 / det, i10 = -m01 / det, i11 = m00 / det;
-  const double mc00 = i00 * c00 + i01 * c10, mc01 = i00 * c01 + i01 * c11;
-  const double mc10 = i10 * c00 + i11 * c10, mc11 = i10 * c01 + i11 * c11;
+  const double mc00 = i00 * c00 + i01 * c10, mc01 = i00 * c01p + i01 * c11;
+  const double mc10 = i10 * c00 + i11 * c10, mc11 = i10 * c01p + i11 * c11;
   xd[0] = x[2];
   xd[1] = x[3];
   xd[2] = -(mc00 * x[2] + mc01 * x[3]) + (i00 * u[0] + i01 * u[1]);
@@ -831,6 +851,11 @@ int oracle_lq_forward(int Bn, int T, int n, int m, const double* A, const double
  * (the reference's `Iteration: i  Total Cost: c` line, :167; NaN if the search failed),
  * the trials of the search (max_trials when exhausted), Σ(ū − u)² (:171); entries past
  * the last iteration untouched — ilqr_fit_ex's history record (include/ilqr.h). */
+/* test-only (tests/test_reference_gifs.py::test_gif_pin_sensitivity): 1 = on convergence
+ * return the iterate just computed instead of the reference's previous one (:171-178). */
+static int FIT_RETURN_POST_UPDATE = 0;
+void oracle_set_fit_return_post_update(int on) { FIT_RETURN_POST_UPDATE = on; }
+
 static void fit_one(const prob_t* P, const double* x_init, const double* u_init,
                     const double* xtraj, int max_iter, double tol, double mu, int sym,
                     int max_trials, double* x_out, double* u_out, double* cost, int* iters,
@@ -854,7 +879,14 @@ static void fit_one(const prob_t* P, const double* x_init, const double* u_init,
     double du2 = 0.0;
     for (size_t i = 0; i < us; ++i) du2 += (un[i] - ui[i]) * (un[i] - ui[i]);
     if (hdu2) hdu2[it - 1] = du2;
-    if (du2 <= tol) { st = 1; break; } /* :171 — break before the update */
+    if (du2 <= tol) { /* :171 — break before the update */
+      st = 1;
+      if (FIT_RETURN_POST_UPDATE) {
+        memcpy(xi, xn, sizeof(double) * xs);
+        memcpy(ui, un, sizeof(double) * us);
+      }
+      break;
+    }
     memcpy(xi, xn, sizeof(double) * xs); /* :174-175 */
     memcpy(ui, un, sizeof(double) * us);
   }

@@ -88,3 +88,16 @@ def test_bench_gpus_flag_spawns_ranks():
     assert out["n_gpus"] == 2
     assert out["allgather_check"]["trajectories"] == 32
     assert out["allgather_check"]["own_block_matches"] and out["allgather_check"]["finite_costs"] == 32
+    # every aggregate field is formed from the MAX over ranks of the per-rank times (here
+    # stand-in times with rank 1 the slower), the default fit's iterations the mean
+    import bench
+    t0, i0 = bench.fake_rank_times(0)
+    t1, i1 = bench.fake_rank_times(1)
+    assert out["rank_times_max"] == {k: max(t0[k], t1[k]) for k in bench.RANK_TIMES}
+    assert out["rank_times_max"] == t1 and out["dflt_iters_mean"] == (i0 + i1) / 2
+    agg = out["aggregates"]
+    assert agg["value"] == 2 * 1000.0 / t1["ms_step"]
+    assert agg["co_headline"] == agg["fit5_batched_it_per_s"] == 2 * 5000.0 / t1["fit5_ms"]
+    assert agg["fit_default_batched_it_per_s"] == 2 * 1000.0 * (i0 + i1) / 2 / t1["dflt_ms"]
+    assert agg["single_iteration_batched_it_per_s"] == 2 * 1000.0 / t1["single_ms"]
+    assert agg == bench.aggregate_fields(t1, (i0 + i1) / 2, 2)
