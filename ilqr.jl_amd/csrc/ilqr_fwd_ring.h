@@ -248,12 +248,35 @@ __device__ FwdOut lq_forward_wave_ring(const LQParams& P, int b0, int B, int T, 
   // producer: lane l moves 16 B per instruction; three instructions fill one slot
   //   #1: K chunk l (of 96)   #2: K chunk 64+l | x chunk l−32 | u chunk l−56
   //   #3: x_traj chunk l | δu chunk l−24 | (lanes 32..63 repeat lanes 0..31)
+  // A candidate pass rolls out ONE trajectory in all four groups: one instruction fills
+  // the slot's first 40 chunks with its step (K 0..23, x 24..29, u 30..31, x_traj 32..37,
+  // δu 38..39; lanes 40..63 repeat lanes 0..23 past them) and every group reads those.
   auto tr = [&](int gg) { return (size_t)(b0 + (gg < nt ? gg : 0)); };
   const double* xt0 = xtraj ? xtraj : x;  // x_traj = NULL: read x with weight 0
   const double xtw = xtraj ? 1.0 : 0.0;
   const char *p1, *p2, *p3;
   uint32_t s1, s2, s3;  // bytes per step
-  {
+  if constexpr (CAND) {
+    const int c = l < 40 ? l : l - 40;
+    if (c < 24) {
+      p1 = reinterpret_cast<const char*>(Kg + tr(0) * T * NU * NX + 2 * c);
+      s1 = NU * NX * 8;
+    } else if (c < 30) {
+      p1 = reinterpret_cast<const char*>(x + tr(0) * (T + 1) * NX + 2 * (c - 24));
+      s1 = NX * 8;
+    } else if (c < 32) {
+      p1 = reinterpret_cast<const char*>(u + tr(0) * T * NU + 2 * (c - 30));
+      s1 = NU * 8;
+    } else if (c < 38) {
+      p1 = reinterpret_cast<const char*>(xt0 + tr(0) * (T + 1) * NX + 2 * (c - 32));
+      s1 = NX * 8;
+    } else {
+      p1 = reinterpret_cast<const char*>(dg + tr(0) * T * NU + 2 * (c - 38));
+      s1 = NU * 8;
+    }
+    p2 = p3 = p1;
+    s2 = s3 = s1;
+  } else {
     const int c = l;
     p1 = reinterpret_cast<const char*>(Kg + tr(c / 24) * T * NU * NX + 2 * (c % 24));
     s1 = NU * NX * 8;
@@ -286,14 +309,17 @@ __device__ FwdOut lq_forward_wave_ring(const LQParams& P, int b0, int B, int T, 
     asm volatile("" : "+s"(tt));  // no hoisting of the prologue's addresses out of the trial loop
     const uint32_t m0 = ring_lds + (uint32_t)((t % R) * RING_SLOT * 8);
     asm volatile(ILQR_FW_LDS_OP1 ::"v"(p1 + (size_t)tt * s1), "{m0}"(m0) : "memory");
-    asm volatile(ILQR_FW_LDS_OP ::"v"(p2 + (size_t)tt * s2), "{m0}"(m0 + 1024) : "memory");
-    asm volatile(ILQR_FW_LDS_OP ::"v"(p3 + (size_t)tt * s3), "{m0}"(m0 + 2048) : "memory");
+    if constexpr (!CAND) {
+      asm volatile(ILQR_FW_LDS_OP ::"v"(p2 + (size_t)tt * s2), "{m0}"(m0 + 1024) : "memory");
+      asm volatile(ILQR_FW_LDS_OP ::"v"(p3 + (size_t)tt * s3), "{m0}"(m0 + 2048) : "memory");
+    }
   };
   // vmcnt immediates (gfx9: vmcnt[3:0] | expcnt 7 << 4 | lgkmcnt 15 << 8 | vmcnt[5:4] << 14):
-  // per step the wave issues 3 slot loads then 2 result stores, so slot t is
-  // complete once ≤ 5·PF − 3 ops are outstanding (≤ 3·PF − 3 while the prologue
-  // loads are the newest)
-  constexpr int N_SS = 5 * PF - 3, N_PRO = 3 * PF - 3;
+  // per step the wave issues NL slot loads then 2 result stores, so slot t is
+  // complete once ≤ (NL + 2)·PF − NL ops are outstanding (≤ NL·PF − NL while the
+  // prologue loads are the newest)
+  constexpr int NL = CAND ? 1 : 3;
+  constexpr int N_SS = (NL + 2) * PF - NL, N_PRO = NL * PF - NL;
   auto wait_slot = [](auto n) {
     constexpr int v = decltype(n)::value;
     static_assert(v >= 0 && v < 64, "vmcnt is 6 bits");
@@ -301,9 +327,11 @@ __device__ FwdOut lq_forward_wave_ring(const LQParams& P, int b0, int B, int T, 
     asm volatile("" ::: "memory");
   };
 
-  const int ka = g * 48 + iu * NX;                                 // K row of (g, iu)
-  const int va = is_x ? 192 + g * 12 + jx : 240 + g * 4 + iu;      // x (x lanes) / u (u lanes)
-  const int vb = is_x ? 256 + g * 12 + jx : 304 + g * 4 + iu;      // x_traj / δu
+  // K row of (g, iu); x (x lanes) / u (u lanes); x_traj / δu — a candidate pass's slot
+  // holds its one trajectory's step at the front (producer above)
+  const int ka = CAND ? iu * NX : g * 48 + iu * NX;
+  const int va = CAND ? (is_x ? 48 + jx : 60 + iu) : (is_x ? 192 + g * 12 + jx : 240 + g * 4 + iu);
+  const int vb = CAND ? (is_x ? 64 + jx : 76 + iu) : (is_x ? 256 + g * 12 + jx : 304 + g * 4 + iu);
   // the resources' words made provably wave-uniform (the candidate passes run inside
   // the cooperative search's loops, where the compiler loses track of it: a divergent
   // resource is a readfirstlane waterfall loop around every store)
@@ -967,7 +995,7 @@ __device__ int coop_evaluate(const LQParams& P, int b, int B, int T, const IterA
   if (l == 0) {
     j0 = __hip_atomic_fetch_add(&R->next, 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     lim0 = coop_lim(R, ls.max_trials);
-    sl = ag_ld(&R->slot);
+    sl = ag_rmw_ld(&R->slot);  // picks the scratch rows: a decision, so read coherently
   }
   j0 = __builtin_amdgcn_readfirstlane(j0);
   lim0 = __builtin_amdgcn_readfirstlane(lim0);
