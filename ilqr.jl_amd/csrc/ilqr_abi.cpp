@@ -473,9 +473,18 @@ ilqr_status ilqr_create(ilqr_handle** out, int device, int nx, int nu, int T, in
     const int nsl = std::min(batch, ilqr::COOP_SCRATCH_SLOTS);
     const size_t sxb = sizeof(double) * nsl * ilqr::COOP_MAX_TRIALS * (size_t)(T + 1) * nx;
     const size_t sub = sizeof(double) * nsl * ilqr::COOP_MAX_TRIALS * (size_t)T * nu;
-    const bool scratch = sxb < (size_t(1) << 31);
-    if (e == hipSuccess && scratch) e = hipMalloc(&h->coop_sx, sxb);
-    if (e == hipSuccess && scratch) e = hipMalloc(&h->coop_su, sub);
+    bool scratch = sxb < (size_t(1) << 31);
+    // the scratch (≈260 MB at T = 1000) is a speed-up, not a need: without it the search
+    // rolls the final trial out again (nslots = 0), so a failed allocation is not an error
+    if (e == hipSuccess && scratch && hipMalloc(&h->coop_sx, sxb) != hipSuccess) scratch = false;
+    if (e == hipSuccess && scratch && hipMalloc(&h->coop_su, sub) != hipSuccess) scratch = false;
+    if (!scratch) {
+      (void)hipGetLastError();  // clear the failed allocation's error
+      (void)hipFree(h->coop_sx);
+      (void)hipFree(h->coop_su);
+      h->coop_sx = nullptr;
+      h->coop_su = nullptr;
+    }
     if (e == hipSuccess) {
       const ilqr::LSCoop c{h->coop_rec, h->coop_cost, h->coop_du2, h->coop_list, h->coop_ctl,
                            h->coop_sx,  h->coop_su,   scratch ? nsl : 0};

@@ -331,24 +331,26 @@ __global__ __launch_bounds__(256) void tl_jacobian_kernel(TwoLinkParams P, int B
                                                           double* __restrict__ A, double* __restrict__ Bm) {
   constexpr int ND = TL_NX + NU;
   const int b = blockIdx.x * 256 + threadIdx.x;
-  const int t = blockIdx.y;
   if (b >= B) return;
-  const double* xb = x + ((size_t)b * (T + 1) + t) * TL_NX;
-  const double* ub = u + ((size_t)b * T + t) * NU;
-  Dual<ND> xs[4], us[NU], out[4];
+  // steps on grid y, strided past 65,535 (HIP's limit for gridDim.y)
+  for (int t = blockIdx.y; t < T; t += gridDim.y) {
+    const double* xb = x + ((size_t)b * (T + 1) + t) * TL_NX;
+    const double* ub = u + ((size_t)b * T + t) * NU;
+    Dual<ND> xs[4], us[NU], out[4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) xs[i] = seed<ND>(xb[i], i);
+    for (int i = 0; i < 4; ++i) xs[i] = seed<ND>(xb[i], i);
 #pragma unroll
-  for (int i = 0; i < NU; ++i) us[i] = seed<ND>(ub[i], 4 + i);
-  rk4_lin<Dual<ND>, NU>(P, xs, us, out);
-  double* At = A + ((size_t)b * T + t) * 16;
-  double* Bt = Bm + ((size_t)b * T + t) * 4 * NU;
+    for (int i = 0; i < NU; ++i) us[i] = seed<ND>(ub[i], 4 + i);
+    rk4_lin<Dual<ND>, NU>(P, xs, us, out);
+    double* At = A + ((size_t)b * T + t) * 16;
+    double* Bt = Bm + ((size_t)b * T + t) * 4 * NU;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < 4; ++i) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) At[i * 4 + k] = out[i].d[k];
+      for (int k = 0; k < 4; ++k) At[i * 4 + k] = out[i].d[k];
 #pragma unroll
-    for (int k = 0; k < NU; ++k) Bt[i * NU + k] = out[i].d[4 + k];
+      for (int k = 0; k < NU; ++k) Bt[i * NU + k] = out[i].d[4 + k];
+    }
   }
 }
 
@@ -851,7 +853,7 @@ hipError_t launch_tl_forward(const TwoLinkParams& P, int nu, int B, int T, const
 hipError_t launch_tl_jacobian(const TwoLinkParams& P, int nu, int B, int T, const double* x,
                               const double* u, double* A, double* Bm, hipStream_t s) {
   if (B <= 0) return hipSuccess;
-  const dim3 g((B + 255) / 256, T);
+  const dim3 g((B + 255) / 256, T < 65535 ? T : 65535);
   if (nu == 1)
     tl_jacobian_kernel<1><<<g, 256, 0, s>>>(P, B, T, x, u, A, Bm);
   else

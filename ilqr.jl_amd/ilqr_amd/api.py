@@ -28,14 +28,13 @@ forward_pass and, in fit, stops that trajectory at its current iterate.
 """
 from __future__ import annotations
 
-import contextlib
-import threading
 import warnings
 
 import numpy as np
 import torch
 
 from . import _lib
+from . import cache as _cache
 from . import tiles as _tiles
 from .chain import ChainSolver, chain_problem_of
 from .cost_functions import simple_costs_of
@@ -111,48 +110,19 @@ def _chain_solver(xb, ub, dynamicsf, immediate_cost, final_cost, dtype):
     return s
 
 
-# The closure path's tiles handles, one per (device, nx, nu, T, batch), kept between
-# calls (an MPC loop calling fit allocates no device workspace per call). A call checks
-# its handle OUT of the cache and back in when done, so two threads fitting the same
-# shape at once never share one (the second builds its own; the surplus is closed on
-# check-in). At most _TILES_MAX shapes stay cached, least recently used evicted.
-_TILES_CACHE: dict = {}
-_TILES_LOCK = threading.Lock()
-_TILES_MAX = 8
-
-
-@contextlib.contextmanager
 def _tiles_solver(xb, ub):
+    """The closure path's tiles handle of this shape, cached between calls (cache.py)."""
     nb, N, nx = xb.shape
     _, M, nu = ub.shape
     assert N == M + 1, "size(x)[1] == size(u)[1] + 1"   # backward_pass.jl:329
-    key = (_device(), nx, nu, M, nb)
-    with _TILES_LOCK:
-        s = _TILES_CACHE.pop(key, None)
-    if s is None:
-        s = Solver(nx, nu, M, nb, device=key[0], kind=_lib.PROBLEM_TILES)
-    try:
-        yield s
-    finally:
-        evicted = []
-        with _TILES_LOCK:
-            if key in _TILES_CACHE:
-                evicted.append(s)
-            else:
-                _TILES_CACHE[key] = s
-                while len(_TILES_CACHE) > _TILES_MAX:
-                    evicted.append(_TILES_CACHE.pop(next(iter(_TILES_CACHE))))
-        for e in evicted:
-            e.close()
+    dev = _device()
+    return _cache.workspace(("tiles", dev, nx, nu, M, nb),
+                            lambda: Solver(nx, nu, M, nb, device=dev, kind=_lib.PROBLEM_TILES))
 
 
 def clear_cache():
-    """Close the tiles handles fit / backward_pass keep per shape for closures."""
-    with _TILES_LOCK:
-        ss = list(_TILES_CACHE.values())
-        _TILES_CACHE.clear()
-    for s in ss:
-        s.close()
+    """Close the device workspaces fit / backward_pass / linearize_dynamics keep per shape."""
+    _cache.clear()
 
 
 def _solver(xb, ub, dynamicsf, immediate_cost, final_cost):

@@ -28,6 +28,7 @@ import numpy as np
 import torch
 
 from . import _lib
+from . import cache as _cache
 from .problems import (LinearDynamics, QuadraticCost, QuadraticFinalCost, TwoLinkArm, TwoLinkCost,
                        TwoLinkDynamics, TwoLinkFinalCost)
 
@@ -85,8 +86,11 @@ def linearize_dynamics(x, u, dynamicsf):
 def _linearize(x, u, dynamicsf, nb, nx, nu, T):
     from .chain import ChainDynamics, ChainSolver
     from .solver import Solver
+    dev = x.device.index
     if isinstance(dynamicsf, TwoLinkDynamics) and (nx, nu) == (4, dynamicsf.nu):
-        return _abi_linearize(Solver(4, nu, T, nb, device=x.device.index, kind=_lib.PROBLEM_TWO_LINK), x, u)
+        with _cache.workspace(("two_link", dev, nu, T, nb),
+                              lambda: Solver(4, nu, T, nb, device=dev, kind=_lib.PROBLEM_TWO_LINK)) as s:
+            return _abi_linearize(s, x, u)
     if isinstance(dynamicsf, LinearDynamics) and (dynamicsf.nx, dynamicsf.nu) == (nx, nu) \
             and _lib.load().ilqr_supported(_lib.PROBLEM_LQ, nx, nu):
         from .problems import LQBatch
@@ -94,12 +98,12 @@ def _linearize(x, u, dynamicsf, nb, nx, nu, T):
         def bc(a, shape):
             a = np.asarray(a, dtype=np.float64)
             return np.broadcast_to(a, (nb,) + shape) if a.ndim == 2 else a
-        s = Solver(nx, nu, T, nb, device=x.device.index)
         z = np.zeros((nb, nx, nx))
-        s.set_problem(LQBatch(bc(dynamicsf.A, (nx, nx)), bc(dynamicsf.B, (nx, nu)), z, np.zeros((nb, nu, nu)), z))
-        return _abi_linearize(s, x, u)
+        with _cache.workspace(("lq", dev, nx, nu, T, nb), lambda: Solver(nx, nu, T, nb, device=dev)) as s:
+            s.set_problem(LQBatch(bc(dynamicsf.A, (nx, nx)), bc(dynamicsf.B, (nx, nu)), z, np.zeros((nb, nu, nu)), z))
+            return _abi_linearize(s, x, u)
     if isinstance(dynamicsf, ChainDynamics) and (dynamicsf.problem.nx, dynamicsf.problem.nu) == (nx, nu):
-        s = ChainSolver(dynamicsf.problem, T, nb, dtype=torch.float64, device=x.device.index)
+        s = ChainSolver(dynamicsf.problem, T, nb, dtype=torch.float64, device=dev)
         try:
             A, Bm = s.linearize(x, u)
             torch.cuda.synchronize(x.device)
@@ -119,15 +123,13 @@ def _linearize(x, u, dynamicsf, nb, nx, nu, T):
 
 
 def _abi_linearize(s, x, u):
+    """ilqr_linearize on the workspace `s` (the caller owns and keeps it)."""
     from .solver import _ptr
-    try:
-        A = torch.empty((s.batch, s.T, s.nx, s.nx), dtype=torch.float64, device=x.device)
-        Bm = torch.empty((s.batch, s.T, s.nx, s.nu), dtype=torch.float64, device=x.device)
-        s._bind_stream()
-        _lib.check(s.lib.ilqr_linearize(s.h, s._p(), _ptr(x), _ptr(u), _ptr(A), _ptr(Bm)), "ilqr_linearize")
-        torch.cuda.current_stream(x.device).synchronize()
-    finally:
-        s.close()
+    A = torch.empty((s.batch, s.T, s.nx, s.nx), dtype=torch.float64, device=x.device)
+    Bm = torch.empty((s.batch, s.T, s.nx, s.nu), dtype=torch.float64, device=x.device)
+    s._bind_stream()
+    _lib.check(s.lib.ilqr_linearize(s.h, s._p(), _ptr(x), _ptr(u), _ptr(A), _ptr(Bm)), "ilqr_linearize")
+    torch.cuda.current_stream(x.device).synchronize()
     return A, Bm
 
 

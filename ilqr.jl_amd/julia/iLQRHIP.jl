@@ -522,6 +522,7 @@ mutable struct Solver
     d::Ptr{Float64}; K::Ptr{Float64}; pc::Ptr{Float64}; cost::Ptr{Float64}
     iters::Ptr{Int32}; status::Ptr{Int32}; trials::Ptr{Int32}
     hc::Ptr{Float64}; ht::Ptr{Int32}; hcap::Int
+    lA::Ptr{Float64}; lB::Ptr{Float64}   # linearize_dynamics' outputs, allocated on first use
     lock::ReentrantLock      # held by the functional entry points for a whole call (with_cached)
 end
 
@@ -535,7 +536,15 @@ function Solver(nx::Integer, nu::Integer, T::Integer, batch::Integer; device::In
                   f(N * nx), f(T * nu), f(N * nx), f(N * nx), f(T * nu),         # x u x_traj x̄ ū
                   f(T * nu), f(T * nu * nx), f(1), f(1),                          # δu K prev_cost cost
                   i(1), i(1), i(1),                                               # iters status trials
-                  Ptr{Float64}(C_NULL), Ptr{Int32}(C_NULL), 0, ReentrantLock())
+                  Ptr{Float64}(C_NULL), Ptr{Int32}(C_NULL), 0,
+                  Ptr{Float64}(C_NULL), Ptr{Float64}(C_NULL), ReentrantLock())
+end
+
+function ensure_linearize!(s::Solver)
+    if s.lA == C_NULL
+        s.lA = alloc(s.h, Float64, s.nb * s.M * s.nx * s.nx); s.lB = alloc(s.h, Float64, s.nb * s.M * s.nx * s.nu)
+    end
+    return s
 end
 
 Base.close(s::Solver) = lock(() -> close(s.h), s.lock)
@@ -754,20 +763,19 @@ function linearize_dynamics(x::AbstractMatrix, u::AbstractMatrix, f)
         return As, Bs
     end
     xa = size(x, 1) == M ? vcat(x, x[end:end, :]) : x                   # the ABI reads T+1 states
-    h = Handle(nx, nu, M, 1)
-    try
-        p = fam == :lq ? Ref(problem(h, f, QuadraticCost(zero(f.A), zeros(nu, nu)), QuadraticFinalCost(zero(f.A)))) :
-                         Ref(Problem(ILQR_PROBLEM_TWO_LINK, 0, C_NULL, C_NULL, C_NULL, C_NULL, C_NULL))
-        xd = upload(h, to_abi(xa)); ud = upload(h, to_abi(u))
-        Ad = alloc(h, Float64, M * nx * nx); Bd = alloc(h, Float64, M * nx * nu)
+    # on the cached Solver of this shape (with_cached): no handle or buffer per call; the A/B
+    # outputs are allocated on its first linearisation
+    return with_cached(SOLVER_CACHE, () -> Solver(nx, nu, M, 1), (nx, nu, M)) do s
+        fam == :lq ? set_problem!(s, f, QuadraticCost(zero(f.A), zeros(nu, nu)), QuadraticFinalCost(zero(f.A))) :
+                     set_problem!(s, f, TwoLinkCost(), TwoLinkFinalCost())
+        ensure_linearize!(s)
+        upload!(s.h, s.x, to_abi(xa)); upload!(s.h, s.u, to_abi(u))
         check(ccall((:ilqr_linearize, libilqr), Cint,
                     (Ptr{Cvoid}, Ref{Problem}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}),
-                    h.ptr, p, xd, ud, Ad, Bd), "ilqr_linearize")
+                    s.h.ptr, problem_ref(s), s.x, s.u, s.lA, s.lB), "ilqr_linearize")
         # (T, nx, nx) row-major = Julia (nx, nx, T), each step transposed → 𝐀s (T × nx × nx)
-        return (permutedims(download!(h, zeros(nx, nx, M), Ad), (3, 2, 1)),
-                permutedims(download!(h, zeros(nu, nx, M), Bd), (3, 2, 1)))
-    finally
-        close(h)
+        (permutedims(download!(s.h, zeros(nx, nx, M), s.lA), (3, 2, 1)),
+         permutedims(download!(s.h, zeros(nu, nx, M), s.lB), (3, 2, 1)))
     end
 end
 

@@ -144,3 +144,32 @@ def test_linearize_dynamics_chain(gpu):
         Afd = np.stack([(f(xs[i] + h * e, us[i]) - f(xs[i] - h * e, us[i])) / (2 * h) for e in np.eye(4)], axis=1)
         Bfd = np.stack([(f(xs[i], us[i] + h * e) - f(xs[i], us[i] - h * e)) / (2 * h) for e in np.eye(2)], axis=1)
         assert rel(As[i], Afd) < 1e-7 and rel(Bs[i], Bfd) < 1e-7
+
+
+def test_linearize_two_link_past_the_grid_y_limit_and_cached(gpu):
+    """A horizon past HIP's 65,535 limit on gridDim.y (the Jacobian kernel strides its
+    steps, advisor r04), and the helper's device workspace kept between calls
+    (ilqr_amd.cache: one Solver for repeated calls of one shape)."""
+    from ilqr_amd import cache
+    f, _, _ = two_link_closures()
+    rng = np.random.default_rng(3)
+    T = 70_000
+    xs, us = rng.random((T + 1, 4)), rng.random((T, 2))
+    cache.clear()
+    made = []
+    orig = Solver.__init__
+
+    def counting(self, *a, **k):
+        made.append(a)
+        orig(self, *a, **k)
+    Solver.__init__ = counting
+    try:
+        As, Bs = H.linearize_dynamics(xs, us, f)
+        As2, Bs2 = H.linearize_dynamics(xs, us, f)
+    finally:
+        Solver.__init__ = orig
+    assert len(made) == 1 and np.array_equal(As, As2) and np.array_equal(Bs, Bs2)
+    for i in (0, 65_534, 65_535, 65_536, T - 1):
+        Ao, Bo = O.linearize_dynamics(xs[i], us[i], O.TwoLink.dynamicsf)
+        assert rel(As[i], Ao) < 1e-12 and rel(Bs[i], Bo) < 1e-12, i
+    cache.clear()

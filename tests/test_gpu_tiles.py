@@ -255,3 +255,44 @@ def test_rbd_caller_fit_t1000(gpu):
     assert info["history"]["trials"][:iters].tolist() == r["history"]["trials"].tolist()
     assert rel(info["cost"], r["cost"]) < 1e-8
     assert rel(xf, r["x"]) < 1e-8 and rel(uf, r["u"]) < 1e-8
+
+
+def test_closure_path_reuses_one_handle_and_is_thread_safe(gpu):
+    """fit with closures keeps one tiles handle per shape between calls (ilqr_amd.cache),
+    and two threads fitting DIFFERENT problems of the same shape at once each get their
+    own result (the advisor's reentrancy case for the Julia shim, here for the mirror)."""
+    import threading
+    from ilqr_amd import cache
+    api.clear_cache()
+    created = []
+    orig = Solver.__init__
+
+    def counting(self, *a, **k):
+        created.append(a)
+        orig(self, *a, **k)
+    ft = coupled_pendula(torch_ns())
+    xs = [pendula_batch(2, 20, seed=s) for s in (21, 22)]
+    ref = [api.fit(torch.from_numpy(x).cuda(), torch.from_numpy(u).cuda(), *ft, max_iter=10) for x, u in xs]
+    Solver.__init__ = counting
+    try:
+        for _ in range(3):
+            api.fit(torch.from_numpy(xs[0][0]).cuda(), torch.from_numpy(xs[0][1]).cuda(), *ft, max_iter=10)
+        assert created == []                        # the cached handle, no new one
+        out = [None, None]
+
+        def run(i):
+            x, u = xs[i]
+            for _ in range(3):
+                out[i] = api.fit(torch.from_numpy(x).cuda(), torch.from_numpy(u).cuda(), *ft, max_iter=10)
+        ths = [threading.Thread(target=run, args=(i,)) for i in range(2)]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
+    finally:
+        Solver.__init__ = orig
+    for i in range(2):
+        assert torch.equal(out[i][0], ref[i][0]) and torch.equal(out[i][1], ref[i][1])
+    assert len(created) <= 1 and cache.size() >= 1
+    api.clear_cache()
+    assert cache.size() == 0
