@@ -4,7 +4,7 @@ alternates they were measured against — the backward's ro
 instruction cuts undone and its probe bits (ABL), the one-wave backward's variants,
 the ring forward's LDS row broadcasts, cache hints and timing-only ablations, the
 chain's Rodrigues-form / unpacked evaluations, the 2-link forward on the generic RK4
-— live in tools/ablation/restore_alternates.patch. This test applies the patch to a
+— live in tools/archive/ablation/restore_alternates.patch. This test applies the patch to a
 copy of the current sources and compiles them with the alternates switched on, so
 that record stays reproducible against the product tree."""
 import os

@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B of the helper-wave build against the product library (one box). The helper library
-# is built here first: apply tools/ablation/coop_helpers.patch in a copy of the tree, compile
+# is built here first: apply tools/archive/ablation/coop_helpers.patch in a copy of the tree, compile
 # ilqr_bw4.hip and ilqr_lq.hip with -DILQR_COOP_HELPERS=1 and link them with the product
 # objects into ilqr.jl_amd/lib/libilqr_hip_helpers.so.
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out

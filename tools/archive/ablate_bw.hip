@@ -1,5 +1,5 @@
 // (Round 3: the ABL bits / -DILQR_* switches this probe uses exist only in the tree
-// tools/ablation/restore_tree.sh restores; build it there.)
+// tools/archive/ablation/restore_tree.sh restores; build it there.)
 // Ablation harness for the backward kernel (not part of the product): times
 // lq_backward_wave<12,4,ABL> for several ABL bit sets at B=4096, T=100 so the
 // share of MFMA / factor+solve / LDS hand-off / stores / gradient can be read off.

@@ -1,7 +1,7 @@
 """Accuracy of a Newton-Schulz (H + μI)⁻¹ in the LQ backward:
 numpy restatement of backward_pass.jl:324-357 (symmetrised step_back) where each step's
 gains come from X ≈ (H + μI)⁻¹ warm-started from the previous step's inverse, with the
-residual check of tools/ablation/bw4_newton_schulz.patch (per wave of four trajectories:
+residual check of tools/archive/ablation/bw4_newton_schulz.patch (per wave of four trajectories:
 the factorisation when max|I − HX| ≥ 2.5e-3 anywhere, else 3 NS steps, 2 below 2.5e-5),
 against the exact solve. Measured: quadrotor 256 trajectories max rel 1.06e-12 (15.6 %
 factorised / 29 % NS2 / 55 % NS3 steps), dense T = 64 1.7e-13. Fixed schedules without

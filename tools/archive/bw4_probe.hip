@@ -1,8 +1,8 @@
 // (Round 3: the ABL bits / -DILQR_* switches this probe uses exist only in the tree
-// tools/ablation/restore_tree.sh restores; build it there.)
+// tools/archive/ablation/restore_tree.sh restores; build it there.)
 // Probe for the four-trajectories-per-wave backward (not part of the product):
 // times lq_backward4_kernel against the one-trajectory-per-wave lq_backward_kernel
-// at B=4096, T=100 (random stable LQ problems, as tools/ablate_bw.hip) and reports
+// at B=4096, T=100 (random stable LQ problems, as tools/archive/ablate_bw.hip) and reports
 // the max relative difference of K and d between the two.
 #include "../ilqr.jl_amd/csrc/ilqr_lq.hip"
 #include "../ilqr.jl_amd/csrc/ilqr_bw4.hip"

@@ -1,5 +1,5 @@
 // (Round 3: the ABL bits / -DILQR_* switches this probe uses exist only in the tree
-// tools/ablation/restore_tree.sh restores; build it there.)
+// tools/archive/ablation/restore_tree.sh restores; build it there.)
 // Probe for backward-kernel schedules (not part of the product): times the v7
 // four-trajectories-per-wave kernel (lq_backward4_kernel) against the v8 schedule
 // variants (lq_backward4_v8_kernel) at B=4096, T=100 on random stable LQ problems,

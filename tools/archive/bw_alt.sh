@@ -1,8 +1,8 @@
 #!/bin/bash
 # (Round 3: the -DILQR_* switches below exist only in the restored tree: run this from
-# the directory tools/ablation/restore_tree.sh makes.)
+# the directory tools/archive/ablation/restore_tree.sh makes.)
 # Alternate builds of the backward file (ilqr_bw4.hip) for A/B timing with
-# tools/fused_probe.py <lib>: tools/fwalt/libilqr_hip_<name>.so
+# tools/archive/fused_probe.py <lib>: tools/fwalt/libilqr_hip_<name>.so
 #   base: the product flags
 #   mu0:  μ added in the factorisation (ILQR_BW4_MU_IN_H=0; the product folds it into H)
 set -e

@@ -1,6 +1,6 @@
 """Critical path of the cooperative line search in the headline's 5-iteration fit, from
-the instrumented build (tools/ablation/build_trace_lib.sh
-tools/ablation/wave_start_trace.patch): per launch, the waves' start and own-work-done
+the instrumented build (tools/archive/ablation/build_trace_lib.sh
+tools/archive/ablation/wave_start_trace.patch): per launch, the waves' start and own-work-done
 times, and for every published trajectory its publication (its wave's own-work-done),
 each quad of trials handed out (start, end of the pass, end of its finalisation) and
 the last wave's exit. Times in µs from the launch's first wave start."""

@@ -7,7 +7,7 @@ from ilqr_amd import _lib
 from ilqr_amd.problems import quadrotor_batch
 from ilqr_amd.solver import Solver, _ptr
 LIBS = [a for a in sys.argv[1:] if a.endswith(".so")]
-if LIBS:  # an alternate build of libilqr_hip.so (tools/fw_alt.sh, tools/fw_ab4.sh)
+if LIBS:  # an alternate build of libilqr_hip.so (tools/archive/fw_alt.sh, tools/archive/fw_ab4.sh)
     _lib._lib = _lib.load(LIBS[0])
     print("library:", LIBS[0])
 

@@ -1,6 +1,6 @@
 #!/bin/bash
 # (Round 3: the -DILQR_* switches below exist only in the restored tree: run this from
-# the directory tools/ablation/restore_tree.sh makes.)
+# the directory tools/archive/ablation/restore_tree.sh makes.)
 # Ablation build: the fused iteration and the ring forward without the K δx product
 # (ILQR_FW_ABLATE=4, wrong results; timing only) -> tools/fwalt/libilqr_hip_ab$AB.so
 set -e

@@ -1,10 +1,10 @@
 #!/bin/bash
 # (Round 3: the -DILQR_* switches below exist only in the restored tree: run this from
-# the directory tools/ablation/restore_tree.sh makes.)
+# the directory tools/archive/ablation/restore_tree.sh makes.)
 # Alternate builds of libilqr_hip.so with flags on BOTH files that hold the ring
 # forward (ilqr_lq.hip: the split schedule's forward; ilqr_bw4.hip: the fused
-# iteration), for A/B timing with tools/fused_probe.py <lib> / tools/gpu_bwab.sh:
-#   tools/fw_alt.sh <name> <flags...>   ->  tools/fwalt/libilqr_hip_<name>.so
+# iteration), for A/B timing with tools/archive/fused_probe.py <lib> / tools/archive/gpu_bwab.sh:
+#   tools/archive/fw_alt.sh <name> <flags...>   ->  tools/fwalt/libilqr_hip_<name>.so
 # e.g. -DILQR_FW_ST_AUX=2 (nt result stores), -DILQR_FW_LD_NT=1 (nt slot loads),
 # -DILQR_FW_ABLATE=<bits> (timing-only ablations), -DILQR_FW_LDS_BCAST=1.
 set -e

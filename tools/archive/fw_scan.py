@@ -9,7 +9,7 @@ from ilqr_amd.solver import Solver, _ptr
 
 MFMA = "mfma" in sys.argv[1:]  # the forward's MFMA form (ILQR_SCHED_FORWARD_MFMA)
 LIBS = [a for a in sys.argv[1:] if a.endswith(".so")]
-if LIBS:  # an alternate build of libilqr_hip.so (tools/fw_alt.sh)
+if LIBS:  # an alternate build of libilqr_hip.so (tools/archive/fw_alt.sh)
     _lib._lib = _lib.load(LIBS[0])
     print("library:", LIBS[0])
 

@@ -1,7 +1,7 @@
 #!/bin/bash
 # A/B of whole-library builds on the GPU box (timing only): runs <cmd> with the product
 # library, then with each tools/fwalt/libilqr_hip_<name>.so copied over it, twice.
-#   tools/gpu_libab.sh "<cmd>" <name>...
+#   tools/archive/gpu_libab.sh "<cmd>" <name>...
 set -o pipefail
 cd "$(dirname "$0")/.."
 CMD=$1; shift

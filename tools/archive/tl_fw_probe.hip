@@ -1,11 +1,11 @@
 // (Round 3: the ABL bits / -DILQR_* switches this probe uses exist only in the tree
-// tools/ablation/restore_tree.sh restores; build it there.)
+// tools/archive/ablation/restore_tree.sh restores; build it there.)
 // Probe: the 2-link forward kernel (ilqr_twolink.hip) at BASELINE config 2's size,
 // B = 1024, T = 50 (argv: B T), for the build variants of the rollout
 // (-DILQR_TL_RK4_SHIFT=0/1, -DILQR_FW_GROUP_PF), the line-search lanes per trajectory L and
 // the waves per workgroup W, with one accepted trial (prev_cost = +Inf) and with a
 // four-trial search (prev_cost = −Inf, max_trials = 4: exhausted after trial 4). Prints
-// one JSON line per NU. Build: tools/tl_fw_probe.sh.
+// one JSON line per NU. Build: tools/archive/tl_fw_probe.sh.
 #include "../ilqr.jl_amd/csrc/ilqr_twolink.hip"
 
 #include <cstdio>

@@ -1,7 +1,7 @@
 #!/bin/bash
 # (Round 3: the -DILQR_* switches below exist only in the restored tree: run this from
-# the directory tools/ablation/restore_tree.sh makes.)
-# Builds tools/tl_fw_probe.hip in its variants into tools/tl_fw_probe_<variant>:
+# the directory tools/archive/ablation/restore_tree.sh makes.)
+# Builds tools/archive/tl_fw_probe.hip in its variants into tools/tl_fw_probe_<variant>:
 # s = rollout RK4 (ILQR_TL_RK4_SHIFT), p = prefetch depth (ILQR_FW_GROUP_PF).
 # Run on the CPU; the binaries travel to the GPU box.
 set -e

@@ -12,7 +12,7 @@
 // step for C = 1, 2, 4 — if C = 2 costs ≈ C = 1, the chain is latency-bound and two
 // rollouts per lane are nearly free; if ≈ 2×, the wave is issue-bound and ILP buys
 // nothing. Also times the product forward kernel (tl_forward_kernel<1, 4, 1>) at B = 1024,
-// T = 50 for the per-step figure of the real pass. Build: tools/tl_ilp_probe.sh.
+// T = 50 for the per-step figure of the real pass. Build: tools/archive/tl_ilp_probe.sh.
 #include "../ilqr.jl_amd/csrc/ilqr_twolink.hip"
 
 #include <cstdio>

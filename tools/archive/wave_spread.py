@@ -1,6 +1,6 @@
 """Per-wave timing of the fused iteration kernel in the headline fit (B = 4096, T = 100),
-from the instrumented build (tools/ablation/build_trace_lib.sh
-tools/ablation/wave_start_trace.patch): every wave records its start (with its hardware
+from the instrumented build (tools/archive/ablation/build_trace_lib.sh
+tools/archive/ablation/wave_start_trace.patch): every wave records its start (with its hardware
 slot: HW_ID, XCC_ID) and the end of its own work (backward + forward), s_memrealtime
 ticks (100 MHz). Question: is the spread of the waves' finishing times (the launch's
 ramp-down) the same waves every launch (placement: XCD, CU) or random — only the latter

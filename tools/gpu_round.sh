@@ -8,7 +8,7 @@
 #   make -C /tmp/prev/ilqr.jl_amd/csrc ../lib/libilqr_hip.so &&
 #   cp /tmp/prev/ilqr.jl_amd/lib/libilqr_hip.so ilqr.jl_amd/lib/variants/libilqr_hip_prev.so
 # (chainab names it libilqr_hip_prevchain.so); spread and tail5 need the instrumented
-# build of tools/ablation/build_trace_lib.sh.
+# build of tools/archive/ablation/build_trace_lib.sh.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -35,7 +35,7 @@ case $WHAT in
   cfg) step pytest_cfg 400 python -u -m pytest tests/test_gpu_configs.py -m gpu -x -v -s --timeout 200 --timeout-method thread ;;
   smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
   prof) step rocprof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 50 --warmup 300 --no-cpu --no-secondary ;;
-  ablate) step ablate 120 ./tools/ablate_bw ;;
+  ablate) step ablate 120 ./tools/archive/ablate_bw ;;
   dist2) ILQR_DIST_BACKEND=gloo step dist2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 2 --steps 5 --warmup 1 --no-cpu ;;
   pmc) step pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- python bench.py --steps 5 --warmup 1 --no-cpu --no-secondary
        step pmc_write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run -- python bench.py --steps 5 --warmup 1 --no-cpu --no-secondary
@@ -54,8 +54,8 @@ case $WHAT in
   tailcap) MODES=coop MAXT=16 step tail_cap16 200 python tools/tail_probe.py
            MODES=coop MAXT=32 step tail_cap32 200 python tools/tail_probe.py
            MODES=coop MAXT=64 step tail_cap64 200 python tools/tail_probe.py ;;
-  ubench) step ubench 120 ./tools/ubench_f64 ;;
-  ilp) step tl_ilp 120 ./tools/tl_ilp_probe ;;
+  ubench) step ubench 120 ./tools/archive/ubench_f64 ;;
+  ilp) step tl_ilp 120 ./tools/archive/tl_ilp_probe ;;
   waitab) for i in 1 2; do
             ILQR_FIT_WAIT=sync step bench_wait_sync_$i 300 python bench.py --no-cpu --no-secondary
             step bench_wait_spin_$i 300 python bench.py --no-cpu --no-secondary
@@ -69,7 +69,7 @@ case $WHAT in
                  ILQR_GATHER_WG=$wg step trace_wg$wg 200 rocprofv3 --kernel-trace -d gpurun_out/trace_wg$wg -o run --output-format csv -- python tools/ab_fit.py
                  python tools/trace_fit_gaps.py gpurun_out/trace_wg$wg/run_kernel_trace.csv > gpurun_out/trace_fit_gaps_wg$wg.txt 2>&1
                done ;;
-  spread) step wave_spread 200 python tools/wave_spread.py ;;
+  spread) step wave_spread 200 python tools/archive/wave_spread.py ;;
   chainab) for i in 1 2; do
              ILQR_LIB=ilqr.jl_amd/lib/variants/libilqr_hip_prevchain.so step rbd_prev_$i 200 python tools/ab_lib.py tools/bench_rbd.py --lin fd --no-cpu --steps 50 --warmup 50
              step rbd_new_$i 200 python tools/bench_rbd.py --lin fd --no-cpu --steps 50 --warmup 50
@@ -80,7 +80,7 @@ case $WHAT in
               MODES=coop step tail_new_$i 200 python tools/tail_probe.py
             done
             grep -h "coop \|per iteration" gpurun_out/tail_prev_*.log gpurun_out/tail_new_*.log > gpurun_out/vanish_ab.log; cat gpurun_out/vanish_ab.log ;;
-  tail5) step coop_tail 200 python tools/coop_tail_analysis.py ;;
+  tail5) step coop_tail 200 python tools/archive/coop_tail_analysis.py ;;
   headab) for i in 1 2; do
             ILQR_LIB=ilqr.jl_amd/lib/variants/libilqr_hip_prev.so step ab_fit_prev_$i 120 python tools/ab_fit.py
             step ab_fit_new_$i 120 python tools/ab_fit.py
