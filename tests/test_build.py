@@ -15,7 +15,7 @@ from concurrent.futures import ThreadPoolExecutor
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-PATCH = os.path.join(ROOT, "tools", "ablation", "restore_alternates.patch")
+PATCH = os.path.join(ROOT, "tools", "archive", "ablation", "restore_alternates.patch")
 HIPCC = "/opt/rocm/bin/hipcc"
 
 
