@@ -322,23 +322,25 @@ __device__ bool tiles_backward_wide_wave(const TileParams& P, int b, int T, int 
   for (int t = T - 1; t >= 0; --t) {
     load(t > 0 ? t - 1 : 0, nxt);  // prefetch
 
-    d4 YA = {0.0, 0.0, 0.0, 0.0};
-    d4 YB;
+    // every product as two independent 2-MFMA chains summed by the VALU: the step is a
+    // latency chain at small batch (the reference's caller fits ONE trajectory) and a
+    // dependent v_mfma_f64_16x16x4 accumulation costs its full latency per link
+    const d4 z4 = {0.0, 0.0, 0.0, 0.0};
+    d4 YB0;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) YB[r] = c8 ? Sx[r] : 0.0;
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk) {
-      YA = mfma(S[kk], cur.fA[kk], YA);
-      YB = mfma(S[kk], cur.fB[kk], YB);
-    }
-    d4 Zxx = cur.Lxx, Zxe = cur.Lxe, Zux = cur.Lux, Zue = cur.Lue;
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk) {
-      Zxx = mfma(cur.fA[kk], YA[kk], Zxx);
-      Zxe = mfma(cur.fA[kk], YB[kk], Zxe);
-      Zux = mfma(cur.fB[kk], YA[kk], Zux);
-      Zue = mfma(cur.fB[kk], YB[kk], Zue);
-    }
+    for (int r = 0; r < 4; ++r) YB0[r] = c8 ? Sx[r] : 0.0;
+    const d4 YA = mfma(S[1], cur.fA[1], mfma(S[0], cur.fA[0], z4)) + mfma(S[3], cur.fA[3], mfma(S[2], cur.fA[2], z4));
+    const d4 YB = mfma(S[1], cur.fB[1], mfma(S[0], cur.fB[0], YB0)) + mfma(S[3], cur.fB[3], mfma(S[2], cur.fB[2], z4));
+    // G and [H | g] first: the hand-off and the factorisation wait for them, the Z_xx and
+    // Z_xe chains run in the MFMA pipe meanwhile
+    const d4 Zux = mfma(cur.fB[1], YA[1], mfma(cur.fB[0], YA[0], cur.Lux)) +
+                   mfma(cur.fB[3], YA[3], mfma(cur.fB[2], YA[2], z4));
+    const d4 Zue = mfma(cur.fB[1], YB[1], mfma(cur.fB[0], YB[0], cur.Lue)) +
+                   mfma(cur.fB[3], YB[3], mfma(cur.fB[2], YB[2], z4));
+    const d4 Zxx = mfma(cur.fA[1], YA[1], mfma(cur.fA[0], YA[0], cur.Lxx)) +
+                   mfma(cur.fA[3], YA[3], mfma(cur.fA[2], YA[2], z4));
+    const d4 Zxe = mfma(cur.fA[1], YB[1], mfma(cur.fA[0], YB[0], cur.Lxe)) +
+                   mfma(cur.fA[3], YB[3], mfma(cur.fA[2], YB[2], z4));
 
     // hand-off: G (rows q, q+4) and [H | g] (rows q, q+4)
     Gl[q * 16 + c] = Zux[0];
@@ -360,7 +362,7 @@ __device__ bool tiles_backward_wide_wave(const TileParams& P, int b, int T, int 
     wave_lds_fence();
 
     // feedback_parameters (:207-218): (H + μI) x = [G[:, c] | g]
-    LDLT<TW_NU> f;
+    LDLT<TW_NU, 1> f;  // one Newton step on each pivot's v_rcp_f64 (11 ulp)
     f.factor(h, mu);
     f.solve_n(xs);
     f.solve_n(xd);

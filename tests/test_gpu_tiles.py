@@ -297,3 +297,38 @@ def test_closure_path_reuses_one_handle_and_is_thread_safe(gpu):
     assert len(created) <= 3 and cache.size() == 1
     api.clear_cache()
     assert cache.size() == 0
+
+
+def test_tiles_wide_zero_input_equals_narrow(gpu):
+    """A (12, 4) problem with a fifth, zero input column runs on the wide kernel: its
+    gains for the four real inputs equal the narrow kernel's (other summation order:
+    rel 1e-12) and the fifth input's gains are exactly zero (H₅₅ + μ = μ, g₅ = G₅ = 0)."""
+    nb, T, n, m = 5, 60, 12, 4   # ragged: the last workgroup holds one trajectory
+    tl = random_tiles(nb, T, n, m, seed=77)
+    s4 = Solver(n, m, T, nb, kind=_lib.PROBLEM_TILES)
+    d4, K4, st4 = s4.backward_tiles(to_dev(tl))
+    pad = dict(tl)
+    pad["B"] = np.concatenate([tl["B"], np.zeros((nb, T, n, 1))], axis=3)
+    pad["lu"] = np.concatenate([tl["lu"], np.zeros((nb, T, 1))], axis=2)
+    pad["lux"] = np.concatenate([tl["lux"], np.zeros((nb, T, 1, n))], axis=2)
+    luu = np.zeros((nb, T, m + 1, m + 1))
+    luu[:, :, :m, :m] = tl["luu"]
+    pad["luu"] = luu
+    s5 = Solver(n, m + 1, T, nb, kind=_lib.PROBLEM_TILES)
+    d5, K5, st5 = s5.backward_tiles(to_dev(pad))
+    assert (st4.cpu().numpy() == 0).all() and (st5.cpu().numpy() == 0).all()
+    assert rel(d5[..., :m], d4) < 1e-12 and rel(K5[:, :, :m], K4) < 1e-12
+    assert (d5[..., m] == 0).all() and (K5[:, :, m] == 0).all()
+    s4.close()
+    s5.close()
+
+
+def test_tiles_wide_single_step(gpu):
+    """T = 1: the terminal value function and one step (the prefetch clamps at t = 0)."""
+    nb, T, n, m = 3, 1, 16, 8
+    tl = random_tiles(nb, T, n, m, seed=91)
+    s = Solver(n, m, T, nb, kind=_lib.PROBLEM_TILES)
+    d, K, st = s.backward_tiles(to_dev(tl))
+    dr, Kr, _ = cref.tiles_backward(tl, symmetrize=True)
+    assert (st.cpu().numpy() == 0).all() and rel(d, dr) < 1e-12 and rel(K, Kr) < 1e-12
+    s.close()
