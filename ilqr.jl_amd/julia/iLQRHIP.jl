@@ -697,7 +697,9 @@ const MAX_CACHED = 8
 
 function evict_idle!(cache::Dict)
     for (k, c) in cache
-        if trylock(c.lock)
+        # not one in use (islocked: by any task — trylock alone would succeed on a lock
+        # this task already holds, the lock being reentrant)
+        if !islocked(c.lock) && trylock(c.lock)
             try
                 close(c.h)
             finally
