@@ -196,6 +196,16 @@ def secondary_configs(device):
                 out[name]["fit_default_mean_iterations"] = r["fit"]["fit_default"]["mean_iterations"]
         except Exception as e:  # reported, never required
             out[name] = {"error": repr(e)}
+    # row f3: the tiles backward of arbitrary closures at the reference RBD caller's shape
+    # (nx = 16, nu = 8; animate_RBD_2_link.jl fits ONE trajectory at T = 1000: a latency
+    # chain) and at a chip-filling batch (HBM-bound: GB/s against the 8 TB/s spec)
+    from tools import bench_tiles
+    for name, args in (("tiles_wide_rbd_caller_B1_T1000", (16, 8, 1, 1000)),
+                       ("tiles_wide_B4096_T100", (16, 8, 4096, 100))):
+        try:
+            out[name] = bench_tiles.measure(*args, reps=20, device=device)
+        except Exception as e:  # reported, never required
+            out[name] = {"error": repr(e)}
     return out
 
 
