@@ -123,3 +123,37 @@ def test_closure_fit_oracle_matches_per_trajectory_oracle():
         assert int(r["iters"][b]) == len(h)
         assert [int(v) for v in r["history"]["trials"][:len(h), b]] == [e["trials"] for e in h]
         assert rel(r["x"][b], xo) < 1e-9 and rel(r["u"][b], uo) < 1e-9
+
+
+def test_jet_matches_dual_forward_mode():
+    """oracle.jet (array-valued forward mode) against oracle.dual (the ForwardDiff
+    restatement, scalar duals) on the same closure written both ways: the Jacobians of
+    linearize_dynamics (src/backward_pass.jl:32-33) agree to rounding."""
+    from oracle import dual
+    fa, _, _ = coupled_pendula_arr(jet_ns())
+    fd, _, _ = coupled_pendula(oracle_ns())
+    rng = np.random.default_rng(5)
+    x, u = rng.uniform(-1, 1, (6, 4)), rng.standard_normal((6, 2))
+    A, B = jet.jacobians(fa, x, u)
+    for p in range(6):
+        Ad = dual.jacobian(lambda z: fd(z, u[p]), x[p])
+        Bd = dual.jacobian(lambda v: fd(x[p], v), u[p])
+        assert rel(A[p], Ad) < 1e-15 and rel(B[p], Bd) < 1e-15
+
+
+def test_jet_elementary_rules():
+    """solve / matmul / cat / tr / division on Jets against central differences."""
+    rng = np.random.default_rng(6)
+    M0 = rng.standard_normal((3, 4, 4)) + 4 * np.eye(4)
+    b0 = rng.standard_normal((3, 4))
+
+    def g(x):  # x (P, 4) → (P, 4): a mix of every Jet operation the closures use
+        M = M0 + jet.tr(x[..., :, None] * x[..., None, :]) * 0.1
+        y = jet.solve(M, b0 + x)
+        z = jet.cat([y[..., :2] / (2.0 + x[..., 2:3] * x[..., 2:3]), jet.sin(y[..., 2:]) - jet.cos(x[..., :2])])
+        return (M @ z[..., None])[..., 0] * 0.5
+    x = rng.standard_normal((3, 4))
+    J, _ = jet.jacobians(lambda a, _u: g(a), x, np.zeros((3, 1)))
+    h = 1e-6
+    Jfd = np.stack([(g(x + h * e) - g(x - h * e)) / (2 * h) for e in np.eye(4)], axis=-1)
+    assert rel(J, Jfd) < 1e-8
