@@ -75,3 +75,23 @@ def test_headline_kernels_have_no_waterfall_loops_or_scratch(tmp_path):
         body = funcs[n]
         assert not _waterfalls(body), f"{n}: waterfall loop(s) at {_waterfalls(body)}"
         assert not [x for x in body if x.startswith("scratch_")], f"{n}: scratch accesses"
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC) and shutil.which("hipcc") is None, reason="no hipcc")
+def test_tiles_kernels_have_no_scratch(tmp_path):
+    """The tiles backward (row f3): the wide kernel (nx ≤ 16, nu ≤ 8, run-time shapes,
+    256 VGPRs + AGPRs at one wave per SIMD) and every narrow instantiation keep their
+    prefetched tiles, LDLᵀ factors and dynamically selected solution entries in
+    registers — a dynamically indexed register array (the first draft's g vector) or a
+    spill would be a scratch access per step."""
+    hipcc = HIPCC if os.path.exists(HIPCC) else shutil.which("hipcc")
+    cmd = [hipcc, "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-save-temps", "-c",
+           os.path.join(CSRC, "ilqr_tiles.hip"), "-o", str(tmp_path / "tiles.o")]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=900, cwd=tmp_path)
+    assert r.returncode == 0, r.stderr[-2000:]
+    asm_file = [f for f in os.listdir(tmp_path) if f.endswith("gfx950.s")]
+    funcs = _functions(open(tmp_path / asm_file[0]).read())
+    kernels = [n for n in funcs if "tiles_backward" in n and "kernel" in n]
+    assert any("wide" in n for n in kernels) and len(kernels) >= 49, len(kernels)
+    for n in kernels:
+        assert not [x for x in funcs[n] if x.startswith("scratch_")], f"{n}: scratch accesses"
