@@ -122,28 +122,12 @@ __device__ bool tiles_backward_wave(const TileParams& P, int b, int T, double* _
   for (int t = T - 1; t >= 0; --t) {
     load(t > 0 ? t - 1 : 0, nxt);  // prefetch
 
-    // each product as two independent MFMA chains (even / odd k-blocks) summed by the
-    // VALU: a dependent v_mfma_f64_16x16x4 accumulation costs its full latency per link,
-    // and at small batch the step is that latency chain
-    const d4 z4 = {0.0, 0.0, 0.0, 0.0};
-    d4 Y0 = z4, Y1 = z4;
+    d4 Y = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-    for (int kk = 0; kk < KS; ++kk) {
-      if (kk & 1)
-        Y1 = mfma(Sp[kk], cur.fB[kk], Y1);
-      else
-        Y0 = mfma(Sp[kk], cur.fB[kk], Y0);
-    }
-    const d4 Y = KS > 1 ? Y0 + Y1 : Y0;
-    d4 Z0 = cur.Lc, Z1 = z4;  // Z = L + FᵀY: [[lxx + AᵀSA, ·], [lux + BᵀSA, luu + BᵀSB]] (:182-183)
+    for (int kk = 0; kk < KS; ++kk) Y = mfma(Sp[kk], cur.fB[kk], Y);
+    d4 Z = cur.Lc;  // Z = L + FᵀY: [[lxx + AᵀSA, ·], [lux + BᵀSA, luu + BᵀSB]] (:182-183)
 #pragma unroll
-    for (int kk = 0; kk < KS; ++kk) {
-      if (kk & 1)
-        Z1 = mfma(cur.fB[kk], Y[kk], Z1);
-      else
-        Z0 = mfma(cur.fB[kk], Y[kk], Z0);
-    }
-    const d4 Z = KS > 1 ? Z0 + Z1 : Z0;
+    for (int kk = 0; kk < KS; ++kk) Z = mfma(cur.fB[kk], Y[kk], Z);
 
     // gq[c] = [lx; lu][c] + (Fᵀ s)[c]: lx + Aᵀs (c < NX), g = lu + Bᵀs (:181, :269)
     double part = (q == 0) ? cur.lv : 0.0;
@@ -333,14 +317,10 @@ __device__ bool tiles_backward_wide_wave(const TileParams& P, int b, int T, int 
   bool nan = false;
   double* Kb = K_out + bt * nu * nx;
   double* db = d_out + bt * nu;
-  // tiles prefetched TW_PF steps ahead in registers (a wave alone on its SIMD has the
-  // register file to itself): at a full chip every wave's loads are in flight while it
-  // computes, at small batch they hide the HBM latency under the step's chain
-  WideTile cur, nxt, nx2;
+  WideTile cur, nxt;
   load(T - 1, cur);
-  load(T > 1 ? T - 2 : 0, nxt);
   for (int t = T - 1; t >= 0; --t) {
-    load(t > 1 ? t - 2 : 0, nx2);  // prefetch
+    load(t > 0 ? t - 1 : 0, nxt);  // prefetch
 
     // every product as two independent 2-MFMA chains summed by the VALU: the step is a
     // latency chain at small batch (the reference's caller fits ONE trajectory) and a
@@ -405,7 +385,6 @@ __device__ bool tiles_backward_wide_wave(const TileParams& P, int b, int T, int 
     S = mfma(a1, w1, mfma(a0, w0, Zxx));
     Sx = mfma(a1, v1, mfma(a0, v0, Zxe));
     cur = nxt;
-    nxt = nx2;
 
     if ((t % TB_SYM_EVERY) == 0) {
 #pragma unroll
