@@ -17,9 +17,22 @@ the reference's eltype-generic Julia closures:
 
 `rollout_forward` is forward_pass (src/forward_pass.jl:55-93) for such closures:
 the rollout calls the user's dynamics, so it runs as torch ops on the device
-(batched over trajectories, sequential over time), not in a HIP kernel.
+(batched over trajectories, sequential over time), not in a HIP kernel. One step of it
+(control law :72-73 + dynamics :74) is captured once per (closure, shape) in a HIP
+graph and replayed T times per line-search trial: a closure of a few hundred small ops
+(the reference's RBD caller) then costs one graph launch per step instead of a few
+hundred dispatches (tools/rollout_probe.py: 4.0 → 0.73 ms per step at nx = 16, B = 1).
+The capture is checked against an eager step bit for bit before it is used; closures
+that cannot be captured (a host synchronisation inside them) run eagerly.
+ILQR_ROLLOUT_GRAPH=0 turns the graphs off.
 """
 from __future__ import annotations
+
+import contextlib
+import ctypes
+import os
+import threading
+import weakref
 
 import torch
 
@@ -71,6 +84,152 @@ def total_cost(xb, ub, x_traj, immediate_cost, final_cost):
     return acc + vmap(final_cost)(xb[:, T])
 
 
+ROLLOUT_GRAPHS = os.environ.get("ILQR_ROLLOUT_GRAPH", "1") != "0"
+MAX_GRAPHS_PER_CLOSURE = 4
+_GRAPHS: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()  # dynamicsf → {shape: graph}
+_GRAPHS_LOCK = threading.Lock()
+_CAPTURE_LOCK = threading.Lock()
+
+
+@contextlib.contextmanager
+def _capturable_linalg():
+    """torch.linalg.solve / inv check their LAPACK info on the host, which a capture
+    forbids; inside the capture they run as solve_ex / inv_ex (the same kernels without
+    the check: a singular system then gives non-finite states, reported as a NaN
+    trajectory, where the eager call raises)."""
+    solve, inv = torch.linalg.solve, torch.linalg.inv
+    torch.linalg.solve = lambda A, B, *, left=True, out=None: torch.linalg.solve_ex(A, B, left=left)[0]
+    torch.linalg.inv = lambda A, *, out=None: torch.linalg.inv_ex(A)[0]
+    try:
+        yield
+    finally:
+        torch.linalg.solve, torch.linalg.inv = solve, inv
+
+
+class _RolloutGraph:
+    """forward_pass's step (:72-74) on static buffers, the step index on the device:
+    XB[:, k+1] = f(XB[:, k], U[:, k] + α·D[:, k] + K[:, k]·(XB[:, k] − X[:, k]))."""
+
+    def __init__(self, f, x, u):
+        dev = x.device
+        nb, N, nx = x.shape
+        nu = u.shape[2]
+        self.f = f
+        self.X, self.U = torch.empty_like(x), torch.empty_like(u)
+        self.D = torch.empty_like(u)
+        self.K = torch.empty((nb, N - 1, nu, nx), dtype=x.dtype, device=dev)
+        self.alpha = torch.empty(nb, dtype=torch.float64, device=dev)
+        self.XB, self.UB = torch.empty_like(x), torch.empty_like(u)
+        self.k = torch.zeros(1, dtype=torch.long, device=dev)
+        self.graph = None
+        self.lock = threading.Lock()
+
+    def step(self):
+        k = self.k
+        k1 = k + 1
+        xk = self.XB.index_select(1, k).squeeze(1)
+        dx = xk - self.X.index_select(1, k).squeeze(1)                              # :72
+        uk = (self.U.index_select(1, k).squeeze(1) + self.alpha[:, None] * self.D.index_select(1, k).squeeze(1)) \
+            + torch.einsum("bij,bj->bi", self.K.index_select(1, k).squeeze(1), dx)  # :73
+        xn = self.f(xk, uk)                                                         # :74
+        self.UB.index_copy_(1, k, uk.unsqueeze(1))
+        self.XB.index_copy_(1, k1, xn.unsqueeze(1))
+        self.k.add_(1)
+
+    def load(self, x, u, d, K):
+        for dst, src in ((self.X, x), (self.U, u), (self.D, d), (self.K, K)):
+            dst.copy_(src)
+
+    def start(self, alpha):
+        self.alpha.copy_(alpha)
+        self.XB[:, 0] = self.X[:, 0]                                                # :65
+        self.k.zero_()
+
+    def capture(self):
+        """Warm up on a side stream, capture, then replay step 0 and compare it with an
+        eager step 0 bit for bit. → True when the graph can be used."""
+        self.start(torch.ones_like(self.alpha))
+        side = torch.cuda.Stream(device=self.X.device)
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(2):
+                self.k.zero_()
+                self.step()
+        torch.cuda.current_stream().wait_stream(side)
+        self.start(torch.ones_like(self.alpha))
+        self.step()                                                                 # the eager reference
+        want_x, want_u = self.XB[:, 1].clone(), self.UB[:, 0].clone()
+        g = torch.cuda.CUDAGraph()
+        self.start(torch.ones_like(self.alpha))
+        torch.cuda.synchronize()
+        # begin/end by hand rather than torch.cuda.graph: a failed capture must still end
+        # it and restore this thread's stream (the context manager skips both when
+        # capture_end raises), then clear the runtime's last error before eager work
+        with _CAPTURE_LOCK, _capturable_linalg(), torch.cuda.stream(side):
+            g.capture_begin(capture_error_mode="thread_local")
+            try:
+                self.step()
+            finally:
+                try:
+                    g.capture_end()
+                except Exception:
+                    _clear_hip_error()
+                    raise
+        torch.cuda.synchronize()
+        self.start(torch.ones_like(self.alpha))
+        g.replay()
+        ok = bool(torch.equal(self.XB[:, 1], want_x)) and bool(torch.equal(self.UB[:, 0], want_u)) \
+            and int(self.k.item()) == 1
+        self.graph = g if ok else None
+        return ok
+
+
+def _clear_hip_error():
+    """Reset the HIP runtime's per-thread last error that an invalidated capture leaves
+    (torch reports it at the next kernel launch otherwise)."""
+    try:
+        hip = ctypes.CDLL("libamdhip64.so.7")  # the runtime torch already loaded (same soname)
+        hip.hipGetLastError()
+    except OSError:
+        pass
+
+
+def _rollout_graph(dynamicsf, f, x, u):
+    """The cached captured step for (dynamicsf, shape), capturing on first use; None
+    when graphs are off, the closure cannot be cached or captured."""
+    if not (ROLLOUT_GRAPHS and x.is_cuda):
+        return None
+    key = (tuple(x.shape), tuple(u.shape), x.dtype, x.device.index)
+    try:
+        with _GRAPHS_LOCK:
+            per = _GRAPHS.setdefault(dynamicsf, {})
+            g = per.get(key)
+            if g is None:
+                if len(per) >= MAX_GRAPHS_PER_CLOSURE:
+                    per.pop(next(iter(per)))
+                g = per[key] = _RolloutGraph(f, x, u)
+    except TypeError:  # not weak-referenceable
+        return None
+    return g or None  # False: this closure failed to capture at this shape
+
+
+def _mark_uncapturable(dynamicsf, x, u):
+    key = (tuple(x.shape), tuple(u.shape), x.dtype, x.device.index)
+    with _GRAPHS_LOCK:
+        _GRAPHS.setdefault(dynamicsf, {})[key] = False
+
+
+def _rollout_eager(f, x, u, d, K, alpha):
+    xb = torch.empty_like(x)
+    ub = torch.empty_like(u)
+    xb[:, 0] = x[:, 0]                                                          # :65
+    for k in range(x.shape[1] - 1):                                             # :71
+        dx = xb[:, k] - x[:, k]                                                 # :72
+        ub[:, k] = (u[:, k] + alpha[:, None] * d[:, k]) + torch.einsum("bij,bj->bi", K[:, k], dx)  # :73
+        xb[:, k + 1] = f(xb[:, k], ub[:, k])                                    # :74
+    return xb, ub
+
+
 def rollout_forward(x, u, x_traj, d, K, prev_cost, dynamicsf, immediate_cost, final_cost,
                     max_trials=64, alpha0=1.0, shrink=0.5):
     """forward_pass (src/forward_pass.jl:55-93) for torch closures, batched over
@@ -79,19 +238,42 @@ def rollout_forward(x, u, x_traj, d, K, prev_cost, dynamicsf, immediate_cost, fi
     f = vmap(dynamicsf)
     nb, N, nx = x.shape
     T = N - 1
+    g = _rollout_graph(dynamicsf, f, x, u)
+    if g is None:
+        return _line_search(x, u, x_traj, prev_cost, immediate_cost, final_cost, max_trials, alpha0, shrink,
+                            lambda alpha: _rollout_eager(f, x, u, d, K, alpha))
+    with g.lock:
+        g.load(x, u, d, K)
+        if g.graph is None:
+            try:
+                g.capture()
+            except Exception:  # a host synchronisation (or another capture error) in the closure
+                g.graph = None
+                _clear_hip_error()
+                torch.cuda.synchronize()
+            if g.graph is None:
+                _mark_uncapturable(dynamicsf, x, u)
+                return _line_search(x, u, x_traj, prev_cost, immediate_cost, final_cost, max_trials, alpha0,
+                                    shrink, lambda alpha: _rollout_eager(f, x, u, d, K, alpha))
+
+        def graphed(alpha):
+            g.start(alpha)
+            for _ in range(T):
+                g.graph.replay()
+            return g.XB.clone(), g.UB.clone()
+        return _line_search(x, u, x_traj, prev_cost, immediate_cost, final_cost, max_trials, alpha0, shrink,
+                            graphed)
+
+
+def _line_search(x, u, x_traj, prev_cost, immediate_cost, final_cost, max_trials, alpha0, shrink, rollout):
+    nb = x.shape[0]
     xo, uo = x.clone(), u.clone()
     cost = torch.full((nb,), float("nan"), dtype=torch.float64, device=x.device)
     trials = torch.zeros(nb, dtype=torch.int32, device=x.device)
     done = torch.zeros(nb, dtype=torch.bool, device=x.device)
     alpha = torch.full((nb,), float(alpha0), dtype=torch.float64, device=x.device)
     for trial in range(1, max_trials + 1):
-        xb = torch.empty_like(x)
-        ub = torch.empty_like(u)
-        xb[:, 0] = x[:, 0]                                                      # :65
-        for k in range(T):                                                      # :71
-            dx = xb[:, k] - x[:, k]                                             # :72
-            ub[:, k] = (u[:, k] + alpha[:, None] * d[:, k]) + torch.einsum("bij,bj->bi", K[:, k], dx)  # :73
-            xb[:, k + 1] = f(xb[:, k], ub[:, k])                                # :74
+        xb, ub = rollout(alpha)                                                 # :65-75
         c = total_cost(xb, ub, x_traj, immediate_cost, final_cost)              # :76
         acc = (~done) & ((prev_cost - c) > 0)                                   # :77-80
         sel = acc | ~done

@@ -157,3 +157,29 @@ def test_jet_elementary_rules():
     h = 1e-6
     Jfd = np.stack([(g(x + h * e) - g(x - h * e)) / (2 * h) for e in np.eye(4)], axis=-1)
     assert rel(J, Jfd) < 1e-8
+
+
+def test_rollout_graph_bookkeeping_on_cpu():
+    """The capture-time linalg swap restores torch.linalg exactly; CPU tensors and
+    ILQR_ROLLOUT_GRAPH=0 never build a graph (the product path is the device)."""
+    import torch
+    from ilqr_amd import tiles
+    solve, inv = torch.linalg.solve, torch.linalg.inv
+    A = torch.tensor([[2.0, 1.0], [1.0, 3.0]], dtype=torch.float64)
+    b = torch.tensor([[1.0], [2.0]], dtype=torch.float64)
+    with tiles._capturable_linalg():
+        assert torch.linalg.solve is not solve
+        assert torch.equal(torch.linalg.solve(A, b), solve(A, b))
+        assert torch.equal(torch.linalg.inv(A), inv(A))
+        # a singular system: no host-side check, non-finite values instead of an exception
+        assert not torch.isfinite(torch.linalg.solve(torch.zeros(2, 2, dtype=torch.float64), b)).all()
+    assert torch.linalg.solve is solve and torch.linalg.inv is inv
+    with pytest.raises(RuntimeError):
+        with tiles._capturable_linalg():
+            raise RuntimeError("capture failed")
+    assert torch.linalg.solve is solve and torch.linalg.inv is inv
+    x = torch.zeros(1, 3, 2, dtype=torch.float64)
+    u = torch.zeros(1, 2, 1, dtype=torch.float64)
+    f = lambda a, v: a  # noqa: E731
+    assert tiles._rollout_graph(f, f, x, u) is None
+    assert f not in tiles._GRAPHS

@@ -332,3 +332,58 @@ def test_tiles_wide_single_step(gpu):
     dr, Kr, _ = cref.tiles_backward(tl, symmetrize=True)
     assert (st.cpu().numpy() == 0).all() and rel(d, dr) < 1e-12 and rel(K, Kr) < 1e-12
     s.close()
+
+
+def test_rollout_graph_matches_eager_rbd(gpu):
+    """The HIP-graph rollout (one captured forward_pass step replayed T times; the
+    reference RBD caller's closure calls torch.linalg.solve, captured as solve_ex) gives
+    the eager rollout's trajectories and line-search outcome, and is cached per closure."""
+    from closures import rbd_floating_arm, torch_arr_ns
+    from ilqr_amd import tiles
+    nb, T = 2, 60
+    x, u = rbd_batch(nb, T)
+    f, l, lf = rbd_floating_arm(torch_arr_ns())
+    xb, ub = torch.from_numpy(x).cuda(), torch.from_numpy(u).cuda()
+    tl = derivative_tiles(xb, ub, f, l, lf)
+    s = Solver(16, 8, T, nb, kind=_lib.PROBLEM_TILES)
+    try:
+        d, K, _ = s.backward_tiles(tl)
+    finally:
+        s.close()
+    prev = torch.full((nb,), float("inf"), dtype=torch.float64, device="cuda")
+    xt = torch.zeros_like(xb)
+    old = tiles.ROLLOUT_GRAPHS
+    try:
+        tiles.ROLLOUT_GRAPHS = False
+        e = tiles.rollout_forward(xb, ub, xt, d, K, prev, f, l, lf, 64)
+        tiles.ROLLOUT_GRAPHS = True
+        g = tiles.rollout_forward(xb, ub, xt, d, K, prev, f, l, lf, 64)
+        g2 = tiles.rollout_forward(xb, ub, xt, d, K, prev * 0.0, f, l, lf, 8)   # every trial rejected
+        tiles.ROLLOUT_GRAPHS = False
+        e2 = tiles.rollout_forward(xb, ub, xt, d, K, prev * 0.0, f, l, lf, 8)
+    finally:
+        tiles.ROLLOUT_GRAPHS = old
+    entry = tiles._GRAPHS[f][(tuple(xb.shape), tuple(ub.shape), xb.dtype, 0)]
+    assert entry and entry.graph is not None                     # captured, not the eager fallback
+    for a, b in ((g, e), (g2, e2)):
+        assert rel(a[0], b[0]) < 1e-12 and rel(a[1], b[1]) < 1e-12 and rel(a[2], b[2]) < 1e-12
+        assert a[3].tolist() == b[3].tolist() and a[4].tolist() == b[4].tolist()
+    assert g2[3].tolist() == [8, 8] and not bool(g2[4].any())
+
+
+def test_rollout_graph_falls_back_for_uncapturable_closure(gpu):
+    """A closure that synchronises with the host cannot be captured: the rollout runs
+    eagerly (still on the device) with the same result, and the closure is remembered."""
+    from ilqr_amd import tiles
+    ft = coupled_pendula(torch_ns())
+    f0 = ft[0]
+
+    def synced(x, u):
+        torch.cuda.synchronize()          # a host synchronisation inside the closure
+        return f0(x, u)
+    x, u = pendula_batch(2, 20, seed=5)
+    xf, uf = api.fit(torch.from_numpy(x).cuda(), torch.from_numpy(u).cuda(), f0, ft[1], ft[2], max_iter=5)
+    xs, us = api.fit(torch.from_numpy(x).cuda(), torch.from_numpy(u).cuda(), synced, ft[1], ft[2], max_iter=5)
+    assert rel(xs, xf) < 1e-12 and rel(us, uf) < 1e-12
+    assert list(tiles._GRAPHS[synced].values()) == [False]
+    assert tiles._GRAPHS[f0] and all(v and v.graph is not None for v in tiles._GRAPHS[f0].values())
