@@ -28,13 +28,13 @@ ILQR_ROLLOUT_GRAPH=0 turns the graphs off.
 """
 from __future__ import annotations
 
-import contextlib
 import ctypes
 import os
 import threading
 import weakref
 
 import torch
+from torch.overrides import TorchFunctionMode
 
 TILE_NAMES = ("A", "B", "lx", "lu", "lxx", "lux", "luu", "lfx", "lfxx")
 
@@ -91,30 +91,34 @@ _GRAPHS_LOCK = threading.Lock()
 _CAPTURE_LOCK = threading.Lock()
 
 
-@contextlib.contextmanager
-def _capturable_linalg():
+class _CapturableLinalg(TorchFunctionMode):
     """torch.linalg.solve / inv check their LAPACK info on the host, which a capture
     forbids; inside the capture they run as solve_ex / inv_ex (the same kernels without
     the check: a singular system then gives non-finite states, reported as a NaN
-    trajectory, where the eager call raises)."""
-    solve, inv = torch.linalg.solve, torch.linalg.inv
-    torch.linalg.solve = lambda A, B, *, left=True, out=None: torch.linalg.solve_ex(A, B, left=left)[0]
-    torch.linalg.inv = lambda A, *, out=None: torch.linalg.inv_ex(A)[0]
-    try:
-        yield
-    finally:
-        torch.linalg.solve, torch.linalg.inv = solve, inv
+    trajectory, where the eager call raises). A torch-function mode is per thread: other
+    threads' calls are untouched."""
+
+    def __torch_function__(self, func, types, args=(), kwargs=None):
+        kwargs = dict(kwargs or {})
+        if func is torch.linalg.solve and "out" not in kwargs:
+            return torch.linalg.solve_ex(*args, **kwargs)[0]
+        if func is torch.linalg.inv and "out" not in kwargs:
+            return torch.linalg.inv_ex(*args, **kwargs)[0]
+        return func(*args, **kwargs)
+
+
+def _capturable_linalg():
+    return _CapturableLinalg()
 
 
 class _RolloutGraph:
     """forward_pass's step (:72-74) on static buffers, the step index on the device:
     XB[:, k+1] = f(XB[:, k], U[:, k] + α·D[:, k] + K[:, k]·(XB[:, k] − X[:, k]))."""
 
-    def __init__(self, f, x, u):
+    def __init__(self, x, u):
         dev = x.device
         nb, N, nx = x.shape
         nu = u.shape[2]
-        self.f = f
         self.X, self.U = torch.empty_like(x), torch.empty_like(u)
         self.D = torch.empty_like(u)
         self.K = torch.empty((nb, N - 1, nu, nx), dtype=x.dtype, device=dev)
@@ -124,14 +128,14 @@ class _RolloutGraph:
         self.graph = None
         self.lock = threading.Lock()
 
-    def step(self):
+    def step(self, f):
         k = self.k
         k1 = k + 1
         xk = self.XB.index_select(1, k).squeeze(1)
         dx = xk - self.X.index_select(1, k).squeeze(1)                              # :72
         uk = (self.U.index_select(1, k).squeeze(1) + self.alpha[:, None] * self.D.index_select(1, k).squeeze(1)) \
             + torch.einsum("bij,bj->bi", self.K.index_select(1, k).squeeze(1), dx)  # :73
-        xn = self.f(xk, uk)                                                         # :74
+        xn = f(xk, uk)                                                              # :74
         self.UB.index_copy_(1, k, uk.unsqueeze(1))
         self.XB.index_copy_(1, k1, xn.unsqueeze(1))
         self.k.add_(1)
@@ -145,7 +149,7 @@ class _RolloutGraph:
         self.XB[:, 0] = self.X[:, 0]                                                # :65
         self.k.zero_()
 
-    def capture(self):
+    def capture(self, f):
         """Warm up on a side stream, capture, then replay step 0 and compare it with an
         eager step 0 bit for bit. → True when the graph can be used."""
         self.start(torch.ones_like(self.alpha))
@@ -154,10 +158,10 @@ class _RolloutGraph:
         with torch.cuda.stream(side):
             for _ in range(2):
                 self.k.zero_()
-                self.step()
+                self.step(f)
         torch.cuda.current_stream().wait_stream(side)
         self.start(torch.ones_like(self.alpha))
-        self.step()                                                                 # the eager reference
+        self.step(f)                                                                # the eager reference
         want_x, want_u = self.XB[:, 1].clone(), self.UB[:, 0].clone()
         g = torch.cuda.CUDAGraph()
         self.start(torch.ones_like(self.alpha))
@@ -168,7 +172,7 @@ class _RolloutGraph:
         with _CAPTURE_LOCK, _capturable_linalg(), torch.cuda.stream(side):
             g.capture_begin(capture_error_mode="thread_local")
             try:
-                self.step()
+                self.step(f)
             finally:
                 try:
                     g.capture_end()
@@ -194,7 +198,7 @@ def _clear_hip_error():
         pass
 
 
-def _rollout_graph(dynamicsf, f, x, u):
+def _rollout_graph(dynamicsf, x, u):
     """The cached captured step for (dynamicsf, shape), capturing on first use; None
     when graphs are off, the closure cannot be cached or captured."""
     if not (ROLLOUT_GRAPHS and x.is_cuda):
@@ -207,7 +211,7 @@ def _rollout_graph(dynamicsf, f, x, u):
             if g is None:
                 if len(per) >= MAX_GRAPHS_PER_CLOSURE:
                     per.pop(next(iter(per)))
-                g = per[key] = _RolloutGraph(f, x, u)
+                g = per[key] = _RolloutGraph(x, u)  # holds no reference to the closure
     except TypeError:  # not weak-referenceable
         return None
     return g or None  # False: this closure failed to capture at this shape
@@ -238,7 +242,7 @@ def rollout_forward(x, u, x_traj, d, K, prev_cost, dynamicsf, immediate_cost, fi
     f = vmap(dynamicsf)
     nb, N, nx = x.shape
     T = N - 1
-    g = _rollout_graph(dynamicsf, f, x, u)
+    g = _rollout_graph(dynamicsf, x, u)
     if g is None:
         return _line_search(x, u, x_traj, prev_cost, immediate_cost, final_cost, max_trials, alpha0, shrink,
                             lambda alpha: _rollout_eager(f, x, u, d, K, alpha))
@@ -246,7 +250,7 @@ def rollout_forward(x, u, x_traj, d, K, prev_cost, dynamicsf, immediate_cost, fi
         g.load(x, u, d, K)
         if g.graph is None:
             try:
-                g.capture()
+                g.capture(f)
             except Exception:  # a host synchronisation (or another capture error) in the closure
                 g.graph = None
                 _clear_hip_error()

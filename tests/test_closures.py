@@ -160,26 +160,50 @@ def test_jet_elementary_rules():
 
 
 def test_rollout_graph_bookkeeping_on_cpu():
-    """The capture-time linalg swap restores torch.linalg exactly; CPU tensors and
-    ILQR_ROLLOUT_GRAPH=0 never build a graph (the product path is the device)."""
+    """The capture-time linalg mode leaves torch.linalg alone outside it and in other
+    threads; CPU tensors never build a graph (the product path is the device); a cached
+    graph does not keep its closure alive."""
+    import gc
+    import threading
+    import weakref
     import torch
     from ilqr_amd import tiles
-    solve, inv = torch.linalg.solve, torch.linalg.inv
     A = torch.tensor([[2.0, 1.0], [1.0, 3.0]], dtype=torch.float64)
     b = torch.tensor([[1.0], [2.0]], dtype=torch.float64)
+    Z = torch.zeros(2, 2, dtype=torch.float64)
+    ref = torch.linalg.solve(A, b)
+    seen = {}
+
+    def other_thread():
+        try:
+            torch.linalg.solve(Z, b)
+            seen["raised"] = False
+        except RuntimeError:
+            seen["raised"] = True
     with tiles._capturable_linalg():
-        assert torch.linalg.solve is not solve
-        assert torch.equal(torch.linalg.solve(A, b), solve(A, b))
-        assert torch.equal(torch.linalg.inv(A), inv(A))
+        assert torch.equal(torch.linalg.solve(A, b), ref)
+        assert torch.equal(torch.linalg.inv(A), torch.linalg.inv_ex(A)[0])
         # a singular system: no host-side check, non-finite values instead of an exception
-        assert not torch.isfinite(torch.linalg.solve(torch.zeros(2, 2, dtype=torch.float64), b)).all()
-    assert torch.linalg.solve is solve and torch.linalg.inv is inv
+        assert not torch.isfinite(torch.linalg.solve(Z, b)).all()
+        # under vmap too (the rollout calls the closure through vmap)
+        from torch.func import vmap
+        assert torch.equal(vmap(lambda M, v: torch.linalg.solve(M, v))(A[None], b.T), ref.T)
+        t = threading.Thread(target=other_thread)
+        t.start()
+        t.join()
+    assert seen["raised"] is True           # the mode is this thread's only
     with pytest.raises(RuntimeError):
-        with tiles._capturable_linalg():
-            raise RuntimeError("capture failed")
-    assert torch.linalg.solve is solve and torch.linalg.inv is inv
+        torch.linalg.solve(Z, b)
     x = torch.zeros(1, 3, 2, dtype=torch.float64)
     u = torch.zeros(1, 2, 1, dtype=torch.float64)
     f = lambda a, v: a  # noqa: E731
-    assert tiles._rollout_graph(f, f, x, u) is None
+    assert tiles._rollout_graph(f, x, u) is None
     assert f not in tiles._GRAPHS
+    # a cached graph holds no reference to its closure: the entry goes with the closure
+    g = lambda a, v: a  # noqa: E731
+    wr = weakref.ref(g)
+    tiles._GRAPHS[g] = {"entry": tiles._RolloutGraph(x, u)}
+    n = len(tiles._GRAPHS)
+    del g
+    gc.collect()
+    assert wr() is None and len(tiles._GRAPHS) == n - 1
