@@ -1,0 +1,1020 @@
+// Floating-base RBD family (include/ilqr.h ilqr_floating_*): the reference's RBD example
+// as its script runs it — test/RBD_2_link_example/RBD_helper_functions.jl:48-116 on
+// test/urdf/2Dof_arm.urdf parsed with `floating = true, gravity = 0` (:7), fitted by
+// animate_RBD_2_link.jl:31 at nx = 16, nu = 8, T = 1000. Every piece of an iteration
+// runs on the device:
+//   * fb_linearize_kernel: linearize_dynamics (backward_pass.jl:25-40) at every (b, t),
+//     one lane per (point, input direction), the RK4 step in forward-mode duals
+//     (ForwardDiff's algorithm, one partial per lane: exact like ForwardDiff), plus the
+//     costs' derivative tiles (:81-109, :134-153) in closed form — the costs are
+//     diagonal weighted squares (:85-116);
+//   * the Riccati recursion: the wide tiles kernel (ilqr_tiles.hip, nx ≤ 16, nu ≤ 8);
+//   * fb_forward_kernel: forward_pass (forward_pass.jl:55-93) — four line-search trials
+//     of a trajectory at once, one per lane, the first accepted one kept (bit for bit
+//     the sequential search's choice: every trial is independent of the others);
+//   * fb_update_kernel: fit's bookkeeping (:161-178).
+//
+// Dynamics (RigidBodyDynamics.jl is absent; restated with Featherstone's algorithms in
+// body coordinates, angular first, as tests/closures.py rbd_floating_arm): the base is a
+// free body with twist (ω, v) in its own frame; joint i turns child body i about axis aᵢ
+// at the origin pᵢ of its parent; M(q) by the composite-rigid-body algorithm, the bias by
+// recursive Newton-Euler at q̈ = 0 (zero gravity, as the script parses the URDF);
+// q̇ = [pdot_from_w(p, ω); v; θ̇] exactly as RBD_helper_functions.jl:66 writes it.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/ilqr.h"
+#include "ilqr_internal.h"
+
+namespace ilqr {
+namespace {
+
+constexpr int FB_NJ = 2;             // joints (the reference's arm)
+constexpr int FB_NQ = 6 + FB_NJ;     // pose coordinates in the cost: p (3), r (3), θ
+constexpr int FB_NX = 2 * FB_NQ;     // 16
+constexpr int FB_NU = FB_NQ;         // 8: base torque, base force, joint torques
+constexpr int FB_CAND = 4;           // line-search trials per trajectory per round
+
+// forward-mode dual with one partial (one input direction per lane)
+struct D1 {
+  double v, d;
+  __device__ D1() = default;
+  __device__ constexpr D1(double a) : v(a), d(0.0) {}
+  __device__ constexpr D1(double a, double b) : v(a), d(b) {}
+};
+__device__ __forceinline__ D1 operator+(D1 a, D1 b) { return D1(a.v + b.v, a.d + b.d); }
+__device__ __forceinline__ D1 operator-(D1 a, D1 b) { return D1(a.v - b.v, a.d - b.d); }
+__device__ __forceinline__ D1 operator-(D1 a) { return D1(-a.v, -a.d); }
+__device__ __forceinline__ D1 operator*(D1 a, D1 b) { return D1(a.v * b.v, fma(a.v, b.d, a.d * b.v)); }
+__device__ __forceinline__ D1 operator*(double a, D1 b) { return D1(a * b.v, a * b.d); }
+__device__ __forceinline__ D1 operator*(D1 b, double a) { return D1(a * b.v, a * b.d); }
+__device__ __forceinline__ D1 operator/(D1 a, D1 b) {
+  const double q = a.v / b.v;
+  return D1(q, (a.d - q * b.d) / b.v);
+}
+__device__ __forceinline__ void sincos_s(double a, double& s, double& c) { sincos(a, &s, &c); }
+__device__ __forceinline__ void sincos_s(D1 a, D1& s, D1& c) {
+  double sv, cv;
+  sincos(a.v, &sv, &cv);
+  s = D1(sv, a.d * cv);
+  c = D1(cv, -a.d * sv);
+}
+
+// the model, by value in the kernel arguments (fp64, prepared on the host)
+struct FbModel {
+  double dt;
+  // bodies 0 (base) .. NJ: mass, h = m·c (first moment), Io = inertia about the body origin
+  double m[FB_NJ + 1];
+  double h[FB_NJ + 1][3];
+  double Io[FB_NJ + 1][9];
+  // joint i (parent body i → child body i+1): R0 (joint frame → parent), R0·[a×], R0·a·aᵀ,
+  // origin p in the parent frame, axis a
+  double R0[FB_NJ][9], R0x[FB_NJ][9], R0aa[FB_NJ][9];
+  double p[FB_NJ][3], ax[FB_NJ][3];
+  // costs (RBD_helper_functions.jl:85-116): ℓ = qs·Σ qwᵢ(tgtᵢ − xᵢ)² + rs·Σ rwⱼ uⱼ²,
+  // ℓ_f = qfs·Σ qfwᵢ(tgtᵢ − xᵢ)², and the derivative coefficients −2·qs·qw, 2·qs·qw, …
+  double tgt[FB_NQ], qw[FB_NQ], rw[FB_NU], qfw[FB_NQ];
+  double qs, rs, qfs;
+  double gx[FB_NQ], hx[FB_NQ], gu[FB_NU], hu[FB_NU], gf[FB_NQ], hf[FB_NQ];
+};
+
+// joint i's child→parent rotation Rc = R0·Rot(a, θ) = c·(R0 − R0aaᵀ) + s·R0[a×] + R0aaᵀ
+template <class S>
+__device__ __forceinline__ void joint_rot(const FbModel& P, int i, S c, S s, S (&Rc)[9]) {
+#pragma unroll
+  for (int k = 0; k < 9; ++k) Rc[k] = c * (P.R0[i][k] - P.R0aa[i][k]) + s * P.R0x[i][k] + P.R0aa[i][k];
+}
+// Rcᵀ·a (parent → child)
+template <class S>
+__device__ __forceinline__ void rot_t(const S (&R)[9], const S (&a)[3], S (&o)[3]) {
+  o[0] = R[0] * a[0] + R[3] * a[1] + R[6] * a[2];
+  o[1] = R[1] * a[0] + R[4] * a[1] + R[7] * a[2];
+  o[2] = R[2] * a[0] + R[5] * a[1] + R[8] * a[2];
+}
+// Rc·a (child → parent)
+template <class S>
+__device__ __forceinline__ void rot(const S (&R)[9], const S (&a)[3], S (&o)[3]) {
+  o[0] = R[0] * a[0] + R[1] * a[1] + R[2] * a[2];
+  o[1] = R[3] * a[0] + R[4] * a[1] + R[5] * a[2];
+  o[2] = R[6] * a[0] + R[7] * a[1] + R[8] * a[2];
+}
+
+// mixed-type helpers: the model's constants stay double (no dual promotion)
+template <class S, class A, class B>
+__device__ __forceinline__ void crossm(const A (&a)[3], const B (&b)[3], S (&o)[3]) {
+  o[0] = a[1] * b[2] - a[2] * b[1];
+  o[1] = a[2] * b[0] - a[0] * b[2];
+  o[2] = a[0] * b[1] - a[1] * b[0];
+}
+template <class S, class A>
+__device__ __forceinline__ S dotm(const A (&a)[3], const S (&b)[3]) {
+  return a[0] * b[0] + a[1] * b[1] + a[2] * b[2];
+}
+
+// continuous dynamics ẋ = [pdot_from_w(p, ω); v; θ̇; M \ (u − bias)] (RBD_helper_functions.jl:50-69).
+// The bias first (recursive Newton-Euler), then M by the composite-rigid-body algorithm
+// kept in blocks — the base's 6×6 composite inertia M₀₀, the base-joint columns M₀ⱼ and
+// the joint block Mⱼⱼ — and M v̇ = b solved through the joint block's Schur complement:
+// M₀₀⁻¹ in closed form (w = I_c⁻¹(n − c × f), v = f/m + c × w, I_c the composite's
+// inertia about its COM c), so no 8 × 8 matrix is ever held.
+template <class S>
+__device__ void fb_xdot(const FbModel& P, const S (&x)[FB_NX], const S (&u)[FB_NU], S (&xd)[FB_NX]) {
+  S R[FB_NJ][9];
+#pragma unroll
+  for (int i = 0; i < FB_NJ; ++i) {
+    S s, c;
+    sincos_s(x[6 + i], s, c);
+    joint_rot(P, i, c, s, R[i]);
+  }
+
+  // --- bias, recursive Newton-Euler at q̈ = 0, zero gravity (:65) -----------------------
+  // outward: v_{i+1} = X v_i + s q̇, a_{i+1} = X a_i + v_{i+1} × (s q̇) (a₀ = 0)
+  S vw[FB_NJ + 1][3], vv[FB_NJ + 1][3], aw[FB_NJ + 1][3], av[FB_NJ + 1][3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    vw[0][k] = x[8 + k];
+    vv[0][k] = x[11 + k];
+    aw[0][k] = 0.0;
+    av[0][k] = 0.0;
+  }
+#pragma unroll
+  for (int i = 0; i < FB_NJ; ++i) {
+    S pw[3], t[3], sw[3], c1[3], c2[3];
+    crossm(P.p[i], vw[i], pw);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) t[k] = vv[i][k] - pw[k];
+    rot_t(R[i], vw[i], vw[i + 1]);
+    rot_t(R[i], t, vv[i + 1]);
+    const S qd = x[14 + i];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      sw[k] = P.ax[i][k] * qd;
+      vw[i + 1][k] = vw[i + 1][k] + sw[k];
+    }
+    if (i == 0) {  // a₀ = 0
+#pragma unroll
+      for (int k = 0; k < 3; ++k) aw[1][k] = av[1][k] = 0.0;
+    } else {
+      crossm(P.p[i], aw[i], pw);
+#pragma unroll
+      for (int k = 0; k < 3; ++k) t[k] = av[i][k] - pw[k];
+      rot_t(R[i], aw[i], aw[i + 1]);
+      rot_t(R[i], t, av[i + 1]);
+    }
+    crossm(vw[i + 1], sw, c1);
+    crossm(vv[i + 1], sw, c2);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      aw[i + 1][k] = aw[i + 1][k] + c1[k];
+      av[i + 1][k] = av[i + 1][k] + c2[k];
+    }
+  }
+  // inward: f_i = I_i a_i + v_i ×* (I_i v_i) + X_{i+1}ᵀ f_{i+1}, τ_i = s_iᵀ f_i
+  S fn[3], ff[3], tau[FB_NJ];
+#pragma unroll
+  for (int i = FB_NJ; i >= 0; --i) {
+    // I·(w, v) = (Io w + h × v, m v − h × w)
+    S pn[3], pf[3], an[3], af[3], t1[3], t2[3];
+    crossm(P.h[i], vv[i], t1);
+    crossm(P.h[i], vw[i], t2);
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      pn[r] = P.Io[i][3 * r] * vw[i][0] + P.Io[i][3 * r + 1] * vw[i][1] + P.Io[i][3 * r + 2] * vw[i][2] + t1[r];
+      pf[r] = P.m[i] * vv[i][r] - t2[r];
+    }
+    crossm(P.h[i], av[i], t1);
+    crossm(P.h[i], aw[i], t2);
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      an[r] = P.Io[i][3 * r] * aw[i][0] + P.Io[i][3 * r + 1] * aw[i][1] + P.Io[i][3 * r + 2] * aw[i][2] + t1[r];
+      af[r] = P.m[i] * av[i][r] - t2[r];
+    }
+    S c1[3], c2[3], c3[3], bn[3], bf[3];
+    crossm(vw[i], pn, c1);
+    crossm(vv[i], pf, c2);
+    crossm(vw[i], pf, c3);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      bn[k] = an[k] + (c1[k] + c2[k]);
+      bf[k] = af[k] + c3[k];
+    }
+    if (i < FB_NJ) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        bn[k] = bn[k] + fn[k];
+        bf[k] = bf[k] + ff[k];
+      }
+    }
+    if (i > 0) {  // τ and the force across joint i−1: f' = Rc f, n' = Rc n + p × f'
+      tau[i - 1] = dotm(P.ax[i - 1], bn);
+      S rn[3], pfx[3];
+      rot(R[i - 1], bf, ff);
+      rot(R[i - 1], bn, rn);
+      crossm(P.p[i - 1], ff, pfx);
+#pragma unroll
+      for (int k = 0; k < 3; ++k) fn[k] = rn[k] + pfx[k];
+    } else {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        fn[k] = bn[k];
+        ff[k] = bf[k];
+      }
+    }
+  }
+  S b[FB_NU];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    b[k] = u[k] - fn[k];
+    b[3 + k] = u[3 + k] - ff[k];
+  }
+#pragma unroll
+  for (int j = 0; j < FB_NJ; ++j) b[6 + j] = u[6 + j] - tau[j];
+
+  // --- M, composite-rigid-body algorithm (:61), tip to base ------------------------------
+  // composite of bodies k..NJ in body k's frame: (m, h, Io)
+  double cm = P.m[FB_NJ];
+  S ch[3], cI[9];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) ch[k] = P.h[FB_NJ][k];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) cI[k] = P.Io[FB_NJ][k];
+  S Mjj[FB_NJ][FB_NJ];  // joint block
+  S Mb[FB_NJ][6];       // base-joint columns: joint j's (n, f) carried to the base frame
+#pragma unroll
+  for (int j = FB_NJ - 1; j >= 0; --j) {
+    // F = C_{j+1} s_j = (Io a, −h × a) in body j+1's frame; M_jj = aᵀ n
+    S n[3], f[3], t[3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) n[r] = cI[3 * r] * P.ax[j][0] + cI[3 * r + 1] * P.ax[j][1] + cI[3 * r + 2] * P.ax[j][2];
+    crossm(ch, P.ax[j], t);
+#pragma unroll
+    for (int r = 0; r < 3; ++r) f[r] = -t[r];
+    Mjj[j][j] = dotm(P.ax[j], n);
+#pragma unroll
+    for (int i = j; i >= 0; --i) {  // across joint i into body i: M_{i-1, j} = a_{i-1}ᵀ n
+      S rn[3], fo[3], pfx[3];
+      rot(R[i], f, fo);
+      rot(R[i], n, rn);
+      crossm(P.p[i], fo, pfx);
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        n[k] = rn[k] + pfx[k];
+        f[k] = fo[k];
+      }
+      if (i > 0) Mjj[i - 1][j] = Mjj[j][i - 1] = dotm(P.ax[i - 1], n);
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      Mb[j][k] = n[k];
+      Mb[j][3 + k] = f[k];
+    }
+    // composite of body j: own inertia + the child composite moved across joint j:
+    // h' = Rc h, Io' = Rc Io Rcᵀ + m(|p|²1 − p pᵀ) + 2(p·h')1 − p h'ᵀ − h' pᵀ, h'' = h' + m p
+    S hp[3], RI[9];
+    rot(R[j], ch, hp);
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int k = 0; k < 3; ++k) RI[3 * r + k] = R[j][3 * r] * cI[k] + R[j][3 * r + 1] * cI[3 + k] + R[j][3 * r + 2] * cI[6 + k];
+    const double* pj = P.p[j];
+    const double pp = pj[0] * pj[0] + pj[1] * pj[1] + pj[2] * pj[2];
+    const S ph = dotm(P.p[j], hp);
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int k = r; k < 3; ++k) {
+        S e = RI[3 * r] * R[j][3 * k] + RI[3 * r + 1] * R[j][3 * k + 1] + RI[3 * r + 2] * R[j][3 * k + 2];
+        e = e - cm * (pj[r] * pj[k]) - pj[r] * hp[k] - hp[r] * pj[k];
+        if (r == k) e = e + (cm * pp + 2.0 * ph);
+        cI[3 * r + k] = P.Io[j][3 * r + k] + e;
+        if (k != r) cI[3 * k + r] = cI[3 * r + k];
+      }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) ch[k] = P.h[j][k] + (hp[k] + cm * pj[k]);
+    cm = P.m[j] + cm;
+  }
+
+  // --- M v̇ = b through the Schur complement of M₀₀ ---------------------------------------
+  // M₀₀ = [[Io, [h×]], [[h×]ᵀ, m1]]: with c = h/m and I_c = Io − m(|c|²1 − c cᵀ),
+  // M₀₀⁻¹(n, f) = (w, f/m + c × w), w = I_c⁻¹(n − c × f)
+  const double minv = 1.0 / cm;
+  S cc[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) cc[k] = ch[k] * minv;
+  S Ic[6];  // I_c lower triangle: 00, 10, 11, 20, 21, 22
+  {
+    const S c2 = dotm(cc, cc);
+    auto ent = [&](int r, int k) { return cI[3 * r + k] - cm * ((r == k ? c2 : S(0.0)) - cc[r] * cc[k]); };
+    Ic[0] = ent(0, 0);
+    Ic[1] = ent(1, 0);
+    Ic[2] = ent(1, 1);
+    Ic[3] = ent(2, 0);
+    Ic[4] = ent(2, 1);
+    Ic[5] = ent(2, 2);
+  }
+  // LDLᵀ of I_c: l10, l20, l21 and 1/d
+  const S d0i = S(1.0) / Ic[0];
+  const S l10 = Ic[1] * d0i, l20 = Ic[3] * d0i;
+  const S d1 = Ic[2] - l10 * Ic[1];
+  const S d1i = S(1.0) / d1;
+  const S l21 = (Ic[4] - l20 * Ic[1]) * d1i;
+  const S d2i = S(1.0) / (Ic[5] - l20 * Ic[3] - l21 * (l21 * d1));
+  auto m00inv = [&](const S (&g)[6], S (&o)[6]) {
+    S cf[3], r[3];
+    const S fv[3] = {g[3], g[4], g[5]};
+    crossm(cc, fv, cf);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) r[k] = g[k] - cf[k];
+    r[1] = r[1] - l10 * r[0];
+    r[2] = r[2] - l20 * r[0] - l21 * r[1];
+    r[0] = r[0] * d0i;
+    r[1] = r[1] * d1i;
+    r[2] = r[2] * d2i;
+    r[1] = r[1] - l21 * r[2];
+    r[0] = r[0] - l10 * r[1] - l20 * r[2];
+    S cw[3];
+    crossm(cc, r, cw);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      o[k] = r[k];
+      o[3 + k] = fv[k] * minv + cw[k];
+    }
+  };
+  S y0[6];
+  {
+    const S g[6] = {b[0], b[1], b[2], b[3], b[4], b[5]};
+    m00inv(g, y0);
+  }
+  S Y[FB_NJ][6];
+#pragma unroll
+  for (int j = 0; j < FB_NJ; ++j) m00inv(Mb[j], Y[j]);
+  // joint block: (Mⱼⱼ − M₀ⱼᵀ Y) v̇ⱼ = bⱼ − M₀ⱼᵀ y₀ (2 × 2)
+  S Sc[FB_NJ][FB_NJ], rj[FB_NJ];
+#pragma unroll
+  for (int i = 0; i < FB_NJ; ++i) {
+    S acc = b[6 + i];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) acc = acc - Mb[i][k] * y0[k];
+    rj[i] = acc;
+#pragma unroll
+    for (int j = 0; j < FB_NJ; ++j) {
+      S e = Mjj[i][j];
+#pragma unroll
+      for (int k = 0; k < 6; ++k) e = e - Mb[i][k] * Y[j][k];
+      Sc[i][j] = e;
+    }
+  }
+  static_assert(FB_NJ == 2, "the joint block's solve is written for two joints");
+  const S det = Sc[0][0] * Sc[1][1] - Sc[0][1] * Sc[1][0];
+  const S q0 = (rj[0] * Sc[1][1] - Sc[0][1] * rj[1]) / det;
+  const S q1 = (Sc[0][0] * rj[1] - Sc[1][0] * rj[0]) / det;
+#pragma unroll
+  for (int k = 0; k < 6; ++k) xd[8 + k] = y0[k] - (Y[0][k] * q0 + Y[1][k] * q1);
+  xd[14] = q0;
+  xd[15] = q1;
+
+  // --- kinematics (:66): q̇ = [pdot_from_w(p, ω); v; θ̇] ----------------------------------
+  const S pv[3] = {x[0], x[1], x[2]};
+  const S w0[3] = {x[8], x[9], x[10]};
+  S pxw[3];
+  crossm(pv, w0, pxw);
+  const S pp = dotm(pv, pv);
+  const S pw = dotm(pv, w0);
+#pragma unroll
+  for (int k = 0; k < 3; ++k) xd[k] = 0.25 * (((1.0 - pp) * w0[k] + 2.0 * pxw[k]) + (2.0 * pw) * pv[k]);
+#pragma unroll
+  for (int k = 0; k < 3; ++k) xd[3 + k] = x[11 + k];
+#pragma unroll
+  for (int j = 0; j < FB_NJ; ++j) xd[6 + j] = x[14 + j];
+}
+
+// dynamicsf: RK4 of fb_xdot (RBD_helper_functions.jl:71-78): kᵢ = Δt·f(·),
+// x + (1/6)·(((k₁ + 2k₂) + 2k₃) + k₄); the stages as a loop (one copy of the dynamics)
+template <class S>
+__device__ void fb_step(const FbModel& P, const S (&x)[FB_NX], const S (&u)[FB_NU], S (&xo)[FB_NX]) {
+  S k[FB_NX], acc[FB_NX], xs[FB_NX];
+#pragma unroll
+  for (int i = 0; i < FB_NX; ++i) xs[i] = x[i];
+#pragma unroll 1
+  for (int st = 0; st < 4; ++st) {
+    // the model's constants are re-read (scalar loads) in every stage instead of being
+    // hoisted into ~200 vector registers
+    asm volatile("" ::: "memory");
+    fb_xdot(P, xs, u, k);
+    const double w = (st == 0 || st == 3) ? 1.0 : 2.0;
+    const double c = st == 2 ? 1.0 : 0.5;
+#pragma unroll
+    for (int i = 0; i < FB_NX; ++i) {
+      k[i] = P.dt * k[i];
+      acc[i] = st == 0 ? k[i] : acc[i] + w * k[i];
+      xs[i] = x[i] + k[i] * c;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < FB_NX; ++i) xo[i] = x[i] + (1.0 / 6.0) * acc[i];
+}
+
+// ℓ(x − x_traj, u) and ℓ_f(x) (RBD_helper_functions.jl:85-116): the weighted squares summed
+// as numpy sums eight terms (((0+1)+(2+3))+((4+5)+(6+7))), then scaled
+__device__ __forceinline__ double sum8(const double (&t)[8]) {
+  return ((t[0] + t[1]) + (t[2] + t[3])) + ((t[4] + t[5]) + (t[6] + t[7]));
+}
+__device__ __forceinline__ double stage_cost(const FbModel& P, const double (&e)[FB_NQ], const double (&u)[FB_NU]) {
+  double a[8], b[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const double d = P.tgt[i] - e[i];
+    a[i] = (d * P.qw[i]) * d;
+    b[i] = (u[i] * P.rw[i]) * u[i];
+  }
+  return sum8(a) * P.qs + sum8(b) * P.rs;
+}
+__device__ __forceinline__ double final_cost(const FbModel& P, const double (&x)[FB_NX]) {
+  double a[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const double d = P.tgt[i] - x[i];
+    a[i] = (d * P.qfw[i]) * d;
+  }
+  return sum8(a) * P.qfs;
+}
+
+__global__ __launch_bounds__(256) void fb_dynamics_kernel(const FbModel* __restrict__ Pm, int n, const double* __restrict__ x,
+                                                          const double* __restrict__ u, double* __restrict__ xo) {
+  const FbModel& P = *Pm;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  double xs[FB_NX], us[FB_NU], y[FB_NX];
+#pragma unroll
+  for (int k = 0; k < FB_NX; ++k) xs[k] = x[(size_t)i * FB_NX + k];
+#pragma unroll
+  for (int k = 0; k < FB_NU; ++k) us[k] = u[(size_t)i * FB_NU + k];
+  fb_step(P, xs, us, y);
+#pragma unroll
+  for (int k = 0; k < FB_NX; ++k) xo[(size_t)i * FB_NX + k] = y[k];
+}
+
+// Derivative tiles at every (b, t): lane (point, dir) seeds input direction dir (x 0..15,
+// u 16..23) and writes column dir of A or B; lane dir = 0 also writes the cost tiles, and
+// the final point's lane the terminal ones. Trajectories whose status is set are skipped.
+__global__ __launch_bounds__(256) void fb_linearize_kernel(const FbModel* __restrict__ Pm, int B, int T, const double* __restrict__ x,
+                                                           const double* __restrict__ u,
+                                                           const int32_t* __restrict__ status,
+                                                           double* __restrict__ A, double* __restrict__ Bm,
+                                                           double* __restrict__ lx, double* __restrict__ lu,
+                                                           double* __restrict__ lxx, double* __restrict__ luu,
+                                                           double* __restrict__ lfx, double* __restrict__ lfxx) {
+  constexpr int ND = FB_NX + FB_NU;
+  const FbModel& P = *Pm;
+  const size_t lane = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (lane >= (size_t)B * T * ND) return;
+  const int dir = (int)(lane % ND);
+  const size_t pt = lane / ND;  // b·T + t
+  const int b = (int)(pt / T);
+  const int t = (int)(pt % T);
+  if (status && status[b] != ILQR_TRAJ_OK) return;
+  const double* xp = x + ((size_t)b * (T + 1) + t) * FB_NX;
+  const double* up = u + pt * FB_NU;
+  D1 xs[FB_NX], us[FB_NU], y[FB_NX];
+#pragma unroll
+  for (int k = 0; k < FB_NX; ++k) xs[k] = D1(xp[k], k == dir ? 1.0 : 0.0);
+#pragma unroll
+  for (int k = 0; k < FB_NU; ++k) us[k] = D1(up[k], k + FB_NX == dir ? 1.0 : 0.0);
+  fb_step(P, xs, us, y);
+  if (dir < FB_NX) {
+#pragma unroll
+    for (int i = 0; i < FB_NX; ++i) A[(pt * FB_NX + i) * FB_NX + dir] = y[i].d;
+  } else {
+#pragma unroll
+    for (int i = 0; i < FB_NX; ++i) Bm[(pt * FB_NX + i) * FB_NU + (dir - FB_NX)] = y[i].d;
+  }
+  if (dir != 0) return;
+  // cost tiles (:95-99): lx = −2qs·qw·(tgt − x), lxx = diag(2qs·qw), lu = 2rs·rw·u, luu = diag(2rs·rw)
+  for (int i = 0; i < FB_NX; ++i) {
+    lx[pt * FB_NX + i] = i < FB_NQ ? P.gx[i] * (P.tgt[i] - xp[i]) : 0.0;
+    for (int k = 0; k < FB_NX; ++k) lxx[(pt * FB_NX + i) * FB_NX + k] = (i == k && i < FB_NQ) ? P.hx[i] : 0.0;
+  }
+  for (int j = 0; j < FB_NU; ++j) {
+    lu[pt * FB_NU + j] = P.gu[j] * up[j];
+    for (int k = 0; k < FB_NU; ++k) luu[(pt * FB_NU + j) * FB_NU + k] = j == k ? P.hu[j] : 0.0;
+  }
+  if (t == T - 1) {  // (:142-143) at x_N
+    const double* xN = x + ((size_t)b * (T + 1) + T) * FB_NX;
+    for (int i = 0; i < FB_NX; ++i) {
+      lfx[(size_t)b * FB_NX + i] = i < FB_NQ ? P.gf[i] * (P.tgt[i] - xN[i]) : 0.0;
+      for (int k = 0; k < FB_NX; ++k)
+        lfxx[((size_t)b * FB_NX + i) * FB_NX + k] = (i == k && i < FB_NQ) ? P.hf[i] : 0.0;
+    }
+  }
+}
+
+struct FbFwd {
+  const double* x;
+  const double* u;
+  const double* xtraj;  // nullable
+  const double* d;
+  const double* K;
+  const double* prev_cost;
+  double* xn;
+  double* un;
+  double* new_cost;
+  double* du2;
+  int32_t* trials;
+  int32_t* fstatus;        // out: 0 accepted, LS_EXHAUSTED, NAN
+  const int32_t* status;   // in: trajectories with a set status are skipped (nullable)
+  double alpha0, shrink;
+  int max_trials;
+};
+
+// One trial's rollout (forward_pass.jl:65-76) → cost, Σ(ū − u)², and whether every
+// ū = u + α·δu equals u (then every later, smaller α rolls out the same); stores x̄, ū
+// when `store`.
+__device__ double fb_rollout(const FbModel& P, const FbFwd& a, int b, int T, double alpha, bool store,
+                             double& du2, bool& same) {
+  const double* x = a.x + (size_t)b * (T + 1) * FB_NX;
+  const double* u = a.u + (size_t)b * T * FB_NU;
+  const double* xt = a.xtraj ? a.xtraj + (size_t)b * (T + 1) * FB_NX : nullptr;
+  const double* d = a.d + (size_t)b * T * FB_NU;
+  const double* K = a.K + (size_t)b * T * FB_NU * FB_NX;
+  double* xn = a.xn + (size_t)b * (T + 1) * FB_NX;
+  double* un = a.un + (size_t)b * T * FB_NU;
+  double xb[FB_NX];
+#pragma unroll
+  for (int k = 0; k < FB_NX; ++k) {
+    xb[k] = x[k];  // x̄₁ = x₁ (:65)
+    if (store) xn[k] = xb[k];
+  }
+  double cost = 0.0, s2 = 0.0;
+  bool eq = true;
+  for (int t = 0; t < T; ++t) {
+    double dx[FB_NX], ub[FB_NU];
+#pragma unroll
+    for (int k = 0; k < FB_NX; ++k) dx[k] = xb[k] - x[(size_t)t * FB_NX + k];  // :72
+#pragma unroll
+    for (int j = 0; j < FB_NU; ++j) {
+      const double uj = u[(size_t)t * FB_NU + j];
+      const double ua = uj + alpha * d[(size_t)t * FB_NU + j];  // :73
+      eq = eq && ua == uj;
+      double kd = 0.0;
+#pragma unroll
+      for (int k = 0; k < FB_NX; ++k) kd = fma(K[((size_t)t * FB_NU + j) * FB_NX + k], dx[k], kd);
+      ub[j] = ua + kd;
+      const double e = ub[j] - uj;
+      s2 = fma(e, e, s2);
+    }
+    // ℓ(x̄ₜ − x_trajₜ, ūₜ) (:187-190, the cost pieces are the first 8 state rows)
+    double ev[FB_NQ];
+#pragma unroll
+    for (int k = 0; k < FB_NQ; ++k) ev[k] = xt ? xb[k] - xt[(size_t)t * FB_NX + k] : xb[k];
+    cost = cost + stage_cost(P, ev, ub);
+    double y[FB_NX];
+    fb_step(P, xb, ub, y);  // :74
+#pragma unroll
+    for (int k = 0; k < FB_NX; ++k) xb[k] = y[k];
+    if (store) {
+#pragma unroll
+      for (int j = 0; j < FB_NU; ++j) un[(size_t)t * FB_NU + j] = ub[j];
+#pragma unroll
+      for (int k = 0; k < FB_NX; ++k) xn[(size_t)(t + 1) * FB_NX + k] = xb[k];
+    }
+  }
+  cost = cost + final_cost(P, xb);  // :192 (raw x̄_N)
+  du2 = s2;
+  same = eq;
+  return cost;
+}
+
+// forward_pass for every trajectory: FB_CAND consecutive lanes roll out trials
+// j, j+1, … at once; the first accepted trial (prev_cost − cost > 0, :77-80) is the
+// sequential search's; a rejected trial whose ū all equal u ends the search (every later
+// trial rolls out identically), as does max_trials (the reference loops unbounded).
+__global__ __launch_bounds__(64) void fb_forward_kernel(const FbModel* __restrict__ Pm, int B, int T, FbFwd a) {
+  const FbModel& P = *Pm;
+  const int lane = threadIdx.x & 63;
+  const int c = lane % FB_CAND;
+  const int b = (blockIdx.x * 64 + lane) / FB_CAND;
+  const bool live = b < B && !(a.status && a.status[b] != ILQR_TRAJ_OK);
+  const double pc = live ? a.prev_cost[b] : 0.0;
+  int done_trial = 0;     // accepted trial (> 0), or −(last trial) when the search ended
+  double done_cost = NAN, done_du2 = 0.0;
+  double alpha = a.alpha0;
+  for (int k = 0; k < c; ++k) alpha *= a.shrink;
+  double step = 1.0;
+  for (int k = 0; k < FB_CAND; ++k) step *= a.shrink;
+  for (int j0 = 1; j0 <= a.max_trials; j0 += FB_CAND) {
+    const int j = j0 + c;
+    const bool run = live && done_trial == 0 && j <= a.max_trials;
+    double cost = NAN, du2 = 0.0;
+    bool same = false;
+    if (run) cost = fb_rollout(P, a, b, T, alpha, j == 1, du2, same);
+    const bool acc = run && (pc - cost > 0.0);
+    // the trajectory's lanes agree on the outcome: the smallest accepted j, else whether a
+    // rejected trial with ū = u ended the search, else the round's last trial
+    const uint64_t accm = __ballot(acc), endm = __ballot(run && !acc && same), runm = __ballot(run);
+    const int g0 = (lane / FB_CAND) * FB_CAND;
+    const uint32_t ga = (uint32_t)((accm >> g0) & ((1u << FB_CAND) - 1));
+    const uint32_t ge = (uint32_t)((endm >> g0) & ((1u << FB_CAND) - 1));
+    const uint32_t gr = (uint32_t)((runm >> g0) & ((1u << FB_CAND) - 1));
+    // the first accepted lane, the first ending lane, the last lane that ran (every lane
+    // takes part in the shuffles)
+    const int ca = ga ? __builtin_ctz(ga) : FB_CAND;
+    const int ce = ge ? __builtin_ctz(ge) : FB_CAND;
+    const int cl = gr ? 31 - __builtin_clz(gr) : 0;
+    const int pick = ca < FB_CAND && ca <= ce ? ca : (ce < FB_CAND ? ce : cl);
+    const double pcost = __shfl(cost, g0 + pick, 64);
+    const double pdu2 = __shfl(du2, g0 + pick, 64);
+    if (live && done_trial == 0 && gr) {
+      if (ca < FB_CAND && ca <= ce) {
+        done_trial = j0 + ca;
+      } else if (ce < FB_CAND || j0 + cl >= a.max_trials) {
+        done_trial = -(ce < FB_CAND ? a.max_trials : j0 + cl);
+      }
+      done_cost = pcost;
+      done_du2 = pdu2;
+      // an accepted trial other than the first is rolled out again by its lane, storing
+      if (done_trial > 1 && c == ca) {
+        double s2;
+        bool sm;
+        (void)fb_rollout(P, a, b, T, alpha, true, s2, sm);
+      }
+    }
+    alpha *= step;
+    if (!__any(live && done_trial == 0)) break;
+  }
+  if (live && c == 0) {
+    const bool acc = done_trial > 0;
+    a.trials[b] = acc ? done_trial : a.max_trials;
+    a.new_cost[b] = done_cost;
+    a.du2[b] = done_du2;
+    a.fstatus[b] = acc ? ILQR_TRAJ_OK : (done_cost != done_cost ? ILQR_TRAJ_NAN : ILQR_TRAJ_LS_EXHAUSTED);
+  }
+}
+
+// fit's bookkeeping for one iteration (forward_pass.jl:161-178): a trajectory whose
+// backward met a NaN stops (status NAN); an exhausted or NaN search stops; an accepted
+// one takes prev_cost = cost (:168), converges when Σ(ū − u)² ≤ tol (:171, returning the
+// iterate it started from) or moves to x̄, ū (:174-175).
+__global__ __launch_bounds__(256) void fb_update_kernel(int B, int T, int it, double tol, const int32_t* __restrict__ bst,
+                                                        const int32_t* __restrict__ fst, const double* __restrict__ cost,
+                                                        const double* __restrict__ du2, int32_t* __restrict__ status,
+                                                        int32_t* __restrict__ iters, double* __restrict__ prev_cost,
+                                                        int32_t* __restrict__ move) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  move[b] = 0;
+  if (status[b] != ILQR_TRAJ_OK) return;
+  if (bst[b] == ILQR_TRAJ_NAN) {
+    status[b] = ILQR_TRAJ_NAN;
+    return;
+  }
+  iters[b] = it;
+  if (fst[b] != ILQR_TRAJ_OK) {
+    status[b] = fst[b];
+    return;
+  }
+  prev_cost[b] = cost[b];
+  if (tol >= 0.0 && du2[b] <= tol) {
+    status[b] = ILQR_TRAJ_CONVERGED;
+    return;
+  }
+  move[b] = 1;
+}
+
+// x ← x̄, u ← ū for the trajectories that moved
+__global__ __launch_bounds__(256) void fb_move_kernel(int B, int T, const int32_t* __restrict__ move,
+                                                      const double* __restrict__ xn, const double* __restrict__ un,
+                                                      double* __restrict__ x, double* __restrict__ u) {
+  const size_t nx = (size_t)(T + 1) * FB_NX, nu = (size_t)T * FB_NU;
+  for (int b = blockIdx.y; b < B; b += gridDim.y) {
+    if (!move[b]) continue;
+    for (size_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nx + nu; i += (size_t)gridDim.x * blockDim.x) {
+      if (i < nx)
+        x[(size_t)b * nx + i] = xn[(size_t)b * nx + i];
+      else
+        u[(size_t)b * nu + (i - nx)] = un[(size_t)b * nu + (i - nx)];
+    }
+  }
+}
+
+__global__ void fb_finish_kernel(int B, int32_t* __restrict__ status, int32_t* __restrict__ flags) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  if (status[b] == ILQR_TRAJ_OK) status[b] = ILQR_TRAJ_MAX_ITER;
+  if (status[b] == ILQR_TRAJ_NAN) atomicOr(flags, 1);
+  if (status[b] == ILQR_TRAJ_LS_EXHAUSTED) atomicOr(flags, 2);
+}
+
+__global__ void fb_count_kernel(int B, const int32_t* __restrict__ status, int32_t* __restrict__ out) {
+  __shared__ int n;
+  if (threadIdx.x == 0) n = 0;
+  __syncthreads();
+  int k = 0;
+  for (int b = threadIdx.x; b < B; b += blockDim.x) k += status[b] == ILQR_TRAJ_OK;
+  atomicAdd(&n, k);
+  __syncthreads();
+  if (threadIdx.x == 0) *out = n;
+}
+
+}  // namespace
+}  // namespace ilqr
+
+// ---------------------------------------------------------------------------------
+// Host side: the handle and its C ABI
+// ---------------------------------------------------------------------------------
+struct ilqr_floating_handle {
+  int device = 0, T = 0, batch = 0;
+  ilqr::FbModel model{};
+  ilqr::FbModel* model_dev = nullptr;
+  hipStream_t stream = nullptr;
+  double *x = nullptr, *u = nullptr, *xn = nullptr, *un = nullptr;
+  double *d = nullptr, *K = nullptr;
+  double *A = nullptr, *Bm = nullptr, *lx = nullptr, *lu = nullptr, *lxx = nullptr, *luu = nullptr;
+  double *lfx = nullptr, *lfxx = nullptr;
+  double *prev_cost = nullptr, *cost = nullptr, *du2 = nullptr;
+  int32_t *trials = nullptr, *status = nullptr, *fstatus = nullptr, *bstatus = nullptr;
+  int32_t *iters = nullptr, *move = nullptr, *words = nullptr;
+};
+
+namespace {
+
+thread_local std::string g_fb_error;
+
+ilqr_status fb_fail(hipError_t e, const char* what) {
+  g_fb_error = std::string(what) + ": " + hipGetErrorString(e);
+  return ILQR_ERR_HIP;
+}
+
+#define FB_TRY(expr)                                    \
+  do {                                                  \
+    hipError_t e_ = (expr);                             \
+    if (e_ != hipSuccess) return fb_fail(e_, #expr);    \
+  } while (0)
+
+// the model from the ABI description (fp64 products formed on the host)
+bool fb_model(const ilqr_floating* m, ilqr::FbModel& P) {
+  using namespace ilqr;
+  P = FbModel{};
+  P.dt = m->dt;
+  auto body = [&](int i, double mass, const double* com, const double* Ic) {
+    P.m[i] = mass;
+    const double cc = com[0] * com[0] + com[1] * com[1] + com[2] * com[2];
+    for (int k = 0; k < 3; ++k) P.h[i][k] = mass * com[k];
+    for (int r = 0; r < 3; ++r)
+      for (int k = 0; k < 3; ++k) P.Io[i][3 * r + k] = Ic[3 * r + k] + mass * ((r == k ? cc : 0.0) - com[r] * com[k]);
+  };
+  body(0, m->base_mass, m->base_com, m->base_inertia);
+  for (int j = 0; j < FB_NJ; ++j) {
+    body(j + 1, m->mass[j], m->com[j], m->inertia[j]);
+    const double* R0 = m->joint_rot[j];
+    const double* a = m->axis[j];
+    const double na = std::sqrt(a[0] * a[0] + a[1] * a[1] + a[2] * a[2]);
+    if (!(na > 0.0)) return false;
+    const double an[3] = {a[0] / na, a[1] / na, a[2] / na};
+    const double ax[9] = {0.0, -an[2], an[1], an[2], 0.0, -an[0], -an[1], an[0], 0.0};
+    for (int r = 0; r < 3; ++r)
+      for (int k = 0; k < 3; ++k) {
+        double s = 0.0, t = 0.0;
+        for (int q = 0; q < 3; ++q) {
+          s += R0[3 * r + q] * ax[3 * q + k];
+          t += R0[3 * r + q] * an[q] * an[k];
+        }
+        P.R0[j][3 * r + k] = R0[3 * r + k];
+        P.R0x[j][3 * r + k] = s;
+        P.R0aa[j][3 * r + k] = t;
+      }
+    for (int k = 0; k < 3; ++k) {
+      P.p[j][k] = m->joint_pos[j][k];
+      P.ax[j][k] = an[k];
+    }
+  }
+  P.qs = m->q_scale;
+  P.rs = m->r_scale;
+  P.qfs = m->qf_scale;
+  for (int i = 0; i < FB_NQ; ++i) {
+    P.tgt[i] = m->target[i];
+    P.qw[i] = m->q_weight[i];
+    P.rw[i] = m->r_weight[i];
+    P.qfw[i] = m->qf_weight[i];
+    // derivative coefficients as the closed forms write them: −(2·qs·qw)·(tgt − x), …
+    P.gx[i] = -(2.0 * P.qs) * P.qw[i];
+    P.hx[i] = (2.0 * P.qs) * P.qw[i];
+    P.gu[i] = (2.0 * P.rs) * P.rw[i];
+    P.hu[i] = (2.0 * P.rs) * P.rw[i];
+    P.gf[i] = -(2.0 * P.qfs) * P.qfw[i];
+    P.hf[i] = (2.0 * P.qfs) * P.qfw[i];
+  }
+  return true;
+}
+
+ilqr::LSParams fb_ls(const ilqr_options* o) {
+  ilqr_options def;
+  ilqr_default_options(&def);
+  if (!o) o = &def;
+  return ilqr::LSParams{o->mu, o->alpha0, o->shrink, o->tol, o->max_trials};
+}
+
+ilqr_status fb_check_options(const ilqr_options* o) {
+  if (!o) return ILQR_OK;
+  if (o->max_trials < 1 || o->max_iter < 0) return ILQR_ERR_BAD_ARG;
+  if (!(o->shrink > 0.0 && o->shrink < 1.0) || !(o->alpha0 > 0.0) || std::isnan(o->mu)) return ILQR_ERR_BAD_ARG;
+  return ILQR_OK;
+}
+
+hipError_t fb_linearize(ilqr_floating_handle* h, const double* x, const double* u, const int32_t* st) {
+  const size_t lanes = (size_t)h->batch * h->T * (ilqr::FB_NX + ilqr::FB_NU);
+  ilqr::fb_linearize_kernel<<<(unsigned)((lanes + 255) / 256), 256, 0, h->stream>>>(
+      h->model_dev, h->batch, h->T, x, u, st, h->A, h->Bm, h->lx, h->lu, h->lxx, h->luu, h->lfx, h->lfxx);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+extern "C" {
+
+int ilqr_floating_supported(int n_joints) { return n_joints == ilqr::FB_NJ ? 1 : 0; }
+
+const char* ilqr_floating_last_error(void) { return g_fb_error.c_str(); }
+
+ilqr_status ilqr_floating_create(ilqr_floating_handle** out, int device, const ilqr_floating* m, int T,
+                                 int batch) {
+  if (!out || !m) return ILQR_ERR_BAD_ARG;
+  *out = nullptr;
+  if (T <= 0 || batch <= 0) return ILQR_ERR_BAD_DIMS;
+  if (!ilqr_floating_supported(m->n_joints)) {
+    g_fb_error = "ilqr_floating_create: n_joints must be 2 (the reference's 2Dof_arm)";
+    return ILQR_ERR_UNSUPPORTED;
+  }
+  if (!(m->dt > 0.0) || !(m->base_mass > 0.0)) return ILQR_ERR_BAD_ARG;
+  if (m->gravity[0] != 0.0 || m->gravity[1] != 0.0 || m->gravity[2] != 0.0) {
+    g_fb_error = "ilqr_floating_create: gravity must be zero (the reference parses the URDF with gravity = 0)";
+    return ILQR_ERR_UNSUPPORTED;
+  }
+  auto* h = new ilqr_floating_handle;
+  if (!fb_model(m, h->model)) {
+    delete h;
+    return ILQR_ERR_BAD_ARG;
+  }
+  FB_TRY(hipSetDevice(device));
+  h->device = device;
+  h->T = T;
+  h->batch = batch;
+  const size_t B = (size_t)batch, nx = ilqr::FB_NX, nu = ilqr::FB_NU, P = B * T;
+  hipError_t e = hipSuccess;
+  auto alloc = [&](auto** p, size_t bytes) {
+    if (e == hipSuccess) e = hipMalloc((void**)p, bytes);
+  };
+  alloc(&h->x, 8 * B * (T + 1) * nx);
+  alloc(&h->u, 8 * P * nu);
+  alloc(&h->xn, 8 * B * (T + 1) * nx);
+  alloc(&h->un, 8 * P * nu);
+  alloc(&h->d, 8 * P * nu);
+  alloc(&h->K, 8 * P * nu * nx);
+  alloc(&h->A, 8 * P * nx * nx);
+  alloc(&h->Bm, 8 * P * nx * nu);
+  alloc(&h->lx, 8 * P * nx);
+  alloc(&h->lu, 8 * P * nu);
+  alloc(&h->lxx, 8 * P * nx * nx);
+  alloc(&h->luu, 8 * P * nu * nu);
+  alloc(&h->lfx, 8 * B * nx);
+  alloc(&h->lfxx, 8 * B * nx * nx);
+  alloc(&h->prev_cost, 8 * B);
+  alloc(&h->cost, 8 * B);
+  alloc(&h->du2, 8 * B);
+  alloc(&h->trials, 4 * B);
+  alloc(&h->status, 4 * B);
+  alloc(&h->fstatus, 4 * B);
+  alloc(&h->bstatus, 4 * B);
+  alloc(&h->iters, 4 * B);
+  alloc(&h->move, 4 * B);
+  alloc(&h->words, 4 * 4);
+  alloc(&h->model_dev, sizeof(ilqr::FbModel));
+  if (e == hipSuccess) e = hipMemcpy(h->model_dev, &h->model, sizeof(ilqr::FbModel), hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    ilqr_floating_destroy(h);
+    return fb_fail(e, "ilqr_floating_create: hipMalloc");
+  }
+  *out = h;
+  return ILQR_OK;
+}
+
+ilqr_status ilqr_floating_destroy(ilqr_floating_handle* h) {
+  if (!h) return ILQR_OK;
+  (void)hipSetDevice(h->device);
+  for (double* p : {h->x, h->u, h->xn, h->un, h->d, h->K, h->A, h->Bm, h->lx, h->lu, h->lxx, h->luu, h->lfx,
+                    h->lfxx, h->prev_cost, h->cost, h->du2})
+    (void)hipFree(p);
+  for (int32_t* p : {h->trials, h->status, h->fstatus, h->bstatus, h->iters, h->move, h->words}) (void)hipFree(p);
+  (void)hipFree(h->model_dev);
+  delete h;
+  return ILQR_OK;
+}
+
+ilqr_status ilqr_floating_set_stream(ilqr_floating_handle* h, void* s) {
+  if (!h) return ILQR_ERR_BAD_ARG;
+  h->stream = (hipStream_t)s;
+  return ILQR_OK;
+}
+
+ilqr_status ilqr_floating_sync(ilqr_floating_handle* h) {
+  if (!h) return ILQR_ERR_BAD_ARG;
+  FB_TRY(hipStreamSynchronize(h->stream));
+  return ILQR_OK;
+}
+
+ilqr_status ilqr_floating_dynamics(ilqr_floating_handle* h, const double* x, const double* u, double* x_next,
+                                   int n) {
+  if (!h || !x || !u || !x_next) return ILQR_ERR_BAD_ARG;
+  if (n <= 0) return ILQR_ERR_BAD_DIMS;
+  FB_TRY(hipSetDevice(h->device));
+  ilqr::fb_dynamics_kernel<<<(n + 255) / 256, 256, 0, h->stream>>>(h->model_dev, n, x, u, x_next);
+  FB_TRY(hipGetLastError());
+  return ILQR_OK;
+}
+
+ilqr_status ilqr_floating_linearize(ilqr_floating_handle* h, const double* x, const double* u, double* A,
+                                    double* B) {
+  if (!h || !x || !u || !A || !B) return ILQR_ERR_BAD_ARG;
+  FB_TRY(hipSetDevice(h->device));
+  FB_TRY(fb_linearize(h, x, u, nullptr));
+  const size_t P = (size_t)h->batch * h->T;
+  FB_TRY(hipMemcpyAsync(A, h->A, 8 * P * ilqr::FB_NX * ilqr::FB_NX, hipMemcpyDeviceToDevice, h->stream));
+  FB_TRY(hipMemcpyAsync(B, h->Bm, 8 * P * ilqr::FB_NX * ilqr::FB_NU, hipMemcpyDeviceToDevice, h->stream));
+  return ILQR_OK;
+}
+
+ilqr_status ilqr_floating_fit(ilqr_floating_handle* h, const ilqr_options* o, const double* x_init,
+                              const double* u_init, const double* x_traj, double* x_out, double* u_out,
+                              double* cost, int32_t* iters, int32_t* status) {
+  if (!h || !x_init || !u_init || !x_out || !u_out) return ILQR_ERR_BAD_ARG;
+  ilqr_status st = fb_check_options(o);
+  if (st != ILQR_OK) return st;
+  FB_TRY(hipSetDevice(h->device));
+  const ilqr::LSParams ls = fb_ls(o);
+  const int max_iter = o ? o->max_iter : 100;
+  const int B = h->batch, T = h->T;
+  const size_t nxe = (size_t)(T + 1) * ilqr::FB_NX, nue = (size_t)T * ilqr::FB_NU;
+  hipStream_t s = h->stream;
+  FB_TRY(hipMemcpyAsync(h->x, x_init, 8 * B * nxe, hipMemcpyDeviceToDevice, s));
+  FB_TRY(hipMemcpyAsync(h->u, u_init, 8 * B * nue, hipMemcpyDeviceToDevice, s));
+  FB_TRY(ilqr::launch_fill_f64(h->prev_cost, B, INFINITY, s));  // :159
+  FB_TRY(ilqr::launch_fill_i32(h->status, B, ILQR_TRAJ_OK, s));
+  FB_TRY(ilqr::launch_fill_i32(h->iters, B, 0, s));
+  FB_TRY(hipMemsetAsync(h->words, 0, 4 * 4, s));
+  const ilqr::TileParams tp{h->A, h->Bm, h->lx, h->lu, h->lxx, nullptr, h->luu, h->lfx, h->lfxx};
+  ilqr::FbFwd fa{};
+  fa.x = h->x;
+  fa.u = h->u;
+  fa.xtraj = x_traj;
+  fa.d = h->d;
+  fa.K = h->K;
+  fa.prev_cost = h->prev_cost;
+  fa.xn = h->xn;
+  fa.un = h->un;
+  fa.new_cost = h->cost;
+  fa.du2 = h->du2;
+  fa.trials = h->trials;
+  fa.fstatus = h->fstatus;
+  fa.status = h->status;
+  fa.alpha0 = ls.alpha0;
+  fa.shrink = ls.shrink;
+  fa.max_trials = ls.max_trials;
+  const unsigned g = (unsigned)((B + 255) / 256);
+  for (int it = 1; it <= max_iter; ++it) {  // forward_pass.jl:161
+    FB_TRY(fb_linearize(h, h->x, h->u, h->status));
+    FB_TRY(ilqr::launch_tiles_backward(ilqr::FB_NX, ilqr::FB_NU, tp, B, T, h->d, h->K, h->bstatus, ls.mu, s));
+    ilqr::fb_forward_kernel<<<(unsigned)((B * ilqr::FB_CAND + 63) / 64), 64, 0, s>>>(h->model_dev, B, T, fa);
+    FB_TRY(hipGetLastError());
+    ilqr::fb_update_kernel<<<g, 256, 0, s>>>(B, T, it, ls.tol, h->bstatus, h->fstatus, h->cost, h->du2,
+                                             h->status, h->iters, h->prev_cost, h->move);
+    FB_TRY(hipGetLastError());
+    const unsigned gx = (unsigned)((nxe + nue + 255) / 256 < 64 ? (nxe + nue + 255) / 256 : 64);
+    ilqr::fb_move_kernel<<<dim3(gx, (unsigned)(B < 65535 ? B : 65535)), 256, 0, s>>>(B, T, h->move, h->xn, h->un,
+                                                                                      h->x, h->u);
+    FB_TRY(hipGetLastError());
+    if (ls.tol >= 0.0 && it < max_iter) {  // :171's break once every trajectory stopped
+      ilqr::fb_count_kernel<<<1, 256, 0, s>>>(B, h->status, h->words);
+      FB_TRY(hipGetLastError());
+      int32_t running = 0;
+      FB_TRY(hipMemcpyAsync(&running, h->words, 4, hipMemcpyDeviceToHost, s));
+      FB_TRY(hipStreamSynchronize(s));
+      if (running == 0) break;
+    }
+  }
+  ilqr::fb_finish_kernel<<<g, 256, 0, s>>>(B, h->status, h->words + 1);
+  FB_TRY(hipGetLastError());
+  FB_TRY(hipMemcpyAsync(x_out, h->x, 8 * B * nxe, hipMemcpyDeviceToDevice, s));
+  FB_TRY(hipMemcpyAsync(u_out, h->u, 8 * B * nue, hipMemcpyDeviceToDevice, s));
+  if (cost) FB_TRY(hipMemcpyAsync(cost, h->prev_cost, 8 * B, hipMemcpyDeviceToDevice, s));
+  if (iters) FB_TRY(hipMemcpyAsync(iters, h->iters, 4 * B, hipMemcpyDeviceToDevice, s));
+  if (status) FB_TRY(hipMemcpyAsync(status, h->status, 4 * B, hipMemcpyDeviceToDevice, s));
+  int32_t flags = 0;
+  FB_TRY(hipMemcpyAsync(&flags, h->words + 1, 4, hipMemcpyDeviceToHost, s));
+  FB_TRY(hipStreamSynchronize(s));
+  return (flags & 1) ? ILQR_ERR_NAN : ((flags & 2) ? ILQR_ERR_LS_EXHAUSTED : ILQR_OK);
+}
+
+}  // extern "C"

@@ -12,7 +12,8 @@ __all__ = ["LinearDynamics", "QuadraticCost", "QuadraticFinalCost", "LQBatch",
            "ChainSolver", "ChainProblem", "rbd_2dof_problem", "chain_closures", "load_robot",
            "rbd_initial_states", "simple_final_cost", "simple_immediate_cost",
            "linearize_dynamics", "immediate_cost_quadratization", "final_cost_quadratization",
-           "optimal_controller_param", "feedback_parameters", "step_back"]
+           "optimal_controller_param", "feedback_parameters", "step_back",
+           "FloatingSolver", "FloatingProblem", "rbd_example_problem", "floating_closures"]
 
 _HELPERS = ("linearize_dynamics", "immediate_cost_quadratization", "final_cost_quadratization",
             "optimal_controller_param", "feedback_parameters", "step_back")
@@ -31,6 +32,9 @@ def __getattr__(name):
                 "rbd_initial_states"):
         from . import chain
         return getattr(chain, name)
+    if name in ("FloatingSolver", "FloatingProblem", "rbd_example_problem", "floating_closures"):
+        from . import floating
+        return getattr(floating, name)
     if name in ("simple_final_cost", "simple_immediate_cost"):
         from . import cost_functions
         return getattr(cost_functions, name)

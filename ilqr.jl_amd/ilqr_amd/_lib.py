@@ -94,6 +94,23 @@ class ChainStruct(C.Structure):
                 ("r_weight", C.c_double * J), ("qf_weight", C.c_double * J)]
 
 
+FLOATING_MAX_JOINTS = 2
+FLOATING_MAX_POSE = 6 + FLOATING_MAX_JOINTS
+
+
+class FloatingStruct(C.Structure):
+    """ilqr_floating (include/ilqr.h): the floating-base RBD family."""
+    J, Q = FLOATING_MAX_JOINTS, FLOATING_MAX_POSE
+    _fields_ = [("n_joints", C.c_int32), ("dt", C.c_double), ("gravity", C.c_double * 3),
+                ("base_mass", C.c_double), ("base_com", C.c_double * 3), ("base_inertia", C.c_double * 9),
+                ("joint_rot", (C.c_double * 9) * J), ("joint_pos", (C.c_double * 3) * J),
+                ("axis", (C.c_double * 3) * J), ("mass", C.c_double * J),
+                ("com", (C.c_double * 3) * J), ("inertia", (C.c_double * 9) * J),
+                ("target", C.c_double * Q), ("q_weight", C.c_double * Q),
+                ("r_weight", C.c_double * Q), ("qf_weight", C.c_double * Q),
+                ("q_scale", C.c_double), ("r_scale", C.c_double), ("qf_scale", C.c_double)]
+
+
 # every symbol declared in include/ilqr.h, with its ctypes signature
 P = C.c_void_p
 SIGNATURES = {
@@ -153,6 +170,15 @@ SIGNATURES = {
     "ilqr_chain_iterate": (C.c_int, [P, C.POINTER(Options), P, P, P, P, P, P, P, P, P, P]),
     "ilqr_chain_fit": (C.c_int, [P, C.POINTER(Options), P, P, P, P, P, P, P, P]),
     "ilqr_chain_fit_ex": (C.c_int, [P, C.POINTER(Options), P, P, P, P, P, P, P, P, C.POINTER(History)]),
+    "ilqr_floating_supported": (C.c_int, [C.c_int]),
+    "ilqr_floating_last_error": (C.c_char_p, []),
+    "ilqr_floating_create": (C.c_int, [C.POINTER(P), C.c_int, C.POINTER(FloatingStruct), C.c_int, C.c_int]),
+    "ilqr_floating_destroy": (C.c_int, [P]),
+    "ilqr_floating_set_stream": (C.c_int, [P, P]),
+    "ilqr_floating_sync": (C.c_int, [P]),
+    "ilqr_floating_dynamics": (C.c_int, [P, P, P, P, C.c_int]),
+    "ilqr_floating_linearize": (C.c_int, [P, P, P, P, P]),
+    "ilqr_floating_fit": (C.c_int, [P, C.POINTER(Options), P, P, P, P, P, P, P, P]),
 }
 
 _lib = None
@@ -182,7 +208,8 @@ class IlqrError(RuntimeError):
     def __init__(self, status: int, where: str):
         lib = load()
         msg = lib.ilqr_status_string(status).decode()
-        extra = lib.ilqr_last_error().decode() or lib.ilqr_chain_last_error().decode()
+        extra = (lib.ilqr_last_error().decode() or lib.ilqr_chain_last_error().decode()
+                 or lib.ilqr_floating_last_error().decode())
         super().__init__(f"{where}: {msg}" + (f" ({extra})" if extra and status == ERR_HIP else ""))
         self.status = status
 

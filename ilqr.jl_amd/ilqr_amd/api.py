@@ -80,6 +80,9 @@ def _family(dynamicsf, immediate_cost, final_cost):
         return "two_link"
     if chain_problem_of(dynamicsf, immediate_cost, final_cost) is not None:
         return "chain"
+    from .floating import floating_problem_of
+    if floating_problem_of(dynamicsf, immediate_cost, final_cost) is not None:
+        return "floating"
     if (isinstance(dynamicsf, LinearDynamics) and isinstance(immediate_cost, QuadraticCost)
             and isinstance(final_cost, QuadraticFinalCost)):
         return "lq"
@@ -120,6 +123,20 @@ def _tiles_solver(xb, ub):
                             lambda: Solver(nx, nu, M, nb, device=dev, kind=_lib.PROBLEM_TILES))
 
 
+def _floating_solver(xb, ub, dynamicsf, immediate_cost, final_cost):
+    """The floating-base family's handle for this model and shape, cached (cache.py)."""
+    from .floating import FloatingSolver, floating_problem_of
+    nb, N, nx = xb.shape
+    _, M, nu = ub.shape
+    assert N == M + 1, "size(x)[1] == size(u)[1] + 1"   # backward_pass.jl:329
+    p = floating_problem_of(dynamicsf, immediate_cost, final_cost)
+    if (p.nx, p.nu) != (nx, nu):
+        raise AssertionError(f"problem is ({p.nx}, {p.nu}) but x/u are ({nx}, {nu})")
+    dev = _device()
+    return _cache.workspace(("floating", dev, bytes(p.struct()), M, nb),
+                            lambda: FloatingSolver(p, M, nb, device=dev))
+
+
 def clear_cache():
     """Close the device workspaces fit / backward_pass / linearize_dynamics keep per shape."""
     _cache.clear()
@@ -151,6 +168,11 @@ def backward_pass(x, u, dynamicsf, immediate_cost, final_cost):
         with _tiles_solver(xb, ub) as s:
             tl = _tiles.derivative_tiles(xb, ub, dynamicsf, immediate_cost, final_cost)
             d, K, st = s.backward_tiles(tl)
+    elif fam == "floating":
+        with _floating_solver(xb, ub, dynamicsf, immediate_cost, final_cost) as s:
+            r = s.fit(xb.to(torch.float64).contiguous(), ub.to(torch.float64).contiguous(),
+                      x_traj=None if xt is None else xt.to(torch.float64).contiguous(),
+                      max_iter=int(max_iter), tol=float(tol))
     elif fam == "chain":
         dt = _eltype(x)
         xb, ub = xb.to(dt), ub.to(dt)

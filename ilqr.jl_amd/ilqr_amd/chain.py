@@ -46,7 +46,9 @@ def load_robot(name: str) -> Chain:
     with open(os.path.join(ROBOTS, name + ".json")) as f:
         d = json.load(f)
     return Chain(d["names"], np.array(d["R0"]), np.array(d["p"]), np.array(d["axis"]),
-                 np.array(d["mass"]), np.array(d["com"]), np.array(d["Ic"]), np.array(d["gravity"]))
+                 np.array(d["mass"]), np.array(d["com"]), np.array(d["Ic"]), np.array(d["gravity"]),
+                 float(d.get("base_mass", 0.0)), np.array(d.get("base_com", [0.0] * 3), float),
+                 np.array(d.get("base_Ic", np.zeros((3, 3)).tolist()), float))
 
 
 @dataclass

@@ -94,6 +94,10 @@ class Chain:
     com: np.ndarray   # (n, 3)    COM in the body frame
     Ic: np.ndarray    # (n, 3, 3) inertia about the COM, body axes
     gravity: np.ndarray = field(default_factory=lambda: np.zeros(3))
+    # the root link (fixed children merged): only a floating base's dynamics see it
+    base_mass: float = 0.0
+    base_com: np.ndarray = field(default_factory=lambda: np.zeros(3))
+    base_Ic: np.ndarray = field(default_factory=lambda: np.zeros((3, 3)))
 
     @property
     def n(self) -> int:
@@ -101,9 +105,10 @@ class Chain:
 
 
 def parse_urdf(path: str, gravity=(0.0, 0.0, 0.0)) -> Chain:
-    """Fixed-base reduction of a serial-chain URDF (the root link is the fixed
-    base; its inertia never enters the dynamics). Branching trees and prismatic
-    joints are rejected."""
+    """Serial-chain URDF → Chain: the joints and their bodies, and the root link's body
+    (base_mass, base_com, base_Ic) — which a fixed base ignores and a floating base
+    (ilqr_amd.floating, `parse_urdf(...; floating = true)` in the reference) moves.
+    Branching trees and prismatic joints are rejected."""
     root = ET.parse(path).getroot()
     links = {l.get("name"): l for l in root.findall("link")}
     joints = root.findall("joint")
@@ -119,6 +124,7 @@ def parse_urdf(path: str, gravity=(0.0, 0.0, 0.0)) -> Chain:
     # owner's frame (-1 = the fixed base)
     place = {roots[0]: (-1, np.eye(3), np.zeros(3))}
     names, R0s, ps, axes, bodies = [], [], [], [], []
+    base = _link_body(links[roots[0]])
     frontier = [roots[0]]
     while frontier:
         lname = frontier.pop()
@@ -144,6 +150,8 @@ def parse_urdf(path: str, gravity=(0.0, 0.0, 0.0)) -> Chain:
             elif jtype == "fixed":
                 if owner >= 0:
                     bodies[owner] = bodies[owner].merged(_link_body(links[child]), R, p)
+                else:
+                    base = base.merged(_link_body(links[child]), R, p)
                 place[child] = (owner, R, p)
             else:
                 raise ValueError(f"joint type {jtype!r} is not supported")
@@ -152,4 +160,5 @@ def parse_urdf(path: str, gravity=(0.0, 0.0, 0.0)) -> Chain:
         raise ValueError("no movable joints")
     return Chain(names, np.array(R0s), np.array(ps), np.array(axes),
                  np.array([b.mass for b in bodies]), np.array([b.com for b in bodies]),
-                 np.array([b.Ic for b in bodies]), np.asarray(gravity, dtype=float))
+                 np.array([b.Ic for b in bodies]), np.asarray(gravity, dtype=float),
+                 float(base.mass), np.asarray(base.com, float), np.asarray(base.Ic, float))

@@ -447,6 +447,74 @@ ilqr_status ilqr_multi_gather(ilqr_multi* m, double* x_out, double* u_out, doubl
 ilqr_status ilqr_host_alloc(size_t bytes, void** ptr);
 ilqr_status ilqr_host_free(void* ptr);
 
+/* ---------------------------------------------------------------------------
+ * Floating-base RBD family: the reference's RBD example as its script runs it —
+ * test/RBD_2_link_example/RBD_helper_functions.jl:48-116 on test/urdf/2Dof_arm.urdf
+ * parsed with `floating = true, gravity = 0` (:7), fitted by animate_RBD_2_link.jl:31
+ * (nx = 16, nu = 8, T = 1000). Replaces, for these closures, the whole of
+ * iLQR.fit (src/forward_pass.jl:148-179): linearize_dynamics in forward-mode duals
+ * (ForwardDiff's algorithm), the cost tiles in closed form, the Riccati recursion of
+ * ilqr_backward_tiles, forward_pass with its line search, and fit's bookkeeping, all on
+ * the device.
+ *   x = [p (MRP, 3); r (3); θ (n_joints); ω (3); v (3); θ̇ (n_joints)], the base twist
+ *       (ω, v) in the base frame; u = [base torque (3); base force (3); joint torques]
+ *   dynamicsf(x, u)     = RK4(dt) of [pdot_from_w(p, ω); v; θ̇; M(q) \ (u − bias(q, v))]
+ *   immediate_cost(x,u) = q_scale·Σᵢ q_weightᵢ(targetᵢ − xᵢ)² + r_scale·Σⱼ r_weightⱼ uⱼ²
+ *   final_cost(x)       = qf_scale·Σᵢ qf_weightᵢ(targetᵢ − xᵢ)²   (i over the 6 + n_joints
+ *                         pose rows; the script: scales 10, 1, 100000)
+ * M by the composite-rigid-body algorithm, the bias by recursive Newton-Euler at q̈ = 0,
+ * in body coordinates (RigidBodyDynamics.jl is not vendored: parity against the
+ * restatement in tests/closures.py). Arrays are device fp64, row-major:
+ * x (batch, T+1, nx), u (batch, T, nu), A (batch, T, nx, nx), B (batch, T, nx, nu).
+ * --------------------------------------------------------------------------- */
+#define ILQR_FLOATING_MAX_JOINTS 2
+#define ILQR_FLOATING_MAX_POSE (6 + ILQR_FLOATING_MAX_JOINTS)
+
+typedef struct {
+  int32_t n_joints;    /* revolute joints root to tip (ilqr_floating_supported)            */
+  double dt;           /* RK4 step (Δt = 0.01 in the script)                                */
+  double gravity[3];   /* must be zero, as the script parses the URDF                      */
+  double base_mass;    /* the root link (fixed children merged), base frame               */
+  double base_com[3];
+  double base_inertia[9];                          /* about the COM, row-major               */
+  double joint_rot[ILQR_FLOATING_MAX_JOINTS][9];   /* joint frame → parent body frame        */
+  double joint_pos[ILQR_FLOATING_MAX_JOINTS][3];   /* joint origin in the parent body frame  */
+  double axis[ILQR_FLOATING_MAX_JOINTS][3];        /* rotation axis, joint (= child) frame   */
+  double mass[ILQR_FLOATING_MAX_JOINTS];
+  double com[ILQR_FLOATING_MAX_JOINTS][3];
+  double inertia[ILQR_FLOATING_MAX_JOINTS][9];
+  double target[ILQR_FLOATING_MAX_POSE];           /* target_pose (animate_RBD_2_link.jl:10) */
+  double q_weight[ILQR_FLOATING_MAX_POSE];
+  double r_weight[ILQR_FLOATING_MAX_POSE];
+  double qf_weight[ILQR_FLOATING_MAX_POSE];
+  double q_scale, r_scale, qf_scale;
+} ilqr_floating;
+
+typedef struct ilqr_floating_handle ilqr_floating_handle;
+
+/* 1 if the kernels are compiled for n_joints (2: the reference's arm) */
+int ilqr_floating_supported(int n_joints);
+const char* ilqr_floating_last_error(void);
+/* ILQR_ERR_UNSUPPORTED for other joint counts or non-zero gravity */
+ilqr_status ilqr_floating_create(ilqr_floating_handle** out, int device, const ilqr_floating* model,
+                                 int T, int batch);
+ilqr_status ilqr_floating_destroy(ilqr_floating_handle* h);
+ilqr_status ilqr_floating_set_stream(ilqr_floating_handle* h, void* hip_stream);
+ilqr_status ilqr_floating_sync(ilqr_floating_handle* h);
+/* dynamicsf for n independent (x, u) pairs: x (n, nx), u (n, nu) → x_next (n, nx) */
+ilqr_status ilqr_floating_dynamics(ilqr_floating_handle* h, const double* x, const double* u,
+                                   double* x_next, int n);
+/* linearize_dynamics (backward_pass.jl:25-40) at every (b, t) of x (batch, T+1, nx),
+ * u (batch, T, nu) → A (batch, T, nx, nx), B (batch, T, nx, nu) */
+ilqr_status ilqr_floating_linearize(ilqr_floating_handle* h, const double* x, const double* u,
+                                    double* A, double* B);
+/* iLQR.fit (forward_pass.jl:148-179) for every trajectory: arguments, per-trajectory
+ * status and the call status as ilqr_fit (x_traj may be NULL: zeros; cost, iters,
+ * status may be NULL). Synchronises. */
+ilqr_status ilqr_floating_fit(ilqr_floating_handle* h, const ilqr_options* o, const double* x_init,
+                              const double* u_init, const double* x_traj, double* x_out,
+                              double* u_out, double* cost, int32_t* iters, int32_t* status);
+
 /* Device memory helpers so a host-language shim (Julia ccall) needs no GPU package. */
 ilqr_status ilqr_malloc(ilqr_handle* h, size_t bytes, void** ptr);
 ilqr_status ilqr_free(ilqr_handle* h, void* ptr);

@@ -1,0 +1,161 @@
+"""GPU parity of the floating-base RBD family (include/ilqr.h ilqr_floating_*): the
+reference's RBD script (test/RBD_2_link_example/, 2Dof_arm.urdf floating, zero gravity,
+nx = 16, nu = 8, T = 1000) fitted natively, against the restatement the generic closure
+path is checked with (tests/closures.py rbd_floating_arm on numpy / oracle.jet; parity
+against RigidBodyDynamics.jl itself is unpinned: it is not runnable here).
+
+Tolerances (fp64): one RK4 step rel 1e-12 (the same algorithms in another operation
+order); the dual-number Jacobians rel 1e-10 against oracle.jet's forward mode; fit
+iterates and costs rel 1e-8 with exact iteration counts and statuses, as the closure
+path's test_rbd_caller_fit_t1000."""
+import numpy as np
+import pytest
+import torch
+
+from closures import jet_ns, rbd_cost_quads, rbd_floating_arm
+from ilqr_amd import _lib, api
+from ilqr_amd.floating import (FloatingSolver, floating_closures, rbd_example_problem,
+                               rbd_initial_state)
+from oracle import closure_fit as CF
+from oracle import jet
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    a = a.cpu().numpy() if isinstance(a, torch.Tensor) else np.asarray(a, float)
+    b = b.cpu().numpy() if isinstance(b, torch.Tensor) else np.asarray(b, float)
+    return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-300))
+
+
+def random_states(n, seed=3):
+    rng = np.random.default_rng(seed)
+    x = np.zeros((n, 16))
+    x[:, 0:3] = 0.4 * rng.standard_normal((n, 3))       # MRP
+    x[:, 3:6] = rng.standard_normal((n, 3))
+    x[:, 6:8] = rng.uniform(-3.0, 3.0, (n, 2))
+    x[:, 8:16] = rng.standard_normal((n, 8))
+    u = 5.0 * rng.standard_normal((n, 8))
+    return x, u
+
+
+def script_batch(nb, T, seed=7):
+    """The script's start (rest state, zero inputs, x_init = rollout: animate_RBD_2_link.jl:19-25)
+    plus perturbed copies, rolled out by the restatement."""
+    fj, _, _ = rbd_floating_arm(jet_ns())
+    x = np.zeros((nb, T + 1, 16))
+    x[:, 0] = rbd_initial_state()
+    x[1:, 0, 8:] = 0.05 * np.random.default_rng(seed).standard_normal((nb - 1, 8))
+    u = np.zeros((nb, T, 8))
+    for t in range(T):
+        x[:, t + 1] = fj(x[:, t], u[:, t])
+    return x, u
+
+
+def test_floating_dynamics_vs_restatement(gpu):
+    fj, _, _ = rbd_floating_arm(jet_ns())
+    x, u = random_states(257)
+    s = FloatingSolver(rbd_example_problem(), 1, 1)
+    try:
+        y = s.dynamics(torch.from_numpy(x).cuda(), torch.from_numpy(u).cuda())
+    finally:
+        s.close()
+    assert rel(y, fj(x, u)) < 1e-12
+
+
+def test_floating_linearize_vs_forward_mode(gpu):
+    fj, _, _ = rbd_floating_arm(jet_ns())
+    nb, T = 3, 5
+    xs, us = random_states(nb * (T + 1), seed=11)
+    x = xs.reshape(nb, T + 1, 16)
+    u = us[: nb * T].reshape(nb, T, 8)
+    s = FloatingSolver(rbd_example_problem(), T, nb)
+    try:
+        A, Bm = s.linearize(torch.from_numpy(x).cuda(), torch.from_numpy(u).cuda())
+    finally:
+        s.close()
+    Aj, Bj = jet.jacobians(fj, x[:, :T].reshape(-1, 16), u.reshape(-1, 8))
+    assert rel(A.reshape(-1, 16, 16), Aj) < 1e-10
+    assert rel(Bm.reshape(-1, 16, 8), Bj) < 1e-10
+
+
+def test_floating_fit_script_shape_vs_closure_oracle(gpu):
+    """The script's fit (T = 1000) natively against the batched closure oracle (ForwardDiff's
+    algorithm for A, B; the closed-form cost tiles; the C restatement's recursion)."""
+    nb, T, iters = 2, 1000, 4
+    x, u = script_batch(nb, T)
+    s = FloatingSolver(rbd_example_problem(), T, nb)
+    try:
+        r = s.fit(torch.from_numpy(x).cuda(), torch.from_numpy(u).cuda(), max_iter=iters, tol=1e-6)
+    finally:
+        s.close()
+    fj, lj, lfj = rbd_floating_arm(jet_ns())
+    o = CF.fit(x, u, fj, lj, lfj, *rbd_cost_quads(), max_iter=iters, tol=1e-6)
+    assert r.iters.tolist() == o["iters"].tolist()
+    assert r.status.tolist() == o["status"].tolist()
+    assert rel(r.cost, o["cost"]) < 1e-8
+    assert rel(r.x, o["x"]) < 1e-8 and rel(r.u, o["u"]) < 1e-8
+
+
+def test_floating_fit_batch_converges_like_the_oracle(gpu):
+    """A batch of 33 perturbed starts at T = 60 until convergence (tol 1e-6): statuses,
+    iteration counts, iterates."""
+    nb, T = 33, 60
+    x, u = script_batch(nb, T, seed=5)
+    s = FloatingSolver(rbd_example_problem(), T, nb)
+    try:
+        r = s.fit(torch.from_numpy(x).cuda(), torch.from_numpy(u).cuda(), max_iter=30, tol=1e-6)
+    finally:
+        s.close()
+    fj, lj, lfj = rbd_floating_arm(jet_ns())
+    o = CF.fit(x, u, fj, lj, lfj, *rbd_cost_quads(), max_iter=30, tol=1e-6)
+    assert r.status.tolist() == o["status"].tolist()
+    assert r.iters.tolist() == o["iters"].tolist()
+    assert rel(r.x, o["x"]) < 1e-8 and rel(r.u, o["u"]) < 1e-8 and rel(r.cost, o["cost"]) < 1e-8
+
+
+def test_api_fit_dispatches_the_recognised_closures(gpu):
+    """ilqr_amd.fit with the family's reference-API callables runs the native fit (same
+    bits as FloatingSolver.fit) and keeps one cached handle."""
+    from ilqr_amd import cache
+    api.clear_cache()
+    p = rbd_example_problem()
+    nb, T = 2, 40
+    x, u = script_batch(nb, T, seed=9)
+    xt, ut = torch.from_numpy(x).cuda(), torch.from_numpy(u).cuda()
+    xf, uf = api.fit(xt, ut, *floating_closures(p), max_iter=6)
+    xf2, uf2 = api.fit(xt, ut, *floating_closures(p), max_iter=6)
+    assert cache.size() == 1
+    s = FloatingSolver(p, T, nb)
+    try:
+        r = s.fit(xt, ut, max_iter=6, tol=1e-6)
+    finally:
+        s.close()
+    assert torch.equal(xf, r.x) and torch.equal(uf, r.u) and torch.equal(xf2, r.x)
+    # the callables evaluate the same functions one point at a time
+    dyn, cost, fcost = floating_closures(p)
+    fj, lj, lfj = rbd_floating_arm(jet_ns())
+    assert rel(dyn(x[0, 0], u[0, 0]), fj(x[:1, 0], u[:1, 0])[0]) < 1e-12
+    assert abs(cost(x[0, 3], u[0, 3]) - float(lj(x[:1, 3], u[:1, 3])[0])) <= 1e-12 * abs(cost(x[0, 3], u[0, 3]))
+    assert abs(fcost(x[0, T]) - float(lfj(x[:1, T])[0])) <= 1e-12 * abs(fcost(x[0, T]))
+    api.clear_cache()
+
+
+def test_floating_nan_state_is_reported(gpu):
+    """A NaN in one trajectory's start stops that trajectory with status NAN; the other
+    one fits as alone (the reference asserts on NaN: forward_pass.jl:89-90)."""
+    nb, T = 2, 30
+    x, u = script_batch(nb, T, seed=13)
+    x[1, 0, 9] = np.nan
+    x[1, 1:] = np.nan
+    s = FloatingSolver(rbd_example_problem(), T, nb)
+    s1 = FloatingSolver(rbd_example_problem(), T, 1)
+    try:
+        r = s.fit(torch.from_numpy(x).cuda(), torch.from_numpy(u).cuda(), max_iter=5)
+        r1 = s1.fit(torch.from_numpy(x[:1].copy()).cuda(), torch.from_numpy(u[:1].copy()).cuda(), max_iter=5)
+    finally:
+        s.close()
+        s1.close()
+    assert r.call_status == _lib.ERR_NAN
+    assert int(r.status[1]) == _lib.TRAJ_NAN
+    assert torch.equal(r.x[0], r1.x[0]) and torch.equal(r.u[0], r1.u[0])
