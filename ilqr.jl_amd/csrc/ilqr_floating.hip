@@ -645,6 +645,11 @@ __global__ __launch_bounds__(64) void fb_forward_kernel(const FbModel* __restric
     alpha *= step;
     if (!__any(live && done_trial == 0)) break;
   }
+  if (live && done_trial <= 0) {  // no trial accepted: x̄, ū = the inputs, as the closure path
+    const size_t nxe = (size_t)(T + 1) * FB_NX, nue = (size_t)T * FB_NU;
+    for (size_t i = c; i < nxe; i += FB_CAND) a.xn[(size_t)b * nxe + i] = a.x[(size_t)b * nxe + i];
+    for (size_t i = c; i < nue; i += FB_CAND) a.un[(size_t)b * nue + i] = a.u[(size_t)b * nue + i];
+  }
   if (live && c == 0) {
     const bool acc = done_trial > 0;
     a.trials[b] = acc ? done_trial : a.max_trials;
@@ -824,6 +829,19 @@ ilqr_status fb_check_options(const ilqr_options* o) {
   return ILQR_OK;
 }
 
+// per-trajectory status → the call status (host copy, synchronising)
+ilqr_status fb_fold(ilqr_floating_handle* h, const int32_t* dev_status) {
+  std::vector<int32_t> st(h->batch);
+  FB_TRY(hipMemcpyAsync(st.data(), dev_status, sizeof(int32_t) * h->batch, hipMemcpyDeviceToHost, h->stream));
+  FB_TRY(hipStreamSynchronize(h->stream));
+  bool nan = false, ls = false;
+  for (int32_t s : st) {
+    nan |= s == ILQR_TRAJ_NAN;
+    ls |= s == ILQR_TRAJ_LS_EXHAUSTED;
+  }
+  return nan ? ILQR_ERR_NAN : (ls ? ILQR_ERR_LS_EXHAUSTED : ILQR_OK);
+}
+
 hipError_t fb_linearize(ilqr_floating_handle* h, const double* x, const double* u, const int32_t* st) {
   const size_t lanes = (size_t)h->batch * h->T * (ilqr::FB_NX + ilqr::FB_NU);
   ilqr::fb_linearize_kernel<<<(unsigned)((lanes + 255) / 256), 256, 0, h->stream>>>(
@@ -944,6 +962,55 @@ ilqr_status ilqr_floating_linearize(ilqr_floating_handle* h, const double* x, co
   FB_TRY(hipMemcpyAsync(A, h->A, 8 * P * ilqr::FB_NX * ilqr::FB_NX, hipMemcpyDeviceToDevice, h->stream));
   FB_TRY(hipMemcpyAsync(B, h->Bm, 8 * P * ilqr::FB_NX * ilqr::FB_NU, hipMemcpyDeviceToDevice, h->stream));
   return ILQR_OK;
+}
+
+ilqr_status ilqr_floating_backward(ilqr_floating_handle* h, const ilqr_options* o, const double* x,
+                                   const double* u, double* d, double* K, int32_t* status) {
+  if (!h || !x || !u || !d || !K) return ILQR_ERR_BAD_ARG;
+  ilqr_status st = fb_check_options(o);
+  if (st != ILQR_OK) return st;
+  FB_TRY(hipSetDevice(h->device));
+  FB_TRY(fb_linearize(h, x, u, nullptr));
+  const ilqr::TileParams tp{h->A, h->Bm, h->lx, h->lu, h->lxx, nullptr, h->luu, h->lfx, h->lfxx};
+  int32_t* sd = status ? status : h->bstatus;
+  FB_TRY(ilqr::launch_tiles_backward(ilqr::FB_NX, ilqr::FB_NU, tp, h->batch, h->T, d, K, sd, fb_ls(o).mu,
+                                     h->stream));
+  return fb_fold(h, sd);
+}
+
+ilqr_status ilqr_floating_forward(ilqr_floating_handle* h, const ilqr_options* o, const double* x,
+                                  const double* u, const double* x_traj, const double* d, const double* K,
+                                  const double* prev_cost, double* x_new, double* u_new, double* new_cost,
+                                  int32_t* trials, int32_t* status) {
+  if (!h || !x || !u || !d || !K || !prev_cost || !x_new || !u_new || !new_cost) return ILQR_ERR_BAD_ARG;
+  ilqr_status st = fb_check_options(o);
+  if (st != ILQR_OK) return st;
+  FB_TRY(hipSetDevice(h->device));
+  const ilqr::LSParams ls = fb_ls(o);
+  ilqr::FbFwd fa{};
+  fa.x = x;
+  fa.u = u;
+  fa.xtraj = x_traj;
+  fa.d = d;
+  fa.K = K;
+  fa.prev_cost = prev_cost;
+  fa.xn = x_new;
+  fa.un = u_new;
+  fa.new_cost = new_cost;
+  fa.du2 = h->du2;
+  fa.trials = trials ? trials : h->trials;
+  fa.fstatus = status ? status : h->fstatus;
+  fa.status = nullptr;
+  fa.alpha0 = ls.alpha0;
+  fa.shrink = ls.shrink;
+  fa.max_trials = ls.max_trials;
+  ilqr::fb_forward_kernel<<<(unsigned)((h->batch * ilqr::FB_CAND + 63) / 64), 64, 0, h->stream>>>(
+      h->model_dev, h->batch, h->T, fa);
+  FB_TRY(hipGetLastError());
+  // x̄, ū of a trajectory whose first trial was accepted are written as it rolled out; a
+  // later accepted trial is rolled out again by its lane (storing); a search that accepted
+  // nothing returns x, u (the closure path's rollout_forward does the same)
+  return fb_fold(h, fa.fstatus);
 }
 
 ilqr_status ilqr_floating_fit(ilqr_floating_handle* h, const ilqr_options* o, const double* x_init,

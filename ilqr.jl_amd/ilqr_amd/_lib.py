@@ -178,6 +178,8 @@ SIGNATURES = {
     "ilqr_floating_sync": (C.c_int, [P]),
     "ilqr_floating_dynamics": (C.c_int, [P, P, P, P, C.c_int]),
     "ilqr_floating_linearize": (C.c_int, [P, P, P, P, P]),
+    "ilqr_floating_backward": (C.c_int, [P, C.POINTER(Options), P, P, P, P, P]),
+    "ilqr_floating_forward": (C.c_int, [P, C.POINTER(Options), P, P, P, P, P, P, P, P, P, P, P]),
     "ilqr_floating_fit": (C.c_int, [P, C.POINTER(Options), P, P, P, P, P, P, P, P]),
 }
 

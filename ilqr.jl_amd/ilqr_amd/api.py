@@ -170,9 +170,7 @@ def backward_pass(x, u, dynamicsf, immediate_cost, final_cost):
             d, K, st = s.backward_tiles(tl)
     elif fam == "floating":
         with _floating_solver(xb, ub, dynamicsf, immediate_cost, final_cost) as s:
-            r = s.fit(xb.to(torch.float64).contiguous(), ub.to(torch.float64).contiguous(),
-                      x_traj=None if xt is None else xt.to(torch.float64).contiguous(),
-                      max_iter=int(max_iter), tol=float(tol))
+            d, K, st = s.backward(xb, ub)
     elif fam == "chain":
         dt = _eltype(x)
         xb, ub = xb.to(dt), ub.to(dt)
@@ -210,6 +208,10 @@ def forward_pass(x, u, x_traj, du, K, prev_cost, dynamicsf, immediate_cost, fina
         xn, un, cost, trials, st = s.forward(xb.to(dt), ub.to(dt), db.to(dt), Kb.to(dt),
                                              pc.to(dt), x_traj=xt.to(dt), options=o)
         s.close()
+    elif fam == "floating":
+        with _floating_solver(xb, ub, dynamicsf, immediate_cost, final_cost) as s:
+            o = _lib.default_options(max_trials=max_trials)
+            xn, un, cost, trials, st = s.forward(xb, ub, db, Kb, pc, x_traj=xt, options=o)
     elif fam == "closures":
         xn, un, cost, trials, ok = _tiles.rollout_forward(
             xb, ub, xt, db, Kb, pc, dynamicsf, immediate_cost, final_cost,
@@ -249,6 +251,9 @@ def fit(x_init, u_init, dynamicsf, immediate_cost, final_cost, *, x_traj=None,
     if fam == "closures":
         r = _fit_closures(xb, ub, xt, dynamicsf, immediate_cost, final_cost, int(max_iter),
                           float(tol), history=verbose or return_info)
+    elif fam == "floating":
+        with _floating_solver(xb, ub, dynamicsf, immediate_cost, final_cost) as s:
+            r = s.fit(xb, ub, x_traj=xt, max_iter=int(max_iter), tol=float(tol))
     elif fam == "chain":
         dt = _eltype(x_init)
         s = _chain_solver(xb, ub, dynamicsf, immediate_cost, final_cost, dt)

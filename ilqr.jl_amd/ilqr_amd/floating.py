@@ -177,6 +177,39 @@ class FloatingSolver:
                    "ilqr_floating_linearize")
         return A, Bm
 
+    def backward(self, x, u, options=None):
+        """iLQR.backward_pass → (d (B,T,nu), K (B,T,nu,nx), status (B,)); synchronises."""
+        self._xu(x, u)
+        d = self._new(self.batch, self.T, self.nu)
+        K = self._new(self.batch, self.T, self.nu, self.nx)
+        st = self._new(self.batch, dtype=torch.int32)
+        o = options or _lib.default_options()
+        self._bind()
+        _lib.check(self.lib.ilqr_floating_backward(self.h, C.byref(o), _ptr(x), _ptr(u), _ptr(d), _ptr(K),
+                                                   _ptr(st)), "ilqr_floating_backward", allow=(_lib.ERR_NAN,))
+        return d, K, st
+
+    def forward(self, x, u, d, K, prev_cost, x_traj=None, options=None):
+        """iLQR.forward_pass → (x̄, ū, new_cost, trials, status); synchronises."""
+        self._xu(x, u)
+        B, T = self.batch, self.T
+        _req(d, torch.float64, (B, T, self.nu), "d")
+        _req(K, torch.float64, (B, T, self.nu, self.nx), "K")
+        _req(prev_cost, torch.float64, (B,), "prev_cost")
+        if x_traj is not None:
+            _req(x_traj, torch.float64, (B, T + 1, self.nx), "x_traj")
+        xn, un = torch.empty_like(x), torch.empty_like(u)
+        cost = self._new(B)
+        trials = self._new(B, dtype=torch.int32)
+        st = self._new(B, dtype=torch.int32)
+        o = options or _lib.default_options()
+        self._bind()
+        _lib.check(self.lib.ilqr_floating_forward(self.h, C.byref(o), _ptr(x), _ptr(u), _ptr(x_traj), _ptr(d),
+                                                  _ptr(K), _ptr(prev_cost), _ptr(xn), _ptr(un), _ptr(cost),
+                                                  _ptr(trials), _ptr(st)),
+                   "ilqr_floating_forward", allow=(_lib.ERR_NAN, _lib.ERR_LS_EXHAUSTED))
+        return xn, un, cost, trials, st
+
     def fit(self, x_init, u_init, max_iter=100, tol=1e-6, x_traj=None, options=None) -> FitResult:
         """iLQR.fit (forward_pass.jl:148-179) for the whole batch; synchronises."""
         self._xu(x_init, u_init)

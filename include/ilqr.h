@@ -508,6 +508,15 @@ ilqr_status ilqr_floating_dynamics(ilqr_floating_handle* h, const double* x, con
  * u (batch, T, nu) → A (batch, T, nx, nx), B (batch, T, nx, nu) */
 ilqr_status ilqr_floating_linearize(ilqr_floating_handle* h, const double* x, const double* u,
                                     double* A, double* B);
+/* iLQR.backward_pass / forward_pass (backward_pass.jl:324-357, forward_pass.jl:55-93)
+ * for every trajectory; arguments, status and return semantics as ilqr_chain_backward /
+ * ilqr_chain_forward (x_traj may be NULL; trials and status may be NULL). Synchronise. */
+ilqr_status ilqr_floating_backward(ilqr_floating_handle* h, const ilqr_options* o, const double* x,
+                                   const double* u, double* d, double* K, int32_t* status);
+ilqr_status ilqr_floating_forward(ilqr_floating_handle* h, const ilqr_options* o, const double* x,
+                                  const double* u, const double* x_traj, const double* d,
+                                  const double* K, const double* prev_cost, double* x_new,
+                                  double* u_new, double* new_cost, int32_t* trials, int32_t* status);
 /* iLQR.fit (forward_pass.jl:148-179) for every trajectory: arguments, per-trajectory
  * status and the call status as ilqr_fit (x_traj may be NULL: zeros; cost, iters,
  * status may be NULL). Synchronises. */

@@ -159,3 +159,34 @@ def test_floating_nan_state_is_reported(gpu):
     assert r.call_status == _lib.ERR_NAN
     assert int(r.status[1]) == _lib.TRAJ_NAN
     assert torch.equal(r.x[0], r1.x[0]) and torch.equal(r.u[0], r1.u[0])
+
+
+def test_floating_backward_forward_vs_closure_oracle(gpu):
+    """backward_pass / forward_pass one at a time (ilqr_floating_backward / _forward, and
+    ilqr_amd.backward_pass / forward_pass with the family's callables) against the closure
+    oracle's tiles recursion and rollout, including a forward that must halve α."""
+    from oracle import cref
+    nb, T = 3, 80
+    x, u = script_batch(nb, T, seed=17)
+    p = rbd_example_problem()
+    fj, lj, lfj = rbd_floating_arm(jet_ns())
+    tl = CF.derivative_tiles(x, u, fj, *rbd_cost_quads())
+    d_o, K_o, _ = cref.tiles_backward(tl, mu=0.01, symmetrize=True)
+    xt, ut = torch.from_numpy(x).cuda(), torch.from_numpy(u).cuda()
+    d, K = api.backward_pass(xt, ut, *floating_closures(p))
+    assert rel(d, d_o) < 1e-9 and rel(K, K_o) < 1e-9
+    # prev_cost: Inf (accept trial 1), the oracle's trial-1 cost minus a bit on trajectory 0
+    # (trial 1 rejected there, a later α accepted)
+    _, _, c1, _, _ = CF.forward_pass(x, u, np.zeros_like(x), d_o, K_o, np.full(nb, np.inf), fj, lj, lfj)
+    prev = np.full(nb, np.inf)
+    prev[0] = c1[0] * (1.0 - 1e-9)
+    xo, uo, co, tro, ok = CF.forward_pass(x, u, np.zeros_like(x), d_o, K_o, prev, fj, lj, lfj)
+    s = FloatingSolver(p, T, nb)
+    try:
+        xn, un, cost, trials, st = s.forward(xt, ut, torch.from_numpy(d_o).cuda(), torch.from_numpy(K_o).cuda(),
+                                             torch.from_numpy(prev).cuda())
+    finally:
+        s.close()
+    assert trials.tolist() == tro.tolist() and st.tolist() == [0 if a else 3 for a in ok]
+    assert rel(cost, co) < 1e-10 and rel(xn, xo) < 1e-10 and rel(un, uo) < 1e-10
+    assert int(trials[0]) > 1
