@@ -206,6 +206,13 @@ def secondary_configs(device):
             out[name] = bench_tiles.measure(*args, reps=20, device=device)
         except Exception as e:  # reported, never required
             out[name] = {"error": repr(e)}
+    # the reference's RBD script (animate_RBD_2_link.jl: floating 2Dof_arm, nx = 16, nu = 8,
+    # T = 1000, one trajectory) fitted natively by the floating-base family
+    from tools import bench_floating
+    try:
+        out["rbd_floating_native_B1_T1000"] = bench_floating.measure(1, iters=3, reps=2)
+    except Exception as e:  # reported, never required
+        out["rbd_floating_native_B1_T1000"] = {"error": repr(e)}
     return out
 
 

@@ -890,4 +890,57 @@ function chain_fit(c::Chain, x_init::Array{E,3}, u_init::Array{E,3}; max_iter::I
     return x, u, status
 end
 
+# -- floating-base RBD family: the reference's RBD script as it runs --------------------
+struct FloatingModel          # ilqr_floating (include/ilqr.h), ILQR_FLOATING_MAX_JOINTS = 2
+    n_joints::Int32; dt::Float64; gravity::NTuple{3,Float64}
+    base_mass::Float64; base_com::NTuple{3,Float64}; base_inertia::NTuple{9,Float64}
+    joint_rot::NTuple{18,Float64}; joint_pos::NTuple{6,Float64}; axis::NTuple{6,Float64}
+    mass::NTuple{2,Float64}; com::NTuple{6,Float64}; inertia::NTuple{18,Float64}
+    target::NTuple{8,Float64}; q_weight::NTuple{8,Float64}; r_weight::NTuple{8,Float64}
+    qf_weight::NTuple{8,Float64}
+    q_scale::Float64; r_scale::Float64; qf_scale::Float64
+end
+
+"""The model behind test/RBD_2_link_example: test/urdf/2Dof_arm.urdf parsed with
+`floating = true, gravity = 0` (RBD_helper_functions.jl:7) — a 30 kg base (50·I), two
+3 kg links (0.5·I) on joints at (.5, .5, 0) about z and (1, 0, 0) about y — with the
+script's Δt, target_pose and cost weights (animate_RBD_2_link.jl:8-10,
+RBD_helper_functions.jl:85-116)."""
+function rbd_2dof_arm_floating(; target=(0., 0., 0., 5., 1., 2., 1., .3))
+    I3 = (1., 0., 0., 0., 1., 0., 0., 0., 1.)
+    FloatingModel(Int32(2), 0.01, (0., 0., 0.), 30.0, (0., 0., 0.), 50.0 .* I3,
+                  (I3..., I3...), (.5, .5, 0., 1., 0., 0.), (0., 0., 1., 0., 1., 0.),
+                  (3.0, 3.0), ntuple(_ -> 0.0, 6), (0.5 .* I3..., 0.5 .* I3...),
+                  Tuple(Float64.(target)), (100., 100., 100., 1., 1., 1., 10., 10.),
+                  (1., 1., 1., 100., 100., 100., 10., 10.),
+                  (100., 100., 100., 1000., 1000., 1000., 10., 10.), 10.0, 1.0, 100000.0)
+end
+
+"""floating_fit(model, x_init, u_init; max_iter, tol) → (x̄, ū, status)
+
+iLQR.fit of the floating-base family on the device (include/ilqr.h ilqr_floating_fit):
+x_init (16, T+1, batch) = [MRP; r; θ; ω; v; θ̇], u_init (8, T, batch), as the script's
+`state_traj` / `input_traj` transposed (animate_RBD_2_link.jl:19-25)."""
+function floating_fit(m::FloatingModel, x_init::Array{Float64,3}, u_init::Array{Float64,3};
+                      max_iter::Int64=100, tol::Float64=1e-6)
+    nx, N, nb = size(x_init); nu = size(u_init, 1); M = N - 1
+    @assert(size(u_init, 2) == M)
+    r = Ref{Ptr{Cvoid}}(C_NULL)
+    check(ccall((:ilqr_floating_create, libilqr), Cint, (Ref{Ptr{Cvoid}}, Cint, Ref{FloatingModel}, Cint, Cint),
+                r, 0, m, M, nb), "ilqr_floating_create")
+    h = Handle(nx, nu, M, 1)                 # device-memory helper only
+    xi = upload(h, x_init); ui = upload(h, u_init)
+    xo = alloc(h, Float64, length(x_init)); uo = alloc(h, Float64, length(u_init)); sd = alloc(h, Int32, nb)
+    o = default_options(); o.max_iter = max_iter; o.tol = tol
+    st = ccall((:ilqr_floating_fit, libilqr), Cint,
+               (Ptr{Cvoid}, Ref{Options}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64},
+                Ptr{Float64}, Ptr{Int32}, Ptr{Int32}),
+               r[], o, xi, ui, C_NULL, xo, uo, C_NULL, C_NULL, sd)
+    st == ILQR_ERR_LS_EXHAUSTED || check(st, "ilqr_floating_fit")
+    x = download!(h, similar(x_init), xo); u = download!(h, similar(u_init), uo)
+    status = download!(h, zeros(Int32, nb), sd)
+    ccall((:ilqr_floating_destroy, libilqr), Cint, (Ptr{Cvoid},), r[])
+    return x, u, status
+end
+
 end # module

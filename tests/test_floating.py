@@ -71,3 +71,30 @@ def test_no_base_mass_is_refused():
     p.chain.base_mass = 0.0
     with pytest.raises(ValueError):
         FloatingProblem(p.chain).struct()
+
+
+def _julia_struct_layout(name):
+    """(size, [offsets]) of a Julia isbits struct of Int32 / Float64 / NTuple{n,Float64}
+    fields as declared in the shim, under C alignment rules (what ccall passes)."""
+    import re
+    src = open(os.path.join(ROOT, "ilqr.jl_amd", "julia", "iLQRHIP.jl")).read()
+    body = src[src.index(f"struct {name}"):]
+    body = body[body.index("\n") + 1:body.index("\nend")]
+    fields = re.findall(r"(\w+)::(Int32|Float64|NTuple\{(\d+),Float64\})", body)
+    off, offs, align = 0, [], 1
+    for _, ty, n in fields:
+        size, a = (4, 4) if ty == "Int32" else ((8, 8) if ty == "Float64" else (8 * int(n), 8))
+        off = (off + a - 1) // a * a
+        offs.append(off)
+        off += size
+        align = max(align, a)
+    return (off + align - 1) // align * align, offs, [f[0] for f in fields]
+
+
+def test_julia_floating_model_matches_the_c_layout():
+    """The shim's FloatingModel (passed by Ref to ilqr_floating_create) has the C struct's
+    field order, offsets and size (the shim cannot run here)."""
+    size, offs, names = _julia_struct_layout("FloatingModel")
+    assert names == [f[0] for f in _lib.FloatingStruct._fields_]
+    assert size == C.sizeof(_lib.FloatingStruct)
+    assert offs == [getattr(_lib.FloatingStruct, f).offset for f in names]
