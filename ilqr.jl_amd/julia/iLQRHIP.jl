@@ -887,6 +887,7 @@ function chain_fit(c::Chain, x_init::Array{E,3}, u_init::Array{E,3}; max_iter::I
     x = download!(h, similar(x_init), xo); u = download!(h, similar(u_init), uo)
     status = download!(h, zeros(Int32, nb), sd)
     ccall((:ilqr_chain_destroy, libilqr), Cint, (Ptr{Cvoid},), r[])
+    close(h)
     return x, u, status
 end
 
@@ -940,6 +941,7 @@ function floating_fit(m::FloatingModel, x_init::Array{Float64,3}, u_init::Array{
     x = download!(h, similar(x_init), xo); u = download!(h, similar(u_init), uo)
     status = download!(h, zeros(Int32, nb), sd)
     ccall((:ilqr_floating_destroy, libilqr), Cint, (Ptr{Cvoid},), r[])
+    close(h)
     return x, u, status
 end
 
