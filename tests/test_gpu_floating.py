@@ -190,3 +190,27 @@ def test_floating_backward_forward_vs_closure_oracle(gpu):
     assert trials.tolist() == tro.tolist() and st.tolist() == [0 if a else 3 for a in ok]
     assert rel(cost, co) < 1e-10 and rel(xn, xo) < 1e-10 and rel(un, uo) < 1e-10
     assert int(trials[0]) > 1
+
+
+def test_floating_fit_x_traj_and_edges(gpu):
+    """x_traj enters the line search's cost (forward_pass.jl:187-190) as in the oracle;
+    max_iter = 0 returns the inputs (status MAX_ITER); two fits on one handle are
+    bit-identical."""
+    nb, T = 2, 40
+    x, u = script_batch(nb, T, seed=21)
+    xtraj = 0.1 * np.random.default_rng(3).standard_normal(x.shape)
+    xt, ut, xtr = (torch.from_numpy(a).cuda() for a in (x, u, xtraj))
+    s = FloatingSolver(rbd_example_problem(), T, nb)
+    try:
+        r = s.fit(xt, ut, max_iter=5, tol=1e-6, x_traj=xtr)
+        r2 = s.fit(xt, ut, max_iter=5, tol=1e-6, x_traj=xtr)
+        r0 = s.fit(xt, ut, max_iter=0)
+    finally:
+        s.close()
+    fj, lj, lfj = rbd_floating_arm(jet_ns())
+    o = CF.fit(x, u, fj, lj, lfj, *rbd_cost_quads(), x_traj=xtraj, max_iter=5, tol=1e-6)
+    assert r.iters.tolist() == o["iters"].tolist() and r.status.tolist() == o["status"].tolist()
+    assert rel(r.x, o["x"]) < 1e-8 and rel(r.cost, o["cost"]) < 1e-8
+    assert torch.equal(r.x, r2.x) and torch.equal(r.u, r2.u) and torch.equal(r.cost, r2.cost)
+    assert torch.equal(r0.x, xt) and torch.equal(r0.u, ut)
+    assert r0.status.tolist() == [_lib.TRAJ_MAX_ITER] * nb and r0.iters.tolist() == [0] * nb
