@@ -471,7 +471,7 @@ __global__ __launch_bounds__(64 * FUSED_WAVES) void lq_iter_fused4_kernel(LQPara
     }
   }
 #if ILQR_FUSED_DEPHASE_PROBE
-  // TIMING-ONLY probe (tools/dephase_probe.sh, not the product): half of the waves
+  // TIMING-ONLY probe (tools/archive/r05/dephase_probe.sh, not the product): half of the waves
   // (PROBE 1: odd waves of every workgroup; 2: odd workgroups) run the forward FIRST on
   // the gains already in K/d, then the backward — the phase mix of a de-phased schedule
   // (forward(i−1) then backward(i) beside backward(i) then forward(i)) at one wave/SIMD.

@@ -21,7 +21,7 @@ the rollout calls the user's dynamics, so it runs as torch ops on the device
 (control law :72-73 + dynamics :74) is captured once per (closure, shape) in a HIP
 graph and replayed T times per line-search trial: a closure of a few hundred small ops
 (the reference's RBD caller) then costs one graph launch per step instead of a few
-hundred dispatches (tools/rollout_probe.py: 4.0 → 0.73 ms per step at nx = 16, B = 1).
+hundred dispatches (tools/archive/r05/rollout_probe.py: 4.0 → 0.73 ms per step at nx = 16, B = 1).
 The capture is checked against an eager step bit for bit before it is used; closures
 that cannot be captured (a host synchronisation inside them) run eagerly.
 ILQR_ROLLOUT_GRAPH=0 turns the graphs off.

@@ -1,8 +1,8 @@
 #!/bin/bash
 # Build libilqr_hip.so of another git revision for an A/B on one box:
-#   tools/build_rev_lib.sh <rev> <name>  →  tools/fwalt/libilqr_hip_<name>.so
+#   tools/archive/r05/build_rev_lib.sh <rev> <name>  →  tools/fwalt/libilqr_hip_<name>.so
 set -e
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../../.."
 rev=$1; name=$2
 tmp=$(mktemp -d)
 git archive "$rev" ilqr.jl_amd/csrc include | tar -x -C "$tmp"

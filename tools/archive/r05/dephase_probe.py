@@ -1,7 +1,7 @@
 """Timing of the fused iteration launch (fit's first iteration, repeated on the same
 inputs: prev_cost = Inf, every trajectory accepts trial 1) with the product build and
-the two timing-only phase-mix builds of tools/dephase_probe.sh, each in its own process
-on one box: `python tools/dephase_probe.py [lib.so]`."""
+the two timing-only phase-mix builds of tools/archive/r05/dephase_probe.sh, each in its own process
+on one box: `python tools/archive/r05/dephase_probe.py [lib.so]`."""
 import ctypes as C
 import os
 import sys
@@ -9,7 +9,7 @@ import time
 
 import torch
 
-R = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+R = os.path.dirname(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 sys.path[:0] = [R, os.path.join(R, "ilqr.jl_amd")]
 from ilqr_amd import _lib  # noqa: E402
 from ilqr_amd.problems import quadrotor_batch  # noqa: E402

@@ -1,9 +1,9 @@
 #!/bin/bash
 # Timing-only builds of the fused iteration with half of the waves in the other phase
 # order (ILQR_FUSED_DEPHASE_PROBE, ilqr_bw4.hip): tools/fwalt/libilqr_hip_dephase{1,2,3,4}.so,
-# timed against the product by tools/dephase_probe.py (round 5).
+# timed against the product by tools/archive/r05/dephase_probe.py (round 5).
 set -e
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../../.."
 make -C ilqr.jl_amd/csrc > /dev/null
 mkdir -p tools/fwalt
 O=ilqr.jl_amd/lib/obj

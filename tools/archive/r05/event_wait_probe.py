@@ -1,5 +1,5 @@
 """Host CPU time of hipEventSynchronize on a ~5 ms kernel with event flags 0, blocking-sync,
-and of a nap-then-spin poll on hipEventQuery (round 5, tools/spin_probe.py follow-up)."""
+and of a nap-then-spin poll on hipEventQuery (round 5, tools/archive/r05/spin_probe.py follow-up)."""
 import ctypes as C
 import resource
 import time

@@ -3,14 +3,14 @@ nu = 8: tests/closures.py rbd_floating_arm) at B = 1, four ways: vmap on the dev
 ilqr_amd.tiles.rollout_forward does), the closure called on the batch directly, one
 step captured in a HIP graph and replayed, and a graph of S unrolled steps.
 
-    PYTHONPATH=.:ilqr.jl_amd:tests python tools/rollout_probe.py
+    PYTHONPATH=.:ilqr.jl_amd:tests python tools/archive/r05/rollout_probe.py
 """
 import json
 import os
 import sys
 import time
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 for p in (ROOT, os.path.join(ROOT, "ilqr.jl_amd"), os.path.join(ROOT, "tests")):
     if p not in sys.path:
         sys.path.insert(0, p)

@@ -1,5 +1,5 @@
 """Host CPU time held by the end-of-fit wait, one library per
-process: `python tools/spin_probe.py [lib.so]`. Per case, median wall ms per fit and
+process: `python tools/archive/r05/spin_probe.py [lib.so]`. Per case, median wall ms per fit and
 the host CPU ms the calling process used per fit (getrusage: every thread, including
 ilqr_multi's shard threads):
   headline  the 3-iteration LQ fit from cold (12×4, T=100, B=4096) — must stay fast;
@@ -14,7 +14,7 @@ import time
 import numpy as np
 import torch
 
-R = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+R = os.path.dirname(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 sys.path[:0] = [R, os.path.join(R, "ilqr.jl_amd")]
 from ilqr_amd import _lib  # noqa: E402
 
