@@ -119,7 +119,21 @@ def _crm_basis():
     return np.stack(cols, axis=1)
 
 
-def rbd_floating_arm(ns, dt=0.01):
+ARM_2DOF = {  # test/urdf/2Dof_arm.urdf (ilqr_amd/robots/2dof_arm.json)
+    "base_mass": 30.0, "base_com": (0.0, 0.0, 0.0), "base_Ic": 50.0 * np.eye(3),
+    "R0": (np.eye(3), np.eye(3)), "p": ((0.5, 0.5, 0.0), (1.0, 0.0, 0.0)),
+    "axis": ((0.0, 0.0, 1.0), (0.0, 1.0, 0.0)), "mass": (3.0, 3.0),
+    "com": ((0.0, 0.0, 0.0), (0.0, 0.0, 0.0)), "Ic": (0.5 * np.eye(3), 0.5 * np.eye(3))}
+
+
+def spatial_inertia(m, c, Ic):
+    """Featherstone's rigid-body inertia about the body origin, angular first:
+    [[Ic + m[c×][c×]ᵀ, m[c×]], [m[c×]ᵀ, m1]]."""
+    cx = _skew(np.asarray(c, float))
+    return np.block([[np.asarray(Ic, float) + m * cx @ cx.T, m * cx], [m * cx.T, m * np.eye(3)]])
+
+
+def rbd_floating_arm(ns, dt=0.01, model=None):
     """test/RBD_2_link_example/RBD_helper_functions.jl:48-116 written with array ops —
     the closures a user of the generic path would write for animate_RBD_2_link.jl:
     nx = 16 ([MRP p (3); base position r (3); θ (2); ω (3); v (3); θ̇ (2)]), nu = 8
@@ -135,21 +149,26 @@ def rbd_floating_arm(ns, dt=0.01):
     written: q̇ = [pdot_from_w(p, ω); v; θ̇] (Attitude.jl's MRP rate; the base position
     integrates v as is). Parity vs RigidBodyDynamics.jl: unpinned (not runnable here).
     Works on 1-D tensors (torch.func) and on (P, n) numpy arrays / oracle.jet Jets."""
-    I0 = np.diag([50.0, 50.0, 50.0, 30.0, 30.0, 30.0])
-    I1 = I2 = np.diag([0.5, 0.5, 0.5, 3.0, 3.0, 3.0])
+    md = ARM_2DOF if model is None else model
+    if model is None:
+        I0 = np.diag([50.0, 50.0, 50.0, 30.0, 30.0, 30.0])
+        I1 = I2 = np.diag([0.5, 0.5, 0.5, 3.0, 3.0, 3.0])
+    else:  # another mechanism of the same shape (a floating base, two revolute joints)
+        I0 = spatial_inertia(md["base_mass"], md["base_com"], md["base_Ic"])
+        I1, I2 = (spatial_inertia(md["mass"][i], md["com"][i], md["Ic"][i]) for i in (0, 1))
 
-    def joint(r, a):
-        r, a = np.asarray(r, float), np.asarray(a, float)
+    def joint(r, a, R0):
+        r, a, R0 = np.asarray(r, float), np.asarray(a, float), np.asarray(R0, float)
         Xt = np.eye(6)
         Xt[3:, :3] = -_skew(r)
         aa = np.outer(a, a)
         bd = lambda m: np.block([[m, np.zeros((3, 3))], [np.zeros((3, 3)), m]])  # noqa: E731
         S = np.concatenate([a, np.zeros(3)])
-        # X(θ) = blockdiag(E, E)·Xt, E = Rot(a, θ)ᵀ = cos θ (1 − aaᵀ) − sin θ [a×] + aaᵀ
-        return bd(np.eye(3) - aa) @ Xt, bd(-_skew(a)) @ Xt, bd(aa) @ Xt, S
+        # X(θ) = blockdiag(E, E)·Xt, E = (R0·Rot(a, θ))ᵀ = (cos θ (1 − aaᵀ) − sin θ [a×] + aaᵀ)·R0ᵀ
+        return bd((np.eye(3) - aa) @ R0.T) @ Xt, bd(-_skew(a) @ R0.T) @ Xt, bd(aa @ R0.T) @ Xt, S
 
-    C1a, C1b, C1c, S1n = joint((0.5, 0.5, 0.0), (0.0, 0.0, 1.0))
-    C2a, C2b, C2c, S2n = joint((1.0, 0.0, 0.0), (0.0, 1.0, 0.0))
+    C1a, C1b, C1c, S1n = joint(md["p"][0], md["axis"][0], md["R0"][0])
+    C2a, C2b, C2c, S2n = joint(md["p"][1], md["axis"][1], md["R0"][1])
     m22 = float(S2n @ I2 @ S2n)
     K = ns.const
     I0c, I1c, I2c = K(I0), K(I1), K(I2)
@@ -293,3 +312,36 @@ def coupled_pendula_arr(ns, dt=0.05):
         return 5.0 * (x[..., 0] * x[..., 0] + x[..., 1] * x[..., 1]) + x[..., 2] * x[..., 2] + x[..., 3] * x[..., 3]
 
     return dynamicsf, immediate_cost, final_cost
+
+
+def coupled_floating_model():
+    """A floating two-joint mechanism without the 2Dof_arm's symmetries (not a reference
+    robot): the base's COM off its origin with products of inertia, joint 1 tilted about
+    x, joint 2 turned about z with an oblique axis, COMs off the joint origins,
+    anisotropic link inertias — every term of the floating-base dynamics nonzero."""
+    def rx(a):
+        c, s = np.cos(a), np.sin(a)
+        return np.array([[1.0, 0.0, 0.0], [0.0, c, -s], [0.0, s, c]])
+
+    def rz(a):
+        c, s = np.cos(a), np.sin(a)
+        return np.array([[c, -s, 0.0], [s, c, 0.0], [0.0, 0.0, 1.0]])
+    ax2 = np.array([0.0, 1.0, 0.2]) / np.linalg.norm([0.0, 1.0, 0.2])
+    return {"base_mass": 20.0, "base_com": (0.1, -0.05, 0.02),
+            "base_Ic": np.array([[8.0, 0.3, -0.2], [0.3, 6.0, 0.1], [-0.2, 0.1, 7.0]]),
+            "R0": (rx(0.3), rz(0.2)), "p": ((0.5, 0.5, 0.0), (1.0, 0.0, 0.1)),
+            "axis": ((0.0, 0.0, 1.0), tuple(ax2)), "mass": (3.0, 2.0),
+            "com": ((0.10, 0.05, 0.20), (0.30, 0.05, -0.15)),
+            "Ic": (np.array([[0.40, 0.02, 0.01], [0.02, 0.60, 0.03], [0.01, 0.03, 0.30]]),
+                   np.array([[0.20, 0.01, -0.02], [0.01, 0.35, 0.015], [-0.02, 0.015, 0.25]]))}
+
+
+def floating_energy(x, model=None):
+    """½ vᵀ M(θ) v of floating states x (P, 16) under rbd_floating_arm's model: conserved
+    by the continuous dynamics at u = 0 and zero gravity (a check that the mass matrix
+    and the bias are one mechanism's)."""
+    ns = jet_ns()
+    f, _, _ = rbd_floating_arm(ns, model=model)
+    M = f.mass_matrix(np.asarray(x, float))
+    v = np.asarray(x, float)[:, 8:16]
+    return 0.5 * np.einsum("pi,pij,pj->p", v, M, v)

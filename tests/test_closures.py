@@ -207,3 +207,23 @@ def test_rollout_graph_bookkeeping_on_cpu():
     del g
     gc.collect()
     assert wr() is None and len(tiles._GRAPHS) == n - 1
+
+
+def test_floating_restatement_conserves_energy():
+    """With u = 0 and zero gravity the floating mechanism's kinetic energy is conserved
+    (up to RK4's O(dt⁴) error): the restated mass matrix and Newton-Euler bias belong
+    to one mechanism — for the 2Dof_arm and for a model with every term nonzero."""
+    from closures import coupled_floating_model, floating_energy, jet_ns, rbd_floating_arm
+    rng = np.random.default_rng(4)
+    for model in (None, coupled_floating_model()):
+        f, _, _ = rbd_floating_arm(jet_ns(), model=model)
+        x = np.zeros((6, 16))
+        x[:, 0:3] = 0.3 * rng.standard_normal((6, 3))
+        x[:, 6:8] = rng.uniform(-2, 2, (6, 2))
+        x[:, 8:16] = rng.standard_normal((6, 8))
+        e0 = floating_energy(x, model)
+        u = np.zeros((6, 8))
+        for _ in range(200):
+            x = f(x, u)
+        e1 = floating_energy(x, model)
+        assert np.abs(e1 - e0).max() / e0.max() < 1e-7, (e0, e1)

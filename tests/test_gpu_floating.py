@@ -214,3 +214,56 @@ def test_floating_fit_x_traj_and_edges(gpu):
     assert torch.equal(r.x, r2.x) and torch.equal(r.u, r2.u) and torch.equal(r.cost, r2.cost)
     assert torch.equal(r0.x, xt) and torch.equal(r0.u, ut)
     assert r0.status.tolist() == [_lib.TRAJ_MAX_ITER] * nb and r0.iters.tolist() == [0] * nb
+
+
+def _problem_of(model):
+    from ilqr_amd.floating import FloatingProblem
+    from ilqr_amd.urdf import Chain
+    ch = Chain(["j1", "j2"], np.array(model["R0"], float), np.array(model["p"], float),
+               np.array(model["axis"], float), np.array(model["mass"], float), np.array(model["com"], float),
+               np.array(model["Ic"], float), np.zeros(3), float(model["base_mass"]),
+               np.array(model["base_com"], float), np.array(model["base_Ic"], float))
+    return FloatingProblem(ch)
+
+
+def test_floating_general_mechanism_vs_restatement(gpu):
+    """A mechanism with every term nonzero (tests/closures.py coupled_floating_model:
+    tilted and oblique joints, COMs off the joint origins, a base with products of
+    inertia): one step, the Jacobians, a fit and energy conservation at u = 0."""
+    from closures import coupled_floating_model, floating_energy
+    md = coupled_floating_model()
+    p = _problem_of(md)
+    fj, lj, lfj = rbd_floating_arm(jet_ns(), model=md)
+    x, u = random_states(129, seed=8)
+    s = FloatingSolver(p, 1, 1)
+    try:
+        y = s.dynamics(torch.from_numpy(x).cuda(), torch.from_numpy(u).cuda())
+        # energy at u = 0 over 200 steps on the device
+        xe = torch.from_numpy(x[:8].copy()).cuda()
+        z = torch.zeros(8, 8, dtype=torch.float64, device="cuda")
+        e0 = floating_energy(x[:8], md)
+        for _ in range(200):
+            xe = s.dynamics(xe, z)
+        e1 = floating_energy(xe.cpu().numpy(), md)
+    finally:
+        s.close()
+    assert rel(y, fj(x, u)) < 1e-12
+    assert np.abs(e1 - e0).max() / e0.max() < 1e-7
+    nb, T = 2, 50
+    x0 = np.zeros((nb, T + 1, 16))
+    x0[:, 0] = rbd_initial_state()
+    x0[1, 0, 8:] = 0.05
+    uu = np.zeros((nb, T, 8))
+    for t in range(T):
+        x0[:, t + 1] = fj(x0[:, t], uu[:, t])
+    s = FloatingSolver(p, T, nb)
+    try:
+        A, Bm = s.linearize(torch.from_numpy(x0).cuda(), torch.from_numpy(uu).cuda())
+        r = s.fit(torch.from_numpy(x0).cuda(), torch.from_numpy(uu).cuda(), max_iter=4)
+    finally:
+        s.close()
+    Aj, Bj = jet.jacobians(fj, x0[:, :T].reshape(-1, 16), uu.reshape(-1, 8))
+    assert rel(A.reshape(-1, 16, 16), Aj) < 1e-10 and rel(Bm.reshape(-1, 16, 8), Bj) < 1e-10
+    o = CF.fit(x0, uu, fj, lj, lfj, *rbd_cost_quads(), max_iter=4)
+    assert r.iters.tolist() == o["iters"].tolist() and r.status.tolist() == o["status"].tolist()
+    assert rel(r.x, o["x"]) < 1e-8 and rel(r.u, o["u"]) < 1e-8
