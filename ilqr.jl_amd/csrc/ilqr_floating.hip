@@ -1016,7 +1016,14 @@ ilqr_status ilqr_floating_forward(ilqr_floating_handle* h, const ilqr_options* o
 ilqr_status ilqr_floating_fit(ilqr_floating_handle* h, const ilqr_options* o, const double* x_init,
                               const double* u_init, const double* x_traj, double* x_out, double* u_out,
                               double* cost, int32_t* iters, int32_t* status) {
+  return ilqr_floating_fit_ex(h, o, x_init, u_init, x_traj, x_out, u_out, cost, iters, status, nullptr);
+}
+
+ilqr_status ilqr_floating_fit_ex(ilqr_floating_handle* h, const ilqr_options* o, const double* x_init,
+                                 const double* u_init, const double* x_traj, double* x_out, double* u_out,
+                                 double* cost, int32_t* iters, int32_t* status, const ilqr_history* hist) {
   if (!h || !x_init || !u_init || !x_out || !u_out) return ILQR_ERR_BAD_ARG;
+  if (hist && !hist->cost && !hist->trials && !hist->alpha && !hist->du2) hist = nullptr;
   ilqr_status st = fb_check_options(o);
   if (st != ILQR_OK) return st;
   FB_TRY(hipSetDevice(h->device));
@@ -1062,6 +1069,9 @@ ilqr_status ilqr_floating_fit(ilqr_floating_handle* h, const ilqr_options* o, co
     ilqr::fb_move_kernel<<<dim3(gx, (unsigned)(B < 65535 ? B : 65535)), 256, 0, s>>>(B, T, h->move, h->xn, h->un,
                                                                                       h->x, h->u);
     FB_TRY(hipGetLastError());
+    if (hist)  // the per-iteration record (ilqr_history), as the other families'
+      FB_TRY(ilqr::launch_record_history(B, it, h->status, h->iters, h->trials, h->prev_cost, h->du2, false,
+                                         ls.alpha0, ls.shrink, hist->cost, hist->trials, hist->alpha, hist->du2, s));
     if (ls.tol >= 0.0 && it < max_iter) {  // :171's break once every trajectory stopped
       ilqr::fb_count_kernel<<<1, 256, 0, s>>>(B, h->status, h->words);
       FB_TRY(hipGetLastError());

@@ -181,6 +181,7 @@ SIGNATURES = {
     "ilqr_floating_backward": (C.c_int, [P, C.POINTER(Options), P, P, P, P, P]),
     "ilqr_floating_forward": (C.c_int, [P, C.POINTER(Options), P, P, P, P, P, P, P, P, P, P, P]),
     "ilqr_floating_fit": (C.c_int, [P, C.POINTER(Options), P, P, P, P, P, P, P, P]),
+    "ilqr_floating_fit_ex": (C.c_int, [P, C.POINTER(Options), P, P, P, P, P, P, P, P, C.POINTER(History)]),
 }
 
 _lib = None

@@ -253,7 +253,8 @@ def fit(x_init, u_init, dynamicsf, immediate_cost, final_cost, *, x_traj=None,
                           float(tol), history=verbose or return_info)
     elif fam == "floating":
         with _floating_solver(xb, ub, dynamicsf, immediate_cost, final_cost) as s:
-            r = s.fit(xb, ub, x_traj=xt, max_iter=int(max_iter), tol=float(tol))
+            r = s.fit(xb, ub, x_traj=xt, max_iter=int(max_iter), tol=float(tol),
+                      history=verbose or return_info)
     elif fam == "chain":
         dt = _eltype(x_init)
         s = _chain_solver(xb, ub, dynamicsf, immediate_cost, final_cost, dt)

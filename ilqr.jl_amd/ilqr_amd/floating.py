@@ -31,7 +31,7 @@ import torch
 
 from . import _lib
 from .chain import load_robot
-from .solver import FitResult, _ptr, _req
+from .solver import FitResult, _ptr, _req, alloc_history
 from .urdf import Chain
 
 # animate_RBD_2_link.jl:8-10 and RBD_helper_functions.jl:85-116
@@ -210,8 +210,10 @@ class FloatingSolver:
                    "ilqr_floating_forward", allow=(_lib.ERR_NAN, _lib.ERR_LS_EXHAUSTED))
         return xn, un, cost, trials, st
 
-    def fit(self, x_init, u_init, max_iter=100, tol=1e-6, x_traj=None, options=None) -> FitResult:
-        """iLQR.fit (forward_pass.jl:148-179) for the whole batch; synchronises."""
+    def fit(self, x_init, u_init, max_iter=100, tol=1e-6, x_traj=None, options=None,
+            history: bool = False) -> FitResult:
+        """iLQR.fit (forward_pass.jl:148-179) for the whole batch; synchronises. history:
+        also return the per-iteration record (ilqr_floating_fit_ex; FitResult.history)."""
         self._xu(x_init, u_init)
         if x_traj is not None:
             _req(x_traj, torch.float64, (self.batch, self.T + 1, self.nx), "x_traj")
@@ -222,11 +224,13 @@ class FloatingSolver:
         st = self._new(B, dtype=torch.int32)
         o = options or _lib.default_options(max_iter=max_iter, tol=tol)
         self._bind()
-        cs = _lib.check(self.lib.ilqr_floating_fit(self.h, C.byref(o), _ptr(x_init), _ptr(u_init),
-                                                   _ptr(x_traj), _ptr(xo), _ptr(uo), _ptr(cost),
-                                                   _ptr(iters), _ptr(st)),
+        hist, hst = alloc_history(o.max_iter, B, x_init.device) if history else (None, None)
+        cs = _lib.check(self.lib.ilqr_floating_fit_ex(self.h, C.byref(o), _ptr(x_init), _ptr(u_init),
+                                                      _ptr(x_traj), _ptr(xo), _ptr(uo), _ptr(cost),
+                                                      _ptr(iters), _ptr(st),
+                                                      C.byref(hst) if hst is not None else None),
                         "ilqr_floating_fit", allow=(_lib.ERR_NAN, _lib.ERR_LS_EXHAUSTED))
-        return FitResult(xo, uo, cost, iters, st, cs, None)
+        return FitResult(xo, uo, cost, iters, st, cs, hist)
 
 
 # -- reference-API callables (recognised by ilqr_amd.fit) ------------------------------------

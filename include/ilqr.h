@@ -523,6 +523,11 @@ ilqr_status ilqr_floating_forward(ilqr_floating_handle* h, const ilqr_options* o
 ilqr_status ilqr_floating_fit(ilqr_floating_handle* h, const ilqr_options* o, const double* x_init,
                               const double* u_init, const double* x_traj, double* x_out,
                               double* u_out, double* cost, int32_t* iters, int32_t* status);
+/* ilqr_floating_fit plus the per-iteration record (history may be NULL) */
+ilqr_status ilqr_floating_fit_ex(ilqr_floating_handle* h, const ilqr_options* o, const double* x_init,
+                                 const double* u_init, const double* x_traj, double* x_out,
+                                 double* u_out, double* cost, int32_t* iters, int32_t* status,
+                                 const ilqr_history* history);
 
 /* Device memory helpers so a host-language shim (Julia ccall) needs no GPU package. */
 ilqr_status ilqr_malloc(ilqr_handle* h, size_t bytes, void** ptr);

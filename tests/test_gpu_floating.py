@@ -86,12 +86,16 @@ def test_floating_fit_script_shape_vs_closure_oracle(gpu):
     x, u = script_batch(nb, T)
     s = FloatingSolver(rbd_example_problem(), T, nb)
     try:
-        r = s.fit(torch.from_numpy(x).cuda(), torch.from_numpy(u).cuda(), max_iter=iters, tol=1e-6)
+        r = s.fit(torch.from_numpy(x).cuda(), torch.from_numpy(u).cuda(), max_iter=iters, tol=1e-6,
+                  history=True)
     finally:
         s.close()
     fj, lj, lfj = rbd_floating_arm(jet_ns())
     o = CF.fit(x, u, fj, lj, lfj, *rbd_cost_quads(), max_iter=iters, tol=1e-6)
     assert r.iters.tolist() == o["iters"].tolist()
+    # the per-iteration record (ilqr_floating_fit_ex): trials and costs as the oracle's
+    assert r.history["trials"][:iters].cpu().tolist() == o["history"]["trials"].tolist()
+    assert rel(r.history["cost"][:iters], o["history"]["cost"]) < 1e-8
     assert r.status.tolist() == o["status"].tolist()
     assert rel(r.cost, o["cost"]) < 1e-8
     assert rel(r.x, o["x"]) < 1e-8 and rel(r.u, o["u"]) < 1e-8
