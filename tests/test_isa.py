@@ -85,13 +85,32 @@ def test_tiles_kernels_have_no_scratch(tmp_path):
     registers — a dynamically indexed register array (the first draft's g vector) or a
     spill would be a scratch access per step."""
     hipcc = HIPCC if os.path.exists(HIPCC) else shutil.which("hipcc")
-    cmd = [hipcc, "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-save-temps", "-c",
-           os.path.join(CSRC, "ilqr_tiles.hip"), "-o", str(tmp_path / "tiles.o")]
+    cmd = [hipcc, "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-mllvm", "-amdgpu-mfma-vgpr-form=1",
+           "-save-temps", "-c", os.path.join(CSRC, "ilqr_tiles.hip"), "-o", str(tmp_path / "tiles.o")]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=900, cwd=tmp_path)
     assert r.returncode == 0, r.stderr[-2000:]
     asm_file = [f for f in os.listdir(tmp_path) if f.endswith("gfx950.s")]
     funcs = _functions(open(tmp_path / asm_file[0]).read())
     kernels = [n for n in funcs if "tiles_backward" in n and "kernel" in n]
     assert any("wide" in n for n in kernels) and len(kernels) >= 49, len(kernels)
+    for n in kernels:
+        assert not [x for x in funcs[n] if x.startswith("scratch_")], f"{n}: scratch accesses"
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC) and shutil.which("hipcc") is None, reason="no hipcc")
+def test_floating_kernels_have_no_scratch(tmp_path):
+    """The floating-base family (ilqr_floating.hip): the dual-number linearisation and the
+    forward keep ~440-490 registers at one wave per SIMD; the model's constants are
+    re-read per RK4 stage instead of hoisted — hoisted, they had spilled to scratch
+    (364 and 140 bytes per lane)."""
+    hipcc = HIPCC if os.path.exists(HIPCC) else shutil.which("hipcc")
+    cmd = [hipcc, "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-save-temps", "-c",
+           os.path.join(CSRC, "ilqr_floating.hip"), "-o", str(tmp_path / "fl.o")]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=900, cwd=tmp_path)
+    assert r.returncode == 0, r.stderr[-2000:]
+    asm_file = [f for f in os.listdir(tmp_path) if f.endswith("gfx950.s")]
+    funcs = _functions(open(tmp_path / asm_file[0]).read())
+    kernels = [n for n in funcs if re.search(r"fb_(dynamics|linearize|forward)_kernel", n)]
+    assert len(kernels) == 3, sorted(funcs)
     for n in kernels:
         assert not [x for x in funcs[n] if x.startswith("scratch_")], f"{n}: scratch accesses"
