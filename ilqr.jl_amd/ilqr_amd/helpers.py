@@ -110,6 +110,11 @@ def _linearize(x, u, dynamicsf, nb, nx, nu, T):
         finally:
             s.close()
         return A, Bm
+    from .floating import FloatingDynamics, FloatingSolver
+    if isinstance(dynamicsf, FloatingDynamics) and (dynamicsf.problem.nx, dynamicsf.problem.nu) == (nx, nu):
+        key = ("floating", dev, bytes(dynamicsf.problem.struct()), T, nb)
+        with _cache.workspace(key, lambda: FloatingSolver(dynamicsf.problem, T, nb, device=dev)) as s:
+            return s.linearize(x, u)
     # any other torch closure: ForwardDiff's role, in reverse mode (tiles.py: PyTorch's
     # vmapped forward-mode derivative of linalg.solve is wrong)
     from torch.func import jacrev, vmap

@@ -271,3 +271,18 @@ def test_floating_general_mechanism_vs_restatement(gpu):
     o = CF.fit(x0, uu, fj, lj, lfj, *rbd_cost_quads(), max_iter=4)
     assert r.iters.tolist() == o["iters"].tolist() and r.status.tolist() == o["status"].tolist()
     assert rel(r.x, o["x"]) < 1e-8 and rel(r.u, o["u"]) < 1e-8
+
+
+def test_linearize_dynamics_helper_dispatches(gpu):
+    """iLQR.linearize_dynamics (backward_pass.jl:25-40) with the family's dynamics callable:
+    the dual-number kernel, one point and a trajectory, against oracle.jet."""
+    from ilqr_amd.helpers import linearize_dynamics
+    from ilqr_amd.floating import FloatingDynamics
+    fj, _, _ = rbd_floating_arm(jet_ns())
+    x, u = random_states(6, seed=31)
+    f = FloatingDynamics(rbd_example_problem())
+    A1, B1 = linearize_dynamics(x[0], u[0], f)
+    AT, BT = linearize_dynamics(x, u[:5], f)          # N = T + 1 rows
+    Aj, Bj = jet.jacobians(fj, x[:5], u[:5])
+    assert rel(A1, Aj[0]) < 1e-10 and rel(B1, Bj[0]) < 1e-10
+    assert rel(AT, Aj) < 1e-10 and rel(BT, Bj) < 1e-10
