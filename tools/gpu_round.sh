@@ -91,6 +91,9 @@ case $WHAT in
           step tl_new_$i 200 python tools/bench_twolink.py --no-cpu
         done
         for f in gpurun_out/tl_prev_*.log gpurun_out/tl_new_*.log; do python -c "import json,sys; d=[json.loads(l) for l in open(sys.argv[1]) if l.startswith('{')][-1]; r=d['roofline']; print(sys.argv[1], round(d['value'],1), {k: round(v['avg_launch_ms']*1000,2) for k,v in r.items() if isinstance(v, dict) and 'avg_launch_ms' in v})" $f; done > gpurun_out/tl_ab.log; cat gpurun_out/tl_ab.log ;;
+  floating) step pytest_floating 400 python -u -m pytest tests/test_gpu_floating.py -m gpu -x -v --timeout 300 --timeout-method thread
+            step bench_floating 300 python tools/bench_floating.py 5 2 1 256 1024
+            step rocprof_floating 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_fb -o run --output-format csv -- python tools/bench_floating.py 3 1 1 ;;
   gtest) step pytest_gather 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_line_search.py tests/test_gpu_multi.py -m gpu -x -q --timeout 120 --timeout-method thread ;;
 esac
 done
