@@ -871,12 +871,11 @@ ilqr_status ilqr_floating_create(ilqr_floating_handle** out, int device, const i
     g_fb_error = "ilqr_floating_create: gravity must be zero (the reference parses the URDF with gravity = 0)";
     return ILQR_ERR_UNSUPPORTED;
   }
+  ilqr::FbModel model;
+  if (!fb_model(m, model)) return ILQR_ERR_BAD_ARG;
+  FB_TRY(hipSetDevice(device));  // before the handle exists: a failure leaks nothing
   auto* h = new ilqr_floating_handle;
-  if (!fb_model(m, h->model)) {
-    delete h;
-    return ILQR_ERR_BAD_ARG;
-  }
-  FB_TRY(hipSetDevice(device));
+  h->model = model;
   h->device = device;
   h->T = T;
   h->batch = batch;

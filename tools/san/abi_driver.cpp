@@ -25,6 +25,38 @@ static int fails = 0;
 
 extern "C" int hipGetDeviceCount(int*);
 
+// the reference's RBD script model (2Dof_arm.urdf floating, zero gravity, its costs)
+static ilqr_floating floating_model() {
+  ilqr_floating m{};
+  m.n_joints = 2;
+  m.dt = 0.01;
+  m.base_mass = 30.0;
+  for (int k = 0; k < 3; ++k) {
+    m.base_inertia[4 * k] = 50.0;
+    for (int j = 0; j < 2; ++j) {
+      m.joint_rot[j][4 * k] = 1.0;
+      m.inertia[j][4 * k] = 0.5;
+    }
+  }
+  m.mass[0] = m.mass[1] = 3.0;
+  m.joint_pos[0][0] = m.joint_pos[0][1] = 0.5;
+  m.joint_pos[1][0] = 1.0;
+  m.axis[0][2] = 1.0;
+  m.axis[1][1] = 1.0;
+  const double tgt[8] = {0, 0, 0, 5, 1, 2, 1, .3}, qw[8] = {100, 100, 100, 1, 1, 1, 10, 10},
+               rw[8] = {1, 1, 1, 100, 100, 100, 10, 10}, qfw[8] = {100, 100, 100, 1000, 1000, 1000, 10, 10};
+  for (int i = 0; i < 8; ++i) {
+    m.target[i] = tgt[i];
+    m.q_weight[i] = qw[i];
+    m.r_weight[i] = rw[i];
+    m.qf_weight[i] = qfw[i];
+  }
+  m.q_scale = 10.0;
+  m.r_scale = 1.0;
+  m.qf_scale = 100000.0;
+  return m;
+}
+
 static void no_gpu_paths() {
   CHECK(ilqr_abi_version() > 0, "abi version");
   for (int s = 0; s <= 7; ++s) CHECK(std::strlen(ilqr_status_string((ilqr_status)s)) > 0, "status string %d", s);
@@ -84,6 +116,18 @@ static void no_gpu_paths() {
   CHECK(ilqr_chain_fit(nullptr, nullptr, buf, buf, nullptr, buf, buf, buf, ibuf, ibuf) == ILQR_ERR_BAD_ARG,
         "chain fit null");
   CHECK(ilqr_chain_destroy(nullptr) == ILQR_OK, "chain destroy null");
+  ilqr_floating fm = floating_model();
+  ilqr_floating_handle* fh = nullptr;
+  CHECK(ilqr_floating_create(nullptr, 0, &fm, 10, 2) == ILQR_ERR_BAD_ARG, "floating null");
+  CHECK(ilqr_floating_create(&fh, 0, &fm, 0, 2) == ILQR_ERR_BAD_DIMS && !fh, "floating bad dims");
+  fm.gravity[2] = -9.81;
+  CHECK(ilqr_floating_create(&fh, 0, &fm, 10, 2) == ILQR_ERR_UNSUPPORTED && !fh, "floating gravity");
+  fm = floating_model();
+  fm.n_joints = 3;
+  CHECK(ilqr_floating_create(&fh, 0, &fm, 10, 2) == ILQR_ERR_UNSUPPORTED && !fh, "floating joints");
+  CHECK(ilqr_floating_fit(nullptr, nullptr, buf, buf, nullptr, buf, buf, buf, ibuf, ibuf) == ILQR_ERR_BAD_ARG,
+        "floating fit null");
+  CHECK(ilqr_floating_destroy(nullptr) == ILQR_OK, "floating destroy null");
   std::printf("no-GPU paths: %d failed checks\n", fails);
 }
 
@@ -196,6 +240,49 @@ static void gpu_paths(int ndev) {
   CHECK(ilqr_multi_gather(m, xo.data(), uo.data(), pinned, io.data(), so.data()) == ILQR_OK, "multi gather all");
   ilqr_host_free(pinned);
   ilqr_multi_destroy(m);
+
+  // the floating-base family: the script's rest state, a 3-iteration fit of 3 trajectories
+  {
+    const int FB = 3, FT = 10;
+    ilqr_floating fm = floating_model();
+    ilqr_floating_handle* fh = nullptr;
+    CHECK(ilqr_floating_create(&fh, 0, &fm, FT, FB) == ILQR_OK, "floating create");
+    std::vector<double> fx((size_t)FB * (FT + 1) * 16, 0.0), fu((size_t)FB * FT * 8, 0.0);
+    void *dfx, *dfu, *dfxo, *dfuo, *dfc;
+    ilqr_handle* mh = nullptr;  // device-memory helper
+    CHECK(ilqr_create(&mh, 0, 16, 8, FT, 1) == ILQR_OK, "helper create");
+    for (void** q : {&dfx, &dfxo}) ilqr_malloc(mh, fx.size() * 8, q);
+    for (void** q : {&dfu, &dfuo}) ilqr_malloc(mh, fu.size() * 8, q);
+    ilqr_malloc(mh, FB * 8, &dfc);
+    for (int b = 0; b < FB; ++b) {
+      double* x0 = fx.data() + (size_t)b * (FT + 1) * 16;
+      x0[2] = 1.0;
+      x0[3] = 0.5;
+      x0[4] = 0.75;
+      x0[5] = 1.0;
+      x0[8 + b] = 0.01;
+    }
+    ilqr_memcpy_h2d(mh, dfx, fx.data(), fx.size() * 8);
+    ilqr_memcpy_h2d(mh, dfu, fu.data(), fu.size() * 8);
+    // x_init = the rollout of u = 0 (the script's state_traj), one step at a time
+    for (int t = 0; t < FT; ++t)
+      for (int b = 0; b < FB; ++b) {
+        double* xb = (double*)dfx + (size_t)b * (FT + 1) * 16;
+        CHECK(ilqr_floating_dynamics(fh, xb + t * 16, (double*)dfu, xb + (t + 1) * 16, 1) == ILQR_OK, "dyn");
+      }
+    ilqr_options fo;
+    ilqr_default_options(&fo);
+    fo.max_iter = 3;
+    const ilqr_status fs2 = ilqr_floating_fit(fh, &fo, (double*)dfx, (double*)dfu, nullptr, (double*)dfxo,
+                                              (double*)dfuo, (double*)dfc, nullptr, nullptr);
+    CHECK(fs2 == ILQR_OK, "floating fit %d", (int)fs2);
+    std::vector<double> fc(FB);
+    ilqr_memcpy_d2h(mh, fc.data(), dfc, FB * 8);
+    for (int b = 0; b < FB; ++b) CHECK(std::isfinite(fc[b]), "floating cost %d", b);
+    for (void* q : {dfx, dfu, dfxo, dfuo, dfc}) ilqr_free(mh, q);
+    ilqr_destroy(mh);
+    CHECK(ilqr_floating_destroy(fh) == ILQR_OK, "floating destroy");
+  }
   std::printf("GPU paths (%d device(s)): %d failed checks\n", ndev, fails);
 }
 
@@ -210,6 +297,9 @@ int main() {
     ilqr_multi* m = nullptr;
     int devs[2] = {0, 1};
     CHECK(ilqr_multi_create(&m, devs, 2, 12, 4, 10, 8) == ILQR_ERR_HIP && !m, "multi create without a GPU");
+    ilqr_floating fm = floating_model();
+    ilqr_floating_handle* fh = nullptr;
+    CHECK(ilqr_floating_create(&fh, 0, &fm, 10, 2) == ILQR_ERR_HIP && !fh, "floating create without a GPU");
     std::printf("no GPU visible: GPU paths skipped, create paths fail with ILQR_ERR_HIP (%d failed checks)\n", fails);
   }
   std::printf("abi sanitizer driver: %s\n", fails ? "FAILED" : "ok");
