@@ -98,3 +98,12 @@ def test_julia_floating_model_matches_the_c_layout():
     assert names == [f[0] for f in _lib.FloatingStruct._fields_]
     assert size == C.sizeof(_lib.FloatingStruct)
     assert offs == [getattr(_lib.FloatingStruct, f).offset for f in names]
+
+
+def test_julia_constructor_equals_the_python_problem():
+    """The shim's rbd_2dof_arm_floating() and ilqr_amd.floating.rbd_example_problem()
+    (whose fits the GPU tests pin to the oracle) hand create the same bytes."""
+    from julia_layout import rbd_2dof_arm_floating
+    j = rbd_2dof_arm_floating()
+    p = rbd_example_problem().struct()
+    assert bytes(j) == bytes(p)

@@ -10,7 +10,8 @@ Covers: backward_pass / forward_pass / fit on the LQ family (per-trajectory
 `to_abi`, `gains_to_abi`/`gains_from_abi`), the 2-link structs (nu = 2 and the nu = 1
 variant) dispatched to ILQR_PROBLEM_TWO_LINK, the TILES fallback for arbitrary closures
 (host derivative tiles → ilqr_backward_tiles), and batched solve! ((2,1,3) per-instance
-matrices, (nx, N, B) trajectories).
+matrices, (nx, N, B) trajectories), and the RBD families' chain_fit (f64 and f32) and
+floating_fit with the shim's own rbd_2dof_arm_floating() model.
 """
 import ctypes as C
 import os
@@ -298,3 +299,101 @@ def test_shim_multisolver_resident(gpu):
             assert rel(xw[:, :, b].T, xr) < 1e-8 and rel(uw[:, :, b].T, ur) < 1e-8
     finally:
         lib.ilqr_multi_destroy(m)
+
+
+def shim_family_fit(create, fit, destroy, x_init, u_init, max_iter, tol, dtype):
+    """The tail shared by iLQRHIP.chain_fit / floating_fit: a memory-helper Handle,
+    upload(h, x_init) of the (nx, N, batch) Julia arrays as they are, the family's fit
+    with x_traj / cost / iterations left C_NULL, download! into similar(x_init), the
+    family handle destroyed and the helper closed."""
+    nx, N, nb = x_init.shape
+    nu, M = u_init.shape[0], u_init.shape[1]
+    r = create(M, nb)
+    h = Handle(nx, nu, M, 1)
+    try:
+        xi, ui = h.upload(x_init, dtype=dtype), h.upload(u_init, dtype=dtype)
+        xo, uo, sd = h.alloc(dtype, x_init.size), h.alloc(dtype, u_init.size), h.alloc(np.int32, nb)
+        o = _lib.default_options(max_iter=max_iter, tol=tol)
+        st = fit(r, C.byref(o), xi, ui, None, xo, uo, None, None, sd)
+        assert st in (_lib.OK, _lib.ERR_LS_EXHAUSTED)
+        return (h.download(x_init.shape, xo, dtype=dtype), h.download(u_init.shape, uo, dtype=dtype),
+                h.download((nb,), sd, dtype=np.int32))
+    finally:
+        destroy(r)
+        h.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_shim_chain_fit(gpu, dtype):
+    """iLQRHIP.chain_fit(::Chain, x_init::Array{E,3}, u_init): Ref{Chain} to
+    ilqr_chain_create with the element type's precision, set_dynamics(AUTO), the helper
+    Handle's buffers — the same trajectories, bit for bit, as ChainSolver.fit on
+    (batch, N, nx) tensors (whose results the chain tests pin to the oracle)."""
+    import torch
+    from ilqr_amd.chain import ChainSolver, rbd_2dof_problem, rbd_initial_states
+    p = rbd_2dof_problem()
+    nb, T, iters = 4, 60, 8
+    x0 = rbd_initial_states(nb)
+    u0 = np.zeros((nb, T, p.nu))
+    tdt = torch.float64 if dtype == np.float64 else torch.float32
+    s = ChainSolver(p, T, nb, dtype=tdt)
+    try:
+        xs = s.rollout(torch.as_tensor(x0, dtype=tdt, device="cuda"), torch.as_tensor(u0, dtype=tdt, device="cuda"))
+        x_init = xs.cpu().numpy().astype(np.float64)
+        ref = s.fit(xs, torch.as_tensor(u0, dtype=tdt, device="cuda"), max_iter=iters, tol=1e-6)
+        rx, ru, rs = ref.x.cpu().numpy(), ref.u.cpu().numpy(), ref.status.cpu().numpy()
+    finally:
+        s.close()
+    lib = _lib.load()
+    st = p.struct()
+
+    def create(M, b):
+        r = C.c_void_p()
+        _lib.check(lib.ilqr_chain_create(C.byref(r), 0, C.byref(st), M, b,
+                                         _lib.F64 if dtype == np.float64 else _lib.F32, _lib.LINEARIZE_DUAL),
+                   "ilqr_chain_create")
+        _lib.check(lib.ilqr_chain_set_dynamics(r, _lib.CHAIN_DYN_AUTO), "ilqr_chain_set_dynamics")
+        return r
+
+    jx = J.jl(np.transpose(x_init, (2, 1, 0)))          # x_init[:, t, b]
+    ju = J.jl(np.transpose(u0, (2, 1, 0)))
+    x, u, status = shim_family_fit(create, lib.ilqr_chain_fit, lib.ilqr_chain_destroy, jx, ju, iters, 1e-6, dtype)
+    assert np.array_equal(np.transpose(x, (2, 1, 0)), rx) and np.array_equal(np.transpose(u, (2, 1, 0)), ru)
+    assert np.array_equal(status, rs)
+
+
+@pytest.mark.gpu
+def test_shim_floating_fit(gpu):
+    """iLQRHIP.floating_fit(rbd_2dof_arm_floating(), x_init, u_init): the shim's model
+    by Ref to ilqr_floating_create and (16, N, batch) / (8, T, batch) arrays through the
+    helper Handle — the same fit, bit for bit, as FloatingSolver.fit on the example
+    problem (pinned to the oracle by tests/test_gpu_floating.py)."""
+    import torch
+    from ilqr_amd.floating import FloatingSolver, rbd_example_problem, rbd_initial_state
+    nb, T, iters = 3, 80, 3
+    x0 = np.tile(rbd_initial_state(), (nb, 1))
+    x0[1:, 8:] = 0.05 * np.random.default_rng(3).standard_normal((nb - 1, 8))
+    u0 = np.zeros((nb, T, 8))
+    s = FloatingSolver(rbd_example_problem(), T, nb)
+    try:
+        xs = s.rollout(torch.from_numpy(x0).cuda(), torch.from_numpy(u0).cuda())
+        x_init = xs.cpu().numpy()
+        ref = s.fit(xs, torch.from_numpy(u0).cuda(), max_iter=iters, tol=1e-6)
+        rx, ru, rs = ref.x.cpu().numpy(), ref.u.cpu().numpy(), ref.status.cpu().numpy()
+    finally:
+        s.close()
+    lib = _lib.load()
+    m = J.rbd_2dof_arm_floating()
+
+    def create(M, b):
+        r = C.c_void_p()
+        _lib.check(lib.ilqr_floating_create(C.byref(r), 0, C.byref(m), M, b), "ilqr_floating_create")
+        return r
+
+    jx = J.jl(np.transpose(x_init, (2, 1, 0)))
+    ju = J.jl(np.transpose(u0, (2, 1, 0)))
+    x, u, status = shim_family_fit(create, lib.ilqr_floating_fit, lib.ilqr_floating_destroy, jx, ju, iters,
+                                   1e-6, np.float64)
+    assert np.array_equal(np.transpose(x, (2, 1, 0)), rx) and np.array_equal(np.transpose(u, (2, 1, 0)), ru)
+    assert np.array_equal(status, rs)
