@@ -11,8 +11,12 @@
 //   * the Riccati recursion: the wide tiles kernel (ilqr_tiles.hip, nx ≤ 16, nu ≤ 8);
 //   * fb_forward_kernel: forward_pass (forward_pass.jl:55-93) — four line-search trials
 //     of a trajectory at once, one per lane, the first accepted one kept (bit for bit
-//     the sequential search's choice: every trial is independent of the others);
-//   * fb_update_kernel: fit's bookkeeping (:161-178).
+//     the sequential search's choice: every trial is independent of the others); each
+//     trial stores its x̄, ū as it rolls out (trial 1 into x̄, ū, the others into a
+//     per-lane slot), so an accepted later trial is taken from its slot, never rolled
+//     out again;
+//   * fb_update_kernel / fb_take_kernel: fit's bookkeeping (:161-178) and the accepted
+//     trial's move into the iterate.
 //
 // Dynamics (RigidBodyDynamics.jl is absent; restated with Featherstone's algorithms in
 // body coordinates, angular first, as tests/closures.py rbd_floating_arm): the base is a
@@ -526,27 +530,26 @@ struct FbFwd {
   int32_t* trials;
   int32_t* fstatus;        // out: 0 accepted, LS_EXHAUSTED, NAN
   const int32_t* status;   // in: trajectories with a set status are skipped (nullable)
+  double* slots;           // (B, FB_CAND, (T+1)·nx + T·nu): trials j > 1, slot (j − 1) mod FB_CAND
   double alpha0, shrink;
   int max_trials;
 };
 
 // One trial's rollout (forward_pass.jl:65-76) → cost, Σ(ū − u)², and whether every
-// ū = u + α·δu equals u (then every later, smaller α rolls out the same); stores x̄, ū
-// when `store`.
-__device__ double fb_rollout(const FbModel& P, const FbFwd& a, int b, int T, double alpha, bool store,
-                             double& du2, bool& same) {
+// ū = u + α·δu equals u (then every later, smaller α rolls out the same); stores x̄
+// into xn, ū into un as it goes.
+__device__ double fb_rollout(const FbModel& P, const FbFwd& a, int b, int T, double alpha, double* __restrict__ xn,
+                             double* __restrict__ un, double& du2, bool& same) {
   const double* x = a.x + (size_t)b * (T + 1) * FB_NX;
   const double* u = a.u + (size_t)b * T * FB_NU;
   const double* xt = a.xtraj ? a.xtraj + (size_t)b * (T + 1) * FB_NX : nullptr;
   const double* d = a.d + (size_t)b * T * FB_NU;
   const double* K = a.K + (size_t)b * T * FB_NU * FB_NX;
-  double* xn = a.xn + (size_t)b * (T + 1) * FB_NX;
-  double* un = a.un + (size_t)b * T * FB_NU;
   double xb[FB_NX];
 #pragma unroll
   for (int k = 0; k < FB_NX; ++k) {
     xb[k] = x[k];  // x̄₁ = x₁ (:65)
-    if (store) xn[k] = xb[k];
+    xn[k] = xb[k];
   }
   double cost = 0.0, s2 = 0.0;
   bool eq = true;
@@ -575,12 +578,10 @@ __device__ double fb_rollout(const FbModel& P, const FbFwd& a, int b, int T, dou
     fb_step(P, xb, ub, y);  // :74
 #pragma unroll
     for (int k = 0; k < FB_NX; ++k) xb[k] = y[k];
-    if (store) {
 #pragma unroll
-      for (int j = 0; j < FB_NU; ++j) un[(size_t)t * FB_NU + j] = ub[j];
+    for (int j = 0; j < FB_NU; ++j) un[(size_t)t * FB_NU + j] = ub[j];
 #pragma unroll
-      for (int k = 0; k < FB_NX; ++k) xn[(size_t)(t + 1) * FB_NX + k] = xb[k];
-    }
+    for (int k = 0; k < FB_NX; ++k) xn[(size_t)(t + 1) * FB_NX + k] = xb[k];
   }
   cost = cost + final_cost(P, xb);  // :192 (raw x̄_N)
   du2 = s2;
@@ -605,12 +606,18 @@ __global__ __launch_bounds__(64) void fb_forward_kernel(const FbModel* __restric
   for (int k = 0; k < c; ++k) alpha *= a.shrink;
   double step = 1.0;
   for (int k = 0; k < FB_CAND; ++k) step *= a.shrink;
+  const size_t nxe = (size_t)(T + 1) * FB_NX, nue = (size_t)T * FB_NU;
+  double* slot = a.slots + ((size_t)b * FB_CAND + c) * (nxe + nue);
   for (int j0 = 1; j0 <= a.max_trials; j0 += FB_CAND) {
     const int j = j0 + c;
     const bool run = live && done_trial == 0 && j <= a.max_trials;
     double cost = NAN, du2 = 0.0;
     bool same = false;
-    if (run) cost = fb_rollout(P, a, b, T, alpha, j == 1, du2, same);
+    if (run) {
+      double* xo = j == 1 ? a.xn + (size_t)b * nxe : slot;
+      double* uo = j == 1 ? a.un + (size_t)b * nue : slot + nxe;
+      cost = fb_rollout(P, a, b, T, alpha, xo, uo, du2, same);
+    }
     const bool acc = run && (pc - cost > 0.0);
     // the trajectory's lanes agree on the outcome: the smallest accepted j, else whether a
     // rejected trial with ū = u ended the search, else the round's last trial
@@ -635,18 +642,11 @@ __global__ __launch_bounds__(64) void fb_forward_kernel(const FbModel* __restric
       }
       done_cost = pcost;
       done_du2 = pdu2;
-      // an accepted trial other than the first is rolled out again by its lane, storing
-      if (done_trial > 1 && c == ca) {
-        double s2;
-        bool sm;
-        (void)fb_rollout(P, a, b, T, alpha, true, s2, sm);
-      }
     }
     alpha *= step;
     if (!__any(live && done_trial == 0)) break;
   }
   if (live && done_trial <= 0) {  // no trial accepted: x̄, ū = the inputs, as the closure path
-    const size_t nxe = (size_t)(T + 1) * FB_NX, nue = (size_t)T * FB_NU;
     for (size_t i = c; i < nxe; i += FB_CAND) a.xn[(size_t)b * nxe + i] = a.x[(size_t)b * nxe + i];
     for (size_t i = c; i < nue; i += FB_CAND) a.un[(size_t)b * nue + i] = a.u[(size_t)b * nue + i];
   }
@@ -689,18 +689,30 @@ __global__ __launch_bounds__(256) void fb_update_kernel(int B, int T, int it, do
   move[b] = 1;
 }
 
-// x ← x̄, u ← ū for the trajectories that moved
-__global__ __launch_bounds__(256) void fb_move_kernel(int B, int T, const int32_t* __restrict__ move,
+// the accepted trial's x̄, ū into (x, u): trial 1 from (xn, un), trial j > 1 from its
+// slot. fit (move ≠ null): the trajectories that move, into the iterate; forward_pass
+// (move = null): every accepted j > 1, into (xn, un) = (x, u) here
+__global__ __launch_bounds__(256) void fb_take_kernel(int B, int T, const int32_t* __restrict__ move,
+                                                      const int32_t* __restrict__ fst,
+                                                      const int32_t* __restrict__ trials,
                                                       const double* __restrict__ xn, const double* __restrict__ un,
-                                                      double* __restrict__ x, double* __restrict__ u) {
+                                                      const double* __restrict__ slots, double* __restrict__ x,
+                                                      double* __restrict__ u) {
   const size_t nx = (size_t)(T + 1) * FB_NX, nu = (size_t)T * FB_NU;
   for (int b = blockIdx.y; b < B; b += gridDim.y) {
-    if (!move[b]) continue;
+    const int j = trials[b];
+    if (move ? !move[b] : (fst[b] != ILQR_TRAJ_OK || j <= 1)) continue;
+    const double* sx = xn + (size_t)b * nx;
+    const double* su = un + (size_t)b * nu;
+    if (j > 1) {
+      sx = slots + ((size_t)b * FB_CAND + (j - 1) % FB_CAND) * (nx + nu);
+      su = sx + nx;
+    }
     for (size_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nx + nu; i += (size_t)gridDim.x * blockDim.x) {
       if (i < nx)
-        x[(size_t)b * nx + i] = xn[(size_t)b * nx + i];
+        x[(size_t)b * nx + i] = sx[i];
       else
-        u[(size_t)b * nu + (i - nx)] = un[(size_t)b * nu + (i - nx)];
+        u[(size_t)b * nu + (i - nx)] = su[i - nx];
     }
   }
 }
@@ -742,6 +754,7 @@ struct ilqr_floating_handle {
   double *prev_cost = nullptr, *cost = nullptr, *du2 = nullptr;
   int32_t *trials = nullptr, *status = nullptr, *fstatus = nullptr, *bstatus = nullptr;
   int32_t *iters = nullptr, *move = nullptr, *words = nullptr;
+  double* slots = nullptr;  // the line search's trial slots (FbFwd::slots)
 };
 
 namespace {
@@ -842,6 +855,16 @@ ilqr_status fb_fold(ilqr_floating_handle* h, const int32_t* dev_status) {
   return nan ? ILQR_ERR_NAN : (ls ? ILQR_ERR_LS_EXHAUSTED : ILQR_OK);
 }
 
+// fb_take_kernel over the batch: one row of blocks per trajectory, ≤ 64 blocks along it
+hipError_t fb_take(ilqr_floating_handle* h, const int32_t* move, const int32_t* fst, const int32_t* trials,
+                   const double* xn, const double* un, double* x, double* u) {
+  const size_t n = (size_t)(h->T + 1) * ilqr::FB_NX + (size_t)h->T * ilqr::FB_NU;
+  const unsigned gx = (unsigned)((n + 255) / 256 < 64 ? (n + 255) / 256 : 64);
+  ilqr::fb_take_kernel<<<dim3(gx, (unsigned)(h->batch < 65535 ? h->batch : 65535)), 256, 0, h->stream>>>(
+      h->batch, h->T, move, fst, trials, xn, un, h->slots, x, u);
+  return hipGetLastError();
+}
+
 hipError_t fb_linearize(ilqr_floating_handle* h, const double* x, const double* u, const int32_t* st) {
   const size_t lanes = (size_t)h->batch * h->T * (ilqr::FB_NX + ilqr::FB_NU);
   ilqr::fb_linearize_kernel<<<(unsigned)((lanes + 255) / 256), 256, 0, h->stream>>>(
@@ -908,6 +931,7 @@ ilqr_status ilqr_floating_create(ilqr_floating_handle** out, int device, const i
   alloc(&h->iters, 4 * B);
   alloc(&h->move, 4 * B);
   alloc(&h->words, 4 * 4);
+  alloc(&h->slots, 8 * B * ilqr::FB_CAND * ((T + 1) * nx + (size_t)T * nu));
   alloc(&h->model_dev, sizeof(ilqr::FbModel));
   if (e == hipSuccess) e = hipMemcpy(h->model_dev, &h->model, sizeof(ilqr::FbModel), hipMemcpyHostToDevice);
   if (e != hipSuccess) {
@@ -922,7 +946,7 @@ ilqr_status ilqr_floating_destroy(ilqr_floating_handle* h) {
   if (!h) return ILQR_OK;
   (void)hipSetDevice(h->device);
   for (double* p : {h->x, h->u, h->xn, h->un, h->d, h->K, h->A, h->Bm, h->lx, h->lu, h->lxx, h->luu, h->lfx,
-                    h->lfxx, h->prev_cost, h->cost, h->du2})
+                    h->lfxx, h->prev_cost, h->cost, h->du2, h->slots})
     (void)hipFree(p);
   for (int32_t* p : {h->trials, h->status, h->fstatus, h->bstatus, h->iters, h->move, h->words}) (void)hipFree(p);
   (void)hipFree(h->model_dev);
@@ -1000,6 +1024,7 @@ ilqr_status ilqr_floating_forward(ilqr_floating_handle* h, const ilqr_options* o
   fa.trials = trials ? trials : h->trials;
   fa.fstatus = status ? status : h->fstatus;
   fa.status = nullptr;
+  fa.slots = h->slots;
   fa.alpha0 = ls.alpha0;
   fa.shrink = ls.shrink;
   fa.max_trials = ls.max_trials;
@@ -1007,8 +1032,9 @@ ilqr_status ilqr_floating_forward(ilqr_floating_handle* h, const ilqr_options* o
       h->model_dev, h->batch, h->T, fa);
   FB_TRY(hipGetLastError());
   // x̄, ū of a trajectory whose first trial was accepted are written as it rolled out; a
-  // later accepted trial is rolled out again by its lane (storing); a search that accepted
-  // nothing returns x, u (the closure path's rollout_forward does the same)
+  // later accepted trial is taken from its slot; a search that accepted nothing returns
+  // x, u (the closure path's rollout_forward does the same)
+  FB_TRY(fb_take(h, nullptr, fa.fstatus, fa.trials, x_new, u_new, x_new, u_new));
   return fb_fold(h, fa.fstatus);
 }
 
@@ -1052,6 +1078,7 @@ ilqr_status ilqr_floating_fit_ex(ilqr_floating_handle* h, const ilqr_options* o,
   fa.trials = h->trials;
   fa.fstatus = h->fstatus;
   fa.status = h->status;
+  fa.slots = h->slots;
   fa.alpha0 = ls.alpha0;
   fa.shrink = ls.shrink;
   fa.max_trials = ls.max_trials;
@@ -1064,10 +1091,7 @@ ilqr_status ilqr_floating_fit_ex(ilqr_floating_handle* h, const ilqr_options* o,
     ilqr::fb_update_kernel<<<g, 256, 0, s>>>(B, T, it, ls.tol, h->bstatus, h->fstatus, h->cost, h->du2,
                                              h->status, h->iters, h->prev_cost, h->move);
     FB_TRY(hipGetLastError());
-    const unsigned gx = (unsigned)((nxe + nue + 255) / 256 < 64 ? (nxe + nue + 255) / 256 : 64);
-    ilqr::fb_move_kernel<<<dim3(gx, (unsigned)(B < 65535 ? B : 65535)), 256, 0, s>>>(B, T, h->move, h->xn, h->un,
-                                                                                      h->x, h->u);
-    FB_TRY(hipGetLastError());
+    FB_TRY(fb_take(h, h->move, h->fstatus, h->trials, h->xn, h->un, h->x, h->u));
     if (hist)  // the per-iteration record (ilqr_history), as the other families'
       FB_TRY(ilqr::launch_record_history(B, it, h->status, h->iters, h->trials, h->prev_cost, h->du2, false,
                                          ls.alpha0, ls.shrink, hist->cost, hist->trials, hist->alpha, hist->du2, s));
