@@ -465,6 +465,11 @@ __global__ __launch_bounds__(256) void fb_dynamics_kernel(const FbModel* __restr
 // Derivative tiles at every (b, t): lane (point, dir) seeds input direction dir (x 0..15,
 // u 16..23) and writes column dir of A or B; lane dir = 0 also writes the cost tiles, and
 // the final point's lane the terminal ones. Trajectories whose status is set are skipped.
+// The base position r = x[3..5] enters neither ẋ (:66: ṙ = v) nor anything else (the
+// family has no gravity), so its three columns of A are the unit columns the dual
+// rollout would return for finite inputs; lane dir = 0 writes them and no lane seeds r:
+// FB_LIN_DIRS lanes per point.
+constexpr int FB_LIN_DIRS = FB_NX + FB_NU - 3;
 __global__ __launch_bounds__(256) void fb_linearize_kernel(const FbModel* __restrict__ Pm, int B, int T, const double* __restrict__ x,
                                                            const double* __restrict__ u,
                                                            const int32_t* __restrict__ status,
@@ -472,11 +477,12 @@ __global__ __launch_bounds__(256) void fb_linearize_kernel(const FbModel* __rest
                                                            double* __restrict__ lx, double* __restrict__ lu,
                                                            double* __restrict__ lxx, double* __restrict__ luu,
                                                            double* __restrict__ lfx, double* __restrict__ lfxx) {
-  constexpr int ND = FB_NX + FB_NU;
+  constexpr int ND = FB_LIN_DIRS;
   const FbModel& P = *Pm;
   const size_t lane = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (lane >= (size_t)B * T * ND) return;
-  const int dir = (int)(lane % ND);
+  const int ld = (int)(lane % ND);
+  const int dir = ld < 3 ? ld : ld + 3;  // directions 3..5 (r) are not seeded
   const size_t pt = lane / ND;  // b·T + t
   const int b = (int)(pt / T);
   const int t = (int)(pt % T);
@@ -497,6 +503,10 @@ __global__ __launch_bounds__(256) void fb_linearize_kernel(const FbModel* __rest
     for (int i = 0; i < FB_NX; ++i) Bm[(pt * FB_NX + i) * FB_NU + (dir - FB_NX)] = y[i].d;
   }
   if (dir != 0) return;
+#pragma unroll
+  for (int i = 0; i < FB_NX; ++i)
+#pragma unroll
+    for (int c = 3; c < 6; ++c) A[(pt * FB_NX + i) * FB_NX + c] = i == c ? 1.0 : 0.0;
   // cost tiles (:95-99): lx = −2qs·qw·(tgt − x), lxx = diag(2qs·qw), lu = 2rs·rw·u, luu = diag(2rs·rw)
   for (int i = 0; i < FB_NX; ++i) {
     lx[pt * FB_NX + i] = i < FB_NQ ? P.gx[i] * (P.tgt[i] - xp[i]) : 0.0;
@@ -866,7 +876,7 @@ hipError_t fb_take(ilqr_floating_handle* h, const int32_t* move, const int32_t* 
 }
 
 hipError_t fb_linearize(ilqr_floating_handle* h, const double* x, const double* u, const int32_t* st) {
-  const size_t lanes = (size_t)h->batch * h->T * (ilqr::FB_NX + ilqr::FB_NU);
+  const size_t lanes = (size_t)h->batch * h->T * ilqr::FB_LIN_DIRS;
   ilqr::fb_linearize_kernel<<<(unsigned)((lanes + 255) / 256), 256, 0, h->stream>>>(
       h->model_dev, h->batch, h->T, x, u, st, h->A, h->Bm, h->lx, h->lu, h->lxx, h->luu, h->lfx, h->lfxx);
   return hipGetLastError();
