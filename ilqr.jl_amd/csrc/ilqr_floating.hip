@@ -119,22 +119,32 @@ __device__ __forceinline__ S dotm(const A (&a)[3], const S (&b)[3]) {
   return a[0] * b[0] + a[1] * b[1] + a[2] * b[2];
 }
 
-// continuous dynamics ẋ = [pdot_from_w(p, ω); v; θ̇; M \ (u − bias)] (RBD_helper_functions.jl:50-69).
-// The bias first (recursive Newton-Euler), then M by the composite-rigid-body algorithm
-// kept in blocks — the base's 6×6 composite inertia M₀₀, the base-joint columns M₀ⱼ and
-// the joint block Mⱼⱼ — and M v̇ = b solved through the joint block's Schur complement:
-// M₀₀⁻¹ in closed form (w = I_c⁻¹(n − c × f), v = f/m + c × w, I_c the composite's
-// inertia about its COM c), so no 8 × 8 matrix is ever held.
+// continuous dynamics ẋ = [pdot_from_w(p, ω); v; θ̇; M \ (u − bias)] (RBD_helper_functions.jl:50-69),
+// in four pieces that fb_xdot composes and the two-wave forward splits between its
+// waves (same operations either way, so the same bits):
+//   fb_rots   the joints' rotations from θ;
+//   fb_bias   the bias (base moment and force, joint torques) by recursive Newton-Euler
+//             at q̈ = 0 — independent of u; b = u − bias;
+//   fb_mass   M by the composite-rigid-body algorithm kept in blocks — the base's 6×6
+//             composite inertia M₀₀, the base-joint columns M₀ⱼ and the joint block Mⱼⱼ —
+//             and what M v̇ = b needs of it: M₀₀⁻¹ in closed form (w = I_c⁻¹(n − c × f),
+//             v = f/m + c × w, I_c the composite's inertia about its COM c), Y = M₀₀⁻¹M₀ⱼ
+//             and the joint block's Schur complement;
+//   fb_solve  v̇ from b through that complement, and the kinematics.
+// No 8 × 8 matrix is ever held.
 template <class S>
-__device__ void fb_xdot(const FbModel& P, const S (&x)[FB_NX], const S (&u)[FB_NU], S (&xd)[FB_NX]) {
-  S R[FB_NJ][9];
+__device__ __forceinline__ void fb_rots(const FbModel& P, const S (&x)[FB_NX], S (&R)[FB_NJ][9]) {
 #pragma unroll
   for (int i = 0; i < FB_NJ; ++i) {
     S s, c;
     sincos_s(x[6 + i], s, c);
     joint_rot(P, i, c, s, R[i]);
   }
+}
 
+template <class S>
+__device__ __forceinline__ void fb_bias(const FbModel& P, const S (&R)[FB_NJ][9], const S (&x)[FB_NX],
+                                        S (&q)[FB_NU]) {
   // --- bias, recursive Newton-Euler at q̈ = 0, zero gravity (:65) -----------------------
   // outward: v_{i+1} = X v_i + s q̇, a_{i+1} = X a_i + v_{i+1} × (s q̇) (a₀ = 0)
   S vw[FB_NJ + 1][3], vv[FB_NJ + 1][3], aw[FB_NJ + 1][3], av[FB_NJ + 1][3];
@@ -229,15 +239,50 @@ __device__ void fb_xdot(const FbModel& P, const S (&x)[FB_NX], const S (&u)[FB_N
       }
     }
   }
-  S b[FB_NU];
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
-    b[k] = u[k] - fn[k];
-    b[3 + k] = u[3 + k] - ff[k];
+    q[k] = fn[k];
+    q[3 + k] = ff[k];
   }
 #pragma unroll
-  for (int j = 0; j < FB_NJ; ++j) b[6 + j] = u[6 + j] - tau[j];
+  for (int j = 0; j < FB_NJ; ++j) q[6 + j] = tau[j];
+}
 
+// M's blocks reduced to what the solve needs (fb_mass → fb_solve)
+template <class S>
+struct FbSchur {
+  S cc[3];                     // the composite's COM c
+  double minv;                 // 1 / total mass
+  S d0i, d1i, d2i, l10, l20, l21;  // LDLᵀ of I_c
+  S Mb[FB_NJ][6];              // base-joint columns M₀ⱼ
+  S Y[FB_NJ][6];               // M₀₀⁻¹ M₀ⱼ
+  S Sc[FB_NJ][FB_NJ];          // Mⱼⱼ − M₀ⱼᵀ Y
+  // M₀₀⁻¹(n, f) = (w, f/m + c × w), w = I_c⁻¹(n − c × f)
+  __device__ __forceinline__ void m00inv(const S (&g)[6], S (&o)[6]) const {
+    S cf[3], r[3];
+    const S fv[3] = {g[3], g[4], g[5]};
+    crossm(cc, fv, cf);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) r[k] = g[k] - cf[k];
+    r[1] = r[1] - l10 * r[0];
+    r[2] = r[2] - l20 * r[0] - l21 * r[1];
+    r[0] = r[0] * d0i;
+    r[1] = r[1] * d1i;
+    r[2] = r[2] * d2i;
+    r[1] = r[1] - l21 * r[2];
+    r[0] = r[0] - l10 * r[1] - l20 * r[2];
+    S cw[3];
+    crossm(cc, r, cw);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      o[k] = r[k];
+      o[3 + k] = fv[k] * minv + cw[k];
+    }
+  }
+};
+
+template <class S>
+__device__ __forceinline__ void fb_mass(const FbModel& P, const S (&R)[FB_NJ][9], FbSchur<S>& F) {
   // --- M, composite-rigid-body algorithm (:61), tip to base ------------------------------
   // composite of bodies k..NJ in body k's frame: (m, h, Io)
   double cm = P.m[FB_NJ];
@@ -247,7 +292,6 @@ __device__ void fb_xdot(const FbModel& P, const S (&x)[FB_NX], const S (&u)[FB_N
 #pragma unroll
   for (int k = 0; k < 9; ++k) cI[k] = P.Io[FB_NJ][k];
   S Mjj[FB_NJ][FB_NJ];  // joint block
-  S Mb[FB_NJ][6];       // base-joint columns: joint j's (n, f) carried to the base frame
 #pragma unroll
   for (int j = FB_NJ - 1; j >= 0; --j) {
     // F = C_{j+1} s_j = (Io a, −h × a) in body j+1's frame; M_jj = aᵀ n
@@ -273,8 +317,8 @@ __device__ void fb_xdot(const FbModel& P, const S (&x)[FB_NX], const S (&u)[FB_N
     }
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-      Mb[j][k] = n[k];
-      Mb[j][3 + k] = f[k];
+      F.Mb[j][k] = n[k];
+      F.Mb[j][3 + k] = f[k];
     }
     // composite of body j: own inertia + the child composite moved across joint j:
     // h' = Rc h, Io' = Rc Io Rcᵀ + m(|p|²1 − p pᵀ) + 2(p·h')1 − p h'ᵀ − h' pᵀ, h'' = h' + m p
@@ -302,17 +346,16 @@ __device__ void fb_xdot(const FbModel& P, const S (&x)[FB_NX], const S (&u)[FB_N
     cm = P.m[j] + cm;
   }
 
-  // --- M v̇ = b through the Schur complement of M₀₀ ---------------------------------------
+  // --- M₀₀⁻¹ and the Schur complement of M₀₀ ---------------------------------------------
   // M₀₀ = [[Io, [h×]], [[h×]ᵀ, m1]]: with c = h/m and I_c = Io − m(|c|²1 − c cᵀ),
   // M₀₀⁻¹(n, f) = (w, f/m + c × w), w = I_c⁻¹(n − c × f)
-  const double minv = 1.0 / cm;
-  S cc[3];
+  F.minv = 1.0 / cm;
 #pragma unroll
-  for (int k = 0; k < 3; ++k) cc[k] = ch[k] * minv;
+  for (int k = 0; k < 3; ++k) F.cc[k] = ch[k] * F.minv;
   S Ic[6];  // I_c lower triangle: 00, 10, 11, 20, 21, 22
   {
-    const S c2 = dotm(cc, cc);
-    auto ent = [&](int r, int k) { return cI[3 * r + k] - cm * ((r == k ? c2 : S(0.0)) - cc[r] * cc[k]); };
+    const S c2 = dotm(F.cc, F.cc);
+    auto ent = [&](int r, int k) { return cI[3 * r + k] - cm * ((r == k ? c2 : S(0.0)) - F.cc[r] * F.cc[k]); };
     Ic[0] = ent(0, 0);
     Ic[1] = ent(1, 0);
     Ic[2] = ent(1, 1);
@@ -321,63 +364,50 @@ __device__ void fb_xdot(const FbModel& P, const S (&x)[FB_NX], const S (&u)[FB_N
     Ic[5] = ent(2, 2);
   }
   // LDLᵀ of I_c: l10, l20, l21 and 1/d
-  const S d0i = S(1.0) / Ic[0];
-  const S l10 = Ic[1] * d0i, l20 = Ic[3] * d0i;
-  const S d1 = Ic[2] - l10 * Ic[1];
-  const S d1i = S(1.0) / d1;
-  const S l21 = (Ic[4] - l20 * Ic[1]) * d1i;
-  const S d2i = S(1.0) / (Ic[5] - l20 * Ic[3] - l21 * (l21 * d1));
-  auto m00inv = [&](const S (&g)[6], S (&o)[6]) {
-    S cf[3], r[3];
-    const S fv[3] = {g[3], g[4], g[5]};
-    crossm(cc, fv, cf);
+  F.d0i = S(1.0) / Ic[0];
+  F.l10 = Ic[1] * F.d0i;
+  F.l20 = Ic[3] * F.d0i;
+  const S d1 = Ic[2] - F.l10 * Ic[1];
+  F.d1i = S(1.0) / d1;
+  F.l21 = (Ic[4] - F.l20 * Ic[1]) * F.d1i;
+  F.d2i = S(1.0) / (Ic[5] - F.l20 * Ic[3] - F.l21 * (F.l21 * d1));
 #pragma unroll
-    for (int k = 0; k < 3; ++k) r[k] = g[k] - cf[k];
-    r[1] = r[1] - l10 * r[0];
-    r[2] = r[2] - l20 * r[0] - l21 * r[1];
-    r[0] = r[0] * d0i;
-    r[1] = r[1] * d1i;
-    r[2] = r[2] * d2i;
-    r[1] = r[1] - l21 * r[2];
-    r[0] = r[0] - l10 * r[1] - l20 * r[2];
-    S cw[3];
-    crossm(cc, r, cw);
+  for (int j = 0; j < FB_NJ; ++j) F.m00inv(F.Mb[j], F.Y[j]);
+  // the joint block's Schur complement Mⱼⱼ − M₀ⱼᵀ Y (2 × 2)
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      o[k] = r[k];
-      o[3 + k] = fv[k] * minv + cw[k];
-    }
-  };
-  S y0[6];
-  {
-    const S g[6] = {b[0], b[1], b[2], b[3], b[4], b[5]};
-    m00inv(g, y0);
-  }
-  S Y[FB_NJ][6];
-#pragma unroll
-  for (int j = 0; j < FB_NJ; ++j) m00inv(Mb[j], Y[j]);
-  // joint block: (Mⱼⱼ − M₀ⱼᵀ Y) v̇ⱼ = bⱼ − M₀ⱼᵀ y₀ (2 × 2)
-  S Sc[FB_NJ][FB_NJ], rj[FB_NJ];
-#pragma unroll
-  for (int i = 0; i < FB_NJ; ++i) {
-    S acc = b[6 + i];
-#pragma unroll
-    for (int k = 0; k < 6; ++k) acc = acc - Mb[i][k] * y0[k];
-    rj[i] = acc;
+  for (int i = 0; i < FB_NJ; ++i)
 #pragma unroll
     for (int j = 0; j < FB_NJ; ++j) {
       S e = Mjj[i][j];
 #pragma unroll
-      for (int k = 0; k < 6; ++k) e = e - Mb[i][k] * Y[j][k];
-      Sc[i][j] = e;
+      for (int k = 0; k < 6; ++k) e = e - F.Mb[i][k] * F.Y[j][k];
+      F.Sc[i][j] = e;
     }
+}
+
+template <class S>
+__device__ __forceinline__ void fb_solve(const FbSchur<S>& F, const S (&b)[FB_NU], const S (&x)[FB_NX],
+                                         S (&xd)[FB_NX]) {
+  // --- M v̇ = b: y₀ = M₀₀⁻¹ b₀, then (Mⱼⱼ − M₀ⱼᵀ Y) v̇ⱼ = bⱼ − M₀ⱼᵀ y₀ ------------------------
+  S y0[6];
+  {
+    const S g[6] = {b[0], b[1], b[2], b[3], b[4], b[5]};
+    F.m00inv(g, y0);
+  }
+  S rj[FB_NJ];
+#pragma unroll
+  for (int i = 0; i < FB_NJ; ++i) {
+    S acc = b[6 + i];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) acc = acc - F.Mb[i][k] * y0[k];
+    rj[i] = acc;
   }
   static_assert(FB_NJ == 2, "the joint block's solve is written for two joints");
-  const S det = Sc[0][0] * Sc[1][1] - Sc[0][1] * Sc[1][0];
-  const S q0 = (rj[0] * Sc[1][1] - Sc[0][1] * rj[1]) / det;
-  const S q1 = (Sc[0][0] * rj[1] - Sc[1][0] * rj[0]) / det;
+  const S det = F.Sc[0][0] * F.Sc[1][1] - F.Sc[0][1] * F.Sc[1][0];
+  const S q0 = (rj[0] * F.Sc[1][1] - F.Sc[0][1] * rj[1]) / det;
+  const S q1 = (F.Sc[0][0] * rj[1] - F.Sc[1][0] * rj[0]) / det;
 #pragma unroll
-  for (int k = 0; k < 6; ++k) xd[8 + k] = y0[k] - (Y[0][k] * q0 + Y[1][k] * q1);
+  for (int k = 0; k < 6; ++k) xd[8 + k] = y0[k] - (F.Y[0][k] * q0 + F.Y[1][k] * q1);
   xd[14] = q0;
   xd[15] = q1;
 
@@ -394,6 +424,19 @@ __device__ void fb_xdot(const FbModel& P, const S (&x)[FB_NX], const S (&u)[FB_N
   for (int k = 0; k < 3; ++k) xd[3 + k] = x[11 + k];
 #pragma unroll
   for (int j = 0; j < FB_NJ; ++j) xd[6 + j] = x[14 + j];
+}
+
+template <class S>
+__device__ void fb_xdot(const FbModel& P, const S (&x)[FB_NX], const S (&u)[FB_NU], S (&xd)[FB_NX]) {
+  S R[FB_NJ][9];
+  fb_rots(P, x, R);
+  S b[FB_NU];
+  fb_bias(P, R, x, b);
+#pragma unroll
+  for (int k = 0; k < FB_NU; ++k) b[k] = u[k] - b[k];
+  FbSchur<S> F;
+  fb_mass(P, R, F);
+  fb_solve(F, b, x, xd);
 }
 
 // dynamicsf: RK4 of fb_xdot (RBD_helper_functions.jl:71-78): kᵢ = Δt·f(·),
@@ -548,54 +591,171 @@ struct FbFwd {
 // One trial's rollout (forward_pass.jl:65-76) → cost, Σ(ū − u)², and whether every
 // ū = u + α·δu equals u (then every later, smaller α rolls out the same); stores x̄
 // into xn, ū into un as it goes.
-__device__ double fb_rollout(const FbModel& P, const FbFwd& a, int b, int T, double alpha, double* __restrict__ xn,
-                             double* __restrict__ un, double& du2, bool& same) {
+//
+// It runs on three waves (fb_forward_kernel): a workgroup of three waves holds the same
+// 64 (trajectory, trial) lanes and splits each step between them —
+//   wave 0 (mass):    the mass blocks and their factors (fb_mass) of every RK4 stage, from
+//                     the stage's joint angles;
+//   wave 1 (main):    the bias of every stage (fb_bias: independent of u), then
+//                     b = ū − bias, the solve and the stage update (fb_solve), storing x̄;
+//   wave 2 (control): the step's ūₜ = uₜ + α·δuₜ + Kₜ(x̄ₜ − xₜ), its cost and Σ(ū − u)²,
+//                     storing ū — beside stage 1's mass and bias.
+// Per stage waves 0 and 2 hand the factors and ū to wave 1 through LDS, and wave 1 hands
+// back the next stage's angles (the next step's state at the last stage), between two
+// workgroup barriers. One wave alone issues a VALU instruction every 4 cycles at best,
+// so a lane's step (≈7,800 instructions on one wave) is bound by its wave's issue; the
+// three waves issue side by side. Same operations as fb_step: the same bits.
+constexpr int FB_SCHUR_N = (int)(sizeof(FbSchur<double>) / sizeof(double));
+static_assert(sizeof(FbSchur<double>) == FB_SCHUR_N * sizeof(double), "FbSchur<double> is doubles only");
+constexpr int FB_XU = FB_SCHUR_N;            // ū (8)
+constexpr int FB_XX = FB_SCHUR_N + FB_NU;    // the stage's state (angles; all 16 at a step's end)
+struct FbXch {
+  double v[FB_XX + FB_NX][64];  // value-major: lane l's k-th value at v[k][l]
+};
+constexpr int FB_FWD_WAVES = 3;
+
+// every wave reaches it: its LDS writes done (lgkmcnt only — the rollout's global stores
+// stay in flight), then the workgroup barrier
+__device__ __forceinline__ void fb_lds_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_waitcnt((15) | (7 << 4) | (0 << 8) | (3 << 14));
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+__device__ double fb_rollout3(const FbModel& P, const FbFwd& a, int b, int T, double alpha, double* __restrict__ xn,
+                              double* __restrict__ un, double& du2, bool& same, int role, int lane, FbXch& X) {
   const double* x = a.x + (size_t)b * (T + 1) * FB_NX;
-  const double* u = a.u + (size_t)b * T * FB_NU;
-  const double* xt = a.xtraj ? a.xtraj + (size_t)b * (T + 1) * FB_NX : nullptr;
-  const double* d = a.d + (size_t)b * T * FB_NU;
-  const double* K = a.K + (size_t)b * T * FB_NU * FB_NX;
-  double xb[FB_NX];
+  if (role == 0) {  // mass: angles in, factors out, four times a step
+    double th[FB_NX];  // only th[6], th[7] (the joint angles) are read by fb_rots
 #pragma unroll
-  for (int k = 0; k < FB_NX; ++k) {
-    xb[k] = x[k];  // x̄₁ = x₁ (:65)
-    xn[k] = xb[k];
-  }
-  double cost = 0.0, s2 = 0.0;
-  bool eq = true;
-  for (int t = 0; t < T; ++t) {
-    double dx[FB_NX], ub[FB_NU];
+    for (int k = 0; k < FB_NX; ++k) th[k] = k == 6 || k == 7 ? x[k] : 0.0;
+    for (int t = 0; t < T; ++t) {
+#pragma unroll 1
+      for (int st = 0; st < 4; ++st) {
+        asm volatile("" ::: "memory");  // the model's constants re-read per stage (fb_step)
+        double R[FB_NJ][9];
+        fb_rots(P, th, R);
+        FbSchur<double> F;
+        fb_mass(P, R, F);
+        const double* f = reinterpret_cast<const double*>(&F);
 #pragma unroll
-    for (int k = 0; k < FB_NX; ++k) dx[k] = xb[k] - x[(size_t)t * FB_NX + k];  // :72
-#pragma unroll
-    for (int j = 0; j < FB_NU; ++j) {
-      const double uj = u[(size_t)t * FB_NU + j];
-      const double ua = uj + alpha * d[(size_t)t * FB_NU + j];  // :73
-      eq = eq && ua == uj;
-      double kd = 0.0;
-#pragma unroll
-      for (int k = 0; k < FB_NX; ++k) kd = fma(K[((size_t)t * FB_NU + j) * FB_NX + k], dx[k], kd);
-      ub[j] = ua + kd;
-      const double e = ub[j] - uj;
-      s2 = fma(e, e, s2);
+        for (int k = 0; k < FB_SCHUR_N; ++k) X.v[k][lane] = f[k];
+        fb_lds_barrier();
+        fb_lds_barrier();
+        th[6] = X.v[FB_XX + 6][lane];
+        th[7] = X.v[FB_XX + 7][lane];
+      }
     }
-    // ℓ(x̄ₜ − x_trajₜ, ūₜ) (:187-190, the cost pieces are the first 8 state rows)
-    double ev[FB_NQ];
+  } else if (role == 2) {  // control: ūₜ (:72-73), its cost (:187-190), Σ(ū − u)²
+    const double* u = a.u + (size_t)b * T * FB_NU;
+    const double* xt = a.xtraj ? a.xtraj + (size_t)b * (T + 1) * FB_NX : nullptr;
+    const double* d = a.d + (size_t)b * T * FB_NU;
+    const double* K = a.K + (size_t)b * T * FB_NU * FB_NX;
+    double xb[FB_NX];
 #pragma unroll
-    for (int k = 0; k < FB_NQ; ++k) ev[k] = xt ? xb[k] - xt[(size_t)t * FB_NX + k] : xb[k];
-    cost = cost + stage_cost(P, ev, ub);
-    double y[FB_NX];
-    fb_step(P, xb, ub, y);  // :74
+    for (int k = 0; k < FB_NX; ++k) xb[k] = x[k];  // x̄₁ = x₁ (:65)
+    double cost = 0.0, s2 = 0.0;
+    bool eq = true;
+    for (int t = 0; t < T; ++t) {
+      double dx[FB_NX], ub[FB_NU];
 #pragma unroll
-    for (int k = 0; k < FB_NX; ++k) xb[k] = y[k];
+      for (int k = 0; k < FB_NX; ++k) dx[k] = xb[k] - x[(size_t)t * FB_NX + k];
 #pragma unroll
-    for (int j = 0; j < FB_NU; ++j) un[(size_t)t * FB_NU + j] = ub[j];
+      for (int j = 0; j < FB_NU; ++j) {
+        const double uj = u[(size_t)t * FB_NU + j];
+        const double ua = uj + alpha * d[(size_t)t * FB_NU + j];
+        eq = eq && ua == uj;
+        double kd = 0.0;
 #pragma unroll
-    for (int k = 0; k < FB_NX; ++k) xn[(size_t)(t + 1) * FB_NX + k] = xb[k];
+        for (int k = 0; k < FB_NX; ++k) kd = fma(K[((size_t)t * FB_NU + j) * FB_NX + k], dx[k], kd);
+        ub[j] = ua + kd;
+        X.v[FB_XU + j][lane] = ub[j];
+        const double e = ub[j] - uj;
+        s2 = fma(e, e, s2);
+      }
+#pragma unroll
+      for (int j = 0; j < FB_NU; ++j) un[(size_t)t * FB_NU + j] = ub[j];
+      double ev[FB_NQ];
+#pragma unroll
+      for (int k = 0; k < FB_NQ; ++k) ev[k] = xt ? xb[k] - xt[(size_t)t * FB_NX + k] : xb[k];
+      cost = cost + stage_cost(P, ev, ub);
+#pragma unroll 1
+      for (int st = 0; st < 4; ++st) {
+        fb_lds_barrier();
+        fb_lds_barrier();
+      }
+#pragma unroll
+      for (int k = 0; k < FB_NX; ++k) xb[k] = X.v[FB_XX + k][lane];  // x̄ₜ₊₁
+    }
+    cost = cost + final_cost(P, xb);  // :192 (raw x̄_N)
+    X.v[0][lane] = cost;  // the outcome to waves 0 and 1
+    X.v[1][lane] = s2;
+    X.v[2][lane] = eq ? 1.0 : 0.0;
+  } else {  // main: bias, solve, stage update
+    double xb[FB_NX];
+#pragma unroll
+    for (int k = 0; k < FB_NX; ++k) {
+      xb[k] = x[k];
+      xn[k] = xb[k];
+    }
+    for (int t = 0; t < T; ++t) {
+      double xs[FB_NX], acc[FB_NX], ub[FB_NU];
+#pragma unroll
+      for (int i = 0; i < FB_NX; ++i) xs[i] = xb[i];
+#pragma unroll 1
+      for (int st = 0; st < 4; ++st) {
+        asm volatile("" ::: "memory");
+        double R[FB_NJ][9];
+        fb_rots(P, xs, R);
+        double bb[FB_NU];
+        fb_bias(P, R, xs, bb);
+        // the bias is complete before the barrier (else the compiler sinks it past the
+        // barrier, behind wave 0's mass, into the serial part of the stage)
+#pragma unroll
+        for (int j = 0; j < FB_NU; ++j) asm volatile("" ::"v"(bb[j]));
+        fb_lds_barrier();
+        if (st == 0) {
+#pragma unroll
+          for (int j = 0; j < FB_NU; ++j) ub[j] = X.v[FB_XU + j][lane];
+        }
+#pragma unroll
+        for (int j = 0; j < FB_NU; ++j) bb[j] = ub[j] - bb[j];
+        FbSchur<double> F;
+        double* f = reinterpret_cast<double*>(&F);
+#pragma unroll
+        for (int k = 0; k < FB_SCHUR_N; ++k) f[k] = X.v[k][lane];
+        double k[FB_NX];
+        fb_solve(F, bb, xs, k);
+        const double w = (st == 0 || st == 3) ? 1.0 : 2.0;
+        const double c = st == 2 ? 1.0 : 0.5;
+#pragma unroll
+        for (int i = 0; i < FB_NX; ++i) {
+          k[i] = P.dt * k[i];
+          acc[i] = st == 0 ? k[i] : acc[i] + w * k[i];
+          xs[i] = st < 3 ? xb[i] + k[i] * c : xb[i] + (1.0 / 6.0) * acc[i];
+        }
+        if (st < 3) {
+          X.v[FB_XX + 6][lane] = xs[6];
+          X.v[FB_XX + 7][lane] = xs[7];
+        } else {
+#pragma unroll
+          for (int i = 0; i < FB_NX; ++i) X.v[FB_XX + i][lane] = xs[i];
+        }
+        fb_lds_barrier();
+      }
+#pragma unroll
+      for (int k = 0; k < FB_NX; ++k) {
+        xb[k] = xs[k];
+        xn[(size_t)(t + 1) * FB_NX + k] = xb[k];
+      }
+    }
   }
-  cost = cost + final_cost(P, xb);  // :192 (raw x̄_N)
-  du2 = s2;
-  same = eq;
+  fb_lds_barrier();
+  const double cost = X.v[0][lane];
+  du2 = X.v[1][lane];
+  same = X.v[2][lane] != 0.0;
+  fb_lds_barrier();  // read before the next rollout writes
   return cost;
 }
 
@@ -603,8 +763,10 @@ __device__ double fb_rollout(const FbModel& P, const FbFwd& a, int b, int T, dou
 // j, j+1, … at once; the first accepted trial (prev_cost − cost > 0, :77-80) is the
 // sequential search's; a rejected trial whose ū all equal u ends the search (every later
 // trial rolls out identically), as does max_trials (the reference loops unbounded).
-__global__ __launch_bounds__(64) void fb_forward_kernel(const FbModel* __restrict__ Pm, int B, int T, FbFwd a) {
+__global__ __launch_bounds__(64 * FB_FWD_WAVES) void fb_forward_kernel(const FbModel* __restrict__ Pm, int B, int T, FbFwd a) {
   const FbModel& P = *Pm;
+  __shared__ FbXch X;
+  const int role = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // the waves of fb_rollout3
   const int lane = threadIdx.x & 63;
   const int c = lane % FB_CAND;
   const int b = (blockIdx.x * 64 + lane) / FB_CAND;
@@ -626,7 +788,7 @@ __global__ __launch_bounds__(64) void fb_forward_kernel(const FbModel* __restric
     if (run) {
       double* xo = j == 1 ? a.xn + (size_t)b * nxe : slot;
       double* uo = j == 1 ? a.un + (size_t)b * nue : slot + nxe;
-      cost = fb_rollout(P, a, b, T, alpha, xo, uo, du2, same);
+      cost = fb_rollout3(P, a, b, T, alpha, xo, uo, du2, same, role, lane, X);
     }
     const bool acc = run && (pc - cost > 0.0);
     // the trajectory's lanes agree on the outcome: the smallest accepted j, else whether a
@@ -657,10 +819,11 @@ __global__ __launch_bounds__(64) void fb_forward_kernel(const FbModel* __restric
     if (!__any(live && done_trial == 0)) break;
   }
   if (live && done_trial <= 0) {  // no trial accepted: x̄, ū = the inputs, as the closure path
-    for (size_t i = c; i < nxe; i += FB_CAND) a.xn[(size_t)b * nxe + i] = a.x[(size_t)b * nxe + i];
-    for (size_t i = c; i < nue; i += FB_CAND) a.un[(size_t)b * nue + i] = a.u[(size_t)b * nue + i];
+    const size_t c2 = (size_t)(FB_FWD_WAVES * c + role);
+    for (size_t i = c2; i < nxe; i += FB_FWD_WAVES * FB_CAND) a.xn[(size_t)b * nxe + i] = a.x[(size_t)b * nxe + i];
+    for (size_t i = c2; i < nue; i += FB_FWD_WAVES * FB_CAND) a.un[(size_t)b * nue + i] = a.u[(size_t)b * nue + i];
   }
-  if (live && c == 0) {
+  if (live && c == 0 && role == 0) {
     const bool acc = done_trial > 0;
     a.trials[b] = acc ? done_trial : a.max_trials;
     a.new_cost[b] = done_cost;
@@ -1038,7 +1201,8 @@ ilqr_status ilqr_floating_forward(ilqr_floating_handle* h, const ilqr_options* o
   fa.alpha0 = ls.alpha0;
   fa.shrink = ls.shrink;
   fa.max_trials = ls.max_trials;
-  ilqr::fb_forward_kernel<<<(unsigned)((h->batch * ilqr::FB_CAND + 63) / 64), 64, 0, h->stream>>>(
+  ilqr::fb_forward_kernel<<<(unsigned)((h->batch * ilqr::FB_CAND + 63) / 64), 64 * ilqr::FB_FWD_WAVES, 0,
+                             h->stream>>>(
       h->model_dev, h->batch, h->T, fa);
   FB_TRY(hipGetLastError());
   // x̄, ū of a trajectory whose first trial was accepted are written as it rolled out; a
@@ -1096,7 +1260,8 @@ ilqr_status ilqr_floating_fit_ex(ilqr_floating_handle* h, const ilqr_options* o,
   for (int it = 1; it <= max_iter; ++it) {  // forward_pass.jl:161
     FB_TRY(fb_linearize(h, h->x, h->u, h->status));
     FB_TRY(ilqr::launch_tiles_backward(ilqr::FB_NX, ilqr::FB_NU, tp, B, T, h->d, h->K, h->bstatus, ls.mu, s));
-    ilqr::fb_forward_kernel<<<(unsigned)((B * ilqr::FB_CAND + 63) / 64), 64, 0, s>>>(h->model_dev, B, T, fa);
+    ilqr::fb_forward_kernel<<<(unsigned)((B * ilqr::FB_CAND + 63) / 64), 64 * ilqr::FB_FWD_WAVES, 0, s>>>(
+        h->model_dev, B, T, fa);
     FB_TRY(hipGetLastError());
     ilqr::fb_update_kernel<<<g, 256, 0, s>>>(B, T, it, ls.tol, h->bstatus, h->fstatus, h->cost, h->du2,
                                              h->status, h->iters, h->prev_cost, h->move);

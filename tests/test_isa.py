@@ -99,10 +99,11 @@ def test_tiles_kernels_have_no_scratch(tmp_path):
 
 @pytest.mark.skipif(not os.path.exists(HIPCC) and shutil.which("hipcc") is None, reason="no hipcc")
 def test_floating_kernels_have_no_scratch(tmp_path):
-    """The floating-base family (ilqr_floating.hip): the dual-number linearisation and the
-    forward keep ~440-490 registers at one wave per SIMD; the model's constants are
-    re-read per RK4 stage instead of hoisted — hoisted, they had spilled to scratch
-    (364 and 140 bytes per lane)."""
+    """The floating-base family (ilqr_floating.hip): the dual-number linearisation keeps
+    ~460 registers at one wave per SIMD, the three-wave forward ~290; the model's
+    constants are re-read per RK4 stage instead of hoisted — hoisted, they had spilled
+    to scratch (364 and 140 bytes per lane), and so did a two-wave forward whose second
+    wave took both the mass and the solve (184 bytes)."""
     hipcc = HIPCC if os.path.exists(HIPCC) else shutil.which("hipcc")
     cmd = [hipcc, "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-save-temps", "-c",
            os.path.join(CSRC, "ilqr_floating.hip"), "-o", str(tmp_path / "fl.o")]
