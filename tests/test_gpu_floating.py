@@ -196,6 +196,48 @@ def test_floating_backward_forward_vs_closure_oracle(gpu):
     assert int(trials[0]) > 1
 
 
+def test_floating_forward_slots_rounds_and_partial_workgroups(gpu):
+    """The line search across rounds of four trials: 17 trajectories (68 trial lanes, the
+    second workgroup partly empty), prev_cost set per trajectory so that the accepted
+    trial falls anywhere in 1..6 or the search exhausts at max_trials = 6 — trials 2..6
+    come from their lanes' slots (trial 5 and 6 from the second round), an exhausted
+    search returns the inputs; every trajectory as the closure oracle's forward_pass."""
+    from oracle import cref
+    nb, T, mt = 17, 30, 6
+    x, u = script_batch(nb, T, seed=29)
+    u = u + 0.5 * np.random.default_rng(31).standard_normal(u.shape)
+    fj, lj, lfj = rbd_floating_arm(jet_ns())
+    # the iterate a rollout of u (the forward's inputs must be a consistent trajectory)
+    for t in range(T):
+        x[:, t + 1] = fj(x[:, t], u[:, t])
+    tl = CF.derivative_tiles(x, u, fj, *rbd_cost_quads())
+    d, K, _ = cref.tiles_backward(tl, mu=0.01, symmetrize=True)
+    d = 32.0 * d  # trial j's step is 2^(6−j)·δu: the cost falls over trials 1..6
+    zt = np.zeros_like(x)
+    # the cost of trial j alone (α = 0.5^(j−1)), j = 1..8
+    c = np.stack([CF.forward_pass(x, u, zt, d, K, np.full(nb, np.inf), fj, lj, lfj, max_trials=1,
+                                  alpha0=0.5 ** (j - 1))[2] for j in range(1, 9)], axis=1)
+    prev = np.full(nb, np.inf)
+    for b in range(nb):
+        k = 1 + b % 7  # aim at trial k: prev = the smallest cost of trials 1..k−1
+        if k > 1:
+            prev[b] = c[b, :k - 1].min()
+    xo, uo, co, tro, ok = CF.forward_pass(x, u, zt, d, K, prev, fj, lj, lfj, max_trials=mt)
+    assert set(tro[ok].tolist()) >= {1, 2, 3} and (~ok).any() and (tro[ok] > 4).any()
+    o = _lib.default_options(max_trials=mt)
+    s = FloatingSolver(rbd_example_problem(), T, nb)
+    try:
+        xn, un, cost, trials, st = s.forward(*(torch.from_numpy(a).cuda() for a in (x, u, d, K, prev)),
+                                             options=o)
+    finally:
+        s.close()
+    assert trials.tolist() == tro.tolist()
+    assert st.tolist() == [_lib.TRAJ_OK if a else _lib.TRAJ_LS_EXHAUSTED for a in ok]
+    assert rel(cost, co) < 1e-10 and rel(xn, xo) < 1e-10 and rel(un, uo) < 1e-10
+    ex = ~ok
+    assert np.array_equal(xn.cpu().numpy()[ex], x[ex]) and np.array_equal(un.cpu().numpy()[ex], u[ex])
+
+
 def test_floating_fit_x_traj_and_edges(gpu):
     """x_traj enters the line search's cost (forward_pass.jl:187-190) as in the oracle;
     max_iter = 0 returns the inputs (status MAX_ITER); two fits on one handle are
