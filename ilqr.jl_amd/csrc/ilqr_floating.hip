@@ -27,6 +27,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <cstdint>
 #include <string>
 #include <vector>
@@ -41,7 +42,7 @@ constexpr int FB_NJ = 2;             // joints (the reference's arm)
 constexpr int FB_NQ = 6 + FB_NJ;     // pose coordinates in the cost: p (3), r (3), θ
 constexpr int FB_NX = 2 * FB_NQ;     // 16
 constexpr int FB_NU = FB_NQ;         // 8: base torque, base force, joint torques
-constexpr int FB_CAND = 4;           // line-search trials per trajectory per round
+constexpr int FB_CAND = 4;           // line-search trials per trajectory per round (large batches)
 
 // forward-mode dual with one partial (one input direction per lane)
 struct D1 {
@@ -583,7 +584,7 @@ struct FbFwd {
   int32_t* trials;
   int32_t* fstatus;        // out: 0 accepted, LS_EXHAUSTED, NAN
   const int32_t* status;   // in: trajectories with a set status are skipped (nullable)
-  double* slots;           // (B, FB_CAND, (T+1)·nx + T·nu): trials j > 1, slot (j − 1) mod FB_CAND
+  double* slots;           // (B, cand, (T+1)·nx + T·nu): trials j > 1, slot (j − 1) mod cand
   double alpha0, shrink;
   int max_trials;
 };
@@ -624,7 +625,11 @@ __device__ __forceinline__ void fb_lds_barrier() {
 }
 
 __device__ double fb_rollout3(const FbModel& P, const FbFwd& a, int b, int T, double alpha, double* __restrict__ xn,
-                              double* __restrict__ un, double& du2, bool& same, int role, int lane, FbXch& X) {
+                              double* __restrict__ un, double& du2, bool& same, int role, int lane) {
+  // the workgroup's exchange, named here rather than passed by reference: through a
+  // reference the compiler lost its address space in some instantiations and read it
+  // with flat loads, whose waits cover the global loads in flight too
+  __shared__ FbXch X;
   const double* x = a.x + (size_t)b * (T + 1) * FB_NX;
   if (role == 0) {  // mass: angles in, factors out, four times a step
     double th[FB_NX];  // only th[6], th[7] (the joint angles) are read by fb_rots
@@ -759,28 +764,31 @@ __device__ double fb_rollout3(const FbModel& P, const FbFwd& a, int b, int T, do
   return cost;
 }
 
-// forward_pass for every trajectory: FB_CAND consecutive lanes roll out trials
+// forward_pass for every trajectory: CAND consecutive lanes roll out trials
 // j, j+1, … at once; the first accepted trial (prev_cost − cost > 0, :77-80) is the
 // sequential search's; a rejected trial whose ū all equal u ends the search (every later
 // trial rolls out identically), as does max_trials (the reference loops unbounded).
+// CAND (fb_cand): 4 lanes a trajectory for large batches; small batches, whose waves
+// would otherwise run a few live lanes, spend the idle ones on further trials (16 or 64
+// a round) — same choice, fewer rounds for a long search. Trial j's α is α₀ multiplied
+// by shrink j − 1 times in order, the reference's repeated `α *= shrink` (:82).
+template <int CAND>
 __global__ __launch_bounds__(64 * FB_FWD_WAVES) void fb_forward_kernel(const FbModel* __restrict__ Pm, int B, int T, FbFwd a) {
+  static_assert(CAND == 4 || CAND == 16 || CAND == 64, "a trajectory's lanes sit in one wave");
   const FbModel& P = *Pm;
-  __shared__ FbXch X;
   const int role = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // the waves of fb_rollout3
   const int lane = threadIdx.x & 63;
-  const int c = lane % FB_CAND;
-  const int b = (blockIdx.x * 64 + lane) / FB_CAND;
+  const int c = lane % CAND;
+  const int b = (blockIdx.x * 64 + lane) / CAND;
   const bool live = b < B && !(a.status && a.status[b] != ILQR_TRAJ_OK);
   const double pc = live ? a.prev_cost[b] : 0.0;
   int done_trial = 0;     // accepted trial (> 0), or −(last trial) when the search ended
   double done_cost = NAN, done_du2 = 0.0;
-  double alpha = a.alpha0;
+  double alpha = a.alpha0;  // trial c + 1's
   for (int k = 0; k < c; ++k) alpha *= a.shrink;
-  double step = 1.0;
-  for (int k = 0; k < FB_CAND; ++k) step *= a.shrink;
   const size_t nxe = (size_t)(T + 1) * FB_NX, nue = (size_t)T * FB_NU;
-  double* slot = a.slots + ((size_t)b * FB_CAND + c) * (nxe + nue);
-  for (int j0 = 1; j0 <= a.max_trials; j0 += FB_CAND) {
+  double* slot = a.slots + ((size_t)b * CAND + c) * (nxe + nue);
+  for (int j0 = 1; j0 <= a.max_trials; j0 += CAND) {
     const int j = j0 + c;
     const bool run = live && done_trial == 0 && j <= a.max_trials;
     double cost = NAN, du2 = 0.0;
@@ -788,40 +796,41 @@ __global__ __launch_bounds__(64 * FB_FWD_WAVES) void fb_forward_kernel(const FbM
     if (run) {
       double* xo = j == 1 ? a.xn + (size_t)b * nxe : slot;
       double* uo = j == 1 ? a.un + (size_t)b * nue : slot + nxe;
-      cost = fb_rollout3(P, a, b, T, alpha, xo, uo, du2, same, role, lane, X);
+      cost = fb_rollout3(P, a, b, T, alpha, xo, uo, du2, same, role, lane);
     }
     const bool acc = run && (pc - cost > 0.0);
     // the trajectory's lanes agree on the outcome: the smallest accepted j, else whether a
     // rejected trial with ū = u ended the search, else the round's last trial
     const uint64_t accm = __ballot(acc), endm = __ballot(run && !acc && same), runm = __ballot(run);
-    const int g0 = (lane / FB_CAND) * FB_CAND;
-    const uint32_t ga = (uint32_t)((accm >> g0) & ((1u << FB_CAND) - 1));
-    const uint32_t ge = (uint32_t)((endm >> g0) & ((1u << FB_CAND) - 1));
-    const uint32_t gr = (uint32_t)((runm >> g0) & ((1u << FB_CAND) - 1));
+    const int g0 = (lane / CAND) * CAND;
+    constexpr uint64_t gm = CAND == 64 ? ~0ull : (1ull << CAND) - 1;
+    const uint64_t ga = (accm >> g0) & gm;
+    const uint64_t ge = (endm >> g0) & gm;
+    const uint64_t gr = (runm >> g0) & gm;
     // the first accepted lane, the first ending lane, the last lane that ran (every lane
     // takes part in the shuffles)
-    const int ca = ga ? __builtin_ctz(ga) : FB_CAND;
-    const int ce = ge ? __builtin_ctz(ge) : FB_CAND;
-    const int cl = gr ? 31 - __builtin_clz(gr) : 0;
-    const int pick = ca < FB_CAND && ca <= ce ? ca : (ce < FB_CAND ? ce : cl);
+    const int ca = ga ? __builtin_ctzll(ga) : CAND;
+    const int ce = ge ? __builtin_ctzll(ge) : CAND;
+    const int cl = gr ? 63 - __builtin_clzll(gr) : 0;
+    const int pick = ca < CAND && ca <= ce ? ca : (ce < CAND ? ce : cl);
     const double pcost = __shfl(cost, g0 + pick, 64);
     const double pdu2 = __shfl(du2, g0 + pick, 64);
     if (live && done_trial == 0 && gr) {
-      if (ca < FB_CAND && ca <= ce) {
+      if (ca < CAND && ca <= ce) {
         done_trial = j0 + ca;
-      } else if (ce < FB_CAND || j0 + cl >= a.max_trials) {
-        done_trial = -(ce < FB_CAND ? a.max_trials : j0 + cl);
+      } else if (ce < CAND || j0 + cl >= a.max_trials) {
+        done_trial = -(ce < CAND ? a.max_trials : j0 + cl);
       }
       done_cost = pcost;
       done_du2 = pdu2;
     }
-    alpha *= step;
+    for (int k = 0; k < CAND; ++k) alpha *= a.shrink;  // trial j + CAND's
     if (!__any(live && done_trial == 0)) break;
   }
   if (live && done_trial <= 0) {  // no trial accepted: x̄, ū = the inputs, as the closure path
     const size_t c2 = (size_t)(FB_FWD_WAVES * c + role);
-    for (size_t i = c2; i < nxe; i += FB_FWD_WAVES * FB_CAND) a.xn[(size_t)b * nxe + i] = a.x[(size_t)b * nxe + i];
-    for (size_t i = c2; i < nue; i += FB_FWD_WAVES * FB_CAND) a.un[(size_t)b * nue + i] = a.u[(size_t)b * nue + i];
+    for (size_t i = c2; i < nxe; i += FB_FWD_WAVES * CAND) a.xn[(size_t)b * nxe + i] = a.x[(size_t)b * nxe + i];
+    for (size_t i = c2; i < nue; i += FB_FWD_WAVES * CAND) a.un[(size_t)b * nue + i] = a.u[(size_t)b * nue + i];
   }
   if (live && c == 0 && role == 0) {
     const bool acc = done_trial > 0;
@@ -865,7 +874,7 @@ __global__ __launch_bounds__(256) void fb_update_kernel(int B, int T, int it, do
 // the accepted trial's x̄, ū into (x, u): trial 1 from (xn, un), trial j > 1 from its
 // slot. fit (move ≠ null): the trajectories that move, into the iterate; forward_pass
 // (move = null): every accepted j > 1, into (xn, un) = (x, u) here
-__global__ __launch_bounds__(256) void fb_take_kernel(int B, int T, const int32_t* __restrict__ move,
+__global__ __launch_bounds__(256) void fb_take_kernel(int B, int T, int cand, const int32_t* __restrict__ move,
                                                       const int32_t* __restrict__ fst,
                                                       const int32_t* __restrict__ trials,
                                                       const double* __restrict__ xn, const double* __restrict__ un,
@@ -878,7 +887,7 @@ __global__ __launch_bounds__(256) void fb_take_kernel(int B, int T, const int32_
     const double* sx = xn + (size_t)b * nx;
     const double* su = un + (size_t)b * nu;
     if (j > 1) {
-      sx = slots + ((size_t)b * FB_CAND + (j - 1) % FB_CAND) * (nx + nu);
+      sx = slots + ((size_t)b * cand + (j - 1) % cand) * (nx + nu);
       su = sx + nx;
     }
     for (size_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nx + nu; i += (size_t)gridDim.x * blockDim.x) {
@@ -927,7 +936,8 @@ struct ilqr_floating_handle {
   double *prev_cost = nullptr, *cost = nullptr, *du2 = nullptr;
   int32_t *trials = nullptr, *status = nullptr, *fstatus = nullptr, *bstatus = nullptr;
   int32_t *iters = nullptr, *move = nullptr, *words = nullptr;
-  double* slots = nullptr;  // the line search's trial slots (FbFwd::slots)
+  double* slots = nullptr;  // the line search's trial slots (FbFwd::slots), cand per trajectory
+  int cand = 4;             // line-search lanes per trajectory (fb_cand)
 };
 
 namespace {
@@ -1001,6 +1011,16 @@ bool fb_model(const ilqr_floating* m, ilqr::FbModel& P) {
   return true;
 }
 
+// line-search lanes per trajectory: 64 up to B = 4 and 16 up to B = 64 (the waves those
+// batches fill would otherwise run a few live lanes), 4 past that
+int fb_cand(int B) {
+  if (const char* e = std::getenv("ILQR_FB_CAND")) {  // A/B measurement override: 4, 16 or 64
+    const int c = std::atoi(e);
+    if (c == 4 || c == 16 || c == 64) return c;
+  }
+  return B <= 4 ? 64 : (B <= 64 ? 16 : ilqr::FB_CAND);
+}
+
 ilqr::LSParams fb_ls(const ilqr_options* o) {
   ilqr_options def;
   ilqr_default_options(&def);
@@ -1034,7 +1054,19 @@ hipError_t fb_take(ilqr_floating_handle* h, const int32_t* move, const int32_t* 
   const size_t n = (size_t)(h->T + 1) * ilqr::FB_NX + (size_t)h->T * ilqr::FB_NU;
   const unsigned gx = (unsigned)((n + 255) / 256 < 64 ? (n + 255) / 256 : 64);
   ilqr::fb_take_kernel<<<dim3(gx, (unsigned)(h->batch < 65535 ? h->batch : 65535)), 256, 0, h->stream>>>(
-      h->batch, h->T, move, fst, trials, xn, un, h->slots, x, u);
+      h->batch, h->T, h->cand, move, fst, trials, xn, un, h->slots, x, u);
+  return hipGetLastError();
+}
+
+// the forward over the batch at the handle's lanes per trajectory
+hipError_t fb_forward(ilqr_floating_handle* h, const ilqr::FbFwd& fa) {
+  const unsigned th = 64 * ilqr::FB_FWD_WAVES, g = (unsigned)(((size_t)h->batch * h->cand + 63) / 64);
+  if (h->cand == 64)
+    ilqr::fb_forward_kernel<64><<<g, th, 0, h->stream>>>(h->model_dev, h->batch, h->T, fa);
+  else if (h->cand == 16)
+    ilqr::fb_forward_kernel<16><<<g, th, 0, h->stream>>>(h->model_dev, h->batch, h->T, fa);
+  else
+    ilqr::fb_forward_kernel<4><<<g, th, 0, h->stream>>>(h->model_dev, h->batch, h->T, fa);
   return hipGetLastError();
 }
 
@@ -1104,7 +1136,8 @@ ilqr_status ilqr_floating_create(ilqr_floating_handle** out, int device, const i
   alloc(&h->iters, 4 * B);
   alloc(&h->move, 4 * B);
   alloc(&h->words, 4 * 4);
-  alloc(&h->slots, 8 * B * ilqr::FB_CAND * ((T + 1) * nx + (size_t)T * nu));
+  h->cand = fb_cand(batch);
+  alloc(&h->slots, 8 * B * h->cand * ((T + 1) * nx + (size_t)T * nu));
   alloc(&h->model_dev, sizeof(ilqr::FbModel));
   if (e == hipSuccess) e = hipMemcpy(h->model_dev, &h->model, sizeof(ilqr::FbModel), hipMemcpyHostToDevice);
   if (e != hipSuccess) {
@@ -1201,10 +1234,7 @@ ilqr_status ilqr_floating_forward(ilqr_floating_handle* h, const ilqr_options* o
   fa.alpha0 = ls.alpha0;
   fa.shrink = ls.shrink;
   fa.max_trials = ls.max_trials;
-  ilqr::fb_forward_kernel<<<(unsigned)((h->batch * ilqr::FB_CAND + 63) / 64), 64 * ilqr::FB_FWD_WAVES, 0,
-                             h->stream>>>(
-      h->model_dev, h->batch, h->T, fa);
-  FB_TRY(hipGetLastError());
+  FB_TRY(fb_forward(h, fa));
   // x̄, ū of a trajectory whose first trial was accepted are written as it rolled out; a
   // later accepted trial is taken from its slot; a search that accepted nothing returns
   // x, u (the closure path's rollout_forward does the same)
@@ -1260,9 +1290,7 @@ ilqr_status ilqr_floating_fit_ex(ilqr_floating_handle* h, const ilqr_options* o,
   for (int it = 1; it <= max_iter; ++it) {  // forward_pass.jl:161
     FB_TRY(fb_linearize(h, h->x, h->u, h->status));
     FB_TRY(ilqr::launch_tiles_backward(ilqr::FB_NX, ilqr::FB_NU, tp, B, T, h->d, h->K, h->bstatus, ls.mu, s));
-    ilqr::fb_forward_kernel<<<(unsigned)((B * ilqr::FB_CAND + 63) / 64), 64 * ilqr::FB_FWD_WAVES, 0, s>>>(
-        h->model_dev, B, T, fa);
-    FB_TRY(hipGetLastError());
+    FB_TRY(fb_forward(h, fa));
     ilqr::fb_update_kernel<<<g, 256, 0, s>>>(B, T, it, ls.tol, h->bstatus, h->fstatus, h->cost, h->du2,
                                              h->status, h->iters, h->prev_cost, h->move);
     FB_TRY(hipGetLastError());

@@ -497,7 +497,8 @@ int ilqr_floating_supported(int n_joints);
 const char* ilqr_floating_last_error(void);
 /* ILQR_ERR_UNSUPPORTED for other joint counts or non-zero gravity. Device memory: the
  * iterate, its tiles and the line search's four trial slots, ≈ batch · T · 8.1 KB
- * (8.1 MB per trajectory at T = 1000) */
+ * (8.1 MB per trajectory at T = 1000) at batch > 64; the slots grow to 16 trials a
+ * trajectory up to batch 64 and 64 up to batch 4 (12.3 MB per trajectory at T = 1000) */
 ilqr_status ilqr_floating_create(ilqr_floating_handle** out, int device, const ilqr_floating* model,
                                  int T, int batch);
 ilqr_status ilqr_floating_destroy(ilqr_floating_handle* h);

@@ -196,14 +196,18 @@ def test_floating_backward_forward_vs_closure_oracle(gpu):
     assert int(trials[0]) > 1
 
 
-def test_floating_forward_slots_rounds_and_partial_workgroups(gpu):
-    """The line search across rounds of four trials: 17 trajectories (68 trial lanes, the
-    second workgroup partly empty), prev_cost set per trajectory so that the accepted
-    trial falls anywhere in 1..6 or the search exhausts at max_trials = 6 — trials 2..6
-    come from their lanes' slots (trial 5 and 6 from the second round), an exhausted
-    search returns the inputs; every trajectory as the closure oracle's forward_pass."""
+@pytest.mark.parametrize("nb,shrink,alpha0", [(17, 0.5, 1.0), (4, 0.7, 0.9), (70, 0.5, 1.0)])
+def test_floating_forward_slots_rounds_and_partial_workgroups(gpu, nb, shrink, alpha0):
+    """The line search across rounds of trials: prev_cost set per trajectory so that the
+    accepted trial falls anywhere in 1..6 or the search exhausts at max_trials = 6 —
+    trials > 1 come from their lanes' slots, an exhausted search returns the inputs;
+    every trajectory as the closure oracle's forward_pass. B = 17 runs 16 lanes a
+    trajectory (17 · 16 lanes: the last workgroup partly empty), B = 4 runs 64 (one round
+    covers every trial) with a non-dyadic shrink (trial j's α = α₀ multiplied by shrink
+    j − 1 times, as the reference's `α *= shrink`), B = 70 runs 4 (trials 5-6 in a second
+    round)."""
     from oracle import cref
-    nb, T, mt = 17, 30, 6
+    T, mt = 30, 6
     x, u = script_batch(nb, T, seed=29)
     u = u + 0.5 * np.random.default_rng(31).standard_normal(u.shape)
     fj, lj, lfj = rbd_floating_arm(jet_ns())
@@ -212,19 +216,23 @@ def test_floating_forward_slots_rounds_and_partial_workgroups(gpu):
         x[:, t + 1] = fj(x[:, t], u[:, t])
     tl = CF.derivative_tiles(x, u, fj, *rbd_cost_quads())
     d, K, _ = cref.tiles_backward(tl, mu=0.01, symmetrize=True)
-    d = 32.0 * d  # trial j's step is 2^(6−j)·δu: the cost falls over trials 1..6
+    d = 32.0 * d  # large early steps: the cost falls over the first trials
     zt = np.zeros_like(x)
-    # the cost of trial j alone (α = 0.5^(j−1)), j = 1..8
+    alphas = [alpha0]
+    for _ in range(7):
+        alphas.append(alphas[-1] * shrink)
+    # the cost of trial j alone, j = 1..8
     c = np.stack([CF.forward_pass(x, u, zt, d, K, np.full(nb, np.inf), fj, lj, lfj, max_trials=1,
-                                  alpha0=0.5 ** (j - 1))[2] for j in range(1, 9)], axis=1)
+                                  alpha0=a)[2] for a in alphas], axis=1)
     prev = np.full(nb, np.inf)
     for b in range(nb):
         k = 1 + b % 7  # aim at trial k: prev just under the smallest cost of trials 1..k−1
         if k > 1:       # (a tie would be decided by rounding: GPU and oracle differ at 1e-12)
             prev[b] = c[b, :k - 1].min() * (1.0 - 1e-9)
-    xo, uo, co, tro, ok = CF.forward_pass(x, u, zt, d, K, prev, fj, lj, lfj, max_trials=mt)
-    assert set(tro[ok].tolist()) >= {1, 2, 3} and (~ok).any() and (tro[ok] > 4).any()
-    o = _lib.default_options(max_trials=mt)
+    xo, uo, co, tro, ok = CF.forward_pass(x, u, zt, d, K, prev, fj, lj, lfj, max_trials=mt, alpha0=alpha0,
+                                          shrink=shrink)
+    assert len(set(tro[ok].tolist())) >= 3 and ((~ok).any() or nb <= 4)
+    o = _lib.default_options(max_trials=mt, alpha0=alpha0, shrink=shrink)
     s = FloatingSolver(rbd_example_problem(), T, nb)
     try:
         xn, un, cost, trials, st = s.forward(*(torch.from_numpy(a).cuda() for a in (x, u, d, K, prev)),
