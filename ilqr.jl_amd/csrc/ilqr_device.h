@@ -106,6 +106,18 @@ __device__ __forceinline__ double ldz(bool ok, const double* p, const double* sa
   return ok ? v : 0.0;
 }
 
+// ldz for loads that must stay in flight (a prefetch): the address is opaque to the
+// optimiser, which otherwise may turn the select back into an exec-masked load in a
+// branch whose join waits (vmcnt) for every load in flight — the tiles kernels' whole
+// prefetch, at the top of each step
+__device__ __forceinline__ double ldz_async(bool ok, const double* p, const double* safe) {
+  const double* a = ok ? p : safe;
+  asm volatile("" : "+v"(a));
+  typedef __attribute__((address_space(1))) const double gdouble;  // a global load, not flat
+  const double v = *(gdouble*)a;
+  return ok ? v : 0.0;
+}
+
 // (H + μI) = L D Lᵀ (no pivoting; H symmetric, lower triangle read) and a solve
 // with a d4 right-hand side; NU ≤ 4, entries ≥ NU unused.
 template <int NU, int NEWTON = 2>

@@ -71,20 +71,20 @@ __device__ bool tiles_backward_wave(const TileParams& P, int b, int T, double* _
       const int i = 4 * kk + q;
       const bool ri = i < NX;
       const int ii = ri ? i : 0;
-      s.fB[kk] = ldz(ri && cx, A + ii * NX + ci, A) + ldz(ri && cu, Bm + ii * NU + cj, Bm);
+      s.fB[kk] = ldz_async(ri & cx, A + ii * NX + ci, A) + ldz_async(ri & cu, Bm + ii * NU + cj, Bm);
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int i = q + 4 * r;
       const bool rx = i < NX, ru = i >= NX && i < NX + NU;
       const int ix = rx ? i : 0, iu = ru ? i - NX : 0;
-      const double xx = ldz(rx && cx, lxx + ix * NX + ci, lxx);
-      const double xu = ldz(rx && cu, lux + cj * NX + ix, lux);  // L[i][NX+j] = 𝐏[j][i]
-      const double ux = ldz(ru && cx, lux + iu * NX + ci, lux);  // L[NX+j][c] = 𝐏[j][c]
-      const double uu = ldz(ru && cu, luu + iu * NU + cj, luu);
+      const double xx = ldz_async(rx & cx, lxx + ix * NX + ci, lxx);
+      const double xu = ldz_async(rx & cu, lux + cj * NX + ix, lux);  // L[i][NX+j] = 𝐏[j][i]
+      const double ux = ldz_async(ru & cx, lux + iu * NX + ci, lux);  // L[NX+j][c] = 𝐏[j][c]
+      const double uu = ldz_async(ru & cu, luu + iu * NU + cj, luu);
       s.Lc[r] = xx + wux * (xu + ux) + uu;
     }
-    s.lv = ldz(cx, lx0 + (size_t)t * NX + ci, lx0) + ldz(cu, lu0 + (size_t)t * NU + cj, lu0);
+    s.lv = ldz_async(cx, lx0 + (size_t)t * NX + ci, lx0) + ldz_async(cu, lu0 + (size_t)t * NU + cj, lu0);
   };
 
   double* Gl = lds;
@@ -110,7 +110,7 @@ __device__ bool tiles_backward_wave(const TileParams& P, int b, int T, double* _
       const int i = q + 4 * r;
       const bool rx = i < NX;
       const int ix = rx ? i : 0;
-      Sp[r] = ldz(rx && cx, lfxx + ix * NX + ci, lfxx) + ldz(rx && c == SROW, lfx + ix, lfx);
+      Sp[r] = ldz_async(rx & cx, lfxx + ix * NX + ci, lfxx) + ldz_async(rx & (c == SROW), lfx + ix, lfx);
     }
   }
 
@@ -277,22 +277,20 @@ __device__ bool tiles_backward_wide_wave(const TileParams& P, int b, int T, int 
     for (int kk = 0; kk < 4; ++kk) {
       const int i = 4 * kk + q;
       const bool ri = i < nx;
-      s.fA[kk] = ldz(ri && cx, A + i * nx + c, A);
-      s.fB[kk] = ldz(ri && cu, Bm + i * nu + c, Bm);
-      s.Lxx[kk] = ldz(ri && cx, lxx + i * nx + c, lxx);
-      s.Lxe[kk] = ldz(ri && c8, lx + i, lx);
+      s.fA[kk] = ldz_async(ri & cx, A + i * nx + c, A);
+      s.fB[kk] = ldz_async(ri & cu, Bm + i * nu + c, Bm);
+      s.Lxx[kk] = ldz_async(ri & cx, lxx + i * nx + c, lxx);
+      s.Lxe[kk] = ldz_async(ri & c8, lx + i, lx);
     }
 #pragma unroll
     for (int r = 0; r < 2; ++r) {
       const int i = q + 4 * r;
       const bool ru = i < nu;
-      if (lux0) {
-        const double* lux = lux0 + (size_t)t * sxu;
-        s.Lux[r] = ldz(ru && cx, lux + i * nx + c, lux);
-      } else {
-        s.Lux[r] = 0.0;
-      }
-      s.Lue[r] = ldz(ru && cu, luu + i * nu + c, luu) + ldz(ru && c8, lu + i, lu);
+      // unconditional (ldz): a load in a branch on lux0 waits for every load in flight at
+      // its join — the whole prefetch, at the top of each step
+      const double* lux = lux0 ? lux0 + (size_t)t * sxu : A;
+      s.Lux[r] = ldz_async((lux0 != nullptr) & ru & cx, lux + i * nx + c, A);
+      s.Lue[r] = ldz_async(ru & cu, luu + i * nu + c, luu) + ldz_async(ru & c8, lu + i, lu);
     }
     s.Lux[2] = s.Lux[3] = s.Lue[2] = s.Lue[3] = 0.0;
   };
@@ -309,8 +307,8 @@ __device__ bool tiles_backward_wide_wave(const TileParams& P, int b, int T, int 
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int i = q + 4 * r;
-      S[r] = ldz(i < nx && cx, lfxx + i * nx + c, lfxx);
-      Sx[r] = ldz(i < nx && c8, lfx + i, lfx);
+      S[r] = ldz_async((i < nx) & cx, lfxx + i * nx + c, lfxx);
+      Sx[r] = ldz_async((i < nx) & c8, lfx + i, lfx);
     }
   }
 
