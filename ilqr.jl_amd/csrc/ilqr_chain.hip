@@ -2247,7 +2247,11 @@ struct ChainOps {
         if (!ilqr::fg_fits<V>(h->T)) return hipErrorInvalidValue;
         const auto Q = trig_consts<V>(h);
         const int B = h->batch;
-        if (ilqr::fg_lanes(B) == 4)
+        const int L = ilqr::fg_lanes(B, pc == nullptr);
+        if (L == 32)
+          ilqr::chain_forward_trig_kernel<V, NU, 32, 1><<<(32 * B + 63) / 64, 64, 0, h->stream>>>(
+              Q, B, h->T, x, u, xt, d, K, pc, xn, un, nc, tr, st, ls);
+        else if (L == 4)
           ilqr::chain_forward_trig_kernel<V, NU, 4, 1><<<(4 * B + 63) / 64, 64, 0, h->stream>>>(
               Q, B, h->T, x, u, xt, d, K, pc, xn, un, nc, tr, st, ls);
         else
@@ -2281,7 +2285,10 @@ struct ChainOps {
         if (!ilqr::fg_fits<V>(h->T)) return hipErrorInvalidValue;
         const auto Q = trig_consts<V>(h);
         const int B = h->batch;
-        if (ilqr::fg_lanes(B) == 4)
+        const int L = ilqr::fg_lanes(B, a.prev_cost == nullptr || a.iter == 1);  // fit's first: +Inf
+        if (L == 32)
+          ilqr::chain_iter_forward_trig_kernel<V, NU, 32, 1><<<(32 * B + 63) / 64, 64, 0, h->stream>>>(Q, B, h->T, a, ls);
+        else if (L == 4)
           ilqr::chain_iter_forward_trig_kernel<V, NU, 4, 1><<<(4 * B + 63) / 64, 64, 0, h->stream>>>(Q, B, h->T, a, ls);
         else
           ilqr::chain_iter_forward_trig_kernel<V, NU, 1, 4><<<(B + 255) / 256, 256, 0, h->stream>>>(Q, B, h->T, a, ls);

@@ -25,6 +25,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "ilqr_device.h"
 #include "ilqr_internal.h"
 
@@ -217,7 +219,8 @@ __device__ FgOut<typename Model::V> fwd_group(const Model& m, int b, int B, int 
     if (rerun) break;  // the accepted candidate's rollout, now stored
     const int k = r * L + sub;  // 0-based trial index of this lane's candidate
     const bool acc = k < ls.max_trials && prev_cost - cost > V(0);  // NaN compares false
-    const unsigned am = (unsigned)(__ballot(acc) >> gbase) & ((1u << L) - 1u);
+    constexpr uint64_t gmask = L >= 64 ? ~0ull : (1ull << L) - 1;
+    const unsigned am = (unsigned)((__ballot(acc) >> gbase) & gmask);
     if (am) {
       const int first = __builtin_ctz(am);
       if (sub != first) break;
@@ -252,9 +255,23 @@ __device__ FgOut<typename Model::V> fwd_group(const Model& m, int b, int B, int 
   return out;
 }
 
-// L = 4 line-search candidates per trajectory up to B = 65536, one lane per trajectory
-// past it (the candidates' extra waves are free at these batches)
-inline int fg_lanes(int B) { return B <= 65536 ? 4 : 1; }
+// line-search candidates per trajectory: 4 up to B = 65536, one lane per trajectory past
+// it (the candidates' extra waves are free at these batches); and
+// when the search may be long (prev_cost given, past a fit's first iteration) 32 up to
+// B = 2048 — the lanes one wave per SIMD holds: a search capped at 64 trials then takes 2
+// rounds, not 16. A cold search (prev_cost = +Inf: trial 1 accepts) keeps 4: 32 lanes a
+// trajectory cost the one-round iteration 7-30 % (the whole chip's lanes busy).
+// ILQR_FG_LANES = 1/4/32 forces a width (measurement).
+inline int fg_lanes(int B, bool cold = true) {
+  static const int forced = [] {
+    const char* e = std::getenv("ILQR_FG_LANES");
+    const int v = e ? std::atoi(e) : 0;
+    return v == 1 || v == 4 || v == 32 ? v : 0;
+  }();
+  if (forced) return forced;
+  if (!cold && B <= 2048) return 32;
+  return B <= 65536 ? 4 : 1;
+}
 
 }  // namespace
 }  // namespace ilqr
