@@ -2247,7 +2247,7 @@ struct ChainOps {
         if (!ilqr::fg_fits<V>(h->T)) return hipErrorInvalidValue;
         const auto Q = trig_consts<V>(h);
         const int B = h->batch;
-        const int L = ilqr::fg_lanes(B, pc == nullptr);
+        const int L = ilqr::fg_lanes(B);
         if (L == 32)
           ilqr::chain_forward_trig_kernel<V, NU, 32, 1><<<(32 * B + 63) / 64, 64, 0, h->stream>>>(
               Q, B, h->T, x, u, xt, d, K, pc, xn, un, nc, tr, st, ls);
@@ -2285,7 +2285,7 @@ struct ChainOps {
         if (!ilqr::fg_fits<V>(h->T)) return hipErrorInvalidValue;
         const auto Q = trig_consts<V>(h);
         const int B = h->batch;
-        const int L = ilqr::fg_lanes(B, a.prev_cost == nullptr || a.iter == 1);  // fit's first: +Inf
+        const int L = ilqr::fg_lanes(B, a.iter >= 2);  // a fit past its first iteration
         if (L == 32)
           ilqr::chain_iter_forward_trig_kernel<V, NU, 32, 1><<<(32 * B + 63) / 64, 64, 0, h->stream>>>(Q, B, h->T, a, ls);
         else if (L == 4)

@@ -257,12 +257,14 @@ __device__ FgOut<typename Model::V> fwd_group(const Model& m, int b, int B, int 
 
 // line-search candidates per trajectory: 4 up to B = 65536, one lane per trajectory past
 // it (the candidates' extra waves are free at these batches); and
-// when the search may be long (prev_cost given, past a fit's first iteration) 32 up to
-// B = 2048 — the lanes one wave per SIMD holds: a search capped at 64 trials then takes 2
-// rounds, not 16. A cold search (prev_cost = +Inf: trial 1 accepts) keeps 4: 32 lanes a
-// trajectory cost the one-round iteration 7-30 % (the whole chip's lanes busy).
+// in a fit past its first iteration (`wide`: prev_cost is finite, the search may be long)
+// 32 up to B = 2048 — the lanes one wave per SIMD holds: a search capped at 64 trials then
+// takes 2 rounds, not 16. Elsewhere 4: a search that accepts in its first round costs 7-30 %
+// more on 32 lanes a trajectory (the whole chip's lanes busy), and a standalone forward
+// cannot tell its prev_cost from +Inf without reading it back.
 // ILQR_FG_LANES = 1/4/32 forces a width (measurement).
-inline int fg_lanes(int B, bool cold = true) {
+inline int fg_lanes(int B, bool wide = false) {
+  const bool cold = !wide;
   static const int forced = [] {
     const char* e = std::getenv("ILQR_FG_LANES");
     const int v = e ? std::atoi(e) : 0;

@@ -683,7 +683,7 @@ __global__ __launch_bounds__(64 * TL_BW4_WAVES) void tl_backward_kernel(TwoLinkP
 // latency (236 vs 275 µs; profiles/r02/tl_fw_probe.log). W waves per workgroup: 1 for
 // the candidate grids (four 1-lane waves on one CU at B = 1024 ran 27.6 → 54.7 µs), 4
 // past B = 65536 (1-wave workgroups past 256 waves were packed two to a SIMD).
-inline int tl_fw_lanes(int B, bool cold = true) { return fg_lanes(B, cold); }
+inline int tl_fw_lanes(int B, bool wide = false) { return fg_lanes(B, wide); }
 
 template <int NU, int L, int W>
 __global__ __launch_bounds__(64 * W) void tl_forward_kernel(
@@ -807,7 +807,7 @@ hipError_t tl_forward_nu(const TwoLinkParams& P, int B, int T, const double* x, 
                          const double* prev_cost, double* xnew, double* unew, double* new_cost,
                          int32_t* trials, int32_t* status, const LSParams& ls, hipStream_t s) {
   if (!tl_fw_fits(T)) return hipErrorInvalidValue;
-  const int L = tl_fw_lanes(B, prev_cost == nullptr);
+  const int L = tl_fw_lanes(B);
   if (L == 32)
     tl_forward_kernel<NU, 32, 1><<<(32 * B + 63) / 64, 64, 0, s>>>(
         P, B, T, x, u, xtraj, d, K, prev_cost, xnew, unew, new_cost, trials, status, ls);
@@ -830,7 +830,7 @@ hipError_t tl_iteration_nu(const TwoLinkParams& P, int B, int T, const IterArgs&
   const int per_wg = 4 * TL_BW4_WAVES;
   tl_iter_backward_kernel<NU><<<(B + per_wg - 1) / per_wg, 64 * TL_BW4_WAVES, 0, s>>>(P, B, T, a, J, ls.mu);
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  const int L = tl_fw_lanes(B, a.prev_cost == nullptr || a.iter == 1);  // fit's first: +Inf
+  const int L = tl_fw_lanes(B, a.iter >= 2);  // a fit past its first iteration
   if (L == 32)
     tl_iter_forward_kernel<NU, 32, 1><<<(32 * B + 63) / 64, 64, 0, s>>>(P, B, T, a, ls);
   else if (L == 4)
