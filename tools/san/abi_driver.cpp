@@ -287,6 +287,7 @@ static void gpu_paths(int ndev) {
 }
 
 int main() {
+  setvbuf(stdout, nullptr, _IONBF, 0);  // every line out before a crash at exit
   no_gpu_paths();
   int n = 0;
   if (hipGetDeviceCount(&n) == 0 && n > 0) gpu_paths(n);
