@@ -8,7 +8,7 @@ wraps RigidBodyDynamics.jl's mass_matrix / dynamics_bias in an RK4 `dynamicsf`
 `iLQR.fit` on 16-state / 8-input trajectories of T = 1000 steps
 (animate_RBD_2_link.jl:8-32). `FloatingSolver.fit` runs that fit natively:
 forward-mode-dual linearisation, the wide tiles Riccati kernel and a line search of
-four trials per trajectory at once, against the generic closure path's 0.76 s per
+4-64 trials per trajectory at once (each RK4 step split over three waves), against the generic closure path's 0.76 s per
 line-search trial (tests/test_gpu_floating.py compares both with the batched closure
 oracle).
 
