@@ -83,7 +83,14 @@ def test_tiles_kernels_have_no_scratch(tmp_path):
     256 VGPRs + AGPRs at one wave per SIMD) and every narrow instantiation keep their
     prefetched tiles, LDLᵀ factors and dynamically selected solution entries in
     registers — a dynamically indexed register array (the first draft's g vector) or a
-    spill would be a scratch access per step."""
+    spill would be a scratch access per step.
+
+    And the step-ahead tile loads stay in flight across the step: inside the step loop,
+    no `s_waitcnt vmcnt` may sit between the loop header and the last prefetch load.
+    Before the opaque load-or-zero (`ldz_async`, DESIGN "The prefetch that waited") the
+    wide kernel's loads were exec-masked branches, each joined by a `vmcnt(0)`, so every
+    step waited for its successor's tiles before its first MFMA — 2.06 ms instead of
+    1.10 ms for 16 × 8 at B = 4096 (`profiles/r05/tiles_bench_async_r05.log`)."""
     hipcc = HIPCC if os.path.exists(HIPCC) else shutil.which("hipcc")
     cmd = [hipcc, "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-mllvm", "-amdgpu-mfma-vgpr-form=1",
            "-save-temps", "-c", os.path.join(CSRC, "ilqr_tiles.hip"), "-o", str(tmp_path / "tiles.o")]
@@ -94,7 +101,15 @@ def test_tiles_kernels_have_no_scratch(tmp_path):
     kernels = [n for n in funcs if "tiles_backward" in n and "kernel" in n]
     assert any("wide" in n for n in kernels) and len(kernels) >= 49, len(kernels)
     for n in kernels:
-        assert not [x for x in funcs[n] if x.startswith("scratch_")], f"{n}: scratch accesses"
+        body = funcs[n]
+        assert not [x for x in body if x.startswith("scratch_")], f"{n}: scratch accesses"
+        headers = [i for i, x in enumerate(body) if "Loop Header" in x]
+        assert len(headers) == 1, f"{n}: step loop headers at {headers}"
+        h = headers[0]
+        loads = [i for i, x in enumerate(body) if i > h and x.startswith("global_load")]
+        assert loads, f"{n}: no prefetch loads in the step loop"
+        waits = [body[i] for i in range(h, loads[-1]) if "vmcnt" in body[i]]
+        assert not waits, f"{n}: the step waits on its prefetch before issuing it all: {waits[:4]}"
 
 
 @pytest.mark.skipif(not os.path.exists(HIPCC) and shutil.which("hipcc") is None, reason="no hipcc")
