@@ -1,6 +1,9 @@
 # A/B of the sincos fallback's calling convention on config 5's kernels and the 2-link
 # bench: libilqr_hip_prevchain.so (out-pointers into the caller's s, c), _byval.so
-# (returned by value), _tmp.so (out-pointers into slow-path temporaries)
+# (returned by value), _tmp.so (out-pointers into slow-path temporaries). The three
+# libraries are built on the CPU before the call (ilqr_math.h edited per variant, `make -C
+# ilqr.jl_amd/csrc ../lib/libilqr_hip.so`, copied into lib/variants/) and not kept.
+# Result: profiles/r05/sincos_fallback_ab_r05.log.
 cd "${GRAFT_REPO_ROOT}"
 mkdir -p gpurun_out && export TMPDIR=/tmp
 for i in 1 2; do
