@@ -43,6 +43,7 @@ import argparse
 import ctypes as C
 import json
 import os
+import re
 import sys
 import time
 
@@ -79,32 +80,49 @@ def algorithmic_counts(T, nx=NX, nu=NU):
                 fw_flops=fw_flops_step * T)
 
 
-def load_pmc_traffic(profiles_dir):
-    """HBM bytes per backward launch from committed rocprofv3 PMC passes
-    (profiles/pmc_*.json, written by profiles/collect_pmc.py), or None."""
+_HEADLINE_RECORD = re.compile(r"^(pmc|mfma)_r(\d+)\.json$")
+
+
+def _latest_headline_record(profiles_dir, prefix):
+    """The newest HEADLINE record `profiles/<prefix>_rNN.json` (highest round NN), by
+    name: records of other benchmarks (`pmc_tiles_r05.json`, variants like
+    `pmc_r01_v6.json`) never match. → (path, record) or (None, None)."""
     best = None
     if os.path.isdir(profiles_dir):
-        for f in sorted(os.listdir(profiles_dir)):
-            if f.startswith("pmc_") and f.endswith(".json"):
-                try:
-                    best = json.load(open(os.path.join(profiles_dir, f)))
-                except Exception:
-                    pass
-    return best
+        for f in os.listdir(profiles_dir):
+            m = _HEADLINE_RECORD.match(f)
+            if m and m.group(1) == prefix and (best is None or int(m.group(2)) > best[0]):
+                best = (int(m.group(2)), f)
+    if best is None:
+        return None, None
+    path = os.path.join(profiles_dir, best[1])
+    with open(path) as fh:
+        return path, json.load(fh)   # a malformed committed record fails loudly
+
+
+def load_pmc_traffic(profiles_dir, batch=4096, T=100):
+    """HBM bytes per launch of the headline kernels from the newest committed
+    rocprofv3 PMC record of bench.py (profiles/pmc_rNN.json, written by
+    profiles/collect_pmc.py). → (record, source) where record is None when the
+    record was taken at another batch / horizon than this run's (source says why).
+    A headline record missing its batch, T or per-launch byte fields raises."""
+    path, rec = _latest_headline_record(profiles_dir, "pmc")
+    if rec is None:
+        return None, "no profiles/pmc_rNN.json"
+    missing = [k for k in ("batch", "T", "hbm_bytes_per_backward_launch", "hbm_bytes_per_fused_launch")
+               if k not in rec]
+    if missing:
+        raise ValueError(f"{path}: headline PMC record lacks {missing}")
+    src = os.path.relpath(path, os.path.dirname(profiles_dir))
+    if rec["batch"] != batch or rec["T"] != T:
+        return None, f"{src} was taken at batch={rec['batch']} T={rec['T']}, this run is batch={batch} T={T}"
+    return rec, src
 
 
 def load_mfma_pmc(profiles_dir):
-    """MFMA utilisation per kernel from the committed rocprofv3 pass
-    (profiles/mfma_*.json, written by profiles/collect_mfma.py), or None."""
-    best = None
-    if os.path.isdir(profiles_dir):
-        for f in sorted(os.listdir(profiles_dir)):
-            if f.startswith("mfma_") and f.endswith(".json"):
-                try:
-                    best = json.load(open(os.path.join(profiles_dir, f)))
-                except Exception:
-                    pass
-    return best
+    """MFMA utilisation per kernel from the newest committed rocprofv3 pass of bench.py
+    (profiles/mfma_rNN.json, written by profiles/collect_mfma.py), or None."""
+    return _latest_headline_record(profiles_dir, "mfma")[1]
 
 
 def mfma_summary(m, key):
@@ -607,10 +625,9 @@ def main():
     fw_bytes = cnt["fw_bytes"] * B
     it_bytes = (cnt["bw_bytes"] + cnt["fw_bytes"]) * B
     it_flops = (cnt["bw_flops"] + cnt["fw_flops"]) * B
-    pmc = load_pmc_traffic(os.path.join(ROOT, "profiles"))
-    traffic = None
-    if pmc and pmc.get("batch") == B and pmc.get("T") == T:
-        traffic = pmc.get("hbm_bytes_per_backward_launch")
+    pmc, pmc_src = load_pmc_traffic(os.path.join(ROOT, "profiles"), B, T)
+    traffic = pmc["hbm_bytes_per_backward_launch"] if pmc else None
+    fused_traffic = pmc["hbm_bytes_per_fused_launch"] if pmc else None
     mf = load_mfma_pmc(os.path.join(ROOT, "profiles"))
     achieved_tf = bw_flops / (bw_ms * 1e-3) / 1e12
     # serial ceiling of the backward-then-forward schedule: backward at the FP64 spec
@@ -645,8 +662,7 @@ def main():
                                                 "4 trajectories per wave, v_mfma_f64_4x4x4_4b + DPP ring forward)",
                      "achieved": it_flops / (fused_ms * 1e-3) / 1e12, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": it_flops / (fused_ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS,
-                     "traffic": (pmc or {}).get("hbm_bytes_per_fused_launch") if pmc and pmc.get("batch") == B
-                     and pmc.get("T") == T else None,
+                     "traffic": fused_traffic, "traffic_source": pmc_src,
                      "avg_launch_ms": fused_ms, "chains_all_ok": fused_ok,
                      "algorithmic_flops_per_launch": it_flops, "algorithmic_bytes_per_launch": it_bytes,
                      "hbm_achieved_gbps": it_bytes / (fused_ms * 1e-3) / 1e9,
@@ -658,6 +674,7 @@ def main():
         "backward_leg": {"bound": "mfma", "kernel": "lq_iter_backward4 (backward_pass alone, 4 trajectories per wave)",
                          "achieved": achieved_tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": achieved_tf / FP64_PEAK_TFLOPS, "traffic": traffic,
+                         "traffic_source": pmc_src,
                          "avg_launch_ms": bw_ms, "algorithmic_flops_per_launch": bw_flops,
                          "algorithmic_bytes_per_launch": bw_bytes,
                          "hbm_achieved_gbps": bw_bytes / (bw_ms * 1e-3) / 1e9,
@@ -698,7 +715,7 @@ def main():
                              "achieved_gbps": it_bytes / (single_ms * 1e-3) / 1e9,
                              "frac_hbm_peak": it_bytes / (single_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
                              "algorithmic_bytes_per_launch": it_bytes,
-                             "traffic": (pmc or {}).get("hbm_bytes_per_fused_launch"),
+                             "traffic": fused_traffic,
                              "mfma_pmc": mfma_summary(mf, "fused")},
         "co_headline": {"metric": "batched iLQR iterations/sec (fwd+bwd pass), nx=12 nu=4 T=100, 1/2/4/8 MI355X",
                         "value": agg["co_headline"], "unit": "batched iterations/s",
