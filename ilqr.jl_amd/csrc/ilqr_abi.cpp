@@ -317,8 +317,9 @@ ilqr_status unpad_u(ilqr_handle* h, const double* pu, double* u) {
 
 // The end of a fit: the stream's last kernel stores this fit's number into a wait word
 // (ilqr::wait_host_seq below).
-hipError_t wait_fit(ilqr_handle* h, uint32_t seq, hipStream_t s) {
-  return ilqr::wait_host_seq(h->host_running + 2, seq, s, &h->host_wait);
+// `units`: the fit iterations enqueued since the host last waited on this fit.
+hipError_t wait_fit(ilqr_handle* h, uint32_t seq, int units, hipStream_t s) {
+  return ilqr::wait_host_seq(h->host_running + 2, seq, units, s, &h->host_wait);
 }
 
 }  // namespace
@@ -326,56 +327,23 @@ hipError_t wait_fit(ilqr_handle* h, uint32_t seq, hipStream_t s) {
 // The stream's last kernel of a fit (gather_flags_kernel) stores the fit's number into
 // the host-mapped call-status word as it runs, after every earlier kernel of the stream
 // completed (in-order stream): when the word carries the number, the outputs are written.
-// The host spins on that word and returns — the runtime's blocking stream sync costs
-// ≈8 µs more per fit after the work is done (A/B in bench.py, 455 → 447 µs per 3-iteration
-// headline fit, profiles/r04/fit_wait_ab_r04.log). The handle remembers how long its
-// previous wait took (est): a wait expected to be long naps (50 µs sleeps) until 150 µs
-// before that, then spins to 1.25 × est (50 µs at least, est + 1 ms at most), then naps
-// between stream queries until the stream is idle. A headline-size fit so spins ≈150 µs
-// of its ≈450; a long one (a config-5 default fit, 9-39 ms; every shard thread of
-// ilqr_multi) holds no core. The fit drivers' per-iteration convergence polls wait the
-// same way on their events (wait_event; the next iteration is already queued, so a nap's
-// wake-up delay idles nothing). hipEventSynchronize busy-waits on this ROCm whatever the
-// event's flags (tools/event_wait_probe.py, profiles/r05/event_wait_probe_r05.log), so
-// no runtime sync is left on these paths. ILQR_FIT_WAIT=sync in the environment forces
-// the stream sync (A/B).
-namespace {
-template <class Done, class Idle>
-hipError_t nap_spin_wait(ilqr::HostWait* hw, Done done, Idle idle) {
-  using clk = std::chrono::steady_clock;
-  const auto t0 = clk::now();
-  const int64_t est = hw->last_us;
-  auto since = [&] { return std::chrono::duration_cast<std::chrono::microseconds>(clk::now() - t0).count(); };
-  const struct timespec nap = {0, 50000};
-  if (est > 300)
-    while (!done() && since() < est - 150) nanosleep(&nap, nullptr);
-  const int64_t budget = est > 0 ? std::min<int64_t>(std::max<int64_t>(est + est / 4, 50), est + 1000) : 1000;
-  hipError_t e = hipSuccess;
-  for (uint32_t k = 0;; ++k) {
-    if (done()) break;
-    if ((k & 255u) == 255u && since() > budget) {
-      while (!done()) {  // past the estimate: nap between queries until the work is done
-        if ((e = idle()) != hipErrorNotReady) break;
-        nanosleep(&nap, nullptr);
-      }
-      if (e == hipErrorNotReady) e = hipSuccess;
-      break;
-    }
-    __builtin_ia32_pause();
-  }
-  hw->last_us = since();
-  return e;
-}
-}  // namespace
-
-hipError_t ilqr::wait_host_seq(const volatile int32_t* w, uint32_t seq, hipStream_t s, HostWait* hw) {
+// The host waits on that word by ilqr_wait.h's policy (spin around the expected end, nap
+// only through the bulk of a wait expected to exceed 1 ms, sized per iteration). A
+// headline-size fit (≈450 µs) never naps; a long one (a config-5 default fit, 2-9 ms; the
+// floating family's fits; every shard thread of ilqr_multi) holds no core. The fit
+// drivers' per-iteration convergence polls wait the same way on their events (wait_event;
+// the next iteration is already queued). hipEventSynchronize busy-waits on this ROCm
+// whatever the event's flags (profiles/r05/event_wait_probe_r05.log), so no runtime sync
+// is left on these paths. ILQR_FIT_WAIT=sync in the environment forces the stream sync (A/B).
+hipError_t ilqr::wait_host_seq(const volatile int32_t* w, uint32_t seq, int units, hipStream_t s,
+                               HostWait* hw) {
   static const bool spin = [] {
     const char* e = getenv("ILQR_FIT_WAIT");
     return !(e && strcmp(e, "sync") == 0);
   }();
   if (!spin) return hipStreamSynchronize(s);
   auto done = [&] { return ((uint32_t)__atomic_load_n(w, __ATOMIC_ACQUIRE) >> 2) == seq; };
-  hipError_t e = nap_spin_wait(hw, done, [&] {
+  hipError_t e = nap_spin_wait(hw, units, hipSuccess, hipErrorNotReady, done, [&] {
     const hipError_t q = hipStreamQuery(s);  // idle, busy (NotReady) or an execution error
     return q == hipSuccess && !done() ? hipErrorLaunchFailure : q;  // idle without the word: lost
   });
@@ -385,7 +353,7 @@ hipError_t ilqr::wait_host_seq(const volatile int32_t* w, uint32_t seq, hipStrea
 hipError_t ilqr::wait_event(hipEvent_t ev, HostWait* hw) {
   hipError_t q = hipErrorNotReady;
   auto done = [&] { return (q = hipEventQuery(ev)) != hipErrorNotReady; };
-  const hipError_t e = nap_spin_wait(hw, done, [&] { return q = hipEventQuery(ev); });
+  const hipError_t e = nap_spin_wait(hw, 1, hipSuccess, hipErrorNotReady, done, [&] { return q = hipEventQuery(ev); });
   return e != hipSuccess ? e : q;
 }
 
@@ -845,10 +813,12 @@ ilqr_status ilqr_fit_ex(ilqr_handle* h, const ilqr_problem* p, const ilqr_option
   // reads iteration it−1's count while the GPU runs iteration it (no idle gap; at most
   // one iteration of already-stopped waves is enqueued past the last useful one).
   const bool poll = o->tol >= 0.0 && o->max_iter > 2;
+  int enqueued = pipe ? o->max_iter : 0, waited = 0;  // iterations (the end-of-fit wait's units)
   for (int it = 1; !pipe && it <= o->max_iter; ++it) {  // forward_pass.jl:161
     // iterations chain per chunk: chunk 0's next backward overlaps chunk 1's forward
     const ilqr_status st = enqueue_iteration(h, p, iter_args(it), ls, /*chain=*/true, hist);
     if (st != ILQR_OK) return st;
+    enqueued = it;
     // the history record and the count run behind every chunk's forward without
     // joining the main stream (a join would keep chunk 0's next backward from
     // overlapping chunk 1's forward): the forwards of all chunks are in order on the
@@ -864,6 +834,7 @@ ilqr_status ilqr_fit_ex(ilqr_handle* h, const ilqr_problem* p, const ilqr_option
     HIP_TRY(hipEventRecord(h->ev_poll[it & 1], ps));
     if (it >= 2) {
       HIP_TRY(ilqr::wait_event(h->ev_poll[(it - 1) & 1], &h->poll_wait));
+      waited = it - 1;
       if (__atomic_load_n(h->host_running + ((it - 1) & 1), __ATOMIC_ACQUIRE) == 0) break;
     }
   }
@@ -880,7 +851,7 @@ ilqr_status ilqr_fit_ex(ilqr_handle* h, const ilqr_problem* p, const ilqr_option
                                      h->ubuf[0], h->xbuf[1], h->ubuf[1], h->res_parity, h->status,
                                      last, h->prev_cost, h->iters, x_out, u_out, cost, iters,
                                      status, h->dev_flags, h->dev_running + 2, s, seq));
-  HIP_TRY(wait_fit(h, seq, s));
+  HIP_TRY(wait_fit(h, seq, enqueued - waited, s));
   const int32_t f = __atomic_load_n(h->host_running + 2, __ATOMIC_ACQUIRE);
   return (f & 1) ? ILQR_ERR_NAN : ((f & 2) ? ILQR_ERR_LS_EXHAUSTED : ILQR_OK);
 }

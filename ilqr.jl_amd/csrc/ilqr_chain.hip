@@ -2395,6 +2395,7 @@ ilqr_status chain_fit_t(ilqr_chain_handle* h, const ilqr_options* o, const void*
                       !overlap(x_out, xb, u_init, ub) && !overlap(u_out, ub, u_init, ub) &&
                       !overlap(u_out, ub, x_init, xb) && !overlap(u_out, ub, x_traj, xb);
   const bool poll = ls.tol >= 0.0 && max_iter > 2;
+  int enqueued = 0, waited = 0;  // iterations (the end-of-fit wait's units)
   for (int it = 1; it <= max_iter; ++it) {  // forward_pass.jl:161
     const int par = (it - 1) & 1;
     const bool last = direct && it == max_iter;
@@ -2406,6 +2407,7 @@ ilqr_status chain_fit_t(ilqr_chain_handle* h, const ilqr_options* o, const void*
     a.parity = it == 1 ? ilqr::PARITY_INPUT : par;  // where the input x̄ⁱ, ūⁱ lie (:174-175)
     a.iter = it;
     CH_TRY(dispatch<V>(h, [&](auto ops) { return decltype(ops)::iteration(h, a, ls); }));
+    enqueued = it;
     if (hist)  // the per-iteration record (ilqr_history)
       CH_TRY(ilqr::launch_record_history(h->batch, it, h->status, h->iters, h->trials, h->prev_cost, h->du2,
                                          sizeof(V) == 4, ls.alpha0, ls.shrink, hist->cost, hist->trials,
@@ -2415,6 +2417,7 @@ ilqr_status chain_fit_t(ilqr_chain_handle* h, const ilqr_options* o, const void*
     CH_TRY(hipEventRecord(h->ev_poll[it & 1], s));
     if (it >= 2) {  // iteration it−1's count, read while iteration it runs (:171's break)
       CH_TRY(ilqr::wait_event(h->ev_poll[(it - 1) & 1], &h->poll_wait));
+      waited = it - 1;
       if (__atomic_load_n(h->host_words + ((it - 1) & 1), __ATOMIC_ACQUIRE) == 0) break;
     }
   }
@@ -2429,7 +2432,7 @@ ilqr_status chain_fit_t(ilqr_chain_handle* h, const ilqr_options* o, const void*
   uint32_t seq = (++h->fit_seq) & 0x3fffffffu;
   if (seq == 0) seq = h->fit_seq = 1;  // 0 is the word's cleared value
   CH_TRY(ilqr::launch_publish_flags(h->dev_flags, h->dev_words + 2, seq, s));
-  CH_TRY(ilqr::wait_host_seq(h->host_words + 2, seq, s, &h->host_wait));
+  CH_TRY(ilqr::wait_host_seq(h->host_words + 2, seq, enqueued - waited, s, &h->host_wait));
   const int32_t f = __atomic_load_n(h->host_words + 2, __ATOMIC_ACQUIRE);
   return (f & 1) ? ILQR_ERR_NAN : ((f & 2) ? ILQR_ERR_LS_EXHAUSTED : ILQR_OK);
 }

@@ -5,6 +5,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include "ilqr_wait.h"
+
 namespace ilqr {
 
 // Per-instance LQ problem data, device pointers, row-major, trajectory slowest.
@@ -170,15 +172,11 @@ hipError_t launch_count_running(int B, const int32_t* status, int32_t* out, hipS
 // The last launch of a fit (gather_flags_kernel): dflags[0] (a gather's call-status
 // bits, re-armed) into the host-mapped word `flags` as (seq << 2) | bits.
 hipError_t launch_publish_flags(int32_t* dflags, int32_t* flags, uint32_t seq, hipStream_t s);
-// The host's end of a fit: wait until the host-mapped word carries `seq` in bits 2..31 —
-// nap through the bulk of a wait the handle's previous one says is long, spin around its
-// expected end, then nap between stream queries (ilqr_abi.cpp; ILQR_FIT_WAIT=sync forces
-// the stream sync). wait_event: the same for an event (the fit drivers' polls). One
-// HostWait per waiting site of a handle.
-struct HostWait {
-  int64_t last_us = 0;  // the previous wait's length
-};
-hipError_t wait_host_seq(const volatile int32_t* word, uint32_t seq, hipStream_t s, HostWait* hw);
+// The host's end of a fit: wait until the host-mapped word carries `seq` in bits 2..31,
+// `units` = the fit iterations the wait covers (the policy: ilqr_wait.h; ILQR_FIT_WAIT=sync
+// forces the stream sync). wait_event: the same for an event (the fit drivers' polls, one
+// iteration each). One HostWait per waiting site of a handle.
+hipError_t wait_host_seq(const volatile int32_t* word, uint32_t seq, int units, hipStream_t s, HostWait* hw);
 hipError_t wait_event(hipEvent_t ev, HostWait* hw);
 bool lq_supported(int nx, int nu);
 

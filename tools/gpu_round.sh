@@ -61,6 +61,12 @@ case $WHAT in
             step bench_wait_spin_$i 300 python bench.py --no-cpu --no-secondary
           done
           for f in gpurun_out/bench_wait_*.log; do python -c "import json,sys; d=[json.loads(l) for l in open(sys.argv[1]) if l.startswith('{')][-1]; print(sys.argv[1], round(d['value'],1), round(d['fit_timing']['median_fit_ms']*1000,1), round(d['roofline']['avg_launch_ms']*1000,1))" $f; done ;;
+  waitab20) for i in 1 2 3; do
+              ILQR_FIT_WAIT=sync step bench20_sync_$i 300 python bench.py --steps 20 --no-cpu --no-secondary
+              step bench20_spin_$i 300 python bench.py --steps 20 --no-cpu --no-secondary
+            done
+            step bench100_spin 300 python bench.py --steps 100 --no-cpu --no-secondary
+            for f in gpurun_out/bench20_*.log gpurun_out/bench100_spin.log; do python -c "import json,sys; d=[json.loads(l) for l in open(sys.argv[1]) if l.startswith('{')][-1]; print(sys.argv[1], round(d['value'],1), 'ms_per_step', round(d['ms_per_step']*1000,2), 'event_us', round(d['iteration']['event_ms']*1000,2), 'traffic', d['roofline']['traffic'])" $f; done > gpurun_out/wait20_ab.log; cat gpurun_out/wait20_ab.log ;;
   gatherab) for i in 1 2 3; do for wg in 0 1 4 16; do
               ILQR_GATHER_WG=$wg step ab_fit_wg${wg}_$i 120 python tools/ab_fit.py
             done; done
