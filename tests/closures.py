@@ -345,3 +345,78 @@ def floating_energy(x, model=None):
     M = f.mass_matrix(np.asarray(x, float))
     v = np.asarray(x, float)[:, 8:16]
     return 0.5 * np.einsum("pi,pij,pj->p", v, M, v)
+
+
+# -- an independent formulation of the floating mechanism ----------
+def _rodrigues(a, th):
+    """Rot(a, θ) = 1 + sin θ [a×] + (1 − cos θ)[a×]² (a unit)."""
+    ax = _skew(np.asarray(a, float))
+    return np.eye(3) + np.sin(th) * ax + (1.0 - np.cos(th)) * ax @ ax
+
+
+def floating_mass_matrix_jacobians(x, model=None):
+    """M(q) of rbd_floating_arm's mechanism as Σᵢ mᵢ Jvᵢᵀ Jvᵢ + Jωᵢᵀ (Rᵢ Icᵢ Rᵢᵀ) Jωᵢ: the
+    kinetic energy ½ vᵀ M v summed over the three bodies from each body's COM velocity
+    and angular velocity. Nothing of the CRBA / spatial-algebra restatement is used:
+    the bodies' poses come from composing the URDF transforms (joint origin p, fixed
+    rotation R0, Rodrigues rotation about the axis) as 3×3 rotations and 3-vectors, and
+    the Jacobians from the geometric rule v_c = v₀ + ω₀ × c + Σ_joints (aⱼ θ̇ⱼ) × (c − oⱼ).
+    Everything is expressed in the base frame, where the base twist (ω₀, v₀) of the
+    generalised velocity lives (body-frame twist, angular first; x[8:16] = [ω₀, v₀, θ̇]).
+    x: (P, 16) → (P, 8, 8)."""
+    md = ARM_2DOF if model is None else model
+    x = np.asarray(x, float)
+    out = np.zeros((x.shape[0], 8, 8))
+    cb = np.asarray(md["base_com"], float)
+    for k, xk in enumerate(x):
+        th = xk[6:8]
+        Js = []   # (m, Jv (3, 8), Jw (3, 8), R, Ic) per body
+        # base: COM velocity v₀ + ω₀ × c = v₀ − [c×] ω₀
+        Jv = np.zeros((3, 8))
+        Jw = np.zeros((3, 8))
+        Jv[:, 0:3] = -_skew(cb)
+        Jv[:, 3:6] = np.eye(3)
+        Jw[:, 0:3] = np.eye(3)
+        Js.append((md["base_mass"], Jv, Jw, np.eye(3), np.asarray(md["base_Ic"], float)))
+        R, o = np.eye(3), np.zeros(3)            # the parent body's pose in the base frame
+        axes = []                                 # (joint origin, world-of-base axis)
+        for j in range(2):
+            Rj0 = R @ np.asarray(md["R0"][j], float)
+            o = o + R @ np.asarray(md["p"][j], float)
+            axes.append((o.copy(), Rj0 @ np.asarray(md["axis"][j], float)))  # Rot(a, θ) a = a
+            R = Rj0 @ _rodrigues(md["axis"][j], th[j])
+            c = o + R @ np.asarray(md["com"][j], float)
+            Jv = np.zeros((3, 8))
+            Jw = np.zeros((3, 8))
+            Jv[:, 0:3] = -_skew(c)
+            Jv[:, 3:6] = np.eye(3)
+            Jw[:, 0:3] = np.eye(3)
+            for i, (oi, ai) in enumerate(axes):
+                Jv[:, 6 + i] = np.cross(ai, c - oi)
+                Jw[:, 6 + i] = ai
+            Js.append((md["mass"][j], Jv, Jw, R, np.asarray(md["Ic"][j], float)))
+        for m, Jv, Jw, Rb, Ic in Js:
+            out[k] += m * Jv.T @ Jv + Jw.T @ (Rb @ Ic @ Rb.T) @ Jw
+    return out
+
+
+def mrp_to_dcm(p):
+    """Body-to-world rotation of MRPs p (P, 3) (the attitude kinematics rbd_floating_arm
+    integrates, pdot_from_w): R = 1 + (8[p×]² + 4(1 − pᵀp)[p×]) / (1 + pᵀp)²."""
+    p = np.asarray(p, float)
+    out = np.zeros((p.shape[0], 3, 3))
+    for k, pk in enumerate(p):
+        S = _skew(pk)
+        pp = float(pk @ pk)
+        out[k] = np.eye(3) + (8.0 * S @ S + 4.0 * (1.0 - pp) * S) / (1.0 + pp) ** 2
+    return out
+
+
+def floating_linear_momentum_world(x, model=None, M=None):
+    """The mechanism's total linear momentum in the world frame: R(p) · (M(q) v)[3:6]
+    (the base rows of M v are the system's spatial momentum in the base frame). Conserved
+    at u = 0 with zero gravity. x: (P, 16) → (P, 3)."""
+    x = np.asarray(x, float)
+    M = floating_mass_matrix_jacobians(x, model) if M is None else M
+    h = np.einsum("pij,pj->pi", M, x[:, 8:16])
+    return np.einsum("pij,pj->pi", mrp_to_dcm(x[:, 0:3]), h[:, 3:6])

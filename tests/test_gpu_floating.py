@@ -336,3 +336,28 @@ def test_linearize_dynamics_helper_dispatches(gpu):
     Aj, Bj = jet.jacobians(fj, x[:5], u[:5])
     assert rel(A1, Aj[0]) < 1e-10 and rel(B1, Bj[0]) < 1e-10
     assert rel(AT, Aj) < 1e-10 and rel(BT, Bj) < 1e-10
+
+
+@pytest.mark.parametrize("name", ["2dof_arm", "coupled"])
+def test_floating_device_conserves_world_linear_momentum(gpu, name):
+    """Zero gravity, u = 0: the device RK4 keeps the world-frame linear momentum
+    R(p)·(M v)[3:6] over 300 steps to RK4 accuracy, with M from the independent
+    Jacobian formulation (tests/closures.py floating_mass_matrix_jacobians; the CPU pins
+    are tests/test_floating_pins.py)."""
+    from closures import coupled_floating_model, floating_linear_momentum_world
+    model = None if name == "2dof_arm" else coupled_floating_model()
+    p = rbd_example_problem() if model is None else _problem_of(model)
+    x, _ = random_states(16, seed=21)
+    s = FloatingSolver(p, 1, 1)
+    try:
+        xe = torch.from_numpy(x).cuda()
+        z = torch.zeros(16, 8, dtype=torch.float64, device="cuda")
+        for _ in range(300):
+            xe = s.dynamics(xe, z)
+        x1 = xe.cpu().numpy()
+    finally:
+        s.close()
+    p0 = floating_linear_momentum_world(x, model)
+    p1 = floating_linear_momentum_world(x1, model)
+    assert np.abs(p0).max() > 1.0
+    assert np.abs(p1 - p0).max() / np.abs(p0).max() < 1e-7, (p0, p1)
