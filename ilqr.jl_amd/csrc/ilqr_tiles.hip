@@ -351,6 +351,13 @@ __device__ bool tiles_backward_wide_wave(const TileParams& P, int b, int T, int 
     for (int i = 0; i < TW_NU; ++i)
 #pragma unroll
       for (int k = 0; k <= i; ++k) h[i][k] = Hl[i * 16 + k];
+    // rows nu..7 are padding (zero H rows and right-hand sides): give their pivots the
+    // value 1 (1 − μ here, + μ in the factor), else a pivot is μ and μ = 0 makes its
+    // reciprocal inf, 0·inf = NaN in the padded unknowns, which back-substitution would
+    // carry into the real ones
+#pragma unroll
+    for (int i = 0; i < TW_NU; ++i)
+      if (i >= nu) h[i][i] = 1.0 - mu;
     double xs[TW_NU], xd[TW_NU];
 #pragma unroll
     for (int j = 0; j < TW_NU; ++j) {

@@ -138,8 +138,11 @@ def _floating_solver(xb, ub, dynamicsf, immediate_cost, final_cost):
 
 
 def clear_cache():
-    """Close the device workspaces fit / backward_pass / linearize_dynamics keep per shape."""
+    """Close the device workspaces fit / backward_pass / linearize_dynamics keep per shape
+    and release the generic closure path's cached rollout graphs (ilqr_amd.tiles)."""
     _cache.clear()
+    from . import tiles
+    tiles.clear_graphs()
 
 
 def _solver(xb, ub, dynamicsf, immediate_cost, final_cost):

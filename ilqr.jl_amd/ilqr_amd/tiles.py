@@ -22,9 +22,14 @@ the rollout calls the user's dynamics, so it runs as torch ops on the device
 graph and replayed T times per line-search trial: a closure of a few hundred small ops
 (the reference's RBD caller) then costs one graph launch per step instead of a few
 hundred dispatches (tools/archive/r05/rollout_probe.py: 4.0 → 0.73 ms per step at nx = 16, B = 1).
-The capture is checked against an eager step bit for bit before it is used; closures
-that cannot be captured (a host synchronisation inside them) run eagerly.
-ILQR_ROLLOUT_GRAPH=0 turns the graphs off.
+The capture is checked against an eager step bit for bit before it is used, and again
+at the start of EVERY later forward_pass on the cached graph: a replay freezes what the
+closure read from Python when it was captured (a rebound global or attribute, a changed
+target or Δt), where the reference calls dynamicsf afresh at every step, so a replay
+that no longer equals the eager step is captured again (and the closure runs eagerly if
+that fails). Closures that cannot be captured (a host synchronisation inside them) run
+eagerly. The graphs' static buffers are bounded (MAX_GRAPH_BYTES in all, oldest evicted)
+and released by ilqr_amd.api.clear_cache(). ILQR_ROLLOUT_GRAPH=0 turns the graphs off.
 """
 from __future__ import annotations
 
@@ -86,6 +91,7 @@ def total_cost(xb, ub, x_traj, immediate_cost, final_cost):
 
 ROLLOUT_GRAPHS = os.environ.get("ILQR_ROLLOUT_GRAPH", "1") != "0"
 MAX_GRAPHS_PER_CLOSURE = 4
+MAX_GRAPH_BYTES = int(os.environ.get("ILQR_ROLLOUT_GRAPH_BYTES", str(2 << 30)))  # all graphs' buffers
 _GRAPHS: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()  # dynamicsf → {shape: graph}
 _GRAPHS_LOCK = threading.Lock()
 _CAPTURE_LOCK = threading.Lock()
@@ -127,6 +133,8 @@ class _RolloutGraph:
         self.k = torch.zeros(1, dtype=torch.long, device=dev)
         self.graph = None
         self.lock = threading.Lock()
+        self.seq = 0  # last use (eviction order)
+        self.nbytes = sum(t.numel() * t.element_size() for t in (self.X, self.U, self.D, self.K, self.XB, self.UB))
 
     def step(self, f):
         k = self.k
@@ -187,6 +195,16 @@ class _RolloutGraph:
         self.graph = g if ok else None
         return ok
 
+    def still_valid(self, f):
+        """Replay step 0 and an eager step 0 on the loaded inputs (α = 1): equal bit for bit
+        when the closure still computes what was captured."""
+        self.start(torch.ones_like(self.alpha))
+        self.step(f)
+        want_x, want_u = self.XB[:, 1].clone(), self.UB[:, 0].clone()
+        self.start(torch.ones_like(self.alpha))
+        self.graph.replay()
+        return bool(torch.equal(self.XB[:, 1], want_x)) and bool(torch.equal(self.UB[:, 0], want_u))
+
 
 def _clear_hip_error():
     """Reset the HIP runtime's per-thread last error that an invalidated capture leaves
@@ -198,12 +216,43 @@ def _clear_hip_error():
         pass
 
 
+def _graph_bytes():
+    return sum(g.nbytes for per in list(_GRAPHS.values()) for g in per.values() if g)
+
+
+def _evict_for(nbytes):
+    """Drop the oldest cached graphs (any closure) until nbytes more fit under
+    MAX_GRAPH_BYTES. Caller holds _GRAPHS_LOCK."""
+    while _graph_bytes() + nbytes > MAX_GRAPH_BYTES:
+        victim = None
+        for per in list(_GRAPHS.values()):
+            for key, g in per.items():
+                if g and not g.lock.locked() and (victim is None or g.seq < victim[2].seq):
+                    victim = (per, key, g)
+        if victim is None:
+            return False
+        del victim[0][victim[1]]
+    return True
+
+
+_SEQ = [0]
+
+
+def clear_graphs():
+    """Release every cached rollout graph and its static buffers (ilqr_amd.api.clear_cache)."""
+    with _GRAPHS_LOCK:
+        _GRAPHS.clear()
+
+
 def _rollout_graph(dynamicsf, x, u):
     """The cached captured step for (dynamicsf, shape), capturing on first use; None
-    when graphs are off, the closure cannot be cached or captured."""
+    when graphs are off, the closure cannot be cached or captured, or its buffers would
+    not fit under MAX_GRAPH_BYTES."""
     if not (ROLLOUT_GRAPHS and x.is_cuda):
         return None
     key = (tuple(x.shape), tuple(u.shape), x.dtype, x.device.index)
+    nb, N, nx = x.shape
+    need = 8 * (2 * nb * N * nx + 3 * nb * (N - 1) * u.shape[2] + nb * (N - 1) * u.shape[2] * nx)
     try:
         with _GRAPHS_LOCK:
             per = _GRAPHS.setdefault(dynamicsf, {})
@@ -211,7 +260,12 @@ def _rollout_graph(dynamicsf, x, u):
             if g is None:
                 if len(per) >= MAX_GRAPHS_PER_CLOSURE:
                     per.pop(next(iter(per)))
+                if not _evict_for(need):
+                    return None
                 g = per[key] = _RolloutGraph(x, u)  # holds no reference to the closure
+            if g:
+                _SEQ[0] += 1
+                g.seq = _SEQ[0]
     except TypeError:  # not weak-referenceable
         return None
     return g or None  # False: this closure failed to capture at this shape
@@ -248,6 +302,8 @@ def rollout_forward(x, u, x_traj, d, K, prev_cost, dynamicsf, immediate_cost, fi
                             lambda alpha: _rollout_eager(f, x, u, d, K, alpha))
     with g.lock:
         g.load(x, u, d, K)
+        if g.graph is not None and not g.still_valid(f):
+            g.graph = None        # the closure changed since the capture: capture again
         if g.graph is None:
             try:
                 g.capture(f)

@@ -115,6 +115,24 @@ def test_tiles_wide_shapes_vs_oracle(gpu, n, m):
     s.close()
 
 
+@pytest.mark.parametrize("n,m", [(16, 5), (13, 7), (4, 6), (16, 8)])
+def test_tiles_wide_mu_zero_padded_pivots(gpu, n, m):
+    """μ = 0 on the wide kernel: with nu < 8 its padded LDLᵀ pivots were μ,
+    so μ = 0 made them 0 and NaN reached the real gains. luu is positive definite here,
+    so the unregularised system is solvable and the gains must match the oracle's."""
+    nb, T = 5, 30
+    tl = random_tiles(nb, T, n, m, seed=7000 + 10 * n + m)
+    s = Solver(n, m, T, nb, kind=_lib.PROBLEM_TILES)
+    try:
+        d, K, st = s.backward_tiles(to_dev(tl), mu=0.0)
+    finally:
+        s.close()
+    assert (st.cpu().numpy() == 0).all()
+    dr, Kr, _ = cref.tiles_backward(tl, mu=0.0, symmetrize=True)
+    assert np.isfinite(d.cpu().numpy()).all() and np.isfinite(K.cpu().numpy()).all()
+    assert rel(d, dr) < 1e-10 and rel(K, Kr) < 1e-10
+
+
 def test_tiles_wide_rbd_shape_long_horizon(gpu):
     """The reference RBD caller's shape: nx = 16, nu = 8, T = 1000
     (test/RBD_2_link_example/animate_RBD_2_link.jl:8,19-20)."""
@@ -387,3 +405,41 @@ def test_rollout_graph_falls_back_for_uncapturable_closure(gpu):
     assert rel(xs, xf) < 1e-12 and rel(us, uf) < 1e-12
     assert list(tiles._GRAPHS[synced].values()) == [False]
     assert tiles._GRAPHS[f0] and all(v and v.graph is not None for v in tiles._GRAPHS[f0].values())
+
+
+def test_rollout_graph_follows_a_changed_closure(gpu):
+    """A closure that reads Python state (here Δt from a dict, like the reference's
+    closures capture globals): after the state changes, the cached graph's replay no
+    longer equals the eager step, so forward_pass captures again — the
+    result equals the eager rollout with the new state. clear_cache() releases the graphs."""
+    from ilqr_amd import tiles
+    state = {"dt": 0.05}
+
+    def f(x, u):
+        dt = state["dt"]
+        return torch.stack([x[0] + dt * x[2], x[1] + dt * x[3],
+                            x[2] + dt * (-9.81 * torch.sin(x[0]) + u[0]),
+                            x[3] + dt * (-9.81 * torch.sin(x[1]) + u[1])])
+
+    _, l, lf = coupled_pendula(torch_ns())
+    x, u = pendula_batch(3, 25, seed=9)
+    xb, ub = torch.from_numpy(x).cuda(), torch.from_numpy(u).cuda()
+    d = 0.1 * torch.ones_like(ub)
+    K = torch.zeros((3, 25, 2, 4), dtype=torch.float64, device="cuda")
+    prev = torch.full((3,), float("inf"), dtype=torch.float64, device="cuda")
+    old = tiles.ROLLOUT_GRAPHS
+    try:
+        tiles.ROLLOUT_GRAPHS = True
+        g1 = tiles.rollout_forward(xb, ub, None, d, K, prev, f, l, lf, 4)
+        state["dt"] = 0.1
+        g2 = tiles.rollout_forward(xb, ub, None, d, K, prev, f, l, lf, 4)
+        tiles.ROLLOUT_GRAPHS = False
+        e2 = tiles.rollout_forward(xb, ub, None, d, K, prev, f, l, lf, 4)
+    finally:
+        tiles.ROLLOUT_GRAPHS = old
+    assert not torch.equal(g1[0], g2[0])
+    assert torch.equal(g2[0], e2[0]) and torch.equal(g2[1], e2[1]) and torch.equal(g2[2], e2[2])
+    entry = tiles._GRAPHS[f][(tuple(xb.shape), tuple(ub.shape), xb.dtype, 0)]
+    assert entry and entry.graph is not None          # captured again, not the eager fallback
+    api.clear_cache()
+    assert f not in tiles._GRAPHS
