@@ -209,6 +209,35 @@ def test_rollout_graph_bookkeeping_on_cpu():
     assert wr() is None and len(tiles._GRAPHS) == n - 1
 
 
+def test_rollout_graph_cache_is_bounded_and_clearable():
+    """The cached graphs' static buffers stay under MAX_GRAPH_BYTES (least recently used
+    evicted first) and api.clear_cache() releases them all."""
+    import torch
+    from ilqr_amd import api, tiles
+    x = torch.zeros(4, 11, 3, dtype=torch.float64)
+    u = torch.zeros(4, 10, 2, dtype=torch.float64)
+    one = tiles._RolloutGraph(x, u).nbytes
+    fs = [lambda a, v, i=i: a for i in range(3)]
+    old = tiles.MAX_GRAPH_BYTES
+    try:
+        tiles.clear_graphs()
+        tiles.MAX_GRAPH_BYTES = 2 * one
+        for i, f in enumerate(fs):
+            g = tiles._RolloutGraph(x, u)
+            g.seq = i + 1
+            with tiles._GRAPHS_LOCK:
+                assert tiles._evict_for(g.nbytes)
+                tiles._GRAPHS[f] = {"k": g}
+        assert tiles._graph_bytes() <= tiles.MAX_GRAPH_BYTES
+        assert not tiles._GRAPHS.get(fs[0]) and tiles._GRAPHS[fs[1]] and tiles._GRAPHS[fs[2]]
+        with tiles._GRAPHS_LOCK:                       # larger than the bound: refused
+            assert not tiles._evict_for(3 * one)
+        api.clear_cache()
+        assert len(tiles._GRAPHS) == 0
+    finally:
+        tiles.MAX_GRAPH_BYTES = old
+
+
 def test_floating_restatement_conserves_energy():
     """With u = 0 and zero gravity the floating mechanism's kinetic energy is conserved
     (up to RK4's O(dt⁴) error): the restated mass matrix and Newton-Euler bias belong
