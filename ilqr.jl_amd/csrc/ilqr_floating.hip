@@ -827,6 +827,12 @@ __global__ __launch_bounds__(64 * FB_FWD_WAVES) void fb_forward_kernel(const FbM
     for (int k = 0; k < CAND; ++k) alpha *= a.shrink;  // trial j + CAND's
     if (!__any(live && done_trial == 0)) break;
   }
+  // trial 1 stored its rollout into xn/un from waves 1 (x̄) and 2 (ū) with plain global
+  // stores, and fb_lds_barrier waits for LDS only: a workgroup release/acquire barrier
+  // orders those stores before the copy below writes the same words from other lanes
+  // (every wave of the block leaves the loop after the same round: the roles run each
+  // rollout together)
+  __syncthreads();
   if (live && done_trial <= 0) {  // no trial accepted: x̄, ū = the inputs, as the closure path
     const size_t c2 = (size_t)(FB_FWD_WAVES * c + role);
     for (size_t i = c2; i < nxe; i += FB_FWD_WAVES * CAND) a.xn[(size_t)b * nxe + i] = a.x[(size_t)b * nxe + i];

@@ -235,19 +235,26 @@ class FloatingSolver:
 
 # -- reference-API callables (recognised by ilqr_amd.fit) ------------------------------------
 class FloatingDynamics:
-    """dynamicsf(x, u) of a FloatingProblem, evaluated on the device (one launch)."""
+    """dynamicsf(x, u) of a FloatingProblem, evaluated on the device (one launch) on a
+    handle cached per (model, device) (cache.py: the reference script calls dynamicsf
+    1000 times to build its state_traj, animate_RBD_2_link.jl:23-25). Device tensors
+    stay on their device (and come back as tensors); anything else is evaluated on the
+    current device and comes back as a numpy array."""
 
     def __init__(self, problem: FloatingProblem):
         self.problem = problem
 
     def __call__(self, x, u):
-        xt = torch.as_tensor(np.asarray(x, float), device="cuda")[None].contiguous()
-        ut = torch.as_tensor(np.asarray(u, float), device="cuda")[None].contiguous()
-        s = FloatingSolver(self.problem, 1, 1)
-        try:
-            return s.dynamics(xt, ut)[0].cpu().numpy()
-        finally:
-            s.close()
+        from . import cache
+        on_dev = isinstance(x, torch.Tensor) and x.is_cuda
+        dev = x.device if on_dev else torch.device("cuda", torch.cuda.current_device())
+        xt = torch.as_tensor(x, dtype=torch.float64, device=dev).reshape(1, -1).contiguous()
+        ut = torch.as_tensor(u, dtype=torch.float64, device=dev).reshape(1, -1).contiguous()
+        key = ("floating", dev.index, bytes(self.problem.struct()), 1, 1)
+        with torch.cuda.device(dev), \
+                cache.workspace(key, lambda: FloatingSolver(self.problem, 1, 1, device=dev.index)) as s:
+            y = s.dynamics(xt, ut)[0]
+        return y if on_dev else y.cpu().numpy()
 
 
 class FloatingCost:

@@ -142,6 +142,12 @@ def test_api_fit_dispatches_the_recognised_closures(gpu):
     assert rel(dyn(x[0, 0], u[0, 0]), fj(x[:1, 0], u[:1, 0])[0]) < 1e-12
     assert abs(cost(x[0, 3], u[0, 3]) - float(lj(x[:1, 3], u[:1, 3])[0])) <= 1e-12 * abs(cost(x[0, 3], u[0, 3]))
     assert abs(fcost(x[0, T]) - float(lfj(x[:1, T])[0])) <= 1e-12 * abs(fcost(x[0, T]))
+    # the script builds state_traj with 1000 dynamicsf calls: one cached handle serves them,
+    # and a device tensor stays on its device
+    n0 = cache.size()
+    ys = [dyn(xt[0, t], ut[0, t]) for t in range(20)]
+    assert cache.size() == n0 and isinstance(ys[0], torch.Tensor) and ys[0].is_cuda
+    assert rel(ys[3], fj(x[:1, 3], u[:1, 3])[0]) < 1e-12
     api.clear_cache()
 
 
