@@ -467,6 +467,323 @@ __device__ FwdOut lq_forward_wave_ring(const LQParams& P, int b0, int B, int T, 
 }
 
 // ---------------------------------------------------------------------------
+// The WIDE candidate pass (round 6, the cooperative search's default: ILQR_COOP_WIDTH).
+// Sixteen trials of ONE trajectory per wave instead of four: trial τ = lane & 15 runs on
+// the four lanes ρ = lane >> 4, lane ρ owning rows 3ρ..3ρ+2 of x̄ and row ρ of ū. Each
+// row is computed with the row form's arithmetic in the row form's order — the same
+// four accumulators per dot product (term k into accumulator k mod 4, k ascending, the
+// x̄ part before the ū part), the same (a0 + a1) + (a2 + a3), the same per-row cost and
+// Σ(ū − u)² accumulators and, at the end, rowsum16's butterfly over the sixteen rows —
+// so a trial's rollout, cost, Σ(ū − u)² and `eo` are bit for bit the row form's
+// (lq_forward_wave_ring<CAND>) and the sequential search's. What changes is how the
+// operands meet: the row form broadcasts x̄ₖ and ūₘ from their lanes with DPP
+// (row_newbcast, the only f64 DPP mode: one trial per 16-lane row); here the rows of a
+// trial exchange x̄, δx = x̄ − x, v = x̄ − x_traj and ū through the LDS (ds_write_b64 by
+// the owner, ds_read_b128 by the trial's four lanes; in-order LDS within the wave, no
+// barrier), and each lane keeps its three [A | B] and Q rows in registers. Per step and
+// lane ≈150 VALU ops for sixteen trials against ≈140 for four in the row form.
+// Exchange area (the ring's LAREA, unused by a candidate pass): per trial C16_ES
+// doubles, x̄ [0,12), δx [12,24), v [24,36), ū [36,40); stride 42 doubles puts the
+// sixteen trials of a ds_read_b128 lane group on sixteen different 4-bank quarters.
+constexpr int C16_ES = 42;
+static_assert(16 * C16_ES <= RING_LAREA, "the exchange area fits the ring's LAREA");
+struct Cand16 {
+  double cost, du2;
+  bool eo;  // fma(α, δuₖ, uₖ) == uₖ at every step (CandPass)
+};
+
+// `alpha`: this lane's trial's α. `st`: this lane's trial stores its rollout through rXN /
+// rUN at rollout index gs (x̄ (T+1)·12, ū T·4 doubles per rollout). Whole wave.
+template <int R, int PF>
+__device__ Cand16 lq_cand16_pass(const LQParams& P, int b, int T, const double* __restrict__ x,
+                                 const double* __restrict__ u, const double* __restrict__ xtraj,
+                                 const double* __restrict__ dg, const double* __restrict__ Kg, double alpha, bool st,
+                                 __amdgpu_buffer_rsrc_t rXN, __amdgpu_buffer_rsrc_t rUN, int gs, double* ring) {
+  constexpr int NX = 12, NU = 4;
+  static_assert(R > PF && PF >= 1, "the slot being refilled must not be the one being read");
+  constexpr uint32_t OOR = 0x80000000u;
+  b = __builtin_amdgcn_readfirstlane(b);
+  const int l = threadIdx.x & 63;
+  const int r = l >> 4;   // rows 3r .. 3r+2 of x̄, row r of ū
+  const int tt = l & 15;  // the trial
+
+  // this lane's rows: [A | B] as the row form's Fr (A + 0, 0 + B) and R in registers;
+  // Q in the slots' tail (ring slot 0, doubles [QO, QO + 144): the candidate producer fills
+  // only a slot's first 80 doubles), read per step
+  constexpr int QO = 96;
+  static_assert(QO >= 80 && QO + NX * NX <= RING_SLOT, "Q fits slot 0's tail");
+  double F[3][16], Rr[NU];
+  {
+    const double* Ab = P.A + (size_t)b * NX * NX;
+    const double* Bb = P.B + (size_t)b * NX * NU;
+    const double* Qb = P.Q + (size_t)b * NX * NX;
+    const double2* rr = reinterpret_cast<const double2*>(P.R + (size_t)b * NU * NU + r * NU);
+    for (int i = l; i < NX * NX; i += 64) ring[QO + i] = Qb[i];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const double2* ar = reinterpret_cast<const double2*>(Ab + (3 * r + i) * NX);
+      const double2* br = reinterpret_cast<const double2*>(Bb + (3 * r + i) * NU);
+#pragma unroll
+      for (int k = 0; k < NX / 2; ++k) {
+        const double2 a2 = ar[k];
+        F[i][2 * k] = a2.x + 0.0;
+        F[i][2 * k + 1] = a2.y + 0.0;
+      }
+#pragma unroll
+      for (int m = 0; m < NU / 2; ++m) {
+        const double2 b2 = br[m];
+        F[i][NX + 2 * m] = 0.0 + b2.x;
+        F[i][NX + 2 * m + 1] = 0.0 + b2.y;
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < NU / 2; ++m) {
+      const double2 r2 = rr[m];
+      Rr[2 * m] = r2.x;
+      Rr[2 * m + 1] = r2.y;
+    }
+  }
+  // the ring's loads below are inline asm, invisible to the compiler's wait counting:
+  // every constant is in its register before the first of them
+  __builtin_amdgcn_s_waitcnt((0) | (7 << 4) | (15 << 8));
+  asm volatile("" ::: "memory");
+
+  // producer: the candidate pass's one instruction per step (lq_forward_wave_ring<CAND>):
+  // K 0..23, x 24..29, u 30..31, x_traj 32..37, δu 38..39 (chunks of 16 B)
+  const double* xt0 = xtraj ? xtraj : x;  // x_traj = NULL: read x with weight 0
+  const double xtw = xtraj ? 1.0 : 0.0;
+  const char* p1;
+  uint32_t s1;
+  {
+    const int c = l < 40 ? l : l - 40;
+    const size_t bb = (size_t)b;
+    if (c < 24) {
+      p1 = reinterpret_cast<const char*>(Kg + bb * T * NU * NX + 2 * c);
+      s1 = NU * NX * 8;
+    } else if (c < 30) {
+      p1 = reinterpret_cast<const char*>(x + bb * (T + 1) * NX + 2 * (c - 24));
+      s1 = NX * 8;
+    } else if (c < 32) {
+      p1 = reinterpret_cast<const char*>(u + bb * T * NU + 2 * (c - 30));
+      s1 = NU * 8;
+    } else if (c < 38) {
+      p1 = reinterpret_cast<const char*>(xt0 + bb * (T + 1) * NX + 2 * (c - 32));
+      s1 = NX * 8;
+    } else {
+      p1 = reinterpret_cast<const char*>(dg + bb * T * NU + 2 * (c - 38));
+      s1 = NU * 8;
+    }
+  }
+  const uint32_t ring_lds = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) double*)ring;
+  auto produce = [&](int t) {
+    uint32_t tq = (uint32_t)(t < T ? t : T - 1);  // clamped: loaded, never read
+    asm volatile("" : "+s"(tq));
+    const uint32_t m0 = ring_lds + (uint32_t)((t % R) * RING_SLOT * 8);
+    asm volatile(ILQR_FW_LDS_OP1 ::"v"(p1 + (size_t)tq * s1), "{m0}"(m0) : "memory");
+  };
+  // per step: one slot load, then four result stores (three x̄ rows, one ū row)
+  constexpr int NL = 1, NS = 4;
+  constexpr int N_SS = (NL + NS) * PF - NL, N_PRO = NL * PF - NL;
+  auto wait_slot = [](auto n) {
+    constexpr int v = decltype(n)::value;
+    static_assert(v >= 0 && v < 64, "vmcnt is 6 bits");
+    __builtin_amdgcn_s_waitcnt((v & 15) | (7 << 4) | (15 << 8) | ((v >> 4) << 14));
+    asm volatile("" ::: "memory");
+  };
+  // slot offsets (doubles): K row m at 12m, x 48, u 60, x_traj 64, δu 76
+  constexpr int SX = 48, SU = 60, SXT = 64, SD = 76;
+
+  double* const my = ring + R * RING_SLOT + tt * C16_ES;  // this trial's exchange row
+  const uint32_t oxs = st ? (uint32_t)(gs * (T + 1) * NX + 3 * r) * 8 : OOR;
+  const uint32_t ous = st ? (uint32_t)(gs * T * NU + r) * 8 : OOR;
+  auto rd12 = [](const double* p, double (&v)[NX]) {
+    const double2* q = reinterpret_cast<const double2*>(p);
+#pragma unroll
+    for (int k = 0; k < NX / 2; ++k) {
+      const double2 w = q[k];
+      v[2 * k] = w.x;
+      v[2 * k + 1] = w.y;
+    }
+  };
+  // Σ_k<12 v[k]·c[k], accumulator k mod 4, (a0 + a1) + (a2 + a3): dpp_dot12's order
+  auto dot12 = [](const double (&v)[NX], const double* c) {
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+#pragma unroll
+    for (int k = 0; k < NX; k += 4) {
+      a0 = fma(v[k], c[k], a0);
+      a1 = fma(v[k + 1], c[k + 1], a1);
+      a2 = fma(v[k + 2], c[k + 2], a2);
+      a3 = fma(v[k + 3], c[k + 3], a3);
+    }
+    return (a0 + a1) + (a2 + a3);
+  };
+
+#pragma unroll
+  for (int t = 0; t < PF; ++t) produce(t);
+  wait_slot(std::integral_constant<int, N_PRO>{});
+  double xo[3], vo[3];  // this lane's rows of x̄ₖ and vₖ = x̄ₖ − x_trajₖ
+  {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const double xk = ring[SX + 3 * r + i];
+      xo[i] = xk;  // x̄₁ = x₁ (:65)
+      vo[i] = fma(-xtw, ring[SXT + 3 * r + i], xo[i]);
+      my[3 * r + i] = xo[i];
+      my[NX + 3 * r + i] = xo[i] - xk;
+      my[2 * NX + 3 * r + i] = vo[i];
+    }
+  }
+  wave_lds_fence();
+  double cost[3] = {0.0, 0.0, 0.0}, costu = 0.0, du2 = 0.0;
+  bool eo = true;
+  auto step = [&](int t, auto next_wait) {
+    const double* sl = ring + (t % R) * RING_SLOT;
+    // ūₖ row r = uₖ + α δuₖ + Kₖ δx (:72-73)
+    double Kr[NX], DX[NX];
+    rd12(sl + NX * r, Kr);
+    rd12(my + NX, DX);
+    const double urk = sl[SU + r], durk = sl[SD + r];
+    const double kdx = dot12(DX, Kr);
+    const double ua = fma(alpha, durk, urk);
+    const double ub = ua + kdx;
+    eo = eo && (ua == urk);
+    const double e = ub - urk;
+    du2 = fma(e, e, du2);
+    my[3 * NX + r] = ub;
+    // x̄ₖ₊₁ = A x̄ₖ + B ūₖ (:74): the A part first, it does not need ūₖ
+    double XB[NX];
+    rd12(my, XB);
+    double acc[3][4];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) acc[i][0] = acc[i][1] = acc[i][2] = acc[i][3] = 0.0;
+#pragma unroll
+    for (int k = 0; k < NX; ++k)
+#pragma unroll
+      for (int i = 0; i < 3; ++i) acc[i][k & 3] = fma(XB[k], F[i][k], acc[i][k & 3]);
+    // ℓ(x̄ₖ − x_trajₖ, ·) rows (:187-190): vᵀ(Q row)
+    double V[NX];
+    rd12(my + 2 * NX, V);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      double qr[NX];
+      rd12(ring + QO + (3 * r + i) * NX, qr);
+      cost[i] = fma(vo[i], dot12(V, qr), cost[i]);
+    }
+    produce(t + PF);  // slot (t+PF)%R was last read at step t+PF−R < t
+    wave_lds_fence();  // ū of every row written before it is read
+    double U4[NU];
+    {
+      const double2* q = reinterpret_cast<const double2*>(my + 3 * NX);
+      const double2 w0 = q[0], w1 = q[1];
+      U4[0] = w0.x;
+      U4[1] = w0.y;
+      U4[2] = w1.x;
+      U4[3] = w1.y;
+    }
+#pragma unroll
+    for (int m = 0; m < NU; ++m)
+#pragma unroll
+      for (int i = 0; i < 3; ++i) acc[i][m] = fma(U4[m], F[i][NX + m], acc[i][m]);
+    // the ū row's cost: ūᵀ(R row) with one accumulator per term (dpp_dot16_bd's bank 3)
+    const double lvu = (fma(U4[0], Rr[0], 0.0) + fma(U4[1], Rr[1], 0.0)) +
+                       (fma(U4[2], Rr[2], 0.0) + fma(U4[3], Rr[3], 0.0));
+    costu = fma(ub, lvu, costu);
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, xo[i]), rXN, oxs,
+                                            (uint32_t)(t * NX + i) * 8, 0);
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, ub), rUN, ous, (uint32_t)t * NU * 8, 0);
+    double xn[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) xn[i] = (acc[i][0] + acc[i][1]) + (acc[i][2] + acc[i][3]);
+    // slot t + 1 (past the horizon: a clamped step's slot, read and never used)
+    wait_slot(next_wait);
+    const double* sn = ring + ((t + 1) % R) * RING_SLOT;
+    double dn[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      dn[i] = xn[i] - sn[SX + 3 * r + i];
+      vo[i] = fma(-xtw, sn[SXT + 3 * r + i], xn[i]);
+      xo[i] = xn[i];
+    }
+    wave_lds_fence();  // this step's reads of the exchange row issued before its overwrite
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      my[3 * r + i] = xo[i];
+      my[NX + 3 * r + i] = dn[i];
+      my[2 * NX + 3 * r + i] = vo[i];
+    }
+    wave_lds_fence();
+  };
+  const int tp = T < PF ? T : PF;
+  for (int t = 0; t < tp - 1; ++t) step(t, std::integral_constant<int, N_PRO>{});
+  for (int t = tp - 1; t < T; ++t) step(t, std::integral_constant<int, N_SS>{});
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, xo[i]), rXN, oxs, (uint32_t)(T * NX + i) * 8, 0);
+  // final_cost(x̄_N) = x̄ᵀQf x̄ on the raw state (:192): the rows' Qf dots; the ū rows
+  // take the row form's 0·(x̄ · 0) (a NaN state stays NaN there as well)
+  {
+    double XB[NX];
+    rd12(my, XB);
+    const double* Qfb = P.Qf + (size_t)b * NX * NX;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      double qf[NX];
+      rd12(Qfb + (3 * r + i) * NX, qf);
+      cost[i] = fma(xo[i], dot12(XB, qf), cost[i]);
+    }
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+    const double z = 0.0;
+#pragma unroll
+    for (int k = 0; k < NX; k += 4) {
+      a0 = fma(XB[k], z, a0);
+      a1 = fma(XB[k + 1], z, a1);
+      a2 = fma(XB[k + 2], z, a2);
+      a3 = fma(XB[k + 3], z, a3);
+    }
+    costu = fma(z, (a0 + a1) + (a2 + a3), costu);
+  }
+  // rowsum16 over the trial's sixteen rows (x̄ rows 0..11, ū rows 12..15): lane 0's
+  // butterfly (xor 8, 4, 2, 1) is (((c0+c8)+(c4+c12)) + ((c2+c10)+(c6+c14))) +
+  // (((c1+c9)+(c5+c13)) + ((c3+c11)+(c7+c15))), and every lane of the row ends equal
+  wave_lds_fence();
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    my[3 * r + i] = cost[i];
+    my[16 + 3 * r + i] = 0.0;  // the x̄ rows' Σ(ū − u)²: fma(0, 0, ·) from 0
+  }
+  my[12 + r] = costu;
+  my[16 + 12 + r] = du2;
+  wave_lds_fence();
+  auto tree16 = [](const double* c) {
+    return (((c[0] + c[8]) + (c[4] + c[12])) + ((c[2] + c[10]) + (c[6] + c[14]))) +
+           (((c[1] + c[9]) + (c[5] + c[13])) + ((c[3] + c[11]) + (c[7] + c[15])));
+  };
+  double cs[16], ds[16];
+#pragma unroll
+  for (int k = 0; k < 16; k += 2) {
+    const double2 w = *reinterpret_cast<const double2*>(my + k);
+    const double2 v = *reinterpret_cast<const double2*>(my + 16 + k);
+    cs[k] = w.x;
+    cs[k + 1] = w.y;
+    ds[k] = v.x;
+    ds[k + 1] = v.y;
+  }
+  Cand16 out;
+  out.cost = tree16(cs);
+  out.du2 = tree16(ds);
+  const uint64_t bad = __ballot(!eo);
+  out.eo = ((bad | (bad >> 16) | (bad >> 32) | (bad >> 48)) & (1ull << tt)) == 0;
+  wave_lds_fence();  // the tree's reads before the next pass writes the exchange rows
+  // the loads of the clamped steps past the horizon are still in flight: drain them (and
+  // the result stores) before the next pass's prologue reuses the slots
+  __builtin_amdgcn_s_waitcnt((0) | (7 << 4) | (0 << 8));
+  asm volatile("" ::: "memory");
+  return out;
+}
+
+// ---------------------------------------------------------------------------
 // The same forward pass on the 4-block f64 MFMA (round 2, ILQR_SCHED_FORWARD_MFMA):
 // the backward's layout — lane 16ρ + 4β + κ holds element [ρ][κ] of trajectory slot β's
 // 4×4 block, fm4(a, b, c) = c + aᵀb, vectors "replicated" (v[4I+ρ] in every κ). Per
@@ -984,16 +1301,25 @@ __device__ void coop_finalize(const LQParams& P, int b, int B, int T, const Iter
   }
 }
 
-// Grab trials j0 .. j0+3 of trajectory b, evaluate them, and finalise b if these were
+// Trials handed out per grab: 16 (lq_cand16_pass, round 6) or 4 (lq_forward_wave_ring's
+// candidate pass, rounds 3-5; built for A/B). Both evaluate every trial bit for bit as the
+// sequential search does.
+#ifndef ILQR_COOP_WIDTH
+#define ILQR_COOP_WIDTH 16
+#endif
+static_assert(ILQR_COOP_WIDTH == 4 || ILQR_COOP_WIDTH == 16, "a grab is four or sixteen trials");
+
+// Grab trials j0 .. j0+W−1 of trajectory b, evaluate them, and finalise b if these were
 // the last needed (whole wave).
 template <int NX, int NU>
 __device__ int coop_evaluate(const LQParams& P, int b, int B, int T, const IterArgs& a, const LSCoop& c,
                               const LSParams& ls, double* ring) {
+  constexpr int W = ILQR_COOP_WIDTH;
   LSCoopRec* R = c.rec + b;
-  const int l = threadIdx.x & 63, g = l >> 4;
+  const int l = threadIdx.x & 63;
   int j0 = 0, lim0 = 0, sl = 0;
   if (l == 0) {
-    j0 = __hip_atomic_fetch_add(&R->next, 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    j0 = __hip_atomic_fetch_add(&R->next, W, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     lim0 = coop_lim(R, ls.max_trials);
     sl = ag_rmw_ld(&R->slot);  // picks the scratch rows: a decision, so read coherently
   }
@@ -1002,28 +1328,60 @@ __device__ int coop_evaluate(const LQParams& P, int b, int B, int T, const IterA
   sl = __builtin_amdgcn_readfirstlane(sl);
   const bool scr = sl < c.nslots;  // every trial's rollout to the scratch
   if (j0 > lim0) return 0;  // raced past the needed set: nothing to do
-  const int j = j0 + g;   // this group's trial
-  const bool mine = j <= lim0;
   // the cost to beat: written before this launch (in place by fit's finaliser of b only,
   // once no trial of b is needed any more)
   const double pc = a.prev_cost ? a.prev_cost[b] : INFINITY;
-  double du2 = 0.0;
-  CandPass cp{trial_alpha(ls, j), j0 == 2 ? 0 : -1};
-  if (scr) {
-    cp.sx = c.sx;
-    cp.su = c.su;
-    cp.sidx = sl * COOP_MAX_TRIALS + j0 - 1;
-    cp.sx_bytes = (uint32_t)(c.nslots * COOP_MAX_TRIALS * (T + 1) * NX * 8);
-    cp.su_bytes = (uint32_t)(c.nslots * COOP_MAX_TRIALS * T * NU * 8);
+  double du2 = 0.0, cost;
+  bool eo;
+  int j;
+  bool mine;
+  if constexpr (W == 16) {
+    const int tt = l & 15;  // this lane's trial
+    j = j0 + tt;
+    mine = j <= lim0;
+    // trial 2's rollout into x_new / u_new as it runs (no scratch), else every trial's
+    // into its scratch row
+    const auto rXN =
+        scr ? buffer_rsrc(uniform_ptr(c.sx),
+                          (uint32_t)__builtin_amdgcn_readfirstlane(c.nslots * COOP_MAX_TRIALS * (T + 1) * NX * 8))
+            : buffer_rsrc(uniform_ptr(a.xnew + (size_t)b * (T + 1) * NX),
+                          (uint32_t)__builtin_amdgcn_readfirstlane((T + 1) * NX * 8));
+    const auto rUN =
+        scr ? buffer_rsrc(uniform_ptr(c.su),
+                          (uint32_t)__builtin_amdgcn_readfirstlane(c.nslots * COOP_MAX_TRIALS * T * NU * 8))
+            : buffer_rsrc(uniform_ptr(a.unew + (size_t)b * T * NU), (uint32_t)__builtin_amdgcn_readfirstlane(T * NU * 8));
+    const bool st = mine && (scr || (j0 == 2 && tt == 0));
+    const int gs = scr ? sl * COOP_MAX_TRIALS + j - 1 : 0;
+    const Cand16 r16 = lq_cand16_pass<PIPE_R, PIPE_PF>(P, b, T, a.x, a.u, a.xtraj, a.d, a.K, trial_alpha(ls, j),
+                                                       st, rXN, rUN, gs, ring);
+    cost = r16.cost;
+    du2 = r16.du2;
+    eo = r16.eo;
+  } else {
+    const int g = l >> 4;  // this group's trial
+    j = j0 + g;
+    mine = j <= lim0;
+    CandPass cp{trial_alpha(ls, j), j0 == 2 ? 0 : -1};
+    if (scr) {
+      cp.sx = c.sx;
+      cp.su = c.su;
+      cp.sidx = sl * COOP_MAX_TRIALS + j0 - 1;
+      cp.sx_bytes = (uint32_t)(c.nslots * COOP_MAX_TRIALS * (T + 1) * NX * 8);
+      cp.su_bytes = (uint32_t)(c.nslots * COOP_MAX_TRIALS * T * NU * 8);
+    }
+    const FwdOut r = lq_forward_wave_ring<NX, NU, PIPE_R, PIPE_PF, true, true>(
+        P, b, B, T, mine, a.x, a.u, a.xtraj, a.d, a.K, pc, a.xnew, a.unew, &du2, ls, ring, cp);
+    cost = r.cost;
+    eo = r.eo;
   }
-  const FwdOut r = lq_forward_wave_ring<NX, NU, PIPE_R, PIPE_PF, true, true>(
-      P, b, B, T, mine, a.x, a.u, a.xtraj, a.d, a.K, pc, a.xnew, a.unew, &du2, ls, ring, cp);
-  if ((l & 15) == 0 && mine) {
-    ag_std(c.cost + (size_t)b * COOP_MAX_TRIALS + j - 1, r.cost);
+  // one lane per trial records it (lanes 0..15 with W = 16; lane 16g with W = 4)
+  const bool rec = W == 16 ? l < 16 : (l & 15) == 0;
+  if (rec && mine) {
+    ag_std(c.cost + (size_t)b * COOP_MAX_TRIALS + j - 1, cost);
     ag_std(c.du2 + (size_t)b * COOP_MAX_TRIALS + j - 1, du2);
-    if (pc - r.cost > 0.0)  // (:77-80); NaN compares false
+    if (pc - cost > 0.0)  // (:77-80); NaN compares false
       __hip_atomic_fetch_min(&R->best, j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else if (r.eo)
+    else if (eo)
       __hip_atomic_fetch_min(&R->stop, j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   // costs and best/stop complete before the mask bits; trial 2's rollout (stored as it
@@ -1035,7 +1393,7 @@ __device__ int coop_evaluate(const LQParams& P, int b, int B, int T, const IterA
   int fin = 0, lim = 0;
   if (l == 0) {
     uint64_t bits = 0;
-    for (int k = 0; k < 4; ++k)
+    for (int k = 0; k < W; ++k)
       if (j0 + k <= lim0) bits |= 1ull << (j0 + k - 1);
     const uint64_t m =
         __hip_atomic_fetch_or(&R->mask, bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) | bits;
@@ -1054,7 +1412,7 @@ __device__ int coop_evaluate(const LQParams& P, int b, int B, int T, const IterA
   fin = __builtin_amdgcn_readfirstlane(fin);
   lim = __builtin_amdgcn_readfirstlane(lim);
   if (fin) coop_finalize<NX, NU>(P, b, B, T, a, c, ls, ring, lim, sl);
-  return fin ? 2 : 1;  // 1: a quad evaluated, the search not finalised here; 2: finalised
+  return fin ? 2 : 1;  // 1: trials evaluated, the search not finalised here; 2: finalised
 }
 
 // The work loop every wave of the launch enters once it is done with its own
@@ -1086,7 +1444,7 @@ __device__ void lq_coop_search(const LQParams& P, int B, int T, const IterArgs& 
 #pragma unroll 1
   for (int q = 0; q < 4; ++q)
     if ((own >> q) & 1u)
-      for (int k = 0; k < COOP_MAX_TRIALS / 4; ++k)
+      for (int k = 0; k < COOP_MAX_TRIALS / ILQR_COOP_WIDTH; ++k)
         if (coop_evaluate<NX, NU>(P, b0 + q, B, T, a, c, ls, ring) != 1) break;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   // 200 µs at the 100 MHz real-time counter; the Makefile's `variants` target builds a

@@ -29,7 +29,11 @@
 # New API: `solve!(::iLQRProblem)` (batched LQ, one or several GPUs), the resident
 # single-GPU `Solver` (set_problem! / fit! / backward! / forward! / solve!, close: one
 # workspace reused by every call — fit / backward_pass / forward_pass run on a cached one),
-# the resident multi-GPU `MultiSolver`, and `chain_fit` (the RBD family of BASELINE config 5).
+# the resident multi-GPU `MultiSolver`, `chain_fit` (the RBD family of BASELINE config 5) and
+# the floating-base family of the reference's RBD script: `FloatingDynamics` /
+# `FloatingCost` / `FloatingFinalCost` (floating_closures(model)), which fit /
+# backward_pass / forward_pass / linearize_dynamics dispatch to ilqr_floating_* on a cached
+# FloatingSolver, and `floating_fit` (batched).
 module iLQRHIP
 
 using ForwardDiff: gradient, jacobian, hessian   # as the reference (src/iLQR.jl:3)
@@ -233,7 +237,8 @@ rowmajor3(A::AbstractArray{<:Real,3}) = Array{Float64}(permutedims(A, (2, 1, 3))
 # -- problem families -----------------------------------------------------------------
 const LQTriple = Tuple{LinearDynamics,QuadraticCost,QuadraticFinalCost}
 const TwoLinkTriple = Tuple{TwoLinkDynamics,TwoLinkCost,TwoLinkFinalCost}
-family(f, l, lf) = (f, l, lf) isa LQTriple ? :lq : (f, l, lf) isa TwoLinkTriple ? :two_link : :tiles
+family(f, l, lf) = (f, l, lf) isa LQTriple ? :lq : (f, l, lf) isa TwoLinkTriple ? :two_link :
+                   is_floating(f, l, lf) ? :floating : :tiles
 
 function problem(h::Handle, f::LinearDynamics, l::QuadraticCost, lf::QuadraticFinalCost)
     return Problem(ILQR_PROBLEM_LQ, 0, upload(h, rowmajor(f.A)), upload(h, rowmajor(f.B)),
@@ -291,8 +296,9 @@ end
 function backward_pass(x::AbstractMatrix, u::AbstractMatrix, dynamicsf, immediate_cost, final_cost)
     N, nx = size(x); M, nu = size(u)
     @assert(N == M + 1)                                                 # backward_pass.jl:329
-    family(dynamicsf, immediate_cost, final_cost) == :tiles &&
-        return backward_tiles_device(x, u, dynamicsf, immediate_cost, final_cost)
+    fam = family(dynamicsf, immediate_cost, final_cost)
+    fam == :tiles && return backward_tiles_device(x, u, dynamicsf, immediate_cost, final_cost)
+    fam == :floating && return floating_backward(dynamicsf, x, u)
     # the resident solver of this shape (no allocation per call): δu (T × nu), K (T × nu × nx) like 𝐊s
     return with_cached(SOLVER_CACHE, () -> Solver(nx, nu, M, 1), (nx, nu, M)) do s
         backward!(set_problem!(s, dynamicsf, immediate_cost, final_cost), x, u)
@@ -336,8 +342,9 @@ function forward_pass(x::AbstractMatrix, u::AbstractMatrix, x_traj::AbstractMatr
                       K::AbstractArray{<:Real,3}, prev_cost::Real, dynamicsf, immediate_cost, final_cost)
     N, nx = size(x); M, nu = size(u)
     @assert(N == M + 1)                                                 # forward_pass.jl:62
-    family(dynamicsf, immediate_cost, final_cost) == :tiles &&
-        return forward_host(x, u, x_traj, δu, K, prev_cost, dynamicsf, immediate_cost, final_cost)
+    fam = family(dynamicsf, immediate_cost, final_cost)
+    fam == :tiles && return forward_host(x, u, x_traj, δu, K, prev_cost, dynamicsf, immediate_cost, final_cost)
+    fam == :floating && return floating_forward(dynamicsf, x, u, x_traj, δu, K, prev_cost)
     return with_cached(SOLVER_CACHE, () -> Solver(nx, nu, M, 1), (nx, nu, M)) do s
         forward!(set_problem!(s, dynamicsf, immediate_cost, final_cost), x, u, x_traj, δu, K, prev_cost)
     end
@@ -359,8 +366,10 @@ function fit(x_init::AbstractMatrix, u_init::AbstractMatrix, dynamicsf, immediat
              x_traj=zero(x_init), max_iter::Int64=100, tol::Float64=1e-6, verbose::Bool=false)
     N, nx = size(x_init); M, nu = size(u_init)
     @assert(N == M + 1, "size(x_init)[2] == size(u_init)[1]")          # forward_pass.jl:156
-    family(dynamicsf, immediate_cost, final_cost) == :tiles &&
+    fam = family(dynamicsf, immediate_cost, final_cost)
+    fam == :tiles &&
         return fit_tiles(x_init, u_init, dynamicsf, immediate_cost, final_cost, x_traj, max_iter, tol, verbose)
+    fam == :floating && return floating_fit1(dynamicsf, x_init, u_init, x_traj, max_iter, tol, verbose)
     # the resident solver of this shape: an MPC loop calling fit allocates nothing per call;
     # an exhausted line search returns the last iterate (fit_resident!)
     return with_cached(SOLVER_CACHE, () -> Solver(nx, nu, M, 1), (nx, nu, M)) do s
@@ -701,7 +710,7 @@ function evict_idle!(cache::Dict)
         # this task already holds, the lock being reentrant)
         if !islocked(c.lock) && trylock(c.lock)
             try
-                close(c.h)
+                close(c)
             finally
                 unlock(c.lock)
             end
@@ -739,6 +748,8 @@ function clear_cache!()
     lock(CACHE_LOCK) do
         foreach(close, values(SOLVER_CACHE)); empty!(SOLVER_CACHE)
         foreach(close, values(TILES_CACHE)); empty!(TILES_CACHE)
+        foreach(close, values(FLOATING_CACHE)); empty!(FLOATING_CACHE)
+        foreach(close, values(CHAIN_CACHE)); empty!(CHAIN_CACHE)
     end
     return nothing
 end
@@ -756,6 +767,7 @@ end
 function linearize_dynamics(x::AbstractMatrix, u::AbstractMatrix, f)
     M, nu = size(u); nx = size(x, 2)
     size(x, 1) in (M, M + 1) || throw(AssertionError("x has $(size(x, 1)) rows for $M inputs"))
+    f isa FloatingDynamics && return floating_linearize(f, x, u)
     fam = f isa LinearDynamics ? :lq : f isa TwoLinkDynamics ? :two_link : :host
     if fam == :host                                                     # ForwardDiff, :32-33
         As = zeros(M, nx, nx); Bs = zeros(M, nx, nu)
@@ -848,6 +860,55 @@ end
 simple_costs(body, point, final_target, weight; euclidean::Bool=false) =
     SimpleCosts(Int32(body), Tuple(Float64.(point)), Tuple(Float64.(final_target)), Float64(weight), euclidean)
 
+"""ChainSolver: one ilqr_chain handle (precision, linearisation, evaluator and costs set at
+creation) plus its device buffers — the iterate, the results, the status — allocated once
+per (chain, T, batch, element type, linearization, dynamics, costs) and reused by every
+chain_fit of that key (CHAIN_CACHE; include/ilqr.h: "hot calls never allocate")."""
+mutable struct ChainSolver
+    ch::Ptr{Cvoid}           # ilqr_chain_handle
+    h::Handle                # device-memory helper (ilqr_malloc / memcpy), closed with it
+    x::Ptr{Cvoid}; u::Ptr{Cvoid}; xo::Ptr{Cvoid}; uo::Ptr{Cvoid}; status::Ptr{Int32}
+    lock::ReentrantLock
+end
+
+function ChainSolver(c::Chain, nx::Integer, nu::Integer, T::Integer, nb::Integer, ::Type{E}, linearization,
+                     dynamics, costs::Union{Nothing,SimpleCosts}; device::Integer=0) where {E<:Union{Float32,Float64}}
+    r = Ref{Ptr{Cvoid}}(C_NULL)
+    dt = E === Float32 ? ILQR_F32 : ILQR_F64
+    check(ccall((:ilqr_chain_create, libilqr), Cint,
+                (Ref{Ptr{Cvoid}}, Cint, Ref{Chain}, Cint, Cint, Int32, Int32),
+                r, device, c, T, nb, dt, linearization), "ilqr_chain_create")
+    destroy() = ccall((:ilqr_chain_destroy, libilqr), Cint, (Ptr{Cvoid},), r[])
+    try
+        check(ccall((:ilqr_chain_set_dynamics, libilqr), Cint, (Ptr{Cvoid}, Int32), r[], dynamics),
+              "ilqr_chain_set_dynamics")
+        if costs !== nothing
+            mode = costs.euclidean ? ILQR_CHAIN_COST_SIMPLE_EUCLIDEAN : ILQR_CHAIN_COST_SIMPLE
+            check(ccall((:ilqr_chain_set_simple_costs, libilqr), Cint,
+                        (Ptr{Cvoid}, Int32, Int32, Ptr{Float64}, Ptr{Float64}, Float64),
+                        r[], mode, costs.body, collect(costs.point), collect(costs.final_target), costs.weight),
+                  "ilqr_chain_set_simple_costs")
+        end
+    catch
+        destroy(); rethrow()
+    end
+    h = Handle(nx, nu, T, 1; device=device)  # device-memory helper only
+    a(n) = Ptr{Cvoid}(alloc(h, E, n))
+    s = ChainSolver(r[], h, a(nb * (T + 1) * nx), a(nb * T * nu), a(nb * (T + 1) * nx), a(nb * T * nu),
+                    alloc(h, Int32, nb), ReentrantLock())
+    finalizer(destroy!, s)      # a backstop; close(s) frees everything at once
+    return s
+end
+
+function destroy!(s::ChainSolver)
+    s.ch != C_NULL && (ccall((:ilqr_chain_destroy, libilqr), Cint, (Ptr{Cvoid},), s.ch); s.ch = C_NULL)
+    close(s.h)
+    return nothing
+end
+Base.close(s::ChainSolver) = lock(() -> destroy!(s), s.lock)
+
+const CHAIN_CACHE = Dict{Tuple{Chain,Int,Int,DataType,Int32,Int32,Union{Nothing,SimpleCosts}},ChainSolver}()
+
 """chain_fit(chain, x_init, u_init; max_iter, tol, linearization, dynamics) → (x̄, ū, status)
 
 Batched fit of the chain family; x_init (nx, T+1, batch), u_init (nu, T, batch) as
@@ -855,40 +916,27 @@ Array{Float32,3} (fp32, BASELINE config 5) or Array{Float64,3}: the element type
 the device precision, as the reference's generic Julia code would. `dynamics` picks the
 2-joint evaluator (AUTO: the closed form sampled from the Newton-Euler recursion at
 creation; RNEA: the recursion itself). `costs = simple_costs(…)` replaces the chain's
-joint-space costs with cost_functions.jl's pair (2-joint chains, closed form)."""
+joint-space costs with cost_functions.jl's pair (2-joint chains, closed form). The handle
+and buffers are cached per (chain, T, batch, element type, options): an MPC loop calling
+chain_fit allocates nothing per call (clear_cache!() closes them)."""
 function chain_fit(c::Chain, x_init::Array{E,3}, u_init::Array{E,3}; max_iter::Int64=100,
                    tol::Float64=1e-6, linearization=ILQR_LINEARIZE_DUAL,
                    dynamics=ILQR_CHAIN_DYN_AUTO,
                    costs::Union{Nothing,SimpleCosts}=nothing) where {E<:Union{Float32,Float64}}
     nx, N, nb = size(x_init); nu = size(u_init, 1); M = N - 1
     @assert(size(u_init, 2) == M)
-    r = Ref{Ptr{Cvoid}}(C_NULL)
-    dt = E === Float32 ? ILQR_F32 : ILQR_F64
-    check(ccall((:ilqr_chain_create, libilqr), Cint,
-                (Ref{Ptr{Cvoid}}, Cint, Ref{Chain}, Cint, Cint, Int32, Int32),
-                r, 0, c, M, nb, dt, linearization), "ilqr_chain_create")
-    check(ccall((:ilqr_chain_set_dynamics, libilqr), Cint, (Ptr{Cvoid}, Int32), r[], dynamics),
-          "ilqr_chain_set_dynamics")
-    if costs !== nothing
-        mode = costs.euclidean ? ILQR_CHAIN_COST_SIMPLE_EUCLIDEAN : ILQR_CHAIN_COST_SIMPLE
-        pt = collect(costs.point); tg = collect(costs.final_target)
-        check(ccall((:ilqr_chain_set_simple_costs, libilqr), Cint,
-                    (Ptr{Cvoid}, Int32, Int32, Ptr{Float64}, Ptr{Float64}, Float64),
-                    r[], mode, costs.body, pt, tg, costs.weight), "ilqr_chain_set_simple_costs")
+    key = (c, M, nb, E, Int32(linearization), Int32(dynamics), costs)
+    return with_cached(CHAIN_CACHE, () -> ChainSolver(c, nx, nu, M, nb, E, linearization, dynamics, costs), key) do s
+        upload!(s.h, s.x, x_init); upload!(s.h, s.u, u_init)
+        o = default_options(); o.max_iter = max_iter; o.tol = tol
+        st = ccall((:ilqr_chain_fit, libilqr), Cint,
+                   (Ptr{Cvoid}, Ref{Options}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid},
+                    Ptr{Int32}, Ptr{Int32}),
+                   s.ch, o, s.x, s.u, C_NULL, s.xo, s.uo, C_NULL, C_NULL, s.status)
+        st == ILQR_ERR_LS_EXHAUSTED || check(st, "ilqr_chain_fit")
+        (download!(s.h, similar(x_init), s.xo), download!(s.h, similar(u_init), s.uo),
+         download!(s.h, zeros(Int32, nb), s.status))
     end
-    h = Handle(nx, nu, M, 1)                 # device-memory helper only
-    xi = upload(h, x_init); ui = upload(h, u_init)
-    xo = alloc(h, E, length(x_init)); uo = alloc(h, E, length(u_init)); sd = alloc(h, Int32, nb)
-    o = default_options(); o.max_iter = max_iter; o.tol = tol
-    st = ccall((:ilqr_chain_fit, libilqr), Cint,
-               (Ptr{Cvoid}, Ref{Options}, Ptr{E}, Ptr{E}, Ptr{E}, Ptr{E}, Ptr{E}, Ptr{E}, Ptr{Int32}, Ptr{Int32}),
-               r[], o, xi, ui, C_NULL, xo, uo, C_NULL, C_NULL, sd)
-    st == ILQR_ERR_LS_EXHAUSTED || check(st, "ilqr_chain_fit")
-    x = download!(h, similar(x_init), xo); u = download!(h, similar(u_init), uo)
-    status = download!(h, zeros(Int32, nb), sd)
-    ccall((:ilqr_chain_destroy, libilqr), Cint, (Ptr{Cvoid},), r[])
-    close(h)
-    return x, u, status
 end
 
 # -- floating-base RBD family: the reference's RBD script as it runs --------------------
@@ -917,32 +965,186 @@ function rbd_2dof_arm_floating(; target=(0., 0., 0., 5., 1., 2., 1., .3))
                   (100., 100., 100., 1000., 1000., 1000., 10., 10.), 10.0, 1.0, 100000.0)
 end
 
+"""FloatingSolver(model, T, batch): one ilqr_floating handle and every device buffer its
+calls need — the iterate, x_traj, the results, the gains, the costs and statuses (the
+linearisation outputs and the verbose history on first use) — allocated once per
+(model, T, batch) and reused (FLOATING_CACHE). fit / backward_pass / forward_pass /
+linearize_dynamics with the FloatingDynamics / FloatingCost / FloatingFinalCost callables,
+and floating_fit, run on a cached one."""
+mutable struct FloatingSolver
+    fh::Ptr{Cvoid}           # ilqr_floating_handle
+    h::Handle                # device-memory helper (ilqr_malloc / memcpy), closed with it
+    nx::Int; nu::Int; M::Int; nb::Int
+    x::Ptr{Float64}; u::Ptr{Float64}; xt::Ptr{Float64}; xo::Ptr{Float64}; uo::Ptr{Float64}
+    d::Ptr{Float64}; K::Ptr{Float64}; pc::Ptr{Float64}; cost::Ptr{Float64}
+    iters::Ptr{Int32}; status::Ptr{Int32}; trials::Ptr{Int32}
+    lA::Ptr{Float64}; lB::Ptr{Float64}       # linearize_dynamics' outputs, on first use
+    hc::Ptr{Float64}; ht::Ptr{Int32}; hcap::Int
+    lock::ReentrantLock
+end
+
+function FloatingSolver(m::FloatingModel, T::Integer, batch::Integer; device::Integer=0)
+    r = Ref{Ptr{Cvoid}}(C_NULL)
+    check(ccall((:ilqr_floating_create, libilqr), Cint, (Ref{Ptr{Cvoid}}, Cint, Ref{FloatingModel}, Cint, Cint),
+                r, device, m, T, batch), "ilqr_floating_create")
+    nu = 6 + Int(m.n_joints); nx = 2 * nu; N = T + 1
+    h = Handle(nx, nu, T, 1; device=device)  # device-memory helper only
+    f(n) = alloc(h, Float64, batch * n)
+    i(n) = alloc(h, Int32, batch * n)
+    s = FloatingSolver(r[], h, nx, nu, T, batch,
+                       f(N * nx), f(T * nu), f(N * nx), f(N * nx), f(T * nu),      # x u x_traj x̄ ū
+                       f(T * nu), f(T * nu * nx), f(1), f(1),                      # δu K prev_cost cost
+                       i(1), i(1), i(1),                                           # iters status trials
+                       Ptr{Float64}(C_NULL), Ptr{Float64}(C_NULL), Ptr{Float64}(C_NULL), Ptr{Int32}(C_NULL), 0,
+                       ReentrantLock())
+    finalizer(destroy!, s)      # a backstop; close(s) frees everything at once
+    return s
+end
+
+function destroy!(s::FloatingSolver)
+    s.fh != C_NULL && (ccall((:ilqr_floating_destroy, libilqr), Cint, (Ptr{Cvoid},), s.fh); s.fh = C_NULL)
+    close(s.h)
+    return nothing
+end
+Base.close(s::FloatingSolver) = lock(() -> destroy!(s), s.lock)
+
+const FLOATING_CACHE = Dict{Tuple{FloatingModel,Int,Int},FloatingSolver}()
+floating_cached(f, m::FloatingModel, M::Integer, nb::Integer) =
+    with_cached(f, FLOATING_CACHE, () -> FloatingSolver(m, M, nb), (m, Int(M), Int(nb)))
+
+# -- the script's closures as callable structs (RBD_helper_functions.jl:48-116) -------------
+# fit / backward_pass / forward_pass / linearize_dynamics recognise the triple (family
+# :floating) and run ilqr_floating_* on a cached FloatingSolver; called directly they are
+# the script's functions: dynamicsf one device RK4 step (a cached T = 1 workspace: the
+# script calls it 1000 times to build state_traj, animate_RBD_2_link.jl:23-25), the costs
+# plain Julia arithmetic (generic, as ForwardDiff needs them).
+struct FloatingDynamics; model::FloatingModel; end
+struct FloatingCost; model::FloatingModel; end
+struct FloatingFinalCost; model::FloatingModel; end
+floating_closures(m::FloatingModel=rbd_2dof_arm_floating()) = (FloatingDynamics(m), FloatingCost(m), FloatingFinalCost(m))
+is_floating(f, l, lf) = f isa FloatingDynamics && l isa FloatingCost && lf isa FloatingFinalCost &&
+                        f.model == l.model == lf.model
+
+function (f::FloatingDynamics)(x::AbstractVector, u::AbstractVector)            # dynamicsf (:48-79)
+    return floating_cached(f.model, 1, 1) do s
+        upload!(s.h, s.x, Vector{Float64}(x)); upload!(s.h, s.u, Vector{Float64}(u))
+        check(ccall((:ilqr_floating_dynamics, libilqr), Cint,
+                    (Ptr{Cvoid}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Cint), s.fh, s.x, s.u, s.xo, 1),
+              "ilqr_floating_dynamics")
+        download!(s.h, zeros(s.nx), s.xo)
+    end
+end
+function (l::FloatingCost)(x, u)                                                  # immediate_cost (:85-101)
+    m = l.model; q = 6 + Int(m.n_joints)
+    δx = [m.target[i] - x[i] for i in 1:q]
+    return sum(δx[i] * m.q_weight[i] * δx[i] for i in 1:q) * m.q_scale +
+           sum(u[j] * m.r_weight[j] * u[j] for j in 1:q) * m.r_scale
+end
+function (l::FloatingFinalCost)(x)                                                # final_cost (:107-116)
+    m = l.model; q = 6 + Int(m.n_joints)
+    δx = [m.target[i] - x[i] for i in 1:q]
+    return sum(δx[i] * m.qf_weight[i] * δx[i] for i in 1:q) * m.qf_scale
+end
+
+function floating_shape(s::FloatingSolver, nx, nu)
+    (nx, nu) == (s.nx, s.nu) || throw(AssertionError("the floating model is ($(s.nx), $(s.nu)), x/u are ($nx, $nu)"))
+end
+
+# iLQR.fit (forward_pass.jl:148-179) of one trajectory (reference layout) on the device
+function floating_fit1(f::FloatingDynamics, x_init, u_init, x_traj, max_iter, tol, verbose)
+    N, nx = size(x_init); M, nu = size(u_init)
+    return floating_cached(f.model, M, 1) do s
+        floating_shape(s, nx, nu)
+        upload!(s.h, s.x, to_abi(x_init)); upload!(s.h, s.u, to_abi(u_init)); upload!(s.h, s.xt, to_abi(x_traj))
+        o = default_options(); o.max_iter = max_iter; o.tol = tol
+        n = max(max_iter, 1)
+        if verbose && s.hcap < n
+            s.hc != C_NULL && (release!(s.h, s.hc); release!(s.h, s.ht))
+            s.hc = alloc(s.h, Float64, n); s.ht = alloc(s.h, Int32, n); s.hcap = n
+        end
+        verbose && upload!(s.h, s.ht, zeros(Int32, n))
+        hist = verbose ? Ref(History(s.hc, s.ht, C_NULL, C_NULL)) : Ref(History(C_NULL, C_NULL, C_NULL, C_NULL))
+        st = ccall((:ilqr_floating_fit_ex, libilqr), Cint,
+                   (Ptr{Cvoid}, Ref{Options}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64},
+                    Ptr{Float64}, Ptr{Int32}, Ptr{Int32}, Ref{History}),
+                   s.fh, o, s.x, s.u, s.xt, s.xo, s.uo, s.cost, s.iters, s.status, hist)
+        st in (ILQR_OK, ILQR_ERR_LS_EXHAUSTED) || check(st, "ilqr_floating_fit")
+        verbose && print_history(download!(s.h, zeros(n), s.hc), download!(s.h, zeros(Int32, n), s.ht))
+        (from_abi(download!(s.h, zeros(nx, N), s.xo)), from_abi(download!(s.h, zeros(nu, M), s.uo)))
+    end
+end
+
+# iLQR.backward_pass (backward_pass.jl:324-357) → (δu::T×nu, K::T×nu×nx)
+function floating_backward(f::FloatingDynamics, x, u)
+    N, nx = size(x); M, nu = size(u)
+    return floating_cached(f.model, M, 1) do s
+        floating_shape(s, nx, nu)
+        upload!(s.h, s.x, to_abi(x)); upload!(s.h, s.u, to_abi(u))
+        check(ccall((:ilqr_floating_backward, libilqr), Cint,
+                    (Ptr{Cvoid}, Ref{Options}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Int32}),
+                    s.fh, default_options(), s.x, s.u, s.d, s.K, s.status), "ilqr_floating_backward")
+        (from_abi(download!(s.h, zeros(nu, M), s.d)), gains_from_abi(download!(s.h, zeros(nx, nu, M), s.K)))
+    end
+end
+
+# iLQR.forward_pass (forward_pass.jl:55-93) → (x̄, ū, new_cost)
+function floating_forward(f::FloatingDynamics, x, u, x_traj, δu, K, prev_cost)
+    N, nx = size(x); M, nu = size(u)
+    return floating_cached(f.model, M, 1) do s
+        floating_shape(s, nx, nu)
+        upload!(s.h, s.x, to_abi(x)); upload!(s.h, s.u, to_abi(u)); upload!(s.h, s.xt, to_abi(x_traj))
+        upload!(s.h, s.d, to_abi(δu)); upload!(s.h, s.K, gains_to_abi(K)); upload!(s.h, s.pc, Float64[prev_cost])
+        check(ccall((:ilqr_floating_forward, libilqr), Cint,
+                    (Ptr{Cvoid}, Ref{Options}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64},
+                     Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Int32}, Ptr{Int32}),
+                    s.fh, default_options(), s.x, s.u, s.xt, s.d, s.K, s.pc, s.xo, s.uo, s.cost, s.trials, s.status),
+              "ilqr_floating_forward")
+        (from_abi(download!(s.h, zeros(nx, N), s.xo)), from_abi(download!(s.h, zeros(nu, M), s.uo)),
+         download!(s.h, zeros(1), s.cost)[1])
+    end
+end
+
+# linearize_dynamics (backward_pass.jl:25-40) at every step: the dual-number kernel
+function floating_linearize(f::FloatingDynamics, x::AbstractMatrix, u::AbstractMatrix)
+    M, nu = size(u); nx = size(x, 2)
+    size(x, 1) in (M, M + 1) || throw(AssertionError("x has $(size(x, 1)) rows for $M inputs"))
+    xa = size(x, 1) == M ? vcat(x, x[end:end, :]) : x                   # the ABI reads T+1 states
+    return floating_cached(f.model, M, 1) do s
+        floating_shape(s, nx, nu)
+        if s.lA == C_NULL
+            s.lA = alloc(s.h, Float64, s.M * s.nx * s.nx); s.lB = alloc(s.h, Float64, s.M * s.nx * s.nu)
+        end
+        upload!(s.h, s.x, to_abi(xa)); upload!(s.h, s.u, to_abi(u))
+        check(ccall((:ilqr_floating_linearize, libilqr), Cint,
+                    (Ptr{Cvoid}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}),
+                    s.fh, s.x, s.u, s.lA, s.lB), "ilqr_floating_linearize")
+        (permutedims(download!(s.h, zeros(nx, nx, M), s.lA), (3, 2, 1)),
+         permutedims(download!(s.h, zeros(nu, nx, M), s.lB), (3, 2, 1)))
+    end
+end
+
 """floating_fit(model, x_init, u_init; max_iter, tol) → (x̄, ū, status)
 
 iLQR.fit of the floating-base family on the device (include/ilqr.h ilqr_floating_fit):
 x_init (16, T+1, batch) = [MRP; r; θ; ω; v; θ̇], u_init (8, T, batch), as the script's
-`state_traj` / `input_traj` transposed (animate_RBD_2_link.jl:19-25)."""
+`state_traj` / `input_traj` transposed (animate_RBD_2_link.jl:19-25); on the cached
+FloatingSolver of (model, T, batch)."""
 function floating_fit(m::FloatingModel, x_init::Array{Float64,3}, u_init::Array{Float64,3};
                       max_iter::Int64=100, tol::Float64=1e-6)
     nx, N, nb = size(x_init); nu = size(u_init, 1); M = N - 1
     @assert(size(u_init, 2) == M)
-    r = Ref{Ptr{Cvoid}}(C_NULL)
-    check(ccall((:ilqr_floating_create, libilqr), Cint, (Ref{Ptr{Cvoid}}, Cint, Ref{FloatingModel}, Cint, Cint),
-                r, 0, m, M, nb), "ilqr_floating_create")
-    h = Handle(nx, nu, M, 1)                 # device-memory helper only
-    xi = upload(h, x_init); ui = upload(h, u_init)
-    xo = alloc(h, Float64, length(x_init)); uo = alloc(h, Float64, length(u_init)); sd = alloc(h, Int32, nb)
-    o = default_options(); o.max_iter = max_iter; o.tol = tol
-    st = ccall((:ilqr_floating_fit, libilqr), Cint,
-               (Ptr{Cvoid}, Ref{Options}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64},
-                Ptr{Float64}, Ptr{Int32}, Ptr{Int32}),
-               r[], o, xi, ui, C_NULL, xo, uo, C_NULL, C_NULL, sd)
-    st == ILQR_ERR_LS_EXHAUSTED || check(st, "ilqr_floating_fit")
-    x = download!(h, similar(x_init), xo); u = download!(h, similar(u_init), uo)
-    status = download!(h, zeros(Int32, nb), sd)
-    ccall((:ilqr_floating_destroy, libilqr), Cint, (Ptr{Cvoid},), r[])
-    close(h)
-    return x, u, status
+    return floating_cached(m, M, nb) do s
+        floating_shape(s, nx, nu)
+        upload!(s.h, s.x, x_init); upload!(s.h, s.u, u_init)
+        o = default_options(); o.max_iter = max_iter; o.tol = tol
+        st = ccall((:ilqr_floating_fit, libilqr), Cint,
+                   (Ptr{Cvoid}, Ref{Options}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64},
+                    Ptr{Float64}, Ptr{Int32}, Ptr{Int32}),
+                   s.fh, o, s.x, s.u, C_NULL, s.xo, s.uo, C_NULL, C_NULL, s.status)
+        st == ILQR_ERR_LS_EXHAUSTED || check(st, "ilqr_floating_fit")
+        (download!(s.h, similar(x_init), s.xo), download!(s.h, similar(u_init), s.uo),
+         download!(s.h, zeros(Int32, nb), s.status))
+    end
 end
 
 end # module

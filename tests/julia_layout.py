@@ -88,7 +88,7 @@ def derivative_tiles(x, u, f, l, lf):
 # -- iLQRHIP.jl: the floating-base model ----------------------------------------------
 
 def rbd_2dof_arm_floating(target=(0., 0., 0., 5., 1., 2., 1., .3)):
-    """The shim's rbd_2dof_arm_floating() (ilqr.jl_amd/julia/iLQRHIP.jl:910-918), field
+    """The shim's rbd_2dof_arm_floating() (ilqr.jl_amd/julia/iLQRHIP.jl:958-966), field
     for field, as the ctypes struct ccall would pass by Ref."""
     I3 = (1., 0., 0., 0., 1., 0., 0., 0., 1.)
     vals = [2, 0.01, (0., 0., 0.), 30.0, (0., 0., 0.), tuple(50.0 * v for v in I3),

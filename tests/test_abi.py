@@ -131,4 +131,19 @@ def test_julia_shim_exposes_reference_api():
     assert "Handle(" not in body("backward_tiles_device")
     assert "with_cached(TILES_CACHE" in body("backward_tiles_device")
     # every cached workspace carries the lock with_cached holds for a call
-    assert src.count("ReentrantLock()") >= 3
+    assert src.count("ReentrantLock()") >= 5
+    # the floating-base family (the reference's RBD script) and the chain family: their
+    # entry points run on cached workspaces too (floating_fit / chain_fit
+    # created and destroyed a handle per call); the reference API reaches the floating
+    # kernels through its recognised callables
+    for name in ("floating_fit1", "floating_backward", "floating_forward", "floating_linearize", "floating_fit"):
+        assert "Handle(" not in body(name) and "ilqr_floating_create" not in body(name), name
+        assert "floating_cached(" in body(name), name
+    assert "Handle(" not in body("chain_fit") and "ilqr_chain_create" not in body("chain_fit")
+    assert "with_cached(CHAIN_CACHE" in body("chain_fit")
+    assert "floating_cached(" in src[src.index("function (f::FloatingDynamics)"):]
+    for name, call in (("fit", "floating_fit1("), ("backward_pass", "floating_backward("),
+                       ("forward_pass", "floating_forward(")):
+        assert "fam == :floating" in body(name) and call in body(name), name
+    assert "is_floating(f, l, lf) ? :floating" in src
+    assert "FLOATING_CACHE" in body("clear_cache!") and "CHAIN_CACHE" in body("clear_cache!")

@@ -25,7 +25,8 @@ GOLD = os.path.join(os.path.dirname(__file__), "golden")
 
 class CountingLib:
     """The loaded library with a call counter on the allocation entry points."""
-    COUNTED = ("ilqr_create", "ilqr_destroy", "ilqr_malloc", "ilqr_free")
+    COUNTED = ("ilqr_create", "ilqr_destroy", "ilqr_malloc", "ilqr_free", "ilqr_floating_create",
+               "ilqr_floating_destroy")
 
     def __init__(self):
         self.lib = _lib.load()
@@ -147,7 +148,8 @@ def test_resident_solver_100_fits_allocate_nothing(gpu):
     s = ShimSolver(lib, nx, nu, M)
     s.set_problem_lq(A, B, Q, R, Qf)
     after_create = dict(lib.n)
-    assert after_create == {"ilqr_create": 1, "ilqr_destroy": 0, "ilqr_malloc": 17, "ilqr_free": 0}
+    assert after_create == {"ilqr_create": 1, "ilqr_destroy": 0, "ilqr_malloc": 17, "ilqr_free": 0,
+                            "ilqr_floating_create": 0, "ilqr_floating_destroy": 0}
     rng = np.random.default_rng(0)
     counts = []
     for call in range(100):
@@ -280,7 +282,8 @@ def test_tiles_path_20_fits_allocate_nothing_rbd_shape(gpu):
             r = CF.fit(x[None], u0[None], fj, lj, lfj, quad, fquad, max_iter=max_iter, tol=1e-6)
             assert iters == int(r["iters"][0])
             assert rel(xo, r["x"][0]) < 1e-8 and rel(uo, r["u"][0]) < 1e-8
-    assert counts[0] == {"ilqr_create": 1, "ilqr_destroy": 0, "ilqr_malloc": 12, "ilqr_free": 0}
+    assert counts[0] == {"ilqr_create": 1, "ilqr_destroy": 0, "ilqr_malloc": 12, "ilqr_free": 0,
+                         "ilqr_floating_create": 0, "ilqr_floating_destroy": 0}
     assert all(c == counts[0] for c in counts)
     for s in cache.values():
         s.close()
@@ -290,3 +293,93 @@ def test_tiles_path_20_fits_allocate_nothing_rbd_shape(gpu):
 def rel(a, b):
     a, b = np.asarray(a, float), np.asarray(b, float)
     return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-300))
+
+
+# -- the floating-base family: iLQRHIP.fit with FloatingDynamics / FloatingCost /
+# FloatingFinalCost → floating_fit1 on the cached FloatingSolver (floating_cached) --------
+class ShimFloatingSolver:
+    """iLQRHIP.FloatingSolver: ilqr_floating_create, then the helper Handle and its 12
+    buffers in the constructor's order (x u x_traj x̄ ū, δu K prev_cost cost, iters status
+    trials); close = ilqr_floating_destroy + the Handle's close (destroy!)."""
+
+    def __init__(self, lib, model, T, nb):
+        self.lib = lib
+        fh = C.c_void_p()
+        _lib.check(lib.ilqr_floating_create(C.byref(fh), 0, C.byref(model), T, nb), "ilqr_floating_create")
+        self.fh = fh
+        nu = 6 + model.n_joints
+        nx = 2 * nu
+        self.nx, self.nu, self.M, self.nb = nx, nu, T, nb
+        self.hd = h = ShimHandle(lib, nx, nu, T, 1)
+        N = T + 1
+        f = lambda n: h.alloc(np.float64, nb * n)  # noqa: E731
+        i = lambda n: h.alloc(np.int32, nb * n)  # noqa: E731
+        (self.x, self.u, self.xt, self.xo, self.uo) = (f(N * nx), f(T * nu), f(N * nx), f(N * nx), f(T * nu))
+        (self.d, self.K, self.pc, self.cost) = (f(T * nu), f(T * nu * nx), f(1), f(1))
+        (self.iters, self.status, self.trials) = (i(1), i(1), i(1))
+
+    def fit1(self, x_init, u_init, x_traj, max_iter, tol):
+        """iLQRHIP.floating_fit1 (verbose = false): the reference-layout trajectory in, fit."""
+        h = self.hd
+        h.upload_into(self.x, J.to_abi(x_init))
+        h.upload_into(self.u, J.to_abi(u_init))
+        h.upload_into(self.xt, J.to_abi(x_traj))
+        o = _lib.default_options(max_iter=max_iter, tol=tol)
+        rc = self.lib.ilqr_floating_fit_ex(self.fh, C.byref(o), self.x, self.u, self.xt, self.xo, self.uo,
+                                           self.cost, self.iters, self.status,
+                                           C.byref(_lib.History(None, None, None, None)))
+        assert rc in (_lib.OK, _lib.ERR_LS_EXHAUSTED)
+        return (J.from_abi(h.download((self.nx, self.M + 1), self.xo)),
+                J.from_abi(h.download((self.nu, self.M), self.uo)))
+
+    def close(self):
+        if self.fh is not None:
+            self.lib.ilqr_floating_destroy(self.fh)
+            self.fh = None
+        self.hd.close()
+
+
+def test_floating_callables_20_fits_allocate_nothing_rbd_script(gpu):
+    """animate_RBD_2_link.jl:31-32 through the shim: iLQRHIP.fit(state_traj, input_traj,
+    FloatingDynamics(m), FloatingCost(m), FloatingFinalCost(m); …) is family :floating and
+    runs floating_fit1 on the cached FloatingSolver of (model, T = 1000, batch 1). Twenty
+    MPC-style calls create one floating handle and 12 buffers once, and every result is
+    bit-equal to the Python mirror's FloatingSolver.fit (same kernels) on the same start."""
+    import torch
+    from closures import jet_ns, rbd_floating_arm, rbd_initial_state
+    from ilqr_amd.floating import FloatingSolver, rbd_example_problem
+    fj, _, _ = rbd_floating_arm(jet_ns())
+    T = 1000
+    model = J.rbd_2dof_arm_floating()
+    lib = CountingLib()
+    cache = {}
+    ref = FloatingSolver(rbd_example_problem(), T, 1)
+    rng = np.random.default_rng(12)
+    u0 = np.zeros((T, 8))
+    counts = []
+    try:
+        for call in range(20):
+            x0 = rbd_initial_state()
+            x0[8:] = 0.02 * rng.standard_normal(8)
+            x = np.zeros((T + 1, 16))
+            x[0] = x0
+            for t in range(T):
+                x[t + 1] = fj(x[t][None], u0[t][None])[0]
+            key = (bytes(model), T, 1)                       # floating_cached(m, M, 1)
+            s = cache.get(key)
+            if s is None:
+                s = cache[key] = ShimFloatingSolver(lib, model, T, 1)
+            max_iter = 3 if call in (0, 19) else 1
+            xo, uo = s.fit1(x, u0, np.zeros_like(x), max_iter, 1e-6)
+            counts.append(dict(lib.n))
+            r = ref.fit(torch.from_numpy(x[None]).cuda(), torch.from_numpy(u0[None]).cuda(), max_iter=max_iter,
+                        tol=1e-6)
+            assert np.array_equal(xo, r.x[0].cpu().numpy()) and np.array_equal(uo, r.u[0].cpu().numpy()), call
+    finally:
+        ref.close()
+    assert counts[0] == {"ilqr_create": 1, "ilqr_destroy": 0, "ilqr_malloc": 12, "ilqr_free": 0,
+                         "ilqr_floating_create": 1, "ilqr_floating_destroy": 0}
+    assert all(c == counts[0] for c in counts)
+    for s in cache.values():
+        s.close()
+    assert lib.n["ilqr_free"] == 12 and lib.n["ilqr_destroy"] == 1 and lib.n["ilqr_floating_destroy"] == 1
