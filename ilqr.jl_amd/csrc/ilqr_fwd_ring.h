@@ -508,10 +508,11 @@ __device__ Cand16 lq_cand16_pass(const LQParams& P, int b, int T, const double* 
   const int tt = l & 15;  // the trial
 
   // this lane's rows: [A | B] as the row form's Fr (A + 0, 0 + B) and R in registers;
-  // Q in the slots' tail (ring slot 0, doubles [QO, QO + 144): the candidate producer fills
-  // only a slot's first 80 doubles), read per step
-  constexpr int QO = 96;
-  static_assert(QO >= 80 && QO + NX * NX <= RING_SLOT, "Q fits slot 0's tail");
+  // Q in slot 0's tail, doubles [QO, QO + 144), read per step: the candidate producer's
+  // one load per step writes a slot's first 128 doubles (lanes 40..63 repeat the K
+  // chunks of lanes 0..23 into [80, 128)) and nothing past them
+  constexpr int QO = 128;
+  static_assert(QO >= 128 && QO + NX * NX <= RING_SLOT, "Q fits slot 0's tail, past the producer's 64 chunks");
   double F[3][16], Rr[NU];
   {
     const double* Ab = P.A + (size_t)b * NX * NX;
