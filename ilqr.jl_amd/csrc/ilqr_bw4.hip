@@ -548,3 +548,19 @@ hipError_t launch_lq_iter_backward4(const LQParams& p, int B, int T, const IterA
 }
 
 }  // namespace ilqr
+
+#ifdef ILQR_COOP_TRACE
+// the trace build's records (ilqr_fwd_ring.h coop_trace): copies up to max_recs of them
+// (4 words each) and resets the count; → the number copied, -1 on a HIP error
+extern "C" int ilqr_debug_trace(unsigned long long* out, int max_recs) {
+  unsigned n = 0;
+  if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(ilqr::g_trace_n), sizeof(n)) != hipSuccess) return -1;
+  if (n > ilqr::COOP_TRACE_MAX) n = ilqr::COOP_TRACE_MAX;
+  const unsigned m = n < (unsigned)max_recs ? n : (unsigned)max_recs;
+  if (m && hipMemcpyFromSymbol(out, HIP_SYMBOL(ilqr::g_trace), sizeof(unsigned long long) * 4 * m) != hipSuccess)
+    return -1;
+  const unsigned z = 0;
+  if (hipMemcpyToSymbol(HIP_SYMBOL(ilqr::g_trace_n), &z, sizeof(z)) != hipSuccess) return -1;
+  return (int)m;
+}
+#endif

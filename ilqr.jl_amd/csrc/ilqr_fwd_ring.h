@@ -1098,6 +1098,28 @@ __device__ __forceinline__ void iter_forward_wave_mfma(const LQParams& P, int b0
 // coherent value); rollout stores that another XCD may overwrite later in the launch
 // (trial 1's by the publisher, trial 2's stored as it ran) are written back by a
 // release fence before the word that hands the trajectory on — a handful per launch.
+// Trace build (ILQR_COOP_TRACE, the Makefile's `tracevariant`; never the product): every
+// grab of the cooperative search records (kind, generation, trajectory, j0, lim,
+// finalised, start / pass end / finaliser end on the 100 MHz real-time counter) and every
+// wave the end of its own trial-1 work; tools/coop_trace.py reads them back through
+// ilqr_debug_trace (ilqr_bw4.hip).
+#ifdef ILQR_COOP_TRACE
+constexpr unsigned COOP_TRACE_MAX = 262144;
+__device__ unsigned long long g_trace[4 * COOP_TRACE_MAX];
+__device__ unsigned g_trace_n;
+__device__ __forceinline__ void coop_trace(unsigned kind, unsigned gen, unsigned id, unsigned j0, unsigned lim,
+                                           unsigned fin, uint64_t t0, uint64_t t1, uint64_t t2) {
+  const unsigned k = __hip_atomic_fetch_add(&g_trace_n, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (k >= COOP_TRACE_MAX) return;
+  g_trace[4 * k] = (unsigned long long)kind | ((unsigned long long)fin << 4) | ((unsigned long long)(j0 & 255) << 8) |
+                   ((unsigned long long)(lim & 255) << 16) | ((unsigned long long)(id & 0xFFFFFF) << 24) |
+                   ((unsigned long long)(gen & 0xFFFF) << 48);
+  g_trace[4 * k + 1] = t0;
+  g_trace[4 * k + 2] = t1;
+  g_trace[4 * k + 3] = t2;
+}
+#endif
+
 #ifndef ILQR_COOP_WAIT_TICKS
 #define ILQR_COOP_WAIT_TICKS 20000
 #endif
@@ -1302,20 +1324,30 @@ __device__ void coop_finalize(const LQParams& P, int b, int B, int T, const Iter
   }
 }
 
-// Trials handed out per grab: 16 (lq_cand16_pass, round 6) or 4 (lq_forward_wave_ring's
-// candidate pass, rounds 3-5; built for A/B). Both evaluate every trial bit for bit as the
-// sequential search does.
+// Trials handed out per grab (round 6): sixteen (lq_cand16_pass: ≈2× the trials per µs of
+// a wave, ≈1.8× the latency of a pass) when the launch published more than
+// COOP_WIDE_MIN searches — the at-floor iteration 5's ~900, where the search phase is
+// throughput-bound — else four (lq_forward_wave_ring's candidate pass, rounds 3-5: a few
+// deep searches and a thousand idle waves, latency-bound; iteration 4's 9 searches of 63
+// trials each: 97 µs in quads against 116 µs in sixteens, tools/coop_trace.py,
+// profiles/r06/). ILQR_COOP_WIDTH = 4 or 16 fixes it (A/B builds). Every width evaluates
+// each trial bit for bit as the sequential search does, so mixing them in one search
+// changes nothing but the schedule.
 #ifndef ILQR_COOP_WIDTH
-#define ILQR_COOP_WIDTH 16
+#define ILQR_COOP_WIDTH 0
 #endif
-static_assert(ILQR_COOP_WIDTH == 4 || ILQR_COOP_WIDTH == 16, "a grab is four or sixteen trials");
+static_assert(ILQR_COOP_WIDTH == 0 || ILQR_COOP_WIDTH == 4 || ILQR_COOP_WIDTH == 16, "a grab is 4 or 16 trials");
+constexpr int COOP_WIDE_MIN = 64;
+__device__ __forceinline__ bool coop_wide(int published) {
+  return ILQR_COOP_WIDTH == 16 || (ILQR_COOP_WIDTH == 0 && published > COOP_WIDE_MIN);
+}
 
-// Grab trials j0 .. j0+W−1 of trajectory b, evaluate them, and finalise b if these were
-// the last needed (whole wave).
+// Grab trials j0 .. j0+W−1 of trajectory b (W = 16 if `wide`, else 4), evaluate them, and
+// finalise b if these were the last needed (whole wave).
 template <int NX, int NU>
 __device__ int coop_evaluate(const LQParams& P, int b, int B, int T, const IterArgs& a, const LSCoop& c,
-                              const LSParams& ls, double* ring) {
-  constexpr int W = ILQR_COOP_WIDTH;
+                              const LSParams& ls, double* ring, bool wide) {
+  const int W = wide ? 16 : 4;
   LSCoopRec* R = c.rec + b;
   const int l = threadIdx.x & 63;
   int j0 = 0, lim0 = 0, sl = 0;
@@ -1329,6 +1361,9 @@ __device__ int coop_evaluate(const LQParams& P, int b, int B, int T, const IterA
   sl = __builtin_amdgcn_readfirstlane(sl);
   const bool scr = sl < c.nslots;  // every trial's rollout to the scratch
   if (j0 > lim0) return 0;  // raced past the needed set: nothing to do
+#ifdef ILQR_COOP_TRACE
+  const uint64_t tq0 = __builtin_amdgcn_s_memrealtime();
+#endif
   // the cost to beat: written before this launch (in place by fit's finaliser of b only,
   // once no trial of b is needed any more)
   const double pc = a.prev_cost ? a.prev_cost[b] : INFINITY;
@@ -1336,7 +1371,7 @@ __device__ int coop_evaluate(const LQParams& P, int b, int B, int T, const IterA
   bool eo;
   int j;
   bool mine;
-  if constexpr (W == 16) {
+  if (wide) {
     const int tt = l & 15;  // this lane's trial
     j = j0 + tt;
     mine = j <= lim0;
@@ -1376,7 +1411,7 @@ __device__ int coop_evaluate(const LQParams& P, int b, int B, int T, const IterA
     eo = r.eo;
   }
   // one lane per trial records it (lanes 0..15 with W = 16; lane 16g with W = 4)
-  const bool rec = W == 16 ? l < 16 : (l & 15) == 0;
+  const bool rec = wide ? l < 16 : (l & 15) == 0;
   if (rec && mine) {
     ag_std(c.cost + (size_t)b * COOP_MAX_TRIALS + j - 1, cost);
     ag_std(c.du2 + (size_t)b * COOP_MAX_TRIALS + j - 1, du2);
@@ -1412,7 +1447,13 @@ __device__ int coop_evaluate(const LQParams& P, int b, int B, int T, const IterA
   }
   fin = __builtin_amdgcn_readfirstlane(fin);
   lim = __builtin_amdgcn_readfirstlane(lim);
+#ifdef ILQR_COOP_TRACE
+  const uint64_t tq1 = __builtin_amdgcn_s_memrealtime();
+#endif
   if (fin) coop_finalize<NX, NU>(P, b, B, T, a, c, ls, ring, lim, sl);
+#ifdef ILQR_COOP_TRACE
+  if (l == 0) coop_trace(2, a.coop_gen, b, j0, fin ? lim : lim0, fin, tq0, tq1, __builtin_amdgcn_s_memrealtime());
+#endif
   return fin ? 2 : 1;  // 1: trials evaluated, the search not finalised here; 2: finalised
 }
 
@@ -1432,21 +1473,25 @@ __device__ void lq_coop_search(const LQParams& P, int B, int T, const IterArgs& 
   // the no-publication launch (every iteration from cold, most of a fit's) leaves after
   // ONE load: the list length straight from the kernel arguments
   if (__builtin_amdgcn_readfirstlane(ag_ld(a.coop_ctl + (gen & 1))) == 0) return;
+#ifdef ILQR_COOP_TRACE
+  if ((threadIdx.x & 63) == 0) coop_trace(1, gen, wid, 0, 0, 0, __builtin_amdgcn_s_memrealtime(), 0, 0);
+#endif
   const LSCoop c = *a.coop;  // scalar loads, only once there is work
   // first the quads of the wave's own published trajectories (`own`, bit q: b0 + q): a
   // search's first quad then starts as its trial 1 ends, not when some wave frees up
   // (≈50 µs later in the at-floor iteration, §4); a quad another wave took already
   // makes this grab the next one, or nothing
+  auto wide_now = [&] { return coop_wide(__builtin_amdgcn_readfirstlane(ag_ld(c.ctl + (gen & 1)))); };
 #pragma unroll 1
   for (int q = 0; q < 4; ++q)
-    if ((own >> q) & 1u) coop_evaluate<NX, NU>(P, b0 + q, B, T, a, c, ls, ring);
+    if ((own >> q) & 1u) coop_evaluate<NX, NU>(P, b0 + q, B, T, a, c, ls, ring, wide_now());
   // then stay on them: each further quad of an own search that is still open (the wave
   // knows its last quad's outcome first), up to the first one with nothing left to grab
 #pragma unroll 1
   for (int q = 0; q < 4; ++q)
     if ((own >> q) & 1u)
-      for (int k = 0; k < COOP_MAX_TRIALS / ILQR_COOP_WIDTH; ++k)
-        if (coop_evaluate<NX, NU>(P, b0 + q, B, T, a, c, ls, ring) != 1) break;
+      for (int k = 0; k < COOP_MAX_TRIALS / 4; ++k)
+        if (coop_evaluate<NX, NU>(P, b0 + q, B, T, a, c, ls, ring, wide_now()) != 1) break;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   // 200 µs at the 100 MHz real-time counter; the Makefile's `variants` target builds a
   // library with 0 (a wave leaves at the first unwritten slot it sees) for the test of
@@ -1459,11 +1504,16 @@ __device__ void lq_coop_search(const LQParams& P, int B, int T, const IterArgs& 
     const int b = coop_find(c, gen, n, ls.max_trials, (int)(((uint64_t)wid * 2654435761u) % (uint32_t)n),
                             unwritten);
     if (b >= 0) {
-      coop_evaluate<NX, NU>(P, b, B, T, a, c, ls, ring);
+      coop_evaluate<NX, NU>(P, b, B, T, a, c, ls, ring, coop_wide(n));
       continue;
     }
     // a reserved entry is written moments after its slot: worth a short wait
-    if (!unwritten || __builtin_amdgcn_s_memrealtime() - t0 > WAIT_TICKS) break;
+    if (!unwritten || __builtin_amdgcn_s_memrealtime() - t0 > WAIT_TICKS) {
+#ifdef ILQR_COOP_TRACE
+      if ((threadIdx.x & 63) == 0) coop_trace(3, gen, wid, 0, 0, 0, __builtin_amdgcn_s_memrealtime(), 0, 0);
+#endif
+      break;
+    }
     __builtin_amdgcn_s_sleep(8);
   }
 }

@@ -68,10 +68,19 @@ case $WHAT in
             step bench100_spin 300 python bench.py --steps 100 --no-cpu --no-secondary
             for f in gpurun_out/bench20_*.log gpurun_out/bench100_spin.log; do python -c "import json,sys; d=[json.loads(l) for l in open(sys.argv[1]) if l.startswith('{')][-1]; print(sys.argv[1], round(d['value'],1), 'ms_per_step', round(d['ms_per_step']*1000,2), 'event_us', round(d['iteration']['event_ms']*1000,2), 'traffic', d['roofline']['traffic'])" $f; done > gpurun_out/wait20_ab.log; cat gpurun_out/wait20_ab.log ;;
   w16ab) for i in 1 2; do
-           ILQR_LIB=ilqr.jl_amd/lib/variants/libilqr_hip_w4.so step bench_w4_$i 300 python tools/ab_lib.py bench.py --no-cpu --no-secondary
-           step bench_w16_$i 300 python bench.py --no-cpu --no-secondary
+           for v in w4 w16; do
+             ILQR_LIB=ilqr.jl_amd/lib/variants/libilqr_hip_$v.so step bench_${v}_$i 300 python tools/ab_lib.py bench.py --no-cpu --no-secondary
+           done
+           step bench_prod_$i 300 python bench.py --no-cpu --no-secondary
          done
-         for f in gpurun_out/bench_w4_*.log gpurun_out/bench_w16_*.log; do python -c "import json,sys; d=[json.loads(l) for l in open(sys.argv[1]) if l.startswith('{')][-1]; print(sys.argv[1], 'value', round(d['value'],1), 'co_headline', round(d['co_headline']['value'],1), 'fit5_ms', round(d['co_headline']['ms_per_fit'],4), 'dflt', round(d['fit_default_options']['batched_it_per_s'],1), 'status5', d['fit_5_iterations']['trajectory_status_counts'], 'trials', [round(v,3) for v in d['fit_5_iterations']['line_search_trials_per_iteration']])" $f; done > gpurun_out/w16_ab.log; cat gpurun_out/w16_ab.log ;;
+         for f in gpurun_out/bench_w4_*.log gpurun_out/bench_w16_*.log gpurun_out/bench_prod_*.log; do python -c "import json,sys; d=[json.loads(l) for l in open(sys.argv[1]) if l.startswith('{')][-1]; print(sys.argv[1], 'value', round(d['value'],1), 'co_headline', round(d['co_headline']['value'],1), 'fit5_ms', round(d['co_headline']['ms_per_fit'],4), 'dflt', round(d['fit_default_options']['batched_it_per_s'],1), 'status5', d['fit_5_iterations']['trajectory_status_counts'])" $f; done > gpurun_out/w16_ab.log; cat gpurun_out/w16_ab.log ;;
+  tailab) for i in 1 2; do
+            for v in w4 w16; do
+              ILQR_LIB=ilqr.jl_amd/lib/variants/libilqr_hip_$v.so MODES=coop step tail_${v}_$i 200 python tools/tail_probe.py
+            done
+            MODES=coop step tail_prod_$i 200 python tools/tail_probe.py
+          done
+          grep -H "coop" gpurun_out/tail_*_[12].log > gpurun_out/tail_ab.log; cat gpurun_out/tail_ab.log ;;
   gatherab) for i in 1 2 3; do for wg in 0 1 4 16; do
               ILQR_GATHER_WG=$wg step ab_fit_wg${wg}_$i 120 python tools/ab_fit.py
             done; done

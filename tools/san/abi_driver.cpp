@@ -6,6 +6,7 @@
 // tools/san/run_gpu.sh (a GPU: small fits through every entry point, the multi-device
 // calls' host threads included). SURVEY §5. Exit 0 on success.
 #include <cmath>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <vector>
@@ -24,6 +25,10 @@ static int fails = 0;
   } while (0)
 
 extern "C" int hipGetDeviceCount(int*);
+extern "C" int hipSetDevice(int);
+extern "C" int hipFree(void*);
+extern "C" int hipDeviceSynchronize(void);
+extern "C" int hipMemGetInfo(size_t*, size_t*);
 
 // the reference's RBD script model (2Dof_arm.urdf floating, zero gravity, its costs)
 static ilqr_floating floating_model() {
@@ -160,7 +165,41 @@ struct LQ {
   }
 };
 
+static void gpu_paths_body(int ndev);
+
+// Device memory the process holds (total − free on device 0), after a synchronise.
+static size_t device_bytes_in_use() {
+  size_t fr = 0, tot = 0;
+  hipDeviceSynchronize();
+  if (hipMemGetInfo(&fr, &tot) != 0) return 0;
+  return tot - fr;
+}
+
 static void gpu_paths(int ndev) {
+  // every handle and buffer a round of the GPU paths creates is released before the round
+  // returns: a second round leaves the device memory in use where it found it. (The first
+  // round's delta is the HIP runtime's own one-time allocations — code objects loaded at
+  // first launch, the private-segment (scratch) pool — which it keeps until exit.) Under
+  // ASan's default quarantine the freed device blocks stay parked in the quarantine until
+  // exit, so the check runs with quarantine_size_mb=0 (tools/san/run_gpu.sh)
+  // and is only reported otherwise.
+  (void)hipSetDevice(0);
+  (void)hipFree(nullptr);
+  const size_t base0 = device_bytes_in_use();
+  gpu_paths_body(ndev);
+  const size_t base = device_bytes_in_use();
+  gpu_paths_body(ndev);
+  const size_t end = device_bytes_in_use();
+  const long long delta = (long long)end - (long long)base;
+  const char* opts = getenv("ASAN_OPTIONS");
+  const bool no_quarantine = opts && strstr(opts, "quarantine_size_mb=0");
+  std::printf("device memory in use: %zu B at start, %zu B after round 1 (the runtime's one-time allocations: "
+              "%lld B), %zu B after round 2 (delta %lld B)%s\n", base0, base, (long long)base - (long long)base0, end,
+              delta, no_quarantine || !opts ? "" : " [quarantine on: freed blocks held, not checked]");
+  if (no_quarantine || !opts) CHECK(delta <= (1ll << 20), "every device buffer and handle released");
+}
+
+static void gpu_paths_body(int ndev) {
   const int B = 96, T = 20, it = 4;
   LQ lq(B, T);
   const size_t xb = lq.x.size() * 8, ub = lq.u.size() * 8;
