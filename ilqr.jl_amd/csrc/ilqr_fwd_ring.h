@@ -514,21 +514,32 @@ __device__ Cand16 lq_cand16_pass(const LQParams& P, int b, int T, const double* 
   constexpr int QO = 128;
   static_assert(QO >= 128 && QO + NX * NX <= RING_SLOT, "Q fits slot 0's tail, past the producer's 64 chunks");
   double F[3][16], Rr[NU];
+#ifndef ILQR_CAND16_QREG
+#define ILQR_CAND16_QREG 0
+#endif
+  double Qr[ILQR_CAND16_QREG ? 3 : 1][NX];  // Q rows in registers (ILQR_CAND16_QREG), else LDS
   {
     const double* Ab = P.A + (size_t)b * NX * NX;
     const double* Bb = P.B + (size_t)b * NX * NU;
     const double* Qb = P.Q + (size_t)b * NX * NX;
     const double2* rr = reinterpret_cast<const double2*>(P.R + (size_t)b * NU * NU + r * NU);
-    for (int i = l; i < NX * NX; i += 64) ring[QO + i] = Qb[i];
+    if constexpr (!ILQR_CAND16_QREG)
+      for (int i = l; i < NX * NX; i += 64) ring[QO + i] = Qb[i];
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
       const double2* ar = reinterpret_cast<const double2*>(Ab + (3 * r + i) * NX);
       const double2* br = reinterpret_cast<const double2*>(Bb + (3 * r + i) * NU);
+      const double2* qr = reinterpret_cast<const double2*>(Qb + (3 * r + i) * NX);
 #pragma unroll
       for (int k = 0; k < NX / 2; ++k) {
         const double2 a2 = ar[k];
         F[i][2 * k] = a2.x + 0.0;
         F[i][2 * k + 1] = a2.y + 0.0;
+        if constexpr (ILQR_CAND16_QREG) {
+          const double2 q2 = qr[k];
+          Qr[i][2 * k] = q2.x;
+          Qr[i][2 * k + 1] = q2.y;
+        }
       }
 #pragma unroll
       for (int m = 0; m < NU / 2; ++m) {
@@ -666,9 +677,13 @@ __device__ Cand16 lq_cand16_pass(const LQParams& P, int b, int T, const double* 
     rd12(my + 2 * NX, V);
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
-      double qr[NX];
-      rd12(ring + QO + (3 * r + i) * NX, qr);
-      cost[i] = fma(vo[i], dot12(V, qr), cost[i]);
+      if constexpr (ILQR_CAND16_QREG) {
+        cost[i] = fma(vo[i], dot12(V, Qr[i]), cost[i]);
+      } else {
+        double qr[NX];
+        rd12(ring + QO + (3 * r + i) * NX, qr);
+        cost[i] = fma(vo[i], dot12(V, qr), cost[i]);
+      }
     }
     produce(t + PF);  // slot (t+PF)%R was last read at step t+PF−R < t
     wave_lds_fence();  // ū of every row written before it is read
@@ -779,6 +794,283 @@ __device__ Cand16 lq_cand16_pass(const LQParams& P, int b, int T, const double* 
   wave_lds_fence();  // the tree's reads before the next pass writes the exchange rows
   // the loads of the clamped steps past the horizon are still in flight: drain them (and
   // the result stores) before the next pass's prologue reuses the slots
+  __builtin_amdgcn_s_waitcnt((0) | (7 << 4) | (0 << 8));
+  asm volatile("" ::: "memory");
+  return out;
+}
+
+// The same sixteen-trial pass with ONE exchange per step (ILQR_CAND16_FORM 2, the
+// default): every lane forms all four ū rows itself (its own K·δx dots, the row form's
+// order) and δx = x̄ − x, v = x̄ − x_traj for all twelve rows from the slot, so only x̄
+// crosses lanes (three ds_write_b64 by the owner, six ds_read_b128 by the trial's lanes)
+// — one LDS round trip on a step's dependent chain instead of three, for 36 more K·δx
+// FMAs and 18 more ds_read_b128 of the (broadcast) slot. Same bits as lq_cand16_pass.
+constexpr int C16B_ES = 14;  // doubles per trial's x̄ row: 16 trials on 16 different 4-bank quarters
+static_assert(16 * C16B_ES <= RING_LAREA, "the exchange area fits the ring's LAREA");
+template <int R, int PF>
+__device__ Cand16 lq_cand16b_pass(const LQParams& P, int b, int T, const double* __restrict__ x,
+                                  const double* __restrict__ u, const double* __restrict__ xtraj,
+                                  const double* __restrict__ dg, const double* __restrict__ Kg, double alpha, bool st,
+                                  __amdgpu_buffer_rsrc_t rXN, __amdgpu_buffer_rsrc_t rUN, int gs, double* ring) {
+  constexpr int NX = 12, NU = 4;
+  static_assert(R > PF && PF >= 1, "the slot being refilled must not be the one being read");
+  constexpr uint32_t OOR = 0x80000000u;
+  b = __builtin_amdgcn_readfirstlane(b);
+  const int l = threadIdx.x & 63;
+  const int r = l >> 4;   // rows 3r .. 3r+2 of x̄, row r of ū's cost and Σ(ū − u)²
+  const int tt = l & 15;  // the trial
+  constexpr int QO = 128;  // Q in slot 0's tail (see lq_cand16_pass)
+  static_assert(QO + NX * NX <= RING_SLOT, "Q fits slot 0's tail, past the producer's 64 chunks");
+  double F[3][16], Rr[NU];
+  {
+    const double* Ab = P.A + (size_t)b * NX * NX;
+    const double* Bb = P.B + (size_t)b * NX * NU;
+    const double* Qb = P.Q + (size_t)b * NX * NX;
+    const double2* rr = reinterpret_cast<const double2*>(P.R + (size_t)b * NU * NU + r * NU);
+    for (int i = l; i < NX * NX; i += 64) ring[QO + i] = Qb[i];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const double2* ar = reinterpret_cast<const double2*>(Ab + (3 * r + i) * NX);
+      const double2* br = reinterpret_cast<const double2*>(Bb + (3 * r + i) * NU);
+#pragma unroll
+      for (int k = 0; k < NX / 2; ++k) {
+        const double2 a2 = ar[k];
+        F[i][2 * k] = a2.x + 0.0;
+        F[i][2 * k + 1] = a2.y + 0.0;
+      }
+#pragma unroll
+      for (int m = 0; m < NU / 2; ++m) {
+        const double2 b2 = br[m];
+        F[i][NX + 2 * m] = 0.0 + b2.x;
+        F[i][NX + 2 * m + 1] = 0.0 + b2.y;
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < NU / 2; ++m) {
+      const double2 r2 = rr[m];
+      Rr[2 * m] = r2.x;
+      Rr[2 * m + 1] = r2.y;
+    }
+  }
+  __builtin_amdgcn_s_waitcnt((0) | (7 << 4) | (15 << 8));
+  asm volatile("" ::: "memory");
+
+  const double* xt0 = xtraj ? xtraj : x;
+  const double xtw = xtraj ? 1.0 : 0.0;
+  const char* p1;
+  uint32_t s1;
+  {
+    const int c = l < 40 ? l : l - 40;
+    const size_t bb = (size_t)b;
+    if (c < 24) {
+      p1 = reinterpret_cast<const char*>(Kg + bb * T * NU * NX + 2 * c);
+      s1 = NU * NX * 8;
+    } else if (c < 30) {
+      p1 = reinterpret_cast<const char*>(x + bb * (T + 1) * NX + 2 * (c - 24));
+      s1 = NX * 8;
+    } else if (c < 32) {
+      p1 = reinterpret_cast<const char*>(u + bb * T * NU + 2 * (c - 30));
+      s1 = NU * 8;
+    } else if (c < 38) {
+      p1 = reinterpret_cast<const char*>(xt0 + bb * (T + 1) * NX + 2 * (c - 32));
+      s1 = NX * 8;
+    } else {
+      p1 = reinterpret_cast<const char*>(dg + bb * T * NU + 2 * (c - 38));
+      s1 = NU * 8;
+    }
+  }
+  const uint32_t ring_lds = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) double*)ring;
+  auto produce = [&](int t) {
+    uint32_t tq = (uint32_t)(t < T ? t : T - 1);
+    asm volatile("" : "+s"(tq));
+    const uint32_t m0 = ring_lds + (uint32_t)((t % R) * RING_SLOT * 8);
+    asm volatile(ILQR_FW_LDS_OP1 ::"v"(p1 + (size_t)tq * s1), "{m0}"(m0) : "memory");
+  };
+  constexpr int NL = 1, NS = 4;
+  constexpr int N_SS = (NL + NS) * PF - NL, N_PRO = NL * PF - NL;
+  auto wait_slot = [](auto n) {
+    constexpr int v = decltype(n)::value;
+    static_assert(v >= 0 && v < 64, "vmcnt is 6 bits");
+    __builtin_amdgcn_s_waitcnt((v & 15) | (7 << 4) | (15 << 8) | ((v >> 4) << 14));
+    asm volatile("" ::: "memory");
+  };
+  constexpr int SX = 48, SU = 60, SXT = 64, SD = 76;
+  double* const my = ring + R * RING_SLOT + tt * C16B_ES;
+  const uint32_t oxs = st ? (uint32_t)(gs * (T + 1) * NX + 3 * r) * 8 : OOR;
+  const uint32_t ous = st ? (uint32_t)(gs * T * NU + r) * 8 : OOR;
+  auto rd12 = [](const double* p, double (&v)[NX]) {
+    const double2* q = reinterpret_cast<const double2*>(p);
+#pragma unroll
+    for (int k = 0; k < NX / 2; ++k) {
+      const double2 w = q[k];
+      v[2 * k] = w.x;
+      v[2 * k + 1] = w.y;
+    }
+  };
+  auto rd4 = [](const double* p, double (&v)[NU]) {
+    const double2* q = reinterpret_cast<const double2*>(p);
+    const double2 w0 = q[0], w1 = q[1];
+    v[0] = w0.x;
+    v[1] = w0.y;
+    v[2] = w1.x;
+    v[3] = w1.y;
+  };
+  auto dot12 = [](const double (&v)[NX], const double* c) {
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+#pragma unroll
+    for (int k = 0; k < NX; k += 4) {
+      a0 = fma(v[k], c[k], a0);
+      a1 = fma(v[k + 1], c[k + 1], a1);
+      a2 = fma(v[k + 2], c[k + 2], a2);
+      a3 = fma(v[k + 3], c[k + 3], a3);
+    }
+    return (a0 + a1) + (a2 + a3);
+  };
+  auto pick4 = [r](const double (&v)[NU]) {
+    const double a = r & 1 ? v[1] : v[0], c = r & 1 ? v[3] : v[2];
+    return r & 2 ? c : a;
+  };
+
+#pragma unroll
+  for (int t = 0; t < PF; ++t) produce(t);
+  wait_slot(std::integral_constant<int, N_PRO>{});
+  double xo[3];  // this lane's rows of x̄ₖ
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    xo[i] = ring[SX + 3 * r + i];  // x̄₁ = x₁ (:65)
+    my[3 * r + i] = xo[i];
+  }
+  wave_lds_fence();
+  double cost[3] = {0.0, 0.0, 0.0}, costu = 0.0, du2 = 0.0;
+  bool eo = true;
+  auto step = [&](int t, auto next_wait) {
+    const double* sl = ring + (t % R) * RING_SLOT;
+    double XB[NX], DX[NX];
+    rd12(my, XB);
+    {
+      double X[NX];
+      rd12(sl + SX, X);
+#pragma unroll
+      for (int k = 0; k < NX; ++k) DX[k] = XB[k] - X[k];  // δx (:72)
+    }
+    // ūₖ = uₖ + α δuₖ + Kₖ δx (:73), all four rows
+    double U4[NU], D4[NU], UB[NU];
+    rd4(sl + SU, U4);
+    rd4(sl + SD, D4);
+#pragma unroll
+    for (int m = 0; m < NU; ++m) {
+      const double kdx = dot12(DX, sl + NX * m);
+      const double ua = fma(alpha, D4[m], U4[m]);
+      UB[m] = ua + kdx;
+      eo = eo && (ua == U4[m]);
+    }
+    const double ubr = pick4(UB), urr = pick4(U4);
+    const double e = ubr - urr;
+    du2 = fma(e, e, du2);
+    // x̄ₖ₊₁ = A x̄ₖ + B ūₖ (:74), this lane's rows
+    double acc[3][4];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) acc[i][0] = acc[i][1] = acc[i][2] = acc[i][3] = 0.0;
+#pragma unroll
+    for (int k = 0; k < NX; ++k)
+#pragma unroll
+      for (int i = 0; i < 3; ++i) acc[i][k & 3] = fma(XB[k], F[i][k], acc[i][k & 3]);
+#pragma unroll
+    for (int m = 0; m < NU; ++m)
+#pragma unroll
+      for (int i = 0; i < 3; ++i) acc[i][m] = fma(UB[m], F[i][NX + m], acc[i][m]);
+    double xn[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) xn[i] = (acc[i][0] + acc[i][1]) + (acc[i][2] + acc[i][3]);
+    produce(t + PF);  // slot (t+PF)%R was last read at step t+PF−R < t
+    wave_lds_fence();  // every lane's reads of the exchange row before its overwrite
+#pragma unroll
+    for (int i = 0; i < 3; ++i) my[3 * r + i] = xn[i];
+    // ℓ(x̄ₖ − x_trajₖ, ūₖ) rows (:187-190): v = x̄ − x_traj, vᵀ(Q row); ūᵀ(R row)
+    {
+      double V[NX];
+      rd12(sl + SXT, V);
+#pragma unroll
+      for (int k = 0; k < NX; ++k) V[k] = fma(-xtw, V[k], XB[k]);
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        const double vi = fma(-xtw, sl[SXT + 3 * r + i], xo[i]);
+        cost[i] = fma(vi, dot12(V, ring + QO + (3 * r + i) * NX), cost[i]);
+      }
+    }
+    const double lvu = (fma(UB[0], Rr[0], 0.0) + fma(UB[1], Rr[1], 0.0)) +
+                       (fma(UB[2], Rr[2], 0.0) + fma(UB[3], Rr[3], 0.0));
+    costu = fma(ubr, lvu, costu);
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, xo[i]), rXN, oxs,
+                                            (uint32_t)(t * NX + i) * 8, 0);
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, ubr), rUN, ous, (uint32_t)t * NU * 8, 0);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) xo[i] = xn[i];
+    wait_slot(next_wait);  // slot t + 1 (past the horizon: a clamped step's, read and never used)
+    wave_lds_fence();      // the x̄ rows written before the next step reads them
+  };
+  const int tp = T < PF ? T : PF;
+  for (int t = 0; t < tp - 1; ++t) step(t, std::integral_constant<int, N_PRO>{});
+  for (int t = tp - 1; t < T; ++t) step(t, std::integral_constant<int, N_SS>{});
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, xo[i]), rXN, oxs, (uint32_t)(T * NX + i) * 8, 0);
+  {
+    double XB[NX];
+    rd12(my, XB);
+    const double* Qfb = P.Qf + (size_t)b * NX * NX;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      double qf[NX];
+      rd12(Qfb + (3 * r + i) * NX, qf);
+      cost[i] = fma(xo[i], dot12(XB, qf), cost[i]);
+    }
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+    const double z = 0.0;
+#pragma unroll
+    for (int k = 0; k < NX; k += 4) {
+      a0 = fma(XB[k], z, a0);
+      a1 = fma(XB[k + 1], z, a1);
+      a2 = fma(XB[k + 2], z, a2);
+      a3 = fma(XB[k + 3], z, a3);
+    }
+    costu = fma(z, (a0 + a1) + (a2 + a3), costu);
+  }
+  // rowsum16 over the trial's sixteen rows (lq_cand16_pass): the partials through the
+  // trial's exchange row (32 doubles: the trial's row and the next one's, both idle now)
+  double* const red = ring + R * RING_SLOT + tt * 32;
+  static_assert(16 * 32 <= RING_LAREA, "the reduction rows fit the ring's LAREA");
+  wave_lds_fence();
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    red[3 * r + i] = cost[i];
+    red[16 + 3 * r + i] = 0.0;
+  }
+  red[12 + r] = costu;
+  red[16 + 12 + r] = du2;
+  wave_lds_fence();
+  auto tree16 = [](const double* c) {
+    return (((c[0] + c[8]) + (c[4] + c[12])) + ((c[2] + c[10]) + (c[6] + c[14]))) +
+           (((c[1] + c[9]) + (c[5] + c[13])) + ((c[3] + c[11]) + (c[7] + c[15])));
+  };
+  double cs[16], ds[16];
+#pragma unroll
+  for (int k = 0; k < 16; k += 2) {
+    const double2 w = *reinterpret_cast<const double2*>(red + k);
+    const double2 v = *reinterpret_cast<const double2*>(red + 16 + k);
+    cs[k] = w.x;
+    cs[k + 1] = w.y;
+    ds[k] = v.x;
+    ds[k + 1] = v.y;
+  }
+  Cand16 out;
+  out.cost = tree16(cs);
+  out.du2 = tree16(ds);
+  // every lane formed all four ū rows: its own eo is the trial's
+  out.eo = eo;
+  wave_lds_fence();
   __builtin_amdgcn_s_waitcnt((0) | (7 << 4) | (0 << 8));
   asm volatile("" ::: "memory");
   return out;
@@ -1336,6 +1628,9 @@ __device__ void coop_finalize(const LQParams& P, int b, int B, int T, const Iter
 #ifndef ILQR_COOP_WIDTH
 #define ILQR_COOP_WIDTH 0
 #endif
+#ifndef ILQR_CAND16_FORM  // 1: lq_cand16_pass (three exchanges a step), 2: lq_cand16b_pass (one)
+#define ILQR_CAND16_FORM 1
+#endif
 static_assert(ILQR_COOP_WIDTH == 0 || ILQR_COOP_WIDTH == 4 || ILQR_COOP_WIDTH == 16, "a grab is 4 or 16 trials");
 constexpr int COOP_WIDE_MIN = 64;
 __device__ __forceinline__ bool coop_wide(int published) {
@@ -1388,8 +1683,13 @@ __device__ int coop_evaluate(const LQParams& P, int b, int B, int T, const IterA
             : buffer_rsrc(uniform_ptr(a.unew + (size_t)b * T * NU), (uint32_t)__builtin_amdgcn_readfirstlane(T * NU * 8));
     const bool st = mine && (scr || (j0 == 2 && tt == 0));
     const int gs = scr ? sl * COOP_MAX_TRIALS + j - 1 : 0;
+#if ILQR_CAND16_FORM == 1
     const Cand16 r16 = lq_cand16_pass<PIPE_R, PIPE_PF>(P, b, T, a.x, a.u, a.xtraj, a.d, a.K, trial_alpha(ls, j),
                                                        st, rXN, rUN, gs, ring);
+#else
+    const Cand16 r16 = lq_cand16b_pass<PIPE_R, PIPE_PF>(P, b, T, a.x, a.u, a.xtraj, a.d, a.K, trial_alpha(ls, j),
+                                                        st, rXN, rUN, gs, ring);
+#endif
     cost = r16.cost;
     du2 = r16.du2;
     eo = r16.eo;
