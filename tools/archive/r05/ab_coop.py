@@ -3,7 +3,7 @@ the headline batch: one cold iteration (ilqr_iterate) and the 5-iteration fit.""
 import sys, os, time
 import numpy as np
 import torch
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "ilqr.jl_amd")]
 from ilqr_amd import _lib
 from ilqr_amd.problems import quadrotor_batch

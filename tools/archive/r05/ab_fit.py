@@ -4,7 +4,7 @@ product library or, with ILQR_LIB, another build — an A/B of the fit driver's 
 import os, sys, time
 import numpy as np
 import torch
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "ilqr.jl_amd")]
 from ilqr_amd import _lib
 if os.environ.get("ILQR_LIB"):

@@ -3,14 +3,14 @@ fp32, central differences, B = 2048, T = 100) spends its iterations: per iterati
 trajectories still running and their line searches' mean and max trials (fit history),
 for the reference's 2Dof_arm and the coupled test chain.
 
-    PYTHONPATH=.:ilqr.jl_amd python tools/chain_fit_probe.py
+    PYTHONPATH=.:ilqr.jl_amd python tools/archive/r05/chain_fit_probe.py
 """
 import json
 import os
 import sys
 import time
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 for p in (ROOT, os.path.join(ROOT, "ilqr.jl_amd")):
     if p not in sys.path:
         sys.path.insert(0, p)

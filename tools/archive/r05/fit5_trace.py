@@ -3,7 +3,7 @@ each fit's launches in order (rocprofv3 --kernel-trace), so the per-iteration ke
 durations of the at-floor iterations 4-5 can be read off."""
 import os, sys
 import torch
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "ilqr.jl_amd")]
 from ilqr_amd.problems import quadrotor_batch
 from ilqr_amd.solver import Solver

@@ -3,14 +3,14 @@ trial lane) at several batch sizes, after 1 s of forwards: host-timed median of 
 calls. A forward's lanes run the same chain at every B, so any difference is the
 launch's placement / clock. ILQR_LIB + tools/ab_lib.py runs it on another build.
 
-    PYTHONPATH=.:ilqr.jl_amd python tools/floating_fw_batch_probe.py [B ...]
+    PYTHONPATH=.:ilqr.jl_amd python tools/archive/r05/floating_fw_batch_probe.py [B ...]
 """
 import json
 import os
 import sys
 import time
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 for p in (ROOT, os.path.join(ROOT, "ilqr.jl_amd")):
     if p not in sys.path:
         sys.path.insert(0, p)

@@ -3,14 +3,14 @@ line search's accepted trial per iteration (fit history) and the median wall tim
 each stage called alone — linearize, backward, forward (its trials) — plus a T-step
 rollout through the one-step dynamics launch.
 
-    PYTHONPATH=.:ilqr.jl_amd python tools/floating_probe.py [iters] [B]
+    PYTHONPATH=.:ilqr.jl_amd python tools/archive/r05/floating_probe.py [iters] [B]
 """
 import json
 import os
 import sys
 import time
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 for p in (ROOT, os.path.join(ROOT, "ilqr.jl_amd")):
     if p not in sys.path:
         sys.path.insert(0, p)

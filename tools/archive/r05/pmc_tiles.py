@@ -3,7 +3,7 @@ tools/bench_tiles.py (B = 4096, T = 100), beside each kernel's algorithmic bytes
 
   rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/tp_fetch -o run -- python tools/bench_tiles.py
   rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/tp_write -o run -- python tools/bench_tiles.py
-  python tools/pmc_tiles.py gpurun_out/tp_fetch gpurun_out/tp_write profiles/pmc_tiles_r05.json
+  python tools/archive/r05/pmc_tiles.py gpurun_out/tp_fetch gpurun_out/tp_write profiles/pmc_tiles_r05.json
 
 FETCH_SIZE / WRITE_SIZE are KiB per dispatch. The tiles kernels read with 8-byte loads
 (global_load_dwordx2), not the 16-byte streaming reads MI355X_MICROARCH.md's ×2 read

@@ -5,14 +5,14 @@ kernel) and the forward_pass rollout of the closures (one accepted trial: the fi
 iteration's prev_cost is Inf), HIP-graph replay and eager. Wall times with a device
 synchronise around each phase, medians over repetitions.
 
-    PYTHONPATH=.:ilqr.jl_amd:tests python tools/rbd_fit_breakdown.py [B] [reps]
+    PYTHONPATH=.:ilqr.jl_amd:tests python tools/archive/r05/rbd_fit_breakdown.py [B] [reps]
 """
 import json
 import os
 import sys
 import time
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 for p in (ROOT, os.path.join(ROOT, "ilqr.jl_amd"), os.path.join(ROOT, "tests")):
     if p not in sys.path:
         sys.path.insert(0, p)

@@ -3,7 +3,7 @@ inside the timed region's fits (runs of 3 launches between gathers) against the
 back-to-back launch sections after it (runs of > 10), and the per-fit timeline — the
 gather and flags kernels and the host turnaround gap before the next fit's first launch.
 
-    python tools/trace_fit_gaps.py gpurun_out/prof/run_kernel_trace.csv
+    python tools/archive/r05/trace_fit_gaps.py gpurun_out/prof/run_kernel_trace.csv
 """
 import csv
 import sys

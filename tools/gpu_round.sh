@@ -28,7 +28,7 @@ case $WHAT in
         step smoke 180 python -c "import __graft_entry__ as g; g.smoke()" ;;
   bench) step bench 300 python bench.py ;;
   hist) step pytest_hist 400 python -u -m pytest tests/test_gpu_history.py -m gpu -x -v --timeout 200 --timeout-method thread ;;
-  ab) step ab 200 python tools/ab_coop.py ;;
+  ab) step ab 200 python tools/archive/r05/ab_coop.py ;;
   multi) step pytest_multi 400 python -u -m pytest tests/test_gpu_multi.py -m gpu -x -v --timeout 200 --timeout-method thread
          step bench_multi 300 python tools/bench_multi.py ;;
   ls) step pytest_ls 400 python -u -m pytest tests/test_gpu_line_search.py -m gpu -x -v --timeout 200 --timeout-method thread ;;
@@ -50,7 +50,7 @@ case $WHAT in
   rbdbench) step bench_rbd 300 python tools/bench_rbd.py ;;
   rbdprof) step rocprof_rbd 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_rbd -o run --output-format csv -- python tools/bench_rbd.py --steps 20 --warmup 5 --no-cpu ;;
   fit5) step tail_probe 200 python tools/tail_probe.py
-        step rocprof_fit5 200 rocprofv3 --kernel-trace -d gpurun_out/prof_fit5 -o run --output-format csv -- python tools/fit5_trace.py ;;
+        step rocprof_fit5 200 rocprofv3 --kernel-trace -d gpurun_out/prof_fit5 -o run --output-format csv -- python tools/archive/r05/fit5_trace.py ;;
   tailcap) MODES=coop MAXT=16 step tail_cap16 200 python tools/tail_probe.py
            MODES=coop MAXT=32 step tail_cap32 200 python tools/tail_probe.py
            MODES=coop MAXT=64 step tail_cap64 200 python tools/tail_probe.py ;;
@@ -82,12 +82,12 @@ case $WHAT in
           done
           grep -H "coop" gpurun_out/tail_*_[12].log > gpurun_out/tail_ab.log; cat gpurun_out/tail_ab.log ;;
   gatherab) for i in 1 2 3; do for wg in 0 1 4 16; do
-              ILQR_GATHER_WG=$wg step ab_fit_wg${wg}_$i 120 python tools/ab_fit.py
+              ILQR_GATHER_WG=$wg step ab_fit_wg${wg}_$i 120 python tools/archive/r05/ab_fit.py
             done; done
             grep -h "fit median" gpurun_out/ab_fit_wg*.log > gpurun_out/gather_ab.log; cat gpurun_out/gather_ab.log ;;
   gathertrace) for wg in 0 4; do
-                 ILQR_GATHER_WG=$wg step trace_wg$wg 200 rocprofv3 --kernel-trace -d gpurun_out/trace_wg$wg -o run --output-format csv -- python tools/ab_fit.py
-                 python tools/trace_fit_gaps.py gpurun_out/trace_wg$wg/run_kernel_trace.csv > gpurun_out/trace_fit_gaps_wg$wg.txt 2>&1
+                 ILQR_GATHER_WG=$wg step trace_wg$wg 200 rocprofv3 --kernel-trace -d gpurun_out/trace_wg$wg -o run --output-format csv -- python tools/archive/r05/ab_fit.py
+                 python tools/archive/r05/trace_fit_gaps.py gpurun_out/trace_wg$wg/run_kernel_trace.csv > gpurun_out/trace_fit_gaps_wg$wg.txt 2>&1
                done ;;
   spread) step wave_spread 200 python tools/archive/wave_spread.py ;;
   chainab) for i in 1 2; do
@@ -102,8 +102,8 @@ case $WHAT in
             grep -h "coop \|per iteration" gpurun_out/tail_prev_*.log gpurun_out/tail_new_*.log > gpurun_out/vanish_ab.log; cat gpurun_out/vanish_ab.log ;;
   tail5) step coop_tail 200 python tools/archive/coop_tail_analysis.py ;;
   headab) for i in 1 2; do
-            ILQR_LIB=ilqr.jl_amd/lib/variants/libilqr_hip_prev.so step ab_fit_prev_$i 120 python tools/ab_fit.py
-            step ab_fit_new_$i 120 python tools/ab_fit.py
+            ILQR_LIB=ilqr.jl_amd/lib/variants/libilqr_hip_prev.so step ab_fit_prev_$i 120 python tools/archive/r05/ab_fit.py
+            step ab_fit_new_$i 120 python tools/archive/r05/ab_fit.py
           done
           grep -h "fit median" gpurun_out/ab_fit_prev_*.log gpurun_out/ab_fit_new_*.log > gpurun_out/head_ab.log; cat gpurun_out/head_ab.log ;;
   tlab) for i in 1 2; do
