@@ -494,7 +494,10 @@ struct Cand16 {
 
 // `alpha`: this lane's trial's α. `st`: this lane's trial stores its rollout through rXN /
 // rUN at rollout index gs (x̄ (T+1)·12, ū T·4 doubles per rollout). Whole wave.
-template <int R, int PF>
+// STORE = false: no lane stores its rollout (a pass neither at trial 2 nor on a scratch
+// row), and the pass issues no store instructions at all — a pass that issues them, even
+// out of range, runs measurably slower (the memory pipeline takes every lane's address)
+template <int R, int PF, bool STORE>
 __device__ Cand16 lq_cand16_pass(const LQParams& P, int b, int T, const double* __restrict__ x,
                                  const double* __restrict__ u, const double* __restrict__ xtraj,
                                  const double* __restrict__ dg, const double* __restrict__ Kg, double alpha, bool st,
@@ -514,8 +517,8 @@ __device__ Cand16 lq_cand16_pass(const LQParams& P, int b, int T, const double* 
   constexpr int QO = 128;
   static_assert(QO >= 128 && QO + NX * NX <= RING_SLOT, "Q fits slot 0's tail, past the producer's 64 chunks");
   double F[3][16], Rr[NU];
-#ifndef ILQR_CAND16_QREG
-#define ILQR_CAND16_QREG 0
+#ifndef ILQR_CAND16_QREG  // 1: Q rows in registers (iteration 5: 540-553 → 518-530 µs), 0: from the slot
+#define ILQR_CAND16_QREG 1
 #endif
   double Qr[ILQR_CAND16_QREG ? 3 : 1][NX];  // Q rows in registers (ILQR_CAND16_QREG), else LDS
   {
@@ -593,8 +596,8 @@ __device__ Cand16 lq_cand16_pass(const LQParams& P, int b, int T, const double* 
     const uint32_t m0 = ring_lds + (uint32_t)((t % R) * RING_SLOT * 8);
     asm volatile(ILQR_FW_LDS_OP1 ::"v"(p1 + (size_t)tq * s1), "{m0}"(m0) : "memory");
   };
-  // per step: one slot load, then four result stores (three x̄ rows, one ū row)
-  constexpr int NL = 1, NS = 4;
+  // per step: one slot load, then four result stores (three x̄ rows, one ū row) if STORE
+  constexpr int NL = 1, NS = STORE ? 4 : 0;
   constexpr int N_SS = (NL + NS) * PF - NL, N_PRO = NL * PF - NL;
   auto wait_slot = [](auto n) {
     constexpr int v = decltype(n)::value;
@@ -704,11 +707,13 @@ __device__ Cand16 lq_cand16_pass(const LQParams& P, int b, int T, const double* 
     const double lvu = (fma(U4[0], Rr[0], 0.0) + fma(U4[1], Rr[1], 0.0)) +
                        (fma(U4[2], Rr[2], 0.0) + fma(U4[3], Rr[3], 0.0));
     costu = fma(ub, lvu, costu);
+    if constexpr (STORE) {
 #pragma unroll
-    for (int i = 0; i < 3; ++i)
-      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, xo[i]), rXN, oxs,
-                                            (uint32_t)(t * NX + i) * 8, 0);
-    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, ub), rUN, ous, (uint32_t)t * NU * 8, 0);
+      for (int i = 0; i < 3; ++i)
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, xo[i]), rXN, oxs,
+                                              (uint32_t)(t * NX + i) * 8, 0);
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, ub), rUN, ous, (uint32_t)t * NU * 8, 0);
+    }
     double xn[3];
 #pragma unroll
     for (int i = 0; i < 3; ++i) xn[i] = (acc[i][0] + acc[i][1]) + (acc[i][2] + acc[i][3]);
@@ -734,9 +739,12 @@ __device__ Cand16 lq_cand16_pass(const LQParams& P, int b, int T, const double* 
   const int tp = T < PF ? T : PF;
   for (int t = 0; t < tp - 1; ++t) step(t, std::integral_constant<int, N_PRO>{});
   for (int t = tp - 1; t < T; ++t) step(t, std::integral_constant<int, N_SS>{});
+  if constexpr (STORE) {
 #pragma unroll
-  for (int i = 0; i < 3; ++i)
-    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, xo[i]), rXN, oxs, (uint32_t)(T * NX + i) * 8, 0);
+    for (int i = 0; i < 3; ++i)
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, xo[i]), rXN, oxs, (uint32_t)(T * NX + i) * 8,
+                                            0);
+  }
   // final_cost(x̄_N) = x̄ᵀQf x̄ on the raw state (:192): the rows' Qf dots; the ū rows
   // take the row form's 0·(x̄ · 0) (a NaN state stays NaN there as well)
   {
@@ -1684,8 +1692,10 @@ __device__ int coop_evaluate(const LQParams& P, int b, int B, int T, const IterA
     const bool st = mine && (scr || (j0 == 2 && tt == 0));
     const int gs = scr ? sl * COOP_MAX_TRIALS + j - 1 : 0;
 #if ILQR_CAND16_FORM == 1
-    const Cand16 r16 = lq_cand16_pass<PIPE_R, PIPE_PF>(P, b, T, a.x, a.u, a.xtraj, a.d, a.K, trial_alpha(ls, j),
-                                                       st, rXN, rUN, gs, ring);
+    // (a store-free instantiation for passes that store nothing measured slower in the
+    // at-floor iteration: pass p50 90.5 → 99.0 µs, profiles/r06/coop_store_split_r06.log)
+    const Cand16 r16 = lq_cand16_pass<PIPE_R, PIPE_PF, true>(P, b, T, a.x, a.u, a.xtraj, a.d, a.K,
+                                                             trial_alpha(ls, j), st, rXN, rUN, gs, ring);
 #else
     const Cand16 r16 = lq_cand16b_pass<PIPE_R, PIPE_PF>(P, b, T, a.x, a.u, a.xtraj, a.d, a.K, trial_alpha(ls, j),
                                                         st, rXN, rUN, gs, ring);

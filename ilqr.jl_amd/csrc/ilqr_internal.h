@@ -54,7 +54,10 @@ struct LSCoop {
   double* su;
   int32_t nslots;     // 0: no scratch (every finaliser rolls out)
 };
-constexpr int COOP_SCRATCH_SLOTS = 32;
+#ifndef ILQR_COOP_SCRATCH_SLOTS  // A/B builds only
+#define ILQR_COOP_SCRATCH_SLOTS 32
+#endif
+constexpr int COOP_SCRATCH_SLOTS = ILQR_COOP_SCRATCH_SLOTS;
 // coop_find reads (next, best) and (stop, fin) as one 64-bit word each
 static_assert(sizeof(LSCoopRec) == 32 && offsetof(LSCoopRec, best) == 4 && offsetof(LSCoopRec, stop) == 8 &&
                   offsetof(LSCoopRec, fin) == 12 && offsetof(LSCoopRec, mask) == 16,
