@@ -1420,6 +1420,10 @@ __device__ __forceinline__ void coop_trace(unsigned kind, unsigned gen, unsigned
 }
 #endif
 
+#ifndef ILQR_COOP_DEEP_FIRST
+#define ILQR_COOP_DEEP_FIRST 1
+#endif
+constexpr int COOP_DEEP_FRONT = 5;  // trials 1..5 known rejected: past a first quad or sixteen
 #ifndef ILQR_COOP_WAIT_TICKS
 #define ILQR_COOP_WAIT_TICKS 20000
 #endif
@@ -1502,7 +1506,7 @@ __device__ __attribute__((unused)) int coop_find(const LSCoop& c, uint32_t gen, 
       e[k] = pos < n ? __hip_atomic_load(c.list + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                      : ((uint64_t)gen << 32) | 0xFFFFFFFFull;  // past the list: no entry
     }
-    int nx[CH], lim[CH], dist[CH];
+    int nx[CH], lim[CH], dist[CH], fr[CH];
 #pragma unroll
     for (int k = 0; k < CH; ++k) {
       const uint32_t bb = (uint32_t)e[k];
@@ -1528,13 +1532,19 @@ __device__ __attribute__((unused)) int coop_find(const LSCoop& c, uint32_t gen, 
       // deep search whose handed-out trials have all come back rejected
       const int front = ~m ? __builtin_ctzll(~m) : 64;
       dist[k] = nx[k] - front;
+      fr[k] = front;
       if ((uint32_t)(e[k] >> 32) != gen) unwritten = true;  // reserved, not yet written
     }
 #pragma unroll
     for (int k = 0; k < CH; ++k) {
       const uint32_t dk = dist[k] < 1 ? 1u : (dist[k] > 127 ? 127u : (uint32_t)dist[k]);
-      const uint64_t key = ((uint64_t)dk << 56) | ((uint64_t)((uint32_t)nx[k] & 0xFFFFFFu) << 32) |
-                           (uint32_t)(base + 64 * k + l);
+      // class: 0 a grab at its search's frontier; 1 a speculative grab of a search whose
+      // first grab came back rejected (front past COOP_DEEP_FRONT: deep at the floor, its
+      // later trials are likely needed); 2 a speculative grab of a search still at its
+      // first grab (round 6, ILQR_COOP_DEEP_FIRST; 0: classes 1 and 2 merge)
+      const uint32_t cls = dk <= 1 ? 0u : ((ILQR_COOP_DEEP_FIRST && fr[k] >= COOP_DEEP_FRONT) ? 1u : 2u);
+      const uint64_t key = ((uint64_t)cls << 62) | ((uint64_t)dk << 55) |
+                           ((uint64_t)((uint32_t)nx[k] & 0x7FFFFFu) << 32) | (uint32_t)(base + 64 * k + l);
       if (nx[k] <= lim[k] && key < best) best = key;
     }
     // wave minimum
@@ -1543,7 +1553,7 @@ __device__ __attribute__((unused)) int coop_find(const LSCoop& c, uint32_t gen, 
       const uint64_t q = __shfl_xor(best, o);
       best = q < best ? q : best;
     }
-    if ((best >> 56) <= 1) break;  // a quad right at its search's frontier: nothing ranks before it
+    if ((best >> 62) == 0) break;  // a grab right at its search's frontier: nothing ranks before it
   }
   unwritten = __any(unwritten);
   if (best == ~0ull) return -1;
