@@ -608,11 +608,16 @@ struct FbFwd {
 // three waves issue side by side. Same operations as fb_step: the same bits.
 constexpr int FB_SCHUR_N = (int)(sizeof(FbSchur<double>) / sizeof(double));
 static_assert(sizeof(FbSchur<double>) == FB_SCHUR_N * sizeof(double), "FbSchur<double> is doubles only");
+#ifndef ILQR_FB_LOOKAHEAD
+#define ILQR_FB_LOOKAHEAD 1
+#endif
+#if !ILQR_FB_LOOKAHEAD
 constexpr int FB_XU = FB_SCHUR_N;            // ū (8)
 constexpr int FB_XX = FB_SCHUR_N + FB_NU;    // the stage's state (angles; all 16 at a step's end)
 struct FbXch {
   double v[FB_XX + FB_NX][64];  // value-major: lane l's k-th value at v[k][l]
 };
+#endif
 constexpr int FB_FWD_WAVES = 3;
 
 // every wave reaches it: its LDS writes done (lgkmcnt only — the rollout's global stores
@@ -624,8 +629,254 @@ __device__ __forceinline__ void fb_lds_barrier() {
   asm volatile("" ::: "memory");
 }
 
+#if ILQR_FB_LOOKAHEAD
+// LDS writes done (lgkmcnt only), no barrier
+__device__ __forceinline__ void fb_lds_wait() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_waitcnt((15) | (7 << 4) | (0 << 8) | (3 << 14));
+  asm volatile("" ::: "memory");
+}
+
+// RK4's bookkeeping of one component at stage st (fb_step's loop body): k = Δt·ẋ, the
+// sum k₁ + 2k₂ + 2k₃ + k₄ and the next stage's value (the step's result at st = 3).
+// Waves 0 and 1 of fb_rollout3 both run it on the joint angles and must agree to the bit
+// (wave 0's rotations are the stored angles'): no contraction, which the compiler would
+// otherwise decide per call site.
+__device__ __forceinline__ double fb_rk_next(int st, double dt, double xd, double xb, double& acc) {
+#pragma clang fp contract(off)  // one rounding per operation wherever it is inlined
+  const double k = dt * xd;
+  const double w = (st == 0 || st == 3) ? 1.0 : 2.0;
+  const double c = st == 2 ? 1.0 : 0.5;
+  acc = st == 0 ? k : acc + w * k;
+  return st < 3 ? xb + k * c : xb + (1.0 / 6.0) * acc;
+}
+
+// The three waves pipelined by one RK4 stage. A stage's mass blocks depend on its joint
+// angles only, and the angles of stage s + 1 on stage s's state alone — θ̇ enters
+// q̇ = [·; ·; θ̇] as it is (fb_solve's kinematics), the solve only moves the velocities —
+// so wave 0 computes stage s + 1's rotations and factors while wave 1 works on stage s:
+//   wave 0 (mass):    from stage s's θ̇ (and its own running RK4 sum of the angles) the
+//                     angles of stage s + 1, their rotations (fb_rots) and factors
+//                     (fb_mass), into buffer (s + 1) & 1;
+//   wave 1 (main):    stage s's bias from its state and the rotations of buffer s & 1,
+//                     b = ū − bias, the solve with that buffer's factors and the stage
+//                     update; stage s + 1's θ̇ (its whole state at a step's start) into the
+//                     state buffer (s + 1) & 1;
+//   wave 2 (control): at a step's start, ūₜ from x̄ₜ, its cost and Σ(ū − u)², storing ū,
+//                     and ūₜ to wave 1 through LDS behind a per-lane sequence word (wave 1
+//                     waits on it once a step, after its bias — ūₜ is in by then).
+// One workgroup barrier a stage (stage s's inputs ready); every buffer a wave reads in a
+// stage is written by the others in the stage before. Wave 1's stage is the bias and the
+// solve (the rotations, ≈ 2 sincos, no longer on it), wave 0's the rotations and the mass,
+// side by side: the one-stage-per-two-barriers rollout (ILQR_FB_LOOKAHEAD=0) ran the
+// rotations + bias beside the rotations + mass, then the solve. Same operations: the same bits.
+constexpr int FB_IN_N = FB_NU * FB_NX + 2 * FB_NU + 2 * FB_NX;  // a step's K, u, δu, x, x_traj
+constexpr int FB_IN_S = FB_IN_N + 2;  // row stride: 16 rows' same element in distinct bank pairs
+template <int CAND>
 __device__ double fb_rollout3(const FbModel& P, const FbFwd& a, int b, int T, double alpha, double* __restrict__ xn,
-                              double* __restrict__ un, double& du2, bool& same, int role, int lane) {
+                              double* __restrict__ un, double& du2, bool& same, int role, int lane, bool run) {
+  struct Pipe {
+    double in[64 / CAND][FB_IN_S];  // wave 2's copy of its trajectories' step inputs
+    double F[2][FB_SCHUR_N][64];   // value-major: lane l's k-th value at [k][l]
+    double R[2][FB_NJ * 9][64];
+    double xs[2][FB_NX][64];       // θ̇ (14, 15) every stage; all 16 at a step's start
+    double u[FB_NU][64];
+    int32_t useq[64];              // t + 1 once ūₜ is in u
+    double out[3][64];
+  };
+  __shared__ Pipe X;  // named here: see the exchange of the two-barrier rollout below
+  const double* x = a.x + (size_t)b * (T + 1) * FB_NX;
+  const int S = 4 * T;
+  if (role == 0) {  // mass, one stage ahead
+    double th[FB_NX];  // only th[6], th[7] (the joint angles) are read by fb_rots
+#pragma unroll
+    for (int k = 0; k < FB_NX; ++k) th[k] = k == 6 || k == 7 ? x[k] : 0.0;
+    double xb6 = th[6], xb7 = th[7], acc6 = 0.0, acc7 = 0.0;
+    for (int s = 0; s <= S; ++s) {
+      if (s > 0) {  // stage s's angles from stage s − 1's θ̇
+        const int st = (s - 1) & 3;
+        const double v6 = X.xs[(s - 1) & 1][14][lane], v7 = X.xs[(s - 1) & 1][15][lane];
+        th[6] = fb_rk_next(st, P.dt, v6, xb6, acc6);
+        th[7] = fb_rk_next(st, P.dt, v7, xb7, acc7);
+        if (st == 3) {
+          xb6 = th[6];
+          xb7 = th[7];
+        }
+      }
+      if (s < S) {
+        asm volatile("" ::: "memory");  // the model's constants re-read per stage (fb_step)
+        double R[FB_NJ][9];
+        fb_rots(P, th, R);
+        FbSchur<double> F;
+        fb_mass(P, R, F);
+        const double* f = reinterpret_cast<const double*>(&F);
+#pragma unroll
+        for (int k = 0; k < FB_SCHUR_N; ++k) X.F[s & 1][k][lane] = f[k];
+#pragma unroll
+        for (int i = 0; i < FB_NJ; ++i)
+#pragma unroll
+          for (int k = 0; k < 9; ++k) X.R[s & 1][9 * i + k][lane] = R[i][k];
+      }
+      fb_lds_barrier();  // stage s's inputs ready
+    }
+  } else if (role == 2) {  // control: ūₜ (:72-73), its cost (:187-190), Σ(ū − u)²
+    const double* u = a.u + (size_t)b * T * FB_NU;
+    const double* xt = a.xtraj ? a.xtraj + (size_t)b * (T + 1) * FB_NX : nullptr;
+    const double* d = a.d + (size_t)b * T * FB_NU;
+    const double* K = a.K + (size_t)b * T * FB_NU * FB_NX;
+    // step tn's K, u, δu, x, x_traj of this lane's trajectory into its row of X.in, the
+    // trajectory's CAND lanes a share each — one stage after ūₜ₋₁, so that ūₜ reads LDS
+    // only: wave 1 needs it right after its bias, about 2,000 cycles after x̄ₜ is known,
+    // and a step's loads from beyond L2 (the batch's K: 1 MB a trajectory at T = 1000)
+    // took longer
+    constexpr int NK = FB_NU * FB_NX, PER = (FB_IN_N + CAND - 1) / CAND;
+    const int c = lane % CAND;
+    double* row = X.in[lane / CAND];
+    auto stage_in = [&](size_t tn) {
+      double v[PER];
+#pragma unroll
+      for (int i = 0; i < PER; ++i) {
+        const int e = c + i * CAND;
+        double w = 0.0;
+        if (e < NK)
+          w = K[tn * NK + e];
+        else if (e < NK + FB_NU)
+          w = u[tn * FB_NU + (e - NK)];
+        else if (e < NK + 2 * FB_NU)
+          w = d[tn * FB_NU + (e - NK - FB_NU)];
+        else if (e < NK + 2 * FB_NU + FB_NX)
+          w = x[tn * FB_NX + (e - NK - 2 * FB_NU)];
+        else if (e < FB_IN_N && xt)
+          w = xt[tn * FB_NX + (e - NK - 2 * FB_NU - FB_NX)];
+        v[i] = w;
+      }
+#pragma unroll
+      for (int i = 0; i < PER; ++i)
+        if (c + i * CAND < FB_IN_N) row[c + i * CAND] = v[i];
+    };
+    const double* rK = row;
+    const double* ru = row + NK;
+    const double* rd = ru + FB_NU;
+    const double* rx = rd + FB_NU;
+    const double* rxt = rx + FB_NX;
+    double xb[FB_NX];
+    double cost = 0.0, s2 = 0.0;
+    bool eq = true;
+    __hip_atomic_store(&X.useq[lane], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    stage_in(0);
+    fb_lds_barrier();
+    for (int t = 0; t < T; ++t) {
+#pragma unroll
+      for (int k = 0; k < FB_NX; ++k) xb[k] = X.xs[0][k][lane];  // x̄ₜ (x̄₁ = x₁, :65)
+      double dx[FB_NX], ub[FB_NU];
+#pragma unroll
+      for (int k = 0; k < FB_NX; ++k) dx[k] = xb[k] - rx[k];
+      // Kₜ(x̄ₜ − xₜ): each row's sum in k order, the eight rows side by side
+      double kd[FB_NU];
+#pragma unroll
+      for (int j = 0; j < FB_NU; ++j) kd[j] = 0.0;
+#pragma unroll
+      for (int k = 0; k < FB_NX; ++k)
+#pragma unroll
+        for (int j = 0; j < FB_NU; ++j) kd[j] = fma(rK[j * FB_NX + k], dx[k], kd[j]);
+#pragma unroll
+      for (int j = 0; j < FB_NU; ++j) {
+        const double uj = ru[j];
+        const double ua = uj + alpha * rd[j];
+        eq = eq && ua == uj;
+        ub[j] = ua + kd[j];
+        const double e = ub[j] - uj;
+        s2 = fma(e, e, s2);
+      }
+      // ūₜ to wave 1 after every read of the row (a store between them would order the
+      // reads one row of K at a time)
+#pragma unroll
+      for (int j = 0; j < FB_NU; ++j) X.u[j][lane] = ub[j];
+      fb_lds_wait();  // ūₜ written before its sequence word
+      __hip_atomic_store(&X.useq[lane], t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#pragma unroll
+      for (int j = 0; j < FB_NU; ++j)
+        if (run) un[(size_t)t * FB_NU + j] = ub[j];
+      double ev[FB_NQ];
+#pragma unroll
+      for (int k = 0; k < FB_NQ; ++k) ev[k] = xt ? xb[k] - rxt[k] : xb[k];
+      cost = cost + stage_cost(P, ev, ub);
+      fb_lds_barrier();
+      if (t + 1 < T) stage_in((size_t)(t + 1));
+#pragma unroll 1
+      for (int st = 1; st < 4; ++st) fb_lds_barrier();
+    }
+#pragma unroll
+    for (int k = 0; k < FB_NX; ++k) xb[k] = X.xs[0][k][lane];  // x̄_N
+    cost = cost + final_cost(P, xb);  // :192 (raw x̄_N)
+    X.out[0][lane] = cost;  // the outcome to waves 0 and 1
+    X.out[1][lane] = s2;
+    X.out[2][lane] = eq ? 1.0 : 0.0;
+  } else {  // main: bias, solve, stage update
+    double xb[FB_NX], xs[FB_NX], acc[FB_NX], ub[FB_NU];
+#pragma unroll
+    for (int k = 0; k < FB_NX; ++k) {
+      xb[k] = x[k];
+      xs[k] = xb[k];
+      if (run) xn[k] = xb[k];
+      X.xs[0][k][lane] = xb[k];
+    }
+    fb_lds_barrier();
+    for (int s = 0; s < S; ++s) {
+      const int t = s >> 2, st = s & 3;
+      asm volatile("" ::: "memory");
+      double R[FB_NJ][9];
+#pragma unroll
+      for (int i = 0; i < FB_NJ; ++i)
+#pragma unroll
+        for (int k = 0; k < 9; ++k) R[i][k] = X.R[s & 1][9 * i + k][lane];
+      double bb[FB_NU];
+      fb_bias(P, R, xs, bb);
+      if (st == 0) {
+        // the bias before the wait (else the compiler sinks it behind the wait)
+#pragma unroll
+        for (int j = 0; j < FB_NU; ++j) asm volatile("" ::"v"(bb[j]));
+        while (__hip_atomic_load(&X.useq[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != t + 1)
+          __builtin_amdgcn_s_sleep(1);
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int j = 0; j < FB_NU; ++j) ub[j] = X.u[j][lane];
+      }
+#pragma unroll
+      for (int j = 0; j < FB_NU; ++j) bb[j] = ub[j] - bb[j];
+      FbSchur<double> F;
+      double* f = reinterpret_cast<double*>(&F);
+#pragma unroll
+      for (int k = 0; k < FB_SCHUR_N; ++k) f[k] = X.F[s & 1][k][lane];
+      double k[FB_NX];
+      fb_solve(F, bb, xs, k);
+#pragma unroll
+      for (int i = 0; i < FB_NX; ++i) xs[i] = fb_rk_next(st, P.dt, k[i], xb[i], acc[i]);
+      if (st < 3) {
+        X.xs[(s + 1) & 1][14][lane] = xs[14];
+        X.xs[(s + 1) & 1][15][lane] = xs[15];
+      } else {
+#pragma unroll
+        for (int i = 0; i < FB_NX; ++i) {
+          xb[i] = xs[i];
+          X.xs[0][i][lane] = xs[i];
+          if (run) xn[(size_t)(t + 1) * FB_NX + i] = xs[i];
+        }
+      }
+      fb_lds_barrier();  // stage s + 1's state ready
+    }
+  }
+  fb_lds_barrier();
+  const double cost = X.out[0][lane];
+  du2 = X.out[1][lane];
+  same = X.out[2][lane] != 0.0;
+  fb_lds_barrier();  // read before the next rollout writes
+  return cost;
+}
+#else
+template <int CAND>
+__device__ double fb_rollout3(const FbModel& P, const FbFwd& a, int b, int T, double alpha, double* __restrict__ xn,
+                              double* __restrict__ un, double& du2, bool& same, int role, int lane, bool run) {
   // the workgroup's exchange, named here rather than passed by reference: through a
   // reference the compiler lost its address space in some instantiations and read it
   // with flat loads, whose waits cover the global loads in flight too
@@ -680,7 +931,8 @@ __device__ double fb_rollout3(const FbModel& P, const FbFwd& a, int b, int T, do
         s2 = fma(e, e, s2);
       }
 #pragma unroll
-      for (int j = 0; j < FB_NU; ++j) un[(size_t)t * FB_NU + j] = ub[j];
+      for (int j = 0; j < FB_NU; ++j)
+        if (run) un[(size_t)t * FB_NU + j] = ub[j];
       double ev[FB_NQ];
 #pragma unroll
       for (int k = 0; k < FB_NQ; ++k) ev[k] = xt ? xb[k] - xt[(size_t)t * FB_NX + k] : xb[k];
@@ -702,7 +954,7 @@ __device__ double fb_rollout3(const FbModel& P, const FbFwd& a, int b, int T, do
 #pragma unroll
     for (int k = 0; k < FB_NX; ++k) {
       xb[k] = x[k];
-      xn[k] = xb[k];
+      if (run) xn[k] = xb[k];
     }
     for (int t = 0; t < T; ++t) {
       double xs[FB_NX], acc[FB_NX], ub[FB_NU];
@@ -752,7 +1004,7 @@ __device__ double fb_rollout3(const FbModel& P, const FbFwd& a, int b, int T, do
 #pragma unroll
       for (int k = 0; k < FB_NX; ++k) {
         xb[k] = xs[k];
-        xn[(size_t)(t + 1) * FB_NX + k] = xb[k];
+        if (run) xn[(size_t)(t + 1) * FB_NX + k] = xb[k];
       }
     }
   }
@@ -763,6 +1015,7 @@ __device__ double fb_rollout3(const FbModel& P, const FbFwd& a, int b, int T, do
   fb_lds_barrier();  // read before the next rollout writes
   return cost;
 }
+#endif  // ILQR_FB_LOOKAHEAD
 
 // forward_pass for every trajectory: CAND consecutive lanes roll out trials
 // j, j+1, … at once; the first accepted trial (prev_cost − cost > 0, :77-80) is the
@@ -793,10 +1046,20 @@ __global__ __launch_bounds__(64 * FB_FWD_WAVES) void fb_forward_kernel(const FbM
     const bool run = live && done_trial == 0 && j <= a.max_trials;
     double cost = NAN, du2 = 0.0;
     bool same = false;
-    if (run) {
+    // a trajectory's lanes enter the rollout together when any of them runs (its first:
+    // j0 ≤ max_trials): wave 2 loads the trajectory's step inputs a share a lane; the
+    // lanes past max_trials roll out without storing, their outcome unused
+    if (live && done_trial == 0 && j0 <= a.max_trials) {
       double* xo = j == 1 ? a.xn + (size_t)b * nxe : slot;
       double* uo = j == 1 ? a.un + (size_t)b * nue : slot + nxe;
-      cost = fb_rollout3(P, a, b, T, alpha, xo, uo, du2, same, role, lane);
+      double d2 = 0.0;
+      bool sm = false;
+      const double cs = fb_rollout3<CAND>(P, a, b, T, alpha, xo, uo, d2, sm, role, lane, run);
+      if (run) {
+        cost = cs;
+        du2 = d2;
+        same = sm;
+      }
     }
     const bool acc = run && (pc - cost > 0.0);
     // the trajectory's lanes agree on the outcome: the smallest accepted j, else whether a

@@ -114,6 +114,16 @@ case $WHAT in
   floating) step pytest_floating 400 python -u -m pytest tests/test_gpu_floating.py -m gpu -x -v --timeout 300 --timeout-method thread
             step bench_floating 300 python tools/bench_floating.py 5 2 1 256 1024
             step rocprof_floating 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_fb -o run --output-format csv -- python tools/bench_floating.py 3 1 1 ;;
+  fbab) for i in 1 2; do
+          ILQR_LIB=ilqr.jl_amd/lib/variants/libilqr_hip_nola.so step fb_nola_$i 200 python tools/ab_lib.py tools/floating_fw_ab.py gpurun_out/fb_nola.npz 1 4 16 64 1024
+          step fb_la_$i 200 python tools/floating_fw_ab.py gpurun_out/fb_la.npz 1 4 16 64 1024
+        done
+        python tools/floating_fw_ab.py --compare gpurun_out/fb_nola.npz gpurun_out/fb_la.npz > gpurun_out/fb_bits.log 2>&1
+        grep -H "forward_ms\|bit_equal" gpurun_out/fb_nola_*.log gpurun_out/fb_la_*.log gpurun_out/fb_bits.log > gpurun_out/fb_ab.log; cat gpurun_out/fb_ab.log ;;
+  fbcand) for c in 4 16 64; do
+            ILQR_FB_CAND=$c step fbc_la_c$c 200 python tools/floating_fw_ab.py gpurun_out/fbc_la_c$c.npz 1 64
+          done
+          grep -H "forward_ms" gpurun_out/fbc_*.log > gpurun_out/fb_cand.log; cat gpurun_out/fb_cand.log ;;
   gtest) step pytest_gather 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_line_search.py tests/test_gpu_multi.py -m gpu -x -q --timeout 120 --timeout-method thread ;;
 esac
 done
