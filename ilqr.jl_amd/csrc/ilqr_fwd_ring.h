@@ -1423,6 +1423,9 @@ __device__ __forceinline__ void coop_trace(unsigned kind, unsigned gen, unsigned
 #ifndef ILQR_COOP_DEEP_FIRST
 #define ILQR_COOP_DEEP_FIRST 1
 #endif
+#ifndef ILQR_COOP_FRONTIER_DEEP
+#define ILQR_COOP_FRONTIER_DEEP 1
+#endif
 constexpr int COOP_DEEP_FRONT = 5;  // trials 1..5 known rejected: past a first quad or sixteen
 #ifndef ILQR_COOP_WAIT_TICKS
 #define ILQR_COOP_WAIT_TICKS 20000
@@ -1483,8 +1486,9 @@ __device__ __forceinline__ void coop_publish(const LSCoop& c, uint32_t gen, int 
 }
 
 // A published trajectory with trials left to hand out, the least speculative first (the
-// smallest distance of `next` past the trials its search has evaluated, then the smallest
-// `next`, then the first entry at or after this wave's rotated start); -1
+// smallest distance of `next` past the trials its search has evaluated, then the largest
+// `next` at the frontier — the smallest past it —, then the first entry at or after this
+// wave's rotated start); -1
 // if none. Relaxed
 // reads: a hint, the grab itself is exact. `unwritten`: a reserved list slot is not
 // written yet (its publisher is mid-way: the slot still holds another launch's entry).
@@ -1543,8 +1547,14 @@ __device__ __attribute__((unused)) int coop_find(const LSCoop& c, uint32_t gen, 
       // later trials are likely needed); 2 a speculative grab of a search still at its
       // first grab (round 6, ILQR_COOP_DEEP_FIRST; 0: classes 1 and 2 merge)
       const uint32_t cls = dk <= 1 ? 0u : ((ILQR_COOP_DEEP_FIRST && fr[k] >= COOP_DEEP_FRONT) ? 1u : 2u);
-      const uint64_t key = ((uint64_t)cls << 62) | ((uint64_t)dk << 55) |
-                           ((uint64_t)((uint32_t)nx[k] & 0x7FFFFFu) << 32) | (uint32_t)(base + 64 * k + l);
+      // within a class the smallest `next` first — except at the frontier (class 0), where
+      // the largest goes first (ILQR_COOP_FRONTIER_DEEP): a deep search's next grab before
+      // a fresh search's first (the co-headline fit 1.192-1.196 → 1.174-1.181 ms,
+      // iteration 6 834-847 → 819-842 µs; profiles/r06/coop_frontier_deep_ab_r06.log)
+      const uint32_t nk = (ILQR_COOP_FRONTIER_DEEP && cls == 0u) ? 0x7FFFFFu - ((uint32_t)nx[k] & 0x7FFFFFu)
+                                                                 : ((uint32_t)nx[k] & 0x7FFFFFu);
+      const uint64_t key = ((uint64_t)cls << 62) | ((uint64_t)dk << 55) | ((uint64_t)nk << 32) |
+                           (uint32_t)(base + 64 * k + l);
       if (nx[k] <= lim[k] && key < best) best = key;
     }
     // wave minimum

@@ -120,6 +120,16 @@ case $WHAT in
         done
         python tools/floating_fw_ab.py --compare gpurun_out/fb_nola.npz gpurun_out/fb_la.npz > gpurun_out/fb_bits.log 2>&1
         grep -H "forward_ms\|bit_equal" gpurun_out/fb_nola_*.log gpurun_out/fb_la_*.log gpurun_out/fb_bits.log > gpurun_out/fb_ab.log; cat gpurun_out/fb_ab.log ;;
+  fdeepab) for i in 1 2; do
+             ILQR_LIB=ilqr.jl_amd/lib/variants/libilqr_hip_fshallow.so MODES=coop step tail_fshallow_$i 200 python tools/tail_probe.py
+             MODES=coop step tail_prod_$i 200 python tools/tail_probe.py
+           done
+           for i in 1 2; do
+             ILQR_LIB=ilqr.jl_amd/lib/variants/libilqr_hip_fshallow.so step bench_fshallow_$i 300 python tools/ab_lib.py bench.py --no-cpu --no-secondary
+             step bench_prod_$i 300 python bench.py --no-cpu --no-secondary
+           done
+           grep -H "coop" gpurun_out/tail_fshallow_*.log gpurun_out/tail_prod_*.log > gpurun_out/fdeep_ab.log
+           for f in gpurun_out/bench_fshallow_*.log gpurun_out/bench_prod_*.log; do python -c "import json,sys; d=[json.loads(l) for l in open(sys.argv[1]) if l.startswith('{')][-1]; print(sys.argv[1], 'value', round(d['value'],1), 'co_headline', round(d['co_headline']['value'],1), 'fit5_ms', round(d['co_headline']['ms_per_fit'],4), 'dflt', round(d['fit_default_options']['batched_it_per_s'],1))" $f; done >> gpurun_out/fdeep_ab.log; cat gpurun_out/fdeep_ab.log ;;
   fbcand) for c in 4 16 64; do
             ILQR_FB_CAND=$c step fbc_la_c$c 200 python tools/floating_fw_ab.py gpurun_out/fbc_la_c$c.npz 1 64
           done
