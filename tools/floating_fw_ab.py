@@ -68,7 +68,13 @@ def main():
         # trial 1's x̄ against fb_step (the dynamics kernel) stepped under its ū
         xr = s.rollout(r1[0][:, 0], r1[1])
         dstep = (xr != r1[0]).sum().item()
-        rstep = ((xr - r1[0]).abs() / r1[0].abs().clamp_min(1e-300)).max().item()
+        relm = (xr - r1[0]).abs() / r1[0].abs().clamp_min(1e-300)
+        rstep = relm.max().item()
+        big = (relm > 1e-12).any(dim=2).any(dim=0).nonzero()  # first step off by more than 1e-12
+        t_off = int(big[0].item()) if big.numel() else -1
+        r1b = s.forward(x, u, d, K, pc)  # the same call again: the same bits
+        again = bool(torch.equal(r1b[0].view(torch.int64), r1[0].view(torch.int64)) and
+                     torch.equal(r1b[2].view(torch.int64), r1[2].view(torch.int64)))  # bits: NaN too
         r = s.forward(x, u, d, K, c1 * (1 - 1e-9))
         for k, v in zip(("x", "u", "cost", "trials", "status"), r):
             saved[f"B{nb}_{k}"] = v[:4].cpu().numpy()  # a few trajectories: the files travel back
@@ -77,7 +83,8 @@ def main():
         s.close()
         print(json.dumps({"B": nb, "forward_ms": float(np.median(ts)), "min_ms": float(np.min(ts)),
                           "trials_shrunk": int(r[3].max()),
-                          "x1_vs_fb_step_differing": dstep, "x1_vs_fb_step_rel": rstep}), flush=True)
+                          "x1_vs_fb_step_differing": dstep, "x1_vs_fb_step_rel": rstep,
+                          "x1_vs_fb_step_first_step_off_1e-12": t_off, "repeat_bit_equal": again}), flush=True)
     np.savez(out, **saved)
 
 
