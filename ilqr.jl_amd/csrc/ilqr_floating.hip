@@ -51,18 +51,39 @@ struct D1 {
   __device__ constexpr D1(double a) : v(a), d(0.0) {}
   __device__ constexpr D1(double a, double b) : v(a), d(b) {}
 };
-__device__ __forceinline__ D1 operator+(D1 a, D1 b) { return D1(a.v + b.v, a.d + b.d); }
-__device__ __forceinline__ D1 operator-(D1 a, D1 b) { return D1(a.v - b.v, a.d - b.d); }
+// The dual operators contract freely across one another once inlined (the file is built
+// with -ffp-contract=on, for the double path's sake: fb_rk_next): the linearisation's
+// products and sums fuse as they did before (−14 % per launch otherwise).
+#define FB_DUAL_CONTRACT _Pragma("clang fp contract(fast)")
+__device__ __forceinline__ D1 operator+(D1 a, D1 b) {
+  FB_DUAL_CONTRACT
+  return D1(a.v + b.v, a.d + b.d);
+}
+__device__ __forceinline__ D1 operator-(D1 a, D1 b) {
+  FB_DUAL_CONTRACT
+  return D1(a.v - b.v, a.d - b.d);
+}
 __device__ __forceinline__ D1 operator-(D1 a) { return D1(-a.v, -a.d); }
-__device__ __forceinline__ D1 operator*(D1 a, D1 b) { return D1(a.v * b.v, fma(a.v, b.d, a.d * b.v)); }
-__device__ __forceinline__ D1 operator*(double a, D1 b) { return D1(a * b.v, a * b.d); }
-__device__ __forceinline__ D1 operator*(D1 b, double a) { return D1(a * b.v, a * b.d); }
+__device__ __forceinline__ D1 operator*(D1 a, D1 b) {
+  FB_DUAL_CONTRACT
+  return D1(a.v * b.v, fma(a.v, b.d, a.d * b.v));
+}
+__device__ __forceinline__ D1 operator*(double a, D1 b) {
+  FB_DUAL_CONTRACT
+  return D1(a * b.v, a * b.d);
+}
+__device__ __forceinline__ D1 operator*(D1 b, double a) {
+  FB_DUAL_CONTRACT
+  return D1(a * b.v, a * b.d);
+}
 __device__ __forceinline__ D1 operator/(D1 a, D1 b) {
+  FB_DUAL_CONTRACT
   const double q = a.v / b.v;
   return D1(q, (a.d - q * b.d) / b.v);
 }
 __device__ __forceinline__ void sincos_s(double a, double& s, double& c) { sincos(a, &s, &c); }
 __device__ __forceinline__ void sincos_s(D1 a, D1& s, D1& c) {
+  FB_DUAL_CONTRACT
   double sv, cv;
   sincos(a.v, &sv, &cv);
   s = D1(sv, a.d * cv);
@@ -618,7 +639,7 @@ struct FbXch {
   double v[FB_XX + FB_NX][64];  // value-major: lane l's k-th value at v[k][l]
 };
 #endif
-constexpr int FB_FWD_WAVES = 3;
+constexpr int FB_FWD_WAVES = ILQR_FB_LOOKAHEAD ? 4 : 3;
 
 // every wave reaches it: its LDS writes done (lgkmcnt only — the rollout's global stores
 // stay in flight), then the workgroup barrier
@@ -637,13 +658,13 @@ __device__ __forceinline__ void fb_lds_wait() {
   asm volatile("" ::: "memory");
 }
 
-// RK4's bookkeeping of one component at stage st (fb_step's loop body): k = Δt·ẋ, the
-// sum k₁ + 2k₂ + 2k₃ + k₄ and the next stage's value (the step's result at st = 3).
-// Waves 0 and 1 of fb_rollout3 both run it on the joint angles and must agree to the bit
-// (wave 0's rotations are the stored angles'): no contraction, which the compiler would
-// otherwise decide per call site.
+// RK4's bookkeeping of one component at stage st (fb_step's loop body, the same
+// expressions): k = Δt·ẋ, the sum k₁ + 2k₂ + 2k₃ + k₄ and the next stage's value (the
+// step's result at st = 3). Waves 0, 1 and 3 of fb_rollout3 all run it on the joint
+// angles and must agree to the bit (the rotations of waves 0 and 3 are the stored
+// angles'): this file is built with -ffp-contract=on, so an FMA forms within one
+// expression only, never by the surrounding code.
 __device__ __forceinline__ double fb_rk_next(int st, double dt, double xd, double xb, double& acc) {
-#pragma clang fp contract(off)  // one rounding per operation wherever it is inlined
   const double k = dt * xd;
   const double w = (st == 0 || st == 3) ? 1.0 : 2.0;
   const double c = st == 2 ? 1.0 : 0.5;
@@ -682,40 +703,51 @@ __device__ double fb_rollout3(const FbModel& P, const FbFwd& a, int b, int T, do
     double xs[2][FB_NX][64];       // θ̇ (14, 15) every stage; all 16 at a step's start
     double u[FB_NU][64];
     int32_t useq[64];              // t + 1 once ūₜ is in u
+    int32_t rseq[64];              // s + 1 once stage s's R₀ is in R (wave 3 → wave 0)
     double out[3][64];
   };
   __shared__ Pipe X;  // named here: see the exchange of the two-barrier rollout below
   const double* x = a.x + (size_t)b * (T + 1) * FB_NX;
   const int S = 4 * T;
-  if (role == 0) {  // mass, one stage ahead
-    double th[FB_NX];  // only th[6], th[7] (the joint angles) are read by fb_rots
-#pragma unroll
-    for (int k = 0; k < FB_NX; ++k) th[k] = k == 6 || k == 7 ? x[k] : 0.0;
-    double xb6 = th[6], xb7 = th[7], acc6 = 0.0, acc7 = 0.0;
+  // the joint-0 hand-off word starts at 0 (the words of the previous rollout, or garbage
+  // at the kernel's start, are behind this barrier)
+  if (role == 3) __hip_atomic_store(&X.rseq[lane], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  fb_lds_barrier();
+  if (role == 0 || role == 3) {  // wave 0: mass; wave 3: joint 0's rotation — one stage ahead
+    // joint q's angle (wave 3: joint 0, wave 0: joint 1) and its rotation, as fb_rots
+    const int q = role == 0 ? 1 : 0;
+    double th = x[6 + q], xb = th, acc = 0.0;
     for (int s = 0; s <= S; ++s) {
-      if (s > 0) {  // stage s's angles from stage s − 1's θ̇
+      if (s > 0) {  // stage s's angle from stage s − 1's θ̇
         const int st = (s - 1) & 3;
-        const double v6 = X.xs[(s - 1) & 1][14][lane], v7 = X.xs[(s - 1) & 1][15][lane];
-        th[6] = fb_rk_next(st, P.dt, v6, xb6, acc6);
-        th[7] = fb_rk_next(st, P.dt, v7, xb7, acc7);
-        if (st == 3) {
-          xb6 = th[6];
-          xb7 = th[7];
-        }
+        th = fb_rk_next(st, P.dt, X.xs[(s - 1) & 1][14 + q][lane], xb, acc);
+        if (st == 3) xb = th;
       }
       if (s < S) {
         asm volatile("" ::: "memory");  // the model's constants re-read per stage (fb_step)
         double R[FB_NJ][9];
-        fb_rots(P, th, R);
-        FbSchur<double> F;
-        fb_mass(P, R, F);
-        const double* f = reinterpret_cast<const double*>(&F);
+        {
+          double sn, cs;
+          sincos_s(th, sn, cs);
+          joint_rot(P, q, cs, sn, R[q]);
+        }
 #pragma unroll
-        for (int k = 0; k < FB_SCHUR_N; ++k) X.F[s & 1][k][lane] = f[k];
+        for (int k = 0; k < 9; ++k) X.R[s & 1][9 * q + k][lane] = R[q][k];
+        if (role == 3) {
+          fb_lds_wait();  // R₀ written before its sequence word
+          __hip_atomic_store(&X.rseq[lane], s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        } else {
+          while (__hip_atomic_load(&X.rseq[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != s + 1)
+            __builtin_amdgcn_s_sleep(1);
+          asm volatile("" ::: "memory");
 #pragma unroll
-        for (int i = 0; i < FB_NJ; ++i)
+          for (int k = 0; k < 9; ++k) R[0][k] = X.R[s & 1][k][lane];
+          FbSchur<double> F;
+          fb_mass(P, R, F);
+          const double* f = reinterpret_cast<const double*>(&F);
 #pragma unroll
-          for (int k = 0; k < 9; ++k) X.R[s & 1][9 * i + k][lane] = R[i][k];
+          for (int k = 0; k < FB_SCHUR_N; ++k) X.F[s & 1][k][lane] = f[k];
+        }
       }
       fb_lds_barrier();  // stage s's inputs ready
     }

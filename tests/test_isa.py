@@ -120,8 +120,8 @@ def test_floating_kernels_have_no_scratch(tmp_path):
     to scratch (364 and 140 bytes per lane), and so did a two-wave forward whose second
     wave took both the mass and the solve (184 bytes)."""
     hipcc = HIPCC if os.path.exists(HIPCC) else shutil.which("hipcc")
-    cmd = [hipcc, "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-save-temps", "-c",
-           os.path.join(CSRC, "ilqr_floating.hip"), "-o", str(tmp_path / "fl.o")]
+    cmd = [hipcc, "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-ffp-contract=on", "-save-temps", "-c",
+           os.path.join(CSRC, "ilqr_floating.hip"), "-o", str(tmp_path / "fl.o")]  # as the Makefile
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=900, cwd=tmp_path)
     assert r.returncode == 0, r.stderr[-2000:]
     asm_file = [f for f in os.listdir(tmp_path) if f.endswith("gfx950.s")]
