@@ -614,7 +614,8 @@ struct FbFwd {
 // ū = u + α·δu equals u (then every later, smaller α rolls out the same); stores x̄
 // into xn, ū into un as it goes.
 //
-// It runs on three waves (fb_forward_kernel): a workgroup of three waves holds the same
+// The two-barrier rollout (ILQR_FB_LOOKAHEAD=0, rounds 5-6; the pipelined one below is the
+// product) runs on three waves (fb_forward_kernel): a workgroup of three waves holds the same
 // 64 (trajectory, trial) lanes and splits each step between them —
 //   wave 0 (mass):    the mass blocks and their factors (fb_mass) of every RK4 stage, from
 //                     the stage's joint angles;
@@ -672,13 +673,15 @@ __device__ __forceinline__ double fb_rk_next(int st, double dt, double xd, doubl
   return st < 3 ? xb + k * c : xb + (1.0 / 6.0) * acc;
 }
 
-// The three waves pipelined by one RK4 stage. A stage's mass blocks depend on its joint
+// Four waves pipelined by one RK4 stage. A stage's mass blocks depend on its joint
 // angles only, and the angles of stage s + 1 on stage s's state alone — θ̇ enters
 // q̇ = [·; ·; θ̇] as it is (fb_solve's kinematics), the solve only moves the velocities —
 // so wave 0 computes stage s + 1's rotations and factors while wave 1 works on stage s:
-//   wave 0 (mass):    from stage s's θ̇ (and its own running RK4 sum of the angles) the
-//                     angles of stage s + 1, their rotations (fb_rots) and factors
-//                     (fb_mass), into buffer (s + 1) & 1;
+//   wave 0 (mass):    from stage s's θ̇ (and its own running RK4 sum of the angle) joint
+//                     1's angle of stage s + 1 and its rotation, then (joint 0's from wave
+//                     3, behind a per-lane sequence word) the factors (fb_mass), into
+//                     buffer (s + 1) & 1;
+//   wave 3 (joint 0): the same for joint 0's angle and rotation;
 //   wave 1 (main):    stage s's bias from its state and the rotations of buffer s & 1,
 //                     b = ū − bias, the solve with that buffer's factors and the stage
 //                     update; stage s + 1's θ̇ (its whole state at a step's start) into the
@@ -688,9 +691,10 @@ __device__ __forceinline__ double fb_rk_next(int st, double dt, double xd, doubl
 //                     waits on it once a step, after its bias — ūₜ is in by then).
 // One workgroup barrier a stage (stage s's inputs ready); every buffer a wave reads in a
 // stage is written by the others in the stage before. Wave 1's stage is the bias and the
-// solve (the rotations, ≈ 2 sincos, no longer on it), wave 0's the rotations and the mass,
+// solve (the rotations, ≈ 2 sincos, no longer on it), wave 0's one rotation and the mass,
 // side by side: the one-stage-per-two-barriers rollout (ILQR_FB_LOOKAHEAD=0) ran the
-// rotations + bias beside the rotations + mass, then the solve. Same operations: the same bits.
+// rotations + bias beside the rotations + mass, then the solve. Same operations, and the
+// file built with -ffp-contract=on: the same bits.
 constexpr int FB_IN_N = FB_NU * FB_NX + 2 * FB_NU + 2 * FB_NX;  // a step's K, u, δu, x, x_traj
 constexpr int FB_IN_S = FB_IN_N + 2;  // row stride: 16 rows' same element in distinct bank pairs
 template <int CAND>
