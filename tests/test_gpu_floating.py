@@ -367,3 +367,33 @@ def test_floating_device_conserves_world_linear_momentum(gpu, name):
     p1 = floating_linear_momentum_world(x1, model)
     assert np.abs(p0).max() > 1.0
     assert np.abs(p1 - p0).max() / np.abs(p0).max() < 1e-7, (p0, p1)
+
+
+@pytest.mark.parametrize("nb", [1, 9, 70])
+def test_floating_forward_rollout_equals_stepping_the_dynamics(gpu, nb):
+    """The forward's trial-1 x̄ equals stepping the dynamics kernel (fb_step) under its ū,
+    bit for bit — at 64, 16 and 4 lanes a trajectory (B = 1, 9, 70), i.e. for every split of
+    the RK4 step over the forward's waves (ilqr_floating.hip is built with
+    -ffp-contract=on: DESIGN.md §4 'Then four waves'); and a second call repeats its bits."""
+    T = 60
+    x, u = script_batch(nb, T, seed=nb)
+    u = u + 0.3 * np.random.default_rng(nb).standard_normal(u.shape)
+    fj, _, _ = rbd_floating_arm(jet_ns())
+    for t in range(T):
+        x[:, t + 1] = fj(x[:, t], u[:, t])
+    tl = CF.derivative_tiles(x, u, fj, *rbd_cost_quads())
+    from oracle import cref
+    d, K, _ = cref.tiles_backward(tl, mu=0.01, symmetrize=True)
+    s = FloatingSolver(rbd_example_problem(), T, nb)
+    try:
+        args = [torch.from_numpy(a).cuda() for a in (x, u, d, K)]
+        pc = torch.full((nb,), float("inf"), dtype=torch.float64, device="cuda")
+        xn, un, cost, trials, st = [v.clone() for v in s.forward(*args, pc)]
+        xr = s.rollout(xn[:, 0], un)
+        again = s.forward(*args, pc)
+    finally:
+        s.close()
+    assert trials.tolist() == [1] * nb and torch.isfinite(xn).all()
+    assert torch.equal(xr.view(torch.int64), xn.view(torch.int64))
+    assert torch.equal(again[0].view(torch.int64), xn.view(torch.int64))
+    assert torch.equal(again[2].view(torch.int64), cost.view(torch.int64))
