@@ -164,80 +164,114 @@ __device__ __forceinline__ void fb_rots(const FbModel& P, const S (&x)[FB_NX], S
   }
 }
 
+// The bias in pieces (the forward splits them over waves; fb_bias composes them — the
+// same expressions either way, so the same bits under -ffp-contract=on):
+//   fb_outward<N>     the outward pass through joints 0..N−1: bodies 0..N's twists and
+//                     velocity-product accelerations;
+//   fb_body_force     body i's own force I·a + v ×* (I·v);
+//   fb_transmit       across joint i−1: τ_{i−1} and the force in body i−1's frame.
 template <class S>
-__device__ __forceinline__ void fb_bias(const FbModel& P, const S (&R)[FB_NJ][9], const S (&x)[FB_NX],
-                                        S (&q)[FB_NU]) {
-  // --- bias, recursive Newton-Euler at q̈ = 0, zero gravity (:65) -----------------------
-  // outward: v_{i+1} = X v_i + s q̇, a_{i+1} = X a_i + v_{i+1} × (s q̇) (a₀ = 0)
+struct FbMotion {
   S vw[FB_NJ + 1][3], vv[FB_NJ + 1][3], aw[FB_NJ + 1][3], av[FB_NJ + 1][3];
+};
+// outward: v_{i+1} = X v_i + s q̇, a_{i+1} = X a_i + v_{i+1} × (s q̇) (a₀ = 0); reads x[8..15]
+template <int NJO, class S>
+__device__ __forceinline__ void fb_outward(const FbModel& P, const S (&R)[FB_NJ][9], const S (&x)[FB_NX],
+                                           FbMotion<S>& M) {
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
-    vw[0][k] = x[8 + k];
-    vv[0][k] = x[11 + k];
-    aw[0][k] = 0.0;
-    av[0][k] = 0.0;
+    M.vw[0][k] = x[8 + k];
+    M.vv[0][k] = x[11 + k];
+    M.aw[0][k] = 0.0;
+    M.av[0][k] = 0.0;
   }
 #pragma unroll
-  for (int i = 0; i < FB_NJ; ++i) {
+  for (int i = 0; i < NJO; ++i) {
     S pw[3], t[3], sw[3], c1[3], c2[3];
-    crossm(P.p[i], vw[i], pw);
+    crossm(P.p[i], M.vw[i], pw);
 #pragma unroll
-    for (int k = 0; k < 3; ++k) t[k] = vv[i][k] - pw[k];
-    rot_t(R[i], vw[i], vw[i + 1]);
-    rot_t(R[i], t, vv[i + 1]);
+    for (int k = 0; k < 3; ++k) t[k] = M.vv[i][k] - pw[k];
+    rot_t(R[i], M.vw[i], M.vw[i + 1]);
+    rot_t(R[i], t, M.vv[i + 1]);
     const S qd = x[14 + i];
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
       sw[k] = P.ax[i][k] * qd;
-      vw[i + 1][k] = vw[i + 1][k] + sw[k];
+      M.vw[i + 1][k] = M.vw[i + 1][k] + sw[k];
     }
     if (i == 0) {  // a₀ = 0
 #pragma unroll
-      for (int k = 0; k < 3; ++k) aw[1][k] = av[1][k] = 0.0;
+      for (int k = 0; k < 3; ++k) M.aw[1][k] = M.av[1][k] = 0.0;
     } else {
-      crossm(P.p[i], aw[i], pw);
+      crossm(P.p[i], M.aw[i], pw);
 #pragma unroll
-      for (int k = 0; k < 3; ++k) t[k] = av[i][k] - pw[k];
-      rot_t(R[i], aw[i], aw[i + 1]);
-      rot_t(R[i], t, av[i + 1]);
+      for (int k = 0; k < 3; ++k) t[k] = M.av[i][k] - pw[k];
+      rot_t(R[i], M.aw[i], M.aw[i + 1]);
+      rot_t(R[i], t, M.av[i + 1]);
     }
-    crossm(vw[i + 1], sw, c1);
-    crossm(vv[i + 1], sw, c2);
+    crossm(M.vw[i + 1], sw, c1);
+    crossm(M.vv[i + 1], sw, c2);
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-      aw[i + 1][k] = aw[i + 1][k] + c1[k];
-      av[i + 1][k] = av[i + 1][k] + c2[k];
+      M.aw[i + 1][k] = M.aw[i + 1][k] + c1[k];
+      M.av[i + 1][k] = M.av[i + 1][k] + c2[k];
     }
   }
+}
+// body i's own force: I·(w, v) = (Io w + h × v, m v − h × w), f = I a + v ×* (I v)
+template <class S>
+__device__ __forceinline__ void fb_body_force(const FbModel& P, int i, const FbMotion<S>& M, S (&bn)[3],
+                                              S (&bf)[3]) {
+  S pn[3], pf[3], an[3], af[3], t1[3], t2[3];
+  crossm(P.h[i], M.vv[i], t1);
+  crossm(P.h[i], M.vw[i], t2);
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+    pn[r] = P.Io[i][3 * r] * M.vw[i][0] + P.Io[i][3 * r + 1] * M.vw[i][1] + P.Io[i][3 * r + 2] * M.vw[i][2] + t1[r];
+    pf[r] = P.m[i] * M.vv[i][r] - t2[r];
+  }
+  crossm(P.h[i], M.av[i], t1);
+  crossm(P.h[i], M.aw[i], t2);
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+    an[r] = P.Io[i][3 * r] * M.aw[i][0] + P.Io[i][3 * r + 1] * M.aw[i][1] + P.Io[i][3 * r + 2] * M.aw[i][2] + t1[r];
+    af[r] = P.m[i] * M.av[i][r] - t2[r];
+  }
+  S c1[3], c2[3], c3[3];
+  crossm(M.vw[i], pn, c1);
+  crossm(M.vv[i], pf, c2);
+  crossm(M.vw[i], pf, c3);
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    bn[k] = an[k] + (c1[k] + c2[k]);
+    bf[k] = af[k] + c3[k];
+  }
+}
+// τ_{i−1} and the force across joint i−1 (i > 0): f' = Rc f, n' = Rc n + p × f'
+template <class S>
+__device__ __forceinline__ void fb_transmit(const FbModel& P, const S (&R)[FB_NJ][9], int i, const S (&bn)[3],
+                                            const S (&bf)[3], S& tau, S (&fn)[3], S (&ff)[3]) {
+  tau = dotm(P.ax[i - 1], bn);
+  S rn[3], pfx[3];
+  rot(R[i - 1], bf, ff);
+  rot(R[i - 1], bn, rn);
+  crossm(P.p[i - 1], ff, pfx);
+#pragma unroll
+  for (int k = 0; k < 3; ++k) fn[k] = rn[k] + pfx[k];
+}
+
+template <class S>
+__device__ __forceinline__ void fb_bias(const FbModel& P, const S (&R)[FB_NJ][9], const S (&x)[FB_NX],
+                                        S (&q)[FB_NU]) {
+  // --- bias, recursive Newton-Euler at q̈ = 0, zero gravity (:65) -----------------------
+  FbMotion<S> M;
+  fb_outward<FB_NJ>(P, R, x, M);
   // inward: f_i = I_i a_i + v_i ×* (I_i v_i) + X_{i+1}ᵀ f_{i+1}, τ_i = s_iᵀ f_i
   S fn[3], ff[3], tau[FB_NJ];
 #pragma unroll
   for (int i = FB_NJ; i >= 0; --i) {
-    // I·(w, v) = (Io w + h × v, m v − h × w)
-    S pn[3], pf[3], an[3], af[3], t1[3], t2[3];
-    crossm(P.h[i], vv[i], t1);
-    crossm(P.h[i], vw[i], t2);
-#pragma unroll
-    for (int r = 0; r < 3; ++r) {
-      pn[r] = P.Io[i][3 * r] * vw[i][0] + P.Io[i][3 * r + 1] * vw[i][1] + P.Io[i][3 * r + 2] * vw[i][2] + t1[r];
-      pf[r] = P.m[i] * vv[i][r] - t2[r];
-    }
-    crossm(P.h[i], av[i], t1);
-    crossm(P.h[i], aw[i], t2);
-#pragma unroll
-    for (int r = 0; r < 3; ++r) {
-      an[r] = P.Io[i][3 * r] * aw[i][0] + P.Io[i][3 * r + 1] * aw[i][1] + P.Io[i][3 * r + 2] * aw[i][2] + t1[r];
-      af[r] = P.m[i] * av[i][r] - t2[r];
-    }
-    S c1[3], c2[3], c3[3], bn[3], bf[3];
-    crossm(vw[i], pn, c1);
-    crossm(vv[i], pf, c2);
-    crossm(vw[i], pf, c3);
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      bn[k] = an[k] + (c1[k] + c2[k]);
-      bf[k] = af[k] + c3[k];
-    }
+    S bn[3], bf[3];
+    fb_body_force(P, i, M, bn, bf);
     if (i < FB_NJ) {
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
@@ -245,14 +279,8 @@ __device__ __forceinline__ void fb_bias(const FbModel& P, const S (&R)[FB_NJ][9]
         bf[k] = bf[k] + ff[k];
       }
     }
-    if (i > 0) {  // τ and the force across joint i−1: f' = Rc f, n' = Rc n + p × f'
-      tau[i - 1] = dotm(P.ax[i - 1], bn);
-      S rn[3], pfx[3];
-      rot(R[i - 1], bf, ff);
-      rot(R[i - 1], bn, rn);
-      crossm(P.p[i - 1], ff, pfx);
-#pragma unroll
-      for (int k = 0; k < 3; ++k) fn[k] = rn[k] + pfx[k];
+    if (i > 0) {
+      fb_transmit(P, R, i, bn, bf, tau[i - 1], fn, ff);
     } else {
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
@@ -303,8 +331,20 @@ struct FbSchur {
   }
 };
 
+// M in two pieces (the forward's waves hand the first to the second; fb_mass composes them):
+//   fb_crba   the composite-rigid-body recursion, tip to base: the base's composite
+//             (m, h, Io), the joint block Mⱼⱼ and the base-joint columns M₀ⱼ;
+//   fb_schur  M₀₀⁻¹ in closed form, Y = M₀₀⁻¹M₀ⱼ and the joint block's Schur complement.
 template <class S>
-__device__ __forceinline__ void fb_mass(const FbModel& P, const S (&R)[FB_NJ][9], FbSchur<S>& F) {
+struct FbCrba {
+  S cI[9];
+  S ch[3];
+  double cm;
+  S Mjj[FB_NJ][FB_NJ];
+  S Mb[FB_NJ][6];
+};
+template <class S>
+__device__ __forceinline__ void fb_crba(const FbModel& P, const S (&R)[FB_NJ][9], FbCrba<S>& C) {
   // --- M, composite-rigid-body algorithm (:61), tip to base ------------------------------
   // composite of bodies k..NJ in body k's frame: (m, h, Io)
   double cm = P.m[FB_NJ];
@@ -339,8 +379,8 @@ __device__ __forceinline__ void fb_mass(const FbModel& P, const S (&R)[FB_NJ][9]
     }
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-      F.Mb[j][k] = n[k];
-      F.Mb[j][3 + k] = f[k];
+      C.Mb[j][k] = n[k];
+      C.Mb[j][3 + k] = f[k];
     }
     // composite of body j: own inertia + the child composite moved across joint j:
     // h' = Rc h, Io' = Rc Io Rcᵀ + m(|p|²1 − p pᵀ) + 2(p·h')1 − p h'ᵀ − h' pᵀ, h'' = h' + m p
@@ -367,17 +407,34 @@ __device__ __forceinline__ void fb_mass(const FbModel& P, const S (&R)[FB_NJ][9]
     for (int k = 0; k < 3; ++k) ch[k] = P.h[j][k] + (hp[k] + cm * pj[k]);
     cm = P.m[j] + cm;
   }
+#pragma unroll
+  for (int k = 0; k < 9; ++k) C.cI[k] = cI[k];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) C.ch[k] = ch[k];
+  C.cm = cm;
+#pragma unroll
+  for (int i = 0; i < FB_NJ; ++i)
+#pragma unroll
+    for (int j = 0; j < FB_NJ; ++j) C.Mjj[i][j] = Mjj[i][j];
+}
 
+template <class S>
+__device__ __forceinline__ void fb_schur(const FbCrba<S>& C, FbSchur<S>& F) {
+  const double cm = C.cm;
+#pragma unroll
+  for (int j = 0; j < FB_NJ; ++j)
+#pragma unroll
+    for (int k = 0; k < 6; ++k) F.Mb[j][k] = C.Mb[j][k];
   // --- M₀₀⁻¹ and the Schur complement of M₀₀ ---------------------------------------------
   // M₀₀ = [[Io, [h×]], [[h×]ᵀ, m1]]: with c = h/m and I_c = Io − m(|c|²1 − c cᵀ),
   // M₀₀⁻¹(n, f) = (w, f/m + c × w), w = I_c⁻¹(n − c × f)
   F.minv = 1.0 / cm;
 #pragma unroll
-  for (int k = 0; k < 3; ++k) F.cc[k] = ch[k] * F.minv;
+  for (int k = 0; k < 3; ++k) F.cc[k] = C.ch[k] * F.minv;
   S Ic[6];  // I_c lower triangle: 00, 10, 11, 20, 21, 22
   {
     const S c2 = dotm(F.cc, F.cc);
-    auto ent = [&](int r, int k) { return cI[3 * r + k] - cm * ((r == k ? c2 : S(0.0)) - F.cc[r] * F.cc[k]); };
+    auto ent = [&](int r, int k) { return C.cI[3 * r + k] - cm * ((r == k ? c2 : S(0.0)) - F.cc[r] * F.cc[k]); };
     Ic[0] = ent(0, 0);
     Ic[1] = ent(1, 0);
     Ic[2] = ent(1, 1);
@@ -400,12 +457,20 @@ __device__ __forceinline__ void fb_mass(const FbModel& P, const S (&R)[FB_NJ][9]
   for (int i = 0; i < FB_NJ; ++i)
 #pragma unroll
     for (int j = 0; j < FB_NJ; ++j) {
-      S e = Mjj[i][j];
+      S e = C.Mjj[i][j];
 #pragma unroll
       for (int k = 0; k < 6; ++k) e = e - F.Mb[i][k] * F.Y[j][k];
       F.Sc[i][j] = e;
     }
 }
+
+template <class S>
+__device__ __forceinline__ void fb_mass(const FbModel& P, const S (&R)[FB_NJ][9], FbSchur<S>& F) {
+  FbCrba<S> C;
+  fb_crba(P, R, C);
+  fb_schur(C, F);
+}
+
 
 template <class S>
 __device__ __forceinline__ void fb_solve(const FbSchur<S>& F, const S (&b)[FB_NU], const S (&x)[FB_NX],

@@ -130,6 +130,10 @@ case $WHAT in
            done
            grep -H "coop" gpurun_out/tail_fshallow_*.log gpurun_out/tail_prod_*.log > gpurun_out/fdeep_ab.log
            for f in gpurun_out/bench_fshallow_*.log gpurun_out/bench_prod_*.log; do python -c "import json,sys; d=[json.loads(l) for l in open(sys.argv[1]) if l.startswith('{')][-1]; print(sys.argv[1], 'value', round(d['value'],1), 'co_headline', round(d['co_headline']['value'],1), 'fit5_ms', round(d['co_headline']['ms_per_fit'],4), 'dflt', round(d['fit_default_options']['batched_it_per_s'],1))" $f; done >> gpurun_out/fdeep_ab.log; cat gpurun_out/fdeep_ab.log ;;
+  fbprev) ILQR_LIB=ilqr.jl_amd/lib/variants/libilqr_hip_prev.so step fbp_prev 200 python tools/ab_lib.py tools/floating_fw_ab.py gpurun_out/fbp_prev.npz 1 9 70 1024
+          step fbp_new 200 python tools/floating_fw_ab.py gpurun_out/fbp_new.npz 1 9 70 1024
+          python tools/floating_fw_ab.py --compare gpurun_out/fbp_prev.npz gpurun_out/fbp_new.npz > gpurun_out/fbp_bits.log 2>&1
+          grep -H "forward_ms\|bit_equal" gpurun_out/fbp_prev.log gpurun_out/fbp_new.log gpurun_out/fbp_bits.log > gpurun_out/fbp_ab.log; cat gpurun_out/fbp_ab.log ;;
   fbcand) for c in 4 16 64; do
             ILQR_FB_CAND=$c step fbc_la_c$c 200 python tools/floating_fw_ab.py gpurun_out/fbc_la_c$c.npz 1 64
           done
