@@ -9,9 +9,10 @@
 //     costs' derivative tiles (:81-109, :134-153) in closed form — the costs are
 //     diagonal weighted squares (:85-116);
 //   * the Riccati recursion: the wide tiles kernel (ilqr_tiles.hip, nx ≤ 16, nu ≤ 8);
-//   * fb_forward_kernel: forward_pass (forward_pass.jl:55-93) — four line-search trials
-//     of a trajectory at once, one per lane, the first accepted one kept (bit for bit
-//     the sequential search's choice: every trial is independent of the others); each
+//   * fb_forward_kernel: forward_pass (forward_pass.jl:55-93) — 4 to 64 line-search
+//     trials of a trajectory at once, one per lane, each RK4 step split over the four
+//     waves of a workgroup, the first accepted trial kept (bit for bit the sequential
+//     search's choice: every trial is independent of the others); each
 //     trial stores its x̄, ū as it rolls out (trial 1 into x̄, ū, the others into a
 //     per-lane slot), so an accepted later trial is taken from its slot, never rolled
 //     out again;
