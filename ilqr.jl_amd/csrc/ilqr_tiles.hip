@@ -230,6 +230,7 @@ __global__ __launch_bounds__(256) void tiles_backward_kernel(TileParams P, int B
 // real ones are unchanged (the LDLᵀ pivots of the padding come last and are exactly μ).
 // ---------------------------------------------------------------------------------
 constexpr int TW_NX = 16, TW_NU = 8;
+constexpr int TW_BUF_MIN_B = 64;  // batches from here load their tiles with raw buffer loads
 constexpr int TW_LDS = 128 + 128 + 16 * 17;  // G rows, [H | g] rows, symmetrisation tile
 
 __device__ __forceinline__ double pick4(const double (&v)[TW_NU], int q, int base) {
@@ -247,26 +248,38 @@ struct WideTile {
   d4 Lxe;        // lx[q+4r] in column 8
 };
 
-__device__ bool tiles_backward_wide_wave(const TileParams& P, int b, int T, int nx, int nu,
-                                         double* __restrict__ d_out, double* __restrict__ K_out,
-                                         double mu, double* lds) {
-  const int l = threadIdx.x & 63;
-  const int c = l & 15;
-  const int q = l >> 4;
-  const bool cx = c < nx;
-  const bool cu = c < nu;
-  const bool c8 = c == 8;
-  const size_t bt = (size_t)b * T;
-  const size_t sxx = (size_t)nx * nx, sxu = (size_t)nx * nu, suu = (size_t)nu * nu;
-  const double* A0 = P.A + bt * sxx;
-  const double* B0 = P.B + bt * sxu;
-  const double* lx0 = P.lx + bt * nx;
-  const double* lu0 = P.lu + bt * nu;
-  const double* lxx0 = P.lxx + bt * sxx;
-  const double* lux0 = P.lux ? P.lux + bt * sxu : nullptr;
-  const double* luu0 = P.luu + bt * suu;
-
-  auto load = [&](int t, WideTile& s) {
+// A step's tiles, zero-padded to 16 × 8, for lane (q, c) of the wide kernel.
+//   WideLoads<false> (small batches): ldz_async per element — a lone trajectory's step is
+//     a latency chain, and this way it is 4 % faster (B = 1, T = 1000: 2.09 against 2.18 ms);
+//   WideLoads<true> (large batches): raw buffer loads — a lane's offset is fixed for the
+//     whole recursion (its element, or out of range when its row or column is padding:
+//     the bounds check returns 0) and the step moves a scalar offset, so a load is one
+//     instruction where ldz_async's address and zero selects and 64-bit address
+//     arithmetic were ≈180 VALU instructions a step (B = 4096, T = 100: 1.07 → 0.85 ms).
+// The same values either way (profiles/r06/tiles_buf_ab_r06.log: bit-equal gains).
+template <bool BUF>
+struct WideLoads;
+template <>
+struct WideLoads<false> {
+  const double *A0, *B0, *lx0, *lu0, *lxx0, *lux0, *luu0;
+  size_t sxx, sxu, suu;
+  int nx, nu, q, c;
+  __device__ WideLoads(const TileParams& P, int b, int T, int nx_, int nu_, int q_, int c_)
+      : nx(nx_), nu(nu_), q(q_), c(c_) {
+    const size_t bt = (size_t)b * T;
+    sxx = (size_t)nx * nx;
+    sxu = (size_t)nx * nu;
+    suu = (size_t)nu * nu;
+    A0 = P.A + bt * sxx;
+    B0 = P.B + bt * sxu;
+    lx0 = P.lx + bt * nx;
+    lu0 = P.lu + bt * nu;
+    lxx0 = P.lxx + bt * sxx;
+    lux0 = P.lux ? P.lux + bt * sxu : nullptr;
+    luu0 = P.luu + bt * suu;
+  }
+  __device__ __forceinline__ void load(int t, WideTile& s) const {
+    const bool cx = c < nx, cu = c < nu, c8 = c == 8;
     const double* A = A0 + (size_t)t * sxx;
     const double* Bm = B0 + (size_t)t * sxu;
     const double* lxx = lxx0 + (size_t)t * sxx;
@@ -293,7 +306,82 @@ __device__ bool tiles_backward_wide_wave(const TileParams& P, int b, int T, int 
       s.Lue[r] = ldz_async(ru & cu, luu + i * nu + c, luu) + ldz_async(ru & c8, lu + i, lu);
     }
     s.Lux[2] = s.Lux[3] = s.Lue[2] = s.Lue[3] = 0.0;
-  };
+  }
+};
+template <>
+struct WideLoads<true> {
+  __amdgpu_buffer_rsrc_t rA, rB, rXX, rX, rU, rUU, rUX;
+  uint32_t oA[4], oB[4], oXe[4], oUX[2], oUU[2], oUe[2];
+  uint32_t sxx, sxu, suu, nx, nu;
+  __device__ WideLoads(const TileParams& P, int b, int T, int nx_, int nu_, int q, int c)
+      : sxx((uint32_t)(nx_ * nx_)), sxu((uint32_t)(nx_ * nu_)), suu((uint32_t)(nu_ * nu_)), nx((uint32_t)nx_),
+        nu((uint32_t)nu_) {
+    constexpr uint32_t OOR = 0x80000000u;
+    const size_t bt = (size_t)b * T;
+    auto rsrc = [&](const double* base, size_t n) {
+      return buffer_rsrc(const_cast<double*>(uniform_ptr(base)), (uint32_t)(n * sizeof(double)));
+    };
+    rA = rsrc(P.A + bt * sxx, (size_t)T * sxx);
+    rB = rsrc(P.B + bt * sxu, (size_t)T * sxu);
+    rXX = rsrc(P.lxx + bt * sxx, (size_t)T * sxx);
+    rX = rsrc(P.lx + bt * nx, (size_t)T * nx);
+    rU = rsrc(P.lu + bt * nu, (size_t)T * nu);
+    rUU = rsrc(P.luu + bt * suu, (size_t)T * suu);
+    rUX = P.lux ? rsrc(P.lux + bt * sxu, (size_t)T * sxu) : rsrc(P.A, 0);  // no lux: every load 0
+    const bool cx = c < nx_, cu = c < nu_, c8 = c == 8;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const int i = 4 * kk + q;
+      const bool ri = i < nx_;
+      oA[kk] = (ri & cx) ? (uint32_t)(i * nx_ + c) * 8 : OOR;
+      oB[kk] = (ri & cu) ? (uint32_t)(i * nu_ + c) * 8 : OOR;
+      oXe[kk] = (ri & c8) ? (uint32_t)i * 8 : OOR;
+    }
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int i = q + 4 * r;
+      const bool ru = i < nu_;
+      oUX[r] = (ru & cx) ? (uint32_t)(i * nx_ + c) * 8 : OOR;
+      oUU[r] = (ru & cu) ? (uint32_t)(i * nu_ + c) * 8 : OOR;
+      oUe[r] = (ru & c8) ? (uint32_t)i * 8 : OOR;
+    }
+  }
+  __device__ static __forceinline__ double ldb(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0));
+  }
+  __device__ __forceinline__ void load(int t, WideTile& s) const {
+    const uint32_t sA = (uint32_t)t * sxx * 8, sB = (uint32_t)t * sxu * 8;
+    const uint32_t sX = (uint32_t)t * nx * 8, sU = (uint32_t)t * nu * 8, sUU = (uint32_t)t * suu * 8;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      s.fA[kk] = ldb(rA, oA[kk], sA);
+      s.fB[kk] = ldb(rB, oB[kk], sB);
+      s.Lxx[kk] = ldb(rXX, oA[kk], sA);
+      s.Lxe[kk] = ldb(rX, oXe[kk], sX);
+    }
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      s.Lux[r] = ldb(rUX, oUX[r], sB);
+      s.Lue[r] = ldb(rUU, oUU[r], sUU) + ldb(rU, oUe[r], sU);
+    }
+    s.Lux[2] = s.Lux[3] = s.Lue[2] = s.Lue[3] = 0.0;
+  }
+};
+
+template <bool BUF>
+__device__ bool tiles_backward_wide_wave(const TileParams& P, int b, int T, int nx, int nu,
+                                         double* __restrict__ d_out, double* __restrict__ K_out,
+                                         double mu, double* lds) {
+  const int l = threadIdx.x & 63;
+  const int c = l & 15;
+  const int q = l >> 4;
+  const bool cx = c < nx;
+  const bool c8 = c == 8;
+  const size_t bt = (size_t)b * T;
+  const size_t sxx = (size_t)nx * nx;
+
+  WideLoads<BUF> L(P, b, T, nx, nu, q, c);
+  auto load = [&](int t, WideTile& s) { L.load(t, s); };
 
   double* Gl = lds;        // G[j][c], j < 8
   double* Hl = lds + 128;  // [H | g][j][c], j < 8, c ≤ 8
@@ -403,6 +491,7 @@ __device__ bool tiles_backward_wide_wave(const TileParams& P, int b, int T, int 
   return __any(nan);
 }
 
+template <bool BUF>
 __global__ __launch_bounds__(256) void tiles_backward_wide_kernel(TileParams P, int B, int T, int nx,
                                                                   int nu, double* __restrict__ d,
                                                                   double* __restrict__ K,
@@ -412,7 +501,7 @@ __global__ __launch_bounds__(256) void tiles_backward_wide_kernel(TileParams P, 
   const int w = threadIdx.x >> 6;
   const int b = blockIdx.x * 4 + w;
   if (b >= B) return;
-  const bool nan = tiles_backward_wide_wave(P, b, T, nx, nu, d, K, mu, lds + w * TW_LDS);
+  const bool nan = tiles_backward_wide_wave<BUF>(P, b, T, nx, nu, d, K, mu, lds + w * TW_LDS);
   if (status && (threadIdx.x & 63) == 0) status[b] = nan ? ILQR_TRAJ_NAN : ILQR_TRAJ_OK;
 }
 
@@ -431,7 +520,10 @@ hipError_t launch_tiles_backward(int nx, int nu, const TileParams& p, int B, int
   const int grid = (B + 3) / 4;
   if (!tiles_narrow(nx, nu)) {
     if (!tiles_supported(nx, nu)) return hipErrorInvalidValue;
-    tiles_backward_wide_kernel<<<grid, 256, 0, s>>>(p, B, T, nx, nu, d, K, status, mu);
+    if (B >= TW_BUF_MIN_B)
+      tiles_backward_wide_kernel<true><<<grid, 256, 0, s>>>(p, B, T, nx, nu, d, K, status, mu);
+    else
+      tiles_backward_wide_kernel<false><<<grid, 256, 0, s>>>(p, B, T, nx, nu, d, K, status, mu);
     return hipGetLastError();
   }
 #define ILQR_TILES_CASE(NXV, NUV)                                                              \

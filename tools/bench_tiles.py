@@ -49,6 +49,9 @@ def measure(nx, nu, B, T, reps=50, device=0):
             assert rc == 0, rc
         run(_ptr(st))
         ok = bool((st == 0).all().item())
+        if os.environ.get("TILES_SAVE"):  # the gains of a few trajectories, for a bit comparison of two builds
+            import numpy as np
+            np.savez(f"{os.environ['TILES_SAVE']}_{nx}x{nu}_B{B}.npz", d=d[:8].cpu().numpy(), K=K[:8].cpu().numpy())
         for _ in range(5):
             run()
         torch.cuda.synchronize(dev)

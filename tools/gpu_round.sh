@@ -134,6 +134,15 @@ case $WHAT in
           step fbp_new 200 python tools/floating_fw_ab.py gpurun_out/fbp_new.npz 1 9 70 1024
           python tools/floating_fw_ab.py --compare gpurun_out/fbp_prev.npz gpurun_out/fbp_new.npz > gpurun_out/fbp_bits.log 2>&1
           grep -H "forward_ms\|bit_equal" gpurun_out/fbp_prev.log gpurun_out/fbp_new.log gpurun_out/fbp_bits.log > gpurun_out/fbp_ab.log; cat gpurun_out/fbp_ab.log ;;
+  tilesab) for i in 1 2; do
+            for v in prev new; do
+              L=""; [ $v = prev ] && L=ilqr.jl_amd/lib/variants/libilqr_hip_prev.so
+              ILQR_LIB=$L TILES_SAVE=gpurun_out/tl_$v step tiles_${v}_1k_$i 200 python tools/ab_lib.py tools/bench_tiles.py 1 1000
+              ILQR_LIB=$L TILES_SAVE=gpurun_out/tl_$v step tiles_${v}_4k_$i 200 python tools/ab_lib.py tools/bench_tiles.py 4096 100
+            done
+          done
+          for f in gpurun_out/tl_prev_*.npz; do python tools/floating_fw_ab.py --compare $f ${f/tl_prev/tl_new}; done > gpurun_out/tiles_bits.log 2>&1
+          grep -H '"nx": 16' gpurun_out/tiles_*_[12].log | sed 's/"algorithmic_bytes.*us_per_step/us_per_step/' > gpurun_out/tiles_ab.log; cat gpurun_out/tiles_ab.log gpurun_out/tiles_bits.log | cut -c1-200 ;;
   fbcand) for c in 4 16 64; do
             ILQR_FB_CAND=$c step fbc_la_c$c 200 python tools/floating_fw_ab.py gpurun_out/fbc_la_c$c.npz 1 64
           done
