@@ -142,7 +142,7 @@ case $WHAT in
             done
           done
           for f in gpurun_out/tl_prev_*.npz; do python tools/floating_fw_ab.py --compare $f ${f/tl_prev/tl_new}; done > gpurun_out/tiles_bits.log 2>&1
-          grep -H '"nx": 16' gpurun_out/tiles_*_[12].log | sed 's/"algorithmic_bytes.*us_per_step/us_per_step/' > gpurun_out/tiles_ab.log; cat gpurun_out/tiles_ab.log gpurun_out/tiles_bits.log | cut -c1-200 ;;
+          grep -H '"nx"' gpurun_out/tiles_*_[12].log | sed 's/"algorithmic_bytes.*us_per_step/us_per_step/' > gpurun_out/tiles_ab.log; cat gpurun_out/tiles_ab.log gpurun_out/tiles_bits.log | cut -c1-200 ;;
   fbcand) for c in 4 16 64; do
             ILQR_FB_CAND=$c step fbc_la_c$c 200 python tools/floating_fw_ab.py gpurun_out/fbc_la_c$c.npz 1 64
           done
