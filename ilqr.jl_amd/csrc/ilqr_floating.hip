@@ -1382,14 +1382,21 @@ bool fb_model(const ilqr_floating* m, ilqr::FbModel& P) {
   return true;
 }
 
-// line-search lanes per trajectory: 64 up to B = 4 and 16 up to B = 64 (the waves those
-// batches fill would otherwise run a few live lanes), 4 past that
-int fb_cand(int B) {
+// line-search lanes per trajectory: the most (64, 16 or 4) with which the launch still
+// has at most one workgroup per CU (B·CAND ≤ 256·64) — a round of trials costs one
+// rollout's latency whatever its width, so idle CUs take further trials (5-iteration
+// fits from the script's start, profiles/r06/floating_cand_fit_r06.log: B = 256 13.25 →
+// 12.91 ms per iteration with 64 against 16, B = 1024 22.9 → 22.2 ms with 16 against 4)
+// — and whose trial slots (B·CAND rollouts) stay within 4 GiB
+int fb_cand(int B, int T) {
   if (const char* e = std::getenv("ILQR_FB_CAND")) {  // A/B measurement override: 4, 16 or 64
     const int c = std::atoi(e);
     if (c == 4 || c == 16 || c == 64) return c;
   }
-  return B <= 4 ? 64 : (B <= 64 ? 16 : ilqr::FB_CAND);
+  const size_t slot = 8 * ((size_t)(T + 1) * ilqr::FB_NX + (size_t)T * ilqr::FB_NU);
+  for (int c : {64, 16})
+    if ((size_t)B * c <= 256 * 64 && (size_t)B * c * slot <= (size_t(4) << 30)) return c;
+  return ilqr::FB_CAND;
 }
 
 ilqr::LSParams fb_ls(const ilqr_options* o) {
@@ -1507,7 +1514,7 @@ ilqr_status ilqr_floating_create(ilqr_floating_handle** out, int device, const i
   alloc(&h->iters, 4 * B);
   alloc(&h->move, 4 * B);
   alloc(&h->words, 4 * 4);
-  h->cand = fb_cand(batch);
+  h->cand = fb_cand(batch, T);
   alloc(&h->slots, 8 * B * h->cand * ((T + 1) * nx + (size_t)T * nu));
   alloc(&h->model_dev, sizeof(ilqr::FbModel));
   if (e == hipSuccess) e = hipMemcpy(h->model_dev, &h->model, sizeof(ilqr::FbModel), hipMemcpyHostToDevice);

@@ -202,12 +202,13 @@ def test_floating_backward_forward_vs_closure_oracle(gpu):
     assert int(trials[0]) > 1
 
 
-@pytest.mark.parametrize("nb,shrink,alpha0", [(17, 0.5, 1.0), (4, 0.7, 0.9), (70, 0.5, 1.0)])
-def test_floating_forward_slots_rounds_and_partial_workgroups(gpu, nb, shrink, alpha0):
+@pytest.mark.parametrize("nb,shrink,alpha0,cand", [(17, 0.5, 1.0, 16), (4, 0.7, 0.9, 64), (70, 0.5, 1.0, 4)])
+def test_floating_forward_slots_rounds_and_partial_workgroups(gpu, nb, shrink, alpha0, cand, monkeypatch):
     """The line search across rounds of trials: prev_cost set per trajectory so that the
     accepted trial falls anywhere in 1..6 or the search exhausts at max_trials = 6 —
     trials > 1 come from their lanes' slots, an exhausted search returns the inputs;
-    every trajectory as the closure oracle's forward_pass. B = 17 runs 16 lanes a
+    every trajectory as the closure oracle's forward_pass, the lanes a trajectory pinned
+    (ILQR_FB_CAND; by default such batches run 64). B = 17 runs 16 lanes a
     trajectory (17 · 16 lanes: the last workgroup partly empty), B = 4 runs 64 (one round
     covers every trial) with a non-dyadic shrink (trial j's α = α₀ multiplied by shrink
     j − 1 times, as the reference's `α *= shrink`), B = 70 runs 4 (trials 5-6 in a second
@@ -239,6 +240,7 @@ def test_floating_forward_slots_rounds_and_partial_workgroups(gpu, nb, shrink, a
                                           shrink=shrink)
     assert len(set(tro[ok].tolist())) >= 3 and ((~ok).any() or nb <= 4)
     o = _lib.default_options(max_trials=mt, alpha0=alpha0, shrink=shrink)
+    monkeypatch.setenv("ILQR_FB_CAND", str(cand))  # the lanes a trajectory, read at creation
     s = FloatingSolver(rbd_example_problem(), T, nb)
     try:
         xn, un, cost, trials, st = s.forward(*(torch.from_numpy(a).cuda() for a in (x, u, d, K, prev)),
@@ -369,8 +371,8 @@ def test_floating_device_conserves_world_linear_momentum(gpu, name):
     assert np.abs(p1 - p0).max() / np.abs(p0).max() < 1e-7, (p0, p1)
 
 
-@pytest.mark.parametrize("nb", [1, 9, 70])
-def test_floating_forward_rollout_equals_stepping_the_dynamics(gpu, nb):
+@pytest.mark.parametrize("nb,cand", [(1, 64), (9, 16), (70, 4)])
+def test_floating_forward_rollout_equals_stepping_the_dynamics(gpu, nb, cand, monkeypatch):
     """The forward's trial-1 x̄ equals stepping the dynamics kernel (fb_step) under its ū,
     bit for bit — at 64, 16 and 4 lanes a trajectory (B = 1, 9, 70), i.e. for every split of
     the RK4 step over the forward's waves (ilqr_floating.hip is built with
@@ -384,6 +386,7 @@ def test_floating_forward_rollout_equals_stepping_the_dynamics(gpu, nb):
     tl = CF.derivative_tiles(x, u, fj, *rbd_cost_quads())
     from oracle import cref
     d, K, _ = cref.tiles_backward(tl, mu=0.01, symmetrize=True)
+    monkeypatch.setenv("ILQR_FB_CAND", str(cand))
     s = FloatingSolver(rbd_example_problem(), T, nb)
     try:
         args = [torch.from_numpy(a).cuda() for a in (x, u, d, K)]

@@ -143,6 +143,12 @@ case $WHAT in
           done
           for f in gpurun_out/tl_prev_*.npz; do python tools/floating_fw_ab.py --compare $f ${f/tl_prev/tl_new}; done > gpurun_out/tiles_bits.log 2>&1
           grep -H '"nx"' gpurun_out/tiles_*_[12].log | sed 's/"algorithmic_bytes.*us_per_step/us_per_step/' > gpurun_out/tiles_ab.log; cat gpurun_out/tiles_ab.log gpurun_out/tiles_bits.log | cut -c1-200 ;;
+  fbcandfit) for i in 1 2; do
+               for c in ${CANDS:-4 16}; do
+                 ILQR_FB_CAND=$c step fbfit_c${c}_$i 300 python tools/bench_floating.py 5 2 ${FBB:-256 1024}
+               done
+             done
+             grep -H ms_per_iteration gpurun_out/fbfit_c*.log | sed 's/"workload[^,]*,//' > gpurun_out/fbfit_cand.log; cat gpurun_out/fbfit_cand.log | cut -c1-220 ;;
   fbcand) for c in 4 16 64; do
             ILQR_FB_CAND=$c step fbc_la_c$c 200 python tools/floating_fw_ab.py gpurun_out/fbc_la_c$c.npz 1 64
           done
