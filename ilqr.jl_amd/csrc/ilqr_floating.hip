@@ -473,9 +473,11 @@ __device__ __forceinline__ void fb_mass(const FbModel& P, const S (&R)[FB_NJ][9]
 }
 
 
+// fb_solve in two pieces (the forward's waves split them; fb_solve composes them):
+//   fb_accel  M v̇ = b, the velocities' rates ẋ[8..15];
+//   fb_kin    the kinematics ẋ[0..7] from the state alone, no solve.
 template <class S>
-__device__ __forceinline__ void fb_solve(const FbSchur<S>& F, const S (&b)[FB_NU], const S (&x)[FB_NX],
-                                         S (&xd)[FB_NX]) {
+__device__ __forceinline__ void fb_accel(const FbSchur<S>& F, const S (&b)[FB_NU], S (&xd)[FB_NX]) {
   // --- M v̇ = b: y₀ = M₀₀⁻¹ b₀, then (Mⱼⱼ − M₀ⱼᵀ Y) v̇ⱼ = bⱼ − M₀ⱼᵀ y₀ ------------------------
   S y0[6];
   {
@@ -498,7 +500,9 @@ __device__ __forceinline__ void fb_solve(const FbSchur<S>& F, const S (&b)[FB_NU
   for (int k = 0; k < 6; ++k) xd[8 + k] = y0[k] - (F.Y[0][k] * q0 + F.Y[1][k] * q1);
   xd[14] = q0;
   xd[15] = q1;
-
+}
+template <class S>
+__device__ __forceinline__ void fb_kin(const S (&x)[FB_NX], S (&xd)[FB_NX]) {
   // --- kinematics (:66): q̇ = [pdot_from_w(p, ω); v; θ̇] ----------------------------------
   const S pv[3] = {x[0], x[1], x[2]};
   const S w0[3] = {x[8], x[9], x[10]};
@@ -512,6 +516,12 @@ __device__ __forceinline__ void fb_solve(const FbSchur<S>& F, const S (&b)[FB_NU
   for (int k = 0; k < 3; ++k) xd[3 + k] = x[11 + k];
 #pragma unroll
   for (int j = 0; j < FB_NJ; ++j) xd[6 + j] = x[14 + j];
+}
+template <class S>
+__device__ __forceinline__ void fb_solve(const FbSchur<S>& F, const S (&b)[FB_NU], const S (&x)[FB_NX],
+                                         S (&xd)[FB_NX]) {
+  fb_accel(F, b, xd);
+  fb_kin(x, xd);
 }
 
 template <class S>
@@ -696,6 +706,8 @@ struct FbFwd {
 // three waves issue side by side. Same operations as fb_step: the same bits.
 constexpr int FB_SCHUR_N = (int)(sizeof(FbSchur<double>) / sizeof(double));
 static_assert(sizeof(FbSchur<double>) == FB_SCHUR_N * sizeof(double), "FbSchur<double> is doubles only");
+constexpr int FB_CRBA_N = (int)(sizeof(FbCrba<double>) / sizeof(double));
+static_assert(sizeof(FbCrba<double>) == FB_CRBA_N * sizeof(double), "FbCrba<double> is doubles only");
 #ifndef ILQR_FB_LOOKAHEAD
 #define ILQR_FB_LOOKAHEAD 1
 #endif
@@ -716,6 +728,50 @@ __device__ __forceinline__ void fb_lds_barrier() {
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
 }
+
+// Trace build (ILQR_FB_TRACE, never the product): per role, the ticks of the 100 MHz
+// counter each wave of workgroup 0 spends working between barriers, waiting at them and
+// polling its sequence words, summed over rollouts (ilqr_debug_fb_trace).
+#ifdef ILQR_FB_TRACE
+__device__ unsigned long long g_fbt[4][8];
+#define FBT_DECL uint64_t fbt_prev = __builtin_amdgcn_s_memrealtime(), fbt_work = 0, fbt_wait = 0, fbt_poll = 0, fbt_n = 0, fbt_mark = fbt_prev, fbt_sub[4] = {0, 0, 0, 0};
+#define FBT_BAR()                                           \
+  do {                                                      \
+    const uint64_t a_ = __builtin_amdgcn_s_memrealtime();   \
+    fb_lds_barrier();                                       \
+    const uint64_t b_ = __builtin_amdgcn_s_memrealtime();   \
+    fbt_work += a_ - fbt_prev;                              \
+    fbt_wait += b_ - a_;                                    \
+    fbt_prev = fbt_mark = b_;                               \
+    ++fbt_n;                                                \
+  } while (0)
+#define FBT_POLL_BEGIN const uint64_t p0_ = __builtin_amdgcn_s_memrealtime();
+#define FBT_POLL_END fbt_poll += __builtin_amdgcn_s_memrealtime() - p0_;
+// phase k's end (k < 4): the doubles of v computed before the mark (sub-phase ticks)
+#define FBT_MARK(k, v)                                                               \
+  do {                                                                               \
+    const double* m_ = reinterpret_cast<const double*>(&(v));                       \
+    for (int i_ = 0; i_ < (int)(sizeof(v) / sizeof(double)); ++i_) asm volatile("" ::"v"(m_[i_])); \
+    const uint64_t t_ = __builtin_amdgcn_s_memrealtime();                            \
+    fbt_sub[k] += t_ - fbt_mark;                                                     \
+    fbt_mark = t_;                                                                   \
+  } while (0)
+#define FBT_FLUSH                                           \
+  if (blockIdx.x == 0 && lane == 0) {                       \
+    atomicAdd(&g_fbt[role][0], (unsigned long long)fbt_work); \
+    atomicAdd(&g_fbt[role][1], (unsigned long long)fbt_wait); \
+    atomicAdd(&g_fbt[role][2], (unsigned long long)fbt_poll); \
+    atomicAdd(&g_fbt[role][3], (unsigned long long)fbt_n);    \
+    for (int k_ = 0; k_ < 4; ++k_) atomicAdd(&g_fbt[role][4 + k_], (unsigned long long)fbt_sub[k_]); \
+  }
+#else
+#define FBT_DECL
+#define FBT_BAR() fb_lds_barrier()
+#define FBT_POLL_BEGIN
+#define FBT_POLL_END
+#define FBT_MARK(k, v)
+#define FBT_FLUSH
+#endif
 
 #if ILQR_FB_LOOKAHEAD
 // LDS writes done (lgkmcnt only), no barrier
@@ -742,25 +798,31 @@ __device__ __forceinline__ double fb_rk_next(int st, double dt, double xd, doubl
 // Four waves pipelined by one RK4 stage. A stage's mass blocks depend on its joint
 // angles only, and the angles of stage s + 1 on stage s's state alone — θ̇ enters
 // q̇ = [·; ·; θ̇] as it is (fb_solve's kinematics), the solve only moves the velocities —
-// so wave 0 computes stage s + 1's rotations and factors while wave 1 works on stage s:
+// so waves 0 and 3 compute stage s + 1's rotations and mass while wave 1 works on stage s:
 //   wave 0 (mass):    from stage s's θ̇ (and its own running RK4 sum of the angle) joint
 //                     1's angle of stage s + 1 and its rotation, then (joint 0's from wave
-//                     3, behind a per-lane sequence word) the factors (fb_mass), into
-//                     buffer (s + 1) & 1;
-//   wave 3 (joint 0): the same for joint 0's angle and rotation;
-//   wave 1 (main):    stage s's bias from its state and the rotations of buffer s & 1,
-//                     b = ū − bias, the solve with that buffer's factors and the stage
-//                     update; stage s + 1's θ̇ (its whole state at a step's start) into the
+//                     3, behind a per-lane sequence word) the CRBA (fb_crba), into buffer
+//                     (s + 1) & 1;
+//   wave 3 (joint 0): the same for joint 0's angle and rotation; then stage s's factors
+//                     (fb_schur of wave 0's CRBA of the stage before), to wave 1 behind a
+//                     second sequence word, and the kinematics: stage s + 1's positions
+//                     and angles from stage s's (fb_kin + RK4; the step's state at its end);
+//   wave 1 (main):    stage s's bias from its velocities and the rotations of buffer s & 1,
+//                     b = ū − bias, the solve for the velocities' rates (fb_accel) with the
+//                     factors and their stage update; stage s + 1's velocities into the
 //                     state buffer (s + 1) & 1;
 //   wave 2 (control): at a step's start, ūₜ from x̄ₜ, its cost and Σ(ū − u)², storing ū,
 //                     and ūₜ to wave 1 through LDS behind a per-lane sequence word (wave 1
 //                     waits on it once a step, after its bias — ūₜ is in by then).
-// One workgroup barrier a stage (stage s's inputs ready); every buffer a wave reads in a
-// stage is written by the others in the stage before. Wave 1's stage is the bias and the
-// solve (the rotations, ≈ 2 sincos, no longer on it), wave 0's one rotation and the mass,
-// side by side: the one-stage-per-two-barriers rollout (ILQR_FB_LOOKAHEAD=0) ran the
-// rotations + bias beside the rotations + mass, then the solve. Same operations, and the
-// file built with -ffp-contract=on: the same bits.
+// One workgroup barrier a stage (stage s's inputs ready); a buffer a wave reads behind a
+// barrier is written by the others in the stage before, one behind a sequence word in
+// the same stage. The split follows tools/fb_trace.py's per-wave ticks: with fb_mass
+// and the kinematics on waves 0 and 1 (round 6's first pipeline) wave 0's rotation +
+// mass took ≈ 1.90 µs a stage and wave 1's bias + solve + update 1.81 µs, while wave 3
+// idled 1.27 µs of its 1.93. The one-stage-per-two-barriers rollout
+// (ILQR_FB_LOOKAHEAD=0) ran the rotations + bias beside the rotations + mass, then the
+// solve. Same operations, and the file built with -ffp-contract=on: the same bits
+// (DESIGN.md §4).
 constexpr int FB_IN_N = FB_NU * FB_NX + 2 * FB_NU + 2 * FB_NX;  // a step's K, u, δu, x, x_traj
 constexpr int FB_IN_S = FB_IN_N + 2;  // row stride: 16 rows' same element in distinct bank pairs
 template <int CAND>
@@ -768,58 +830,116 @@ __device__ double fb_rollout3(const FbModel& P, const FbFwd& a, int b, int T, do
                               double* __restrict__ un, double& du2, bool& same, int role, int lane, bool run) {
   struct Pipe {
     double in[64 / CAND][FB_IN_S];  // wave 2's copy of its trajectories' step inputs
-    double F[2][FB_SCHUR_N][64];   // value-major: lane l's k-th value at [k][l]
+    double C[2][FB_CRBA_N][64];    // value-major: lane l's k-th value at [k][l]
+    double F[FB_SCHUR_N][64];      // wave 1's stage's factors
     double R[2][FB_NJ * 9][64];
-    double xs[2][FB_NX][64];       // θ̇ (14, 15) every stage; all 16 at a step's start
+    double xs[2][FB_NX][64];       // velocities (8-15) every stage; all 16 at a step's start
     double u[FB_NU][64];
     int32_t useq[64];              // t + 1 once ūₜ is in u
-    int32_t rseq[64];              // s + 1 once stage s's R₀ is in R (wave 3 → wave 0)
+    int32_t fseq[64];              // s + 1 once stage s's factors are in F (wave 3 → wave 1)
+    int32_t pseq[64];              // t once x̄ₜ's positions and angles are in xs (wave 3 → 2)
     double out[3][64];
   };
   __shared__ Pipe X;  // named here: see the exchange of the two-barrier rollout below
+  FBT_DECL
   const double* x = a.x + (size_t)b * (T + 1) * FB_NX;
   const int S = 4 * T;
-  // the joint-0 hand-off word starts at 0 (the words of the previous rollout, or garbage
-  // at the kernel's start, are behind this barrier)
-  if (role == 3) __hip_atomic_store(&X.rseq[lane], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  fb_lds_barrier();
-  if (role == 0 || role == 3) {  // wave 0: mass; wave 3: joint 0's rotation — one stage ahead
-    // joint q's angle (wave 3: joint 0, wave 0: joint 1) and its rotation, as fb_rots
-    const int q = role == 0 ? 1 : 0;
-    double th = x[6 + q], xb = th, acc = 0.0;
+  // the hand-off words start at 0 (the words of the previous rollout, or garbage at the
+  // kernel's start, are behind this barrier)
+  if (role == 3) {
+    __hip_atomic_store(&X.fseq[lane], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __hip_atomic_store(&X.pseq[lane], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+  FBT_BAR();
+  if (role == 0) {  // mass: the joints' angles and rotations, the CRBA — one stage ahead
+    double th[FB_NJ], xb[FB_NJ], acc[FB_NJ];
+#pragma unroll
+    for (int q = 0; q < FB_NJ; ++q) th[q] = xb[q] = x[6 + q];
     for (int s = 0; s <= S; ++s) {
-      if (s > 0) {  // stage s's angle from stage s − 1's θ̇
+      if (s > 0) {  // stage s's angles from stage s − 1's θ̇
         const int st = (s - 1) & 3;
-        th = fb_rk_next(st, P.dt, X.xs[(s - 1) & 1][14 + q][lane], xb, acc);
-        if (st == 3) xb = th;
+#pragma unroll
+        for (int q = 0; q < FB_NJ; ++q) {
+          th[q] = fb_rk_next(st, P.dt, X.xs[(s - 1) & 1][14 + q][lane], xb[q], acc[q]);
+          if (st == 3) xb[q] = th[q];
+        }
       }
       if (s < S) {
         asm volatile("" ::: "memory");  // the model's constants re-read per stage (fb_step)
-        double R[FB_NJ][9];
-        {
-          double sn, cs;
-          sincos_s(th, sn, cs);
-          joint_rot(P, q, cs, sn, R[q]);
-        }
+        double xa[FB_NX], R[FB_NJ][9];
 #pragma unroll
-        for (int k = 0; k < 9; ++k) X.R[s & 1][9 * q + k][lane] = R[q][k];
-        if (role == 3) {
-          fb_lds_wait();  // R₀ written before its sequence word
-          __hip_atomic_store(&X.rseq[lane], s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        } else {
-          while (__hip_atomic_load(&X.rseq[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != s + 1)
-            __builtin_amdgcn_s_sleep(1);
-          asm volatile("" ::: "memory");
+        for (int q = 0; q < FB_NJ; ++q) xa[6 + q] = th[q];
+        fb_rots(P, xa, R);  // reads the angles only
 #pragma unroll
-          for (int k = 0; k < 9; ++k) R[0][k] = X.R[s & 1][k][lane];
-          FbSchur<double> F;
-          fb_mass(P, R, F);
-          const double* f = reinterpret_cast<const double*>(&F);
+        for (int k = 0; k < FB_NJ * 9; ++k) X.R[s & 1][k][lane] = R[k / 9][k % 9];
+        FBT_MARK(0, R);
+        FbCrba<double> C;  // fb_mass's first piece (wave 3 runs the second)
+        fb_crba(P, R, C);
+        const double* c = reinterpret_cast<const double*>(&C);
 #pragma unroll
-          for (int k = 0; k < FB_SCHUR_N; ++k) X.F[s & 1][k][lane] = f[k];
-        }
+        for (int k = 0; k < FB_CRBA_N; ++k) X.C[s & 1][k][lane] = c[k];
+        FBT_MARK(1, C);
       }
-      fb_lds_barrier();  // stage s's inputs ready
+      FBT_BAR();  // stage s's inputs ready
+    }
+  } else if (role == 3) {
+    // the factors of stage s − 1 (fb_schur of wave 0's CRBA, to wave 1 behind a sequence
+    // word), then the kinematics: the positions and angles of stage s from stage s − 1's
+    // velocities (the step's state at its end)
+    double th[FB_NJ], xb[FB_NJ], acc[FB_NJ];
+#pragma unroll
+    for (int q = 0; q < FB_NJ; ++q) th[q] = xb[q] = x[6 + q];
+    double pos[6], pb[6], pacc[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) pos[k] = pb[k] = x[k];
+    FBT_BAR();  // stage 0's rotations and CRBA ready
+    for (int s = 1; s <= S; ++s) {
+      const int st = (s - 1) & 3;
+      asm volatile("" ::: "memory");  // the model's constants re-read per stage (fb_step)
+      {
+        FbCrba<double> C;
+        double* c = reinterpret_cast<double*>(&C);
+#pragma unroll
+        for (int k = 0; k < FB_CRBA_N; ++k) c[k] = X.C[(s - 1) & 1][k][lane];
+        FbSchur<double> F;
+        fb_schur(C, F);
+        const double* f = reinterpret_cast<const double*>(&F);
+#pragma unroll
+        for (int k = 0; k < FB_SCHUR_N; ++k) X.F[k][lane] = f[k];
+        fb_lds_wait();  // the factors written before their sequence word
+        __hip_atomic_store(&X.fseq[lane], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        FBT_MARK(0, F);
+      }
+      double xv[FB_NX], xd[FB_NX];
+#pragma unroll
+      for (int k = 0; k < 6; ++k) xv[k] = pos[k];
+      xv[6] = xv[7] = 0.0;  // not read by fb_kin
+#pragma unroll
+      for (int k = 8; k < FB_NX; ++k) xv[k] = X.xs[(s - 1) & 1][k][lane];
+      fb_kin(xv, xd);
+#pragma unroll
+      for (int k = 0; k < 6; ++k) pos[k] = fb_rk_next(st, P.dt, xd[k], pb[k], pacc[k]);
+#pragma unroll
+      for (int q = 0; q < FB_NJ; ++q) th[q] = fb_rk_next(st, P.dt, xv[14 + q], xb[q], acc[q]);
+      if (st == 3) {  // the step's end: x_{t+1}'s positions and angles
+        double* xo = xn + (size_t)(s >> 2) * FB_NX;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+          pb[k] = pos[k];
+          X.xs[0][k][lane] = pos[k];
+          if (run) xo[k] = pos[k];
+        }
+#pragma unroll
+        for (int q = 0; q < FB_NJ; ++q) {
+          xb[q] = th[q];
+          X.xs[0][6 + q][lane] = th[q];
+          if (run) xo[6 + q] = th[q];
+        }
+        fb_lds_wait();  // written before their sequence word
+        __hip_atomic_store(&X.pseq[lane], s >> 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      FBT_MARK(1, pos);
+      FBT_BAR();  // stage s − 1's factors ready
     }
   } else if (role == 2) {  // control: ūₜ (:72-73), its cost (:187-190), Σ(ū − u)²
     const double* u = a.u + (size_t)b * T * FB_NU;
@@ -864,23 +984,34 @@ __device__ double fb_rollout3(const FbModel& P, const FbFwd& a, int b, int T, do
     double xb[FB_NX];
     double cost = 0.0, s2 = 0.0;
     bool eq = true;
-    __hip_atomic_store(&X.useq[lane], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    stage_in(0);
-    fb_lds_barrier();
-    for (int t = 0; t < T; ++t) {
-#pragma unroll
-      for (int k = 0; k < FB_NX; ++k) xb[k] = X.xs[0][k][lane];  // x̄ₜ (x̄₁ = x₁, :65)
-      double dx[FB_NX], ub[FB_NU];
-#pragma unroll
-      for (int k = 0; k < FB_NX; ++k) dx[k] = xb[k] - rx[k];
-      // Kₜ(x̄ₜ − xₜ): each row's sum in k order, the eight rows side by side
-      double kd[FB_NU];
+    // Kₜ(x̄ₜ − xₜ): each row's sum in k order, the eight rows side by side. Its first half
+    // (k < 8: the positions and angles, wave 3's, known mid-way through the step's last
+    // stage) runs in that stage; after the barrier only the velocities' half is left
+    double kd[FB_NU];
+    auto kd_lo = [&]() {
 #pragma unroll
       for (int j = 0; j < FB_NU; ++j) kd[j] = 0.0;
 #pragma unroll
-      for (int k = 0; k < FB_NX; ++k)
+      for (int k = 0; k < FB_NX / 2; ++k) {
+        const double dxk = X.xs[0][k][lane] - rx[k];
 #pragma unroll
-        for (int j = 0; j < FB_NU; ++j) kd[j] = fma(rK[j * FB_NX + k], dx[k], kd[j]);
+        for (int j = 0; j < FB_NU; ++j) kd[j] = fma(rK[j * FB_NX + k], dxk, kd[j]);
+      }
+    };
+    __hip_atomic_store(&X.useq[lane], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    stage_in(0);
+    FBT_BAR();
+    kd_lo();
+    for (int t = 0; t < T; ++t) {
+#pragma unroll
+      for (int k = 0; k < FB_NX; ++k) xb[k] = X.xs[0][k][lane];  // x̄ₜ (x̄₁ = x₁, :65)
+      double ub[FB_NU];
+#pragma unroll
+      for (int k = FB_NX / 2; k < FB_NX; ++k) {
+        const double dxk = xb[k] - rx[k];
+#pragma unroll
+        for (int j = 0; j < FB_NU; ++j) kd[j] = fma(rK[j * FB_NX + k], dxk, kd[j]);
+      }
 #pragma unroll
       for (int j = 0; j < FB_NU; ++j) {
         const double uj = ru[j];
@@ -896,6 +1027,7 @@ __device__ double fb_rollout3(const FbModel& P, const FbFwd& a, int b, int T, do
       for (int j = 0; j < FB_NU; ++j) X.u[j][lane] = ub[j];
       fb_lds_wait();  // ūₜ written before its sequence word
       __hip_atomic_store(&X.useq[lane], t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      FBT_MARK(0, ub);
 #pragma unroll
       for (int j = 0; j < FB_NU; ++j)
         if (run) un[(size_t)t * FB_NU + j] = ub[j];
@@ -903,10 +1035,20 @@ __device__ double fb_rollout3(const FbModel& P, const FbFwd& a, int b, int T, do
 #pragma unroll
       for (int k = 0; k < FB_NQ; ++k) ev[k] = xt ? xb[k] - rxt[k] : xb[k];
       cost = cost + stage_cost(P, ev, ub);
-      fb_lds_barrier();
+      FBT_MARK(1, cost);
+      FBT_BAR();
       if (t + 1 < T) stage_in((size_t)(t + 1));
-#pragma unroll 1
-      for (int st = 1; st < 4; ++st) fb_lds_barrier();
+      FBT_MARK(2, cost);
+      FBT_BAR();
+      FBT_BAR();
+      if (t + 1 < T) {  // x̄ₜ₊₁'s first half from wave 3, then its part of Kₜ₊₁(x̄ₜ₊₁ − xₜ₊₁)
+        while (__hip_atomic_load(&X.pseq[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != t + 1)
+          __builtin_amdgcn_s_sleep(1);
+        asm volatile("" ::: "memory");
+        kd_lo();
+        FBT_MARK(3, kd);
+      }
+      FBT_BAR();
     }
 #pragma unroll
     for (int k = 0; k < FB_NX; ++k) xb[k] = X.xs[0][k][lane];  // x̄_N
@@ -914,7 +1056,7 @@ __device__ double fb_rollout3(const FbModel& P, const FbFwd& a, int b, int T, do
     X.out[0][lane] = cost;  // the outcome to waves 0 and 1
     X.out[1][lane] = s2;
     X.out[2][lane] = eq ? 1.0 : 0.0;
-  } else {  // main: bias, solve, stage update
+  } else {  // main: bias, solve, the velocities' stage update
     double xb[FB_NX], xs[FB_NX], acc[FB_NX], ub[FB_NU];
 #pragma unroll
     for (int k = 0; k < FB_NX; ++k) {
@@ -923,7 +1065,7 @@ __device__ double fb_rollout3(const FbModel& P, const FbFwd& a, int b, int T, do
       if (run) xn[k] = xb[k];
       X.xs[0][k][lane] = xb[k];
     }
-    fb_lds_barrier();
+    FBT_BAR();
     for (int s = 0; s < S; ++s) {
       const int t = s >> 2, st = s & 3;
       asm volatile("" ::: "memory");
@@ -934,13 +1076,20 @@ __device__ double fb_rollout3(const FbModel& P, const FbFwd& a, int b, int T, do
         for (int k = 0; k < 9; ++k) R[i][k] = X.R[s & 1][9 * i + k][lane];
       double bb[FB_NU];
       fb_bias(P, R, xs, bb);
-      if (st == 0) {
-        // the bias before the wait (else the compiler sinks it behind the wait)
+      FBT_MARK(0, bb);
+      // the bias before the waits (else the compiler sinks it behind them)
 #pragma unroll
-        for (int j = 0; j < FB_NU; ++j) asm volatile("" ::"v"(bb[j]));
+      for (int j = 0; j < FB_NU; ++j) asm volatile("" ::"v"(bb[j]));
+      FBT_POLL_BEGIN
+      if (st == 0)
         while (__hip_atomic_load(&X.useq[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != t + 1)
           __builtin_amdgcn_s_sleep(1);
-        asm volatile("" ::: "memory");
+      FBT_MARK(3, bb);
+      while (__hip_atomic_load(&X.fseq[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != s + 1)
+        __builtin_amdgcn_s_sleep(1);
+      FBT_POLL_END
+      asm volatile("" ::: "memory");
+      if (st == 0) {
 #pragma unroll
         for (int j = 0; j < FB_NU; ++j) ub[j] = X.u[j][lane];
       }
@@ -949,30 +1098,33 @@ __device__ double fb_rollout3(const FbModel& P, const FbFwd& a, int b, int T, do
       FbSchur<double> F;
       double* f = reinterpret_cast<double*>(&F);
 #pragma unroll
-      for (int k = 0; k < FB_SCHUR_N; ++k) f[k] = X.F[s & 1][k][lane];
+      for (int k = 0; k < FB_SCHUR_N; ++k) f[k] = X.F[k][lane];
       double k[FB_NX];
-      fb_solve(F, bb, xs, k);
+      fb_accel(F, bb, k);
+      FBT_MARK(1, k);
+      // the velocities (wave 3 keeps the positions and angles)
 #pragma unroll
-      for (int i = 0; i < FB_NX; ++i) xs[i] = fb_rk_next(st, P.dt, k[i], xb[i], acc[i]);
-      if (st < 3) {
-        X.xs[(s + 1) & 1][14][lane] = xs[14];
-        X.xs[(s + 1) & 1][15][lane] = xs[15];
-      } else {
+      for (int i = 8; i < FB_NX; ++i) {
+        xs[i] = fb_rk_next(st, P.dt, k[i], xb[i], acc[i]);
+        X.xs[(s + 1) & 1][i][lane] = xs[i];
+      }
+      if (st == 3) {
 #pragma unroll
-        for (int i = 0; i < FB_NX; ++i) {
+        for (int i = 8; i < FB_NX; ++i) {
           xb[i] = xs[i];
-          X.xs[0][i][lane] = xs[i];
           if (run) xn[(size_t)(t + 1) * FB_NX + i] = xs[i];
         }
       }
-      fb_lds_barrier();  // stage s + 1's state ready
+      FBT_MARK(2, xs);
+      FBT_BAR();  // stage s + 1's velocities ready
     }
   }
-  fb_lds_barrier();
+  FBT_BAR();
   const double cost = X.out[0][lane];
   du2 = X.out[1][lane];
   same = X.out[2][lane] != 0.0;
-  fb_lds_barrier();  // read before the next rollout writes
+  FBT_BAR();  // read before the next rollout writes
+  FBT_FLUSH
   return cost;
 }
 #else
@@ -1699,3 +1851,12 @@ ilqr_status ilqr_floating_fit_ex(ilqr_floating_handle* h, const ilqr_options* o,
 }
 
 }  // extern "C"
+
+#ifdef ILQR_FB_TRACE
+// the trace build's per-role totals (work, barrier wait, poll wait, barriers), then reset
+extern "C" int ilqr_debug_fb_trace(unsigned long long* out) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(ilqr::g_fbt), sizeof(unsigned long long) * 32) != hipSuccess) return -1;
+  unsigned long long z[32] = {};
+  return hipMemcpyToSymbol(HIP_SYMBOL(ilqr::g_fbt), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+#endif
